@@ -1,0 +1,181 @@
+"""ctypes binding of the oracle (oracle/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = None
+
+
+class MbInfo(ctypes.Structure):
+    _fields_ = [("luma_mode", ctypes.c_uint8), ("bpred", ctypes.c_uint8 * 16),
+                ("chroma_mode", ctypes.c_uint8), ("segment", ctypes.c_uint8),
+                ("skip", ctypes.c_uint8), ("non_zero_dct", ctypes.c_uint8)]
+
+
+class EncDebug(ctypes.Structure):
+    _fields_ = [("src_y", ctypes.c_void_p), ("src_u", ctypes.c_void_p), ("src_v", ctypes.c_void_p),
+                ("recon_y", ctypes.c_void_p), ("recon_u", ctypes.c_void_p), ("recon_v", ctypes.c_void_p),
+                ("recon1_y", ctypes.c_void_p),
+                ("mb_alpha", ctypes.c_void_p), ("seg_map", ctypes.c_void_p),
+                ("p1_info", ctypes.c_void_p), ("p2_info", ctypes.c_void_p),
+                ("levels", ctypes.c_void_p),
+                ("p1_stats", ctypes.c_uint32 * (4 * 8 * 3 * 11)),
+                ("final_probs", ctypes.c_uint8 * (4 * 8 * 3 * 11)),
+                ("seg_quant_index", ctypes.c_int * 4),
+                ("segments_enabled", ctypes.c_int), ("filter_level", ctypes.c_int),
+                ("base_quant_index", ctypes.c_int), ("skip_prob", ctypes.c_int),
+                ("p1_top_derr_last", ctypes.c_int8 * 1)]
+
+
+class FrameHdr(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("mbw", ctypes.c_int), ("mbh", ctypes.c_int),
+                ("filter_type", ctypes.c_int), ("filter_level", ctypes.c_int), ("sharpness", ctypes.c_int),
+                ("segments_enabled", ctypes.c_int), ("seg_delta_values", ctypes.c_int),
+                ("seg_lf_level", ctypes.c_int * 4), ("seg_quant_level", ctypes.c_int * 4),
+                ("lf_adj_enabled", ctypes.c_int), ("ref_delta0", ctypes.c_int), ("mode_delta0", ctypes.c_int),
+                ("num_partitions", ctypes.c_int)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(ROOT, "oracle", "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(path)
+        L.or_encode.restype = ctypes.c_int
+        L.or_encode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+        L.or_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_void_p] * 8
+        L.or_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.or_free.argtypes = [ctypes.c_void_p]
+        for n in ("or_fdct_c", "or_fdct_sse2_c", "or_idct_c", "or_idct_scalar_c", "or_wht_c", "or_iwht_c"):
+            getattr(L, n).argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.or_rgb_to_yuv420_c.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3
+        L.or_loop_filter_c.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.or_yuv_to_rgb_fancy_c.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+        L.or_analyze.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.or_bool_encoder_kat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.or_trellis_kat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.or_debug_struct_size.restype = ctypes.c_size_t
+        assert L.or_debug_struct_size() == ctypes.sizeof(EncDebug), "EncDebug layout mismatch"
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def blocks(fn, arr):
+    a = np.ascontiguousarray(arr, dtype=np.int32).copy()
+    getattr(lib(), fn)(_p(a), a.size // 16)
+    return a
+
+
+def rgb_to_yuv420(img, w, h, bpp):
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    y = np.zeros(mbw * 16 * mbh * 16, np.uint8)
+    u = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    v = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    lib().or_rgb_to_yuv420_c(_p(img), w, h, bpp, _p(y), _p(u), _p(v))
+    return y, u, v
+
+
+def encode(img, w, h, color, quality=75, method=4, debug=False):
+    """Returns (rc, vp8_bytes, debug_dict_or_None)."""
+    L = lib()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    dbg = None
+    keep = {}
+    if debug:
+        mbw, mbh = (w + 15) // 16, (h + 15) // 16
+        ys, cs = mbw * 16 * mbh * 16, mbw * 8 * mbh * 8
+        keep = dict(src_y=np.zeros(ys, np.uint8), src_u=np.zeros(cs, np.uint8), src_v=np.zeros(cs, np.uint8),
+                    recon_y=np.zeros(ys, np.uint8), recon_u=np.zeros(cs, np.uint8), recon_v=np.zeros(cs, np.uint8),
+                    recon1_y=np.zeros(ys, np.uint8),
+                    mb_alpha=np.zeros(mbw * mbh, np.uint8), seg_map=np.zeros(mbw * mbh, np.uint8),
+                    levels=np.zeros(mbw * mbh * 25 * 16, np.int32))
+        p1 = (MbInfo * (mbw * mbh))()
+        p2 = (MbInfo * (mbw * mbh))()
+        dbg = EncDebug()
+        for k, a in keep.items():
+            setattr(dbg, k, a.ctypes.data)
+        dbg.p1_info = ctypes.addressof(p1)
+        dbg.p2_info = ctypes.addressof(p2)
+        keep["p1_info"] = p1
+        keep["p2_info"] = p2
+    rc = L.or_encode(_p(img), img.size, w, h, color, quality, method, ctypes.byref(out), ctypes.byref(n),
+                     ctypes.byref(dbg) if dbg is not None else None)
+    data = b""
+    if rc == 0:
+        data = ctypes.string_at(out.value, n.value)
+        L.or_free(out)
+    if debug and rc == 0:
+        keep["p1_stats"] = np.ctypeslib.as_array(dbg.p1_stats).copy()
+        keep["final_probs"] = np.ctypeslib.as_array(dbg.final_probs).copy()
+        keep["seg_quant_index"] = list(dbg.seg_quant_index)
+        keep["segments_enabled"] = dbg.segments_enabled
+        keep["filter_level"] = dbg.filter_level
+        keep["base_quant_index"] = dbg.base_quant_index
+        keep["skip_prob"] = dbg.skip_prob
+        return rc, data, keep
+    return rc, data, None
+
+
+def decode_header(vp8):
+    h = FrameHdr()
+    buf = np.frombuffer(vp8, np.uint8).copy()
+    rc = lib().or_decode_header(_p(buf), buf.size, ctypes.byref(h))
+    return rc, h
+
+
+def decode(vp8, want_unfiltered=False, want_info=False):
+    rc, h = decode_header(vp8)
+    if rc != 0:
+        return rc, None
+    mbw, mbh = h.mbw, h.mbh
+    y = np.zeros(mbw * 16 * mbh * 16, np.uint8)
+    u = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    v = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    uy = uu = uv = None
+    if want_unfiltered:
+        uy, uu, uv = np.zeros_like(y), np.zeros_like(u), np.zeros_like(v)
+    info = (MbInfo * (mbw * mbh))() if want_info else None
+    buf = np.frombuffer(vp8, np.uint8).copy()
+    hdr = FrameHdr()
+    rc = lib().or_decode(_p(buf), buf.size, _p(y), _p(u), _p(v), _p(uy), _p(uu), _p(uv),
+                         ctypes.addressof(info) if info is not None else None, ctypes.byref(hdr))
+    res = dict(y=y, u=u, v=v, hdr=hdr, mbw=mbw, mbh=mbh, uy=uy, uu=uu, uv=uv, info=info)
+    return rc, res
+
+
+def yuv_to_rgb_fancy(y, u, v, w, h, bpp=3):
+    out = np.zeros(w * h * bpp, np.uint8)
+    lib().or_yuv_to_rgb_fancy_c(_p(y), _p(u), _p(v), w, h, bpp, _p(out))
+    return out
+
+
+def riff_vp8_chunk(data):
+    """Extract the 'VP8 ' chunk payload from a RIFF WebP file."""
+    assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"
+    off = 12
+    while off + 8 <= len(data):
+        tag = data[off:off + 4]
+        size = int.from_bytes(data[off + 4:off + 8], "little")
+        if tag == b"VP8 ":
+            return data[off + 8:off + 8 + size]
+        off += 8 + size + (size & 1)
+    raise ValueError("no VP8 chunk")
