@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Benchmark: 1080p lossy VP8 encodes/s at Q75 method 4 (BASELINE.json metric).
+
+One step = one full encode of a batch of `--frames` synthetic 1920x1080 RGBA
+frames already resident in HBM: rgb->yuv, analysis, segments, pass 1, host
+statistics/probabilities, pass 2 (mode search + DCT/quant/trellis + recon) and
+host token emission to finished VP8 bitstreams.  value = frames encoded by all
+ranks / max-over-ranks wall time of the K timed steps.
+
+Multi-GPU: one process per GPU (torch.distributed.run); frames are sharded by
+rank (independent frames, no data-path collective); a barrier brackets the
+timed region and the max time is taken with an all-reduce.
+
+The roofline object reports the dominant kernel (k_encode pass 2, the final
+DCT+quant pass fused with the mode search) against HBM: algorithmic bytes
+1568 B/MB (src YUV 384 + levels 800 + recon 384) x MBs per
+launch / average launch time measured with HIP events on the pipeline stream.
+cpu_baseline times the C restatement of the reference encoder (oracle/, 1
+thread) on a bounded sample of the same frames.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "image-webp_amd"))
+
+ALG_BYTES_PER_MB = 1568
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=int(os.environ.get("ZW_BENCH_FRAMES", "128")))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--quality", type=int, default=75)
+    ap.add_argument("--method", type=int, default=4)
+    ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic frames per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("ZW_BENCH_CPU_SECONDS", "12")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(imgs, w, h, q, m, budget_s):
+    """Oracle (C port of the reference CPU encoder), 1 thread, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        rc, _, _ = O.encode(imgs[n % len(imgs)], w, h, 3, q, m)
+        assert rc == 0
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 64:
+            break
+    return {"value": n / el, "unit": "encodes/s", "cores": 1, "kind": "port",
+            "sample": f"{n} synthetic {w}x{h} RGBA frames, Q{q} m{m}, oracle/ C restatement, 1 thread, {el:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import zwebp
+    from zwebp.synth import synth_rgba
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    w, h, F = a.width, a.height, a.frames
+    ctx = zwebp.Context(local)
+    pipe = zwebp.Pipeline(F, w, h, zwebp.ColorType.Rgba8, a.quality, a.method, ctx=ctx)
+    imgs = [synth_rgba(w, h, 0x5EED0000 + rank * 1000 + i) for i in range(min(a.distinct, F))]
+    for i in range(F):
+        pipe.upload(i, imgs[i % len(imgs)])
+    nmb = pipe.mbw * pipe.mbh
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(a.warmup):
+        pipe.encode()
+    barrier()
+    kt = np.zeros(4)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pipe.encode()
+        kt += np.array(pipe.kernel_times())
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_frames = F * a.steps * world
+    bytes_out = sum(len(pipe.output(i)) for i in range(min(F, 4)))
+
+    if rank == 0:
+        k = kt / max(a.steps, 1)  # ms per launch: rgb2yuv, analysis+segments, pass1, pass2
+        p2_ms = float(k[3])
+        achieved = ALG_BYTES_PER_MB * nmb * F / (p2_ms * 1e-3) / 1e9 if p2_ms > 0 else 0.0
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
+        line = {
+            "metric": f"{w}x{h} lossy encodes/s (Q{a.quality}, method {a.method})",
+            "value": total_frames / el,
+            "unit": "encodes/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": el / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {"workload": f"encode_frame_lossy {w}x{h} RGBA Q{a.quality} m{a.method}",
+                       "frames_per_step_per_gpu": F, "distinct_frames": len(imgs), "mbs_per_frame": nmb,
+                       "parallelism": f"frames sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_encode (pass 2)", "alg_bytes_per_launch": ALG_BYTES_PER_MB * nmb * F},
+            "cpu_baseline": cpu,
+            "kernel_ms_per_step": {"rgb2yuv": float(k[0]), "analysis_segments": float(k[1]),
+                                   "encode_pass1": float(k[2]), "encode_pass2": p2_ms},
+            "avg_frame_bytes": bytes_out / min(F, 4),
+        }
+        print(json.dumps(line), flush=True)
+    pipe.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,522 @@
+// zw_dec_host.cpp -- VP8 keyframe decoder: host bool decoder + device
+// reconstruction / loop filter.
+//
+//   host  : frame header (decoder/vp8.rs:553-670), partitions (:421-450),
+//           quantiser indices (:452-504), MB modes (:681-734) and residual
+//           tokens (:872-1058) -> one ZwDecMb record per macroblock.  The
+//           boolean decoder follows decoder/bit_reader.rs (libwebp-style
+//           56-bit refill, one zero byte past the end then eof).
+//   device: k_dec_recon (dequant, iWHT, iDCT, prediction) and k_loopfilter.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "../../include/zwebp.h"
+#include "zw_common.h"
+#include "zw_host_entropy.h"
+#include "zw_host_internal.h"
+
+extern "C" {
+hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
+                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
+hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
+                          const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes);
+}
+
+namespace {
+
+using namespace zwh;
+
+struct DecQuant {
+    int32_t ydc, yac, y2dc, y2ac, uvdc, uvac;
+};
+
+// bit_reader.rs:254-640
+struct BitReader {
+    const uint8_t* d = nullptr;
+    size_t len = 0, pos = 0;
+    uint64_t value = 0;
+    uint32_t range = 254;  // range - 1
+    int bits = -8;
+    bool eof = false;
+
+    void init(const uint8_t* data, size_t n)
+    {
+        d = data;
+        len = n;
+        pos = 0;
+        value = 0;
+        range = 254;
+        bits = -8;
+        eof = false;
+        load();
+    }
+    void load()
+    {
+        const size_t rem = len - pos;
+        if (rem >= 7) {
+            uint64_t v = 0;
+            if (rem >= 8) {
+                for (int i = 0; i < 8; i++) v = (v << 8) | d[pos + i];
+                v >>= 8;
+            } else {
+                for (int i = 0; i < 7; i++) v = (v << 8) | d[pos + i];
+            }
+            value = v | (value << 56);
+            bits += 56;
+            pos += 7;
+        } else if (pos < len) {
+            bits += 8;
+            value = (uint64_t)d[pos] | (value << 8);
+            pos++;
+        } else if (!eof) {
+            value <<= 8;
+            bits += 8;
+            eof = true;
+        } else {
+            bits = 0;
+        }
+    }
+    inline int bit(int prob)
+    {
+        uint32_t r = range;
+        if (bits < 0) load();
+        const int p = bits;
+        const uint32_t split = (r * (uint32_t)prob) >> 8;
+        const uint32_t v = (uint32_t)(value >> p);
+        const int b = v > split;
+        if (b) {
+            r -= split;
+            value -= ((uint64_t)split + 1) << p;
+        } else {
+            r = split + 1;
+        }
+        const int shift = 7 ^ (31 ^ __builtin_clz(r));
+        r <<= shift;
+        bits -= shift;
+        range = r - 1;
+        return b;
+    }
+    int lit(int n)
+    {
+        int v = 0;
+        for (int i = 0; i < n; i++) v = (v << 1) | bit(128);
+        return v;
+    }
+    int sgn(int n)
+    {
+        if (!bit(128)) return 0;
+        const int m = lit(n);
+        return bit(128) ? -m : m;
+    }
+    int tree(const int8_t* t, const uint8_t* probs)
+    {
+        int i = 0;
+        for (;;) {
+            const int n = t[i + bit(probs[i >> 1])];
+            if (n <= 0) return -n;
+            i = n;
+        }
+    }
+};
+
+struct DecFrame {
+    int width = 0, height = 0, mbw = 0, mbh = 0;
+    int filter_type = 0, filter_level = 0, sharpness = 0;
+    int segments_enabled = 0, seg_update_map = 0, seg_delta_values = 0;
+    int lf_adj_enabled = 0, ref_delta0 = 0, mode_delta0 = 0;
+    int8_t seg_quant[4] = {0, 0, 0, 0}, seg_lf[4] = {0, 0, 0, 0};
+    uint8_t seg_probs[3] = {255, 255, 255};
+    int nparts = 1;
+    int skip_prob = -1;
+    DecQuant q[4];
+    uint8_t probs[4][8][3][11];
+    BitReader hdr;
+    BitReader part[8];
+};
+
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// read_frame_header decoder/vp8.rs:553-670 (+ partitions :421-450, quant :452-504)
+static int parse_header(DecFrame& F, const uint8_t* data, size_t len)
+{
+    if (len < 3) return ZW_EBITSTREAM;
+    const uint32_t tag = data[0] | (data[1] << 8) | (data[2] << 16);
+    if (tag & 1) return ZW_EUNSUPPORTED_FEATURE;  // interframes
+    const uint32_t fps = tag >> 5;
+    if (len < 6) return ZW_EBITSTREAM;
+    if (data[3] != 0x9d || data[4] != 0x01 || data[5] != 0x2a) return ZW_EVP8_MAGIC;
+    if (len < 10) return ZW_EBITSTREAM;
+    F.width = (data[6] | (data[7] << 8)) & 0x3fff;
+    F.height = (data[8] | (data[9] << 8)) & 0x3fff;
+    F.mbw = (F.width + 15) / 16;
+    F.mbh = (F.height + 15) / 16;
+    size_t off = 10;
+    if (len - off < fps) return ZW_EBITSTREAM;
+    if (fps == 0) return ZW_ENOT_ENOUGH_INIT_DATA;
+    BitReader& b = F.hdr;
+    b.init(data + off, fps);
+    off += fps;
+    const int cs = b.lit(1);
+    (void)b.lit(1);
+    if (cs != 0) return ZW_ECOLORSPACE;
+    F.segments_enabled = b.bit(128);
+    int delta_values[4] = {0, 0, 0, 0};
+    if (F.segments_enabled) {
+        F.seg_update_map = b.bit(128);
+        if (b.bit(128)) {
+            const int mode = b.bit(128);
+            for (int i = 0; i < 4; i++) delta_values[i] = !mode;
+            for (int i = 0; i < 4; i++) F.seg_quant[i] = (int8_t)b.sgn(7);
+            for (int i = 0; i < 4; i++) F.seg_lf[i] = (int8_t)b.sgn(6);
+        }
+        if (F.seg_update_map)
+            for (int i = 0; i < 3; i++) F.seg_probs[i] = b.bit(128) ? (uint8_t)b.lit(8) : 255;
+        if (b.eof) return ZW_EBITSTREAM;
+    }
+    F.filter_type = b.bit(128);
+    F.filter_level = b.lit(6);
+    F.sharpness = b.lit(3);
+    F.lf_adj_enabled = b.bit(128);
+    if (F.lf_adj_enabled) {
+        if (b.bit(128)) {
+            int rd[4], md[4];
+            for (int i = 0; i < 4; i++) rd[i] = b.sgn(6);
+            for (int i = 0; i < 4; i++) md[i] = b.sgn(6);
+            F.ref_delta0 = rd[0];
+            F.mode_delta0 = md[0];
+        }
+        if (b.eof) return ZW_EBITSTREAM;
+    }
+    F.nparts = 1 << b.lit(2);
+    if (b.eof) return ZW_EBITSTREAM;
+    const size_t sz_off = off;
+    if (F.nparts > 1) {
+        if (len - off < (size_t)(3 * F.nparts - 3)) return ZW_EBITSTREAM;
+        off += 3 * F.nparts - 3;
+    }
+    for (int p = 0; p < F.nparts; p++) {
+        size_t psz;
+        if (p < F.nparts - 1) {
+            const uint8_t* s = data + sz_off + 3 * p;
+            psz = s[0] | (s[1] << 8) | (s[2] << 16);
+            if (len - off < psz) return ZW_EBITSTREAM;
+        } else {
+            psz = len - off;
+        }
+        F.part[p].init(data + off, psz);
+        off += psz;
+    }
+    const int yac = b.lit(7);
+    const int ydc_d = b.sgn(4), y2dc_d = b.sgn(4), y2ac_d = b.sgn(4), uvdc_d = b.sgn(4), uvac_d = b.sgn(4);
+    const int n = F.segments_enabled ? 4 : 1;
+    for (int i = 0; i < n; i++) {
+        const int base = F.segments_enabled ? (delta_values[i] ? F.seg_quant[i] + yac : F.seg_quant[i]) : yac;
+        DecQuant& s = F.q[i];
+        s.ydc = DC_QUANT[clampi(base + ydc_d, 0, 127)];
+        s.yac = AC_QUANT[clampi(base, 0, 127)];
+        s.y2dc = DC_QUANT[clampi(base + y2dc_d, 0, 127)] * 2;
+        s.y2ac = AC_QUANT[clampi(base + y2ac_d, 0, 127)] * 155 / 100;
+        s.uvdc = DC_QUANT[clampi(base + uvdc_d, 0, 127)];
+        s.uvac = AC_QUANT[clampi(base + uvac_d, 0, 127)];
+        if (s.y2ac < 8) s.y2ac = 8;
+        if (s.uvdc > 132) s.uvdc = 132;
+    }
+    for (int i = n; i < 4; i++) F.q[i] = F.q[0];
+    if (b.eof) return ZW_EBITSTREAM;
+    (void)b.lit(1);  // refresh_entropy_probs
+    memcpy(F.probs, COEFF_PROBS, sizeof F.probs);
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 8; j++)
+            for (int k = 0; k < 3; k++)
+                for (int t = 0; t < 11; t++)
+                    if (b.bit(COEFF_UPDATE_PROBS[i][j][k][t])) F.probs[i][j][k][t] = (uint8_t)b.lit(8);
+    if (b.eof) return ZW_EBITSTREAM;
+    F.skip_prob = b.lit(1) ? b.lit(8) : -1;
+    if (b.eof) return ZW_EBITSTREAM;
+    F.seg_delta_values = delta_values[0];
+    return ZW_OK;
+}
+
+// read_coefficients decoder/vp8.rs:872-1058: levels (not dequantised) into blk
+// at natural positions.  Returns -1 on eof, else whether the run was non-empty.
+static int read_levels(BitReader& r, const uint8_t P[8][3][11], int16_t* blk, int first, int ctx)
+{
+    int n = first;
+    const uint8_t* p = P[COEFF_BANDS[n]][ctx];
+    while (n < 16) {
+        if (!r.bit(p[0])) break;
+        while (!r.bit(p[1])) {
+            n++;
+            if (n >= 16) return r.eof ? -1 : 1;
+            p = P[COEFF_BANDS[n]][0];
+        }
+        int v, nctx;
+        if (!r.bit(p[2])) {
+            v = 1;
+            nctx = 1;
+        } else {
+            if (!r.bit(p[3])) {
+                if (!r.bit(p[4])) v = 2;
+                else v = 3 + r.bit(p[5]);
+            } else if (!r.bit(p[6])) {
+                if (!r.bit(p[7])) v = 5 + r.bit(159);
+                else {
+                    v = 7 + 2 * r.bit(165);
+                    v += r.bit(145);
+                }
+            } else {
+                const int b1 = r.bit(p[8]);
+                const int b0 = r.bit(p[9 + b1]);
+                const int cat = 2 * b1 + b0;
+                const uint8_t* cp = PROB_DCT_CAT[2 + cat];
+                int extra = 0;
+                for (int k = 0; k < 12 && cp[k]; k++) extra = extra + extra + r.bit(cp[k]);
+                v = 3 + (8 << cat) + extra;
+            }
+            nctx = 2;
+        }
+        blk[ZIGZAG[n]] = (int16_t)(r.bit(128) ? -v : v);
+        n++;
+        if (n < 16) p = P[COEFF_BANDS[n]][nctx];
+    }
+    if (r.eof) return -1;
+    return n > first;
+}
+
+// MB headers + tokens for the whole frame (decoder/vp8.rs:681-734, :1060-1168).
+static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
+{
+    const int mbw = F.mbw, mbh = F.mbh;
+    std::vector<uint8_t> top_cx((size_t)mbw * 9, 0), top_bp((size_t)mbw * 4, 0);
+    BitReader& b = F.hdr;
+    for (int mby = 0; mby < mbh; mby++) {
+        BitReader& pr = F.part[mby % F.nparts];
+        uint8_t left_cx[9] = {0}, left_bp[4] = {0};
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            ZwDecMb& M = mbs[(size_t)mby * mbw + mbx];
+            memset(&M, 0, sizeof M);
+            uint8_t* tcx = &top_cx[(size_t)mbx * 9];
+            uint8_t* tbp = &top_bp[(size_t)mbx * 4];
+            int seg = 0;
+            if (F.segments_enabled && F.seg_update_map) seg = b.tree(SEGMENT_ID_TREE, F.seg_probs);
+            const int skip = F.skip_prob >= 0 ? b.bit(F.skip_prob) : 0;
+            const int lm = b.tree(YMODE_TREE, KEYFRAME_YMODE_PROBS);
+            if (lm == 4) {
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++) {
+                        const int m = b.tree(BMODE_TREE, KEYFRAME_BPRED_MODE_PROBS[tbp[x]][left_bp[y]]);
+                        M.bpred[x + y * 4] = (uint8_t)m;
+                        tbp[x] = (uint8_t)m;
+                        left_bp[y] = (uint8_t)m;
+                    }
+            } else {
+                static const uint8_t intra_of[4] = {0, 2, 3, 1};  // DC,V,H,TM -> B_DC,B_VE,B_HE,B_TM
+                for (int i = 0; i < 4; i++) tbp[i] = left_bp[i] = intra_of[lm];
+            }
+            const int cm = b.tree(UVMODE_TREE, KEYFRAME_UV_MODE_PROBS);
+            if (b.eof) return ZW_EBITSTREAM;
+            M.luma_mode = (uint8_t)lm;
+            M.chroma_mode = (uint8_t)cm;
+            M.segment = (uint8_t)seg;
+            M.skip = (uint8_t)skip;
+            if (skip) {
+                if (lm != 4) left_cx[0] = tcx[0] = 0;
+                for (int i = 1; i < 9; i++) left_cx[i] = tcx[i] = 0;
+                continue;
+            }
+            uint32_t nzm = 0;
+            int first = 0;
+            if (lm != 4) {
+                const int nz = read_levels(pr, F.probs[1], M.y2, 0, tcx[0] + left_cx[0]);
+                if (nz < 0) return ZW_EBITSTREAM;
+                left_cx[0] = tcx[0] = (uint8_t)nz;
+                first = 1;
+            }
+            const int plane = lm != 4 ? 0 : 3;
+            for (int y = 0; y < 4; y++) {
+                int left = left_cx[y + 1];
+                for (int x = 0; x < 4; x++) {
+                    const int i = x + y * 4;
+                    const int nz = read_levels(pr, F.probs[plane], M.coeffs[i], first, tcx[x + 1] + left);
+                    if (nz < 0) return ZW_EBITSTREAM;
+                    nzm |= (uint32_t)nz << i;
+                    left = nz;
+                    tcx[x + 1] = (uint8_t)nz;
+                }
+                left_cx[y + 1] = (uint8_t)left;
+            }
+            for (int j = 5; j <= 7; j += 2) {
+                for (int y = 0; y < 2; y++) {
+                    int left = left_cx[y + j];
+                    for (int x = 0; x < 2; x++) {
+                        const int i = x + y * 2 + (j == 5 ? 16 : 20);
+                        const int nz = read_levels(pr, F.probs[2], M.coeffs[i], 0, tcx[x + j] + left);
+                        if (nz < 0) return ZW_EBITSTREAM;
+                        nzm |= (uint32_t)nz << i;
+                        left = nz;
+                        tcx[x + j] = (uint8_t)nz;
+                    }
+                    left_cx[y + j] = (uint8_t)left;
+                }
+            }
+            M.nz_mask = nzm;
+        }
+    }
+    return ZW_OK;
+}
+
+// calculate_filter_parameters decoder/vp8.rs:1470-1523, tabulated per
+// (segment, is_i4).
+static void filter_table(ZwFilterParams& fp, int filter_type, int filter_level, int sharpness, int seg_enabled,
+                         int seg_delta, const int8_t* seg_lf, int adj, int ref_delta0, int mode_delta0, int mbw, int mbh)
+{
+    memset(&fp, 0, sizeof fp);
+    fp.filter_type = filter_type;
+    fp.mbw = mbw;
+    fp.mbh = mbh;
+    for (int s = 0; s < 4; s++)
+        for (int i4 = 0; i4 < 2; i4++) {
+            int fl = filter_level, L = 0, I = 0, H = 0;
+            if (fl != 0) {
+                if (seg_enabled) fl = seg_delta ? fl + seg_lf[s] : seg_lf[s];
+                fl = clampi(fl, 0, 63);
+                if (adj) {
+                    fl += ref_delta0;
+                    if (i4) fl += mode_delta0;
+                }
+                fl = clampi(fl, 0, 63);
+                int il = fl;
+                if (sharpness > 0) {
+                    il >>= sharpness > 4 ? 2 : 1;
+                    if (il > 9 - sharpness) il = 9 - sharpness;
+                }
+                if (il == 0) il = 1;
+                L = fl;
+                I = il;
+                H = fl >= 40 ? 2 : (fl >= 15 ? 1 : 0);
+            }
+            fp.level[s][i4] = (uint8_t)L;
+            fp.ilimit[s][i4] = (uint8_t)I;
+            fp.hev[s][i4] = (uint8_t)H;
+        }
+}
+
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" void zw_frame_free(zw_frame* f)
+{
+    if (f && f->y) {
+        free(f->y);
+        f->y = f->u = f->v = nullptr;
+    }
+}
+
+// Vp8Decoder::decode_frame for n frames of identical dimensions, one device pass.
+extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
+{
+    if (!ctx || n <= 0 || !data || !lens || !outs) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
+    std::vector<DecFrame> F(n);
+    std::vector<int> rc(n, ZW_OK);
+    parallel_for(n, [&](int i) { rc[i] = parse_header(F[i], data[i], lens[i]); });
+    for (int i = 0; i < n; i++)
+        if (rc[i] != ZW_OK) return rc[i];
+    const int mbw = F[0].mbw, mbh = F[0].mbh;
+    for (int i = 1; i < n; i++)
+        if (F[i].mbw != mbw || F[i].mbh != mbh) return ZW_EINVAL;
+    if (mbw == 0 || mbh == 0) return ZW_EINVALID_DIMENSIONS;
+    const size_t nmb = (size_t)mbw * mbh;
+    const size_t ysz = nmb * 256, csz = nmb * 64;
+    std::vector<ZwDecMb> mbs((size_t)n * nmb);
+    std::vector<DecQuant> quant((size_t)n * 4);
+    std::vector<ZwFilterParams> fps(n);
+    parallel_for(n, [&](int i) {
+        rc[i] = parse_mbs(F[i], &mbs[(size_t)i * nmb]);
+        for (int s = 0; s < 4; s++) quant[(size_t)i * 4 + s] = F[i].q[s];
+        filter_table(fps[i], F[i].filter_type, F[i].filter_level, F[i].sharpness, F[i].segments_enabled,
+                     F[i].seg_delta_values, F[i].seg_lf, F[i].lf_adj_enabled, F[i].ref_delta0, F[i].mode_delta0, mbw,
+                     mbh);
+    });
+    for (int i = 0; i < n; i++)
+        if (rc[i] != ZW_OK) return rc[i];
+
+    HIPOK(hipSetDevice(ctx->device));
+    const size_t o_mbs = 0, o_q = al256(o_mbs + mbs.size() * sizeof(ZwDecMb));
+    const size_t o_fp = al256(o_q + quant.size() * sizeof(DecQuant));
+    const size_t o_fl = al256(o_fp + fps.size() * sizeof(ZwFilterParams));
+    const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
+    const size_t o_u = al256(o_y + (size_t)n * ysz), o_v = al256(o_u + (size_t)n * csz);
+    const size_t total = al256(o_v + (size_t)n * csz);
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx->stream;
+    HIPOK(hipMemcpyAsync(d + o_mbs, mbs.data(), mbs.size() * sizeof(ZwDecMb), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
+    HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_mbs), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
+                        csz, n));
+    HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
+    for (int i = 0; i < n; i++) {
+        uint8_t* buf = (uint8_t*)malloc(ysz + 2 * csz);
+        if (!buf) return ZW_ENOMEM;
+        zw_frame& o = outs[i];
+        o.width = (uint16_t)F[i].width;
+        o.height = (uint16_t)F[i].height;
+        o.y_stride = (uint32_t)mbw * 16;
+        o.uv_stride = (uint32_t)mbw * 8;
+        o.mb_rows = (uint32_t)mbh;
+        o.y = buf;
+        o.u = buf + ysz;
+        o.v = buf + ysz + csz;
+        o.filter_type = (uint8_t)F[i].filter_type;
+        o.filter_level = (uint8_t)F[i].filter_level;
+        o.sharpness_level = (uint8_t)F[i].sharpness;
+        HIPOK(hipMemcpyAsync(o.y, d + o_y + (size_t)i * ysz, ysz, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(o.u, d + o_u + (size_t)i * csz, csz, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(o.v, d + o_v + (size_t)i * csz, csz, hipMemcpyDeviceToHost, s));
+    }
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+extern "C" int zw_vp8_decode_frame(zw_ctx* ctx, const uint8_t* vp8, size_t len, zw_frame* out)
+{
+    if (!vp8 && len) return ZW_EINVAL;
+    const uint8_t* d[1] = {vp8};
+    size_t l[1] = {len};
+    return zw_vp8_decode_batch(ctx, 1, d, l, out);
+}
+
+extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v, uint32_t mbw, uint32_t mbh,
+                                    const uint8_t* mb_flags, int filter_type, int filter_level, int sharpness,
+                                    int segments_enabled, int seg_delta_values, const int8_t seg_lf_level[4],
+                                    int lf_adj_enabled, int ref_delta0, int mode_delta0)
+{
+    if (!ctx || !y || !u || !v || !mb_flags || mbw == 0 || mbh == 0) return ZW_EINVAL;
+    const int8_t zero[4] = {0, 0, 0, 0};
+    ZwFilterParams fp;
+    filter_table(fp, filter_type, filter_level, sharpness, segments_enabled, seg_delta_values,
+                 seg_lf_level ? seg_lf_level : zero, lf_adj_enabled, ref_delta0, mode_delta0, (int)mbw, (int)mbh);
+    const size_t nmb = (size_t)mbw * mbh, ysz = nmb * 256, csz = nmb * 64;
+    const size_t o_fp = 0, o_fl = 256, o_y = al256(o_fl + nmb * 4), o_u = al256(o_y + ysz), o_v = al256(o_u + csz);
+    const size_t total = al256(o_v + csz);
+    HIPOK(hipSetDevice(ctx->device));
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx->stream;
+    HIPOK(hipMemcpyAsync(d + o_fp, &fp, sizeof fp, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_fl, mb_flags, nmb * 4, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_y, y, ysz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_u, u, csz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_v, v, csz, hipMemcpyHostToDevice, s));
+    HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1));
+    HIPOK(hipMemcpyAsync(y, d + o_y, ysz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(v, d + o_v, csz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}

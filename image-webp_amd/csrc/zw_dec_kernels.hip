@@ -1,0 +1,503 @@
+// zw_dec_kernels.hip -- device half of the VP8 decoder (gfx950).
+//
+//   k_dec_recon    dequant + iWHT + iDCT (exact i16 SSE2 semantics) + intra
+//                  prediction + residual add  (decoder/vp8.rs:736-870, :1060-1168)
+//   k_loopfilter   in-loop deblocking filter   (decoder/vp8.rs:1172-1345,
+//                  decoder/loop_filter.rs)
+//
+// Both kernels run one workgroup per frame; macroblock rows go round-robin to
+// NWD waves and advance as an x+2y wavefront (MB x of row y starts once row
+// y-1 has finished MB x+1).  Reconstruction keeps the prediction borders in LDS
+// (they are the unfiltered pixels, vp8.rs:791-797).  The loop filter stages
+// each MB's 20x20 luma / 12x12 chroma neighbourhood in LDS, filters it in the
+// reference's edge order and writes it back; the wavefront order makes every
+// overlapping access happen in raster order, as in the reference.
+#include "zw_dev.h"
+
+#define NWD 8
+#define WGD (NWD * 64)
+
+struct ZwDecQuant {
+    int32_t ydc, yac, y2dc, y2ac, uvdc, uvac;
+};
+
+struct DecLds {
+    uint8_t ws[17 * ZW_BPS];
+    uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
+    uint8_t left_y[20], left_u[12], left_v[12];
+    int V[40];
+    int dc[16];
+    int res[16];
+    int misc[4];
+};
+
+__device__ __forceinline__ void dec_wait(const int* progress, int w, int need)
+{
+    while (__hip_atomic_load(&progress[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void dec_publish(int* progress, int w, int val)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(&progress[w], val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// I4 value vector for sub-block (x0,y0) of ws (see zw_dev.h d_I4_IDX).
+__device__ void dec_i4_values(DecLds* W, int lane, int x0, int y0)
+{
+    const uint8_t* ws = W->ws;
+    auto E = [&](int k) -> int {
+        if (k < 4) return ws[(y0 + 3 - k) * ZW_BPS + x0 - 1];
+        if (k == 4) return ws[(y0 - 1) * ZW_BPS + x0 - 1];
+        return ws[(y0 - 1) * ZW_BPS + x0 + (k - 5)];
+    };
+    if (lane < 13) W->V[lane] = E(lane);
+    else if (lane < 24) { int k = lane - 13; W->V[lane] = (E(k) + 2 * E(k + 1) + E(k + 2) + 2) >> 2; }
+    else if (lane < 36) { int k = lane - 24; W->V[lane] = (E(k) + E(k + 1) + 1) >> 1; }
+    else if (lane == 36) W->V[36] = (E(11) + 3 * E(12) + 2) >> 2;
+    else if (lane == 37) W->V[37] = (E(1) + 3 * E(0) + 2) >> 2;
+    else if (lane == 38) {
+        int v = 4;
+        for (int k = 0; k < 4; k++) v += E(k) + E(5 + k);
+        W->V[38] = v >> 3;
+    }
+    wsync();
+}
+__device__ __forceinline__ int dec_i4_px(const DecLds* W, int mode, int p)
+{
+    const int idx = d_I4_IDX[mode][p];
+    if (idx == 255) return W->V[38];
+    if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
+    return W->V[idx];
+}
+
+// Residual of one 4x4 block: full iDCT when the block's token run was
+// non-empty, DC-only iDCT when only the DC is set (vp8.rs:1110-1117).
+__device__ __forceinline__ void dec_block_residual(int* c, int nz)
+{
+    if (nz) idct16_exact(c);
+    else if (c[0] != 0) {
+        const int d = (c[0] + 4) >> 3;
+#pragma unroll
+        for (int k = 0; k < 16; k++) c[k] = d;
+    }
+}
+
+extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
+                                                              const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
+                                                              uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
+                                                              size_t csz)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    size_t off = 0;
+    DecLds* Wall = (DecLds*)smem;
+    off += ((sizeof(DecLds) + 15) & ~(size_t)15) * NWD;
+    int* progress = (int*)(smem + off);
+    off += 64;
+    uint8_t* top_y = smem + off;
+    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
+    uint8_t* top_u = smem + off;
+    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    uint8_t* top_v = smem + off;
+    DecLds* W = (DecLds*)((uint8_t*)Wall + ((sizeof(DecLds) + 15) & ~(size_t)15) * wv);
+    for (int i = threadIdx.x; i < mbw * 16 + 48; i += WGD) top_y[i] = 127;
+    for (int i = threadIdx.x; i < mbw * 8 + 48; i += WGD) top_u[i] = top_v[i] = 127;
+    if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
+    __syncthreads();
+    const int ys = mbw * 16, cs = mbw * 8;
+    const size_t nmb = (size_t)mbw * mbh;
+    for (int mby = wv; mby < mbh; mby += NWD) {
+        if (lane < 20) W->left_y[lane] = 129;
+        if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
+        wsync();
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
+            const ZwDecMb& M = mbs[(size_t)f * nmb + (size_t)mby * mbw + mbx];
+            const ZwDecQuant& Q = quant[(size_t)f * 4 + M.segment];
+            const int lm = M.luma_mode;
+            // --- luma border (create_border_luma) ---
+            uint8_t* ws = W->ws;
+            if (lane < 32) {
+                int v;
+                if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
+                else if (mby == 0) v = 127;
+                else if (lane <= 16) v = top_y[mbx * 16 + lane - 1];
+                else if (mbx == mbw - 1) v = top_y[mbx * 16 + 15];
+                else v = top_y[mbx * 16 + lane - 1];
+                ws[lane] = (uint8_t)v;
+                if (lane >= 17 && lane < 21) ws[4 * ZW_BPS + lane] = ws[8 * ZW_BPS + lane] = ws[12 * ZW_BPS + lane] = (uint8_t)v;
+            } else if (lane < 48) {
+                ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
+            }
+            wsync();
+            int nzdct = 0;
+            if (lm != 4) {
+                if (lane == 0) {
+                    int d[16];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) d[k] = 0;
+                    if (!M.skip) {
+#pragma unroll
+                        for (int k = 0; k < 16; k++) d[k] = (int)M.y2[k] * (k ? Q.y2ac : Q.y2dc);
+                        iwht16(d);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 16; k++) W->dc[k] = d[k];
+                }
+                wsync();
+                // DC predictor sum
+                const int above = mby != 0, left = mbx != 0;
+                int s = 0;
+                if (lane < 16) s = above ? ws[1 + lane] : 0;
+                else if (lane < 32) s = left ? ws[(lane - 15) * ZW_BPS] : 0;
+                s = wave_sum(s);
+                const int shf = 3 + above + left;
+                const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
+                int blocknz = 0;
+                if (lane < 16) {
+                    const int b = lane, bx = b & 3, by = b >> 2;
+                    int c[16];
+                    c[0] = W->dc[b];
+#pragma unroll
+                    for (int k = 1; k < 16; k++) c[k] = (int)M.coeffs[b][k] * Q.yac;
+                    const int nz = (M.nz_mask >> b) & 1;
+                    blocknz = (c[0] != 0) || nz;
+                    dec_block_residual(c, nz);
+                    const int P0 = ws[0];
+                    int px[16];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+                        const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
+                        const int p = lm == 0 ? dcv : (lm == 1 ? T : (lm == 2 ? L : clamp255(L + T - P0)));
+                        px[k] = clamp255(p + c[k]);
+                    }
+                    wsync();
+#pragma unroll
+                    for (int k = 0; k < 16; k++) ws[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
+                } else {
+                    wsync();
+                }
+                nzdct |= __any(blocknz) ? 1 : 0;
+                wsync();
+            } else {
+                for (int i = 0; i < 16; i++) {
+                    const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
+                    dec_i4_values(W, lane, x0, y0);
+                    if (lane == 0) {
+                        int c[16];
+#pragma unroll
+                        for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
+                        const int nz = (M.nz_mask >> i) & 1;
+                        W->misc[0] = (c[0] != 0) || nz;
+                        dec_block_residual(c, nz);
+#pragma unroll
+                        for (int k = 0; k < 16; k++) W->res[k] = c[k];
+                    }
+                    wsync();
+                    nzdct |= W->misc[0];
+                    if (lane < 16) {
+                        const int v = clamp255(dec_i4_px(W, M.bpred[i], lane) + W->res[lane]);
+                        ws[(y0 + (lane >> 2)) * ZW_BPS + x0 + (lane & 3)] = (uint8_t)v;
+                    }
+                    wsync();
+                }
+            }
+            // --- chroma ---
+            if (lane < 36) {
+                const int pl = lane >= 18;
+                const int i = pl ? lane - 18 : lane;
+                uint8_t* w = pl ? W->cv : W->cu;
+                const uint8_t* top = pl ? top_v : top_u;
+                const uint8_t* lft = pl ? W->left_v : W->left_u;
+                if (i == 0) w[0] = mby == 0 ? 127 : (mbx == 0 ? 129 : lft[0]);
+                else if (i <= 8) w[i] = mby == 0 ? 127 : top[mbx * 8 + i - 1];
+                else w[(i - 8) * ZW_BPS] = mbx == 0 ? 129 : lft[i - 8];
+            }
+            wsync();
+            {
+                int blocknz = 0;
+                int px[16];
+                const int b = lane & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
+                uint8_t* w = pl ? W->cv : W->cu;
+                if (lane < 8) {
+                    const int cm = M.chroma_mode;
+                    const int above = mby != 0, left = mbx != 0;
+                    int dcv = 128;
+                    {
+                        uint32_t s = 0;
+                        int shf = 2;
+                        if (left) {
+                            for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
+                            shf++;
+                        }
+                        if (above) {
+                            for (int x = 1; x <= 8; x++) s += w[x];
+                            shf++;
+                        }
+                        if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
+                    }
+                    int c[16];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[16 + b][k] * (k ? Q.uvac : Q.uvdc);
+                    const int nz = (M.nz_mask >> (16 + b)) & 1;
+                    blocknz = (c[0] != 0) || nz;
+                    dec_block_residual(c, nz);
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+                        const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
+                        const int p = cm == 0 ? dcv : (cm == 1 ? T : (cm == 2 ? L : clamp255(L + T - w[0])));
+                        px[k] = clamp255(p + c[k]);
+                    }
+                }
+                wsync();
+                if (lane < 8) {
+#pragma unroll
+                    for (int k = 0; k < 16; k++) w[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
+                }
+                nzdct |= __any(blocknz) ? 1 : 0;
+                wsync();
+            }
+            // --- borders, output ---
+            if (lane < 17) W->left_y[lane] = ws[lane * ZW_BPS + 16];
+            else if (lane < 33) top_y[mbx * 16 + lane - 17] = ws[16 * ZW_BPS + lane - 17 + 1];
+            if (lane < 9) {
+                W->left_u[lane] = W->cu[lane * ZW_BPS + 8];
+                W->left_v[lane] = W->cv[lane * ZW_BPS + 8];
+            } else if (lane >= 40 && lane < 48) {
+                top_u[mbx * 8 + lane - 40] = W->cu[8 * ZW_BPS + lane - 40 + 1];
+                top_v[mbx * 8 + lane - 40] = W->cv[8 * ZW_BPS + lane - 40 + 1];
+            }
+            uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
+            for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
+            uint8_t* uo = U + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
+            uint8_t* vo = V + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
+            uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+            vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+            if (lane < 4) {
+                const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
+                flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
+            }
+            wsync();
+            dec_publish(progress, wv, mby * 65536 + mbx + 1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Loop filter (decoder/loop_filter.rs) on LDS-staged neighbourhoods.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int c8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+__device__ __forceinline__ int u2s(int v) { return v - 128; }
+__device__ __forceinline__ uint8_t s2u(int v) { return (uint8_t)(c8(v) + 128); }
+
+// p points at q0; s = step across the edge.
+__device__ __forceinline__ int lf_common(int outer, uint8_t* p, int s)
+{
+    const int p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]), q0 = u2s(p[0]), q1 = u2s(p[s]);
+    const int o = outer ? c8(p1 - q1) : 0;
+    int a = c8(o + 3 * (q0 - p0));
+    const int b = c8(a + 3) >> 3;
+    a = c8(a + 4) >> 3;
+    p[0] = s2u(q0 - a);
+    p[-s] = s2u(p0 + b);
+    return a;
+}
+__device__ __forceinline__ bool lf_simple_th(int lim, const uint8_t* p, int s)
+{
+    return iabs(p[-s] - p[0]) * 2 + iabs(p[-2 * s] - p[s]) / 2 <= lim;
+}
+__device__ __forceinline__ bool lf_should(int il, int el, const uint8_t* p, int s)
+{
+    return lf_simple_th(el, p, s) && iabs(p[-4 * s] - p[-3 * s]) <= il && iabs(p[-3 * s] - p[-2 * s]) <= il &&
+           iabs(p[-2 * s] - p[-s]) <= il && iabs(p[3 * s] - p[2 * s]) <= il && iabs(p[2 * s] - p[s]) <= il &&
+           iabs(p[s] - p[0]) <= il;
+}
+__device__ __forceinline__ bool lf_hev(int t, const uint8_t* p, int s) { return iabs(p[-2 * s] - p[-s]) > t || iabs(p[s] - p[0]) > t; }
+
+__device__ void lf_simple(int el, uint8_t* p, int s)
+{
+    if (lf_simple_th(el, p, s)) lf_common(1, p, s);
+}
+__device__ void lf_inner(int ht, int il, int el, uint8_t* p, int s)
+{
+    if (lf_should(il, el, p, s)) {
+        const bool hv = lf_hev(ht, p, s);
+        const int a = (lf_common(hv, p, s) + 1) >> 1;
+        if (!hv) {
+            p[s] = s2u(u2s(p[s]) - a);
+            p[-2 * s] = s2u(u2s(p[-2 * s]) + a);
+        }
+    }
+}
+__device__ void lf_mb(int ht, int il, int el, uint8_t* p, int s)
+{
+    if (lf_should(il, el, p, s)) {
+        if (!lf_hev(ht, p, s)) {
+            const int p2 = u2s(p[-3 * s]), p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]);
+            const int q0 = u2s(p[0]), q1 = u2s(p[s]), q2 = u2s(p[2 * s]);
+            const int w = c8(c8(p1 - q1) + 3 * (q0 - p0));
+            int a = c8((27 * w + 63) >> 7);
+            p[0] = s2u(q0 - a);
+            p[-s] = s2u(p0 + a);
+            a = c8((18 * w + 63) >> 7);
+            p[s] = s2u(q1 - a);
+            p[-2 * s] = s2u(p1 + a);
+            a = c8((9 * w + 63) >> 7);
+            p[2 * s] = s2u(q2 - a);
+            p[-3 * s] = s2u(p2 + a);
+        } else {
+            lf_common(1, p, s);
+        }
+    }
+}
+
+#define LFY 20   // luma staging: rows/cols -4..15 around the MB
+#define LFC 12   // chroma staging: -4..7
+
+struct LfLds {
+    uint8_t y[LFY * LFY];
+    uint8_t u[LFC * LFC], v[LFC * LFC];
+};
+
+extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8_t* U, uint8_t* V,
+                                                               const uint8_t* __restrict__ flags,
+                                                               const ZwFilterParams* __restrict__ fp, size_t ysz,
+                                                               size_t csz)
+{
+    __shared__ LfLds lds[NWD];
+    __shared__ int progress[NWD];
+    const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const ZwFilterParams& F = fp[f];
+    const int mbw = F.mbw, mbh = F.mbh, ys = mbw * 16, cs = mbw * 8;
+    const size_t nmb = (size_t)mbw * mbh;
+    if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
+    __syncthreads();
+    LfLds* L = &lds[wv];
+    uint8_t* Yf = Y + (size_t)f * ysz;
+    uint8_t* Uf = U + (size_t)f * csz;
+    uint8_t* Vf = V + (size_t)f * csz;
+    for (int mby = wv; mby < mbh; mby += NWD) {
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
+            const uint8_t* fl = flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4;
+            const int i4 = fl[0] == 4, seg = fl[1], skip = fl[2], nzd = fl[3];
+            const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
+            if (lvl != 0) {
+                const int x0 = mbx * 16, y0 = mby * 16;
+                // stage (rows/cols outside the frame are never touched by the filters)
+                for (int k = lane; k < LFY * LFY; k += 64) {
+                    const int r = k / LFY - 4, c = k % LFY - 4;
+                    const int gy = y0 + r, gx = x0 + c;
+                    if (gy >= 0 && gx >= 0) L->y[k] = Yf[(size_t)gy * ys + gx];
+                }
+                if (!F.filter_type) {
+                    for (int k = lane; k < LFC * LFC; k += 64) {
+                        const int r = k / LFC - 4, c = k % LFC - 4;
+                        const int gy = mby * 8 + r, gx = mbx * 8 + c;
+                        if (gy >= 0 && gx >= 0) {
+                            L->u[k] = Uf[(size_t)gy * cs + gx];
+                            L->v[k] = Vf[(size_t)gy * cs + gx];
+                        }
+                    }
+                }
+                wsync();
+                const int mbe = (lvl + 2) * 2 + il, sube = lvl * 2 + il;
+                const int inner = i4 || (!skip && nzd);
+                // lane roles: 0..15 luma line, 16..23 U line, 24..31 V line
+                const bool isy = lane < 16, isu = lane >= 16 && lane < 24, isv = lane >= 24 && lane < 32;
+                const int li = isy ? lane : (lane - 16) & 7;
+                uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
+                const int W_ = isy ? LFY : LFC;
+                const bool act = isy || (!F.filter_type && (isu || isv));
+                // left MB edge (vertical edge, filter along rows)
+                if (mbx > 0 && act) {
+                    uint8_t* p = buf + (li + 4) * W_ + 4;
+                    if (F.filter_type) lf_simple(mbe, p, 1);
+                    else lf_mb(ht, il, mbe, p, 1);
+                }
+                wsync();
+                if (inner) {
+                    for (int x = 4; x < 16; x += 4) {
+                        if (isy) {
+                            uint8_t* p = buf + (li + 4) * W_ + 4 + x;
+                            if (F.filter_type) lf_simple(sube, p, 1);
+                            else lf_inner(ht, il, sube, p, 1);
+                        } else if (act && x == 4) {
+                            lf_inner(ht, il, sube, buf + (li + 4) * W_ + 4 + 4, 1);
+                        }
+                        wsync();
+                    }
+                }
+                if (mby > 0 && act) {
+                    uint8_t* p = buf + 4 * W_ + 4 + li;
+                    if (F.filter_type) lf_simple(mbe, p, W_);
+                    else lf_mb(ht, il, mbe, p, W_);
+                }
+                wsync();
+                if (inner) {
+                    for (int y = 4; y < 16; y += 4) {
+                        if (isy) {
+                            uint8_t* p = buf + (4 + y) * W_ + 4 + li;
+                            if (F.filter_type) lf_simple(sube, p, W_);
+                            else lf_inner(ht, il, sube, p, W_);
+                        } else if (act && y == 4) {
+                            lf_inner(ht, il, sube, buf + (4 + 4) * W_ + 4 + li, W_);
+                        }
+                        wsync();
+                    }
+                }
+                // write back
+                for (int k = lane; k < LFY * LFY; k += 64) {
+                    const int r = k / LFY - 4, c = k % LFY - 4;
+                    const int gy = y0 + r, gx = x0 + c;
+                    if (gy >= 0 && gx >= 0) Yf[(size_t)gy * ys + gx] = L->y[k];
+                }
+                if (!F.filter_type) {
+                    for (int k = lane; k < LFC * LFC; k += 64) {
+                        const int r = k / LFC - 4, c = k % LFC - 4;
+                        const int gy = mby * 8 + r, gx = mbx * 8 + c;
+                        if (gy >= 0 && gx >= 0) {
+                            Uf[(size_t)gy * cs + gx] = L->u[k];
+                            Vf[(size_t)gy * cs + gx] = L->v[k];
+                        }
+                    }
+                }
+            }
+            wsync();
+            dec_publish(progress, wv, mby * 65536 + mbx + 1);
+        }
+    }
+}
+
+extern "C" size_t zw_dec_lds_bytes(int mbw)
+{
+    size_t off = ((sizeof(DecLds) + 15) & ~(size_t)15) * NWD + 64;
+    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
+    off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
+    return off;
+}
+
+extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
+                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
+{
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs, (const ZwDecQuant*)quant,
+                       Y, U, V, flags, mbw, mbh, ysz, csz);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
+                                     const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes)
+{
+    hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), 0, s, Y, U, V, flags, fp, ysz, csz);
+    return hipGetLastError();
+}

@@ -1,0 +1,377 @@
+// zw_dev.h -- device-side helpers shared by the HIP kernels: constant tables,
+// exact integer transforms, quantizer, residual cost and trellis.  Every
+// function restates the reference function named in its comment; the HIP
+// kernels compose them per macroblock.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "zw_common.h"
+
+#define ZW_TABLE(T, N, D, ...) __constant__ T d_##N D = {__VA_ARGS__};
+#include "zw_tables.inc"
+#undef ZW_TABLE
+
+// (mode, pixel) -> index into the I4 value vector (tools/gen_i4_table.py);
+// 255 = DC, 254 = TM.  Value vector: E = [L3 L2 L1 L0 P A0..A7], then
+// avg3 of consecutive triples (13..23), avg2 of pairs (24..35),
+// avg3(A6,A7,A7) (36), avg3(L2,L3,L3) (37).
+__constant__ uint8_t d_I4_IDX[10][16] = {
+    {255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255},
+    {254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254},
+    {17, 18, 19, 20, 17, 18, 19, 20, 17, 18, 19, 20, 17, 18, 19, 20},
+    {15, 15, 15, 15, 14, 14, 14, 14, 13, 13, 13, 13, 37, 37, 37, 37},
+    {18, 19, 20, 21, 19, 20, 21, 22, 20, 21, 22, 23, 21, 22, 23, 36},
+    {16, 17, 18, 19, 15, 16, 17, 18, 14, 15, 16, 17, 13, 14, 15, 16},
+    {28, 29, 30, 31, 16, 17, 18, 19, 15, 28, 29, 30, 14, 16, 17, 18},
+    {29, 30, 31, 32, 18, 19, 20, 21, 30, 31, 32, 22, 19, 20, 21, 23},
+    {27, 16, 17, 18, 26, 15, 27, 16, 25, 14, 26, 15, 24, 13, 25, 14},
+    {26, 14, 25, 13, 25, 13, 24, 37, 24, 37, 0, 0, 0, 0, 0, 0},
+};
+
+#define DI __device__ __forceinline__
+
+DI int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+DI int iabs(int v) { return v < 0 ? -v : v; }
+
+// Intra-wave LDS hand-off: lanes of one wave exchange data through LDS; a
+// workgroup-scope fence orders the LDS traffic and stops the compiler from
+// moving accesses across it.
+DI void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+DI int wave_sum(int v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+DI int red16(int v)  // sum within aligned 16-lane groups
+{
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
+    return v;
+}
+DI int red8(int v)
+{
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
+    return v;
+}
+DI long long shfl64(long long v, int src)
+{
+    int lo = __shfl((int)(v & 0xffffffff), src);
+    int hi = __shfl((int)(v >> 32), src);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// VP8Matrix::quantize_coeff (cost.rs:457): sign * ((|c| * iq + bias) >> 17).
+// |c| * iq < 2^31 for every coefficient an 8-bit source can produce.
+DI int quantz(int c, uint32_t iq, uint32_t bias)
+{
+    uint32_t a = (uint32_t)iabs(c);
+    int l = (int)((a * iq + bias) >> 17);
+    return c < 0 ? -l : l;
+}
+
+// dct4x4_scalar (transform.rs:176).  For residuals in [-255,255] it equals the
+// SSE2 build the reference ships (verified exhaustively in tests).
+DI void fdct16(int* b)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a = (b[i * 4] + b[i * 4 + 3]) * 8, bb = (b[i * 4 + 1] + b[i * 4 + 2]) * 8;
+        int c = (b[i * 4 + 1] - b[i * 4 + 2]) * 8, d = (b[i * 4] - b[i * 4 + 3]) * 8;
+        b[i * 4] = a + bb;
+        b[i * 4 + 2] = a - bb;
+        b[i * 4 + 1] = (c * 2217 + d * 5352 + 14500) >> 12;
+        b[i * 4 + 3] = (d * 2217 - c * 5352 + 7500) >> 12;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a = b[i] + b[i + 12], bb = b[i + 4] + b[i + 8];
+        int c = b[i + 4] - b[i + 8], d = b[i] - b[i + 12];
+        b[i] = (a + bb + 7) >> 4;
+        b[i + 8] = (a - bb + 7) >> 4;
+        b[i + 4] = ((c * 2217 + d * 5352 + 12000) >> 16) + (d != 0 ? 1 : 0);
+        b[i + 12] = (d * 2217 - c * 5352 + 51000) >> 16;
+    }
+}
+
+// idct4x4 in i32.  Equal to the reference's SSE2 i16 iDCT for every
+// dequantized block the encoder produces (no i16 overflow is reachable).
+DI void idct16(int* b)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a1 = b[i] + b[8 + i], b1 = b[i] - b[8 + i];
+        int c1 = ((b[4 + i] * 35468) >> 16) - (b[12 + i] + ((b[12 + i] * 20091) >> 16));
+        int d1 = (b[4 + i] + ((b[4 + i] * 20091) >> 16)) + ((b[12 + i] * 35468) >> 16);
+        b[i] = a1 + d1;
+        b[4 + i] = b1 + c1;
+        b[12 + i] = a1 - d1;
+        b[8 + i] = b1 - c1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a1 = b[4 * i] + b[4 * i + 2], b1 = b[4 * i] - b[4 * i + 2];
+        int c1 = ((b[4 * i + 1] * 35468) >> 16) - (b[4 * i + 3] + ((b[4 * i + 3] * 20091) >> 16));
+        int d1 = (b[4 * i + 1] + ((b[4 * i + 1] * 20091) >> 16)) + ((b[4 * i + 3] * 35468) >> 16);
+        b[4 * i] = (a1 + d1 + 4) >> 3;
+        b[4 * i + 3] = (a1 - d1 + 4) >> 3;
+        b[4 * i + 1] = (b1 + c1 + 4) >> 3;
+        b[4 * i + 2] = (b1 - c1 + 4) >> 3;
+    }
+}
+
+// idct4x4_sse2 with exact i16 semantics (transform_simd_intrinsics.rs:478):
+// saturating pack, wrapping i16 adds, _mm_mulhi_epi16, i16 >>3.  Used by the
+// decoder, whose inputs come from arbitrary bitstreams.
+DI int w16(int v) { return (int)(short)(unsigned short)(unsigned)v; }
+DI int sat16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+DI int mulhi16(int x, int k) { return (x * k) >> 16; }
+DI void idct16_exact(int* b)
+{
+    int t[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) b[i] = sat16(b[i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int x0 = b[i], x1 = b[4 + i], x2 = b[8 + i], x3 = b[12 + i];
+        int a = w16(x0 + x2), bb = w16(x0 - x2);
+        int c = w16(w16(x1 - x3) + w16(mulhi16(x1, -30068) - mulhi16(x3, 20091)));
+        int d = w16(w16(x1 + x3) + w16(mulhi16(x1, 20091) + mulhi16(x3, -30068)));
+        t[i] = w16(a + d);
+        t[4 + i] = w16(bb + c);
+        t[8 + i] = w16(bb - c);
+        t[12 + i] = w16(a - d);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        int y0 = t[r * 4], y1 = t[r * 4 + 1], y2 = t[r * 4 + 2], y3 = t[r * 4 + 3];
+        int dc = w16(y0 + 4);
+        int a = w16(dc + y2), bb = w16(dc - y2);
+        int c = w16(w16(y1 - y3) + w16(mulhi16(y1, -30068) - mulhi16(y3, 20091)));
+        int d = w16(w16(y1 + y3) + w16(mulhi16(y1, 20091) + mulhi16(y3, -30068)));
+        b[r * 4] = w16(a + d) >> 3;
+        b[r * 4 + 1] = w16(bb + c) >> 3;
+        b[r * 4 + 2] = w16(bb - c) >> 3;
+        b[r * 4 + 3] = w16(a - d) >> 3;
+    }
+}
+
+// wht4x4 (transform.rs:116)
+DI void wht16(int* b)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a = b[i * 4] + b[i * 4 + 3], bb = b[i * 4 + 1] + b[i * 4 + 2];
+        int c = b[i * 4 + 1] - b[i * 4 + 2], d = b[i * 4] - b[i * 4 + 3];
+        b[i * 4] = a + bb;
+        b[i * 4 + 1] = c + d;
+        b[i * 4 + 2] = a - bb;
+        b[i * 4 + 3] = d - c;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a1 = b[i] + b[i + 12], b1 = b[i + 4] + b[i + 8];
+        int c1 = b[i + 4] - b[i + 8], d1 = b[i] - b[i + 12];
+        int a2 = a1 + b1, b2 = c1 + d1, c2 = a1 - b1, d2 = d1 - c1;
+        b[i] = (a2 + (a2 > 0 ? 1 : 0)) / 2;
+        b[i + 4] = (b2 + (b2 > 0 ? 1 : 0)) / 2;
+        b[i + 8] = (c2 + (c2 > 0 ? 1 : 0)) / 2;
+        b[i + 12] = (d2 + (d2 > 0 ? 1 : 0)) / 2;
+    }
+}
+
+// iwht4x4 (transform.rs:82)
+DI void iwht16(int* b)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a1 = b[i] + b[12 + i], b1 = b[4 + i] + b[8 + i];
+        int c1 = b[4 + i] - b[8 + i], d1 = b[i] - b[12 + i];
+        b[i] = a1 + b1;
+        b[4 + i] = c1 + d1;
+        b[8 + i] = a1 - b1;
+        b[12 + i] = d1 - c1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        int a1 = b[4 * r] + b[4 * r + 3], b1 = b[4 * r + 1] + b[4 * r + 2];
+        int c1 = b[4 * r + 1] - b[4 * r + 2], d1 = b[4 * r] - b[4 * r + 3];
+        b[4 * r] = (a1 + b1 + 3) >> 3;
+        b[4 * r + 1] = (c1 + d1 + 3) >> 3;
+        b[4 * r + 2] = (a1 - b1 + 3) >> 3;
+        b[4 * r + 3] = (d1 - c1 + 3) >> 3;
+    }
+}
+
+// t_transform (cost.rs:59): weighted Hadamard magnitude of a 4x4 u8 block.
+DI int ttransform(const int* in)
+{
+    int tmp[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int* r = in + i * 4;
+        int a0 = r[0] + r[2], a1 = r[1] + r[3], a2 = r[1] - r[3], a3 = r[0] - r[2];
+        tmp[i * 4] = a0 + a1;
+        tmp[i * 4 + 1] = a3 + a2;
+        tmp[i * 4 + 2] = a3 - a2;
+        tmp[i * 4 + 3] = a0 - a1;
+    }
+    int sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a0 = tmp[i] + tmp[8 + i], a1 = tmp[4 + i] + tmp[12 + i];
+        int a2 = tmp[4 + i] - tmp[12 + i], a3 = tmp[i] - tmp[8 + i];
+        sum += d_VP8_WEIGHT_Y[i] * iabs(a0 + a1) + d_VP8_WEIGHT_Y[4 + i] * iabs(a3 + a2) +
+               d_VP8_WEIGHT_Y[8 + i] * iabs(a3 - a2) + d_VP8_WEIGHT_Y[12 + i] * iabs(a0 - a1);
+    }
+    return sum;
+}
+
+DI uint32_t bitcost(int bit, int p) { return bit ? d_VP8_ENTROPY_COST[255 - p] : d_VP8_ENTROPY_COST[p]; }
+
+// Tables the encoder kernels keep in LDS.
+struct LdsTables {
+    uint16_t lc[4][8][3][68];
+    uint16_t eob[4][8][3];
+    uint16_t init[4][8][3];
+    uint8_t probs[4][8][3][11];
+};
+
+// get_residual_cost (cost.rs:1670 / SSE2 :1735).  'c' is indexed by position n
+// exactly as the reference indexes Residual::coeffs (natural-order arrays are
+// passed by the RD code: quirk A1).  'last' spans all 16 entries.
+template <int FIRST>
+DI uint32_t rcost(const int* c, int ctx0, int ctype, const LdsTables* T)
+{
+    int last = -1;
+#pragma unroll
+    for (int n = 0; n < 16; n++)
+        if (c[n] != 0) last = n;
+    const int p0 = T->probs[ctype][d_VP8_ENC_BANDS[FIRST]][ctx0][0];
+    if (last < 0) return bitcost(0, p0);
+    uint32_t cost = ctx0 == 0 ? bitcost(1, p0) : 0;
+    int ctx = ctx0;
+#pragma unroll
+    for (int n = FIRST; n < 16; n++) {
+        if (n <= last) {
+            int v = iabs(c[n]);
+            cost += d_VP8_LEVEL_FIXED_COSTS[v < 2047 ? v : 2047] + T->lc[ctype][d_VP8_ENC_BANDS[n]][ctx][v < 67 ? v : 67];
+            ctx = v < 2 ? v : 2;
+        }
+    }
+    if (last < 15) cost += bitcost(0, T->probs[ctype][d_VP8_ENC_BANDS[last + 1]][ctx][0]);
+    return cost;
+}
+
+// trellis_quantize_block (cost.rs:788-1006).  coeffs (natural order) become the
+// dequantized values; out (zigzag) the levels.  Returns has_nz.
+template <int FIRST>
+DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen, uint32_t lambda,
+               const LdsTables* T, int ctype, int ctx0)
+{
+    const long long MAXC = 0x3fffffffffffffffLL;
+    const int qac = (int)m.q[1];
+    const int thresh = (qac * qac) / 4;
+    int last = FIRST - 1;
+#pragma unroll
+    for (int n = FIRST; n < 16; n++) {
+        int j = d_ZIGZAG[n];
+        if (coeffs[j] * coeffs[j] > thresh) last = n;
+    }
+    if (last < 15) last++;
+    const int bfirst = d_VP8_ENC_BANDS[FIRST];
+    long long best = (long long)T->eob[ctype][bfirst][ctx0] * lambda;
+    long long init = ctx0 == 0 ? (long long)T->init[ctype][bfirst][ctx0] * lambda : 0;
+    long long s0 = init, s1 = init;
+    int c0 = ctx0, c1 = ctx0;  // ctx selecting the predecessor's cost table
+    int bn = -1, bd = 0, bp = 0;
+    unsigned prevbits = 0;
+    int lv0[16], sg[16];
+    const uint32_t nbias = ((0u << 17) + 128) >> 8, tbias = ((0x80u << 17) + 128) >> 8;
+#pragma unroll
+    for (int n = FIRST; n < 16; n++) {
+        lv0[n] = 0;
+        sg[n] = 0;
+        if (n <= last) {
+            const int j = d_ZIGZAG[n];
+            const int q = j == 0 ? (int)m.q[0] : qac;
+            const uint32_t iq = j == 0 ? m.iq[0] : m.iq[1];
+            const int sign = coeffs[j] < 0;
+            const int cws = iabs(coeffs[j]) + sharpen[j];
+            int l0 = (int)(((uint32_t)cws * iq + nbias) >> 17);
+            l0 = l0 < 2047 ? l0 : 2047;
+            int thr = (int)(((uint32_t)cws * iq + tbias) >> 17);
+            thr = thr < 2047 ? thr : 2047;
+            const int band = d_VP8_ENC_BANDS[n];
+            long long ns0 = MAXC, ns1 = MAXC;
+            int nc0 = 0, nc1 = 0;
+#pragma unroll
+            for (int d = 0; d < 2; d++) {
+                const int level = l0 + d;
+                const int ctx = level < 2 ? level : 2;
+                if (d == 0) nc0 = ctx;
+                else nc1 = ctx;
+                if (level <= thr) {
+                    const int ne = cws - level * q;
+                    const long long dd = (long long)d_VP8_WEIGHT_TRELLIS[j] * ((long long)(ne * ne) - (long long)(cws * cws));
+                    const long long base = 256 * dd;
+                    const int lv = level < 67 ? level : 67;
+                    const int fixed = d_VP8_LEVEL_FIXED_COSTS[level] + (level > 0 ? 256 : 0);
+                    long long sc0 = s0 + (long long)(fixed + T->lc[ctype][band][c0][lv]) * lambda;
+                    long long sc1 = s1 + (long long)(fixed + T->lc[ctype][band][c1][lv]) * lambda;
+                    int pb = sc1 < sc0;
+                    long long cur = (pb ? sc1 : sc0) + base;
+                    prevbits |= (unsigned)pb << (2 * n + d);
+                    if (d == 0) ns0 = cur;
+                    else ns1 = cur;
+                    if (level != 0 && cur < best) {
+                        long long eob = 0;
+                        if (n < 15) eob = (long long)T->eob[ctype][d_VP8_ENC_BANDS[n + 1]][ctx] * lambda;
+                        long long term = cur + eob;
+                        if (term < best) {
+                            best = term;
+                            bn = n;
+                            bd = d;
+                            bp = pb;
+                        }
+                    }
+                }
+            }
+            s0 = ns0;
+            s1 = ns1;
+            c0 = nc0;
+            c1 = nc1;
+            lv0[n] = l0;
+            sg[n] = sign;
+        }
+    }
+#pragma unroll
+    for (int n = FIRST; n < 16; n++) {
+        out[n] = 0;
+        coeffs[d_ZIGZAG[n]] = 0;
+    }
+    if (bn < 0) return 0;
+    int nz = 0, cd = bd;
+#pragma unroll
+    for (int n = 15; n >= FIRST; n--) {
+        if (n <= bn) {
+            const int j = d_ZIGZAG[n];
+            const int level = lv0[n] + cd;
+            const int v = sg[n] ? -level : level;
+            out[n] = v;
+            coeffs[j] = v * (int)(j == 0 ? m.q[0] : m.q[1]);
+            nz |= v != 0;
+            cd = (n == bn) ? bp : (int)((prevbits >> (2 * n + cd)) & 1);
+        }
+    }
+    return nz;
+}

@@ -1,0 +1,1386 @@
+// zw_enc_kernels.hip -- device half of the lossy encoder (gfx950).
+//
+//   k_rgb2yuv     convert_image_yuv / convert_image_y      (decoder/yuv.rs:656, :806)
+//   k_analysis    analyze_image per-MB alpha + histogram    (encoder/analysis.rs:964)
+//   k_segments    k-means, segment quant, matrices, lambdas (analysis.rs:1029, :1145;
+//                 vp8.rs:2278-2388, types.rs:806)
+//   k_encode      one encode pass over a batch of frames:   (vp8.rs:1281-1488)
+//                 RD mode search (pick_best_intra16/intra4/uv), final transform,
+//                 quantization (simple or trellis), recon, error diffusion, skip.
+//
+// Parallel structure: one workgroup per frame, NW waves.  Macroblock rows are
+// dealt to waves round-robin and advance as an x+2y wavefront (a row may work
+// on MB x once the row above has finished MB x+1), synchronised through LDS
+// progress counters.  Within a macroblock the 64 lanes work block-parallel.
+// Pass 1's chroma is a raster chain (left_derr is not reset per row, quirk A5)
+// and runs on wave 0 while waves 1..NW-1 do the luma wavefront.
+#include "zw_dev.h"
+
+#define NW 8
+#define WG (NW * 64)
+
+// ---------------------------------------------------------------------------
+// RGB(A)/L(A) -> padded YUV420.  One thread per chroma sample; it produces the
+// 2x2 luma pixels and the U/V sample.  Padding (x >= w, y >= h) is produced by
+// clamping the source coordinate, which equals the reference's edge
+// replication (yuv.rs:765-803).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int rgb_y(const uint8_t* p)
+{
+    return (16839 * p[0] + 33059 * p[1] + 6420 * p[2] + (1 << 15) + (16 << 16)) >> 16;
+}
+__device__ __forceinline__ int rgb_u(const uint8_t* p) { return -9719 * p[0] - 19081 * p[1] + 28800 * p[2] + (128 << 16); }
+__device__ __forceinline__ int rgb_v(const uint8_t* p) { return 28800 * p[0] - 24116 * p[1] - 4684 * p[2] + (128 << 16); }
+
+extern "C" __global__ void k_rgb2yuv(const uint8_t* __restrict__ img, int w, int h, int bpp, int mbw, int mbh,
+                                     uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V,
+                                     size_t img_stride, size_t ysz, size_t csz)
+{
+    const int cw = mbw * 8, chh = mbh * 8, lw = mbw * 16;
+    const int f = blockIdx.y;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= cw * chh) return;
+    const int cx = idx % cw, cy = idx / cw;
+    const uint8_t* im = img + (size_t)f * img_stride;
+    uint8_t* Yf = Y + (size_t)f * ysz;
+    const int acw = (w + 1) / 2, ach = (h + 1) / 2;
+    const int scx = cx < acw ? cx : acw - 1, scy = cy < ach ? cy : ach - 1;
+    int xs[2] = {min(2 * scx, w - 1), min(2 * scx + 1, w - 1)};
+    int ys[2] = {min(2 * scy, h - 1), min(2 * scy + 1, h - 1)};
+    // luma: the 2x2 pixels this thread owns in the padded plane
+#pragma unroll
+    for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+        for (int dx = 0; dx < 2; dx++) {
+            int px = min(2 * cx + dx, w - 1), py = min(2 * cy + dy, h - 1);
+            const uint8_t* p = im + ((size_t)py * w + px) * bpp;
+            Yf[(size_t)(2 * cy + dy) * lw + 2 * cx + dx] = (uint8_t)(bpp <= 2 ? p[0] : rgb_y(p));
+        }
+    uint8_t uo = 127, vo = 127;
+    if (bpp > 2) {
+        int su = 0, sv = 0;
+#pragma unroll
+        for (int dy = 0; dy < 2; dy++)
+#pragma unroll
+            for (int dx = 0; dx < 2; dx++) {
+                const uint8_t* p = im + ((size_t)ys[dy] * w + xs[dx]) * bpp;
+                su += rgb_u(p);
+                sv += rgb_v(p);
+            }
+        uo = (uint8_t)((su + (1 << 17)) >> 18);
+        vo = (uint8_t)((sv + (1 << 17)) >> 18);
+    }
+    U[(size_t)f * csz + (size_t)cy * cw + cx] = uo;
+    V[(size_t)f * csz + (size_t)cy * cw + cx] = vo;
+}
+
+// ---------------------------------------------------------------------------
+// Analysis (analysis.rs:964): one wave per MB.  Lanes 0..31: luma (mode DC/TM
+// x 16 blocks), lanes 32..47: chroma (mode x 8 blocks).  Predictors use source
+// pixels; on the MB-padded planes libwebp's import/replicate rules reduce to
+// direct reads (analysis.rs:520-745).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fdct_analysis(int* d, int16_t* out)
+{
+    int tmp[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int d0 = d[i * 4], d1 = d[i * 4 + 1], d2 = d[i * 4 + 2], d3 = d[i * 4 + 3];
+        int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+        tmp[0 + i * 4] = (a0 + a1) * 8;
+        tmp[2 + i * 4] = (a0 - a1) * 8;
+        tmp[1 + i * 4] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
+        tmp[3 + i * 4] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int a0 = tmp[i] + tmp[12 + i], a1 = tmp[4 + i] + tmp[8 + i];
+        int a2 = tmp[4 + i] - tmp[8 + i], a3 = tmp[i] - tmp[12 + i];
+        out[i] = (int16_t)((a0 + a1 + 7) >> 4);
+        out[8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
+        out[4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0 ? 1 : 0));
+        out[12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
+                                                             const uint8_t* __restrict__ V, int mbw, int mbh,
+                                                             size_t ysz, size_t csz, uint8_t* __restrict__ alpha,
+                                                             uint32_t* __restrict__ histo)
+{
+    __shared__ uint32_t hist[4][4][32];  // [wave][histogram][bin]
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int mb = blockIdx.x * 4 + wv;
+    const int nmb = mbw * mbh;
+    for (int i = lane; i < 128; i += 64) (&hist[wv][0][0])[i] = 0;
+    wsync();
+    if (mb < nmb) {
+        const int mbx = mb % mbw, mby = mb / mbw;
+        const int ys = mbw * 16, cs = mbw * 8;
+        const uint8_t* Yf = Y + (size_t)f * ysz;
+        const uint8_t* Uf = U + (size_t)f * csz;
+        const uint8_t* Vf = V + (size_t)f * csz;
+        if (lane < 48) {
+            const bool luma = lane < 32;
+            const int mode = luma ? (lane >> 4) : ((lane - 32) >> 3);
+            const int b = luma ? (lane & 15) : ((lane - 32) & 7);
+            const int size = luma ? 16 : 8;
+            const uint8_t* P = luma ? Yf : (b < 4 ? Uf : Vf);
+            const int st = luma ? ys : cs;
+            const int bb = luma ? b : (b & 3);
+            const int bx = luma ? (bb & 3) : (bb & 1), by = luma ? (bb >> 2) : (bb >> 1);
+            const int ox = mbx * size, oy = mby * size;
+            const bool ht = mby > 0, hl = mbx > 0;
+            // predictor value at (r, c) of the MB
+            int dcv = 0x80;
+            {
+                uint32_t s = 0;
+                if (ht && hl) {
+                    for (int i = 0; i < size; i++) s += P[(size_t)(oy - 1) * st + ox + i] + P[(size_t)(oy + i) * st + ox - 1];
+                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
+                } else if (ht) {
+                    for (int i = 0; i < size; i++) s += P[(size_t)(oy - 1) * st + ox + i];
+                    s += s;
+                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
+                } else if (hl) {
+                    for (int i = 0; i < size; i++) s += P[(size_t)(oy + i) * st + ox - 1];
+                    s += s;
+                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
+                }
+            }
+            const int corner = (ht && hl) ? P[(size_t)(oy - 1) * st + ox - 1] : 0;
+            int d[16];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int r = by * 4 + i, c = bx * 4 + j;
+                    const int s = P[(size_t)(oy + r) * st + ox + c];
+                    int p;
+                    if (mode == 0) p = dcv;
+                    else if (ht && hl) p = clamp255(P[(size_t)(oy + r) * st + ox - 1] + P[(size_t)(oy - 1) * st + ox + c] - corner);
+                    else if (hl) p = P[(size_t)(oy + r) * st + ox - 1];
+                    else if (ht) p = P[(size_t)(oy - 1) * st + ox + c];
+                    else p = 129;
+                    d[i * 4 + j] = s - p;
+                }
+            int16_t o[16];
+            fdct_analysis(d, o);
+            const int hidx = luma ? mode : 2 + mode;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                int v = iabs(o[k]) >> 3;
+                atomicAdd(&hist[wv][hidx][v < 31 ? v : 31], 1u);
+            }
+        }
+        wsync();
+        int a = 0;
+        if (lane < 4) {
+            uint32_t mx = 0;
+            int lnz = 1;
+            for (int k = 0; k < 32; k++) {
+                uint32_t c = hist[wv][lane][k];
+                if (c > 0) {
+                    if (c > mx) mx = c;
+                    lnz = k;
+                }
+            }
+            a = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
+        }
+        const int a0 = __shfl(a, 0), a1 = __shfl(a, 1), a2 = __shfl(a, 2), a3 = __shfl(a, 3);
+        if (lane == 0) {
+            int best = max(-1, max(a0, a1));
+            int buv = max(-1, max(a2, a3));
+            int al = (3 * best + buv + 2) >> 2;
+            al = 255 - al;
+            al = al < 0 ? 0 : (al > 255 ? 255 : al);
+            alpha[(size_t)f * nmb + mb] = (uint8_t)al;
+            atomicAdd(&histo[(size_t)f * 256 + al], 1u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Segments: one thread per frame.  k-means over the alpha histogram
+// (assign_segments_kmeans analysis.rs:1029), per-segment quant via the
+// reference's f64 fast_math pow (compute_segment_quant :1145; this file is
+// built with -ffp-contract=off), matrices/lambdas (Segment::init_matrices
+// types.rs:806), segment tree probabilities (vp8.rs:2340-2368).
+// ---------------------------------------------------------------------------
+__device__ double fm_log2(double x)
+{
+    unsigned long long bits = __double_as_longlong(x);
+    long long e = (long long)((bits >> 52) & 0x7FF) - 1023;
+    unsigned long long mb = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m = __longlong_as_double((long long)mb);
+    double y = (m - 1.0) / (m + 1.0);
+    double y2 = y * y;
+    const double C0 = 2.8853900817779268, C1 = 0.9617966939259756, C2 = 0.5770780163555854,
+                 C3 = 0.4121985831111324, C4 = 0.3205988987531030;
+    double poly = C0 + y2 * (C1 + y2 * (C2 + y2 * (C3 + y2 * C4)));
+    return (double)e + y * poly;
+}
+__device__ double fm_exp2(double x)
+{
+    if (x < -1022.0) x = -1022.0;
+    if (x > 1023.0) x = 1023.0;
+    long long xi = x >= 0.0 ? (long long)x : (long long)x - 1;
+    double xf = x - (double)xi;
+    const double LN2 = 0.6931471805599453;
+    const double C1 = LN2, C2 = LN2 * LN2 / 2.0, C3 = LN2 * LN2 * LN2 / 6.0, C4 = LN2 * LN2 * LN2 * LN2 / 24.0,
+                 C5 = LN2 * LN2 * LN2 * LN2 * LN2 / 120.0;
+    double poly = 1.0 + xf * (C1 + xf * (C2 + xf * (C3 + xf * (C4 + xf * C5))));
+    double scale = __longlong_as_double((long long)((unsigned long long)(xi + 1023) << 52));
+    return poly * scale;
+}
+__device__ double fm_pow(double x, double n)
+{
+    if (x <= 0.0) return 0.0;
+    if (x == 1.0 || n == 0.0) return 1.0;
+    if (n == 1.0) return x;
+    return fm_exp2(n * fm_log2(x));
+}
+__device__ int segment_quant(int base, int alpha, int sns)
+{
+    double amp = 0.9 * (double)sns / 100.0 / 128.0;
+    double expn = 1.0 - amp * (double)alpha;
+    if (expn <= 0.0) return base;
+    double cb = 1.0 - ((double)base / 127.0);
+    double c = fm_pow(cb, expn);
+    int q = (int)(127.0 * (1.0 - c));
+    return q < 0 ? 0 : (q > 127 ? 127 : q);
+}
+
+__device__ void matrix_init(ZwMatrix& m, int qdc, int qac, int bdc, int bac)
+{
+    m.q[0] = (uint32_t)qdc;
+    m.q[1] = (uint32_t)qac;
+    for (int i = 0; i < 2; i++) {
+        uint32_t b = i ? bac : bdc;
+        m.iq[i] = (1u << 17) / m.q[i];
+        m.bias[i] = ((b << 17) + 128) >> 8;
+        m.zthresh[i] = ((1u << 17) - 1 - m.bias[i]) / m.iq[i];
+    }
+}
+
+__device__ void segment_init(ZwSegment& s, int qi, int delta)
+{
+    int ydc = d_DC_QUANT[qi], yac = d_AC_QUANT[qi];
+    int y2dc = d_DC_QUANT[qi] * 2;
+    int y2ac = (int)d_AC_QUANT[qi] * 155 / 100;
+    if (y2ac < 8) y2ac = 8;
+    int uvdc = d_DC_QUANT[qi], uvac = d_AC_QUANT[qi];
+    matrix_init(s.y1, ydc, yac, 96, 110);
+    matrix_init(s.y2, y2dc, y2ac, 96, 108);
+    matrix_init(s.uv, uvdc, uvac, 110, 115);
+    for (int i = 0; i < 16; i++) {
+        uint32_t q = i == 0 ? (uint32_t)ydc : (uint32_t)yac;
+        s.sharpen[i] = (uint16_t)(((uint32_t)d_VP8_FREQ_SHARPENING[i] * q) >> 11);
+    }
+    uint32_t qi4 = ((uint32_t)ydc + 15u * (uint32_t)yac + 8) >> 4;
+    uint32_t qi16 = ((uint32_t)y2dc + 15u * (uint32_t)y2ac + 8) >> 4;
+    uint32_t quv = ((uint32_t)uvdc + 15u * (uint32_t)uvac + 8) >> 4;
+#define MAX1(v) ((v) ? (v) : 1u)
+    s.lt_i4 = MAX1((7 * qi4 * qi4) >> 3);
+    s.lt_i16 = MAX1((qi16 * qi16) >> 2);
+    s.lt_uv = MAX1((quv * quv) << 1);
+    s.l_i4 = MAX1((3 * qi4 * qi4) >> 7);
+    s.l_i16 = MAX1(3 * qi16 * qi16);
+    s.l_uv = MAX1((3 * quv * quv) >> 6);
+    s.l_mode = MAX1((qi4 * qi4) >> 7);
+#undef MAX1
+    s.tlambda = (50 * qi4) >> 5;
+    s.quant_index = qi;
+    s.quantizer_level = delta;
+}
+
+extern "C" __global__ void k_segments(const uint32_t* __restrict__ histo, const ZwFrameParams* __restrict__ tmpl,
+                                      ZwFrameParams* __restrict__ params, int nframes)
+{
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    ZwFrameParams P = *tmpl;
+    const int base = P.base_qi;
+    const int nmb = P.mbw * P.mbh;
+    for (int i = 0; i < 4; i++) segment_init(P.seg[i], base, 0);
+    for (int i = 0; i < 256; i++) P.seg_map_lut[i] = 0;
+    P.seg_probs[0] = P.seg_probs[1] = P.seg_probs[2] = 255;
+    P.seg_enabled = 0;
+    P.seg_update_map = 0;
+    if (nmb >= 256) {
+        const uint32_t* H = histo + (size_t)f * 256;
+        uint8_t centers[4] = {0, 0, 0, 0};
+        uint8_t* map = P.seg_map_lut;
+        int min_a = 0, max_a = 255;
+        for (int n = 0; n < 256; n++)
+            if (H[n] > 0) { min_a = n; break; }
+        for (int n = 255; n >= min_a; n--)
+            if (H[n] > 0) { max_a = n; break; }
+        int range = max_a > min_a ? max_a - min_a : 0;
+        for (int k = 0; k < 4; k++) centers[k] = (uint8_t)(min_a + ((1 + 2 * k) * range) / 8);
+        uint32_t accum[4], dacc[4];
+        int wa = 0;
+        uint32_t tw = 0;
+        for (int it = 0; it < 6; it++) {
+            for (int i = 0; i < 4; i++) accum[i] = dacc[i] = 0;
+            int cc = 0;
+            for (int a = min_a; a <= max_a; a++) {
+                if (H[a] > 0) {
+                    while (cc + 1 < 4) {
+                        int dc = iabs(a - centers[cc]), dn = iabs(a - centers[cc + 1]);
+                        if (dn < dc) cc++;
+                        else break;
+                    }
+                    map[a] = (uint8_t)cc;
+                    dacc[cc] += (uint32_t)a * H[a];
+                    accum[cc] += H[a];
+                }
+            }
+            int displaced = 0;
+            wa = 0;
+            tw = 0;
+            for (int n = 0; n < 4; n++) {
+                if (accum[n] > 0) {
+                    uint8_t nc = (uint8_t)((dacc[n] + accum[n] / 2) / accum[n]);
+                    displaced += iabs(centers[n] - nc);
+                    centers[n] = nc;
+                    wa += (int)nc * (int)accum[n];
+                    tw += accum[n];
+                }
+            }
+            if (displaced < 5) break;
+        }
+        int mid = tw > 0 ? (wa + (int)tw / 2) / (int)tw : 128;
+        int minc = centers[0], maxc = centers[0];
+        for (int i = 1; i < 4; i++) {
+            minc = min(minc, (int)centers[i]);
+            maxc = max(maxc, (int)centers[i]);
+        }
+        int rng = maxc == minc ? 1 : maxc - minc;
+        for (int s = 0; s < 4; s++) {
+            int ta = 255 * ((int)centers[s] - mid) / rng;
+            ta = ta < -127 ? -127 : (ta > 127 ? 127 : ta);
+            int sq = segment_quant(base, ta, 50);
+            int delta = (int)(int8_t)((int8_t)sq - (int8_t)base);
+            segment_init(P.seg[s], sq, delta);
+        }
+        uint32_t cnt[4] = {0, 0, 0, 0};
+        for (int a = 0; a < 256; a++) cnt[map[a]] += H[a];
+        uint32_t t01 = cnt[0] + cnt[1], t23 = cnt[2] + cnt[3];
+#define GETP(a, b) ((a) + (b) == 0 ? 255 : (uint8_t)((255 * (a) + ((a) + (b)) / 2) / ((a) + (b))))
+        P.seg_probs[0] = GETP(t01, t23);
+        P.seg_probs[1] = GETP(cnt[0], cnt[1]);
+        P.seg_probs[2] = GETP(cnt[2], cnt[3]);
+#undef GETP
+        P.seg_update_map = P.seg_probs[0] != 255 || P.seg_probs[1] != 255 || P.seg_probs[2] != 255;
+        P.seg_enabled = 1;
+    }
+    params[f] = P;
+}
+
+// ---------------------------------------------------------------------------
+// The encode pass.
+// ---------------------------------------------------------------------------
+struct EncArgs {
+    const uint8_t *Y, *U, *V;
+    const uint8_t* alpha;       // per MB (segment lookup)
+    const ZwFrameParams* params;
+    const ZwLevelCosts* lcost;  // per frame; null in pass 1 (all-zero tables, quirk A2)
+    int8_t* derr;               // [nframes][mbw][4] top_derr: pass 1 writes, pass 2 reads
+    ZwMbOut* out;
+    uint8_t *ry, *ru, *rv;      // reconstruction (pass 2), may be null
+    size_t ysz, csz;
+    int mbw, mbh, pass;
+};
+
+// per-wave LDS scratch
+struct WaveLds {
+    uint8_t ws[17 * ZW_BPS];      // luma work buffer (create_border_luma layout)
+    uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
+    uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
+    int8_t left_derr[4];
+    int dc[64];
+    int y2d[64];
+    int y2cost[4];
+    int V[40];
+    uint8_t pred[10][16];
+    uint32_t msse[12];
+    int cand[12];
+    int cres[10][24];             // per I4 candidate: score lo/hi, sse, rate, hnz, q[16]
+    int nzt[4], nzl[4];
+    uint8_t modes[16];
+    int16_t lev[25][16];
+    int misc[16];
+};
+
+struct SharedHdr {
+    int progress[NW];
+};
+
+struct Ctx {
+    const EncArgs* a;
+    const ZwFrameParams* P;
+    const ZwSegment* S;
+    const LdsTables* T;
+    WaveLds* W;
+    uint8_t *top_y, *top_u, *top_v, *top_c;
+    int8_t* top_derr;
+    const uint8_t *srcY, *srcU, *srcV;  // MB origin
+    int ys, cs;
+    int mbx, mby, lane, seg;
+};
+
+// create_border_luma (prediction.rs:15) into W->ws
+__device__ void build_luma_border(const Ctx& C)
+{
+    uint8_t* ws = C.W->ws;
+    const int l = C.lane;
+    const int mbw = C.a->mbw;
+    // row 0 entries 0..31
+    if (l < 32) {
+        int v;
+        if (l == 0) v = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : C.W->left_y[0]);
+        else if (C.mby == 0) v = 127;
+        else if (l <= 16) v = C.top_y[C.mbx * 16 + l - 1];
+        else if (C.mbx == mbw - 1) v = C.top_y[C.mbx * 16 + 15];
+        else v = C.top_y[C.mbx * 16 + l - 1];
+        ws[l] = (uint8_t)v;
+        if (l >= 17 && l < 21) {
+            ws[4 * ZW_BPS + l] = (uint8_t)v;
+            ws[8 * ZW_BPS + l] = (uint8_t)v;
+            ws[12 * ZW_BPS + l] = (uint8_t)v;
+        }
+    } else if (l < 48) {
+        int i = l - 32;
+        ws[(i + 1) * ZW_BPS] = C.mbx == 0 ? 129 : C.W->left_y[1 + i];
+    }
+    wsync();
+}
+
+// create_border_chroma (prediction.rs:85) into cu / cv
+__device__ void build_chroma_border(const Ctx& C)
+{
+    const int l = C.lane;
+    if (l < 36) {
+        const int pl = l >= 18;
+        const int i = pl ? l - 18 : l;
+        uint8_t* w = pl ? C.W->cv : C.W->cu;
+        const uint8_t* top = pl ? C.top_v : C.top_u;
+        const uint8_t* left = pl ? C.W->left_v : C.W->left_u;
+        if (i == 0) w[0] = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : left[0]);
+        else if (i <= 8) w[i] = C.mby == 0 ? 127 : top[C.mbx * 8 + i - 1];
+        else w[(i - 8) * ZW_BPS] = C.mbx == 0 ? 129 : left[i - 8];
+    }
+    wsync();
+}
+
+// pick_best_intra16 (vp8.rs:1504-1687).  lane = mode*16 + block.
+__device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_score)
+{
+    const int lane = C.lane, m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+    WaveLds* W = C.W;
+    const uint8_t* ws = W->ws;
+    const ZwSegment& S = *C.S;
+    const int above = C.mby != 0, left = C.mbx != 0;
+    int s = 0;
+    if (lane < 16) s = above ? ws[1 + lane] : 0;
+    else if (lane < 32) s = left ? ws[(lane - 15) * ZW_BPS] : 0;
+    s = wave_sum(s);
+    const int shf = 3 + above + left;
+    const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
+    int src[16], pr[16], r[16];
+    const int P0 = ws[0];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int y = by * 4 + i, x = bx * 4 + j;
+            const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
+            int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - P0)));
+            const int sv = C.srcY[(size_t)y * C.ys + x];
+            src[i * 4 + j] = sv;
+            pr[i * 4 + j] = p;
+            r[i * 4 + j] = sv - p;
+        }
+    fdct16(r);
+    W->dc[m * 16 + b] = r[0];
+    int q[16];
+    q[0] = 0;
+    int nzac = 0;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+        q[k] = quantz(r[k], S.y1.iq[1], S.y1.bias[1]);
+        nzac |= q[k] != 0;
+    }
+    int cost = (int)rcost<1>(q, 0, 0, C.T);
+    wsync();
+    if (b == 0) {
+        int d[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k] = W->dc[m * 16 + k];
+        wht16(d);
+        int y2q[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) y2q[k] = quantz(d[k], S.y2.iq[k > 0], S.y2.bias[k > 0]);
+        W->y2cost[m] = (int)rcost<0>(y2q, 0, 1, C.T);
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k] = y2q[k] * (int)S.y2.q[k > 0];
+        iwht16(d);
+#pragma unroll
+        for (int k = 0; k < 16; k++) W->y2d[m * 16 + k] = d[k];
+    }
+    wsync();
+    int dq[16];
+    dq[0] = W->y2d[m * 16 + b];
+#pragma unroll
+    for (int k = 1; k < 16; k++) dq[k] = q[k] * (int)S.y1.q[1];
+    idct16(dq);
+    int rec[16], sse = 0, flat = 1;
+    const int s00 = C.srcY[0];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        rec[k] = clamp255(pr[k] + dq[k]);
+        const int d = src[k] - rec[k];
+        sse += d * d;
+        flat &= src[k] == s00;
+    }
+    int td = iabs(ttransform(rec) - ttransform(src)) >> 5;
+    sse = red16(sse);
+    td = red16(td);
+    cost = red16(cost);
+    nzac = red16(nzac);
+    flat = red16(flat);
+    // per mode (uniform within the 16-lane group)
+    const int srcflat = __shfl(flat, 0) == 16;  // mode-0 group covers all 256 pixels
+    cost += W->y2cost[m];
+    int sd = S.tlambda > 0 ? ((int)S.tlambda * td + 128) >> 8 : 0;
+    int dfin = sse;
+    if (srcflat && nzac == 0) {
+        dfin = sse * 2;
+        sd = sd * 2;
+    }
+    const long long mc = d_FIXED_COSTS_I16[m];
+    const long long rd = (mc + cost) * (long long)S.l_i16 + 256LL * ((long long)dfin + sd);
+    const long long fin = (mc + cost) * (long long)S.l_mode + 256LL * ((long long)dfin + sd);
+    long long brd = 0x7fffffffffffffffLL, bfin = 0;
+    int bm = 0;
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++) {
+        const long long r_m = shfl64(rd, mm * 16);
+        const long long f_m = shfl64(fin, mm * 16);
+        const int avail = mm == 0 || (mm == 1 && above) || (mm == 2 && left) || (mm == 3 && above && left);
+        if (avail && r_m < brd) {
+            brd = r_m;
+            bfin = f_m;
+            bm = mm;
+        }
+    }
+    best_mode = bm;
+    best_score = bfin < 0 ? 0ull : (unsigned long long)bfin;
+}
+
+// Fill the I4 value vector V (and DC) for sub-block (x0, y0) of W->ws.
+__device__ void i4_values(const Ctx& C, int x0, int y0)
+{
+    WaveLds* W = C.W;
+    const uint8_t* ws = W->ws;
+    const int l = C.lane;
+    auto E = [&](int k) -> int {  // [L3 L2 L1 L0 P A0..A7]
+        if (k < 4) return ws[(y0 + 3 - k) * ZW_BPS + x0 - 1];
+        if (k == 4) return ws[(y0 - 1) * ZW_BPS + x0 - 1];
+        return ws[(y0 - 1) * ZW_BPS + x0 + (k - 5)];
+    };
+    if (l < 13) W->V[l] = E(l);
+    else if (l < 24) { int k = l - 13; W->V[l] = (E(k) + 2 * E(k + 1) + E(k + 2) + 2) >> 2; }
+    else if (l < 36) { int k = l - 24; W->V[l] = (E(k) + E(k + 1) + 1) >> 1; }
+    else if (l == 36) W->V[36] = (E(11) + 2 * E(12) + E(12) + 2) >> 2;
+    else if (l == 37) W->V[37] = (E(1) + 2 * E(0) + E(0) + 2) >> 2;
+    else if (l == 38) {
+        int v = 4;
+        for (int k = 0; k < 4; k++) v += E(k) + E(5 + k);
+        W->V[38] = v >> 3;
+    }
+    wsync();
+}
+__device__ __forceinline__ int i4_pred_px(const WaveLds* W, int mode, int p)
+{
+    const int idx = d_I4_IDX[mode][p];
+    if (idx == 255) return W->V[38];
+    if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
+    return W->V[idx];
+}
+
+__device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rate, uint32_t lambda)
+{
+    return (unsigned long long)sse * 256ull + (unsigned long long)(uint16_t)rate * lambda;
+}
+
+// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
+__device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const int l = C.lane;
+    const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
+    unsigned long long running = 211ull * S.l_mode;
+    uint32_t total_mc = 0;
+    int top_nz[4] = {0, 0, 0, 0}, left_nz[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; i++) {
+        const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
+        const int tctx = sby == 0 ? 0 : W->modes[i - 4];
+        const int lctx = sbx == 0 ? 0 : W->modes[i - 1];
+        const int nzt = sby == 0 ? 0 : top_nz[sbx];
+        const int nzl = sbx == 0 ? 0 : left_nz[sby];
+        i4_values(C, x0, y0);
+        // predictions + SSE: lane = g*16 + p, modes g, g+4, g+8
+        {
+            const int g = l >> 4, p = l & 15;
+            const int sv = C.srcY[(size_t)(sby * 4 + (p >> 2)) * C.ys + sbx * 4 + (p & 3)];
+#pragma unroll
+            for (int t = 0; t < 3; t++) {
+                const int mm = g + 4 * t;
+                int e = 0;
+                if (mm < 10) {
+                    const int v = i4_pred_px(W, mm, p);
+                    W->pred[mm][p] = (uint8_t)v;
+                    e = (sv - v) * (sv - v);
+                }
+                e = red16(e);
+                if (p == 0 && mm < 10) W->msse[mm] = (uint32_t)e;
+            }
+        }
+        wsync();
+        if (l < 10) {
+            const uint32_t me = W->msse[l];
+            int rank = 0;
+            for (int o = 0; o < 10; o++) {
+                const uint32_t oe = W->msse[o];
+                rank += (oe < me) || (oe == me && o < l);
+            }
+            W->cand[rank] = l;
+        }
+        wsync();
+        if (l < K) {
+            const int mm = W->cand[l];
+            int src[16], r[16], q[16];
+            const uint8_t* sp = C.srcY + (size_t)(sby * 4) * C.ys + sbx * 4;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                src[k] = sp[(size_t)(k >> 2) * C.ys + (k & 3)];
+                r[k] = src[k] - W->pred[mm][k];
+            }
+            fdct16(r);
+            int hnz = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                q[k] = quantz(r[k], S.y1.iq[k > 0], S.y1.bias[k > 0]);
+                hnz |= q[k] != 0;
+            }
+            const uint32_t cc = rcost<0>(q, nzt + nzl, 3, C.T);
+            int dq[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) dq[k] = q[k] * (int)S.y1.q[k > 0];
+            idct16(dq);
+            uint32_t sse = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int d = src[k] - clamp255(W->pred[mm][k] + dq[k]);
+                sse += (uint32_t)(d * d);
+            }
+            const uint32_t rate = (uint32_t)d_VP8_FIXED_COSTS_I4[tctx][lctx][mm] + cc;
+            const unsigned long long sc = rdscore(sse, rate, S.l_i4);
+            int* R = W->cres[l];
+            R[0] = (int)(sc & 0xffffffff);
+            R[1] = (int)(sc >> 32);
+            R[2] = (int)sse;
+            R[3] = (int)rate;
+            R[4] = hnz;
+#pragma unroll
+            for (int k = 0; k < 16; k++) R[5 + k] = dq[k];
+        }
+        wsync();
+        // best candidate in rank order (strict <)
+        unsigned long long bs = ~0ull;
+        int bk = 0;
+        for (int k = 0; k < K; k++) {
+            const unsigned long long sc = ((unsigned long long)(unsigned)W->cres[k][1] << 32) | (unsigned)W->cres[k][0];
+            if (sc < bs) {
+                bs = sc;
+                bk = k;
+            }
+        }
+        const int bmode = W->cand[bk];
+        const int bnz = W->cres[bk][4];
+        top_nz[sbx] = bnz;
+        left_nz[sby] = bnz;
+        total_mc += d_VP8_FIXED_COSTS_I4[tctx][lctx][bmode];
+        running += rdscore((uint32_t)W->cres[bk][2], (uint32_t)W->cres[bk][3], S.l_mode);
+        if (l == 0) W->modes[i] = (uint8_t)bmode;
+        if (running >= i16_score) { wsync(); return false; }
+        if (total_mc > 256u * 16u * 16u / 4u) { wsync(); return false; }
+        if (l < 16) {
+            const int p = l;
+            W->ws[(y0 + (p >> 2)) * ZW_BPS + x0 + (p & 3)] = (uint8_t)clamp255(W->pred[bmode][p] + W->cres[bk][5 + p]);
+        }
+        wsync();
+    }
+    return true;
+}
+
+// pick_best_uv (vp8.rs:2050-2200): lane = mode*8 + block (U 0..3, V 4..7).
+__device__ int pick_uv(const Ctx& C)
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const int l = C.lane;
+    const int above = C.mby != 0, left = C.mbx != 0;
+    long long rd = 0x7fffffffffffffffLL;
+    if (l < 32) {
+        const int m = l >> 3, b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
+        const uint8_t* w = pl ? W->cv : W->cu;
+        const uint8_t* sp = (pl ? C.srcV : C.srcU) + (size_t)(by * 4) * C.cs + bx * 4;
+        int dcv = 128;
+        {
+            uint32_t s = 0;
+            int shf = 2;
+            if (left) {
+                for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
+                shf++;
+            }
+            if (above) {
+                for (int x = 1; x <= 8; x++) s += w[x];
+                shf++;
+            }
+            if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
+        }
+        int src[16], pr[16], r[16], q[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int y = by * 4 + i, x = bx * 4 + j;
+                const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
+                const int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - w[0])));
+                const int sv = sp[(size_t)i * C.cs + j];
+                src[i * 4 + j] = sv;
+                pr[i * 4 + j] = p;
+                r[i * 4 + j] = sv - p;
+            }
+        fdct16(r);
+        int nzac = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            q[k] = quantz(r[k], S.uv.iq[k > 0], S.uv.bias[k > 0]);
+            if (k > 0) nzac += q[k] != 0;
+        }
+        int cost = (int)rcost<0>(q, 0, 2, C.T);
+#pragma unroll
+        for (int k = 0; k < 16; k++) r[k] = q[k] * (int)S.uv.q[k > 0];
+        idct16(r);
+        int sse = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int d = src[k] - clamp255(pr[k] + r[k]);
+            sse += d * d;
+        }
+        sse = red8(sse);
+        cost = red8(cost);
+        nzac = red8(nzac);
+        const int pen = (m > 0 && nzac <= 2) ? 140 * 8 : 0;
+        rd = ((long long)d_FIXED_COSTS_UV[m] + cost + pen) * (long long)S.l_uv + 256LL * sse;
+    }
+    long long brd = 0x7fffffffffffffffLL;
+    int bm = 0;
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++) {
+        const long long r_m = shfl64(rd, mm * 8);
+        const int avail = mm == 0 || (mm == 1 && above) || (mm == 2 && left) || (mm == 3 && above && left);
+        if (avail && r_m < brd) {
+            brd = r_m;
+            bm = mm;
+        }
+    }
+    return bm;
+}
+
+// Final luma transform (transform_luma_block vp8.rs:2647 / _4x4 :2785).
+// Writes zigzag levels to W->lev[0..16], recon into W->ws.  Returns the
+// simple-quant "any nonzero" flag for skip detection (check_all_coeffs_zero).
+__device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const int l = C.lane;
+    int anynz = 0;
+    if (mode != 4) {
+        build_luma_border(C);
+        const uint8_t* ws = W->ws;
+        const int above = C.mby != 0, left = C.mbx != 0;
+        int s = 0;
+        if (l < 16) s = above ? ws[1 + l] : 0;
+        else if (l < 32) s = left ? ws[(l - 15) * ZW_BPS] : 0;
+        s = wave_sum(s);
+        const int shf = 3 + above + left;
+        const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
+        int c[16], pr[16];
+        const int b = l & 15, bx = b & 3, by = b >> 2;
+        if (l < 16) {
+            const int P0 = ws[0];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int y = by * 4 + i, x = bx * 4 + j;
+                    const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
+                    const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - P0)));
+                    pr[i * 4 + j] = p;
+                    c[i * 4 + j] = (int)C.srcY[(size_t)y * C.ys + x] - p;
+                }
+            fdct16(c);
+            W->dc[b] = c[0];
+        }
+        wsync();
+        if (l == 0) {
+            int d[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) d[k] = W->dc[k];
+            wht16(d);
+            int y2q[16];
+            int nz = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                y2q[k] = quantz(d[k], S.y2.iq[k > 0], S.y2.bias[k > 0]);
+                nz |= y2q[k] != 0;
+            }
+#pragma unroll
+            for (int n = 0; n < 16; n++) W->lev[16][n] = (int16_t)y2q[d_ZIGZAG[n]];
+#pragma unroll
+            for (int k = 0; k < 16; k++) d[k] = y2q[k] * (int)S.y2.q[k > 0];
+            iwht16(d);
+#pragma unroll
+            for (int k = 0; k < 16; k++) W->y2d[k] = d[k];
+            W->misc[0] = nz;
+            for (int k = 0; k < 4; k++) {
+                W->nzt[k] = C.top_c[C.mbx * 12 + 1 + k];
+                W->nzl[k] = W->left_c[1 + k];
+            }
+        }
+        wsync();
+        anynz = W->misc[0];
+        int dq[16], lv[16];
+        int nzb = 0;
+        {
+            // simple-quant check on the AC coefficients (check_all_coeffs_zero)
+            int snz = 0;
+            if (l < 16) {
+#pragma unroll
+                for (int k = 1; k < 16; k++) snz |= quantz(c[k], S.y1.iq[1], S.y1.bias[1]) != 0;
+            }
+            anynz |= __any(snz) ? 1 : 0;
+        }
+        if (trel) {
+            for (int t = 0; t < 7; t++) {
+                if (l < 16 && bx + by == t) {
+                    int ctx0 = W->nzl[by] + W->nzt[bx];
+                    ctx0 = ctx0 > 2 ? 2 : ctx0;
+#pragma unroll
+                    for (int k = 0; k < 16; k++) dq[k] = c[k];
+                    nzb = trellis<1>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, ctx0);
+                    W->nzt[bx] = nzb;
+                    W->nzl[by] = nzb;
+                }
+                wsync();
+            }
+        } else if (l < 16) {
+#pragma unroll
+            for (int n = 1; n < 16; n++) {
+                const int j = d_ZIGZAG[n];
+                lv[n] = quantz(c[j], S.y1.iq[1], S.y1.bias[1]);
+                nzb |= lv[n] != 0;
+            }
+            dq[0] = 0;
+#pragma unroll
+            for (int n = 1; n < 16; n++) dq[d_ZIGZAG[n]] = lv[n] * (int)S.y1.q[1];
+        }
+        wsync();
+        if (l < 16) {
+            lv[0] = 0;
+#pragma unroll
+            for (int n = 0; n < 16; n++) W->lev[b][n] = (int16_t)lv[n];
+            dq[0] = W->y2d[b];
+            idct16(dq);
+            uint8_t* wsp = W->ws;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+                wsp[(y + 1) * ZW_BPS + 1 + x] = (uint8_t)clamp255(pr[k] + dq[k]);
+            }
+        }
+        for (int k = 0; k < 16; k++) y_nz_out[k] = __shfl(nzb, k);
+        wsync();
+    } else {
+        build_luma_border(C);
+        int top_nz[4], left_nz[4];
+        for (int k = 0; k < 4; k++) {
+            top_nz[k] = C.top_c[C.mbx * 12 + 1 + k];
+            left_nz[k] = W->left_c[1 + k];
+        }
+        for (int i = 0; i < 16; i++) {
+            const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
+            const int bm = W->modes[i];
+            i4_values(C, x0, y0);
+            if (l < 16) W->pred[0][l] = (uint8_t)i4_pred_px(W, bm, l);
+            wsync();
+            if (l == 0) {
+                int c[16], pr[16], lv[16];
+                const uint8_t* sp = C.srcY + (size_t)(sby * 4) * C.ys + sbx * 4;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    pr[k] = W->pred[0][k];
+                    c[k] = (int)sp[(size_t)(k >> 2) * C.ys + (k & 3)] - pr[k];
+                }
+                fdct16(c);
+                int snz = 0;
+#pragma unroll
+                for (int k = 0; k < 16; k++) snz |= quantz(c[k], S.y1.iq[k > 0], S.y1.bias[k > 0]) != 0;
+                int nz = 0;
+                if (trel) {
+                    int ctx0 = left_nz[sby] + top_nz[sbx];
+                    ctx0 = ctx0 > 2 ? 2 : ctx0;
+                    nz = trellis<0>(c, lv, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0);
+                } else {
+#pragma unroll
+                    for (int n = 0; n < 16; n++) {
+                        const int j = d_ZIGZAG[n];
+                        lv[n] = quantz(c[j], S.y1.iq[j > 0], S.y1.bias[j > 0]);
+                        nz |= lv[n] != 0;
+                    }
+#pragma unroll
+                    for (int n = 0; n < 16; n++) {
+                        const int j = d_ZIGZAG[n];
+                        c[j] = lv[n] * (int)S.y1.q[j > 0];
+                    }
+                }
+#pragma unroll
+                for (int n = 0; n < 16; n++) W->lev[i][n] = (int16_t)lv[n];
+                idct16(c);
+#pragma unroll
+                for (int k = 0; k < 16; k++) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pr[k] + c[k]);
+                W->misc[1] = nz;
+                W->misc[2] = snz;
+            }
+            wsync();
+            const int nz = W->misc[1];
+            anynz |= W->misc[2];
+            top_nz[sbx] = nz;
+            left_nz[sby] = nz;
+            y_nz_out[i] = nz;
+            wsync();
+        }
+        if (l < 16) W->lev[16][l] = 0;
+        wsync();
+    }
+    return anynz;
+}
+
+// Final chroma transform with error diffusion (transform_chroma_blocks
+// vp8.rs:3039, apply_chroma_error_diffusion :572).  Levels to W->lev[17..24],
+// recon into cu/cv.  Returns the simple-quant "any nonzero" flag; uv_nz[8]
+// receives per-block has-coefficients.
+__device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[8])
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const int l = C.lane;
+    const int above = C.mby != 0, left = C.mbx != 0;
+    int c[16], pr[16];
+    const int b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
+    if (l < 8) {
+        const uint8_t* w = pl ? W->cv : W->cu;
+        const uint8_t* sp = (pl ? C.srcV : C.srcU) + (size_t)(by * 4) * C.cs + bx * 4;
+        int dcv = 128;
+        {
+            uint32_t s = 0;
+            int shf = 2;
+            if (left) {
+                for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
+                shf++;
+            }
+            if (above) {
+                for (int x = 1; x <= 8; x++) s += w[x];
+                shf++;
+            }
+            if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int y = by * 4 + i, x = bx * 4 + j;
+                const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
+                const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - w[0])));
+                pr[i * 4 + j] = p;
+                c[i * 4 + j] = (int)sp[(size_t)i * C.cs + j] - p;
+            }
+        fdct16(c);
+        W->dc[b] = c[0];
+    }
+    wsync();
+    if (l == 0 || l == 4) {
+        const int ch = l >> 2;
+        const int q = (int)S.uv.q[0];
+        const uint32_t iq = S.uv.iq[0], bias = S.uv.bias[0];
+        const uint32_t zt = ((1u << 17) - 1 - bias) / iq;
+        int8_t* top = top_derr + ch * 2;
+        int8_t* lft = W->left_derr + ch * 2;
+        auto diffuse = [&](int k, int te, int le) -> int {
+            int dc = W->dc[ch * 4 + k] + ((7 * te + 8 * le) >> 3);
+            W->dc[ch * 4 + k] = dc;
+            const int sign = dc < 0;
+            const uint32_t a = (uint32_t)(sign ? -dc : dc);
+            const int level = a > zt ? (int)((a * iq + bias) >> 17) : 0;
+            const int err = (int)a - level * q;
+            const int se = sign ? -err : err;
+            int v = se >> 1;
+            return v < -127 ? -127 : (v > 127 ? 127 : v);
+        };
+        const int e0 = (int8_t)diffuse(0, top[0], lft[0]);
+        const int e1 = (int8_t)diffuse(1, top[1], e0);
+        const int e2 = (int8_t)diffuse(2, e0, lft[1]);
+        const int e3 = (int8_t)diffuse(3, e1, e2);
+        lft[0] = (int8_t)e1;
+        lft[1] = (int8_t)((3 * e3) >> 2);
+        top[0] = (int8_t)e2;
+        top[1] = (int8_t)(e3 - lft[1]);
+    }
+    wsync();
+    int snz = 0, nzb = 0;
+    if (l < 8) {
+        c[0] = W->dc[b];
+        int lv[16];
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const int j = d_ZIGZAG[n];
+            lv[n] = quantz(c[j], S.uv.iq[j > 0], S.uv.bias[j > 0]);
+            nzb |= lv[n] != 0;
+        }
+        snz = nzb;
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            W->lev[17 + b][n] = (int16_t)lv[n];
+            c[d_ZIGZAG[n]] = lv[n] * (int)S.uv.q[d_ZIGZAG[n] > 0];
+        }
+        idct16(c);
+        uint8_t* w = pl ? W->cv : W->cu;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+            w[(y + 1) * ZW_BPS + 1 + x] = (uint8_t)clamp255(pr[k] + c[k]);
+        }
+    }
+    for (int k = 0; k < 8; k++) uv_nz[k] = __shfl(nzb, k);
+    int any = 0;
+    for (int k = 0; k < 8; k++) any |= __shfl(snz, k);
+    wsync();
+    return any;
+}
+
+// Publish borders for the next MBs (vp8.rs:2771-2777, :3101-3118).
+__device__ void store_luma_borders(const Ctx& C)
+{
+    const int l = C.lane;
+    WaveLds* W = C.W;
+    if (l < 17) W->left_y[l] = W->ws[l * ZW_BPS + 16];
+    else if (l < 33) C.top_y[C.mbx * 16 + (l - 17)] = W->ws[16 * ZW_BPS + (l - 17) + 1];
+    if (C.a->ry && l < 64) {
+        uint8_t* ry = C.a->ry + (size_t)blockIdx.x * C.a->ysz + (size_t)C.mby * 16 * C.ys + C.mbx * 16;
+        for (int k = l; k < 256; k += 64) ry[(size_t)(k >> 4) * C.ys + (k & 15)] = W->ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
+    }
+    wsync();
+}
+__device__ void store_chroma_borders(const Ctx& C)
+{
+    const int l = C.lane;
+    WaveLds* W = C.W;
+    if (l < 9) {
+        W->left_u[l] = W->cu[l * ZW_BPS + 8];
+        W->left_v[l] = W->cv[l * ZW_BPS + 8];
+    } else if (l < 17) {
+        C.top_u[C.mbx * 8 + (l - 9)] = W->cu[8 * ZW_BPS + (l - 9) + 1];
+        C.top_v[C.mbx * 8 + (l - 9)] = W->cv[8 * ZW_BPS + (l - 9) + 1];
+    }
+    if (C.a->ru) {
+        uint8_t* ru = C.a->ru + (size_t)blockIdx.x * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
+        uint8_t* rv = C.a->rv + (size_t)blockIdx.x * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
+        const int k = l;
+        ru[(size_t)(k >> 3) * C.cs + (k & 7)] = W->cu[((k >> 3) + 1) * ZW_BPS + 1 + (k & 7)];
+        rv[(size_t)(k >> 3) * C.cs + (k & 7)] = W->cv[((k >> 3) + 1) * ZW_BPS + 1 + (k & 7)];
+    }
+    wsync();
+}
+
+__device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
+{
+    ZwMbOut* o = C.a->out + (size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx;
+    int16_t* dst = &o->levels[0][0];
+    const int16_t* srcl = &C.W->lev[0][0];
+    for (int k = C.lane; k < nblk * 16; k += 64) dst[first_blk * 16 + k] = zero ? (int16_t)0 : srcl[first_blk * 16 + k];
+}
+
+__device__ void setup_ctx(Ctx& C, const EncArgs* a, const ZwFrameParams* P, const LdsTables* T, WaveLds* W,
+                          uint8_t* shared_base, int mbx, int mby)
+{
+    C.mbx = mbx;
+    C.mby = mby;
+    const int f = blockIdx.x;
+    C.ys = a->mbw * 16;
+    C.cs = a->mbw * 8;
+    C.srcY = a->Y + (size_t)f * a->ysz + (size_t)mby * 16 * C.ys + mbx * 16;
+    C.srcU = a->U + (size_t)f * a->csz + (size_t)mby * 8 * C.cs + mbx * 8;
+    C.srcV = a->V + (size_t)f * a->csz + (size_t)mby * 8 * C.cs + mbx * 8;
+    int seg = 0;
+    if (P->seg_enabled) seg = P->seg_map_lut[a->alpha[(size_t)f * a->mbw * a->mbh + (size_t)mby * a->mbw + mbx]];
+    C.seg = seg;
+    C.S = &P->seg[seg];
+    (void)shared_base;
+}
+
+__device__ void wait_row(const int* progress, int wave_of_prev, int need)
+{
+    while (__hip_atomic_load(&progress[wave_of_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+        __builtin_amdgcn_s_sleep(1);
+}
+__device__ void publish(int* progress, int wave, int val)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(&progress[wave], val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_wave_barrier();
+}
+
+extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int f = blockIdx.x;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mbw = a.mbw, mbh = a.mbh;
+    const ZwFrameParams* P = a.params + f;
+    // carve LDS
+    size_t off = 0;
+    LdsTables* T = (LdsTables*)(smem + off);
+    off += (sizeof(LdsTables) + 15) & ~(size_t)15;
+    WaveLds* Wall = (WaveLds*)(smem + off);
+    off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
+    int* progress = (int*)(smem + off);
+    off += 64;
+    uint8_t* top_y = smem + off;
+    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
+    uint8_t* top_u = smem + off;
+    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    uint8_t* top_v = smem + off;
+    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    uint8_t* top_c = smem + off;  // [mbw][12]: y2, y[4], u[2], v[2]
+    off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
+    int8_t* top_derr = (int8_t*)(smem + off);  // [mbw][4]
+    WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
+
+    // init shared state
+    for (int i = threadIdx.x; i < (int)(sizeof(T->lc) / 2); i += WG)
+        (&T->lc[0][0][0][0])[i] = a.lcost ? (&a.lcost[f].lc[0][0][0][0])[i] : 0;
+    for (int i = threadIdx.x; i < 96; i += WG) {
+        (&T->eob[0][0][0])[i] = a.lcost ? (&a.lcost[f].eob[0][0][0])[i] : 0;
+        (&T->init[0][0][0])[i] = a.lcost ? (&a.lcost[f].init[0][0][0])[i] : 0;
+    }
+    for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&T->probs[0][0][0][0])[i] = (&P->probs[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
+    for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
+        top_u[i] = 127;
+        top_v[i] = 127;
+    }
+    for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
+    for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = a.pass == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
+    if (threadIdx.x < NW) progress[threadIdx.x] = -1;
+    __syncthreads();
+
+    Ctx C;
+    C.a = &a;
+    C.P = P;
+    C.T = T;
+    C.W = W;
+    C.lane = lane;
+    C.top_y = top_y;
+    C.top_u = top_u;
+    C.top_v = top_v;
+    C.top_c = top_c;
+    C.top_derr = top_derr;
+    const bool trel = a.pass == 2 && P->do_trellis;
+    const size_t nmb = (size_t)mbw * mbh;
+
+    if (a.pass == 1 && wv == 0) {
+        // ---- pass-1 chroma raster chain ----
+        if (lane < 4) W->left_derr[lane] = 0;
+        for (int mby = 0; mby < mbh; mby++) {
+            if (lane < 12) {
+                W->left_u[lane] = 129;
+                W->left_v[lane] = 129;
+            }
+            wsync();
+            for (int mbx = 0; mbx < mbw; mbx++) {
+                setup_ctx(C, &a, P, T, W, smem, mbx, mby);
+                build_chroma_border(C);
+                const int cm = pick_uv(C);
+                int uvnz[8];
+                final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+                store_chroma_borders(C);
+                ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
+                if (lane == 0) o->chroma_mode = (uint8_t)cm;
+                write_levels(C, 17, 8, false);
+                wsync();
+            }
+        }
+        for (int i = lane; i < mbw * 4; i += 64) a.derr[(size_t)f * mbw * 4 + i] = top_derr[i];
+        return;
+    }
+
+    const int nrw = a.pass == 1 ? NW - 1 : NW;  // waves on the luma wavefront
+    const int rw = a.pass == 1 ? wv - 1 : wv;
+    for (int mby = rw; mby < mbh; mby += nrw) {
+        if (lane < 20) W->left_y[lane] = 129;
+        if (lane < 12) {
+            W->left_u[lane] = 129;
+            W->left_v[lane] = 129;
+            W->left_c[lane] = 0;
+        }
+        if (lane < 4) W->left_derr[lane] = 0;
+        wsync();
+        const int prevw = mby > 0 ? ((mby - 1) % nrw) + (a.pass == 1 ? 1 : 0) : 0;
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
+            setup_ctx(C, &a, P, T, W, smem, mbx, mby);
+            build_luma_border(C);
+            int lm;
+            unsigned long long i16s;
+            pick_i16(C, lm, i16s);
+            wsync();
+            if (P->method > 1) {
+                const unsigned long long thr = 211ull * C.S->l_mode;
+                if (P->method >= 5 || i16s > thr || lm != 0) {
+                    if (pick_i4(C, i16s)) lm = 4;
+                }
+            }
+            int cm = 0;
+            if (a.pass == 2) {
+                build_chroma_border(C);
+                cm = pick_uv(C);
+            }
+            int ynz[16];
+            const int lnz = final_luma(C, lm, trel, ynz);
+            int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            int cnz = 0;
+            if (a.pass == 2) cnz = final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+            ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
+            if (a.pass == 2) {
+                const int skip = !(lnz | cnz);
+                // complexity (encode_residual_data semantics / skip clearing)
+                if (lane == 0) {
+                    uint8_t* tc = top_c + mbx * 12;
+                    uint8_t* lc = W->left_c;
+                    if (skip) {
+                        for (int k = 1; k < 9; k++) tc[k] = lc[k] = 0;
+                        if (lm != 4) tc[0] = lc[0] = 0;
+                    } else {
+                        if (lm != 4) {
+                            int y2nz = 0;
+                            for (int n = 0; n < 16; n++) y2nz |= W->lev[16][n] != 0;
+                            tc[0] = lc[0] = (uint8_t)y2nz;
+                        }
+                        for (int x = 0; x < 4; x++) tc[1 + x] = (uint8_t)ynz[12 + x];
+                        for (int y = 0; y < 4; y++) lc[1 + y] = (uint8_t)ynz[y * 4 + 3];
+                        tc[5] = (uint8_t)uvnz[2];
+                        tc[6] = (uint8_t)uvnz[3];
+                        lc[5] = (uint8_t)uvnz[1];
+                        lc[6] = (uint8_t)uvnz[3];
+                        tc[7] = (uint8_t)uvnz[6];
+                        tc[8] = (uint8_t)uvnz[7];
+                        lc[7] = (uint8_t)uvnz[5];
+                        lc[8] = (uint8_t)uvnz[7];
+                    }
+                    o->skip = (uint8_t)skip;
+                    o->chroma_mode = (uint8_t)cm;
+                }
+                store_chroma_borders(C);
+                write_levels(C, 0, 25, skip);
+            } else {
+                write_levels(C, 0, 17, false);
+            }
+            if (lane == 0) {
+                o->luma_mode = (uint8_t)lm;
+                o->segment = (uint8_t)C.seg;
+            }
+            if (lane < 16) o->bpred[lane] = lm == 4 ? W->modes[lane] : 0;
+            store_luma_borders(C);
+            publish(progress, wv, mby * 65536 + mbx + 1);
+        }
+    }
+}
+
+extern "C" size_t zw_encode_lds_bytes(int mbw)
+{
+    size_t off = 0;
+    off += (sizeof(LdsTables) + 15) & ~(size_t)15;
+    off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
+    off += 64;
+    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
+    off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
+    off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
+    off += (size_t)mbw * 4;
+    return off;
+}
+extern "C" int zw_encode_wg_threads(void) { return WG; }
+
+// ---------------------------------------------------------------------------
+// Host-side launch wrappers (called from zw_host.cpp).
+// ---------------------------------------------------------------------------
+extern "C" hipError_t zwk_rgb2yuv(hipStream_t s, const uint8_t* img, int w, int h, int bpp, int mbw, int mbh,
+                                  uint8_t* Y, uint8_t* U, uint8_t* V, size_t img_stride, size_t ysz, size_t csz,
+                                  int nframes)
+{
+    const int n = mbw * 8 * mbh * 8;
+    hipLaunchKernelGGL(k_rgb2yuv, dim3((n + 255) / 256, nframes), dim3(256), 0, s, img, w, h, bpp, mbw, mbh, Y, U, V,
+                       img_stride, ysz, csz);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int mbw,
+                                   int mbh, size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes)
+{
+    const int nmb = mbw * mbh;
+    hipLaunchKernelGGL(k_analysis, dim3((nmb + 3) / 4, nframes), dim3(256), 0, s, Y, U, V, mbw, mbh, ysz, csz, alpha,
+                       histo);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl,
+                                   ZwFrameParams* params, int nframes)
+{
+    hipLaunchKernelGGL(k_segments, dim3((nframes + 63) / 64), dim3(64), 0, s, histo, tmpl, params, nframes);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
+                                 const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost,
+                                 int8_t* derr, ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz,
+                                 size_t csz, int mbw, int mbh, int nframes)
+{
+    EncArgs a;
+    a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
+    a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
+    const size_t lds = zw_encode_lds_bytes(mbw);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_encode, dim3(nframes), dim3(WG), lds, s, a);
+    return hipGetLastError();
+}

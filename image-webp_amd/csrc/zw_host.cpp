@@ -1,0 +1,498 @@
+// zw_host.cpp -- host runtime of the MI355X VP8 pipeline: context, batch
+// pipeline (HBM buffers + kernel orchestration), host entropy stage, C ABI.
+//
+// Encode flow for a batch of frames (encode_frame_lossy, vp8.rs:1281-1488):
+//   k_rgb2yuv -> k_analysis -> k_segments -> k_encode(pass 1)
+//   -> D2H pass-1 MB records -> host: statistics replay, probability update,
+//      level costs (one thread per frame)
+//   -> H2D params/costs -> k_encode(pass 2) -> D2H pass-2 MB records
+//   -> host: header + token emission (one thread per frame).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/zwebp.h"
+#include "zw_common.h"
+#include "zw_host_entropy.h"
+#include "zw_host_internal.h"
+
+extern "C" {
+hipError_t zwk_rgb2yuv(hipStream_t s, const uint8_t* img, int w, int h, int bpp, int mbw, int mbh, uint8_t* Y,
+                       uint8_t* U, uint8_t* V, size_t img_stride, size_t ysz, size_t csz, int nframes);
+hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int mbw, int mbh,
+                        size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes);
+hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
+                        int nframes);
+hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
+                      const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost, int8_t* derr,
+                      ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
+                      int nframes);
+}
+
+extern "C" const char* zw_strerror(int code)
+{
+    switch (code) {
+    case ZW_OK: return "ok";
+    case ZW_EINVALID_DIMENSIONS: return "invalid dimensions";
+    case ZW_EINVALID_BUFFER_SIZE: return "invalid buffer size";
+    case ZW_EINVAL: return "invalid argument";
+    case ZW_EDEVICE: return "device error";
+    case ZW_EUNSUPPORTED: return "unsupported";
+    case ZW_ENOMEM: return "out of memory";
+    case ZW_EVP8_MAGIC: return "invalid VP8 magic";
+    case ZW_ECOLORSPACE: return "invalid VP8 color space";
+    case ZW_ELUMA_MODE: return "invalid luma prediction mode";
+    case ZW_EINTRA_MODE: return "invalid intra prediction mode";
+    case ZW_ECHROMA_MODE: return "invalid chroma prediction mode";
+    case ZW_EBITSTREAM: return "bitstream error";
+    case ZW_EUNSUPPORTED_FEATURE: return "unsupported feature";
+    case ZW_ENOT_ENOUGH_INIT_DATA: return "not enough VP8 init data";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int zw_ctx_create(int device, zw_ctx** out)
+{
+    if (!out) return ZW_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return ZW_EDEVICE;
+    HIPOK(hipSetDevice(device));
+    zw_ctx* c = new zw_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ZW_EDEVICE;
+    }
+    *out = c;
+    return ZW_OK;
+}
+
+extern "C" void zw_ctx_destroy(zw_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->dscratch) (void)hipFree(c->dscratch);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" void zw_bytes_free(zw_bytes* b)
+{
+    if (b && b->data) {
+        free(b->data);
+        b->data = nullptr;
+        b->len = 0;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Batch pipeline
+// --------------------------------------------------------------------------
+struct zw_pipe {
+    zw_ctx* ctx;
+    int n, w, h, color, bpp, quality, method, mbw, mbh, nmb, qi, filter;
+    size_t img_stride, ysz, csz;
+    uint8_t *d_img, *d_Y, *d_U, *d_V, *d_ry, *d_ru, *d_rv, *d_alpha;
+    uint32_t* d_histo;
+    ZwFrameParams *d_tmpl, *d_params;
+    ZwLevelCosts* d_lcost;
+    int8_t* d_derr;
+    ZwMbOut *d_out1, *d_out2;
+    std::vector<ZwMbOut> h_out1, h_out2;
+    std::vector<ZwFrameParams> h_params;
+    std::vector<ZwLevelCosts> h_lcost;
+    std::vector<uint8_t> h_have_upd;
+    std::vector<uint8_t> h_upd;  // [n][4*8*3*11]
+    std::vector<std::vector<uint8_t>> bitstreams;
+    hipEvent_t ev[8];
+    float kms[8];
+};
+
+static void pipe_free(zw_pipe* p)
+{
+    if (!p) return;
+    void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
+                    p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    for (int i = 0; i < 8; i++)
+        if (p->ev[i]) (void)hipEventDestroy(p->ev[i]);
+    delete p;
+}
+
+extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t height, int color, uint8_t quality,
+                              uint8_t method, zw_pipe** out)
+{
+    if (!ctx || !out || n <= 0) return ZW_EINVAL;
+    *out = nullptr;
+    if (width == 0 || height == 0 || width > 16383 || height > 16383) return ZW_EINVALID_DIMENSIONS;
+    if (color < 0 || color > 3) return ZW_EINVAL;
+    if (quality > 100) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    zw_pipe* p = new zw_pipe();
+    memset(p->ev, 0, sizeof p->ev);
+    p->ctx = ctx;
+    p->n = n;
+    p->w = (int)width;
+    p->h = (int)height;
+    p->color = color;
+    static const int bpp_of[4] = {1, 2, 3, 4};
+    p->bpp = bpp_of[color];
+    p->quality = quality;
+    p->method = method > 6 ? 6 : method;
+    p->mbw = (p->w + 15) / 16;
+    p->mbh = (p->h + 15) / 16;
+    p->nmb = p->mbw * p->mbh;
+    p->img_stride = (size_t)p->w * p->h * p->bpp;
+    p->ysz = (size_t)p->mbw * 16 * p->mbh * 16;
+    p->csz = (size_t)p->mbw * 8 * p->mbh * 8;
+    p->qi = zwh::quality_to_qi(quality);
+    p->filter = zwh::filter_level_for(p->qi);
+    p->d_img = p->d_Y = p->d_U = p->d_V = p->d_ry = p->d_ru = p->d_rv = p->d_alpha = nullptr;
+    p->d_histo = nullptr;
+    p->d_tmpl = p->d_params = nullptr;
+    p->d_lcost = nullptr;
+    p->d_derr = nullptr;
+    p->d_out1 = p->d_out2 = nullptr;
+    const size_t N = (size_t)n;
+    bool ok = hipMalloc(&p->d_img, N * p->img_stride + 64) == hipSuccess &&
+              hipMalloc(&p->d_Y, N * p->ysz) == hipSuccess && hipMalloc(&p->d_U, N * p->csz) == hipSuccess &&
+              hipMalloc(&p->d_V, N * p->csz) == hipSuccess && hipMalloc(&p->d_ry, N * p->ysz) == hipSuccess &&
+              hipMalloc(&p->d_ru, N * p->csz) == hipSuccess && hipMalloc(&p->d_rv, N * p->csz) == hipSuccess &&
+              hipMalloc(&p->d_alpha, N * p->nmb) == hipSuccess &&
+              hipMalloc(&p->d_histo, N * 256 * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&p->d_tmpl, sizeof(ZwFrameParams)) == hipSuccess &&
+              hipMalloc(&p->d_params, N * sizeof(ZwFrameParams)) == hipSuccess &&
+              hipMalloc(&p->d_lcost, N * sizeof(ZwLevelCosts)) == hipSuccess &&
+              hipMalloc(&p->d_derr, N * p->mbw * 4) == hipSuccess &&
+              hipMalloc(&p->d_out1, N * p->nmb * sizeof(ZwMbOut)) == hipSuccess &&
+              hipMalloc(&p->d_out2, N * p->nmb * sizeof(ZwMbOut)) == hipSuccess;
+    for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&p->ev[i]) == hipSuccess;
+    if (!ok) {
+        pipe_free(p);
+        return ZW_ENOMEM;
+    }
+    p->h_params.resize(N);
+    p->h_lcost.resize(N);
+    p->h_have_upd.assign(N, 0);
+    p->h_upd.assign(N * 4 * 8 * 3 * 11, 0);
+    p->bitstreams.resize(N);
+    ZwFrameParams t;
+    memset(&t, 0, sizeof t);
+    t.width = p->w;
+    t.height = p->h;
+    t.mbw = p->mbw;
+    t.mbh = p->mbh;
+    t.method = p->method;
+    t.do_trellis = p->method >= 4;
+    t.base_qi = p->qi;
+    t.filter_level = p->filter;
+    t.skip_prob = 200;
+    memcpy(t.probs, zwh::COEFF_PROBS, sizeof t.probs);
+    HIPOK(hipMemcpy(p->d_tmpl, &t, sizeof t, hipMemcpyHostToDevice));
+    *out = p;
+    return ZW_OK;
+}
+
+extern "C" void zw_pipe_destroy(zw_pipe* p)
+{
+    if (p) (void)hipSetDevice(p->ctx->device);
+    pipe_free(p);
+}
+
+extern "C" void* zw_pipe_input_device_ptr(zw_pipe* p) { return p ? p->d_img : nullptr; }
+
+extern "C" int zw_pipe_upload(zw_pipe* p, int frame, const uint8_t* data, size_t len)
+{
+    if (!p || frame < 0 || frame >= p->n || !data) return ZW_EINVAL;
+    if (len != p->img_stride) return ZW_EINVALID_BUFFER_SIZE;
+    HIPOK(hipMemcpy(p->d_img + (size_t)frame * p->img_stride, data, len, hipMemcpyHostToDevice));
+    return ZW_OK;
+}
+
+static int pipe_pass1(zw_pipe* p)
+{
+    hipStream_t s = p->ctx->stream;
+    const int n = p->n;
+    HIPOK(hipEventRecord(p->ev[0], s));
+    HIPOK(zwk_rgb2yuv(s, p->d_img, p->w, p->h, p->bpp, p->mbw, p->mbh, p->d_Y, p->d_U, p->d_V, p->img_stride, p->ysz,
+                      p->csz, n));
+    HIPOK(hipEventRecord(p->ev[1], s));
+    HIPOK(hipMemsetAsync(p->d_histo, 0, (size_t)n * 256 * sizeof(uint32_t), s));
+    HIPOK(zwk_analysis(s, p->d_Y, p->d_U, p->d_V, p->mbw, p->mbh, p->ysz, p->csz, p->d_alpha, p->d_histo, n));
+    HIPOK(zwk_segments(s, p->d_histo, p->d_tmpl, p->d_params, n));
+    HIPOK(hipEventRecord(p->ev[2], s));
+    HIPOK(zwk_encode(s, 1, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, nullptr, p->d_derr, p->d_out1, nullptr,
+                     nullptr, nullptr, p->ysz, p->csz, p->mbw, p->mbh, n));
+    HIPOK(hipEventRecord(p->ev[3], s));
+    return ZW_OK;
+}
+
+static int pipe_host_stats(zw_pipe* p)
+{
+    hipStream_t s = p->ctx->stream;
+    const size_t N = (size_t)p->n;
+    p->h_out1.resize(N * p->nmb);
+    HIPOK(hipMemcpyAsync(p->h_out1.data(), p->d_out1, N * p->nmb * sizeof(ZwMbOut), hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(p->h_params.data(), p->d_params, N * sizeof(ZwFrameParams), hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    parallel_for(p->n, [&](int f) {
+        zwh::Stats st;
+        int sp = zwh::replay_stats(st, p->h_out1.data() + (size_t)f * p->nmb, p->mbw, p->mbh);
+        uint8_t* upd = p->h_upd.data() + (size_t)f * 4 * 8 * 3 * 11;
+        bool have = zwh::updated_probs(st, (uint8_t(*)[8][3][11])upd);
+        p->h_have_upd[f] = have;
+        ZwFrameParams& P = p->h_params[f];
+        P.skip_prob = sp;
+        memcpy(P.probs, upd, sizeof P.probs);
+        zwh::level_costs(p->h_lcost[f], (const uint8_t(*)[8][3][11])upd);
+    });
+    HIPOK(hipMemcpyAsync(p->d_params, p->h_params.data(), N * sizeof(ZwFrameParams), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(p->d_lcost, p->h_lcost.data(), N * sizeof(ZwLevelCosts), hipMemcpyHostToDevice, s));
+    return ZW_OK;
+}
+
+static int pipe_pass2(zw_pipe* p)
+{
+    hipStream_t s = p->ctx->stream;
+    HIPOK(hipEventRecord(p->ev[4], s));
+    HIPOK(zwk_encode(s, 2, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, p->d_lcost, p->d_derr, p->d_out2,
+                     p->d_ry, p->d_ru, p->d_rv, p->ysz, p->csz, p->mbw, p->mbh, p->n));
+    HIPOK(hipEventRecord(p->ev[5], s));
+    return ZW_OK;
+}
+
+static int pipe_emit(zw_pipe* p)
+{
+    hipStream_t s = p->ctx->stream;
+    const size_t N = (size_t)p->n;
+    p->h_out2.resize(N * p->nmb);
+    HIPOK(hipMemcpyAsync(p->h_out2.data(), p->d_out2, N * p->nmb * sizeof(ZwMbOut), hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    parallel_for(p->n, [&](int f) {
+        zwh::emit_frame(p->bitstreams[f], p->h_params[f], p->h_out2.data() + (size_t)f * p->nmb, p->w, p->h,
+                        p->h_have_upd[f] != 0,
+                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + (size_t)f * 4 * 8 * 3 * 11));
+    });
+    return ZW_OK;
+}
+
+static void pipe_times(zw_pipe* p)
+{
+    for (int i = 0; i < 8; i++) p->kms[i] = 0.f;
+    (void)hipEventElapsedTime(&p->kms[0], p->ev[0], p->ev[1]);  // rgb2yuv
+    (void)hipEventElapsedTime(&p->kms[1], p->ev[1], p->ev[2]);  // analysis + segments
+    (void)hipEventElapsedTime(&p->kms[2], p->ev[2], p->ev[3]);  // pass 1
+    (void)hipEventElapsedTime(&p->kms[3], p->ev[4], p->ev[5]);  // pass 2
+}
+
+extern "C" int zw_pipe_run_device(zw_pipe* p)
+{
+    if (!p) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    int r = pipe_pass1(p);
+    if (r) return r;
+    r = pipe_host_stats(p);
+    if (r) return r;
+    r = pipe_pass2(p);
+    if (r) return r;
+    HIPOK(hipStreamSynchronize(p->ctx->stream));
+    pipe_times(p);
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_encode(zw_pipe* p)
+{
+    if (!p) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    int r = pipe_pass1(p);
+    if (r) return r;
+    r = pipe_host_stats(p);
+    if (r) return r;
+    r = pipe_pass2(p);
+    if (r) return r;
+    r = pipe_emit(p);
+    if (r) return r;
+    pipe_times(p);
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_kernel_times(zw_pipe* p, float* ms, int n)
+{
+    if (!p || !ms) return ZW_EINVAL;
+    for (int i = 0; i < n && i < 8; i++) ms[i] = p->kms[i];
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_output(zw_pipe* p, int frame, zw_bytes* out)
+{
+    if (!p || !out || frame < 0 || frame >= p->n) return ZW_EINVAL;
+    const std::vector<uint8_t>& b = p->bitstreams[frame];
+    out->data = (uint8_t*)malloc(b.size() ? b.size() : 1);
+    if (!out->data) return ZW_ENOMEM;
+    memcpy(out->data, b.data(), b.size());
+    out->len = b.size();
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_read_planes(zw_pipe* p, int frame, int which, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!p || frame < 0 || frame >= p->n) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    uint8_t* Y = which ? p->d_ry : p->d_Y;
+    uint8_t* U = which ? p->d_ru : p->d_U;
+    uint8_t* V = which ? p->d_rv : p->d_V;
+    if (y) HIPOK(hipMemcpy(y, Y + (size_t)frame * p->ysz, p->ysz, hipMemcpyDeviceToHost));
+    if (u) HIPOK(hipMemcpy(u, U + (size_t)frame * p->csz, p->csz, hipMemcpyDeviceToHost));
+    if (v) HIPOK(hipMemcpy(v, V + (size_t)frame * p->csz, p->csz, hipMemcpyDeviceToHost));
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_read_mbinfo(zw_pipe* p, int frame, int pass, uint8_t* modes, int16_t* levels)
+{
+    if (!p || frame < 0 || frame >= p->n) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    std::vector<ZwMbOut> tmp(p->nmb);
+    HIPOK(hipMemcpy(tmp.data(), (pass == 1 ? p->d_out1 : p->d_out2) + (size_t)frame * p->nmb,
+                    p->nmb * sizeof(ZwMbOut), hipMemcpyDeviceToHost));
+    for (int i = 0; i < p->nmb; i++) {
+        if (modes) {
+            uint8_t* m = modes + (size_t)i * 20;
+            m[0] = tmp[i].luma_mode;
+            m[1] = tmp[i].chroma_mode;
+            m[2] = tmp[i].skip;
+            m[3] = tmp[i].segment;
+            memcpy(m + 4, tmp[i].bpred, 16);
+        }
+        if (levels) memcpy(levels + (size_t)i * 400, tmp[i].levels, 800);
+    }
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_read_alpha(zw_pipe* p, int frame, uint8_t* alpha)
+{
+    if (!p || frame < 0 || frame >= p->n || !alpha) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    HIPOK(hipMemcpy(alpha, p->d_alpha + (size_t)frame * p->nmb, p->nmb, hipMemcpyDeviceToHost));
+    return ZW_OK;
+}
+
+// --------------------------------------------------------------------------
+// Single-image entry points
+// --------------------------------------------------------------------------
+static int check_encode_args(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                             uint8_t quality)
+{
+    if (width > 65535 || height > 65535 || width == 0 || height == 0) return ZW_EINVALID_DIMENSIONS;
+    if (width > 16383 || height > 16383) return ZW_EINVALID_DIMENSIONS; /* 14-bit VP8 header fields */
+    if (color < 0 || color > 3) return ZW_EINVAL;
+    static const int bpp_of[4] = {1, 2, 3, 4};
+    if ((uint64_t)width * height * bpp_of[color] != len || !data) return ZW_EINVALID_BUFFER_SIZE;
+    if (quality > 100) return ZW_EINVAL;
+    return ZW_OK;
+}
+
+extern "C" int zw_encode_batch(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t quality, uint8_t method,
+                               zw_bytes* outs)
+{
+    if (!ctx || n <= 0 || !imgs || !outs) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) {
+        outs[i].data = nullptr;
+        outs[i].len = 0;
+        int r = check_encode_args(imgs[i].data, imgs[i].len, imgs[i].width, imgs[i].height, imgs[i].color, quality);
+        if (r) return r;
+        if (imgs[i].width != imgs[0].width || imgs[i].height != imgs[0].height || imgs[i].color != imgs[0].color)
+            return ZW_EINVAL;
+    }
+    zw_pipe* p = nullptr;
+    int r = zw_pipe_create(ctx, n, imgs[0].width, imgs[0].height, imgs[0].color, quality, method, &p);
+    if (r) return r;
+    for (int i = 0; i < n && !r; i++) r = zw_pipe_upload(p, i, imgs[i].data, imgs[i].len);
+    if (!r) r = zw_pipe_encode(p);
+    for (int i = 0; i < n && !r; i++) r = zw_pipe_output(p, i, &outs[i]);
+    zw_pipe_destroy(p);
+    return r;
+}
+
+extern "C" int zw_encode_frame_lossy(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
+                                     int color, uint8_t quality, uint8_t method, zw_bytes* out)
+{
+    if (!ctx || !out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    int r = check_encode_args(data, len, width, height, color, quality);
+    if (r) return r;
+    zw_image im = {data, len, width, height, color};
+    return zw_encode_batch(ctx, 1, &im, quality, method, out);
+}
+
+extern "C" int zw_encode_webp(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
+                              int color, uint8_t quality, uint8_t method, zw_bytes* out)
+{
+    if (!ctx || !out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    if (color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8) return ZW_EUNSUPPORTED; /* VP8X+ALPH needs VP8L */
+    zw_bytes frame = {nullptr, 0};
+    int r = zw_encode_frame_lossy(ctx, data, len, width, height, color, quality, method, &frame);
+    if (r) return r;
+    // simple container: RIFF size = 4 + chunk (8 + payload + pad)  (api.rs:1325-1330)
+    const size_t pad = frame.len & 1;
+    const size_t total = 12 + 8 + frame.len + pad;
+    out->data = (uint8_t*)malloc(total);
+    if (!out->data) {
+        zw_bytes_free(&frame);
+        return ZW_ENOMEM;
+    }
+    uint8_t* o = out->data;
+    auto le32 = [](uint8_t* d, uint32_t v) {
+        d[0] = (uint8_t)v;
+        d[1] = (uint8_t)(v >> 8);
+        d[2] = (uint8_t)(v >> 16);
+        d[3] = (uint8_t)(v >> 24);
+    };
+    memcpy(o, "RIFF", 4);
+    le32(o + 4, (uint32_t)(total - 8));
+    memcpy(o + 8, "WEBPVP8 ", 8);
+    le32(o + 16, (uint32_t)frame.len);
+    memcpy(o + 20, frame.data, frame.len);
+    if (pad) o[20 + frame.len] = 0;
+    out->len = total;
+    zw_bytes_free(&frame);
+    return ZW_OK;
+}
+
+extern "C" int zw_rgb_to_yuv420(zw_ctx* ctx, const uint8_t* img, uint32_t width, uint32_t height, int bpp, uint8_t* y,
+                                uint8_t* u, uint8_t* v)
+{
+    if (!ctx || !img || !y || !u || !v || width == 0 || height == 0 || width > 16383 || height > 16383) return ZW_EINVAL;
+    if (bpp < 1 || bpp > 4) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    const int mbw = ((int)width + 15) / 16, mbh = ((int)height + 15) / 16;
+    const size_t isz = (size_t)width * height * bpp, ysz = (size_t)mbw * 16 * mbh * 16, csz = (size_t)mbw * 8 * mbh * 8;
+    uint8_t *d_img = nullptr, *d_y = nullptr, *d_u = nullptr, *d_v = nullptr;
+    hipStream_t s = ctx->stream;
+    int rc = ZW_OK;
+    if (hipMalloc(&d_img, isz) != hipSuccess || hipMalloc(&d_y, ysz) != hipSuccess || hipMalloc(&d_u, csz) != hipSuccess ||
+        hipMalloc(&d_v, csz) != hipSuccess)
+        rc = ZW_ENOMEM;
+    if (!rc && hipMemcpyAsync(d_img, img, isz, hipMemcpyHostToDevice, s) != hipSuccess) rc = ZW_EDEVICE;
+    if (!rc && zwk_rgb2yuv(s, d_img, (int)width, (int)height, bpp, mbw, mbh, d_y, d_u, d_v, isz, ysz, csz, 1) != hipSuccess)
+        rc = ZW_EDEVICE;
+    if (!rc && (hipMemcpyAsync(y, d_y, ysz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(u, d_u, csz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(v, d_v, csz, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+        rc = ZW_EDEVICE;
+    (void)hipFree(d_img);
+    (void)hipFree(d_y);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    return rc;
+}

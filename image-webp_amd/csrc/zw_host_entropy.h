@@ -1,0 +1,536 @@
+// zw_host_entropy.h -- host half of the encoder: the sequential boolean coder
+// stays on the CPU (north star).  Restates, for the product path:
+//   ArithmeticEncoder               encoder/arithmetic.rs:7-196
+//   record_coeffs / ProbaStats      encoder/cost.rs:1173-1397
+//   compute_updated_probabilities   encoder/vp8.rs:1202-1238
+//   LevelCosts::calculate           encoder/cost.rs:1500-1545
+//   encode_coefficients / residuals encoder/vp8.rs:650-958
+//   headers                         encoder/vp8.rs:315-560
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+#include "zw_common.h"
+
+namespace zwh {
+
+#define ZW_TABLE(T, N, D, ...) static const T N D = {__VA_ARGS__};
+#include "zw_tables.inc"
+#undef ZW_TABLE
+
+static const int8_t SEGMENT_ID_TREE[6] = {2, 4, -0, -1, -2, -3};
+static const int8_t YMODE_TREE[8] = {-4, 2, 4, 6, -0, -1, -2, -3};
+static const int8_t BMODE_TREE[18] = {-0, 2, -1, 4, -2, 6, 8, 12, -3, 10, -5, -6, -4, 14, -7, 16, -8, -9};
+static const int8_t UVMODE_TREE[6] = {-0, 2, -1, 4, -2, -3};
+static const int8_t TOKEN_TREE[22] = {-11, 2, -0, 4, -1, 6, 8, 12, -2, 10, -3, -4,
+                                      14, 16, -5, -6, 18, 20, -7, -8, -9, -10};
+
+struct BoolEncoder {
+    std::vector<uint8_t> buf;
+    uint32_t bottom = 0, range = 255;
+    int bit_num = 24;
+
+    void add_one()
+    {
+        size_t i = buf.size();
+        while (i > 0) {
+            i--;
+            if (buf[i] < 255) {
+                buf[i]++;
+                return;
+            }
+            buf[i] = 0;
+        }
+        buf.insert(buf.begin(), 1);
+    }
+    inline void put(int bit, int prob)
+    {
+        uint32_t split = 1 + (((range - 1) * (uint32_t)prob) >> 8);
+        if (bit) {
+            bottom += split;
+            range -= split;
+        } else {
+            range = split;
+        }
+        while (range < 128) {
+            range <<= 1;
+            if (bottom & (1u << 31)) add_one();
+            bottom <<= 1;
+            if (--bit_num == 0) {
+                buf.push_back((uint8_t)(bottom >> 24));
+                bottom &= (1u << 24) - 1;
+                bit_num = 8;
+            }
+        }
+    }
+    void flag(int f) { put(f, 128); }
+    void literal(int nbits, int v)
+    {
+        for (int b = nbits - 1; b >= 0; b--) put(((1 << b) & v) > 0, 128);
+    }
+    void tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start = 0)
+    {
+        int cur = -1;
+        for (int i = 0; i < tlen; i++)
+            if (t[i] == -value) { cur = i; break; }
+        int enc[16], pr[16], cnt = 0;
+        for (;;) {
+            if (cur == start) { enc[cnt] = 0; pr[cnt++] = probs[cur / 2]; break; }
+            if (cur == start + 1) { enc[cnt] = 1; pr[cnt++] = probs[cur / 2]; break; }
+            int ev = 0;
+            if (cur % 2) { cur -= 1; ev = 1; }
+            enc[cnt] = ev;
+            pr[cnt++] = probs[cur / 2];
+            int pi = -1;
+            for (int i = 0; i < tlen; i++)
+                if (t[i] == cur) { pi = i; break; }
+            cur = pi;
+        }
+        for (int i = cnt - 1; i >= 0; i--) put(enc[i], pr[i]);
+    }
+    void flush()
+    {
+        int c = bit_num;
+        uint32_t v = bottom;
+        if (bottom & (1u << (32 - bit_num))) add_one();
+        v <<= (c & 7);
+        c = (c >> 3) - 1;
+        while (c >= 0) { v <<= 8; c--; }
+        for (c = 3; c >= 0; c--) { buf.push_back((uint8_t)(v >> 24)); v <<= 8; }
+    }
+};
+
+inline uint16_t bitcost(int bit, int p) { return bit ? VP8_ENTROPY_COST[255 - p] : VP8_ENTROPY_COST[p]; }
+
+// LevelCosts::calculate (cost.rs:1500)
+inline void level_costs(ZwLevelCosts& L, const uint8_t probs[4][8][3][11])
+{
+    for (int t = 0; t < 4; t++)
+        for (int b = 0; b < 8; b++)
+            for (int c = 0; c < 3; c++) {
+                const uint8_t* p = probs[t][b][c];
+                uint16_t cost0 = c > 0 ? bitcost(1, p[0]) : 0;
+                uint16_t base = (uint16_t)(bitcost(1, p[1]) + cost0);
+                L.lc[t][b][c][0] = (uint16_t)(bitcost(0, p[1]) + cost0);
+                for (int v = 1; v <= 67; v++) {
+                    int idx = (v < 67 ? v : 67) - 1;
+                    int pat = VP8_LEVEL_CODES[idx][0], bits = VP8_LEVEL_CODES[idx][1];
+                    uint16_t vc = 0;
+                    for (int i = 2; pat; i++) {
+                        if (pat & 1) vc = (uint16_t)(vc + bitcost(bits & 1, p[i]));
+                        bits >>= 1;
+                        pat >>= 1;
+                    }
+                    L.lc[t][b][c][v] = (uint16_t)(base + vc);
+                }
+                L.eob[t][b][c] = bitcost(0, p[0]);
+                L.init[t][b][c] = bitcost(1, p[0]);
+            }
+}
+
+struct Stats {
+    uint32_t s[4][8][3][11];
+};
+
+inline void rec_stat(uint32_t& s, int bit)
+{
+    if (s >= 0xfffe0000u) s = ((s + 1) >> 1) & 0x7fff7fffu;
+    s += 0x00010000u + (bit ? 1u : 0u);
+}
+
+// record_coeffs (cost.rs:1297); c = zigzag levels
+inline void record_coeffs(Stats& S, const int16_t* c, int t, int first, int ctx)
+{
+    int last = -1;
+    for (int i = 15; i >= 0; i--)
+        if (c[i] != 0) { last = i; break; }
+    int eob = last >= 0 ? last + 1 : 0;
+    if (eob <= first) {
+        rec_stat(S.s[t][VP8_ENC_BANDS[first]][ctx][0], 0);
+        return;
+    }
+    int n = first, skip_eob = 0;
+    while (n < eob) {
+        uint32_t* st = S.s[t][VP8_ENC_BANDS[n]][ctx];
+        int v = c[n] < 0 ? -c[n] : c[n];
+        n++;
+        if (!skip_eob) rec_stat(st[0], 1);
+        if (v == 0) {
+            rec_stat(st[1], 0);
+            skip_eob = 1;
+            ctx = 0;
+            continue;
+        }
+        rec_stat(st[1], 1);
+        if (v == 1) {
+            rec_stat(st[2], 0);
+            ctx = 1;
+        } else {
+            rec_stat(st[2], 1);
+            if (v > 67) v = 67;
+            if (v <= 4) {
+                rec_stat(st[3], 0);
+                if (v == 2) rec_stat(st[4], 0);
+                else {
+                    rec_stat(st[4], 1);
+                    rec_stat(st[5], v == 4);
+                }
+            } else if (v <= 10) {
+                rec_stat(st[3], 1);
+                rec_stat(st[6], 0);
+                rec_stat(st[7], v > 6);
+            } else {
+                rec_stat(st[3], 1);
+                rec_stat(st[6], 1);
+                if (v < 3 + (8 << 2)) {
+                    rec_stat(st[8], 0);
+                    rec_stat(st[9], v >= 3 + (8 << 1));
+                } else {
+                    rec_stat(st[8], 1);
+                    rec_stat(st[10], v >= 3 + (8 << 3));
+                }
+            }
+            ctx = 2;
+        }
+    }
+    if (n < 16) rec_stat(S.s[t][VP8_ENC_BANDS[n]][ctx][0], 0);
+}
+
+struct Cplx {
+    uint8_t y2, y[4], u[2], v[2];
+    void clear(bool with_y2)
+    {
+        memset(y, 0, 4);
+        memset(u, 0, 2);
+        memset(v, 0, 2);
+        if (with_y2) y2 = 0;
+    }
+};
+
+inline bool any_nz(const int16_t* c, int first)
+{
+    for (int i = first; i < 16; i++)
+        if (c[i]) return true;
+    return false;
+}
+
+// check_all_coeffs_zero on pass-1 (simple-quant) levels.
+inline bool mb_all_zero_p1(const ZwMbOut& m)
+{
+    const bool i4 = m.luma_mode == 4;
+    if (!i4 && any_nz(m.levels[16], 0)) return false;
+    for (int b = 0; b < 16; b++)
+        if (any_nz(m.levels[b], i4 ? 0 : 1)) return false;
+    for (int b = 17; b < 25; b++)
+        if (any_nz(m.levels[b], 0)) return false;
+    return true;
+}
+
+// Pass-1 statistics replay in raster order (vp8.rs:1337-1385 + record_residual_stats :1027).
+// Returns the skip probability.
+inline int replay_stats(Stats& S, const ZwMbOut* mbs, int mbw, int mbh)
+{
+    memset(&S, 0, sizeof S);
+    std::vector<Cplx> top(mbw);
+    memset(top.data(), 0, sizeof(Cplx) * mbw);
+    uint32_t total = 0, skipped = 0;
+    for (int y = 0; y < mbh; y++) {
+        Cplx left;
+        memset(&left, 0, sizeof left);
+        for (int x = 0; x < mbw; x++) {
+            const ZwMbOut& m = mbs[(size_t)y * mbw + x];
+            total++;
+            const bool i4 = m.luma_mode == 4;
+            if (mb_all_zero_p1(m)) {
+                skipped++;
+                left.clear(!i4);
+                top[x].clear(!i4);
+                continue;
+            }
+            if (!i4) {
+                int cx = left.y2 + top[x].y2;
+                record_coeffs(S, m.levels[16], 1, 0, cx < 2 ? cx : 2);
+                left.y2 = top[x].y2 = any_nz(m.levels[16], 0);
+            }
+            const int tt = i4 ? 3 : 0, first = i4 ? 0 : 1;
+            for (int by = 0; by < 4; by++) {
+                int l = left.y[by];
+                for (int bx = 0; bx < 4; bx++) {
+                    int cx = l + top[x].y[bx];
+                    const int16_t* c = m.levels[by * 4 + bx];
+                    record_coeffs(S, c, tt, first, cx < 2 ? cx : 2);
+                    l = any_nz(c, first);
+                    top[x].y[bx] = (uint8_t)l;
+                }
+                left.y[by] = (uint8_t)l;
+            }
+            for (int pl = 0; pl < 2; pl++) {
+                uint8_t* lc = pl ? left.v : left.u;
+                uint8_t* tc = pl ? top[x].v : top[x].u;
+                for (int by = 0; by < 2; by++) {
+                    int l = lc[by];
+                    for (int bx = 0; bx < 2; bx++) {
+                        int cx = l + tc[bx];
+                        const int16_t* c = m.levels[17 + 4 * pl + by * 2 + bx];
+                        record_coeffs(S, c, 2, 0, cx < 2 ? cx : 2);
+                        l = any_nz(c, 0);
+                        tc[bx] = (uint8_t)l;
+                    }
+                    lc[by] = (uint8_t)l;
+                }
+            }
+        }
+    }
+    uint32_t ns = total - skipped;
+    uint32_t p = (255 * ns + total / 2) / total;
+    if (p > 255) p = 255;
+    int sp = (int)(uint8_t)p;
+    return sp < 1 ? 1 : (sp > 254 ? 254 : sp);
+}
+
+// compute_updated_probabilities (vp8.rs:1202); returns whether any update applies.
+inline bool updated_probs(const Stats& S, uint8_t out[4][8][3][11])
+{
+    memcpy(out, COEFF_PROBS, sizeof(COEFF_PROBS));
+    int32_t total = 0;
+    uint32_t nup = 0;
+    for (int t = 0; t < 4; t++)
+        for (int b = 0; b < 8; b++)
+            for (int c = 0; c < 3; c++)
+                for (int p = 0; p < 11; p++) {
+                    uint32_t st = S.s[t][b][c][p];
+                    int nb = (int)(st & 0xffff), tot = (int)(st >> 16);
+                    if (tot == 0) continue;
+                    uint8_t oldp = COEFF_PROBS[t][b][c][p], upp = COEFF_UPDATE_PROBS[t][b][c][p];
+                    uint8_t newp = (uint8_t)(255 - (uint32_t)nb * 255 / (uint32_t)tot);
+                    int oc = nb * VP8_ENTROPY_COST[255 - oldp] + (tot - nb) * VP8_ENTROPY_COST[oldp] + bitcost(0, upp);
+                    int nc = nb * VP8_ENTROPY_COST[255 - newp] + (tot - nb) * VP8_ENTROPY_COST[newp] + bitcost(1, upp) + 8 * 256;
+                    int sav = oc - nc;
+                    if (sav > 0) {
+                        out[t][b][c][p] = newp;
+                        total += sav;
+                        nup++;
+                    }
+                }
+    if (!(total > 0 && nup > 0)) {
+        memcpy(out, COEFF_PROBS, sizeof(COEFF_PROBS));
+        return false;
+    }
+    return true;
+}
+
+// encode_coefficients token part (vp8.rs:845-958) for already-quantized zigzag levels.
+inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const int16_t* zz, int first, int ctx)
+{
+    int eobi = 0;
+    for (int i = 15; i >= 0; i--)
+        if (zz[i] != 0) { eobi = i + 1; break; }
+    int skip_eob = 0;
+    for (int idx = first; idx < eobi; idx++) {
+        const int coeff = zz[idx];
+        const uint8_t* pr = P[COEFF_BANDS[idx]][ctx];
+        const int start = skip_eob ? 2 : 0;
+        const int a = coeff < 0 ? -coeff : coeff;
+        int token;
+        if (a == 0) {
+            E.tree(TOKEN_TREE, 22, pr, 0, start);
+            skip_eob = 1;
+            token = 0;
+        } else if (a <= 4) {
+            E.tree(TOKEN_TREE, 22, pr, a, start);
+            skip_eob = 0;
+            token = a;
+        } else {
+            int cat = a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10;
+            E.tree(TOKEN_TREE, 22, pr, cat, start);
+            const uint8_t* cp = PROB_DCT_CAT[cat - 5];
+            int extra = a - DCT_CAT_BASE[cat - 5];
+            int mask = cat == 10 ? 1 << 10 : 1 << (cat - 5);
+            for (int k = 0; k < 12 && cp[k]; k++) {
+                E.put((extra & mask) > 0, cp[k]);
+                mask >>= 1;
+            }
+            skip_eob = 0;
+            token = cat;
+        }
+        if (token != 0) E.flag(!(coeff > 0));
+        ctx = token == 0 ? 0 : (token == 1 ? 1 : 2);
+    }
+    if (eobi < 16) {
+        int bi = first > eobi ? first : eobi;
+        E.tree(TOKEN_TREE, 22, P[COEFF_BANDS[bi]][ctx], 11, 0);
+    }
+    return eobi > 0;
+}
+
+// Frame assembly: compressed header (vp8.rs:332), MB headers (:498), residual
+// partition (:650), frame tag (:315).
+inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const ZwMbOut* mbs, int width, int height,
+                       bool have_updated, const uint8_t upd[4][8][3][11])
+{
+    const int mbw = P.mbw, mbh = P.mbh;
+    BoolEncoder H, T;
+    uint8_t probs[4][8][3][11];
+    memcpy(probs, COEFF_PROBS, sizeof probs);
+    H.literal(1, 0);
+    H.literal(1, 0);
+    H.flag(P.seg_enabled);
+    if (P.seg_enabled) {
+        H.flag(P.seg_update_map);
+        H.flag(1);
+        H.flag(0);
+        for (int s = 0; s < 4; s++) {
+            int ql = P.seg[s].quantizer_level;
+            H.flag(ql != 0);
+            if (ql != 0) {
+                H.literal(7, ql < 0 ? -ql : ql);
+                H.flag(ql < 0);
+            }
+        }
+        for (int s = 0; s < 4; s++) H.flag(0);
+        if (P.seg_update_map)
+            for (int i = 0; i < 3; i++) {
+                H.flag(P.seg_probs[i] != 255);
+                if (P.seg_probs[i] != 255) H.literal(8, P.seg_probs[i]);
+            }
+    }
+    H.flag(0);
+    H.literal(6, P.filter_level);
+    H.literal(3, 0);
+    H.flag(0);
+    H.literal(2, 0);
+    H.literal(7, P.base_qi);
+    for (int i = 0; i < 5; i++) H.flag(0);
+    H.literal(1, 0);
+    for (int t = 0; t < 4; t++)
+        for (int b = 0; b < 8; b++)
+            for (int c = 0; c < 3; c++)
+                for (int p = 0; p < 11; p++) {
+                    uint8_t oldp = probs[t][b][c][p];
+                    if (have_updated && upd[t][b][c][p] != oldp) {
+                        H.put(1, COEFF_UPDATE_PROBS[t][b][c][p]);
+                        H.literal(8, upd[t][b][c][p]);
+                        probs[t][b][c][p] = upd[t][b][c][p];
+                    } else {
+                        H.put(0, COEFF_UPDATE_PROBS[t][b][c][p]);
+                    }
+                }
+    H.literal(1, 1);
+    H.literal(8, P.skip_prob);
+
+    std::vector<Cplx> top(mbw);
+    memset(top.data(), 0, sizeof(Cplx) * mbw);
+    std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
+    for (int y = 0; y < mbh; y++) {
+        Cplx left;
+        memset(&left, 0, sizeof left);
+        uint8_t left_bp[4] = {0, 0, 0, 0};
+        for (int x = 0; x < mbw; x++) {
+            const ZwMbOut& m = mbs[(size_t)y * mbw + x];
+            if (P.seg_enabled && P.seg_update_map) H.tree(SEGMENT_ID_TREE, 6, P.seg_probs, m.segment);
+            H.put(m.skip, P.skip_prob);
+            H.tree(YMODE_TREE, 8, KEYFRAME_YMODE_PROBS, m.luma_mode);
+            if (m.luma_mode == 4) {
+                for (int by = 0; by < 4; by++) {
+                    int l = left_bp[by];
+                    for (int bx = 0; bx < 4; bx++) {
+                        int t = top_bp[x * 4 + bx], md = m.bpred[by * 4 + bx];
+                        H.tree(BMODE_TREE, 18, KEYFRAME_BPRED_MODE_PROBS[t][l], md);
+                        l = md;
+                        top_bp[x * 4 + bx] = (uint8_t)md;
+                    }
+                    left_bp[by] = (uint8_t)l;
+                }
+            } else {
+                static const int intra_of[4] = {0, 2, 3, 1};
+                for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma_mode];
+            }
+            H.tree(UVMODE_TREE, 6, KEYFRAME_UV_MODE_PROBS, m.chroma_mode);
+            const bool i4 = m.luma_mode == 4;
+            if (m.skip) {
+                left.clear(!i4);
+                top[x].clear(!i4);
+                continue;
+            }
+            int plane = i4 ? 3 : 0;
+            if (!i4) {
+                int hc = emit_block(T, probs[1], m.levels[16], 0, left.y2 + top[x].y2);
+                left.y2 = top[x].y2 = (uint8_t)hc;
+            }
+            const int first = i4 ? 0 : 1;
+            for (int by = 0; by < 4; by++) {
+                int l = left.y[by];
+                for (int bx = 0; bx < 4; bx++) {
+                    int hc = emit_block(T, probs[plane], m.levels[by * 4 + bx], first, l + top[x].y[bx]);
+                    l = hc;
+                    top[x].y[bx] = (uint8_t)hc;
+                }
+                left.y[by] = (uint8_t)l;
+            }
+            for (int pl = 0; pl < 2; pl++) {
+                uint8_t* lc = pl ? left.v : left.u;
+                uint8_t* tc = pl ? top[x].v : top[x].u;
+                for (int by = 0; by < 2; by++) {
+                    int l = lc[by];
+                    for (int bx = 0; bx < 2; bx++) {
+                        int hc = emit_block(T, probs[2], m.levels[17 + 4 * pl + by * 2 + bx], 0, l + tc[bx]);
+                        l = hc;
+                        tc[bx] = (uint8_t)hc;
+                    }
+                    lc[by] = (uint8_t)l;
+                }
+            }
+        }
+    }
+    H.flush();
+    T.flush();
+    out.resize(10 + H.buf.size() + T.buf.size());
+    uint8_t* o = out.data();
+    uint32_t tag = ((uint32_t)H.buf.size() << 5) | (1u << 4);
+    o[0] = (uint8_t)tag;
+    o[1] = (uint8_t)(tag >> 8);
+    o[2] = (uint8_t)(tag >> 16);
+    o[3] = 0x9d;
+    o[4] = 0x01;
+    o[5] = 0x2a;
+    o[6] = (uint8_t)(width & 0xff);
+    o[7] = (uint8_t)((width >> 8) & 0x3f);
+    o[8] = (uint8_t)(height & 0xff);
+    o[9] = (uint8_t)((height >> 8) & 0x3f);
+    memcpy(o + 10, H.buf.data(), H.buf.size());
+    memcpy(o + 10 + H.buf.size(), T.buf.data(), T.buf.size());
+}
+
+// quality_to_quant_index (vp8.rs:37-55) with fast_math::cbrt/round (fast_math.rs:15-42).
+inline int quality_to_qi(int quality)
+{
+    double c = (double)quality / 100.0;
+    double lin = c < 0.75 ? c * (2.0 / 3.0) : 2.0 * c - 1.0;
+    double y = 0.0;
+    if (lin != 0.0) {
+        uint64_t bits;
+        memcpy(&bits, &lin, 8);
+        uint64_t ab = bits / 3 + (uint64_t)(1023ull * 2 / 3) * (1ull << 52);
+        memcpy(&y, &ab, 8);
+        for (int i = 0; i < 4; i++) {
+            double y2 = y * y;
+            y = (2.0 * y + lin / y2) / 3.0;
+        }
+    }
+    double r = (double)(int64_t)(127.0 * (1.0 - y) + 0.5);
+    int q = (int)r;
+    return q < 0 ? 0 : (q > 127 ? 127 : q);
+}
+
+// compute_filter_level (cost.rs:271) with sharpness 0, strength 50.
+inline int filter_level_for(int qi)
+{
+    uint32_t level0 = 250;
+    int qstep = (uint8_t)(VP8_AC_TABLE[qi] >> 2);
+    uint32_t base = LEVELS_FROM_DELTA[0][qstep < 63 ? qstep : 63];
+    uint32_t f = base * level0 / 256;
+    if (f < 2) return 0;
+    return f > 63 ? 63 : (int)f;
+}
+
+}  // namespace zwh

@@ -1,0 +1,74 @@
+// zw_host_internal.h -- state shared by the host translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+struct zw_ctx {
+    int device;
+    hipStream_t stream;
+    // grow-only device scratch for the single-call decode / filter entry points
+    void* dscratch = nullptr;
+    size_t dscratch_cap = 0;
+};
+
+#define HIPOK(x)                                  \
+    do {                                          \
+        hipError_t e_ = (x);                      \
+        if (e_ != hipSuccess) {                   \
+            fprintf(stderr, "zwebp: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return ZW_EDEVICE;                    \
+        }                                         \
+    } while (0)
+
+
+static inline int host_threads()
+{
+    const char* e = getenv("ZW_HOST_THREADS");
+    int n = e ? atoi(e) : 0;
+    if (n <= 0) {
+        n = (int)std::thread::hardware_concurrency();
+        if (n > 16) n = 16;
+        if (n < 1) n = 1;
+    }
+    return n;
+}
+
+template <class F>
+static inline void parallel_for(int n, F fn)
+{
+    int nt = std::min(host_threads(), n);
+    if (nt <= 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<int> next(0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&]() {
+            for (;;) {
+                int i = next.fetch_add(1);
+                if (i >= n) break;
+                fn(i);
+            }
+        });
+    for (auto& t : th) t.join();
+}
+
+
+// Device scratch of at least `bytes` owned by the context.
+static inline void* ctx_scratch(zw_ctx* c, size_t bytes)
+{
+    if (c->dscratch_cap < bytes) {
+        if (c->dscratch) (void)hipFree(c->dscratch);
+        c->dscratch = nullptr;
+        c->dscratch_cap = 0;
+        if (hipMalloc(&c->dscratch, bytes) != hipSuccess) return nullptr;
+        c->dscratch_cap = bytes;
+    }
+    return c->dscratch;
+}

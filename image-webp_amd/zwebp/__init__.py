@@ -1,0 +1,413 @@
+"""zwebp -- MI355X-native VP8 lossy block-transform pipeline (Python host side).
+
+Thin ctypes layer over the C ABI in ``include/zwebp.h`` (``zwebp/libzwebp.so``,
+built by ``make -C image-webp_amd``).  The names mirror the reference crate's
+public surface for the lossy path:
+
+  ===============================  =============================================
+  here                             reference (zenwebp 0.2.0)
+  ===============================  =============================================
+  ``encode_frame_lossy``           ``encoder/vp8.rs:3132`` encode_frame_lossy
+  ``EncoderParams.lossy``          ``encoder/api.rs:445`` EncoderParams::lossy
+  ``WebPEncoder.encode``           ``encoder/api.rs:1291`` WebPEncoder::encode
+  ``vp8_decode_frame``             ``decoder/vp8.rs:1526`` Vp8Decoder::decode_frame
+  ``rgb_to_yuv420``                ``decoder/yuv.rs:656`` convert_image_yuv
+  ``loop_filter_frame``            ``decoder/vp8.rs:1172`` filter_row_in_cache
+  ``EncodingError/DecodingError``  ``encoder/api.rs:35``, ``decoder/api.rs:79``
+  ===============================  =============================================
+
+Every call runs on the GPU.  There is no CPU fallback: if the library is not
+built, or no HIP device is visible, the first call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+__all__ = [
+    "ColorType", "EncoderParams", "WebPEncoder", "ZwError", "EncodingError", "DecodingError", "Context",
+    "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
+    "rgb_to_yuv420", "loop_filter_frame", "library_path", "load_library",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libzwebp.so"
+
+
+class ColorType:
+    """ColorType (encoder/api.rs:83-92), same discriminants as the C ABI."""
+    L8 = 0
+    La8 = 1
+    Rgb8 = 2
+    Rgba8 = 3
+    BYTES = {0: 1, 1: 2, 2: 3, 3: 4}
+
+
+_ERRS = {
+    1: "InvalidDimensions", 2: "InvalidBufferSize", 3: "InvalidArgument", 4: "DeviceError",
+    5: "Unsupported", 6: "OutOfMemory", 10: "Vp8MagicInvalid", 11: "ColorSpaceInvalid",
+    12: "LumaPredictionModeInvalid", 13: "IntraPredictionModeInvalid", 14: "ChromaPredictionModeInvalid",
+    15: "BitStreamError", 16: "UnsupportedFeature", 17: "NotEnoughInitData",
+}
+
+
+class ZwError(Exception):
+    def __init__(self, code, what=""):
+        self.code = code
+        self.name = _ERRS.get(code, "Unknown")
+        super().__init__(f"{what}: {self.name} (code {code})" if what else f"{self.name} (code {code})")
+
+
+class EncodingError(ZwError):
+    pass
+
+
+class DecodingError(ZwError):
+    pass
+
+
+def library_path():
+    return os.environ.get("ZWEBP_LIB", os.path.join(_HERE, LIB_NAME))
+
+
+class _Frame(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint16), ("height", ctypes.c_uint16),
+                ("y_stride", ctypes.c_uint32), ("uv_stride", ctypes.c_uint32), ("mb_rows", ctypes.c_uint32),
+                ("y", ctypes.c_void_p), ("u", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("filter_type", ctypes.c_uint8), ("filter_level", ctypes.c_uint8),
+                ("sharpness_level", ctypes.c_uint8), ("pad", ctypes.c_uint8)]
+
+
+class _Bytes(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class _Image(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t), ("width", ctypes.c_uint32),
+                ("height", ctypes.c_uint32), ("color", ctypes.c_int)]
+
+
+# (name, restype, argtypes) for every symbol in include/zwebp.h
+_VP, _SZ, _U32, _I, _U8 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint8
+SIGNATURES = [
+    ("zw_ctx_create", _I, [_I, ctypes.POINTER(_VP)]),
+    ("zw_ctx_destroy", None, [_VP]),
+    ("zw_strerror", ctypes.c_char_p, [_I]),
+    ("zw_bytes_free", None, [ctypes.POINTER(_Bytes)]),
+    ("zw_frame_free", None, [ctypes.POINTER(_Frame)]),
+    ("zw_encode_frame_lossy", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_webp", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
+    ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
+    ("zw_rgb_to_yuv420", _I, [_VP, _VP, _U32, _U32, _I, _VP, _VP, _VP]),
+    ("zw_loop_filter_frame", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I]),
+    ("zw_pipe_create", _I, [_VP, _I, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_VP)]),
+    ("zw_pipe_destroy", None, [_VP]),
+    ("zw_pipe_input_device_ptr", _VP, [_VP]),
+    ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
+    ("zw_pipe_encode", _I, [_VP]),
+    ("zw_pipe_run_device", _I, [_VP]),
+    ("zw_pipe_output", _I, [_VP, _I, ctypes.POINTER(_Bytes)]),
+    ("zw_pipe_read_planes", _I, [_VP, _I, _I, _VP, _VP, _VP]),
+    ("zw_pipe_read_mbinfo", _I, [_VP, _I, _I, _VP, _VP]),
+    ("zw_pipe_read_alpha", _I, [_VP, _I, _VP]),
+    ("zw_pipe_kernel_times", _I, [_VP, ctypes.POINTER(ctypes.c_float), _I]),
+]
+
+_LIB = None
+
+
+def load_library():
+    """Load libzwebp.so (no device access).  Raises if it is not built."""
+    global _LIB
+    if _LIB is None:
+        path = library_path()
+        if not os.path.exists(path):
+            raise ImportError(f"zwebp: HIP library not built ({path}); run `make -C image-webp_amd`")
+        L = ctypes.CDLL(path)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _check(rc, what, cls=ZwError):
+    if rc != 0:
+        raise cls(rc, what)
+
+
+class Context:
+    """One HIP device + stream (zw_ctx).  Not thread-safe; one per thread."""
+
+    def __init__(self, device=0):
+        L = load_library()
+        h = ctypes.c_void_p()
+        _check(L.zw_ctx_create(device, ctypes.byref(h)), "zw_ctx_create")
+        self._h = h
+        self._lib = L
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            self._lib.zw_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_DEFAULT = {}
+
+
+def _ctx(ctx):
+    if ctx is not None:
+        return ctx
+    pid = os.getpid()
+    if pid not in _DEFAULT:
+        dev = int(os.environ.get("LOCAL_RANK", "0")) if os.environ.get("ZWEBP_DEVICE") is None else int(
+            os.environ["ZWEBP_DEVICE"])
+        _DEFAULT[pid] = Context(dev)
+    return _DEFAULT[pid]
+
+
+def _take_bytes(L, b):
+    out = ctypes.string_at(b.data, b.len) if b.len else b""
+    L.zw_bytes_free(ctypes.byref(b))
+    return out
+
+
+def _as_u8(data):
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(data), np.uint8)
+    return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+
+
+def encode_frame_lossy(data, width, height, color, quality=75, method=4, ctx=None):
+    """encode_frame_lossy (encoder/vp8.rs:3132): raw VP8 frame bytes."""
+    c = _ctx(ctx)
+    L = c._lib
+    a = _as_u8(data)
+    out = _Bytes()
+    _check(L.zw_encode_frame_lossy(c.handle, _ptr(a), a.size, width, height, color, quality, method,
+                                   ctypes.byref(out)), "encode_frame_lossy", EncodingError)
+    return _take_bytes(L, out)
+
+
+def encode_batch(images, width, height, color, quality=75, method=4, ctx=None):
+    """Encode many same-sized frames in one device pass; returns list of VP8 frames."""
+    c = _ctx(ctx)
+    L = c._lib
+    arrs = [_as_u8(im) for im in images]
+    n = len(arrs)
+    imgs = (_Image * n)()
+    for i, a in enumerate(arrs):
+        imgs[i] = _Image(a.ctypes.data, a.size, width, height, color)
+    outs = (_Bytes * n)()
+    _check(L.zw_encode_batch(c.handle, n, imgs, quality, method, outs), "encode_batch", EncodingError)
+    return [_take_bytes(L, outs[i]) for i in range(n)]
+
+
+class EncoderParams:
+    """EncoderParams (encoder/api.rs:430-460); only the lossy variant is on this path."""
+
+    def __init__(self, quality=75, method=4, lossless=False):
+        self.quality = quality
+        self.method = method
+        self.lossless = lossless
+
+    @classmethod
+    def lossy(cls, quality, method=4):
+        return cls(quality, method, False)
+
+    @classmethod
+    def lossless(cls):
+        return cls(100, 4, True)
+
+    @classmethod
+    def default(cls):
+        return cls()
+
+
+class WebPEncoder:
+    """WebPEncoder (encoder/api.rs:1244-1398) writing to a bytearray-like sink."""
+
+    def __init__(self, writer=None, ctx=None):
+        self.writer = writer if writer is not None else bytearray()
+        self.params = EncoderParams.default()
+        self.ctx = ctx
+
+    def set_params(self, params):
+        self.params = params
+
+    def encode(self, data, width, height, color):
+        if self.params.lossless:
+            raise EncodingError(5, "lossless (VP8L) encoding is outside the accelerated path")
+        c = _ctx(self.ctx)
+        L = c._lib
+        a = _as_u8(data)
+        out = _Bytes()
+        _check(L.zw_encode_webp(c.handle, _ptr(a), a.size, width, height, color, self.params.quality,
+                                self.params.method, ctypes.byref(out)), "WebPEncoder.encode", EncodingError)
+        self.writer += _take_bytes(L, out)
+        return self.writer
+
+
+class Frame:
+    """Decoded keyframe (decoder/vp8.rs:153-183): MB-aligned Y/U/V planes."""
+
+    def __init__(self, width, height, ybuf, ubuf, vbuf, y_stride, uv_stride, filter_type, filter_level,
+                 sharpness_level):
+        self.width, self.height = width, height
+        self.ybuf, self.ubuf, self.vbuf = ybuf, ubuf, vbuf
+        self.y_stride, self.uv_stride = y_stride, uv_stride
+        self.filter_type, self.filter_level, self.sharpness_level = filter_type, filter_level, sharpness_level
+
+
+def _take_frame(L, f):
+    ysz = f.y_stride * f.mb_rows * 16
+    csz = f.uv_stride * f.mb_rows * 8
+    y = np.ctypeslib.as_array((ctypes.c_uint8 * ysz).from_address(f.y)).copy()
+    u = np.ctypeslib.as_array((ctypes.c_uint8 * csz).from_address(f.u)).copy()
+    v = np.ctypeslib.as_array((ctypes.c_uint8 * csz).from_address(f.v)).copy()
+    fr = Frame(f.width, f.height, y, u, v, f.y_stride, f.uv_stride, f.filter_type, f.filter_level,
+               f.sharpness_level)
+    L.zw_frame_free(ctypes.byref(f))
+    return fr
+
+
+def vp8_decode_frame(data, ctx=None):
+    """Vp8Decoder::decode_frame (decoder/vp8.rs:1526)."""
+    c = _ctx(ctx)
+    L = c._lib
+    a = _as_u8(data)
+    f = _Frame()
+    _check(L.zw_vp8_decode_frame(c.handle, _ptr(a) if a.size else None, a.size, ctypes.byref(f)),
+           "decode_frame", DecodingError)
+    return _take_frame(L, f)
+
+
+def decode_batch(frames, ctx=None):
+    c = _ctx(ctx)
+    L = c._lib
+    arrs = [_as_u8(d) for d in frames]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    lens = (ctypes.c_size_t * n)(*[a.size for a in arrs])
+    outs = (_Frame * n)()
+    _check(L.zw_vp8_decode_batch(c.handle, n, ptrs, lens, outs), "decode_batch", DecodingError)
+    return [_take_frame(L, outs[i]) for i in range(n)]
+
+
+def rgb_to_yuv420(img, width, height, bpp, ctx=None):
+    """convert_image_yuv (decoder/yuv.rs:656): MB-padded Y, U, V planes."""
+    c = _ctx(ctx)
+    mbw, mbh = (width + 15) // 16, (height + 15) // 16
+    y = np.zeros(mbw * 16 * mbh * 16, np.uint8)
+    u = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    v = np.zeros(mbw * 8 * mbh * 8, np.uint8)
+    a = _as_u8(img)
+    if a.size != width * height * bpp:
+        raise EncodingError(2, "rgb_to_yuv420")
+    _check(c._lib.zw_rgb_to_yuv420(c.handle, _ptr(a), width, height, bpp, _ptr(y), _ptr(u), _ptr(v)),
+           "rgb_to_yuv420")
+    return y, u, v
+
+
+def loop_filter_frame(y, u, v, mbw, mbh, mb_flags, filter_type, filter_level, sharpness, segments_enabled=0,
+                      seg_delta_values=0, seg_lf_level=(0, 0, 0, 0), lf_adj_enabled=0, ref_delta0=0, mode_delta0=0,
+                      ctx=None):
+    """In-place VP8 loop filter (decoder/vp8.rs:1172-1345) of MB-aligned planes.
+
+    mb_flags: (mbw*mbh, 4) uint8 rows of (luma_mode, segment, skip, non_zero_dct)."""
+    c = _ctx(ctx)
+    fl = np.ascontiguousarray(mb_flags, dtype=np.uint8).reshape(-1)
+    assert fl.size == mbw * mbh * 4
+    for p, n in ((y, mbw * mbh * 256), (u, mbw * mbh * 64), (v, mbw * mbh * 64)):
+        assert p.dtype == np.uint8 and p.flags.c_contiguous and p.size == n
+    lf = np.asarray(seg_lf_level, dtype=np.int8)
+    _check(c._lib.zw_loop_filter_frame(c.handle, _ptr(y), _ptr(u), _ptr(v), mbw, mbh, _ptr(fl), filter_type,
+                                       filter_level, sharpness, segments_enabled, seg_delta_values, _ptr(lf),
+                                       lf_adj_enabled, ref_delta0, mode_delta0), "loop_filter_frame")
+
+
+class Pipeline:
+    """Device-resident batch encoder (zw_pipe): n frames of one size in HBM."""
+
+    def __init__(self, nframes, width, height, color=ColorType.Rgba8, quality=75, method=4, ctx=None):
+        self.ctx = _ctx(ctx)
+        L = self._lib = self.ctx._lib
+        h = ctypes.c_void_p()
+        _check(L.zw_pipe_create(self.ctx.handle, nframes, width, height, color, quality, method, ctypes.byref(h)),
+               "zw_pipe_create", EncodingError)
+        self._h = h
+        self.n, self.width, self.height, self.color = nframes, width, height, color
+        self.mbw, self.mbh = (width + 15) // 16, (height + 15) // 16
+
+    @property
+    def input_ptr(self):
+        """Device pointer of the packed input frames (n * w*h*bpp bytes)."""
+        return self._lib.zw_pipe_input_device_ptr(self._h)
+
+    def upload(self, i, img):
+        a = _as_u8(img)
+        _check(self._lib.zw_pipe_upload(self._h, i, _ptr(a), a.size), "zw_pipe_upload")
+
+    def encode(self):
+        _check(self._lib.zw_pipe_encode(self._h), "zw_pipe_encode", EncodingError)
+
+    def run_device(self):
+        _check(self._lib.zw_pipe_run_device(self._h), "zw_pipe_run_device", EncodingError)
+
+    def output(self, i):
+        b = _Bytes()
+        _check(self._lib.zw_pipe_output(self._h, i, ctypes.byref(b)), "zw_pipe_output")
+        return _take_bytes(self._lib, b)
+
+    def planes(self, i, which=0):
+        ys, cs = self.mbw * self.mbh * 256, self.mbw * self.mbh * 64
+        y, u, v = np.zeros(ys, np.uint8), np.zeros(cs, np.uint8), np.zeros(cs, np.uint8)
+        _check(self._lib.zw_pipe_read_planes(self._h, i, which, _ptr(y), _ptr(u), _ptr(v)), "zw_pipe_read_planes")
+        return y, u, v
+
+    def mbinfo(self, i, pass_=2):
+        nmb = self.mbw * self.mbh
+        modes = np.zeros((nmb, 20), np.uint8)
+        levels = np.zeros((nmb, 25, 16), np.int16)
+        _check(self._lib.zw_pipe_read_mbinfo(self._h, i, pass_, _ptr(modes), _ptr(levels)), "zw_pipe_read_mbinfo")
+        return modes, levels
+
+    def alpha(self, i):
+        a = np.zeros(self.mbw * self.mbh, np.uint8)
+        _check(self._lib.zw_pipe_read_alpha(self._h, i, _ptr(a)), "zw_pipe_read_alpha")
+        return a
+
+    def kernel_times(self):
+        ms = (ctypes.c_float * 8)()
+        n = self._lib.zw_pipe_kernel_times(self._h, ms, 8)
+        _check(n, "zw_pipe_kernel_times")
+        return list(ms)[:4]
+
+    def close(self):
+        if self._h:
+            self._lib.zw_pipe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,137 @@
+/* zwebp.h -- C ABI of the MI355X-native VP8 lossy block-transform pipeline.
+ *
+ * Drop-in boundary for zenwebp 0.2.0's lossy path (reference crate at
+ * imazen/image-webp).  The reference has no FFI of its own; each entry point
+ * below replaces one internal seam or public Rust API and cites it:
+ *
+ *   zw_encode_frame_lossy   encode_frame_lossy        src/encoder/vp8.rs:3132-3153
+ *   zw_encode_webp          WebPEncoder::encode       src/encoder/api.rs:1291-1398
+ *                           (simple RIFF container; alpha inputs -> ZW_EUNSUPPORTED,
+ *                            the ALPH/VP8L lossless encoder is out of scope)
+ *   zw_encode_batch         many independent encode_frame_lossy calls (new: batch)
+ *   zw_vp8_decode_frame     Vp8Decoder::decode_frame  src/decoder/vp8.rs:1526
+ *   zw_rgb_to_yuv420        convert_image_yuv/_y      src/decoder/yuv.rs:656 / :806
+ *   zw_loop_filter_frame    filter_row_in_cache       src/decoder/vp8.rs:1172-1345
+ *
+ * Conventions: plain pointers + sizes, no ownership transfer except zw_bytes /
+ * zw_frame buffers (free with zw_bytes_free / zw_frame_free).  A zw_ctx owns one
+ * HIP device's streams and device buffers; it is not thread-safe (one ctx per
+ * host thread), matching the reference's single-threaded encoder/decoder.
+ * Every compute entry point runs on the GPU; there is no CPU fallback: without
+ * a usable device zw_ctx_create fails with ZW_EDEVICE.
+ */
+#ifndef ZWEBP_H
+#define ZWEBP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes.  Encoder: EncodingError (api.rs:35-48) plus the reference's panics
+ * (quality > 100 vp8.rs:2401, data length mismatch vp8.rs:1307).  Decoder:
+ * DecodingError variants used by the VP8 path (decoder/api.rs:79-110). */
+enum {
+    ZW_OK = 0,
+    ZW_EINVALID_DIMENSIONS = 1,
+    ZW_EINVALID_BUFFER_SIZE = 2,
+    ZW_EINVAL = 3,
+    ZW_EDEVICE = 4,
+    ZW_EUNSUPPORTED = 5,
+    ZW_ENOMEM = 6,
+    ZW_EVP8_MAGIC = 10,
+    ZW_ECOLORSPACE = 11,
+    ZW_ELUMA_MODE = 12,
+    ZW_EINTRA_MODE = 13,
+    ZW_ECHROMA_MODE = 14,
+    ZW_EBITSTREAM = 15,
+    ZW_EUNSUPPORTED_FEATURE = 16,
+    ZW_ENOT_ENOUGH_INIT_DATA = 17
+};
+
+/* ColorType (api.rs:83-92), same order. */
+enum { ZW_COLOR_L8 = 0, ZW_COLOR_LA8 = 1, ZW_COLOR_RGB8 = 2, ZW_COLOR_RGBA8 = 3 };
+
+typedef struct zw_ctx zw_ctx;
+
+typedef struct {
+    uint8_t *data;
+    size_t len;
+} zw_bytes;
+
+/* Decoded VP8 frame (decoder/vp8.rs Frame :153-183): MB-aligned planes. */
+typedef struct {
+    uint16_t width, height;
+    uint32_t y_stride, uv_stride; /* mbw*16, mbw*8 */
+    uint32_t mb_rows;             /* planes hold mb_rows*16 (Y) / *8 (U,V) rows */
+    uint8_t *y, *u, *v;
+    uint8_t filter_type, filter_level, sharpness_level, pad;
+} zw_frame;
+
+typedef struct {
+    const uint8_t *data; /* host pointer, w*h*bpp bytes */
+    size_t len;
+    uint32_t width, height;
+    int color;
+} zw_image;
+
+int zw_ctx_create(int device, zw_ctx **out);
+void zw_ctx_destroy(zw_ctx *ctx);
+const char *zw_strerror(int code);
+void zw_bytes_free(zw_bytes *b);
+void zw_frame_free(zw_frame *f);
+
+/* encode_frame_lossy: raw VP8 frame bytes ("VP8 " chunk payload). */
+int zw_encode_frame_lossy(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
+                          int color, uint8_t quality, uint8_t method, zw_bytes *out);
+
+/* WebPEncoder::encode with EncoderParams::lossy(quality, method): RIFF container. */
+int zw_encode_webp(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
+                   uint8_t quality, uint8_t method, zw_bytes *out);
+
+/* n independent frames of identical size/color; outs[i] receives frame i. */
+int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method, zw_bytes *outs);
+
+/* Vp8Decoder::decode_frame */
+int zw_vp8_decode_frame(zw_ctx *ctx, const uint8_t *vp8, size_t len, zw_frame *out);
+/* n independent decode_frame calls on frames of identical dimensions (new: batch). */
+int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, zw_frame *outs);
+
+/* Kernel-level entry points (host buffers in/out) for parity testing. */
+int zw_rgb_to_yuv420(zw_ctx *ctx, const uint8_t *img, uint32_t width, uint32_t height, int bpp, uint8_t *y,
+                     uint8_t *u, uint8_t *v);
+/* In-place loop filter of MB-aligned planes; per-MB flags (luma_mode 0..4,
+ * segment, skip, non_zero_dct) as 4 bytes per MB, raster order. */
+int zw_loop_filter_frame(zw_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, uint32_t mbw, uint32_t mbh,
+                         const uint8_t *mb_flags, int filter_type, int filter_level, int sharpness,
+                         int segments_enabled, int seg_delta_values, const int8_t seg_lf_level[4],
+                         int lf_adj_enabled, int ref_delta0, int mode_delta0);
+
+/* ---- Device-resident batch pipeline (benchmarks, multi-frame serving) ----
+ * A pipeline owns HBM buffers for n frames of one size.  Inputs may be written
+ * directly to the device RGBA buffer (zw_pipe_input_device_ptr, e.g. from a
+ * PyTorch tensor) so that timing excludes PCIe. */
+typedef struct zw_pipe zw_pipe;
+int zw_pipe_create(zw_ctx *ctx, int nframes, uint32_t width, uint32_t height, int color, uint8_t quality,
+                   uint8_t method, zw_pipe **out);
+void zw_pipe_destroy(zw_pipe *p);
+void *zw_pipe_input_device_ptr(zw_pipe *p);
+int zw_pipe_upload(zw_pipe *p, int frame, const uint8_t *data, size_t len);
+/* Runs the full encode of all frames; bitstreams retrievable afterwards. */
+int zw_pipe_encode(zw_pipe *p);
+/* Device-only passes (rgb2yuv, analysis, segments, pass 1, stats, pass 2) without
+ * token emission, for kernel timing.  Returns 0 or an error. */
+int zw_pipe_run_device(zw_pipe *p);
+int zw_pipe_output(zw_pipe *p, int frame, zw_bytes *out);
+/* Debug/parity taps (host copies). */
+int zw_pipe_read_planes(zw_pipe *p, int frame, int which /*0 src,1 recon*/, uint8_t *y, uint8_t *u, uint8_t *v);
+int zw_pipe_read_mbinfo(zw_pipe *p, int frame, int pass, uint8_t *modes /*nmb*20*/, int16_t *levels /*nmb*400*/);
+int zw_pipe_read_alpha(zw_pipe *p, int frame, uint8_t *alpha);
+/* Per-kernel device time of the last zw_pipe_encode/run_device (ms). */
+int zw_pipe_kernel_times(zw_pipe *p, float *ms, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -535,3 +535,14 @@ void or_yuv_to_rgb_fancy_c(const uint8_t *y, const uint8_t *u, const uint8_t *v,
         for (size_t i = 0; i < (size_t)w * h; i++) out[i * 4 + 3] = 255;
 }
 size_t or_debug_struct_size(void) { return sizeof(or_enc_debug); }
+/* all ten I4 predictions for a 13-pixel edge (L3,L2,L1,L0,P,A0..A7) */
+void or_i4_preds_edge_c(const uint8_t e[13], uint8_t out[160])
+{
+    uint8_t ws[8 * OR_BPS];
+    memset(ws, 0, sizeof ws);
+    int x0 = 1, y0 = 1;
+    ws[(y0 - 1) * OR_BPS + x0 - 1] = e[4];
+    for (int i = 0; i < 8; i++) ws[(y0 - 1) * OR_BPS + x0 + i] = e[5 + i];
+    for (int i = 0; i < 4; i++) ws[(y0 + i) * OR_BPS + x0 - 1] = e[3 - i];
+    or_i4_preds(ws, x0, y0, OR_BPS, (uint8_t(*)[16])out);
+}

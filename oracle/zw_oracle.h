@@ -104,6 +104,7 @@ int or_trellis_kat(const int32_t coeffs_in[16], int q_dc, int q_ac, int iq_dc, i
 uint32_t or_fixed_cost_i16(int mode);
 uint32_t or_fixed_cost_uv(int mode);
 size_t or_debug_struct_size(void);
+void or_i4_preds_edge_c(const uint8_t e[13], uint8_t out[160]);
 
 #ifdef __cplusplus
 }

@@ -163,6 +163,18 @@ def decode(vp8, want_unfiltered=False, want_info=False):
 
 
 def yuv_to_rgb_fancy(y, u, v, w, h, bpp=3):
+    """fill_rgb_buffer_fancy on MB-aligned planes; cropped (w*h) planes are padded."""
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    if y.size == w * h and (w % 16 or h % 16):
+        cw, ch = (w + 1) // 2, (h + 1) // 2
+        Y = np.zeros((mbh * 16, mbw * 16), np.uint8)
+        U = np.zeros((mbh * 8, mbw * 8), np.uint8)
+        V = np.zeros((mbh * 8, mbw * 8), np.uint8)
+        Y[:h, :w] = y.reshape(h, w)
+        U[:ch, :cw] = u.reshape(ch, cw)
+        V[:ch, :cw] = v.reshape(ch, cw)
+        y, u, v = Y.reshape(-1), U.reshape(-1), V.reshape(-1)
+    y, u, v = (np.ascontiguousarray(a, dtype=np.uint8) for a in (y, u, v))
     out = np.zeros(w * h * bpp, np.uint8)
     lib().or_yuv_to_rgb_fancy_c(_p(y), _p(u), _p(v), w, h, bpp, _p(out))
     return out

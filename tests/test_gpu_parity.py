@@ -1,0 +1,266 @@
+"""GPU parity: the HIP product path (through the C ABI) against the CPU oracle.
+
+Every comparison is bit-exact.  Encoder checks go stage by stage (YUV planes,
+analysis alphas, pass-2 modes, quantised levels, reconstruction, bitstream) so a
+failure names the first stage and macroblock that diverged.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import zwebp
+from zwebp.synth import synth_rgba
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return zwebp.Context(0)
+
+
+def _img(w, h, kind, seed, color):
+    rgba = synth_rgba(w, h, seed, kind)
+    if color == zwebp.ColorType.Rgba8:
+        return rgba
+    if color == zwebp.ColorType.Rgb8:
+        return np.ascontiguousarray(rgba[..., :3])
+    if color == zwebp.ColorType.La8:
+        return np.ascontiguousarray(rgba[..., [0, 3]])
+    return np.ascontiguousarray(rgba[..., 0])
+
+
+# --------------------------------------------------------------------------
+# a1: RGB -> YUV 4:2:0
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("w,h", [(1, 1), (17, 9), (64, 48), (333, 211), (250, 31)])
+@pytest.mark.parametrize("bpp", [1, 2, 3, 4])
+def test_rgb_to_yuv420(ctx, w, h, bpp):
+    img = np.ascontiguousarray(synth_rgba(w, h, 7 + w, "noise")[..., :bpp])
+    gy, gu, gv = zwebp.rgb_to_yuv420(img, w, h, bpp, ctx=ctx)
+    oy, ou, ov = O.rgb_to_yuv420(img, w, h, bpp)
+    assert np.array_equal(gy, oy)
+    assert np.array_equal(gu, ou)
+    assert np.array_equal(gv, ov)
+
+
+# --------------------------------------------------------------------------
+# a2..a18: the full encoder, stage by stage
+# --------------------------------------------------------------------------
+def _first_bad(a, b, per):
+    d = np.nonzero((a.reshape(-1, per) != b.reshape(-1, per)).any(axis=1))[0]
+    return int(d[0]) if d.size else -1
+
+
+def _mb_of_plane(i, stride, mbsz):
+    r, c = divmod(i, stride)
+    return (r // mbsz) * (stride // mbsz) + c // mbsz
+
+
+ENC_CASES = [
+    (64, 48, "natural", 75, 4, 3),
+    (300, 257, "natural", 75, 4, 3),
+    (768, 512, "natural", 75, 4, 3),
+    (333, 211, "noise", 75, 4, 2),
+    (256, 256, "flat", 75, 4, 3),
+    (200, 120, "natural", 20, 4, 3),
+    (96, 80, "natural", 95, 4, 3),
+    (160, 128, "natural", 75, 0, 3),
+    (160, 128, "natural", 75, 2, 3),
+    (160, 128, "natural", 75, 3, 3),
+    (160, 128, "natural", 75, 5, 3),
+    (160, 128, "natural", 75, 6, 3),
+    (123, 77, "natural", 0, 4, 0),
+    (123, 77, "natural", 100, 4, 1),
+    (1, 1, "natural", 75, 4, 3),
+    (4000, 16, "natural", 75, 4, 3),
+    (16, 1100, "natural", 60, 4, 3),
+]
+
+
+def _check_encode(ctx, w, h, kind, q, m, color, seed):
+    img = _img(w, h, kind, seed, color)
+    rc, ref, dbg = O.encode(img, w, h, color, q, m, debug=True)
+    assert rc == 0
+    p = zwebp.Pipeline(1, w, h, color, q, m, ctx=ctx)
+    try:
+        p.upload(0, img)
+        p.encode()
+        ys, cs = p.mbw * 16, p.mbw * 8
+        y, u, v = p.planes(0, 0)
+        for a, b, s, n in ((y, dbg["src_y"], ys, "Y"), (u, dbg["src_u"], cs, "U"), (v, dbg["src_v"], cs, "V")):
+            assert np.array_equal(a, b), f"source plane {n} differs"
+        al = p.alpha(0)
+        bad = _first_bad(al, dbg["mb_alpha"], 1)
+        assert bad < 0, f"analysis alpha differs at MB {bad}: {al[bad]} vs {dbg['mb_alpha'][bad]}"
+        modes, levels = p.mbinfo(0, 2)
+        info = dbg["p2_info"]
+        nmb = p.mbw * p.mbh
+        om = np.array([[info[i].luma_mode, info[i].chroma_mode, info[i].skip, info[i].segment] + list(info[i].bpred)
+                       for i in range(nmb)], np.uint8)
+        gm = modes.copy()
+        gm[gm[:, 0] != 4, 4:] = 0  # bpred only meaningful for I4
+        om[om[:, 0] != 4, 4:] = 0
+        bad = _first_bad(gm, om, 20)
+        assert bad < 0, f"pass-2 modes differ at MB {bad} (mbx={bad % p.mbw}, mby={bad // p.mbw}): {gm[bad]} vs {om[bad]}"
+        ol = dbg["levels"].reshape(nmb, 25, 16)
+        gl = levels.astype(np.int32)
+        gl[gm[:, 2] == 1] = 0
+        bad = _first_bad(gl, ol, 400)
+        if bad >= 0:
+            blk = int(np.nonzero((gl[bad] != ol[bad]).any(axis=1))[0][0])
+            raise AssertionError(f"levels differ at MB {bad} block {blk}: {gl[bad, blk]} vs {ol[bad, blk]}")
+        ry, ru, rv = p.planes(0, 1)
+        for a, b, s, mb, n in ((ry, dbg["recon_y"], ys, 16, "Y"), (ru, dbg["recon_u"], cs, 8, "U"),
+                               (rv, dbg["recon_v"], cs, 8, "V")):
+            d = np.nonzero(a != b)[0]
+            assert d.size == 0, f"recon {n} differs first at MB {_mb_of_plane(int(d[0]), s, mb)}"
+        out = p.output(0)
+        assert out == ref, f"bitstream differs (len {len(out)} vs {len(ref)})"
+    finally:
+        p.close()
+    return ref
+
+
+@pytest.mark.parametrize("w,h,kind,q,m,color", ENC_CASES)
+def test_encode_matches_oracle(ctx, w, h, kind, q, m, color):
+    _check_encode(ctx, w, h, kind, q, m, color, 0x5EED0000 + w * 7 + h)
+
+
+def test_encode_batch_independent_frames(ctx):
+    w, h = 176, 144
+    imgs = [synth_rgba(w, h, 0x5EED0000 + i, "natural" if i % 3 else "noise") for i in range(5)]
+    outs = zwebp.encode_batch(imgs, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    for i, img in enumerate(imgs):
+        rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
+        assert outs[i] == ref, f"frame {i}"
+
+
+def test_encode_api_errors(ctx):
+    img = synth_rgba(16, 16)
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossy(img, 0, 16, 3, ctx=ctx)
+    assert e.value.code == 1
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossy(img[:8], 16, 16, 3, ctx=ctx)
+    assert e.value.code == 2
+    with pytest.raises(zwebp.EncodingError):
+        zwebp.encode_frame_lossy(img, 16, 16, 3, quality=101, ctx=ctx)
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossy(img, 20000, 1, 3, ctx=ctx)
+    assert e.value.code in (1, 2)
+
+
+def test_webp_container(ctx):
+    w, h = 48, 32
+    img = np.ascontiguousarray(synth_rgba(w, h)[..., :3])
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    riff = bytes(enc.encode(img, w, h, zwebp.ColorType.Rgb8))
+    assert O.riff_vp8_chunk(riff) == zwebp.encode_frame_lossy(img, w, h, 2, 75, 4, ctx=ctx)
+
+
+# --------------------------------------------------------------------------
+# a19..a21: decoder (recon + loop filter)
+# --------------------------------------------------------------------------
+def _manifest():
+    with open(os.path.join(GOLD, "decode_golden.json")) as f:
+        return json.load(f)["streams"]
+
+
+@pytest.mark.parametrize("entry", _manifest(), ids=lambda e: e["name"])
+def test_decode_goldens(ctx, entry):
+    vp8 = open(os.path.join(GOLD, entry["name"] + ".vp8"), "rb").read()
+    fr = zwebp.vp8_decode_frame(vp8, ctx=ctx)
+    w, h = entry["width"], entry["height"]
+    assert (fr.width, fr.height) == (w, h)
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    planes = (fr.ybuf.reshape(-1, fr.y_stride)[:h, :w], fr.ubuf.reshape(-1, fr.uv_stride)[:ch, :cw],
+              fr.vbuf.reshape(-1, fr.uv_stride)[:ch, :cw])
+    got = [hashlib.sha256(np.ascontiguousarray(p).tobytes()).hexdigest() for p in planes]
+    assert got == entry["yuv_sha256"]
+
+
+@pytest.mark.parametrize("w,h,kind,q,m", [(333, 211, "natural", 75, 4), (256, 256, "noise", 40, 6),
+                                          (96, 64, "flat", 75, 4), (512, 384, "natural", 90, 2)])
+def test_decode_oracle_streams(ctx, w, h, kind, q, m):
+    img = synth_rgba(w, h, 0x5EED0000 + h, kind)
+    rc, vp8, _ = O.encode(img, w, h, 3, q, m)
+    rc, r = O.decode(vp8)
+    fr = zwebp.vp8_decode_frame(vp8, ctx=ctx)
+    assert np.array_equal(fr.ybuf, r["y"])
+    assert np.array_equal(fr.ubuf, r["u"])
+    assert np.array_equal(fr.vbuf, r["v"])
+
+
+def test_decode_batch(ctx):
+    w, h = 128, 96
+    streams = [O.encode(synth_rgba(w, h, 0x5EED0000 + i), w, h, 3, 30 + 10 * i, 4)[1] for i in range(4)]
+    frames = zwebp.decode_batch(streams, ctx=ctx)
+    for s, fr in zip(streams, frames):
+        rc, r = O.decode(s)
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"])
+
+
+def test_decode_errors(ctx):
+    vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
+    bad = bytearray(vp8)
+    bad[3] = 0
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.vp8_decode_frame(bytes(bad), ctx=ctx)
+    assert e.value.code == 10
+    with pytest.raises(zwebp.DecodingError):
+        zwebp.vp8_decode_frame(vp8[:2], ctx=ctx)
+    with pytest.raises(zwebp.DecodingError):
+        zwebp.vp8_decode_frame(vp8[:40], ctx=ctx)
+
+
+@pytest.mark.parametrize("ftype,level,sharp,seg", [(0, 6, 0, 0), (0, 40, 3, 1), (1, 20, 0, 0), (0, 63, 7, 1),
+                                                   (1, 63, 5, 1), (0, 15, 1, 0)])
+def test_loop_filter_frame(ctx, ftype, level, sharp, seg):
+    rng = np.random.default_rng(level * 10 + sharp)
+    mbw, mbh = 23, 17
+    nmb = mbw * mbh
+    base = synth_rgba(mbw * 16, mbh * 16, 11, "natural")[..., 0]
+    y = np.ascontiguousarray((base.astype(np.int32) + rng.integers(-12, 13, base.shape)).clip(0, 255).astype(np.uint8))
+    u = np.ascontiguousarray(y[::2, ::2])
+    v = np.ascontiguousarray(255 - y[::2, ::2])
+    flags = np.zeros((nmb, 4), np.uint8)
+    flags[:, 0] = rng.integers(0, 5, nmb)
+    flags[:, 1] = rng.integers(0, 4, nmb) if seg else 0
+    flags[:, 2] = rng.integers(0, 2, nmb)
+    flags[:, 3] = rng.integers(0, 2, nmb)
+    seg_lf = (0, -5, 7, 20)
+    gy, gu, gv = y.reshape(-1).copy(), u.reshape(-1).copy(), v.reshape(-1).copy()
+    zwebp.loop_filter_frame(gy, gu, gv, mbw, mbh, flags, ftype, level, sharp, seg, 1, seg_lf, 1, 2, -3, ctx=ctx)
+    infos = (O.MbInfo * nmb)()
+    for i in range(nmb):
+        infos[i].luma_mode, infos[i].segment, infos[i].skip, infos[i].non_zero_dct = (int(x) for x in flags[i])
+    hdr = O.FrameHdr()
+    hdr.filter_type, hdr.filter_level, hdr.sharpness = ftype, level, sharp
+    hdr.segments_enabled, hdr.seg_delta_values = seg, 1
+    for i in range(4):
+        hdr.seg_lf_level[i] = seg_lf[i]
+    hdr.lf_adj_enabled, hdr.ref_delta0, hdr.mode_delta0 = 1, 2, -3
+    oy, ou, ov = y.reshape(-1).copy(), u.reshape(-1).copy(), v.reshape(-1).copy()
+    import ctypes
+    O.lib().or_loop_filter_c(O._p(oy), O._p(ou), O._p(ov), mbw, mbh, ctypes.addressof(infos), ctypes.byref(hdr))
+    assert np.array_equal(gy, oy)
+    assert np.array_equal(gu, ou)
+    assert np.array_equal(gv, ov)
+
+
+# --------------------------------------------------------------------------
+# Full-size (BASELINE configs) properties
+# --------------------------------------------------------------------------
+def test_1080p_encode_decode_roundtrip(ctx):
+    """1920x1080 Q75 m4: GPU bitstream == oracle bitstream; GPU decode of it == oracle decode."""
+    ref = _check_encode(ctx, 1920, 1080, "natural", 75, 4, 3, 0x5EED0000)
+    fr = zwebp.vp8_decode_frame(ref, ctx=ctx)
+    rc, r = O.decode(ref)
+    assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
