@@ -392,6 +392,7 @@ struct EncArgs {
     uint8_t *ry, *ru, *rv;      // reconstruction (pass 2), may be null
     size_t ysz, csz;
     int mbw, mbh, pass;
+    int* dbg;                   // optional pass-2 I4 dump (16*34 ints per MB), may be null
 };
 
 // per-wave LDS scratch
@@ -941,6 +942,16 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                     c[k] = (int)sp[(size_t)(k >> 2) * C.ys + (k & 3)] - pr[k];
                 }
                 fdct16(c);
+                if (C.a->dbg && C.a->pass == 2) {
+                    int* d = C.a->dbg + (((size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx) * 16 + i) * 34;
+                    for (int k = 0; k < 16; k++) {
+                        d[k] = c[k];
+                        d[16 + k] = pr[k];
+                    }
+                    const int c0 = left_nz[sby] + top_nz[sbx];
+                    d[32] = c0 > 2 ? 2 : c0;
+                    d[33] = bm;
+                }
                 int snz = 0;
 #pragma unroll
                 for (int k = 0; k < 16; k++) snz |= quantz(c[k], S.y1.iq[k > 0], S.y1.bias[k > 0]) != 0;
@@ -1324,6 +1335,71 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Kernel-level entry: quantisation (simple or trellis) of independent 4x4
+// coefficient blocks, one block per thread (quantize_coeff cost.rs:457,
+// trellis_quantize_block cost.rs:788).  Used by the parity tests and as the
+// building block the encoder kernels share.
+// ---------------------------------------------------------------------------
+struct QuantBlocksArgs {
+    ZwMatrix m;
+    uint16_t sharpen[16];
+    uint32_t lambda;
+    int32_t ctype, first, trel, n;
+};
+
+extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __restrict__ coeffs,
+                                                                const uint8_t* __restrict__ ctx0s,
+                                                                const ZwLevelCosts* __restrict__ lcost,
+                                                                const uint8_t* __restrict__ probs, QuantBlocksArgs a,
+                                                                int* __restrict__ levels, int* __restrict__ dq)
+{
+    __shared__ LdsTables T;
+    for (int i = threadIdx.x; i < (int)(sizeof(T.lc) / 2); i += 256) (&T.lc[0][0][0][0])[i] = (&lcost->lc[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < 96; i += 256) {
+        (&T.eob[0][0][0])[i] = (&lcost->eob[0][0][0])[i];
+        (&T.init[0][0][0])[i] = (&lcost->init[0][0][0])[i];
+    }
+    for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += 256) (&T.probs[0][0][0][0])[i] = probs[i];
+    __syncthreads();
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= a.n) return;
+    int c[16], lv[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) c[k] = coeffs[(size_t)b * 16 + k];
+    const int ctx0 = ctx0s[b];
+    if (a.trel) {
+        if (a.first) trellis<1>(c, lv, a.m, a.sharpen, a.lambda, &T, a.ctype, ctx0);
+        else trellis<0>(c, lv, a.m, a.sharpen, a.lambda, &T, a.ctype, ctx0);
+        if (a.first) lv[0] = 0;
+    } else {
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const int j = d_ZIGZAG[n];
+            lv[n] = n < a.first ? 0 : quantz(c[j], a.m.iq[j > 0], a.m.bias[j > 0]);
+        }
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const int j = d_ZIGZAG[n];
+            c[j] = n < a.first ? 0 : lv[n] * (int)a.m.q[j > 0];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        levels[(size_t)b * 16 + k] = lv[k];
+        dq[(size_t)b * 16 + k] = c[k];
+    }
+}
+
+extern "C" hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
+                                       const uint8_t* probs, const void* args, int* levels, int* dq)
+{
+    const QuantBlocksArgs& a = *(const QuantBlocksArgs*)args;
+    hipLaunchKernelGGL(k_quant_blocks, dim3((a.n + 255) / 256), dim3(256), 0, s, coeffs, ctx0s, lcost, probs, a, levels,
+                       dq);
+    return hipGetLastError();
+}
+
 extern "C" size_t zw_encode_lds_bytes(int mbw)
 {
     size_t off = 0;
@@ -1370,9 +1446,10 @@ extern "C" hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const Z
 extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                                  const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost,
                                  int8_t* derr, ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz,
-                                 size_t csz, int mbw, int mbh, int nframes)
+                                 size_t csz, int mbw, int mbh, int nframes, int* dbg)
 {
     EncArgs a;
+    a.dbg = dbg;
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
     const size_t lds = zw_encode_lds_bytes(mbw);

@@ -29,10 +29,12 @@ hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const
                         size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes);
 hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
                         int nframes);
+hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
+                            const uint8_t* probs, const void* args, int* levels, int* dq);
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                       const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost, int8_t* derr,
                       ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
-                      int nframes);
+                      int nframes, int* dbg);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -105,6 +107,7 @@ struct zw_pipe {
     ZwLevelCosts* d_lcost;
     int8_t* d_derr;
     ZwMbOut *d_out1, *d_out2;
+    int* d_dbg = nullptr;  // optional pass-2 I4 dump
     std::vector<ZwMbOut> h_out1, h_out2;
     std::vector<ZwFrameParams> h_params;
     std::vector<ZwLevelCosts> h_lcost;
@@ -119,7 +122,7 @@ static void pipe_free(zw_pipe* p)
 {
     if (!p) return;
     void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
-                    p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2};
+                    p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     for (int i = 0; i < 8; i++)
@@ -217,7 +220,7 @@ extern "C" int zw_pipe_upload(zw_pipe* p, int frame, const uint8_t* data, size_t
     return ZW_OK;
 }
 
-static int pipe_pass1(zw_pipe* p)
+static int pipe_pass1(zw_pipe* p, bool write_recon = false)
 {
     hipStream_t s = p->ctx->stream;
     const int n = p->n;
@@ -229,8 +232,9 @@ static int pipe_pass1(zw_pipe* p)
     HIPOK(zwk_analysis(s, p->d_Y, p->d_U, p->d_V, p->mbw, p->mbh, p->ysz, p->csz, p->d_alpha, p->d_histo, n));
     HIPOK(zwk_segments(s, p->d_histo, p->d_tmpl, p->d_params, n));
     HIPOK(hipEventRecord(p->ev[2], s));
-    HIPOK(zwk_encode(s, 1, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, nullptr, p->d_derr, p->d_out1, nullptr,
-                     nullptr, nullptr, p->ysz, p->csz, p->mbw, p->mbh, n));
+    HIPOK(zwk_encode(s, 1, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, nullptr, p->d_derr, p->d_out1,
+                     write_recon ? p->d_ry : nullptr, write_recon ? p->d_ru : nullptr, write_recon ? p->d_rv : nullptr,
+                     p->ysz, p->csz, p->mbw, p->mbh, n, nullptr));
     HIPOK(hipEventRecord(p->ev[3], s));
     return ZW_OK;
 }
@@ -264,7 +268,7 @@ static int pipe_pass2(zw_pipe* p)
     hipStream_t s = p->ctx->stream;
     HIPOK(hipEventRecord(p->ev[4], s));
     HIPOK(zwk_encode(s, 2, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, p->d_lcost, p->d_derr, p->d_out2,
-                     p->d_ry, p->d_ru, p->d_rv, p->ysz, p->csz, p->mbw, p->mbh, p->n));
+                     p->d_ry, p->d_ru, p->d_rv, p->ysz, p->csz, p->mbw, p->mbh, p->n, p->d_dbg));
     HIPOK(hipEventRecord(p->ev[5], s));
     return ZW_OK;
 }
@@ -305,6 +309,16 @@ extern "C" int zw_pipe_run_device(zw_pipe* p)
     if (r) return r;
     HIPOK(hipStreamSynchronize(p->ctx->stream));
     pipe_times(p);
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
+{
+    if (!p) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    int r = pipe_pass1(p, write_recon != 0);
+    if (r) return r;
+    HIPOK(hipStreamSynchronize(p->ctx->stream));
     return ZW_OK;
 }
 
@@ -373,6 +387,34 @@ extern "C" int zw_pipe_read_mbinfo(zw_pipe* p, int frame, int pass, uint8_t* mod
         }
         if (levels) memcpy(levels + (size_t)i * 400, tmp[i].levels, 800);
     }
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_read_probs(zw_pipe* p, int frame, uint8_t* probs, int* skip_prob)
+{
+    if (!p || frame < 0 || frame >= p->n) return ZW_EINVAL;
+    if (probs) memcpy(probs, p->h_params[frame].probs, sizeof p->h_params[frame].probs);
+    if (skip_prob) *skip_prob = p->h_params[frame].skip_prob;
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_enable_debug(zw_pipe* p)
+{
+    if (!p) return ZW_EINVAL;
+    if (p->d_dbg) return ZW_OK;
+    HIPOK(hipSetDevice(p->ctx->device));
+    const size_t b = (size_t)p->n * p->nmb * 16 * 34 * sizeof(int);
+    if (hipMalloc(&p->d_dbg, b) != hipSuccess) return ZW_ENOMEM;
+    HIPOK(hipMemset(p->d_dbg, 0, b));
+    return ZW_OK;
+}
+
+extern "C" int zw_pipe_read_debug(zw_pipe* p, int frame, int32_t* out)
+{
+    if (!p || !p->d_dbg || frame < 0 || frame >= p->n || !out) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    const size_t b = (size_t)p->nmb * 16 * 34 * sizeof(int);
+    HIPOK(hipMemcpy(out, (uint8_t*)p->d_dbg + (size_t)frame * b, b, hipMemcpyDeviceToHost));
     return ZW_OK;
 }
 
@@ -495,4 +537,62 @@ extern "C" int zw_rgb_to_yuv420(zw_ctx* ctx, const uint8_t* img, uint32_t width,
     (void)hipFree(d_u);
     (void)hipFree(d_v);
     return rc;
+}
+
+// Kernel-level quantisation of n coefficient blocks (see zwebp.h).
+extern "C" int zw_quant_blocks(zw_ctx* ctx, int n, const int32_t* coeffs, const uint8_t* ctx0, int ctype, int first,
+                               int use_trellis, uint32_t lambda, int q_dc, int q_ac, int matrix_type,
+                               const uint8_t* probs, int32_t* levels, int32_t* dequant)
+{
+    if (!ctx || n <= 0 || !coeffs || !ctx0 || !levels || !dequant) return ZW_EINVAL;
+    if (ctype < 0 || ctype > 3 || (first != 0 && first != 1) || q_dc <= 0 || q_ac <= 0 || matrix_type < 0 ||
+        matrix_type > 2)
+        return ZW_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (ctx0[i] > 2) return ZW_EINVAL;
+    struct {
+        ZwMatrix m;
+        uint16_t sharpen[16];
+        uint32_t lambda;
+        int32_t ctype, first, trel, n;
+    } a;
+    memset(&a, 0, sizeof a);
+    static const uint32_t bdc[3] = {96, 96, 110}, bac[3] = {110, 108, 115};
+    a.m.q[0] = (uint32_t)q_dc;
+    a.m.q[1] = (uint32_t)q_ac;
+    for (int i = 0; i < 2; i++) {
+        const uint32_t b = i ? bac[matrix_type] : bdc[matrix_type];
+        a.m.iq[i] = (1u << 17) / a.m.q[i];
+        a.m.bias[i] = ((b << 17) + 128) >> 8;
+        a.m.zthresh[i] = ((1u << 17) - 1 - a.m.bias[i]) / a.m.iq[i];
+    }
+    if (matrix_type == 0)
+        for (int i = 0; i < 16; i++)
+            a.sharpen[i] = (uint16_t)(((uint32_t)zwh::VP8_FREQ_SHARPENING[i] * (i ? a.m.q[1] : a.m.q[0])) >> 11);
+    a.lambda = lambda;
+    a.ctype = ctype;
+    a.first = first;
+    a.trel = use_trellis != 0;
+    a.n = n;
+    uint8_t P[4][8][3][11];
+    memcpy(P, probs ? probs : &zwh::COEFF_PROBS[0][0][0][0], sizeof P);
+    ZwLevelCosts L;
+    zwh::level_costs(L, P);
+    HIPOK(hipSetDevice(ctx->device));
+    const size_t cb = (size_t)n * 16 * sizeof(int32_t);
+    const size_t o_c = 0, o_x = cb, o_l = (o_x + n + 255) & ~(size_t)255, o_p = o_l + sizeof(ZwLevelCosts);
+    const size_t o_lv = (o_p + sizeof P + 255) & ~(size_t)255, o_dq = o_lv + cb, total = o_dq + cb;
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx->stream;
+    HIPOK(hipMemcpyAsync(d + o_c, coeffs, cb, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_x, ctx0, (size_t)n, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_l, &L, sizeof L, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_p, P, sizeof P, hipMemcpyHostToDevice, s));
+    HIPOK(zwk_quant_blocks(s, (const int*)(d + o_c), d + o_x, (const ZwLevelCosts*)(d + o_l), d + o_p, &a,
+                           (int*)(d + o_lv), (int*)(d + o_dq)));
+    HIPOK(hipMemcpyAsync(levels, d + o_lv, cb, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(dequant, d + o_dq, cb, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
 }

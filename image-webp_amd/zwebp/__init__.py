@@ -27,7 +27,7 @@ import numpy as np
 __all__ = [
     "ColorType", "EncoderParams", "WebPEncoder", "ZwError", "EncodingError", "DecodingError", "Context",
     "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
-    "rgb_to_yuv420", "loop_filter_frame", "library_path", "load_library",
+    "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "library_path", "load_library",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -101,17 +101,22 @@ SIGNATURES = [
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
     ("zw_rgb_to_yuv420", _I, [_VP, _VP, _U32, _U32, _I, _VP, _VP, _VP]),
+    ("zw_quant_blocks", _I, [_VP, _I, _VP, _VP, _I, _I, _I, _U32, _I, _I, _I, _VP, _VP, _VP]),
     ("zw_loop_filter_frame", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I]),
     ("zw_pipe_create", _I, [_VP, _I, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_VP)]),
     ("zw_pipe_destroy", None, [_VP]),
     ("zw_pipe_input_device_ptr", _VP, [_VP]),
     ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
     ("zw_pipe_encode", _I, [_VP]),
+    ("zw_pipe_run_pass1", _I, [_VP, _I]),
     ("zw_pipe_run_device", _I, [_VP]),
     ("zw_pipe_output", _I, [_VP, _I, ctypes.POINTER(_Bytes)]),
     ("zw_pipe_read_planes", _I, [_VP, _I, _I, _VP, _VP, _VP]),
     ("zw_pipe_read_mbinfo", _I, [_VP, _I, _I, _VP, _VP]),
     ("zw_pipe_read_alpha", _I, [_VP, _I, _VP]),
+    ("zw_pipe_enable_debug", _I, [_VP]),
+    ("zw_pipe_read_debug", _I, [_VP, _I, _VP]),
+    ("zw_pipe_read_probs", _I, [_VP, _I, _VP, ctypes.POINTER(_I)]),
     ("zw_pipe_kernel_times", _I, [_VP, ctypes.POINTER(ctypes.c_float), _I]),
 ]
 
@@ -327,6 +332,22 @@ def rgb_to_yuv420(img, width, height, bpp, ctx=None):
     return y, u, v
 
 
+def quant_blocks(coeffs, ctx0, ctype, first, use_trellis, lambda_, q_dc, q_ac, matrix_type, probs=None, ctx=None):
+    """Quantise (n,16) natural-order coefficient blocks on the GPU.
+
+    Returns (levels zigzag (n,16) int32, dequantised natural (n,16) int32)."""
+    c = _ctx(ctx)
+    co = np.ascontiguousarray(coeffs, dtype=np.int32).reshape(-1, 16)
+    n = co.shape[0]
+    cx = np.ascontiguousarray(np.broadcast_to(np.asarray(ctx0, np.uint8), (n,)))
+    pr = None if probs is None else np.ascontiguousarray(probs, dtype=np.uint8).reshape(-1)
+    lv = np.zeros((n, 16), np.int32)
+    dq = np.zeros((n, 16), np.int32)
+    _check(c._lib.zw_quant_blocks(c.handle, n, _ptr(co), _ptr(cx), ctype, first, 1 if use_trellis else 0, lambda_,
+                                  q_dc, q_ac, matrix_type, _ptr(pr), _ptr(lv), _ptr(dq)), "quant_blocks")
+    return lv, dq
+
+
 def loop_filter_frame(y, u, v, mbw, mbh, mb_flags, filter_type, filter_level, sharpness, segments_enabled=0,
                       seg_delta_values=0, seg_lf_level=(0, 0, 0, 0), lf_adj_enabled=0, ref_delta0=0, mode_delta0=0,
                       ctx=None):
@@ -369,6 +390,9 @@ class Pipeline:
     def encode(self):
         _check(self._lib.zw_pipe_encode(self._h), "zw_pipe_encode", EncodingError)
 
+    def run_pass1(self, write_recon=True):
+        _check(self._lib.zw_pipe_run_pass1(self._h, 1 if write_recon else 0), "zw_pipe_run_pass1", EncodingError)
+
     def run_device(self):
         _check(self._lib.zw_pipe_run_device(self._h), "zw_pipe_run_device", EncodingError)
 
@@ -394,6 +418,20 @@ class Pipeline:
         a = np.zeros(self.mbw * self.mbh, np.uint8)
         _check(self._lib.zw_pipe_read_alpha(self._h, i, _ptr(a)), "zw_pipe_read_alpha")
         return a
+
+    def enable_debug(self):
+        _check(self._lib.zw_pipe_enable_debug(self._h), "zw_pipe_enable_debug")
+
+    def i4_dump(self, i):
+        d = np.zeros(self.mbw * self.mbh * 16 * 34, np.int32)
+        _check(self._lib.zw_pipe_read_debug(self._h, i, _ptr(d)), "zw_pipe_read_debug")
+        return d.reshape(self.mbw * self.mbh, 16, 34)
+
+    def probs(self, i):
+        pr = np.zeros(4 * 8 * 3 * 11, np.uint8)
+        sp = ctypes.c_int()
+        _check(self._lib.zw_pipe_read_probs(self._h, i, _ptr(pr), ctypes.byref(sp)), "zw_pipe_read_probs")
+        return pr, sp.value
 
     def kernel_times(self):
         ms = (ctypes.c_float * 8)()

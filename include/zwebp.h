@@ -101,6 +101,14 @@ int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const si
 /* Kernel-level entry points (host buffers in/out) for parity testing. */
 int zw_rgb_to_yuv420(zw_ctx *ctx, const uint8_t *img, uint32_t width, uint32_t height, int bpp, uint8_t *y,
                      uint8_t *u, uint8_t *v);
+/* Quantisation of n 4x4 coefficient blocks (natural order in, zigzag levels and
+ * natural-order dequantised values out): VP8Matrix::quantize_coeff
+ * (encoder/cost.rs:457) or trellis_quantize_block (cost.rs:788-1006) with level
+ * costs from `probs` (NULL = default COEFF_PROBS).  ctype: 0 I16-AC, 1 Y2,
+ * 2 UV, 3 I4; matrix_type 0 Y1 (sharpened), 1 Y2, 2 UV; ctx0[i] in 0..2. */
+int zw_quant_blocks(zw_ctx *ctx, int n, const int32_t *coeffs, const uint8_t *ctx0, int ctype, int first,
+                    int use_trellis, uint32_t lambda, int q_dc, int q_ac, int matrix_type, const uint8_t *probs,
+                    int32_t *levels, int32_t *dequant);
 /* In-place loop filter of MB-aligned planes; per-MB flags (luma_mode 0..4,
  * segment, skip, non_zero_dct) as 4 bytes per MB, raster order. */
 int zw_loop_filter_frame(zw_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, uint32_t mbw, uint32_t mbh,
@@ -124,10 +132,19 @@ int zw_pipe_encode(zw_pipe *p);
  * token emission, for kernel timing.  Returns 0 or an error. */
 int zw_pipe_run_device(zw_pipe *p);
 int zw_pipe_output(zw_pipe *p, int frame, zw_bytes *out);
-/* Debug/parity taps (host copies). */
+/* Debug/parity taps (host copies).  zw_pipe_run_pass1 runs only the analysis
+ * and pass-1 kernels, optionally writing the pass-1 reconstruction into the
+ * recon planes (read with which=1). */
+int zw_pipe_run_pass1(zw_pipe *p, int write_recon);
 int zw_pipe_read_planes(zw_pipe *p, int frame, int which /*0 src,1 recon*/, uint8_t *y, uint8_t *u, uint8_t *v);
 int zw_pipe_read_mbinfo(zw_pipe *p, int frame, int pass, uint8_t *modes /*nmb*20*/, int16_t *levels /*nmb*400*/);
 int zw_pipe_read_alpha(zw_pipe *p, int frame, uint8_t *alpha);
+/* Pass-2 I4 dump for parity debugging: per MB 16 sub-blocks x 34 int32
+ * (fDCT coefficients[16], prediction[16], ctx0, sub-mode).  Enable before encoding. */
+int zw_pipe_enable_debug(zw_pipe *p);
+int zw_pipe_read_debug(zw_pipe *p, int frame, int32_t *out);
+/* Token probabilities (4*8*3*11) and skip probability used by pass 2. */
+int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
 /* Per-kernel device time of the last zw_pipe_encode/run_device (ms). */
 int zw_pipe_kernel_times(zw_pipe *p, float *ms, int n);
 

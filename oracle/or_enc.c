@@ -1138,8 +1138,9 @@ static void choose_mb(const enc_t *e, int mbx, int mby, mbinfo_t *mi)
     mi->skipped = 0;
 }
 
-static void store_recon(enc_t *e, const uint8_t *ws, int size, int stride_ws, uint8_t *plane, int ps, int x0, int y0)
+static void store_recon(const enc_t *e, const uint8_t *ws, int size, int stride_ws, uint8_t *plane, int ps, int x0, int y0)
 {
+    (void)e;
     for (int y = 0; y < size; y++) memcpy(plane + (size_t)(y0 + y) * ps + x0, ws + (y + 1) * stride_ws + 1, size);
 }
 
@@ -1202,6 +1203,14 @@ static void transform_luma(enc_t *e, int mbx, int mby, const mbinfo_t *mi, int32
                 const uint8_t *src = e->Y + (mby * 16 + sby * 4) * e->ys + mbx * 16 + sbx * 4;
                 fdct_res(src, e->ys, ws + y0 * OR_BPS + x0, OR_BPS, cur);
                 memcpy(lb + i * 16, cur, sizeof cur);
+                if (e->dbg && e->dbg->i4_dump && e->pass == 2) {
+                    int32_t *d = e->dbg->i4_dump + ((size_t)(mby * e->mbw + mbx) * 16 + i) * 34;
+                    memcpy(d, cur, 16 * sizeof(int32_t));
+                    for (int k = 0; k < 16; k++) d[16 + k] = ws[(y0 + k / 4) * OR_BPS + x0 + k % 4];
+                    int c0 = left_nz[sby] + top_nz[sbx];
+                    d[32] = c0 > 2 ? 2 : c0;
+                    d[33] = mi->bpred[i];
+                }
                 int nz;
                 if (e->do_trellis) {
                     int ctx0 = left_nz[sby] + top_nz[sbx];
@@ -1940,6 +1949,37 @@ int or_trellis_kat(const int32_t coeffs_in[16], int q_dc, int q_ac, int iq_dc, i
     int nz = trellis(c, out_levels, &m, lambda, first, &L, ctype, ctx0);
     memcpy(out_coeffs, c, sizeof c);
     return nz;
+}
+
+/* Batch form of quantize_coeff / trellis_quantize_block, same contract as the
+ * product's zw_quant_blocks (levels zigzag, dequantised natural). */
+void or_quant_blocks_c(int n, const int32_t *coeffs, const uint8_t *ctx0, int ctype, int first, int use_trellis,
+                       uint32_t lambda, int q_dc, int q_ac, int matrix_type, const uint8_t *probs, int32_t *levels,
+                       int32_t *dq_out)
+{
+    mtx_t m;
+    mtx_init(&m, q_dc, q_ac, matrix_type);
+    lcost_t *L = (lcost_t *)malloc(sizeof(lcost_t));
+    lcost_calc(L, probs ? (const uint8_t(*)[8][3][11])probs : COEFF_PROBS);
+    for (int b = 0; b < n; b++) {
+        int32_t c[16], lv[16] = {0};
+        memcpy(c, coeffs + 16 * b, sizeof c);
+        if (use_trellis) {
+            trellis(c, lv, &m, lambda, first, L, ctype, ctx0[b]);
+        } else {
+            for (int k = 0; k < 16; k++) {
+                int j = ZIGZAG[k];
+                lv[k] = k < first ? 0 : quant(&m, c[j], j);
+            }
+            for (int k = 0; k < 16; k++) {
+                int j = ZIGZAG[k];
+                c[j] = k < first ? 0 : dequant(&m, lv[k], j);
+            }
+        }
+        memcpy(levels + 16 * b, lv, sizeof lv);
+        memcpy(dq_out + 16 * b, c, sizeof c);
+    }
+    free(L);
 }
 
 uint32_t or_fixed_cost_i16(int mode) { return FIXED_COSTS_I16[mode]; }

@@ -54,6 +54,7 @@ typedef struct {
     uint8_t *seg_map;                     /* mbw*mbh */
     or_mb_info *p1_info, *p2_info;        /* mbw*mbh each */
     int32_t *levels;                      /* pass 2: mbw*mbh*25*16 zigzag levels (0..15 Y, 16 Y2, 17..20 U, 21..24 V) */
+    int32_t *i4_dump;                     /* pass 2 I4 MBs: mbw*mbh*16*34 (coeffs[16], pred[16], ctx0, mode) */
     uint32_t p1_stats[4][8][3][11];
     uint8_t final_probs[4][8][3][11];
     int seg_quant_index[4];
@@ -101,6 +102,9 @@ int or_bool_encoder_kat(const int *ops, int nops, uint8_t *out, int out_cap);
 int or_trellis_kat(const int32_t coeffs_in[16], int q_dc, int q_ac, int iq_dc, int iq_ac, uint32_t lambda,
                    int ctype, int first, int ctx0, int use_default_costs, int32_t out_levels[16],
                    int32_t out_coeffs[16]);
+void or_quant_blocks_c(int n, const int32_t *coeffs, const uint8_t *ctx0, int ctype, int first, int use_trellis,
+                       uint32_t lambda, int q_dc, int q_ac, int matrix_type, const uint8_t *probs, int32_t *levels,
+                       int32_t *dequant);
 uint32_t or_fixed_cost_i16(int mode);
 uint32_t or_fixed_cost_uv(int mode);
 size_t or_debug_struct_size(void);

@@ -23,7 +23,7 @@ class EncDebug(ctypes.Structure):
                 ("recon1_y", ctypes.c_void_p),
                 ("mb_alpha", ctypes.c_void_p), ("seg_map", ctypes.c_void_p),
                 ("p1_info", ctypes.c_void_p), ("p2_info", ctypes.c_void_p),
-                ("levels", ctypes.c_void_p),
+                ("levels", ctypes.c_void_p), ("i4_dump", ctypes.c_void_p),
                 ("p1_stats", ctypes.c_uint32 * (4 * 8 * 3 * 11)),
                 ("final_probs", ctypes.c_uint8 * (4 * 8 * 3 * 11)),
                 ("seg_quant_index", ctypes.c_int * 4),
@@ -66,6 +66,9 @@ def lib():
         L.or_trellis_kat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.or_quant_blocks_c.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.or_debug_struct_size.restype = ctypes.c_size_t
         assert L.or_debug_struct_size() == ctypes.sizeof(EncDebug), "EncDebug layout mismatch"
         _LIB = L
@@ -80,6 +83,18 @@ def blocks(fn, arr):
     a = np.ascontiguousarray(arr, dtype=np.int32).copy()
     getattr(lib(), fn)(_p(a), a.size // 16)
     return a
+
+
+def quant_blocks(coeffs, ctx0, ctype, first, use_trellis, lambda_, q_dc, q_ac, matrix_type, probs=None):
+    co = np.ascontiguousarray(coeffs, dtype=np.int32).reshape(-1, 16)
+    n = co.shape[0]
+    cx = np.ascontiguousarray(np.broadcast_to(np.asarray(ctx0, np.uint8), (n,)))
+    pr = None if probs is None else np.ascontiguousarray(probs, dtype=np.uint8).reshape(-1)
+    lv = np.zeros((n, 16), np.int32)
+    dq = np.zeros((n, 16), np.int32)
+    lib().or_quant_blocks_c(n, _p(co), _p(cx), ctype, first, 1 if use_trellis else 0, lambda_, q_dc, q_ac,
+                            matrix_type, _p(pr), _p(lv), _p(dq))
+    return lv, dq
 
 
 def rgb_to_yuv420(img, w, h, bpp):
@@ -107,7 +122,8 @@ def encode(img, w, h, color, quality=75, method=4, debug=False):
                     recon_y=np.zeros(ys, np.uint8), recon_u=np.zeros(cs, np.uint8), recon_v=np.zeros(cs, np.uint8),
                     recon1_y=np.zeros(ys, np.uint8),
                     mb_alpha=np.zeros(mbw * mbh, np.uint8), seg_map=np.zeros(mbw * mbh, np.uint8),
-                    levels=np.zeros(mbw * mbh * 25 * 16, np.int32))
+                    levels=np.zeros(mbw * mbh * 25 * 16, np.int32),
+                    i4_dump=np.zeros(mbw * mbh * 16 * 34, np.int32))
         p1 = (MbInfo * (mbw * mbh))()
         p2 = (MbInfo * (mbw * mbh))()
         dbg = EncDebug()

@@ -52,16 +52,6 @@ def test_rgb_to_yuv420(ctx, w, h, bpp):
 # --------------------------------------------------------------------------
 # a2..a18: the full encoder, stage by stage
 # --------------------------------------------------------------------------
-def _first_bad(a, b, per):
-    d = np.nonzero((a.reshape(-1, per) != b.reshape(-1, per)).any(axis=1))[0]
-    return int(d[0]) if d.size else -1
-
-
-def _mb_of_plane(i, stride, mbsz):
-    r, c = divmod(i, stride)
-    return (r // mbsz) * (stride // mbsz) + c // mbsz
-
-
 ENC_CASES = [
     (64, 48, "natural", 75, 4, 3),
     (300, 257, "natural", 75, 4, 3),
@@ -83,47 +73,109 @@ ENC_CASES = [
 ]
 
 
+def _mb_rows(a, per):
+    return a.reshape(-1, per)
+
+
+def _plane_mb_diff(a, b, stride, mb):
+    """MB indices whose (mb x mb) tile differs."""
+    A = a.reshape(-1, stride)
+    B = b.reshape(-1, stride)
+    d = (A != B).reshape(A.shape[0] // mb, mb, stride // mb, mb).any(axis=(1, 3))
+    return np.nonzero(d.reshape(-1))[0]
+
+
+def _modes_of(info, nmb):
+    m = np.array([[info[i].luma_mode, info[i].chroma_mode, info[i].skip, info[i].segment] + list(info[i].bpred)
+                  for i in range(nmb)], np.uint8)
+    m[m[:, 0] != 4, 4:] = 0
+    return m
+
+
 def _check_encode(ctx, w, h, kind, q, m, color, seed):
+    """Stage-by-stage comparison; collects every stage's first divergence."""
     img = _img(w, h, kind, seed, color)
     rc, ref, dbg = O.encode(img, w, h, color, q, m, debug=True)
     assert rc == 0
     p = zwebp.Pipeline(1, w, h, color, q, m, ctx=ctx)
+    rep = []
     try:
         p.upload(0, img)
-        p.encode()
-        ys, cs = p.mbw * 16, p.mbw * 8
-        y, u, v = p.planes(0, 0)
-        for a, b, s, n in ((y, dbg["src_y"], ys, "Y"), (u, dbg["src_u"], cs, "U"), (v, dbg["src_v"], cs, "V")):
-            assert np.array_equal(a, b), f"source plane {n} differs"
-        al = p.alpha(0)
-        bad = _first_bad(al, dbg["mb_alpha"], 1)
-        assert bad < 0, f"analysis alpha differs at MB {bad}: {al[bad]} vs {dbg['mb_alpha'][bad]}"
-        modes, levels = p.mbinfo(0, 2)
-        info = dbg["p2_info"]
         nmb = p.mbw * p.mbh
-        om = np.array([[info[i].luma_mode, info[i].chroma_mode, info[i].skip, info[i].segment] + list(info[i].bpred)
-                       for i in range(nmb)], np.uint8)
+        ys, cs = p.mbw * 16, p.mbw * 8
+        # pass 1 alone (with its reconstruction)
+        p.run_pass1(True)
+        y, u, v = p.planes(0, 0)
+        for a, b, n in ((y, dbg["src_y"], "Y"), (u, dbg["src_u"], "U"), (v, dbg["src_v"], "V")):
+            if not np.array_equal(a, b):
+                rep.append(f"source plane {n} differs")
+        if dbg["segments_enabled"]:
+            al = p.alpha(0)
+            d = np.nonzero(al != dbg["mb_alpha"])[0]
+            if d.size:
+                rep.append(f"alpha: {d.size} MBs differ, first {d[0]}: {al[d[0]]} vs {dbg['mb_alpha'][d[0]]}")
+        m1, _ = p.mbinfo(0, 1)
+        g1 = m1.copy()
+        g1[g1[:, 0] != 4, 4:] = 0
+        o1 = _modes_of(dbg["p1_info"], nmb)
+        d = np.nonzero((g1[:, [0, 1]] != o1[:, [0, 1]]).any(axis=1) | (g1[:, 4:] != o1[:, 4:]).any(axis=1))[0]
+        if d.size:
+            i = int(d[0])
+            rep.append(f"pass-1 modes: {d.size} MBs differ, first MB {i} (x={i % p.mbw},y={i // p.mbw}): "
+                       f"{g1[i].tolist()} vs {o1[i].tolist()}")
+        r1y, _, _ = p.planes(0, 1)
+        d = _plane_mb_diff(r1y, dbg["recon1_y"], ys, 16)
+        if d.size:
+            rep.append(f"pass-1 recon Y: {d.size} MBs differ, first MB {d[0]}")
+        # full encode
+        p.enable_debug()
+        p.encode()
+        gp, gsp = p.probs(0)
+        if not np.array_equal(gp, dbg["final_probs"]):
+            rep.append(f"pass-2 probabilities differ in {int((gp != dbg['final_probs']).sum())} entries")
+        if gsp != dbg["skip_prob"]:
+            rep.append(f"skip prob {gsp} vs {dbg['skip_prob']}")
+        modes, levels = p.mbinfo(0, 2)
         gm = modes.copy()
-        gm[gm[:, 0] != 4, 4:] = 0  # bpred only meaningful for I4
-        om[om[:, 0] != 4, 4:] = 0
-        bad = _first_bad(gm, om, 20)
-        assert bad < 0, f"pass-2 modes differ at MB {bad} (mbx={bad % p.mbw}, mby={bad // p.mbw}): {gm[bad]} vs {om[bad]}"
+        gm[gm[:, 0] != 4, 4:] = 0
+        om = _modes_of(dbg["p2_info"], nmb)
+        d = np.nonzero((gm != om).any(axis=1))[0]
+        if d.size:
+            i = int(d[0])
+            rep.append(f"pass-2 modes: {d.size} MBs differ, first MB {i} (x={i % p.mbw},y={i // p.mbw}): "
+                       f"{gm[i].tolist()} vs {om[i].tolist()}")
         ol = dbg["levels"].reshape(nmb, 25, 16)
         gl = levels.astype(np.int32)
         gl[gm[:, 2] == 1] = 0
-        bad = _first_bad(gl, ol, 400)
-        if bad >= 0:
-            blk = int(np.nonzero((gl[bad] != ol[bad]).any(axis=1))[0][0])
-            raise AssertionError(f"levels differ at MB {bad} block {blk}: {gl[bad, blk]} vs {ol[bad, blk]}")
+        gl[gm[:, 0] == 4, 16] = 0
+        d = np.nonzero((gl != ol).reshape(nmb, -1).any(axis=1))[0]
+        if d.size:
+            i = int(d[0])
+            blk = int(np.nonzero((gl[i] != ol[i]).any(axis=1))[0][0])
+            rep.append(f"levels: {d.size} MBs differ, first MB {i} block {blk} (mode {gm[i, 0]}): "
+                       f"{gl[i, blk].tolist()} vs {ol[i, blk].tolist()}")
+            if gm[i, 0] == 4:
+                gd = p.i4_dump(0)[i, blk]
+                od = dbg["i4_dump"].reshape(nmb, 16, 34)[i, blk]
+                rep.append(f"  I4 dump gpu coeffs {gd[:16].tolist()} pred {gd[16:32].tolist()} ctx0 {gd[32]} mode {gd[33]}")
+                rep.append(f"  I4 dump orc coeffs {od[:16].tolist()} pred {od[16:32].tolist()} ctx0 {od[32]} mode {od[33]}")
         ry, ru, rv = p.planes(0, 1)
         for a, b, s, mb, n in ((ry, dbg["recon_y"], ys, 16, "Y"), (ru, dbg["recon_u"], cs, 8, "U"),
                                (rv, dbg["recon_v"], cs, 8, "V")):
-            d = np.nonzero(a != b)[0]
-            assert d.size == 0, f"recon {n} differs first at MB {_mb_of_plane(int(d[0]), s, mb)}"
+            d = _plane_mb_diff(a, b, s, mb)
+            if d.size:
+                A, B = a.reshape(-1, s), b.reshape(-1, s)
+                r0, c0 = (d[0] // (s // mb)) * mb, (d[0] % (s // mb)) * mb
+                ta, tb = A[r0:r0 + mb, c0:c0 + mb], B[r0:r0 + mb, c0:c0 + mb]
+                pos = np.argwhere(ta != tb)
+                rep.append(f"recon {n}: {d.size} MBs differ, first MB {d[0]}, {len(pos)} px, first at {pos[0].tolist()}"
+                           f" gpu {int(ta[tuple(pos[0])])} oracle {int(tb[tuple(pos[0])])}")
         out = p.output(0)
-        assert out == ref, f"bitstream differs (len {len(out)} vs {len(ref)})"
+        if out != ref:
+            rep.append(f"bitstream differs (len {len(out)} vs {len(ref)})")
     finally:
         p.close()
+    assert not rep, "\n".join(rep)
     return ref
 
 
@@ -264,3 +316,28 @@ def test_1080p_encode_decode_roundtrip(ctx):
     fr = zwebp.vp8_decode_frame(ref, ctx=ctx)
     rc, r = O.decode(ref)
     assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+
+
+# --------------------------------------------------------------------------
+# a7/a8: quantisation and trellis on independent blocks
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("ctype,first,mtype", [(3, 0, 0), (0, 1, 0), (2, 0, 2), (1, 0, 1)])
+@pytest.mark.parametrize("trel", [False, True])
+@pytest.mark.parametrize("qi", [0, 10, 26, 60, 127])
+def test_quant_blocks(ctx, ctype, first, mtype, trel, qi):
+    rng = np.random.default_rng(qi * 31 + ctype * 7 + first + trel)
+    n = 3000
+    scale = rng.choice([8, 40, 200, 1000, 2000], size=(n, 1))
+    co = (rng.standard_normal((n, 16)) * scale / (1 + np.arange(16))).astype(np.int32)
+    ctx0 = rng.integers(0, 3, n).astype(np.uint8)
+    dc_q = [4, 13, 24, 50, 157][[0, 10, 26, 60, 127].index(qi)]
+    ac_q = [4, 13, 30, 74, 284][[0, 10, 26, 60, 127].index(qi)]
+    probs = rng.integers(1, 256, size=(4, 8, 3, 11)).astype(np.uint8)
+    lam = int(rng.integers(1, 5000))
+    for pr in (None, probs):
+        g = zwebp.quant_blocks(co, ctx0, ctype, first, trel, lam, dc_q, ac_q, mtype, pr, ctx=ctx)
+        o = O.quant_blocks(co, ctx0, ctype, first, trel, lam, dc_q, ac_q, mtype, pr)
+        bad = np.nonzero((g[0] != o[0]).any(axis=1))[0]
+        assert bad.size == 0, f"{bad.size} blocks differ; first {co[bad[0]].tolist()} ctx {ctx0[bad[0]]}: " \
+                              f"{g[0][bad[0]].tolist()} vs {o[0][bad[0]].tolist()}"
+        assert np.array_equal(g[1], o[1])
