@@ -207,9 +207,9 @@ extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __r
                 }
             }
             // --- chroma ---
-            if (lane < 36) {
-                const int pl = lane >= 18;
-                const int i = pl ? lane - 18 : lane;
+            if (lane < 34) {  // per plane: corner, 8 top, 8 left
+                const int pl = lane >= 17;
+                const int i = pl ? lane - 17 : lane;
                 uint8_t* w = pl ? W->cv : W->cu;
                 const uint8_t* top = pl ? top_v : top_u;
                 const uint8_t* lft = pl ? W->left_v : W->left_u;

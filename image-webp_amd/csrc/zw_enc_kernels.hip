@@ -463,9 +463,9 @@ __device__ void build_luma_border(const Ctx& C)
 __device__ void build_chroma_border(const Ctx& C)
 {
     const int l = C.lane;
-    if (l < 36) {
-        const int pl = l >= 18;
-        const int i = pl ? l - 18 : l;
+    if (l < 34) {  // per plane: corner, 8 top, 8 left
+        const int pl = l >= 17;
+        const int i = pl ? l - 17 : l;
         uint8_t* w = pl ? C.W->cv : C.W->cu;
         const uint8_t* top = pl ? C.top_v : C.top_u;
         const uint8_t* left = pl ? C.W->left_v : C.W->left_u;
