@@ -73,6 +73,7 @@ def main():
     import torch
     import torch.distributed as dist
     import zwebp
+    from zwebp.shard import frame_seed, reduce_max
     from zwebp.synth import synth_rgba
 
     if world > 1:
@@ -84,7 +85,8 @@ def main():
     w, h, F = a.width, a.height, a.frames
     ctx = zwebp.Context(local)
     pipe = zwebp.Pipeline(F, w, h, zwebp.ColorType.Rgba8, a.quality, a.method, ctx=ctx)
-    imgs = [synth_rgba(w, h, 0x5EED0000 + rank * 1000 + i) for i in range(min(a.distinct, F))]
+    # weak scaling: rank r owns global frames [r*F, (r+1)*F); `distinct` of them are generated
+    imgs = [synth_rgba(w, h, frame_seed(rank * F + i)) for i in range(min(a.distinct, F))]
     for i in range(F):
         pipe.upload(i, imgs[i % len(imgs)])
     nmb = pipe.mbw * pipe.mbh
@@ -104,10 +106,7 @@ def main():
         kt += np.array(pipe.kernel_times())
     barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = reduce_max(el, dev)
     total_frames = F * a.steps * world
     bytes_out = sum(len(pipe.output(i)) for i in range(min(F, 4)))
 

@@ -1169,7 +1169,32 @@ __device__ void publish(int* progress, int wave, int val)
     __builtin_amdgcn_wave_barrier();
 }
 
-extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
+#ifdef ZW_PHASE_PROF
+// Per-phase cycle counters (profiling builds only): [pass-1][phase].
+__device__ unsigned long long zw_phase_cycles_dev[2][16];
+#define PH_START() long long ph_t_ = clock64()
+#define PH_MARK(k)                                                                  \
+    do {                                                                            \
+        const long long n_ = clock64();                                             \
+        if (lane == 0) atomicAdd(&zw_phase_cycles_dev[PASS - 1][k], (unsigned long long)(n_ - ph_t_)); \
+        ph_t_ = n_;                                                                 \
+    } while (0)
+extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_phase_cycles_dev), sizeof(zw_phase_cycles_dev)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long z[2][16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(zw_phase_cycles_dev), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define PH_START() (void)0
+#define PH_MARK(k) (void)0
+#endif
+
+template <int PASS>
+__device__ __forceinline__ void encode_body(const EncArgs& a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x;
@@ -1209,7 +1234,7 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
         top_v[i] = 127;
     }
     for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
-    for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = a.pass == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
+    for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     if (threadIdx.x < NW) progress[threadIdx.x] = -1;
     __syncthreads();
 
@@ -1224,10 +1249,10 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
     C.top_v = top_v;
     C.top_c = top_c;
     C.top_derr = top_derr;
-    const bool trel = a.pass == 2 && P->do_trellis;
+    const bool trel = PASS == 2 && P->do_trellis;
     const size_t nmb = (size_t)mbw * mbh;
 
-    if (a.pass == 1 && wv == 0) {
+    if (PASS == 1 && wv == 0) {
         // ---- pass-1 chroma raster chain ----
         if (lane < 4) W->left_derr[lane] = 0;
         for (int mby = 0; mby < mbh; mby++) {
@@ -1237,11 +1262,14 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
             }
             wsync();
             for (int mbx = 0; mbx < mbw; mbx++) {
+                PH_START();
                 setup_ctx(C, &a, P, T, W, smem, mbx, mby);
                 build_chroma_border(C);
                 const int cm = pick_uv(C);
+                PH_MARK(8);
                 int uvnz[8];
                 final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+                PH_MARK(9);
                 store_chroma_borders(C);
                 ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
                 if (lane == 0) o->chroma_mode = (uint8_t)cm;
@@ -1253,8 +1281,8 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
         return;
     }
 
-    const int nrw = a.pass == 1 ? NW - 1 : NW;  // waves on the luma wavefront
-    const int rw = a.pass == 1 ? wv - 1 : wv;
+    const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
+    const int rw = PASS == 1 ? wv - 1 : wv;
     for (int mby = rw; mby < mbh; mby += nrw) {
         if (lane < 20) W->left_y[lane] = 129;
         if (lane < 12) {
@@ -1264,33 +1292,40 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
         }
         if (lane < 4) W->left_derr[lane] = 0;
         wsync();
-        const int prevw = mby > 0 ? ((mby - 1) % nrw) + (a.pass == 1 ? 1 : 0) : 0;
+        const int prevw = mby > 0 ? ((mby - 1) % nrw) + (PASS == 1 ? 1 : 0) : 0;
         for (int mbx = 0; mbx < mbw; mbx++) {
+            PH_START();
             if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
+            PH_MARK(0);
             setup_ctx(C, &a, P, T, W, smem, mbx, mby);
             build_luma_border(C);
             int lm;
             unsigned long long i16s;
             pick_i16(C, lm, i16s);
             wsync();
+            PH_MARK(1);
             if (P->method > 1) {
                 const unsigned long long thr = 211ull * C.S->l_mode;
                 if (P->method >= 5 || i16s > thr || lm != 0) {
                     if (pick_i4(C, i16s)) lm = 4;
                 }
             }
+            PH_MARK(2);
             int cm = 0;
-            if (a.pass == 2) {
+            if (PASS == 2) {
                 build_chroma_border(C);
                 cm = pick_uv(C);
             }
+            PH_MARK(3);
             int ynz[16];
             const int lnz = final_luma(C, lm, trel, ynz);
+            PH_MARK(4);
             int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             int cnz = 0;
-            if (a.pass == 2) cnz = final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+            if (PASS == 2) cnz = final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+            PH_MARK(5);
             ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
-            if (a.pass == 2) {
+            if (PASS == 2) {
                 const int skip = !(lnz | cnz);
                 // complexity (encode_residual_data semantics / skip clearing)
                 if (lane == 0) {
@@ -1331,9 +1366,13 @@ extern "C" __global__ __launch_bounds__(WG) void k_encode(EncArgs a)
             if (lane < 16) o->bpred[lane] = lm == 4 ? W->modes[lane] : 0;
             store_luma_borders(C);
             publish(progress, wv, mby * 65536 + mbx + 1);
+            PH_MARK(6);
         }
     }
 }
+
+extern "C" __global__ __launch_bounds__(WG) void k_encode_pass1(EncArgs a) { encode_body<1>(a); }
+extern "C" __global__ __launch_bounds__(WG) void k_encode_pass2(EncArgs a) { encode_body<2>(a); }
 
 // ---------------------------------------------------------------------------
 // Kernel-level entry: quantisation (simple or trellis) of independent 4x4
@@ -1455,9 +1494,11 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
     const size_t lds = zw_encode_lds_bytes(mbw);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_encode, dim3(nframes), dim3(WG), lds, s, a);
+    if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(WG), lds, s, a);
+    else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(WG), lds, s, a);
     return hipGetLastError();
 }
