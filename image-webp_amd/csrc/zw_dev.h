@@ -30,6 +30,29 @@ __constant__ uint8_t d_I4_IDX[10][16] = {
 
 #define DI __device__ __forceinline__
 
+// Compile-time copies of the small position tables: indexed with constants
+// inside unrolled loops they fold into immediates.
+DI int kZZ(int n)
+{
+    constexpr uint8_t t[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+    return t[n];
+}
+DI int kBand(int n)
+{
+    constexpr uint8_t t[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+    return t[n];
+}
+DI int kWTrellis(int j)
+{
+    constexpr uint16_t t[16] = {30, 27, 19, 11, 27, 24, 17, 10, 19, 17, 12, 8, 11, 10, 8, 6};
+    return t[j];
+}
+DI int kWY(int j)
+{
+    constexpr uint16_t t[16] = {38, 32, 20, 9, 32, 28, 17, 7, 20, 17, 10, 4, 9, 7, 4, 2};
+    return t[j];
+}
+
 DI int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 DI int iabs(int v) { return v < 0 ? -v : v; }
 
@@ -230,21 +253,40 @@ DI int ttransform(const int* in)
     for (int i = 0; i < 4; i++) {
         int a0 = tmp[i] + tmp[8 + i], a1 = tmp[4 + i] + tmp[12 + i];
         int a2 = tmp[4 + i] - tmp[12 + i], a3 = tmp[i] - tmp[8 + i];
-        sum += d_VP8_WEIGHT_Y[i] * iabs(a0 + a1) + d_VP8_WEIGHT_Y[4 + i] * iabs(a3 + a2) +
-               d_VP8_WEIGHT_Y[8 + i] * iabs(a3 - a2) + d_VP8_WEIGHT_Y[12 + i] * iabs(a0 - a1);
+        sum += kWY(i) * iabs(a0 + a1) + kWY(4 + i) * iabs(a3 + a2) +
+               kWY(8 + i) * iabs(a3 - a2) + kWY(12 + i) * iabs(a0 - a1);
     }
     return sum;
 }
 
-DI uint32_t bitcost(int bit, int p) { return bit ? d_VP8_ENTROPY_COST[255 - p] : d_VP8_ENTROPY_COST[p]; }
-
-// Tables the encoder kernels keep in LDS.
+// Tables the encoder kernels keep in LDS (per-lane indexed lookups must not go
+// to constant memory: a divergent index turns into a vector load from L2).
 struct LdsTables {
     uint16_t lc[4][8][3][68];
     uint16_t eob[4][8][3];
     uint16_t init[4][8][3];
     uint8_t probs[4][8][3][11];
+    uint16_t lfc[2048];       // VP8_LEVEL_FIXED_COSTS
+    uint16_t ent[256];        // VP8_ENTROPY_COST
+    uint16_t fci4[10][10][10];  // VP8_FIXED_COSTS_I4
+    uint8_t i4idx[10][16];    // d_I4_IDX
+    uint8_t zz[16];           // ZIGZAG
+    uint8_t bands[17];        // VP8_ENC_BANDS
+    uint8_t pad[15];
 };
+
+// Static (frame-independent) part of LdsTables; all threads of the block call it.
+DI void load_static_tables(LdsTables* T, int tid, int nt)
+{
+    for (int i = tid; i < 2048; i += nt) T->lfc[i] = d_VP8_LEVEL_FIXED_COSTS[i];
+    for (int i = tid; i < 256; i += nt) T->ent[i] = d_VP8_ENTROPY_COST[i];
+    for (int i = tid; i < 1000; i += nt) (&T->fci4[0][0][0])[i] = (&d_VP8_FIXED_COSTS_I4[0][0][0])[i];
+    for (int i = tid; i < 160; i += nt) (&T->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
+    for (int i = tid; i < 16; i += nt) T->zz[i] = d_ZIGZAG[i];
+    for (int i = tid; i < 17; i += nt) T->bands[i] = d_VP8_ENC_BANDS[i];
+}
+
+DI uint32_t bitcost(const LdsTables* T, int bit, int p) { return bit ? T->ent[255 - p] : T->ent[p]; }
 
 // get_residual_cost (cost.rs:1670 / SSE2 :1735).  'c' is indexed by position n
 // exactly as the reference indexes Residual::coeffs (natural-order arrays are
@@ -256,20 +298,87 @@ DI uint32_t rcost(const int* c, int ctx0, int ctype, const LdsTables* T)
 #pragma unroll
     for (int n = 0; n < 16; n++)
         if (c[n] != 0) last = n;
-    const int p0 = T->probs[ctype][d_VP8_ENC_BANDS[FIRST]][ctx0][0];
-    if (last < 0) return bitcost(0, p0);
-    uint32_t cost = ctx0 == 0 ? bitcost(1, p0) : 0;
+    const int p0 = T->probs[ctype][T->bands[FIRST]][ctx0][0];
+    if (last < 0) return bitcost(T, 0, p0);
+    uint32_t cost = ctx0 == 0 ? bitcost(T, 1, p0) : 0;
     int ctx = ctx0;
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
         if (n <= last) {
             int v = iabs(c[n]);
-            cost += d_VP8_LEVEL_FIXED_COSTS[v < 2047 ? v : 2047] + T->lc[ctype][d_VP8_ENC_BANDS[n]][ctx][v < 67 ? v : 67];
+            cost += T->lfc[v < 2047 ? v : 2047] + T->lc[ctype][T->bands[n]][ctx][v < 67 ? v : 67];
             ctx = v < 2 ? v : 2;
         }
     }
-    if (last < 15) cost += bitcost(0, T->probs[ctype][d_VP8_ENC_BANDS[last + 1]][ctx][0]);
+    if (last < 15) cost += bitcost(T, 0, T->probs[ctype][T->bands[last + 1]][ctx][0]);
     return cost;
+}
+
+// ---------------------------------------------------------------------------
+// 16-lane group forms: lane k = lane & 15 holds element k of one 4x4 block
+// (row k >> 2, column k & 3); four blocks per wave.  Same arithmetic as the
+// serial forms above, exchanged through ds_bpermute within the group.
+// ---------------------------------------------------------------------------
+DI int gget(int v, int k) { return __shfl(v, k, 16); }
+
+DI int fdct_g(int d, int k)
+{
+    const int i = k >> 2, j = k & 3;
+    const int d0 = gget(d, i * 4), d1 = gget(d, i * 4 + 1), d2 = gget(d, i * 4 + 2), d3 = gget(d, i * 4 + 3);
+    const int a = (d0 + d3) * 8, bb = (d1 + d2) * 8, c = (d1 - d2) * 8, dd = (d0 - d3) * 8;
+    const int t = j == 0 ? a + bb : (j == 2 ? a - bb : (j == 1 ? (c * 2217 + dd * 5352 + 14500) >> 12
+                                                                : (dd * 2217 - c * 5352 + 7500) >> 12));
+    const int t0 = gget(t, j), t1 = gget(t, 4 + j), t2 = gget(t, 8 + j), t3 = gget(t, 12 + j);
+    const int A = t0 + t3, B = t1 + t2, Cc = t1 - t2, D = t0 - t3;
+    return i == 0 ? (A + B + 7) >> 4
+                  : (i == 2 ? (A - B + 7) >> 4
+                            : (i == 1 ? ((Cc * 2217 + D * 5352 + 12000) >> 16) + (D != 0 ? 1 : 0)
+                                      : (D * 2217 - Cc * 5352 + 51000) >> 16));
+}
+
+DI int idct_g(int x, int k)
+{
+    const int i = k >> 2, j = k & 3;
+    const int x0 = gget(x, j), x1 = gget(x, 4 + j), x2 = gget(x, 8 + j), x3 = gget(x, 12 + j);
+    int a1 = x0 + x2, b1 = x0 - x2;
+    int c1 = ((x1 * 35468) >> 16) - (x3 + ((x3 * 20091) >> 16));
+    int d1 = (x1 + ((x1 * 20091) >> 16)) + ((x3 * 35468) >> 16);
+    const int t = i == 0 ? a1 + d1 : (i == 1 ? b1 + c1 : (i == 2 ? b1 - c1 : a1 - d1));
+    const int y0 = gget(t, i * 4), y1 = gget(t, i * 4 + 1), y2 = gget(t, i * 4 + 2), y3 = gget(t, i * 4 + 3);
+    a1 = y0 + y2;
+    b1 = y0 - y2;
+    c1 = ((y1 * 35468) >> 16) - (y3 + ((y3 * 20091) >> 16));
+    d1 = (y1 + ((y1 * 20091) >> 16)) + ((y3 * 35468) >> 16);
+    return j == 0 ? (a1 + d1 + 4) >> 3 : (j == 1 ? (b1 + c1 + 4) >> 3 : (j == 2 ? (b1 - c1 + 4) >> 3 : (a1 - d1 + 4) >> 3));
+}
+
+// 16-bit nonzero mask of the lane's group.
+DI unsigned gmask(bool pred)
+{
+    const unsigned long long b = __ballot(pred);
+    return (unsigned)(b >> (__lane_id() & 48)) & 0xffffu;
+}
+
+// rcost<FIRST> with lane k holding c[k] (position n = k, quirk A1).  Result is
+// uniform across the group.
+template <int FIRST>
+DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
+{
+    const unsigned m = gmask(v != 0);
+    const int last = m ? 31 - __clz((int)m) : -1;
+    const int av = iabs(v);
+    const int pav = gget(av, (k + 15) & 15);
+    const int ctx = k == FIRST ? ctx0 : (pav < 2 ? pav : 2);
+    int term = 0;
+    if (k >= FIRST && k <= last)
+        term = T->lfc[av < 2047 ? av : 2047] + T->lc[ctype][T->bands[k]][ctx][av < 67 ? av : 67];
+    uint32_t sum = (uint32_t)red16(term);
+    const int p0 = T->probs[ctype][T->bands[FIRST]][ctx0][0];
+    const int lastv = gget(av, last < 0 ? 0 : last);
+    if (last < 0) return bitcost(T, 0, p0);
+    sum += ctx0 == 0 ? bitcost(T, 1, p0) : 0;
+    if (last < 15) sum += bitcost(T, 0, T->probs[ctype][T->bands[last + 1]][lastv == 1 ? 1 : 2][0]);
+    return sum;
 }
 
 // trellis_quantize_block (cost.rs:788-1006).  coeffs (natural order) become the
@@ -284,11 +393,11 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
     int last = FIRST - 1;
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
-        int j = d_ZIGZAG[n];
+        int j = kZZ(n);
         if (coeffs[j] * coeffs[j] > thresh) last = n;
     }
     if (last < 15) last++;
-    const int bfirst = d_VP8_ENC_BANDS[FIRST];
+    const int bfirst = kBand(FIRST);
     long long best = (long long)T->eob[ctype][bfirst][ctx0] * lambda;
     long long init = ctx0 == 0 ? (long long)T->init[ctype][bfirst][ctx0] * lambda : 0;
     long long s0 = init, s1 = init;
@@ -302,7 +411,7 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
         lv0[n] = 0;
         sg[n] = 0;
         if (n <= last) {
-            const int j = d_ZIGZAG[n];
+            const int j = kZZ(n);
             const int q = j == 0 ? (int)m.q[0] : qac;
             const uint32_t iq = j == 0 ? m.iq[0] : m.iq[1];
             const int sign = coeffs[j] < 0;
@@ -311,7 +420,7 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
             l0 = l0 < 2047 ? l0 : 2047;
             int thr = (int)(((uint32_t)cws * iq + tbias) >> 17);
             thr = thr < 2047 ? thr : 2047;
-            const int band = d_VP8_ENC_BANDS[n];
+            const int band = kBand(n);
             long long ns0 = MAXC, ns1 = MAXC;
             int nc0 = 0, nc1 = 0;
 #pragma unroll
@@ -322,10 +431,10 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
                 else nc1 = ctx;
                 if (level <= thr) {
                     const int ne = cws - level * q;
-                    const long long dd = (long long)d_VP8_WEIGHT_TRELLIS[j] * ((long long)(ne * ne) - (long long)(cws * cws));
+                    const long long dd = (long long)kWTrellis(j) * ((long long)(ne * ne) - (long long)(cws * cws));
                     const long long base = 256 * dd;
                     const int lv = level < 67 ? level : 67;
-                    const int fixed = d_VP8_LEVEL_FIXED_COSTS[level] + (level > 0 ? 256 : 0);
+                    const int fixed = T->lfc[level] + (level > 0 ? 256 : 0);
                     long long sc0 = s0 + (long long)(fixed + T->lc[ctype][band][c0][lv]) * lambda;
                     long long sc1 = s1 + (long long)(fixed + T->lc[ctype][band][c1][lv]) * lambda;
                     int pb = sc1 < sc0;
@@ -335,7 +444,7 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
                     else ns1 = cur;
                     if (level != 0 && cur < best) {
                         long long eob = 0;
-                        if (n < 15) eob = (long long)T->eob[ctype][d_VP8_ENC_BANDS[n + 1]][ctx] * lambda;
+                        if (n < 15) eob = (long long)T->eob[ctype][kBand(n + 1)][ctx] * lambda;
                         long long term = cur + eob;
                         if (term < best) {
                             best = term;
@@ -357,14 +466,14 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
         out[n] = 0;
-        coeffs[d_ZIGZAG[n]] = 0;
+        coeffs[kZZ(n)] = 0;
     }
     if (bn < 0) return 0;
     int nz = 0, cd = bd;
 #pragma unroll
     for (int n = 15; n >= FIRST; n--) {
         if (n <= bn) {
-            const int j = d_ZIGZAG[n];
+            const int j = kZZ(n);
             const int level = lv0[n] + cd;
             const int v = sg[n] ? -level : level;
             out[n] = v;

@@ -397,6 +397,7 @@ struct EncArgs {
 
 // per-wave LDS scratch
 struct WaveLds {
+    uint8_t sy[256], su[64], sv[64];  // source MB (staged per MB)
     uint8_t ws[17 * ZW_BPS];      // luma work buffer (create_border_luma layout)
     uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
     uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
@@ -427,7 +428,8 @@ struct Ctx {
     WaveLds* W;
     uint8_t *top_y, *top_u, *top_v, *top_c;
     int8_t* top_derr;
-    const uint8_t *srcY, *srcU, *srcV;  // MB origin
+    const uint8_t *srcY, *srcU, *srcV;  // MB origin (HBM)
+    const uint8_t *sY, *sU, *sV;        // the same MB staged in LDS (strides 16 / 8)
     int ys, cs;
     int mbx, mby, lane, seg;
 };
@@ -499,7 +501,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
             const int y = by * 4 + i, x = bx * 4 + j;
             const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
             int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - P0)));
-            const int sv = C.srcY[(size_t)y * C.ys + x];
+            const int sv = C.sY[y * 16 + x];
             src[i * 4 + j] = sv;
             pr[i * 4 + j] = p;
             r[i * 4 + j] = sv - p;
@@ -538,7 +540,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     for (int k = 1; k < 16; k++) dq[k] = q[k] * (int)S.y1.q[1];
     idct16(dq);
     int rec[16], sse = 0, flat = 1;
-    const int s00 = C.srcY[0];
+    const int s00 = C.sY[0];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         rec[k] = clamp255(pr[k] + dq[k]);
@@ -604,9 +606,9 @@ __device__ void i4_values(const Ctx& C, int x0, int y0)
     }
     wsync();
 }
-__device__ __forceinline__ int i4_pred_px(const WaveLds* W, int mode, int p)
+__device__ __forceinline__ int i4_pred_px(const WaveLds* W, const LdsTables* T, int mode, int p)
 {
-    const int idx = d_I4_IDX[mode][p];
+    const int idx = T->i4idx[mode][p];
     if (idx == 255) return W->V[38];
     if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
     return W->V[idx];
@@ -637,13 +639,13 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         // predictions + SSE: lane = g*16 + p, modes g, g+4, g+8
         {
             const int g = l >> 4, p = l & 15;
-            const int sv = C.srcY[(size_t)(sby * 4 + (p >> 2)) * C.ys + sbx * 4 + (p & 3)];
+            const int sv = C.sY[(sby * 4 + (p >> 2)) * 16 + sbx * 4 + (p & 3)];
 #pragma unroll
             for (int t = 0; t < 3; t++) {
                 const int mm = g + 4 * t;
                 int e = 0;
                 if (mm < 10) {
-                    const int v = i4_pred_px(W, mm, p);
+                    const int v = i4_pred_px(W, C.T, mm, p);
                     W->pred[mm][p] = (uint8_t)v;
                     e = (sv - v) * (sv - v);
                 }
@@ -665,10 +667,10 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         if (l < K) {
             const int mm = W->cand[l];
             int src[16], r[16], q[16];
-            const uint8_t* sp = C.srcY + (size_t)(sby * 4) * C.ys + sbx * 4;
+            const uint8_t* sp = C.sY + (sby * 4) * 16 + sbx * 4;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                src[k] = sp[(size_t)(k >> 2) * C.ys + (k & 3)];
+                src[k] = sp[(k >> 2) * 16 + (k & 3)];
                 r[k] = src[k] - W->pred[mm][k];
             }
             fdct16(r);
@@ -689,7 +691,7 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
                 const int d = src[k] - clamp255(W->pred[mm][k] + dq[k]);
                 sse += (uint32_t)(d * d);
             }
-            const uint32_t rate = (uint32_t)d_VP8_FIXED_COSTS_I4[tctx][lctx][mm] + cc;
+            const uint32_t rate = (uint32_t)C.T->fci4[tctx][lctx][mm] + cc;
             const unsigned long long sc = rdscore(sse, rate, S.l_i4);
             int* R = W->cres[l];
             R[0] = (int)(sc & 0xffffffff);
@@ -715,7 +717,7 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         const int bnz = W->cres[bk][4];
         top_nz[sbx] = bnz;
         left_nz[sby] = bnz;
-        total_mc += d_VP8_FIXED_COSTS_I4[tctx][lctx][bmode];
+        total_mc += C.T->fci4[tctx][lctx][bmode];
         running += rdscore((uint32_t)W->cres[bk][2], (uint32_t)W->cres[bk][3], S.l_mode);
         if (l == 0) W->modes[i] = (uint8_t)bmode;
         if (running >= i16_score) { wsync(); return false; }
@@ -740,7 +742,7 @@ __device__ int pick_uv(const Ctx& C)
     if (l < 32) {
         const int m = l >> 3, b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
         const uint8_t* w = pl ? W->cv : W->cu;
-        const uint8_t* sp = (pl ? C.srcV : C.srcU) + (size_t)(by * 4) * C.cs + bx * 4;
+        const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
         int dcv = 128;
         {
             uint32_t s = 0;
@@ -763,7 +765,7 @@ __device__ int pick_uv(const Ctx& C)
                 const int y = by * 4 + i, x = bx * 4 + j;
                 const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
                 const int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - w[0])));
-                const int sv = sp[(size_t)i * C.cs + j];
+                const int sv = sp[i * 8 + j];
                 src[i * 4 + j] = sv;
                 pr[i * 4 + j] = p;
                 r[i * 4 + j] = sv - p;
@@ -836,7 +838,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                     const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
                     const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - P0)));
                     pr[i * 4 + j] = p;
-                    c[i * 4 + j] = (int)C.srcY[(size_t)y * C.ys + x] - p;
+                    c[i * 4 + j] = (int)C.sY[y * 16 + x] - p;
                 }
             fdct16(c);
             W->dc[b] = c[0];
@@ -855,7 +857,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                 nz |= y2q[k] != 0;
             }
 #pragma unroll
-            for (int n = 0; n < 16; n++) W->lev[16][n] = (int16_t)y2q[d_ZIGZAG[n]];
+            for (int n = 0; n < 16; n++) W->lev[16][n] = (int16_t)y2q[kZZ(n)];
 #pragma unroll
             for (int k = 0; k < 16; k++) d[k] = y2q[k] * (int)S.y2.q[k > 0];
             iwht16(d);
@@ -896,13 +898,13 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
         } else if (l < 16) {
 #pragma unroll
             for (int n = 1; n < 16; n++) {
-                const int j = d_ZIGZAG[n];
+                const int j = kZZ(n);
                 lv[n] = quantz(c[j], S.y1.iq[1], S.y1.bias[1]);
                 nzb |= lv[n] != 0;
             }
             dq[0] = 0;
 #pragma unroll
-            for (int n = 1; n < 16; n++) dq[d_ZIGZAG[n]] = lv[n] * (int)S.y1.q[1];
+            for (int n = 1; n < 16; n++) dq[kZZ(n)] = lv[n] * (int)S.y1.q[1];
         }
         wsync();
         if (l < 16) {
@@ -931,15 +933,15 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
             const int bm = W->modes[i];
             i4_values(C, x0, y0);
-            if (l < 16) W->pred[0][l] = (uint8_t)i4_pred_px(W, bm, l);
+            if (l < 16) W->pred[0][l] = (uint8_t)i4_pred_px(W, C.T, bm, l);
             wsync();
             if (l == 0) {
                 int c[16], pr[16], lv[16];
-                const uint8_t* sp = C.srcY + (size_t)(sby * 4) * C.ys + sbx * 4;
+                const uint8_t* sp = C.sY + (sby * 4) * 16 + sbx * 4;
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     pr[k] = W->pred[0][k];
-                    c[k] = (int)sp[(size_t)(k >> 2) * C.ys + (k & 3)] - pr[k];
+                    c[k] = (int)sp[(k >> 2) * 16 + (k & 3)] - pr[k];
                 }
                 fdct16(c);
                 if (C.a->dbg && C.a->pass == 2) {
@@ -963,13 +965,13 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                 } else {
 #pragma unroll
                     for (int n = 0; n < 16; n++) {
-                        const int j = d_ZIGZAG[n];
+                        const int j = kZZ(n);
                         lv[n] = quantz(c[j], S.y1.iq[j > 0], S.y1.bias[j > 0]);
                         nz |= lv[n] != 0;
                     }
 #pragma unroll
                     for (int n = 0; n < 16; n++) {
-                        const int j = d_ZIGZAG[n];
+                        const int j = kZZ(n);
                         c[j] = lv[n] * (int)S.y1.q[j > 0];
                     }
                 }
@@ -1009,7 +1011,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
     const int b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
     if (l < 8) {
         const uint8_t* w = pl ? W->cv : W->cu;
-        const uint8_t* sp = (pl ? C.srcV : C.srcU) + (size_t)(by * 4) * C.cs + bx * 4;
+        const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
         int dcv = 128;
         {
             uint32_t s = 0;
@@ -1032,7 +1034,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
                 const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
                 const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - w[0])));
                 pr[i * 4 + j] = p;
-                c[i * 4 + j] = (int)sp[(size_t)i * C.cs + j] - p;
+                c[i * 4 + j] = (int)sp[i * 8 + j] - p;
             }
         fdct16(c);
         W->dc[b] = c[0];
@@ -1072,7 +1074,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
         int lv[16];
 #pragma unroll
         for (int n = 0; n < 16; n++) {
-            const int j = d_ZIGZAG[n];
+            const int j = kZZ(n);
             lv[n] = quantz(c[j], S.uv.iq[j > 0], S.uv.bias[j > 0]);
             nzb |= lv[n] != 0;
         }
@@ -1080,7 +1082,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
 #pragma unroll
         for (int n = 0; n < 16; n++) {
             W->lev[17 + b][n] = (int16_t)lv[n];
-            c[d_ZIGZAG[n]] = lv[n] * (int)S.uv.q[d_ZIGZAG[n] > 0];
+            c[kZZ(n)] = lv[n] * (int)S.uv.q[kZZ(n) > 0];
         }
         idct16(c);
         uint8_t* w = pl ? W->cv : W->cu;
@@ -1150,6 +1152,21 @@ __device__ void setup_ctx(Ctx& C, const EncArgs* a, const ZwFrameParams* P, cons
     C.srcY = a->Y + (size_t)f * a->ysz + (size_t)mby * 16 * C.ys + mbx * 16;
     C.srcU = a->U + (size_t)f * a->csz + (size_t)mby * 8 * C.cs + mbx * 8;
     C.srcV = a->V + (size_t)f * a->csz + (size_t)mby * 8 * C.cs + mbx * 8;
+    // stage the source MB in LDS: 64 lanes x 4 B luma, 32 lanes x 4 B chroma
+    {
+        const int l = C.lane;
+        uint32_t* sy = (uint32_t*)W->sy;
+        sy[l] = *(const uint32_t*)(C.srcY + (size_t)(l >> 2) * C.ys + (l & 3) * 4);
+        if (l < 32) {
+            const int pl = l >> 4, k = l & 15;
+            const uint8_t* sp = pl ? C.srcV : C.srcU;
+            ((uint32_t*)(pl ? W->sv : W->su))[k] = *(const uint32_t*)(sp + (size_t)(k >> 1) * C.cs + (k & 1) * 4);
+        }
+        C.sY = W->sy;
+        C.sU = W->su;
+        C.sV = W->sv;
+    }
+    wsync();
     int seg = 0;
     if (P->seg_enabled) seg = P->seg_map_lut[a->alpha[(size_t)f * a->mbw * a->mbh + (size_t)mby * a->mbw + mbx]];
     C.seg = seg;
@@ -1228,6 +1245,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         (&T->init[0][0][0])[i] = a.lcost ? (&a.lcost[f].init[0][0][0])[i] : 0;
     }
     for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&T->probs[0][0][0][0])[i] = (&P->probs[0][0][0][0])[i];
+    load_static_tables(T, threadIdx.x, WG);
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
         top_u[i] = 127;
@@ -1400,6 +1418,7 @@ extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __re
         (&T.init[0][0][0])[i] = (&lcost->init[0][0][0])[i];
     }
     for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += 256) (&T.probs[0][0][0][0])[i] = probs[i];
+    load_static_tables(&T, threadIdx.x, 256);
     __syncthreads();
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= a.n) return;
@@ -1414,12 +1433,12 @@ extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __re
     } else {
 #pragma unroll
         for (int n = 0; n < 16; n++) {
-            const int j = d_ZIGZAG[n];
+            const int j = kZZ(n);
             lv[n] = n < a.first ? 0 : quantz(c[j], a.m.iq[j > 0], a.m.bias[j > 0]);
         }
 #pragma unroll
         for (int n = 0; n < 16; n++) {
-            const int j = d_ZIGZAG[n];
+            const int j = kZZ(n);
             c[j] = n < a.first ? 0 : lv[n] * (int)a.m.q[j > 0];
         }
     }
