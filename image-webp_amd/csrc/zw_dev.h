@@ -56,12 +56,14 @@ DI int kWY(int j)
 DI int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 DI int iabs(int v) { return v < 0 ? -v : v; }
 
-// Intra-wave LDS hand-off: lanes of one wave exchange data through LDS; a
-// workgroup-scope fence orders the LDS traffic and stops the compiler from
-// moving accesses across it.
+// Intra-wave LDS hand-off: lanes of one wave exchange data through LDS.  A
+// wave's DS instructions execute in issue order, so a wavefront-scope fence
+// (compiler ordering only, no s_waitcnt on outstanding global stores) is all
+// the hand-off needs.  Cross-wave hand-offs use release/acquire at workgroup
+// scope (publish / wait_row).
 DI void wsync()
 {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -69,14 +71,6 @@ DI int wave_sum(int v)
 {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-DI int red16(int v)  // sum within aligned 16-lane groups
-{
-    v += __shfl_xor(v, 8);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 1);
     return v;
 }
 DI int red8(int v)
@@ -272,18 +266,27 @@ struct LdsTables {
     uint8_t i4idx[10][16];    // d_I4_IDX
     uint8_t zz[16];           // ZIGZAG
     uint8_t bands[17];        // VP8_ENC_BANDS
+    uint8_t izz[16];          // inverse zigzag: natural index -> position
     uint8_t pad[15];
+    uint16_t beob[4][8][3];   // bitcost(0, probs[..][0]) of the current probabilities
+    uint16_t binit[4][8][3];  // bitcost(1, probs[..][0])
 };
 
 // Static (frame-independent) part of LdsTables; all threads of the block call it.
-DI void load_static_tables(LdsTables* T, int tid, int nt)
+DI void load_static_tables(LdsTables* T, int tid, int nt, const uint8_t* probs /* [4][8][3][11] */)
 {
+    for (int i = tid; i < 96; i += nt) {
+        const int p0 = probs[i * 11];
+        (&T->beob[0][0][0])[i] = d_VP8_ENTROPY_COST[p0];
+        (&T->binit[0][0][0])[i] = d_VP8_ENTROPY_COST[255 - p0];
+    }
     for (int i = tid; i < 2048; i += nt) T->lfc[i] = d_VP8_LEVEL_FIXED_COSTS[i];
     for (int i = tid; i < 256; i += nt) T->ent[i] = d_VP8_ENTROPY_COST[i];
     for (int i = tid; i < 1000; i += nt) (&T->fci4[0][0][0])[i] = (&d_VP8_FIXED_COSTS_I4[0][0][0])[i];
     for (int i = tid; i < 160; i += nt) (&T->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
     for (int i = tid; i < 16; i += nt) T->zz[i] = d_ZIGZAG[i];
     for (int i = tid; i < 17; i += nt) T->bands[i] = d_VP8_ENC_BANDS[i];
+    for (int i = tid; i < 16; i += nt) T->izz[d_ZIGZAG[i]] = (uint8_t)i;
 }
 
 DI uint32_t bitcost(const LdsTables* T, int bit, int p) { return bit ? T->ent[255 - p] : T->ent[p]; }
@@ -317,18 +320,48 @@ DI uint32_t rcost(const int* c, int ctx0, int ctype, const LdsTables* T)
 // ---------------------------------------------------------------------------
 // 16-lane group forms: lane k = lane & 15 holds element k of one 4x4 block
 // (row k >> 2, column k & 3); four blocks per wave.  Same arithmetic as the
-// serial forms above, exchanged through ds_bpermute within the group.
+// serial forms above.  Row exchanges use DPP quad_perm, column exchanges DPP
+// row_ror (lane i reads lane (i - n) mod 16 of its row), sums the DPP
+// butterfly xor1 / xor2 / half_mirror / mirror: no LDS round trips.
 // ---------------------------------------------------------------------------
+#define DPP(v, ctrl) __builtin_amdgcn_mov_dpp((v), (ctrl), 0xf, 0xf, false)
+DI int qb0(int v) { return DPP(v, 0x00); }
+DI int qb1(int v) { return DPP(v, 0x55); }
+DI int qb2(int v) { return DPP(v, 0xAA); }
+DI int qb3(int v) { return DPP(v, 0xFF); }
+DI int ror4(int v) { return DPP(v, 0x124); }
+DI int ror8(int v) { return DPP(v, 0x128); }
+DI int ror12(int v) { return DPP(v, 0x12C); }
+DI int shr1(int v) { return __builtin_amdgcn_update_dpp(0, (v), 0x111, 0xf, 0xf, false); }
+DI int red16(int v)  // sum within aligned 16-lane groups, result in every lane
+{
+    v += DPP(v, 0xB1);   // quad xor 1
+    v += DPP(v, 0x4E);   // quad xor 2
+    v += DPP(v, 0x141);  // row half mirror (lane i <-> 7-i)
+    v += DPP(v, 0x140);  // row mirror (lane i <-> 15-i)
+    return v;
+}
 DI int gget(int v, int k) { return __shfl(v, k, 16); }
+
+// column values t_0..t_3 (rows 0..3 of this lane's column) from the lane's row i
+DI void gcol(int t, int i, int& t0, int& t1, int& t2, int& t3)
+{
+    const int m1 = ror4(t), p2 = ror8(t), p1 = ror12(t);  // rows i-1, i+2, i+1
+    t0 = i == 0 ? t : (i == 1 ? m1 : (i == 2 ? p2 : p1));
+    t1 = i == 0 ? p1 : (i == 1 ? t : (i == 2 ? m1 : p2));
+    t2 = i == 0 ? p2 : (i == 1 ? p1 : (i == 2 ? t : m1));
+    t3 = i == 0 ? m1 : (i == 1 ? p2 : (i == 2 ? p1 : t));
+}
 
 DI int fdct_g(int d, int k)
 {
     const int i = k >> 2, j = k & 3;
-    const int d0 = gget(d, i * 4), d1 = gget(d, i * 4 + 1), d2 = gget(d, i * 4 + 2), d3 = gget(d, i * 4 + 3);
+    const int d0 = qb0(d), d1 = qb1(d), d2 = qb2(d), d3 = qb3(d);
     const int a = (d0 + d3) * 8, bb = (d1 + d2) * 8, c = (d1 - d2) * 8, dd = (d0 - d3) * 8;
     const int t = j == 0 ? a + bb : (j == 2 ? a - bb : (j == 1 ? (c * 2217 + dd * 5352 + 14500) >> 12
                                                                 : (dd * 2217 - c * 5352 + 7500) >> 12));
-    const int t0 = gget(t, j), t1 = gget(t, 4 + j), t2 = gget(t, 8 + j), t3 = gget(t, 12 + j);
+    int t0, t1, t2, t3;
+    gcol(t, i, t0, t1, t2, t3);
     const int A = t0 + t3, B = t1 + t2, Cc = t1 - t2, D = t0 - t3;
     return i == 0 ? (A + B + 7) >> 4
                   : (i == 2 ? (A - B + 7) >> 4
@@ -339,12 +372,13 @@ DI int fdct_g(int d, int k)
 DI int idct_g(int x, int k)
 {
     const int i = k >> 2, j = k & 3;
-    const int x0 = gget(x, j), x1 = gget(x, 4 + j), x2 = gget(x, 8 + j), x3 = gget(x, 12 + j);
+    int x0, x1, x2, x3;
+    gcol(x, i, x0, x1, x2, x3);
     int a1 = x0 + x2, b1 = x0 - x2;
     int c1 = ((x1 * 35468) >> 16) - (x3 + ((x3 * 20091) >> 16));
     int d1 = (x1 + ((x1 * 20091) >> 16)) + ((x3 * 35468) >> 16);
     const int t = i == 0 ? a1 + d1 : (i == 1 ? b1 + c1 : (i == 2 ? b1 - c1 : a1 - d1));
-    const int y0 = gget(t, i * 4), y1 = gget(t, i * 4 + 1), y2 = gget(t, i * 4 + 2), y3 = gget(t, i * 4 + 3);
+    const int y0 = qb0(t), y1 = qb1(t), y2 = qb2(t), y3 = qb3(t);
     a1 = y0 + y2;
     b1 = y0 - y2;
     c1 = ((y1 * 35468) >> 16) - (y3 + ((y3 * 20091) >> 16));
@@ -359,26 +393,32 @@ DI unsigned gmask(bool pred)
     return (unsigned)(b >> (__lane_id() & 48)) & 0xffffu;
 }
 
+DI int band_of(int n)  // VP8_ENC_BANDS without a table
+{
+    return n < 4 ? n : (n == 4 ? 6 : (n == 5 ? 4 : (n == 6 ? 5 : (n == 15 ? 7 : (n == 16 ? 0 : 6)))));
+}
+
 // rcost<FIRST> with lane k holding c[k] (position n = k, quirk A1).  Result is
-// uniform across the group.
+// uniform across the group.  T->beob / T->binit are bitcost(0/1, p[0]) of the
+// current probabilities.
 template <int FIRST>
 DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
 {
     const unsigned m = gmask(v != 0);
     const int last = m ? 31 - __clz((int)m) : -1;
     const int av = iabs(v);
-    const int pav = gget(av, (k + 15) & 15);
+    const int pav = shr1(av);
     const int ctx = k == FIRST ? ctx0 : (pav < 2 ? pav : 2);
     int term = 0;
     if (k >= FIRST && k <= last)
-        term = T->lfc[av < 2047 ? av : 2047] + T->lc[ctype][T->bands[k]][ctx][av < 67 ? av : 67];
-    uint32_t sum = (uint32_t)red16(term);
-    const int p0 = T->probs[ctype][T->bands[FIRST]][ctx0][0];
+        term = T->lfc[av < 2047 ? av : 2047] + T->lc[ctype][band_of(k)][ctx][av < 67 ? av : 67];
     const int lastv = gget(av, last < 0 ? 0 : last);
-    if (last < 0) return bitcost(T, 0, p0);
-    sum += ctx0 == 0 ? bitcost(T, 1, p0) : 0;
-    if (last < 15) sum += bitcost(T, 0, T->probs[ctype][T->bands[last + 1]][lastv == 1 ? 1 : 2][0]);
-    return sum;
+    const int bf = band_of(FIRST);
+    uint32_t extra;
+    if (last < 0) extra = T->beob[ctype][bf][ctx0];
+    else extra = (ctx0 == 0 ? T->binit[ctype][bf][ctx0] : 0) +
+                 (last < 15 ? T->beob[ctype][band_of(last + 1)][lastv == 1 ? 1 : 2] : 0);
+    return (uint32_t)red16(term) + extra;
 }
 
 // trellis_quantize_block (cost.rs:788-1006).  coeffs (natural order) become the

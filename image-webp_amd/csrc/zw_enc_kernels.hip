@@ -414,6 +414,9 @@ struct WaveLds {
     uint8_t modes[16];
     int16_t lev[25][16];
     int misc[16];
+#ifdef ZW_PHASE_PROF
+    unsigned long long ph[16];
+#endif
 };
 
 struct SharedHdr {
@@ -583,6 +586,33 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     best_score = bfin < 0 ? 0ull : (unsigned long long)bfin;
 }
 
+#ifdef ZW_PHASE_PROF
+// Per-phase cycle counters (profiling builds only): [pass-1][phase].
+__device__ unsigned long long zw_phase_cycles_dev[2][16];
+#define PH_START() long long ph_t_ = clock64()
+#define PH_MARK(k) PH_MARK_L(k, lane, PASS)
+// accumulate in the wave's LDS slot; flushed once per kernel (ph_flush)
+#define PH_MARK_L(k, ln, ps)                                                        \
+    do {                                                                            \
+        const long long n_ = clock64();                                             \
+        if ((ln) == 0) C.W->ph[k] += (unsigned long long)(n_ - ph_t_);               \
+        ph_t_ = n_;                                                                 \
+    } while (0)
+extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_phase_cycles_dev), sizeof(zw_phase_cycles_dev)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long z[2][16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(zw_phase_cycles_dev), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define PH_START() (void)0
+#define PH_MARK(k) (void)0
+#define PH_MARK_L(k, ln, ps) (void)0
+#endif
+
 // Fill the I4 value vector V (and DC) for sub-block (x0, y0) of W->ws.
 __device__ void i4_values(const Ctx& C, int x0, int y0)
 {
@@ -635,7 +665,9 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         const int lctx = sbx == 0 ? 0 : W->modes[i - 1];
         const int nzt = sby == 0 ? 0 : top_nz[sbx];
         const int nzl = sbx == 0 ? 0 : left_nz[sby];
+        PH_START();
         i4_values(C, x0, y0);
+        PH_MARK_L(10, l, 0);
         // predictions + SSE: lane = g*16 + p, modes g, g+4, g+8
         {
             const int g = l >> 4, p = l & 15;
@@ -664,45 +696,41 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
             W->cand[rank] = l;
         }
         wsync();
-        if (l < K) {
-            const int mm = W->cand[l];
-            int src[16], r[16], q[16];
-            const uint8_t* sp = C.sY + (sby * 4) * 16 + sbx * 4;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                src[k] = sp[(k >> 2) * 16 + (k & 3)];
-                r[k] = src[k] - W->pred[mm][k];
+        PH_MARK_L(11, l, 0);
+        // candidate evaluation: 16 lanes per candidate (lane k = coefficient /
+        // pixel k), four candidates per round
+        {
+            const int g = l >> 4, k = l & 15;
+            const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
+            for (int base = 0; base < K; base += 4) {
+                const int c = base + g;
+                const bool act = c < K;
+                const int mm = act ? W->cand[c] : 0;
+                const int pk = W->pred[mm][k];
+                const int r = fdct_g(svk - pk, k);
+                const int qv = quantz(r, S.y1.iq[k > 0], S.y1.bias[k > 0]);
+                const unsigned nzm = gmask(qv != 0);
+                const uint32_t cc = rcost_g<0>(qv, k, nzt + nzl, 3, C.T);
+                const int dq = idct_g(qv * (int)S.y1.q[k > 0], k);
+                const int d = svk - clamp255(pk + dq);
+                const uint32_t sse = (uint32_t)red16(d * d);
+                if (act) {
+                    int* R = W->cres[c];
+                    R[5 + k] = dq;
+                    if (k == 0) {
+                        const uint32_t rate = (uint32_t)C.T->fci4[tctx][lctx][mm] + cc;
+                        const unsigned long long sc = rdscore(sse, rate, S.l_i4);
+                        R[0] = (int)(sc & 0xffffffff);
+                        R[1] = (int)(sc >> 32);
+                        R[2] = (int)sse;
+                        R[3] = (int)rate;
+                        R[4] = nzm != 0;
+                    }
+                }
             }
-            fdct16(r);
-            int hnz = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                q[k] = quantz(r[k], S.y1.iq[k > 0], S.y1.bias[k > 0]);
-                hnz |= q[k] != 0;
-            }
-            const uint32_t cc = rcost<0>(q, nzt + nzl, 3, C.T);
-            int dq[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) dq[k] = q[k] * (int)S.y1.q[k > 0];
-            idct16(dq);
-            uint32_t sse = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int d = src[k] - clamp255(W->pred[mm][k] + dq[k]);
-                sse += (uint32_t)(d * d);
-            }
-            const uint32_t rate = (uint32_t)C.T->fci4[tctx][lctx][mm] + cc;
-            const unsigned long long sc = rdscore(sse, rate, S.l_i4);
-            int* R = W->cres[l];
-            R[0] = (int)(sc & 0xffffffff);
-            R[1] = (int)(sc >> 32);
-            R[2] = (int)sse;
-            R[3] = (int)rate;
-            R[4] = hnz;
-#pragma unroll
-            for (int k = 0; k < 16; k++) R[5 + k] = dq[k];
         }
         wsync();
+        PH_MARK_L(12, l, 0);
         // best candidate in rank order (strict <)
         unsigned long long bs = ~0ull;
         int bk = 0;
@@ -727,6 +755,7 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
             W->ws[(y0 + (p >> 2)) * ZW_BPS + x0 + (p & 3)] = (uint8_t)clamp255(W->pred[bmode][p] + W->cres[bk][5 + p]);
         }
         wsync();
+        PH_MARK_L(13, l, 0);
     }
     return true;
 }
@@ -828,7 +857,8 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
         const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
         int c[16], pr[16];
         const int b = l & 15, bx = b & 3, by = b >> 2;
-        if (l < 16) {
+        // lanes 16..47 recompute their block's coefficients for the ctx-parallel trellis
+        if (l < (trel ? 48 : 16)) {
             const int P0 = ws[0];
 #pragma unroll
             for (int i = 0; i < 4; i++)
@@ -841,7 +871,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                     c[i * 4 + j] = (int)C.sY[y * 16 + x] - p;
                 }
             fdct16(c);
-            W->dc[b] = c[0];
+            if (l < 16) W->dc[b] = c[0];
         }
         wsync();
         if (l == 0) {
@@ -864,10 +894,6 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
 #pragma unroll
             for (int k = 0; k < 16; k++) W->y2d[k] = d[k];
             W->misc[0] = nz;
-            for (int k = 0; k < 4; k++) {
-                W->nzt[k] = C.top_c[C.mbx * 12 + 1 + k];
-                W->nzl[k] = W->left_c[1 + k];
-            }
         }
         wsync();
         anynz = W->misc[0];
@@ -883,18 +909,39 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             anynz |= __any(snz) ? 1 : 0;
         }
         if (trel) {
-            for (int t = 0; t < 7; t++) {
-                if (l < 16 && bx + by == t) {
-                    int ctx0 = W->nzl[by] + W->nzt[bx];
-                    ctx0 = ctx0 > 2 ? 2 : ctx0;
+            // Trellis for every block under all three contexts at once (lane =
+            // ctx0*16 + block), then resolve the raster-order nz context chain
+            // (left / top neighbours) on the scalar unit and pick each block's result.
+            int tnz = 0;
+            if (l < 48) {
 #pragma unroll
-                    for (int k = 0; k < 16; k++) dq[k] = c[k];
-                    nzb = trellis<1>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, ctx0);
-                    W->nzt[bx] = nzb;
-                    W->nzl[by] = nzb;
-                }
-                wsync();
+                for (int k = 0; k < 16; k++) dq[k] = c[k];
+                tnz = trellis<1>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, l >> 4);
             }
+            const unsigned long long nzm = __ballot(l < 48 && tnz);
+            int nt[4], nl[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                nt[q] = __builtin_amdgcn_readfirstlane(C.top_c[C.mbx * 12 + 1 + q]);
+                nl[q] = __builtin_amdgcn_readfirstlane(W->left_c[1 + q]);
+            }
+            unsigned code = 0, nzbits = 0;
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) {
+                const int cx = min(nl[bb >> 2] + nt[bb & 3], 2);
+                const int z = (int)((nzm >> (cx * 16 + bb)) & 1ull);
+                nt[bb & 3] = z;
+                nl[bb >> 2] = z;
+                code |= (unsigned)cx << (2 * bb);
+                nzbits |= (unsigned)z << bb;
+            }
+            const int srcl = (int)((code >> (2 * b)) & 3u) * 16 + b;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                lv[k] = __shfl(lv[k], srcl);
+                dq[k] = __shfl(dq[k], srcl);
+            }
+            nzb = (nzbits >> b) & 1u;
         } else if (l < 16) {
 #pragma unroll
             for (int n = 1; n < 16; n++) {
@@ -933,54 +980,51 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
             const int bm = W->modes[i];
             i4_values(C, x0, y0);
-            if (l < 16) W->pred[0][l] = (uint8_t)i4_pred_px(W, C.T, bm, l);
-            wsync();
-            if (l == 0) {
-                int c[16], pr[16], lv[16];
-                const uint8_t* sp = C.sY + (sby * 4) * 16 + sbx * 4;
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    pr[k] = W->pred[0][k];
-                    c[k] = (int)sp[(k >> 2) * 16 + (k & 3)] - pr[k];
-                }
-                fdct16(c);
-                if (C.a->dbg && C.a->pass == 2) {
-                    int* d = C.a->dbg + (((size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx) * 16 + i) * 34;
-                    for (int k = 0; k < 16; k++) {
-                        d[k] = c[k];
-                        d[16 + k] = pr[k];
-                    }
-                    const int c0 = left_nz[sby] + top_nz[sbx];
-                    d[32] = c0 > 2 ? 2 : c0;
+            // 16-lane group form: every group computes the same block; group 0 stores
+            const int k = l & 15;
+            const int pk = i4_pred_px(W, C.T, bm, k);
+            const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
+            const int ck = fdct_g(svk - pk, k);
+            const int ctx0 = min(left_nz[sby] + top_nz[sbx], 2);
+            if (C.a->dbg && C.a->pass == 2 && l < 16) {
+                int* d = C.a->dbg + (((size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx) * 16 + i) * 34;
+                d[k] = ck;
+                d[16 + k] = pk;
+                if (k == 0) {
+                    d[32] = ctx0;
                     d[33] = bm;
                 }
-                int snz = 0;
+            }
+            const int qs = quantz(ck, S.y1.iq[k > 0], S.y1.bias[k > 0]);
+            const int snz = gmask(qs != 0) != 0;
+            int dqk, nzq;
+            if (trel) {
+                if (l < 16) W->cres[0][5 + k] = ck;
+                wsync();
+                if (l == 0) {
+                    int c[16], lv[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) snz |= quantz(c[k], S.y1.iq[k > 0], S.y1.bias[k > 0]) != 0;
-                int nz = 0;
-                if (trel) {
-                    int ctx0 = left_nz[sby] + top_nz[sbx];
-                    ctx0 = ctx0 > 2 ? 2 : ctx0;
-                    nz = trellis<0>(c, lv, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0);
-                } else {
+                    for (int kk = 0; kk < 16; kk++) c[kk] = W->cres[0][5 + kk];
+                    const int tnz = trellis<0>(c, lv, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0);
 #pragma unroll
-                    for (int n = 0; n < 16; n++) {
-                        const int j = kZZ(n);
-                        lv[n] = quantz(c[j], S.y1.iq[j > 0], S.y1.bias[j > 0]);
-                        nz |= lv[n] != 0;
-                    }
+                    for (int n = 0; n < 16; n++) W->lev[i][n] = (int16_t)lv[n];
 #pragma unroll
-                    for (int n = 0; n < 16; n++) {
-                        const int j = kZZ(n);
-                        c[j] = lv[n] * (int)S.y1.q[j > 0];
-                    }
+                    for (int kk = 0; kk < 16; kk++) W->cres[0][5 + kk] = c[kk];
+                    W->misc[1] = tnz;
                 }
-#pragma unroll
-                for (int n = 0; n < 16; n++) W->lev[i][n] = (int16_t)lv[n];
-                idct16(c);
-#pragma unroll
-                for (int k = 0; k < 16; k++) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pr[k] + c[k]);
-                W->misc[1] = nz;
+                wsync();
+                dqk = W->cres[0][5 + k];
+                nzq = W->misc[1];
+            } else {
+                if (l < 16) W->lev[i][C.T->izz[k]] = (int16_t)qs;
+                nzq = snz;
+                dqk = qs * (int)S.y1.q[k > 0];
+            }
+            const int rk = idct_g(dqk, k);
+            if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pk + rk);
+            wsync();
+            if (l == 0) {
+                W->misc[1] = nzq;
                 W->misc[2] = snz;
             }
             wsync();
@@ -1186,29 +1230,6 @@ __device__ void publish(int* progress, int wave, int val)
     __builtin_amdgcn_wave_barrier();
 }
 
-#ifdef ZW_PHASE_PROF
-// Per-phase cycle counters (profiling builds only): [pass-1][phase].
-__device__ unsigned long long zw_phase_cycles_dev[2][16];
-#define PH_START() long long ph_t_ = clock64()
-#define PH_MARK(k)                                                                  \
-    do {                                                                            \
-        const long long n_ = clock64();                                             \
-        if (lane == 0) atomicAdd(&zw_phase_cycles_dev[PASS - 1][k], (unsigned long long)(n_ - ph_t_)); \
-        ph_t_ = n_;                                                                 \
-    } while (0)
-extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_phase_cycles_dev), sizeof(zw_phase_cycles_dev)) != hipSuccess) return -1;
-    if (reset) {
-        static unsigned long long z[2][16];
-        if (hipMemcpyToSymbol(HIP_SYMBOL(zw_phase_cycles_dev), z, sizeof z) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#else
-#define PH_START() (void)0
-#define PH_MARK(k) (void)0
-#endif
 
 template <int PASS>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
@@ -1245,7 +1266,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         (&T->init[0][0][0])[i] = a.lcost ? (&a.lcost[f].init[0][0][0])[i] : 0;
     }
     for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&T->probs[0][0][0][0])[i] = (&P->probs[0][0][0][0])[i];
-    load_static_tables(T, threadIdx.x, WG);
+    load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
         top_u[i] = 127;
@@ -1269,6 +1290,15 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.top_derr = top_derr;
     const bool trel = PASS == 2 && P->do_trellis;
     const size_t nmb = (size_t)mbw * mbh;
+#ifdef ZW_PHASE_PROF
+    if (lane < 16) W->ph[lane] = 0;
+    wsync();
+    auto ph_flush = [&]() {
+        if (lane < 16) atomicAdd(&zw_phase_cycles_dev[PASS - 1][lane], W->ph[lane]);
+    };
+#else
+    auto ph_flush = []() {};
+#endif
 
     if (PASS == 1 && wv == 0) {
         // ---- pass-1 chroma raster chain ----
@@ -1296,6 +1326,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             }
         }
         for (int i = lane; i < mbw * 4; i += 64) a.derr[(size_t)f * mbw * 4 + i] = top_derr[i];
+        ph_flush();
         return;
     }
 
@@ -1387,6 +1418,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             PH_MARK(6);
         }
     }
+    ph_flush();
 }
 
 extern "C" __global__ __launch_bounds__(WG) void k_encode_pass1(EncArgs a) { encode_body<1>(a); }
@@ -1418,7 +1450,7 @@ extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __re
         (&T.init[0][0][0])[i] = (&lcost->init[0][0][0])[i];
     }
     for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += 256) (&T.probs[0][0][0][0])[i] = probs[i];
-    load_static_tables(&T, threadIdx.x, 256);
+    load_static_tables(&T, threadIdx.x, 256, probs);
     __syncthreads();
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= a.n) return;

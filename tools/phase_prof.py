@@ -16,7 +16,8 @@ import zwebp  # noqa: E402
 from zwebp.synth import synth_rgba  # noqa: E402
 
 NAMES = {0: "wait(row above)", 1: "border+pick_i16", 2: "pick_i4", 3: "pick_uv", 4: "final_luma",
-         5: "final_chroma", 6: "store/levels/publish", 8: "p1 chroma pick_uv", 9: "p1 chroma final"}
+         5: "final_chroma", 6: "store/levels/publish", 8: "p1 chroma pick_uv", 9: "p1 chroma final",
+         10: "  i4: values", 11: "  i4: preds+sse+rank", 12: "  i4: candidates", 13: "  i4: select+recon"}
 
 
 def main():
@@ -41,7 +42,7 @@ def main():
     nmb = p.mbw * p.mbh * F
     print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt]}")
     for ps in (0, 1):
-        tot = sum(buf[ps * 16 + k] for k in range(16)) or 1
+        tot = sum(buf[ps * 16 + k] for k in range(10)) or 1
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
         for k in range(16):
             v = buf[ps * 16 + k]
