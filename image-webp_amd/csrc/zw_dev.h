@@ -53,6 +53,15 @@ DI int kWY(int j)
     return t[j];
 }
 
+// Small position tables packed 4 bits per entry into 64-bit immediates: a
+// lane-varying index becomes one 64-bit shift (no memory access, no branches).
+DI int band_of(int n)  // VP8_ENC_BANDS[n], n in 0..16
+{
+    return n >= 16 ? 0 : (int)((0x7666666665463210ull >> (4 * n)) & 15);
+}
+DI int zz_of(int n) { return (int)((0xfeb7adc963258410ull >> (4 * n)) & 15); }   // ZIGZAG
+DI int izz_of(int k) { return (int)((0xfea9db83c7426510ull >> (4 * k)) & 15); }  // inverse ZIGZAG
+
 DI int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 DI int iabs(int v) { return v < 0 ? -v : v; }
 
@@ -301,7 +310,7 @@ DI uint32_t rcost(const int* c, int ctx0, int ctype, const LdsTables* T)
 #pragma unroll
     for (int n = 0; n < 16; n++)
         if (c[n] != 0) last = n;
-    const int p0 = T->probs[ctype][T->bands[FIRST]][ctx0][0];
+    const int p0 = T->probs[ctype][kBand(FIRST)][ctx0][0];
     if (last < 0) return bitcost(T, 0, p0);
     uint32_t cost = ctx0 == 0 ? bitcost(T, 1, p0) : 0;
     int ctx = ctx0;
@@ -309,11 +318,11 @@ DI uint32_t rcost(const int* c, int ctx0, int ctype, const LdsTables* T)
     for (int n = FIRST; n < 16; n++) {
         if (n <= last) {
             int v = iabs(c[n]);
-            cost += T->lfc[v < 2047 ? v : 2047] + T->lc[ctype][T->bands[n]][ctx][v < 67 ? v : 67];
+            cost += T->lfc[v < 2047 ? v : 2047] + T->lc[ctype][kBand(n)][ctx][v < 67 ? v : 67];
             ctx = v < 2 ? v : 2;
         }
     }
-    if (last < 15) cost += bitcost(T, 0, T->probs[ctype][T->bands[last + 1]][ctx][0]);
+    if (last < 15) cost += bitcost(T, 0, T->probs[ctype][band_of(last + 1)][ctx][0]);
     return cost;
 }
 
@@ -343,14 +352,25 @@ DI int red16(int v)  // sum within aligned 16-lane groups, result in every lane
 }
 DI int gget(int v, int k) { return __shfl(v, k, 16); }
 
+// Arithmetic select: both operands already computed; never becomes a branch.
+DI int csel(bool c, int a, int b) { return b + ((a - b) & -(int)c); }
+
+// Branch-free 4-way select (lane-varying i in 0..3): all operands are already
+// computed, so the compiler cannot turn the choice into divergent branches.
+DI int sel4(int i, int a, int b, int c, int d)
+{
+    const int m0 = -(int)(i == 0), m1 = -(int)(i == 1), m2 = -(int)(i == 2), m3 = -(int)(i == 3);
+    return (a & m0) | (b & m1) | (c & m2) | (d & m3);
+}
+
 // column values t_0..t_3 (rows 0..3 of this lane's column) from the lane's row i
 DI void gcol(int t, int i, int& t0, int& t1, int& t2, int& t3)
 {
     const int m1 = ror4(t), p2 = ror8(t), p1 = ror12(t);  // rows i-1, i+2, i+1
-    t0 = i == 0 ? t : (i == 1 ? m1 : (i == 2 ? p2 : p1));
-    t1 = i == 0 ? p1 : (i == 1 ? t : (i == 2 ? m1 : p2));
-    t2 = i == 0 ? p2 : (i == 1 ? p1 : (i == 2 ? t : m1));
-    t3 = i == 0 ? m1 : (i == 1 ? p2 : (i == 2 ? p1 : t));
+    t0 = sel4(i, t, m1, p2, p1);
+    t1 = sel4(i, p1, t, m1, p2);
+    t2 = sel4(i, p2, p1, t, m1);
+    t3 = sel4(i, m1, p2, p1, t);
 }
 
 DI int fdct_g(int d, int k)
@@ -358,15 +378,12 @@ DI int fdct_g(int d, int k)
     const int i = k >> 2, j = k & 3;
     const int d0 = qb0(d), d1 = qb1(d), d2 = qb2(d), d3 = qb3(d);
     const int a = (d0 + d3) * 8, bb = (d1 + d2) * 8, c = (d1 - d2) * 8, dd = (d0 - d3) * 8;
-    const int t = j == 0 ? a + bb : (j == 2 ? a - bb : (j == 1 ? (c * 2217 + dd * 5352 + 14500) >> 12
-                                                                : (dd * 2217 - c * 5352 + 7500) >> 12));
+    const int t = sel4(j, a + bb, (c * 2217 + dd * 5352 + 14500) >> 12, a - bb, (dd * 2217 - c * 5352 + 7500) >> 12);
     int t0, t1, t2, t3;
     gcol(t, i, t0, t1, t2, t3);
     const int A = t0 + t3, B = t1 + t2, Cc = t1 - t2, D = t0 - t3;
-    return i == 0 ? (A + B + 7) >> 4
-                  : (i == 2 ? (A - B + 7) >> 4
-                            : (i == 1 ? ((Cc * 2217 + D * 5352 + 12000) >> 16) + (D != 0 ? 1 : 0)
-                                      : (D * 2217 - Cc * 5352 + 51000) >> 16));
+    return sel4(i, (A + B + 7) >> 4, ((Cc * 2217 + D * 5352 + 12000) >> 16) + (D != 0 ? 1 : 0), (A - B + 7) >> 4,
+                (D * 2217 - Cc * 5352 + 51000) >> 16);
 }
 
 DI int idct_g(int x, int k)
@@ -377,13 +394,13 @@ DI int idct_g(int x, int k)
     int a1 = x0 + x2, b1 = x0 - x2;
     int c1 = ((x1 * 35468) >> 16) - (x3 + ((x3 * 20091) >> 16));
     int d1 = (x1 + ((x1 * 20091) >> 16)) + ((x3 * 35468) >> 16);
-    const int t = i == 0 ? a1 + d1 : (i == 1 ? b1 + c1 : (i == 2 ? b1 - c1 : a1 - d1));
+    const int t = sel4(i, a1 + d1, b1 + c1, b1 - c1, a1 - d1);
     const int y0 = qb0(t), y1 = qb1(t), y2 = qb2(t), y3 = qb3(t);
     a1 = y0 + y2;
     b1 = y0 - y2;
     c1 = ((y1 * 35468) >> 16) - (y3 + ((y3 * 20091) >> 16));
     d1 = (y1 + ((y1 * 20091) >> 16)) + ((y3 * 35468) >> 16);
-    return j == 0 ? (a1 + d1 + 4) >> 3 : (j == 1 ? (b1 + c1 + 4) >> 3 : (j == 2 ? (b1 - c1 + 4) >> 3 : (a1 - d1 + 4) >> 3));
+    return sel4(j, (a1 + d1 + 4) >> 3, (b1 + c1 + 4) >> 3, (b1 - c1 + 4) >> 3, (a1 - d1 + 4) >> 3);
 }
 
 // 16-bit nonzero mask of the lane's group.
@@ -391,11 +408,6 @@ DI unsigned gmask(bool pred)
 {
     const unsigned long long b = __ballot(pred);
     return (unsigned)(b >> (__lane_id() & 48)) & 0xffffu;
-}
-
-DI int band_of(int n)  // VP8_ENC_BANDS without a table
-{
-    return n < 4 ? n : (n == 4 ? 6 : (n == 5 ? 4 : (n == 6 ? 5 : (n == 15 ? 7 : (n == 16 ? 0 : 6)))));
 }
 
 // rcost<FIRST> with lane k holding c[k] (position n = k, quirk A1).  Result is
@@ -408,17 +420,18 @@ DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
     const int last = m ? 31 - __clz((int)m) : -1;
     const int av = iabs(v);
     const int pav = shr1(av);
-    const int ctx = k == FIRST ? ctx0 : (pav < 2 ? pav : 2);
-    int term = 0;
-    if (k >= FIRST && k <= last)
-        term = T->lfc[av < 2047 ? av : 2047] + T->lc[ctype][band_of(k)][ctx][av < 67 ? av : 67];
-    const int lastv = gget(av, last < 0 ? 0 : last);
+    const int ctx = k == FIRST ? ctx0 : min(pav, 2);
+    // unconditional lookups with clamped indices, masked arithmetic (no branches)
+    const int tl = T->lfc[min(av, 2047)] + T->lc[ctype][band_of(k)][ctx][min(av, 67)];
+    const int term = tl & -(int)(k >= FIRST && k <= last);
+    const int lastc = max(last, 0);
+    const int lastv = gget(av, lastc);
     const int bf = band_of(FIRST);
-    uint32_t extra;
-    if (last < 0) extra = T->beob[ctype][bf][ctx0];
-    else extra = (ctx0 == 0 ? T->binit[ctype][bf][ctx0] : 0) +
-                 (last < 15 ? T->beob[ctype][band_of(last + 1)][lastv == 1 ? 1 : 2] : 0);
-    return (uint32_t)red16(term) + extra;
+    const int e_none = T->beob[ctype][bf][ctx0];
+    const int e_init = T->binit[ctype][bf][ctx0] & -(int)(ctx0 == 0);
+    const int e_tail = T->beob[ctype][band_of(min(lastc + 1, 15))][lastv == 1 ? 1 : 2] & -(int)(last < 15);
+    const int extra = last < 0 ? e_none : e_init + e_tail;
+    return (uint32_t)(red16(term) + extra);
 }
 
 // trellis_quantize_block (cost.rs:788-1006).  coeffs (natural order) become the

@@ -613,35 +613,46 @@ extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
 #define PH_MARK_L(k, ln, ps) (void)0
 #endif
 
-// Fill the I4 value vector V (and DC) for sub-block (x0, y0) of W->ws.
+// Fill the I4 value vector V for sub-block (x0, y0) of W->ws (branch-free:
+// every lane reads up to three edge pixels and forms an avg2/avg3/copy).
+//   V[0..12]  E = [L3 L2 L1 L0 P A0..A7]      V[13..23] avg3(E[k], E[k+1], E[k+2])
+//   V[24..35] avg2(E[k], E[k+1])              V[36] avg3(A6,A7,A7)  V[37] avg3(L2,L3,L3)
+//   V[38] DC = (4 + L0..L3 + A0..A3) >> 3
 __device__ void i4_values(const Ctx& C, int x0, int y0)
 {
     WaveLds* W = C.W;
     const uint8_t* ws = W->ws;
     const int l = C.lane;
-    auto E = [&](int k) -> int {  // [L3 L2 L1 L0 P A0..A7]
-        if (k < 4) return ws[(y0 + 3 - k) * ZW_BPS + x0 - 1];
-        if (k == 4) return ws[(y0 - 1) * ZW_BPS + x0 - 1];
-        return ws[(y0 - 1) * ZW_BPS + x0 + (k - 5)];
-    };
-    if (l < 13) W->V[l] = E(l);
-    else if (l < 24) { int k = l - 13; W->V[l] = (E(k) + 2 * E(k + 1) + E(k + 2) + 2) >> 2; }
-    else if (l < 36) { int k = l - 24; W->V[l] = (E(k) + E(k + 1) + 1) >> 1; }
-    else if (l == 36) W->V[36] = (E(11) + 2 * E(12) + E(12) + 2) >> 2;
-    else if (l == 37) W->V[37] = (E(1) + 2 * E(0) + E(0) + 2) >> 2;
-    else if (l == 38) {
-        int v = 4;
-        for (int k = 0; k < 4; k++) v += E(k) + E(5 + k);
-        W->V[38] = v >> 3;
-    }
+    // lane -> (ka, kb, kc) and weights; t: 0 copy, 1 avg3, 2 avg2, 3/4 special avg3
+    // (arithmetic only: lane-dependent selects must not become branches)
+    const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
+    const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
+    const int t3 = (int)(t == 3), t4 = (int)(t >= 4), t12 = (int)(t == 1 || t == 2);
+    const int ka = k + t3 * (11 - k) + t4 * (1 - k);
+    const int kb = k + t12 + t3 * (12 - k) - t4 * k;
+    const int kc = min(k + 2 * (int)(t == 1), 12);
+    const int rowL = (y0 + 3) * ZW_BPS + x0 - 1, rowT = (y0 - 1) * ZW_BPS + x0 - 5;
+    const int aa = csel(ka < 4, rowL - ka * ZW_BPS, rowT + ka);
+    const int ab = csel(kb < 4, rowL - kb * ZW_BPS, rowT + kb);
+    const int ac = csel(kc < 4, rowL - kc * ZW_BPS, rowT + kc);
+    const int ea = ws[aa], eb = ws[ab], ec = ws[ac];
+    // v = (ea + wb*eb + wc*ec + rnd) >> sh
+    const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
+    const int wc = (int)(t == 1);
+    const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
+    const int v = (ea + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh;
+    const int dsum = red16((l < 4 || (l >= 5 && l < 9)) ? ea : 0);
+    if (l < 38) W->V[l] = v;
+    if (l == 0) W->V[38] = (dsum + 4) >> 3;
     wsync();
 }
 __device__ __forceinline__ int i4_pred_px(const WaveLds* W, const LdsTables* T, int mode, int p)
 {
     const int idx = T->i4idx[mode][p];
-    if (idx == 255) return W->V[38];
-    if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
-    return W->V[idx];
+    const bool tm = idx == 254;
+    const int ia = csel(tm, 3 - (p >> 2), csel(idx == 255, 38, idx));
+    const int va = W->V[ia], vb = W->V[5 + (p & 3)], vc = W->V[4];
+    return csel(tm, clamp255(va + vb - vc), va);
 }
 
 __device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rate, uint32_t lambda)
@@ -650,110 +661,109 @@ __device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rat
 }
 
 // pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
+// Per sub-block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8),
+// ranking on the scalar unit, top-K candidates 16 lanes each (quirk A12 order).
 __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
 {
     WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
-    const int l = C.lane;
+    const LdsTables* T = C.T;
+    const int l = C.lane, g = l >> 4, k = l & 15;
     const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
+    const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
+    const int qk = (int)S.y1.q[k > 0];
     unsigned long long running = 211ull * S.l_mode;
     uint32_t total_mc = 0;
+    unsigned long long mpack = 0;  // chosen sub-modes, 4 bits each
     int top_nz[4] = {0, 0, 0, 0}, left_nz[4] = {0, 0, 0, 0};
     for (int i = 0; i < 16; i++) {
         const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
-        const int tctx = sby == 0 ? 0 : W->modes[i - 4];
-        const int lctx = sbx == 0 ? 0 : W->modes[i - 1];
+        const int tctx = sby == 0 ? 0 : (int)((mpack >> (4 * (i - 4))) & 15);
+        const int lctx = sbx == 0 ? 0 : (int)((mpack >> (4 * (i - 1))) & 15);
         const int nzt = sby == 0 ? 0 : top_nz[sbx];
         const int nzl = sbx == 0 ? 0 : left_nz[sby];
         PH_START();
         i4_values(C, x0, y0);
         PH_MARK_L(10, l, 0);
-        // predictions + SSE: lane = g*16 + p, modes g, g+4, g+8
+        const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
+        int e0, e1, e2;
         {
-            const int g = l >> 4, p = l & 15;
-            const int sv = C.sY[(sby * 4 + (p >> 2)) * 16 + sbx * 4 + (p & 3)];
-#pragma unroll
-            for (int t = 0; t < 3; t++) {
-                const int mm = g + 4 * t;
-                int e = 0;
-                if (mm < 10) {
-                    const int v = i4_pred_px(W, C.T, mm, p);
-                    W->pred[mm][p] = (uint8_t)v;
-                    e = (sv - v) * (sv - v);
-                }
-                e = red16(e);
-                if (p == 0 && mm < 10) W->msse[mm] = (uint32_t)e;
-            }
+            int v = i4_pred_px(W, T, g, k);
+            W->pred[g][k] = (uint8_t)v;
+            e0 = red16((svk - v) * (svk - v));
+            v = i4_pred_px(W, T, g + 4, k);
+            W->pred[g + 4][k] = (uint8_t)v;
+            e1 = red16((svk - v) * (svk - v));
+            v = i4_pred_px(W, T, g < 2 ? g + 8 : 0, k);
+            if (g < 2) W->pred[g + 8][k] = (uint8_t)v;
+            e2 = red16((svk - v) * (svk - v));
         }
-        wsync();
-        if (l < 10) {
-            const uint32_t me = W->msse[l];
-            int rank = 0;
-            for (int o = 0; o < 10; o++) {
-                const uint32_t oe = W->msse[o];
-                rank += (oe < me) || (oe == me && o < l);
-            }
-            W->cand[rank] = l;
+        // stable ascending rank of the 10 SSEs (ties by mode index), on SGPRs
+        uint32_t se[10];
+#pragma unroll
+        for (int m = 0; m < 10; m++) {
+            const int ev = m < 4 ? e0 : (m < 8 ? e1 : e2);
+            se[m] = (uint32_t)__builtin_amdgcn_readlane(ev, (m & 3) * 16);
+        }
+        unsigned long long cpack = 0;  // candidate c -> mode, 4 bits each
+#pragma unroll
+        for (int m = 0; m < 10; m++) {
+            int r = 0;
+#pragma unroll
+            for (int o = 0; o < 10; o++) r += (se[o] < se[m]) || (se[o] == se[m] && o < m);
+            cpack |= (unsigned long long)m << (4 * r);
         }
         wsync();
         PH_MARK_L(11, l, 0);
-        // candidate evaluation: 16 lanes per candidate (lane k = coefficient /
-        // pixel k), four candidates per round
-        {
-            const int g = l >> 4, k = l & 15;
-            const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
-            for (int base = 0; base < K; base += 4) {
-                const int c = base + g;
-                const bool act = c < K;
-                const int mm = act ? W->cand[c] : 0;
-                const int pk = W->pred[mm][k];
-                const int r = fdct_g(svk - pk, k);
-                const int qv = quantz(r, S.y1.iq[k > 0], S.y1.bias[k > 0]);
-                const unsigned nzm = gmask(qv != 0);
-                const uint32_t cc = rcost_g<0>(qv, k, nzt + nzl, 3, C.T);
-                const int dq = idct_g(qv * (int)S.y1.q[k > 0], k);
-                const int d = svk - clamp255(pk + dq);
-                const uint32_t sse = (uint32_t)red16(d * d);
-                if (act) {
-                    int* R = W->cres[c];
-                    R[5 + k] = dq;
-                    if (k == 0) {
-                        const uint32_t rate = (uint32_t)C.T->fci4[tctx][lctx][mm] + cc;
-                        const unsigned long long sc = rdscore(sse, rate, S.l_i4);
-                        R[0] = (int)(sc & 0xffffffff);
-                        R[1] = (int)(sc >> 32);
-                        R[2] = (int)sse;
-                        R[3] = (int)rate;
-                        R[4] = nzm != 0;
-                    }
+        unsigned long long bsc = ~0ull;
+        uint32_t bsse = 0, brate = 0;
+        int bmode = 0, bnz = 0, bdq = 0, bpk = 0;
+        for (int base = 0; base < K; base += 4) {
+            const int c = base + g;
+            const bool act = c < K;
+            const int mm = act ? (int)((cpack >> (4 * c)) & 15) : 0;
+            const int pk = W->pred[mm][k];
+            const int r = fdct_g(svk - pk, k);
+            const int qv = quantz(r, iqk, biask);
+            const unsigned nzm = gmask(qv != 0);
+            const uint32_t cc = rcost_g<0>(qv, k, nzt + nzl, 3, T);
+            const int dq = idct_g(qv * qk, k);
+            const int d = svk - clamp255(pk + dq);
+            const uint32_t sse = (uint32_t)red16(d * d);
+            const uint32_t rate = (uint32_t)T->fci4[tctx][lctx][mm] + cc;
+            const unsigned long long sc = rdscore(sse, rate, S.l_i4);
+            // best of this round's groups in rank order (strict <), all in VGPRs
+            const unsigned slo = (unsigned)sc, shi = (unsigned)(sc >> 32);
+            int bg = -1;
+#pragma unroll
+            for (int gg = 0; gg < 4; gg++) {
+                const unsigned long long sg =
+                    ((unsigned long long)(unsigned)__shfl((int)shi, gg * 16) << 32) | (unsigned)__shfl((int)slo, gg * 16);
+                if (base + gg < K && sg < bsc) {
+                    bsc = sg;
+                    bg = gg;
                 }
             }
-        }
-        wsync();
-        PH_MARK_L(12, l, 0);
-        // best candidate in rank order (strict <)
-        unsigned long long bs = ~0ull;
-        int bk = 0;
-        for (int k = 0; k < K; k++) {
-            const unsigned long long sc = ((unsigned long long)(unsigned)W->cres[k][1] << 32) | (unsigned)W->cres[k][0];
-            if (sc < bs) {
-                bs = sc;
-                bk = k;
+            if (bg >= 0) {
+                const int src = bg * 16;
+                bsse = (uint32_t)__shfl((int)sse, src);
+                brate = (uint32_t)__shfl((int)rate, src);
+                bnz = __shfl((int)(nzm != 0), src);
+                bmode = (int)((cpack >> (4 * (base + bg))) & 15);
+                bdq = __shfl(dq, src + k);
+                bpk = __shfl(pk, src + k);
             }
         }
-        const int bmode = W->cand[bk];
-        const int bnz = W->cres[bk][4];
+        PH_MARK_L(12, l, 0);
         top_nz[sbx] = bnz;
         left_nz[sby] = bnz;
-        total_mc += C.T->fci4[tctx][lctx][bmode];
-        running += rdscore((uint32_t)W->cres[bk][2], (uint32_t)W->cres[bk][3], S.l_mode);
+        total_mc += T->fci4[tctx][lctx][bmode];
+        running += rdscore(bsse, brate, S.l_mode);
+        mpack |= (unsigned long long)bmode << (4 * i);
         if (l == 0) W->modes[i] = (uint8_t)bmode;
         if (running >= i16_score) { wsync(); return false; }
         if (total_mc > 256u * 16u * 16u / 4u) { wsync(); return false; }
-        if (l < 16) {
-            const int p = l;
-            W->ws[(y0 + (p >> 2)) * ZW_BPS + x0 + (p & 3)] = (uint8_t)clamp255(W->pred[bmode][p] + W->cres[bk][5 + p]);
-        }
+        if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(bpk + bdq);
         wsync();
         PH_MARK_L(13, l, 0);
     }
@@ -1016,7 +1026,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                 dqk = W->cres[0][5 + k];
                 nzq = W->misc[1];
             } else {
-                if (l < 16) W->lev[i][C.T->izz[k]] = (int16_t)qs;
+                if (l < 16) W->lev[i][izz_of(k)] = (int16_t)qs;
                 nzq = snz;
                 dqk = qs * (int)S.y1.q[k > 0];
             }
