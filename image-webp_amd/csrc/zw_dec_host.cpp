@@ -453,7 +453,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     const size_t total = al256(o_v + (size_t)n * csz);
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = ctx_stream(ctx);
     HIPOK(hipMemcpyAsync(d + o_mbs, mbs.data(), mbs.size() * sizeof(ZwDecMb), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
@@ -507,7 +507,7 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipSetDevice(ctx->device));
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = ctx_stream(ctx);
     HIPOK(hipMemcpyAsync(d + o_fp, &fp, sizeof fp, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fl, mb_flags, nmb * 4, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_y, y, ysz, hipMemcpyHostToDevice, s));

@@ -485,11 +485,11 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
 extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
                                     uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
 {
-    static bool attr = false;
-    if (!attr) {
+    static const bool attr = []() {
         (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+        return true;
+    }();
+    (void)attr;
     hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs, (const ZwDecQuant*)quant,
                        Y, U, V, flags, mbw, mbh, ysz, csz);
     return hipGetLastError();

@@ -1417,6 +1417,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 write_levels(C, 0, 25, skip);
             } else {
                 write_levels(C, 0, 17, false);
+                if (lane == 0) o->skip = 0;  // pass-1 skip is decided on the host from the levels
             }
             if (lane == 0) {
                 o->luma_mode = (uint8_t)lm;
@@ -1553,12 +1554,12 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
     const size_t lds = zw_encode_lds_bytes(mbw);
-    static bool attr_set = false;
-    if (!attr_set) {
+    static const bool attr_set = []() {
         (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
+        return true;
+    }();
+    (void)attr_set;
     if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(WG), lds, s, a);
     else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(WG), lds, s, a);
     return hipGetLastError();

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +30,8 @@ hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const
                         size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes);
 hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
                         int nframes);
+hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
+                     unsigned long long* counter, unsigned long long* frame_info, uint8_t* out);
 hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
                             const uint8_t* probs, const void* args, int* levels, int* dq);
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
@@ -68,10 +71,7 @@ extern "C" int zw_ctx_create(int device, zw_ctx** out)
     HIPOK(hipSetDevice(device));
     zw_ctx* c = new zw_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return ZW_EDEVICE;
-    }
+
     *out = c;
     return ZW_OK;
 }
@@ -81,7 +81,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->dscratch) (void)hipFree(c->dscratch);
-    (void)hipStreamDestroy(c->stream);
+    if (c->stream_) (void)hipStreamDestroy(c->stream_);
     delete c;
 }
 
@@ -96,25 +96,86 @@ extern "C" void zw_bytes_free(zw_bytes* b)
 
 // --------------------------------------------------------------------------
 // Batch pipeline
+//
+// The frames of a pipe are split into up to ZW_PIPE_LANES lanes (default 4,
+// the number of hardware queues HIP uses per process).  Each lane owns a HIP
+// stream and runs the sequential per-frame flow on its slice:
+//   rgb2yuv, analysis, segments, pass 1 -> pack + D2H -> host stats/probs ->
+//   H2D -> pass 2 -> pack + D2H -> host token emission.
+// Lanes run concurrently (one host thread each), so one lane's host stages
+// overlap the other lanes' kernels and the GPU stays busy.
 // --------------------------------------------------------------------------
+// Pinned host array: copies to/from pageable memory are staged and can
+// synchronise with unrelated device work, so every async copy of the pipeline
+// goes through page-locked buffers.
+template <class T>
+struct Pinned {
+    T* p = nullptr;
+    size_t n = 0;
+    bool alloc(size_t count)
+    {
+        free();
+        if (hipHostMalloc((void**)&p, count * sizeof(T) + 64, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        n = count;
+        memset((void*)p, 0, count * sizeof(T));
+        return true;
+    }
+    void free()
+    {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    T* data() { return p; }
+    T& operator[](size_t i) { return p[i]; }
+    size_t size() const { return n; }
+    ~Pinned() { free(); }
+};
+
+struct PipeLane {
+    int f0 = 0, n = 0;  // frame slice
+    int chunk = 0;      // frames per chunk (kernels are launched per chunk)
+    hipStream_t stream = nullptr;   // kernels of the lane
+    hipStream_t stream2 = nullptr;  // packing + copies (runs beside the next chunk's kernels)
+    std::vector<hipEvent_t> cev;    // per chunk: [p1 done, p2 done]
+    hipEvent_t ev[8] = {};
+    unsigned long long* d_ctr = nullptr;
+    uint8_t* h_pack = nullptr;
+    size_t h_pack_cap = 0;
+    Pinned<unsigned long long> h_finfo;  // [2*n] offset, bytes of each frame's packed stream
+    Pinned<unsigned long long> h_total;
+    float kms[4] = {0, 0, 0, 0};
+    double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
+    int rc = 0;
+};
+
 struct zw_pipe {
     zw_ctx* ctx;
     int n, w, h, color, bpp, quality, method, mbw, mbh, nmb, qi, filter;
     size_t img_stride, ysz, csz;
-    uint8_t *d_img, *d_Y, *d_U, *d_V, *d_ry, *d_ru, *d_rv, *d_alpha;
-    uint32_t* d_histo;
-    ZwFrameParams *d_tmpl, *d_params;
-    ZwLevelCosts* d_lcost;
-    int8_t* d_derr;
-    ZwMbOut *d_out1, *d_out2;
+    uint8_t *d_img = nullptr, *d_Y = nullptr, *d_U = nullptr, *d_V = nullptr;
+    uint8_t *d_ry = nullptr, *d_ru = nullptr, *d_rv = nullptr, *d_alpha = nullptr;
+    uint32_t* d_histo = nullptr;
+    ZwFrameParams *d_tmpl = nullptr, *d_params = nullptr;
+    ZwLevelCosts* d_lcost = nullptr;
+    int8_t* d_derr = nullptr;
+    ZwMbOut *d_out1 = nullptr, *d_out2 = nullptr;
     int* d_dbg = nullptr;  // optional pass-2 I4 dump
-    std::vector<ZwMbOut> h_out1, h_out2;
-    std::vector<ZwFrameParams> h_params;
-    std::vector<ZwLevelCosts> h_lcost;
+    // packed MB streams (zw_pack_kernels.hip)
+    uint8_t* d_eobs = nullptr;
+    uint32_t* d_sizes = nullptr;
+    unsigned long long* d_finfo = nullptr;
+    uint8_t* d_pack = nullptr;
+    size_t pack_stride = 0;  // worst-case packed bytes per frame
+    Pinned<ZwFrameParams> h_params;
+    Pinned<ZwLevelCosts> h_lcost;
     std::vector<uint8_t> h_have_upd;
     std::vector<uint8_t> h_upd;  // [n][4*8*3*11]
     std::vector<std::vector<uint8_t>> bitstreams;
-    hipEvent_t ev[8];
+    std::vector<PipeLane> lanes;
     float kms[8];
 };
 
@@ -122,12 +183,49 @@ static void pipe_free(zw_pipe* p)
 {
     if (!p) return;
     void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
-                    p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg};
+                    p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg,
+                    p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
-    for (int i = 0; i < 8; i++)
-        if (p->ev[i]) (void)hipEventDestroy(p->ev[i]);
+    for (PipeLane& L : p->lanes) {
+        if (L.d_ctr) (void)hipFree(L.d_ctr);
+        if (L.h_pack) (void)hipHostFree(L.h_pack);
+        for (int i = 0; i < 8; i++)
+            if (L.ev[i]) (void)hipEventDestroy(L.ev[i]);
+        for (hipEvent_t e : L.cev)
+            if (e) (void)hipEventDestroy(e);
+        if (L.stream) (void)hipStreamDestroy(L.stream);
+        if (L.stream2) (void)hipStreamDestroy(L.stream2);
+    }
     delete p;
+}
+
+// One lane by default: an encode launch of one frame per CU already fills the
+// GPU, and chunking inside the lane overlaps host and device work.  More lanes
+// (two streams each) only help for batches smaller than two launches.
+static int pipe_lanes_for(int n)
+{
+    const char* e = getenv("ZW_PIPE_LANES");
+    int g = e ? atoi(e) : 1;
+    if (g < 1) g = 1;
+    if (g > 16) g = 16;
+    while (g > 1 && n / g < 8) g--;  // keep >= 8 frames per lane
+    return g;
+}
+// Frames per kernel launch inside a lane: one encode workgroup occupies a
+// whole CU (512 threads x 256 VGPRs), so a launch of one frame per CU fills
+// the device; the lane runs pass 1 of chunk c+1 while the host works on chunk c.
+static int pipe_chunk_for(int lane_frames, int device)
+{
+    const char* e = getenv("ZW_PIPE_CHUNK");
+    int c = e ? atoi(e) : 0;
+    if (c < 1) {
+        hipDeviceProp_t prop;
+        c = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
+                ? prop.multiProcessorCount
+                : 256;
+    }
+    return c > lane_frames ? lane_frames : c;
 }
 
 extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t height, int color, uint8_t quality,
@@ -140,7 +238,6 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
     if (quality > 100) return ZW_EINVAL;
     HIPOK(hipSetDevice(ctx->device));
     zw_pipe* p = new zw_pipe();
-    memset(p->ev, 0, sizeof p->ev);
     p->ctx = ctx;
     p->n = n;
     p->w = (int)width;
@@ -158,12 +255,7 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
     p->csz = (size_t)p->mbw * 8 * p->mbh * 8;
     p->qi = zwh::quality_to_qi(quality);
     p->filter = zwh::filter_level_for(p->qi);
-    p->d_img = p->d_Y = p->d_U = p->d_V = p->d_ry = p->d_ru = p->d_rv = p->d_alpha = nullptr;
-    p->d_histo = nullptr;
-    p->d_tmpl = p->d_params = nullptr;
-    p->d_lcost = nullptr;
-    p->d_derr = nullptr;
-    p->d_out1 = p->d_out2 = nullptr;
+    p->pack_stride = (size_t)p->nmb * (1 + 8 + 25 + 800);
     const size_t N = (size_t)n;
     bool ok = hipMalloc(&p->d_img, N * p->img_stride + 64) == hipSuccess &&
               hipMalloc(&p->d_Y, N * p->ysz) == hipSuccess && hipMalloc(&p->d_U, N * p->csz) == hipSuccess &&
@@ -176,14 +268,37 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
               hipMalloc(&p->d_lcost, N * sizeof(ZwLevelCosts)) == hipSuccess &&
               hipMalloc(&p->d_derr, N * p->mbw * 4) == hipSuccess &&
               hipMalloc(&p->d_out1, N * p->nmb * sizeof(ZwMbOut)) == hipSuccess &&
-              hipMalloc(&p->d_out2, N * p->nmb * sizeof(ZwMbOut)) == hipSuccess;
-    for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&p->ev[i]) == hipSuccess;
+              hipMalloc(&p->d_out2, N * p->nmb * sizeof(ZwMbOut)) == hipSuccess &&
+              hipMalloc(&p->d_eobs, N * p->nmb * 25) == hipSuccess &&
+              hipMalloc(&p->d_sizes, N * p->nmb * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&p->d_finfo, N * 2 * sizeof(unsigned long long)) == hipSuccess &&
+              hipMalloc(&p->d_pack, N * p->pack_stride) == hipSuccess;
+    const int G = pipe_lanes_for(n);
+    p->lanes.resize(G);
+    for (int g = 0; ok && g < G; g++) {
+        PipeLane& L = p->lanes[g];
+        L.f0 = (int)((long long)n * g / G);
+        L.n = (int)((long long)n * (g + 1) / G) - L.f0;
+        ok = L.h_finfo.alloc(2 * (size_t)L.n);
+        L.chunk = pipe_chunk_for(L.n, ctx->device);
+        const int nch = (L.n + L.chunk - 1) / L.chunk;
+        L.cev.assign(2 * (size_t)nch, nullptr);
+        ok = ok && hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) == hipSuccess &&
+             hipStreamCreateWithFlags(&L.stream2, hipStreamNonBlocking) == hipSuccess &&
+             hipMalloc(&L.d_ctr, 2 * (size_t)nch * sizeof(unsigned long long)) == hipSuccess &&
+             L.h_total.alloc(2 * (size_t)nch);
+        for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
+        for (size_t i = 0; ok && i < L.cev.size(); i++)
+            ok = hipEventCreateWithFlags(&L.cev[i], hipEventDisableTiming) == hipSuccess;
+    }
     if (!ok) {
         pipe_free(p);
         return ZW_ENOMEM;
     }
-    p->h_params.resize(N);
-    p->h_lcost.resize(N);
+    if (!p->h_params.alloc(N) || !p->h_lcost.alloc(N)) {
+        pipe_free(p);
+        return ZW_ENOMEM;
+    }
     p->h_have_upd.assign(N, 0);
     p->h_upd.assign(N * 4 * 8 * 3 * 11, 0);
     p->bitstreams.resize(N);
@@ -220,37 +335,84 @@ extern "C" int zw_pipe_upload(zw_pipe* p, int frame, const uint8_t* data, size_t
     return ZW_OK;
 }
 
-static int pipe_pass1(zw_pipe* p, bool write_recon = false)
+static double now_ms()
 {
-    hipStream_t s = p->ctx->stream;
-    const int n = p->n;
-    HIPOK(hipEventRecord(p->ev[0], s));
-    HIPOK(zwk_rgb2yuv(s, p->d_img, p->w, p->h, p->bpp, p->mbw, p->mbh, p->d_Y, p->d_U, p->d_V, p->img_stride, p->ysz,
-                      p->csz, n));
-    HIPOK(hipEventRecord(p->ev[1], s));
-    HIPOK(hipMemsetAsync(p->d_histo, 0, (size_t)n * 256 * sizeof(uint32_t), s));
-    HIPOK(zwk_analysis(s, p->d_Y, p->d_U, p->d_V, p->mbw, p->mbh, p->ysz, p->csz, p->d_alpha, p->d_histo, n));
-    HIPOK(zwk_segments(s, p->d_histo, p->d_tmpl, p->d_params, n));
-    HIPOK(hipEventRecord(p->ev[2], s));
-    HIPOK(zwk_encode(s, 1, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, nullptr, p->d_derr, p->d_out1,
-                     write_recon ? p->d_ry : nullptr, write_recon ? p->d_ru : nullptr, write_recon ? p->d_rv : nullptr,
-                     p->ysz, p->csz, p->mbw, p->mbh, n, nullptr));
-    HIPOK(hipEventRecord(p->ev[3], s));
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- per-chunk stages (frames [fa, fa + na) of a lane) ----
+static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false)
+{
+    hipStream_t s = L.stream;
+    const size_t F = (size_t)fa;
+    const int n = na;
+    if (timed) HIPOK(hipEventRecord(L.ev[0], s));
+    HIPOK(zwk_rgb2yuv(s, p->d_img + F * p->img_stride, p->w, p->h, p->bpp, p->mbw, p->mbh, p->d_Y + F * p->ysz,
+                      p->d_U + F * p->csz, p->d_V + F * p->csz, p->img_stride, p->ysz, p->csz, n));
+    if (timed) HIPOK(hipEventRecord(L.ev[1], s));
+    HIPOK(hipMemsetAsync(p->d_histo + F * 256, 0, (size_t)n * 256 * sizeof(uint32_t), s));
+    HIPOK(zwk_analysis(s, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->mbw, p->mbh, p->ysz,
+                       p->csz, p->d_alpha + F * p->nmb, p->d_histo + F * 256, n));
+    HIPOK(zwk_segments(s, p->d_histo + F * 256, p->d_tmpl, p->d_params + F, n));
+    if (timed) HIPOK(hipEventRecord(L.ev[2], s));
+    HIPOK(zwk_encode(s, 1, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
+                     p->d_params + F, nullptr, p->d_derr + F * p->mbw * 4, p->d_out1 + F * p->nmb,
+                     write_recon ? p->d_ry + F * p->ysz : nullptr, write_recon ? p->d_ru + F * p->csz : nullptr,
+                     write_recon ? p->d_rv + F * p->csz : nullptr, p->ysz, p->csz, p->mbw, p->mbh, n, nullptr));
+    if (timed) HIPOK(hipEventRecord(L.ev[3], s));
     return ZW_OK;
 }
 
-static int pipe_host_stats(zw_pipe* p)
+// Pack the chunk's MB records on the kernel stream (right after the pass that
+// produced them: the encode kernels occupy every CU, so a pack kernel queued
+// elsewhere would wait for the next chunk's pass).  slot: 2*chunk + pass-1.
+static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_out, int slot)
 {
-    hipStream_t s = p->ctx->stream;
-    const size_t N = (size_t)p->n;
-    p->h_out1.resize(N * p->nmb);
-    HIPOK(hipMemcpyAsync(p->h_out1.data(), p->d_out1, N * p->nmb * sizeof(ZwMbOut), hipMemcpyDeviceToHost, s));
-    HIPOK(hipMemcpyAsync(p->h_params.data(), p->d_params, N * sizeof(ZwFrameParams), hipMemcpyDeviceToHost, s));
+    const size_t F = (size_t)fa;
+    HIPOK(zwk_pack(L.stream, d_out + F * p->nmb, p->nmb, na, p->d_eobs + F * p->nmb * 25, p->d_sizes + F * p->nmb,
+                   L.d_ctr + slot, p->d_finfo + 2 * F, p->d_pack + F * p->pack_stride));
+    return ZW_OK;
+}
+
+// Copy a packed chunk to the lane's pinned buffer on the copy stream once
+// `ready` (recorded after chunk_pack) has fired.  h_finfo[2*i] = offset of frame fa+i.
+static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEvent_t ready)
+{
+    hipStream_t s = L.stream2;
+    const size_t F = (size_t)fa;
+    HIPOK(hipStreamWaitEvent(s, ready, 0));
+    HIPOK(hipMemcpyAsync(L.h_total.data() + slot, L.d_ctr + slot, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         s));
+    HIPOK(hipMemcpyAsync(L.h_finfo.data(), p->d_finfo + 2 * F, 2 * (size_t)na * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
-    parallel_for(p->n, [&](int f) {
+    const unsigned long long total = L.h_total[slot];
+    if (total > L.h_pack_cap) {
+        if (L.h_pack) (void)hipHostFree(L.h_pack);
+        L.h_pack = nullptr;
+        L.h_pack_cap = 0;
+        const size_t cap = (size_t)(total * 1.25) + 4096;
+        if (hipHostMalloc((void**)&L.h_pack, cap, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
+        L.h_pack_cap = cap;
+    }
+    HIPOK(hipMemcpyAsync(L.h_pack, p->d_pack + F * p->pack_stride, total, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
+{
+    hipStream_t s = L.stream;
+    const size_t F = (size_t)fa, n = (size_t)na;
+    // segment params of the chunk (written by k_segments before pass 1)
+    HIPOK(hipMemcpyAsync(p->h_params.data() + F, p->d_params + F, n * sizeof(ZwFrameParams), hipMemcpyDeviceToHost,
+                         L.stream2));
+    HIPOK(hipStreamSynchronize(L.stream2));
+    parallel_for(na, [&](int i) {
+        const size_t f = F + i;
         zwh::Stats st;
-        int sp = zwh::replay_stats(st, p->h_out1.data() + (size_t)f * p->nmb, p->mbw, p->mbh);
-        uint8_t* upd = p->h_upd.data() + (size_t)f * 4 * 8 * 3 * 11;
+        int sp = zwh::replay_stats(st, L.h_pack + L.h_finfo[2 * i], p->mbw, p->mbh);
+        uint8_t* upd = p->h_upd.data() + f * 4 * 8 * 3 * 11;
         bool have = zwh::updated_probs(st, (uint8_t(*)[8][3][11])upd);
         p->h_have_upd[f] = have;
         ZwFrameParams& P = p->h_params[f];
@@ -258,85 +420,173 @@ static int pipe_host_stats(zw_pipe* p)
         memcpy(P.probs, upd, sizeof P.probs);
         zwh::level_costs(p->h_lcost[f], (const uint8_t(*)[8][3][11])upd);
     });
-    HIPOK(hipMemcpyAsync(p->d_params, p->h_params.data(), N * sizeof(ZwFrameParams), hipMemcpyHostToDevice, s));
-    HIPOK(hipMemcpyAsync(p->d_lcost, p->h_lcost.data(), N * sizeof(ZwLevelCosts), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(p->d_params + F, p->h_params.data() + F, n * sizeof(ZwFrameParams), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(p->d_lcost + F, p->h_lcost.data() + F, n * sizeof(ZwLevelCosts), hipMemcpyHostToDevice, s));
     return ZW_OK;
 }
 
-static int pipe_pass2(zw_pipe* p)
+static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
 {
-    hipStream_t s = p->ctx->stream;
-    HIPOK(hipEventRecord(p->ev[4], s));
-    HIPOK(zwk_encode(s, 2, p->d_Y, p->d_U, p->d_V, p->d_alpha, p->d_params, p->d_lcost, p->d_derr, p->d_out2,
-                     p->d_ry, p->d_ru, p->d_rv, p->ysz, p->csz, p->mbw, p->mbh, p->n, p->d_dbg));
-    HIPOK(hipEventRecord(p->ev[5], s));
+    hipStream_t s = L.stream;
+    const size_t F = (size_t)fa;
+    if (timed) HIPOK(hipEventRecord(L.ev[4], s));
+    HIPOK(zwk_encode(s, 2, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
+                     p->d_params + F, p->d_lcost + F, p->d_derr + F * p->mbw * 4, p->d_out2 + F * p->nmb,
+                     p->d_ry + F * p->ysz, p->d_ru + F * p->csz, p->d_rv + F * p->csz, p->ysz, p->csz, p->mbw, p->mbh,
+                     na, p->d_dbg ? p->d_dbg + F * p->nmb * 16 * 34 : nullptr));
+    if (timed) HIPOK(hipEventRecord(L.ev[5], s));
     return ZW_OK;
 }
 
-static int pipe_emit(zw_pipe* p)
+static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na)
 {
-    hipStream_t s = p->ctx->stream;
-    const size_t N = (size_t)p->n;
-    p->h_out2.resize(N * p->nmb);
-    HIPOK(hipMemcpyAsync(p->h_out2.data(), p->d_out2, N * p->nmb * sizeof(ZwMbOut), hipMemcpyDeviceToHost, s));
-    HIPOK(hipStreamSynchronize(s));
-    parallel_for(p->n, [&](int f) {
-        zwh::emit_frame(p->bitstreams[f], p->h_params[f], p->h_out2.data() + (size_t)f * p->nmb, p->w, p->h,
-                        p->h_have_upd[f] != 0,
-                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + (size_t)f * 4 * 8 * 3 * 11));
+    const size_t F = (size_t)fa;
+    parallel_for(na, [&](int i) {
+        const size_t f = F + i;
+        zwh::emit_frame(p->bitstreams[f], p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h,
+                        p->h_have_upd[f] != 0, (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
     });
+}
+
+static void lane_times(PipeLane& L)
+{
+    for (int i = 0; i < 4; i++) L.kms[i] = 0.f;
+    (void)hipEventElapsedTime(&L.kms[0], L.ev[0], L.ev[1]);  // rgb2yuv
+    (void)hipEventElapsedTime(&L.kms[1], L.ev[1], L.ev[2]);  // analysis + segments
+    (void)hipEventElapsedTime(&L.kms[2], L.ev[2], L.ev[3]);  // pass 1
+    (void)hipEventElapsedTime(&L.kms[3], L.ev[4], L.ev[5]);  // pass 2
+}
+
+// Software-pipelined encode of one lane: all pass-1 launches are queued first;
+// the host works on chunk c (stats, then tokens) while the GPU runs later chunks.
+//   GPU (stream):  P1(0) P1(1) .. P1(C-1) P2(0) P2(1) .. P2(C-1)
+//   host:                 S(0)   S(1) ..          E(0)   E(1) .. E(C-1)
+static double g_trace_t0 = 0;
+static bool g_trace = false;
+static int lane_encode(zw_pipe* p, PipeLane& L, bool emit)
+{
+    const int nch = (L.n + L.chunk - 1) / L.chunk;
+    auto ca = [&](int c) { return L.f0 + c * L.chunk; };
+    auto cn = [&](int c) { return std::min(L.chunk, L.n - c * L.chunk); };
+    for (int c = 0; c < nch; c++) {
+        int r = chunk_pass1(p, L, ca(c), cn(c), c == 0);
+        if (!r) r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
+        if (r) return r;
+        HIPOK(hipEventRecord(L.cev[2 * c], L.stream));
+    }
+    double fetch = 0, stats = 0, fetch2 = 0, tok = 0;
+    for (int c = 0; c < nch; c++) {
+        double t0 = now_ms();
+        int r = chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c]);
+        if (r) return r;
+        double t1 = now_ms();
+        r = chunk_stats(p, L, ca(c), cn(c));
+        if (r) return r;
+        stats += now_ms() - t1;
+        fetch += t1 - t0;
+        if (g_trace) fprintf(stderr, "  lane %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, c, t1 - g_trace_t0, now_ms() - g_trace_t0);
+        r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
+        if (!r && emit) r = chunk_pack(p, L, ca(c), cn(c), p->d_out2, 2 * c + 1);
+        if (r) return r;
+        HIPOK(hipEventRecord(L.cev[2 * c + 1], L.stream));
+    }
+    if (emit) {
+        for (int c = 0; c < nch; c++) {
+            double t0 = now_ms();
+            int r = chunk_fetch(p, L, ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
+            if (r) return r;
+            double t1 = now_ms();
+            chunk_emit(p, L, ca(c), cn(c));
+            tok += now_ms() - t1;
+            fetch2 += t1 - t0;
+            if (g_trace) fprintf(stderr, "  lane %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, c, t1 - g_trace_t0, now_ms() - g_trace_t0);
+        }
+    }
+    HIPOK(hipStreamSynchronize(L.stream));
+    L.hms[0] = fetch;
+    L.hms[1] = stats;
+    L.hms[2] = fetch2;
+    L.hms[3] = tok;
+    lane_times(L);
     return ZW_OK;
 }
 
-static void pipe_times(zw_pipe* p)
+// Run fn(lane) for every lane concurrently; returns the first error.
+template <class F>
+static int run_lanes(zw_pipe* p, F fn)
 {
+    const int G = (int)p->lanes.size();
+    if (G == 1) return fn(p->lanes[0]);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++)
+        th.emplace_back([&, g]() {
+            (void)hipSetDevice(p->ctx->device);
+            p->lanes[g].rc = fn(p->lanes[g]);
+        });
+    for (auto& t : th) t.join();
+    for (PipeLane& L : p->lanes)
+        if (L.rc) return L.rc;
+    return ZW_OK;
+}
+
+static void pipe_collect_times(zw_pipe* p)
+{
+    // per-kernel: mean over lanes of each lane's launch duration; host: max over lanes
     for (int i = 0; i < 8; i++) p->kms[i] = 0.f;
-    (void)hipEventElapsedTime(&p->kms[0], p->ev[0], p->ev[1]);  // rgb2yuv
-    (void)hipEventElapsedTime(&p->kms[1], p->ev[1], p->ev[2]);  // analysis + segments
-    (void)hipEventElapsedTime(&p->kms[2], p->ev[2], p->ev[3]);  // pass 1
-    (void)hipEventElapsedTime(&p->kms[3], p->ev[4], p->ev[5]);  // pass 2
-}
-
-extern "C" int zw_pipe_run_device(zw_pipe* p)
-{
-    if (!p) return ZW_EINVAL;
-    HIPOK(hipSetDevice(p->ctx->device));
-    int r = pipe_pass1(p);
-    if (r) return r;
-    r = pipe_host_stats(p);
-    if (r) return r;
-    r = pipe_pass2(p);
-    if (r) return r;
-    HIPOK(hipStreamSynchronize(p->ctx->stream));
-    pipe_times(p);
-    return ZW_OK;
+    for (PipeLane& L : p->lanes)
+        for (int i = 0; i < 4; i++) {
+            p->kms[i] += L.kms[i] / (float)p->lanes.size();
+            p->kms[4 + i] = std::max(p->kms[4 + i], (float)L.hms[i]);
+        }
 }
 
 extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
 {
     if (!p) return ZW_EINVAL;
     HIPOK(hipSetDevice(p->ctx->device));
-    int r = pipe_pass1(p, write_recon != 0);
-    if (r) return r;
-    HIPOK(hipStreamSynchronize(p->ctx->stream));
-    return ZW_OK;
+    return run_lanes(p, [&](PipeLane& L) -> int {
+        for (int fa = L.f0; fa < L.f0 + L.n; fa += L.chunk) {
+            int r = chunk_pass1(p, L, fa, std::min(L.chunk, L.f0 + L.n - fa), false, write_recon != 0);
+            if (r) return r;
+        }
+        HIPOK(hipStreamSynchronize(L.stream));
+        return ZW_OK;
+    });
+}
+
+extern "C" int zw_pipe_run_device(zw_pipe* p)
+{
+    if (!p) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    int r = run_lanes(p, [&](PipeLane& L) -> int { return lane_encode(p, L, false); });
+    pipe_collect_times(p);
+    return r;
 }
 
 extern "C" int zw_pipe_encode(zw_pipe* p)
 {
     if (!p) return ZW_EINVAL;
     HIPOK(hipSetDevice(p->ctx->device));
-    int r = pipe_pass1(p);
-    if (r) return r;
-    r = pipe_host_stats(p);
-    if (r) return r;
-    r = pipe_pass2(p);
-    if (r) return r;
-    r = pipe_emit(p);
-    if (r) return r;
-    pipe_times(p);
-    return ZW_OK;
+    static const bool trace = getenv("ZW_PIPE_TRACE") != nullptr;
+    const double T0 = now_ms();
+    g_trace = trace;
+    g_trace_t0 = T0;
+    int r = run_lanes(p, [&](PipeLane& L) -> int {
+        const int q = lane_encode(p, L, true);
+        if (trace)
+            fprintf(stderr, "lane f0=%d n=%d chunk=%d: done %.1f ms (fetch %.1f stats %.1f fetch2 %.1f emit %.1f) "
+                            "k: %.1f %.1f %.1f %.1f\n",
+                    L.f0, L.n, L.chunk, now_ms() - T0, L.hms[0], L.hms[1], L.hms[2], L.hms[3], L.kms[0], L.kms[1],
+                    L.kms[2], L.kms[3]);
+        return q;
+    });
+    pipe_collect_times(p);
+    return r;
 }
+
+extern "C" int zw_pipe_launch_frames(zw_pipe* p) { return p && !p->lanes.empty() ? p->lanes[0].chunk : 0; }
+
+extern "C" int zw_pipe_lanes(zw_pipe* p) { return p ? (int)p->lanes.size() : 0; }
 
 extern "C" int zw_pipe_kernel_times(zw_pipe* p, float* ms, int n)
 {
@@ -520,7 +770,7 @@ extern "C" int zw_rgb_to_yuv420(zw_ctx* ctx, const uint8_t* img, uint32_t width,
     const int mbw = ((int)width + 15) / 16, mbh = ((int)height + 15) / 16;
     const size_t isz = (size_t)width * height * bpp, ysz = (size_t)mbw * 16 * mbh * 16, csz = (size_t)mbw * 8 * mbh * 8;
     uint8_t *d_img = nullptr, *d_y = nullptr, *d_u = nullptr, *d_v = nullptr;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = ctx_stream(ctx);
     int rc = ZW_OK;
     if (hipMalloc(&d_img, isz) != hipSuccess || hipMalloc(&d_y, ysz) != hipSuccess || hipMalloc(&d_u, csz) != hipSuccess ||
         hipMalloc(&d_v, csz) != hipSuccess)
@@ -584,7 +834,7 @@ extern "C" int zw_quant_blocks(zw_ctx* ctx, int n, const int32_t* coeffs, const 
     const size_t o_lv = (o_p + sizeof P + 255) & ~(size_t)255, o_dq = o_lv + cb, total = o_dq + cb;
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = ctx_stream(ctx);
     HIPOK(hipMemcpyAsync(d + o_c, coeffs, cb, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_x, ctx0, (size_t)n, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_l, &L, sizeof L, hipMemcpyHostToDevice, s));

@@ -128,6 +128,37 @@ inline void level_costs(ZwLevelCosts& L, const uint8_t probs[4][8][3][11])
             }
 }
 
+// Packed MB record (zw_pack_kernels.hip) -> ZwMbOut (levels beyond each
+// block's eob are zero).  Returns the pointer past the record.
+inline const uint8_t* unpack_mb(const uint8_t* p, ZwMbOut& m)
+{
+    const uint8_t h = p[0];
+    m.luma_mode = h & 7;
+    m.skip = (h >> 3) & 1;
+    m.segment = (h >> 4) & 3;
+    m.chroma_mode = h >> 6;
+    p++;
+    if (m.luma_mode == 4) {
+        for (int i = 0; i < 8; i++) {
+            m.bpred[2 * i] = p[i] & 15;
+            m.bpred[2 * i + 1] = p[i] >> 4;
+        }
+        p += 8;
+    } else {
+        memset(m.bpred, 0, 16);
+    }
+    const uint8_t* eob = p;
+    p += 25;
+    for (int b = 0; b < 25; b++) {
+        const int e = eob[b];
+        int16_t* d = m.levels[b];
+        int n = 0;
+        for (; n < e; n++, p += 2) d[n] = (int16_t)(uint16_t)(p[0] | (p[1] << 8));
+        for (; n < 16; n++) d[n] = 0;
+    }
+    return p;
+}
+
 struct Stats {
     uint32_t s[4][8][3][11];
 };
@@ -228,8 +259,9 @@ inline bool mb_all_zero_p1(const ZwMbOut& m)
 
 // Pass-1 statistics replay in raster order (vp8.rs:1337-1385 + record_residual_stats :1027).
 // Returns the skip probability.
-inline int replay_stats(Stats& S, const ZwMbOut* mbs, int mbw, int mbh)
+inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
 {
+    ZwMbOut m;
     memset(&S, 0, sizeof S);
     std::vector<Cplx> top(mbw);
     memset(top.data(), 0, sizeof(Cplx) * mbw);
@@ -238,7 +270,7 @@ inline int replay_stats(Stats& S, const ZwMbOut* mbs, int mbw, int mbh)
         Cplx left;
         memset(&left, 0, sizeof left);
         for (int x = 0; x < mbw; x++) {
-            const ZwMbOut& m = mbs[(size_t)y * mbw + x];
+            packed = unpack_mb(packed, m);
             total++;
             const bool i4 = m.luma_mode == 4;
             if (mb_all_zero_p1(m)) {
@@ -365,9 +397,10 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const int16_t* 
 
 // Frame assembly: compressed header (vp8.rs:332), MB headers (:498), residual
 // partition (:650), frame tag (:315).
-inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const ZwMbOut* mbs, int width, int height,
-                       bool have_updated, const uint8_t upd[4][8][3][11])
+inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const uint8_t* packed, int width,
+                       int height, bool have_updated, const uint8_t upd[4][8][3][11])
 {
+    ZwMbOut m;
     const int mbw = P.mbw, mbh = P.mbh;
     BoolEncoder H, T;
     uint8_t probs[4][8][3][11];
@@ -426,7 +459,7 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
         memset(&left, 0, sizeof left);
         uint8_t left_bp[4] = {0, 0, 0, 0};
         for (int x = 0; x < mbw; x++) {
-            const ZwMbOut& m = mbs[(size_t)y * mbw + x];
+            packed = unpack_mb(packed, m);
             if (P.seg_enabled && P.seg_update_map) H.tree(SEGMENT_ID_TREE, 6, P.seg_probs, m.segment);
             H.put(m.skip, P.skip_prob);
             H.tree(YMODE_TREE, 8, KEYFRAME_YMODE_PROBS, m.luma_mode);

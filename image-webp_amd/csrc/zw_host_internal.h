@@ -10,7 +10,7 @@
 
 struct zw_ctx {
     int device;
-    hipStream_t stream;
+    hipStream_t stream_ = nullptr;  // created on first use (hardware queues are scarce)
     // grow-only device scratch for the single-call decode / filter entry points
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
@@ -71,4 +71,12 @@ static inline void* ctx_scratch(zw_ctx* c, size_t bytes)
         c->dscratch_cap = bytes;
     }
     return c->dscratch;
+}
+
+// The context's own stream (single-call entry points); created lazily so a
+// context that only drives pipes does not hold a hardware queue.
+static inline hipStream_t ctx_stream(zw_ctx* c)
+{
+    if (!c->stream_) (void)hipStreamCreateWithFlags(&c->stream_, hipStreamNonBlocking);
+    return c->stream_;
 }

@@ -1,0 +1,131 @@
+// zw_pack_kernels.hip -- device-side compaction of the per-MB encoder records
+// before they cross PCIe to the host entropy stage.
+//
+// ZwMbOut is 820 B/MB (modes + 25x16 int16 levels, mostly zero).  The host
+// only needs each block's levels up to its last nonzero (zigzag eob), so the
+// records are packed into a byte stream per frame:
+//
+//   MB := u8 hdr (luma 0..4 | skip << 3 | segment << 4 | chroma << 6)
+//         [8 B sub-modes, 4 bits each, if luma == 4]
+//         u8 eob[25]            (blocks 0..15 Y, 16 Y2, 17..20 U, 21..24 V)
+//         i16 levels[sum eob]   (block order, zigzag positions 0..eob-1)
+//
+// k_pack_size: one wave per MB -> eobs + MB size; k_pack_scan: one workgroup
+// per frame -> MB offsets and an atomically reserved slice of the output
+// buffer (frames land contiguously, in any order; offsets are reported);
+// k_pack_write: one wave per MB.
+#include "zw_dev.h"
+
+#define PK_WAVES 4
+
+__device__ __forceinline__ int pk_mb_size(int luma, int eobsum) { return 1 + (luma == 4 ? 8 : 0) + 25 + 2 * eobsum; }
+
+extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_size(const ZwMbOut* __restrict__ mbs, int nmb,
+                                                                      int nframes, uint8_t* __restrict__ eobs,
+                                                                      uint32_t* __restrict__ sizes)
+{
+    const size_t mb = (size_t)blockIdx.x * PK_WAVES + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (mb >= (size_t)nmb * nframes) return;
+    const ZwMbOut& M = mbs[mb];
+    int eob = 0;
+    if (lane < 25) {
+        const uint32_t* p = (const uint32_t*)&M.levels[lane][0];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const uint32_t v = p[w];
+            if (v & 0xffffu) eob = 2 * w + 1;
+            if (v >> 16) eob = 2 * w + 2;
+        }
+        if (M.skip) eob = 0;
+        eobs[mb * 25 + lane] = (uint8_t)eob;
+    }
+    int s = eob;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) sizes[mb] = (uint32_t)pk_mb_size(M.luma_mode, s);
+}
+
+// One workgroup (1024 threads) per frame: exclusive scan of MB sizes in place,
+// frame slice reservation.  frame_info[f] = {offset, bytes}.
+extern "C" __global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restrict__ sizes, int nmb,
+                                                              unsigned long long* __restrict__ counter,
+                                                              unsigned long long* __restrict__ frame_info)
+{
+    __shared__ uint32_t part[1024];
+    __shared__ unsigned long long base;
+    const int f = blockIdx.x, t = threadIdx.x;
+    uint32_t* S = sizes + (size_t)f * nmb;
+    const int per = (nmb + 1023) / 1024;
+    const int b0 = t * per, b1 = min(b0 + per, nmb);
+    uint32_t acc = 0;
+    for (int i = b0; i < b1; i++) acc += S[i];
+    part[t] = acc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - acc;  // exclusive prefix of this thread's chunk
+    for (int i = b0; i < b1; i++) {
+        const uint32_t v = S[i];
+        S[i] = run;
+        run += v;
+    }
+    if (t == 1023) {
+        const unsigned long long tot = part[1023];
+        base = atomicAdd(counter, tot);
+        frame_info[2 * f] = base;
+        frame_info[2 * f + 1] = tot;
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
+    const ZwMbOut* __restrict__ mbs, int nmb, int nframes, const uint8_t* __restrict__ eobs,
+    const uint32_t* __restrict__ offs, const unsigned long long* __restrict__ frame_info, uint8_t* __restrict__ out)
+{
+    const size_t mb = (size_t)blockIdx.x * PK_WAVES + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (mb >= (size_t)nmb * nframes) return;
+    const int f = (int)(mb / nmb);
+    const ZwMbOut& M = mbs[mb];
+    uint8_t* o = out + frame_info[2 * f] + offs[mb];
+    const int luma = M.luma_mode;
+    const int hdr = 1 + (luma == 4 ? 8 : 0);
+    if (lane == 0) o[0] = (uint8_t)(luma | (M.skip << 3) | (M.segment << 4) | (M.chroma_mode << 6));
+    if (luma == 4 && lane < 8) o[1 + lane] = (uint8_t)(M.bpred[2 * lane] | (M.bpred[2 * lane + 1] << 4));
+    const int eob = lane < 25 ? eobs[mb * 25 + lane] : 0;
+    if (lane < 25) o[hdr + lane] = (uint8_t)eob;
+    // exclusive prefix of eobs over lanes 0..24
+    int pre = eob;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {
+        const int v = __shfl_up(pre, d);
+        if (lane >= d) pre += v;
+    }
+    pre -= eob;
+    if (lane < 25) {
+        uint8_t* lv = o + hdr + 25 + 2 * pre;  // byte stream: i16 little-endian, unaligned
+        for (int n = 0; n < eob; n++) {
+            const int16_t v = M.levels[lane][n];
+            lv[2 * n] = (uint8_t)(v & 0xff);
+            lv[2 * n + 1] = (uint8_t)((uint16_t)v >> 8);
+        }
+    }
+}
+
+extern "C" hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
+                               unsigned long long* counter, unsigned long long* frame_info, uint8_t* out)
+{
+    const size_t total = (size_t)nmb * nframes;
+    const unsigned grid = (unsigned)((total + PK_WAVES - 1) / PK_WAVES);
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);  // this chunk's own counter
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pack_size, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes);
+    hipLaunchKernelGGL(k_pack_scan, dim3(nframes), dim3(1024), 0, s, sizes, nmb, counter, frame_info);
+    hipLaunchKernelGGL(k_pack_write, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes, frame_info,
+                       out);
+    return hipGetLastError();
+}

@@ -118,6 +118,8 @@ SIGNATURES = [
     ("zw_pipe_read_debug", _I, [_VP, _I, _VP]),
     ("zw_pipe_read_probs", _I, [_VP, _I, _VP, ctypes.POINTER(_I)]),
     ("zw_pipe_kernel_times", _I, [_VP, ctypes.POINTER(ctypes.c_float), _I]),
+    ("zw_pipe_lanes", _I, [_VP]),
+    ("zw_pipe_launch_frames", _I, [_VP]),
 ]
 
 _LIB = None
@@ -433,11 +435,19 @@ class Pipeline:
         _check(self._lib.zw_pipe_read_probs(self._h, i, _ptr(pr), ctypes.byref(sp)), "zw_pipe_read_probs")
         return pr, sp.value
 
+    @property
+    def lanes(self):
+        return self._lib.zw_pipe_lanes(self._h)
+
+    @property
+    def launch_frames(self):
+        return self._lib.zw_pipe_launch_frames(self._h)
+
     def kernel_times(self):
         ms = (ctypes.c_float * 8)()
         n = self._lib.zw_pipe_kernel_times(self._h, ms, 8)
         _check(n, "zw_pipe_kernel_times")
-        return list(ms)[:4]
+        return list(ms)  # ms: rgb2yuv, analysis+segments, pass1, pass2 (device); fetch1, stats, fetch2, emit (host)
 
     def close(self):
         if self._h:

@@ -145,7 +145,15 @@ int zw_pipe_enable_debug(zw_pipe *p);
 int zw_pipe_read_debug(zw_pipe *p, int frame, int32_t *out);
 /* Token probabilities (4*8*3*11) and skip probability used by pass 2. */
 int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
-/* Per-kernel device time of the last zw_pipe_encode/run_device (ms). */
+/* The pipe splits its frames into lanes (env ZW_PIPE_LANES, default 2), each with
+ * a kernel stream and a copy stream, and each lane into chunks (env
+ * ZW_PIPE_CHUNK, default 128 frames per launch): the host entropy work on one
+ * chunk overlaps the kernels of the next.  zw_pipe_kernel_times: ms[0..3] = mean per-launch device time of
+ * rgb2yuv, analysis+segments, pass 1, pass 2 (each launch covers one lane's
+ * frames); ms[4..7] = host ms of fetch1, stats, fetch2, emit (max over lanes). */
+int zw_pipe_lanes(zw_pipe *p);
+/* frames covered by one encode-kernel launch (a lane's chunk) */
+int zw_pipe_launch_frames(zw_pipe *p);
 int zw_pipe_kernel_times(zw_pipe *p, float *ms, int n);
 
 #ifdef __cplusplus

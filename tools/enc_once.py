@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Encode a batch once (after one warm-up encode) -- a small target for rocprofv3 runs."""
 import os
+
+# Two pipeline lanes x (kernel + copy stream) plus the runtime's own streams:
+# ask HIP for 8 hardware queues (default 4) so no two busy streams share one.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

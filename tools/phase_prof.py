@@ -6,6 +6,10 @@ usage: python tools/phase_prof.py [frames] [width] [height] [method]
 """
 import ctypes
 import os
+
+# Two pipeline lanes x (kernel + copy stream) plus the runtime's own streams:
+# ask HIP for 8 hardware queues (default 4) so no two busy streams share one.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 import time
 
@@ -40,7 +44,8 @@ def main():
     assert L.zw_phase_cycles(buf, 0) == 0
     kt = p.kernel_times()
     nmb = p.mbw * p.mbh * F
-    print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt]}")
+    print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt[:4]]} "
+          f"host(ms) fetch1/stats/fetch2/emit {[round(x, 2) for x in kt[4:8]]}")
     for ps in (0, 1):
         tot = sum(buf[ps * 16 + k] for k in range(10)) or 1
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
