@@ -11,10 +11,16 @@ Multi-GPU: one process per GPU (torch.distributed.run); frames are sharded by
 rank (independent frames, no data-path collective); a barrier brackets the
 timed region and the max time is taken with an all-reduce.
 
-The roofline object reports the dominant kernel (k_encode pass 2, the final
-DCT+quant pass fused with the mode search) against HBM: algorithmic bytes
-1568 B/MB (src YUV 384 + levels 800 + recon 384) x MBs per
-launch / average launch time measured with HIP events on the pipeline stream.
+The `roofline` object is SURVEY.md 8(d)'s designated HBM-bound kernel, the
+streaming DCT+quant pass k_fdct_quant: 80 algorithmic bytes per 4x4 block
+(16 src + 16 pred + 32 levels + 16 recon) x blocks per launch / average launch
+time from HIP events on the launch stream, over 256 frames' worth of blocks
+(24 per MB) resident in HBM; `traffic` is the PMC-measured HBM bytes per launch
+from profiles/ (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_pmc_xform.sh), scaled to
+this launch size.  `encode_kernel` reports the step's dominant kernel
+(k_encode pass 2, whose final DCT+quant is fused with the RD mode search)
+against the same HBM peak using 8(d)'s 1568 B/MB -- it is VALU-latency bound,
+not HBM bound.
 cpu_baseline times the C restatement of the reference encoder (oracle/, 1
 thread) on a bounded sample of the same frames.
 """
@@ -33,6 +39,18 @@ sys.path.insert(0, os.path.join(ROOT, "image-webp_amd"))
 
 ALG_BYTES_PER_MB = 1568
 HBM_PEAK_GBS = 8000.0
+XFORM_PMC = os.path.join(ROOT, "profiles", "r01_xform_pmc_traffic.json")
+
+
+def xform_traffic(blocks):
+    """PMC-measured HBM bytes of one k_fdct_quant launch over `blocks` blocks
+    (profiles/, scaled per block), or None when no profile is committed."""
+    try:
+        with open(XFORM_PMC) as f:
+            d = json.load(f)
+        return d["traffic_bytes"] / d["blocks"] * blocks
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -66,6 +84,46 @@ def cpu_baseline(imgs, w, h, q, m, budget_s):
             break
     return {"value": n / el, "unit": "encodes/s", "cores": 1, "kind": "port",
             "sample": f"{n} synthetic {w}x{h} RGBA frames, Q{q} m{m}, oracle/ C restatement, 1 thread, {el:.1f} s"}
+
+
+def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
+    """Streaming DCT+quant pass (k_fdct_quant) over `frames` frames' worth of 4x4
+    blocks (24 per MB), device-resident synthetic src/pred; HIP events on the
+    launch stream.  Algorithmic bytes per block: 16 src + 16 pred + 32 levels + 16 recon."""
+    import zwebp
+    n = frames * nmb * 24
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED)
+    base = torch.randint(0, 256, (n, 1), dtype=torch.int16, device=dev, generator=g)
+    src = (base + torch.randint(-40, 41, (n, 16), dtype=torch.int16, device=dev, generator=g)).clamp(0, 255).to(torch.uint8)
+    pred = (base + torch.randint(-20, 21, (n, 16), dtype=torch.int16, device=dev, generator=g)).clamp(0, 255).to(torch.uint8)
+    del base
+    lv = torch.empty((n, 16), dtype=torch.int16, device=dev)
+    rc = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the kernel and the events share it
+    sh = stream.cuda_stream
+    torch.cuda.synchronize(dev)
+
+    def run():
+        zwebp.transform_quant_blocks_device(n, src.data_ptr(), pred.data_ptr(), 24, 30, 0, 0, lv.data_ptr(),
+                                            rc.data_ptr(), stream=sh, ctx=ctx)
+
+    run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    byts = n * 80
+    ach = byts / (ms * 1e-3) / 1e9
+    del src, pred, lv, rc
+    torch.cuda.empty_cache()
+    return {"kernel": "k_fdct_quant", "workload": f"{frames} frames x {nmb} MBs x 24 4x4 blocks, Q75 Y1 matrix",
+            "blocks": n, "ms_per_launch": ms, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": byts}
 
 
 def main():
@@ -119,6 +177,7 @@ def main():
         p2_ms = float(k[3])
         per_launch = pipe.launch_frames  # frames covered by one k_encode_pass2 launch (one lane chunk)
         achieved = ALG_BYTES_PER_MB * nmb * per_launch / (p2_ms * 1e-3) / 1e9 if p2_ms > 0 else 0.0
+        dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
@@ -138,11 +197,16 @@ def main():
             "config": {"workload": f"encode_frame_lossy {w}x{h} RGBA Q{a.quality} m{a.method}",
                        "frames_per_step_per_gpu": F, "distinct_frames": len(imgs), "mbs_per_frame": nmb,
                        "parallelism": f"frames sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_encode_pass2", "alg_bytes_per_launch": ALG_BYTES_PER_MB * nmb * per_launch,
-                         "launch_frames": per_launch},
+            "roofline": {"bound": "hbm", "achieved": dq["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": dq["frac"], "traffic": xform_traffic(dq["blocks"]),
+                         "kernel": "k_fdct_quant", "workload": dq["workload"], "blocks_per_launch": dq["blocks"],
+                         "alg_bytes_per_launch": dq["alg_bytes_per_launch"], "ms_per_launch": dq["ms_per_launch"],
+                         "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"},
             "cpu_baseline": cpu,
+            "encode_kernel": {"kernel": "k_encode_pass2", "bound": "valu", "hbm_achieved": achieved,
+                              "hbm_frac": achieved / HBM_PEAK_GBS, "unit": "GB/s",
+                              "alg_bytes_per_launch": ALG_BYTES_PER_MB * nmb * per_launch,
+                              "launch_frames": per_launch, "ms_per_launch": p2_ms},
             "kernel_ms_per_step": {"rgb2yuv": float(k[0]), "analysis_segments": float(k[1]),
                                    "encode_pass1": float(k[2]), "encode_pass2": p2_ms},
             "host_ms_per_step": {"fetch_pass1": float(k[4]), "stats_probs": float(k[5]),

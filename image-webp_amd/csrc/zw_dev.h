@@ -96,12 +96,17 @@ DI long long shfl64(long long v, int src)
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// 24-bit multiplies (full-rate v_mul_*_24 instead of quarter-rate v_mul_lo_u32).
+// Every operand on these paths is below 2^23 in magnitude and every product
+// fits in 32 bits, so the low 32 bits equal the plain int product.
+DI int m24(int a, int b) { return __mul24(a, b); }
+
 // VP8Matrix::quantize_coeff (cost.rs:457): sign * ((|c| * iq + bias) >> 17).
 // |c| * iq < 2^31 for every coefficient an 8-bit source can produce.
 DI int quantz(int c, uint32_t iq, uint32_t bias)
 {
     uint32_t a = (uint32_t)iabs(c);
-    int l = (int)((a * iq + bias) >> 17);
+    int l = (int)((__umul24(a, iq) + bias) >> 17);
     return c < 0 ? -l : l;
 }
 
@@ -136,8 +141,8 @@ DI void idct16(int* b)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         int a1 = b[i] + b[8 + i], b1 = b[i] - b[8 + i];
-        int c1 = ((b[4 + i] * 35468) >> 16) - (b[12 + i] + ((b[12 + i] * 20091) >> 16));
-        int d1 = (b[4 + i] + ((b[4 + i] * 20091) >> 16)) + ((b[12 + i] * 35468) >> 16);
+        int c1 = (m24(b[4 + i], 35468) >> 16) - (b[12 + i] + (m24(b[12 + i], 20091) >> 16));
+        int d1 = (b[4 + i] + (m24(b[4 + i], 20091) >> 16)) + (m24(b[12 + i], 35468) >> 16);
         b[i] = a1 + d1;
         b[4 + i] = b1 + c1;
         b[12 + i] = a1 - d1;
@@ -146,8 +151,8 @@ DI void idct16(int* b)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         int a1 = b[4 * i] + b[4 * i + 2], b1 = b[4 * i] - b[4 * i + 2];
-        int c1 = ((b[4 * i + 1] * 35468) >> 16) - (b[4 * i + 3] + ((b[4 * i + 3] * 20091) >> 16));
-        int d1 = (b[4 * i + 1] + ((b[4 * i + 1] * 20091) >> 16)) + ((b[4 * i + 3] * 35468) >> 16);
+        int c1 = (m24(b[4 * i + 1], 35468) >> 16) - (b[4 * i + 3] + (m24(b[4 * i + 3], 20091) >> 16));
+        int d1 = (b[4 * i + 1] + (m24(b[4 * i + 1], 20091) >> 16)) + (m24(b[4 * i + 3], 35468) >> 16);
         b[4 * i] = (a1 + d1 + 4) >> 3;
         b[4 * i + 3] = (a1 - d1 + 4) >> 3;
         b[4 * i + 1] = (b1 + c1 + 4) >> 3;
@@ -373,34 +378,75 @@ DI void gcol(int t, int i, int& t0, int& t1, int& t2, int& t3)
     t3 = sel4(i, m1, p2, p1, t);
 }
 
-DI int fdct_g(int d, int k)
+DI int qrev(int v) { return DPP(v, 0x1B); }   // quad lane j <- 3-j
+DI int qnext(int v) { return DPP(v, 0x39); }  // quad lane j <- (j+1)&3
+DI int qprev(int v) { return DPP(v, 0x93); }  // quad lane j <- (j-1)&3
+DI int qxor2(int v) { return DPP(v, 0x4E); }  // quad lane j <- j^2
+DI int rrev(int v) { return DPP(DPP(v, 0x140), 0x1B); }  // row r <- 3-r, same column
+
+// dct4x4 (transform.rs:176) in butterfly form: every lane forms the partner
+// sum / difference (s, d) of its pair, then takes one value from the
+// neighbouring row / column -- ~35 VALU ops instead of a full gather.
+DI int fdct_g(int v, int k)
 {
     const int i = k >> 2, j = k & 3;
-    const int d0 = qb0(d), d1 = qb1(d), d2 = qb2(d), d3 = qb3(d);
-    const int a = (d0 + d3) * 8, bb = (d1 + d2) * 8, c = (d1 - d2) * 8, dd = (d0 - d3) * 8;
-    const int t = sel4(j, a + bb, (c * 2217 + dd * 5352 + 14500) >> 12, a - bb, (dd * 2217 - c * 5352 + 7500) >> 12);
-    int t0, t1, t2, t3;
-    gcol(t, i, t0, t1, t2, t3);
-    const int A = t0 + t3, B = t1 + t2, Cc = t1 - t2, D = t0 - t3;
-    return sel4(i, (A + B + 7) >> 4, ((Cc * 2217 + D * 5352 + 12000) >> 16) + (D != 0 ? 1 : 0), (A - B + 7) >> 4,
-                (D * 2217 - Cc * 5352 + 51000) >> 16);
+    // rows: pair columns j <-> 3-j
+    {
+        const int r = qrev(v);
+        const int s = v + r, d = v - r;              // col0: a/8, dd/8  col1: bb/8, c/8  col2: bb/8,-c/8  col3: a/8,-dd/8
+        const int X = qnext(s), Y = qprev(d);
+        const int ev = csel(j == 0, s + X, X - s) * 8;  // col0: a+bb  col2: a-bb
+        const int sg = csel(j == 1, 1, -1);
+        const int od = (Y * 8 * 5352 + sg * d * 8 * 2217 + csel(j == 1, 14500, 7500)) >> 12;
+        v = csel((j & 1) == 0, ev, od);
+    }
+    // columns: pair rows i <-> 3-i
+    {
+        const int r = rrev(v);
+        const int s = v + r, d = v - r;              // row0: A, D  row1: B, C  row2: B,-C  row3: A,-D
+        const int X = ror12(s), Y = ror4(d);          // row i+1 / row i-1
+        const int ev = (csel(i == 0, s + X, X - s) + 7) >> 4;
+        const int sg = csel(i == 1, 1, -1);
+        const int od = ((Y * 5352 + sg * d * 2217 + csel(i == 1, 12000, 51000)) >> 16) + (int)(i == 1 && Y != 0);
+        return csel((i & 1) == 0, ev, od);
+    }
 }
 
+// idct4x4 in butterfly form (same arithmetic as idct16).
 DI int idct_g(int x, int k)
 {
     const int i = k >> 2, j = k & 3;
-    int x0, x1, x2, x3;
-    gcol(x, i, x0, x1, x2, x3);
-    int a1 = x0 + x2, b1 = x0 - x2;
-    int c1 = ((x1 * 35468) >> 16) - (x3 + ((x3 * 20091) >> 16));
-    int d1 = (x1 + ((x1 * 20091) >> 16)) + ((x3 * 35468) >> 16);
-    const int t = sel4(i, a1 + d1, b1 + c1, b1 - c1, a1 - d1);
-    const int y0 = qb0(t), y1 = qb1(t), y2 = qb2(t), y3 = qb3(t);
-    a1 = y0 + y2;
-    b1 = y0 - y2;
-    c1 = ((y1 * 35468) >> 16) - (y3 + ((y3 * 20091) >> 16));
-    d1 = (y1 + ((y1 * 20091) >> 16)) + ((y3 * 35468) >> 16);
-    return sel4(j, (a1 + d1 + 4) >> 3, (b1 + c1 + 4) >> 3, (b1 - c1 + 4) >> 3, (a1 - d1 + 4) >> 3);
+    // vertical: rows i and i^2 pair up; even rows hold (a1, b1), odd rows (d1, c1)
+    {
+        const int o = ror8(x);                 // row i+2
+        const bool even = (i & 1) == 0;
+        const int x0 = csel(i == 0, x, o), x2 = csel(i == 0, o, x);      // even rows
+        const int x1 = csel(i == 1, x, o), x3 = csel(i == 1, o, x);      // odd rows
+        const int a1 = x0 + x2, b1 = x0 - x2;
+        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
+        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
+        const int p = csel(even, a1, d1), q = csel(even, b1, c1);
+        // row0 <- d1 (row1, i+1); row1 <- b1 (row0, i-1); row2 <- c1 (row3, i+1); row3 <- a1 (row2, i-1)
+        const int send = csel(i == 0 || i == 3, q, p);
+        const int nb = csel(even, ror12(send), ror4(send));
+        const int base = csel(i == 0 || i == 3, p, q);
+        x = csel(i == 3, -base, base) + csel(i == 2, -nb, nb);
+    }
+    // horizontal: columns j and j^2 pair up
+    {
+        const int o = qxor2(x);
+        const bool even = (j & 1) == 0;
+        const int y0 = csel(j == 0, x, o), y2 = csel(j == 0, o, x);
+        const int y1 = csel(j == 1, x, o), y3 = csel(j == 1, o, x);
+        const int a1 = y0 + y2, b1 = y0 - y2;
+        const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
+        const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
+        const int p = csel(even, a1, d1), q = csel(even, b1, c1);
+        const int send = csel(j == 0 || j == 3, q, p);
+        const int nb = csel(even, qnext(send), qprev(send));
+        const int base = csel(j == 0 || j == 3, p, q);
+        return (csel(j == 3, -base, base) + csel(j == 2, -nb, nb) + 4) >> 3;
+    }
 }
 
 // 16-bit nonzero mask of the lane's group.

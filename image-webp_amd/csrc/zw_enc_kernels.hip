@@ -531,7 +531,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
         for (int k = 0; k < 16; k++) y2q[k] = quantz(d[k], S.y2.iq[k > 0], S.y2.bias[k > 0]);
         W->y2cost[m] = (int)rcost<0>(y2q, 0, 1, C.T);
 #pragma unroll
-        for (int k = 0; k < 16; k++) d[k] = y2q[k] * (int)S.y2.q[k > 0];
+        for (int k = 0; k < 16; k++) d[k] = m24(y2q[k], (int)S.y2.q[k > 0]);
         iwht16(d);
 #pragma unroll
         for (int k = 0; k < 16; k++) W->y2d[m * 16 + k] = d[k];
@@ -540,7 +540,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     int dq[16];
     dq[0] = W->y2d[m * 16 + b];
 #pragma unroll
-    for (int k = 1; k < 16; k++) dq[k] = q[k] * (int)S.y1.q[1];
+    for (int k = 1; k < 16; k++) dq[k] = m24(q[k], (int)S.y1.q[1]);
     idct16(dq);
     int rec[16], sse = 0, flat = 1;
     const int s00 = C.sY[0];
@@ -818,7 +818,7 @@ __device__ int pick_uv(const Ctx& C)
         }
         int cost = (int)rcost<0>(q, 0, 2, C.T);
 #pragma unroll
-        for (int k = 0; k < 16; k++) r[k] = q[k] * (int)S.uv.q[k > 0];
+        for (int k = 0; k < 16; k++) r[k] = m24(q[k], (int)S.uv.q[k > 0]);
         idct16(r);
         int sse = 0;
 #pragma unroll
@@ -899,7 +899,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
 #pragma unroll
             for (int n = 0; n < 16; n++) W->lev[16][n] = (int16_t)y2q[kZZ(n)];
 #pragma unroll
-            for (int k = 0; k < 16; k++) d[k] = y2q[k] * (int)S.y2.q[k > 0];
+            for (int k = 0; k < 16; k++) d[k] = m24(y2q[k], (int)S.y2.q[k > 0]);
             iwht16(d);
 #pragma unroll
             for (int k = 0; k < 16; k++) W->y2d[k] = d[k];
@@ -961,7 +961,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             }
             dq[0] = 0;
 #pragma unroll
-            for (int n = 1; n < 16; n++) dq[kZZ(n)] = lv[n] * (int)S.y1.q[1];
+            for (int n = 1; n < 16; n++) dq[kZZ(n)] = m24(lv[n], (int)S.y1.q[1]);
         }
         wsync();
         if (l < 16) {
@@ -1028,7 +1028,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             } else {
                 if (l < 16) W->lev[i][izz_of(k)] = (int16_t)qs;
                 nzq = snz;
-                dqk = qs * (int)S.y1.q[k > 0];
+                dqk = m24(qs, (int)S.y1.q[k > 0]);
             }
             const int rk = idct_g(dqk, k);
             if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pk + rk);
@@ -1136,7 +1136,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
 #pragma unroll
         for (int n = 0; n < 16; n++) {
             W->lev[17 + b][n] = (int16_t)lv[n];
-            c[kZZ(n)] = lv[n] * (int)S.uv.q[kZZ(n) > 0];
+            c[kZZ(n)] = m24(lv[n], (int)S.uv.q[kZZ(n) > 0]);
         }
         idct16(c);
         uint8_t* w = pl ? W->cv : W->cu;
@@ -1482,7 +1482,7 @@ extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __re
 #pragma unroll
         for (int n = 0; n < 16; n++) {
             const int j = kZZ(n);
-            c[j] = n < a.first ? 0 : lv[n] * (int)a.m.q[j > 0];
+            c[j] = n < a.first ? 0 : m24(lv[n], (int)a.m.q[j > 0]);
         }
     }
 #pragma unroll

@@ -32,6 +32,8 @@ hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParam
                         int nframes);
 hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
                      unsigned long long* counter, unsigned long long* frame_info, uint8_t* out);
+hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m, int first,
+                          void* levels, void* recon, int cus);
 hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
                             const uint8_t* probs, const void* args, int* levels, int* dq);
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
@@ -843,6 +845,66 @@ extern "C" int zw_quant_blocks(zw_ctx* ctx, int n, const int32_t* coeffs, const 
                            (int*)(d + o_lv), (int*)(d + o_dq)));
     HIPOK(hipMemcpyAsync(levels, d + o_lv, cb, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(dequant, d + o_dq, cb, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming DCT+quant pass (zw_xform_kernels.hip)
+// ---------------------------------------------------------------------------
+static int make_matrix(ZwMatrix& m, int q_dc, int q_ac, int matrix_type)
+{
+    if (q_dc <= 0 || q_ac <= 0 || q_dc > 2048 || q_ac > 2048 || matrix_type < 0 || matrix_type > 2) return ZW_EINVAL;
+    static const uint32_t bdc[3] = {96, 96, 110}, bac[3] = {110, 108, 115};
+    m.q[0] = (uint32_t)q_dc;
+    m.q[1] = (uint32_t)q_ac;
+    for (int i = 0; i < 2; i++) {
+        const uint32_t b = i ? bac[matrix_type] : bdc[matrix_type];
+        m.iq[i] = (1u << 17) / m.q[i];
+        m.bias[i] = ((b << 17) + 128) >> 8;
+        m.zthresh[i] = ((1u << 17) - 1 - m.bias[i]) / m.iq[i];
+    }
+    return ZW_OK;
+}
+
+static int device_cus(int device)
+{
+    hipDeviceProp_t prop;
+    return hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
+}
+
+extern "C" int zw_transform_quant_blocks_device(zw_ctx* ctx, void* stream, size_t n, const void* d_src,
+                                                const void* d_pred, int q_dc, int q_ac, int matrix_type, int first,
+                                                void* d_levels, void* d_recon)
+{
+    if (!ctx || !d_src || !d_pred || !d_levels || !d_recon || (first != 0 && first != 1)) return ZW_EINVAL;
+    ZwMatrix m;
+    int r = make_matrix(m, q_dc, q_ac, matrix_type);
+    if (r) return r;
+    if (n == 0) return ZW_OK;
+    static const int cus = device_cus(ctx->device);
+    HIPOK(zwk_fdct_quant(stream ? (hipStream_t)stream : ctx_stream(ctx), d_src, d_pred, n, &m, first, d_levels, d_recon,
+                         cus));
+    return ZW_OK;
+}
+
+extern "C" int zw_transform_quant_blocks(zw_ctx* ctx, size_t n, const uint8_t* src, const uint8_t* pred, int q_dc,
+                                         int q_ac, int matrix_type, int first, int16_t* levels, uint8_t* recon)
+{
+    if (!ctx || (n && (!src || !pred || !levels || !recon))) return ZW_EINVAL;
+    if (n == 0) return ZW_OK;
+    HIPOK(hipSetDevice(ctx->device));
+    const size_t o_s = 0, o_p = n * 16, o_l = n * 32, o_r = n * 64, total = n * 80;
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx_stream(ctx);
+    HIPOK(hipMemcpyAsync(d + o_s, src, n * 16, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_p, pred, n * 16, hipMemcpyHostToDevice, s));
+    int r = zw_transform_quant_blocks_device(ctx, s, n, d + o_s, d + o_p, q_dc, q_ac, matrix_type, first, d + o_l,
+                                             d + o_r);
+    if (r) return r;
+    HIPOK(hipMemcpyAsync(levels, d + o_l, n * 32, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(recon, d + o_r, n * 16, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
     return ZW_OK;
 }

@@ -1,0 +1,191 @@
+// zw_xform_kernels.hip -- the streaming DCT+quant pass (SURVEY.md 8(a) a5/a7/a9/a10,
+// the arithmetic of transform_luma_block / transform_chroma_blocks,
+// encoder/vp8.rs:2647-2780, :3039-3121, with the prediction materialised):
+//
+//   residual = src - pred                         (u8 blocks)
+//   coeffs   = dct4x4(residual)                   transform.rs:176
+//   levels   = quantize_coeff(coeffs), zigzag     cost.rs:457
+//   recon    = clamp(pred + idct4x4(levels * q))  transform.rs:19, prediction.rs:138
+//
+// One thread per 4x4 block (4 blocks per thread per pass), block-major
+// streams: 16 B src + 16 B pred in, 32 B levels + 16 B recon out = 80 B of
+// compulsory HBM traffic per block against ~405 VALU instructions (packed i16
+// butterflies, v_dot2 rotations, 24-bit multiplies).  Bound by HBM.
+#include "zw_dev.h"
+#include <cstdlib>
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+struct XformArgs {
+    // [0] = DC, [1] = AC.  bp/bn: rounding bias for c >= 0 / c < 0 (see quant below).
+    // first == 1 zeroes the DC set (iq = bp = bn = 0 -> level 0).
+    int32_t iq[2], bp[2], bn[2], q[2];
+};
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+DI s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
+DI uint32_t as_u(s2 v) { return __builtin_bit_cast(uint32_t, v); }
+// VOP3P v_dot2_i32_i16 with the accumulator from an SGPR (the builtin selects
+// the VOP2 dot2c form, which needs a v_mov of the accumulator every time).
+DI int dot2(s2 a, s2 b, int c)
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+// (lo16(a), lo16(b)) packed
+DI uint32_t pack_lo(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+
+// One 4x4 block, packed-i16 form.  Residual rows are held as i16 pairs
+// (r0,r1),(r3,r2) so both butterfly stages are one v_pk_add/v_pk_sub each and
+// every rotation is one v_dot2_i32_i16 with the rounding folded in:
+//   pass 1: (8*(c*2217+d*5352)+14500)>>12 == (dot2((d,c),(10704,4434))+3625)>>10
+//           (8*(d*2217-c*5352)+ 7500)>>12 == (dot2((d,c),(4434,-10704))+1875)>>10
+//   pass 2: the reference constants as they stand.
+// Every pass-1 output and pass-2 butterfly fits i16 for residuals in
+// [-255,255] (tests/test_xform_algebra.py; GPU parity in test_gpu_parity.py).
+// quantize_coeff: sign(c)*((|c|*iq+bias)>>17) == (c*iq + (c<0 ? 2^17-1-bias : bias))>>17.
+__device__ __forceinline__ void xform_block(const v4u s4, const v4u p4, const XformArgs& a, v4u& l0, v4u& l1, v4u& r0)
+{
+    const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w}, pw[4] = {p4.x, p4.y, p4.z, p4.w};
+    uint32_t P01[4], P32[4];
+    int o[16];
+    const s2 k8p = {8, 8}, k8m = {8, -8}, k1a = {10704, 4434}, k1b = {4434, -10704};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        P01[i] = __builtin_amdgcn_perm(0u, pw[i], 0x0c010c00u);
+        P32[i] = __builtin_amdgcn_perm(0u, pw[i], 0x0c020c03u);
+        const s2 R01 = as_s2(__builtin_amdgcn_perm(0u, sw[i], 0x0c010c00u)) - as_s2(P01[i]);
+        const s2 R32 = as_s2(__builtin_amdgcn_perm(0u, sw[i], 0x0c020c03u)) - as_s2(P32[i]);
+        const s2 A = R01 + R32, D = R01 - R32;  // (a, b) / 8, (d, c) / 8
+        o[4 * i] = dot2(A, k8p, 0);
+        o[4 * i + 2] = dot2(A, k8m, 0);
+        o[4 * i + 1] = dot2(D, k1a, 3625) >> 10;
+        o[4 * i + 3] = dot2(D, k1b, 1875) >> 10;
+    }
+    const s2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+    int c[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const s2 X03 = as_s2(pack_lo(o[i], o[4 + i])), X32 = as_s2(pack_lo(o[12 + i], o[8 + i]));
+        const s2 A = X03 + X32, D = X03 - X32;  // (a, b), (d, c)
+        c[i] = dot2(A, k1p, 7) >> 4;
+        c[8 + i] = dot2(A, k1m, 7) >> 4;
+        c[4 + i] = (dot2(D, k2a, 12000) >> 16) + ((as_u(D) & 0xffffu) != 0u ? 1 : 0);
+        c[12 + i] = dot2(D, k2b, 51000) >> 16;
+    }
+    int lv[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int t = j > 0;
+        lv[j] = __mul24(c[j], a.iq[t]) + (c[j] < 0 ? a.bn[t] : a.bp[t]);
+        lv[j] >>= 17;
+        c[j] = __mul24(lv[j], a.q[t]);
+    }
+    uint32_t lw[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) lw[q] = pack_lo(lv[kZZ(2 * q)], lv[kZZ(2 * q + 1)]);
+    idct16(c);
+    uint32_t rw[4];
+    const s2 z = {0, 0}, m255 = {255, 255};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s2 A = as_s2(pack_lo(c[4 * i], c[4 * i + 1])) + as_s2(P01[i]);
+        s2 B = as_s2(pack_lo(c[4 * i + 3], c[4 * i + 2])) + as_s2(P32[i]);
+        A = __builtin_elementwise_min(__builtin_elementwise_max(A, z), m255);
+        B = __builtin_elementwise_min(__builtin_elementwise_max(B, z), m255);
+        rw[i] = __builtin_amdgcn_perm(as_u(B), as_u(A), 0x04060200u);
+    }
+    l0 = v4u{lw[0], lw[1], lw[2], lw[3]};
+    l1 = v4u{lw[4], lw[5], lw[6], lw[7]};
+    r0 = v4u{rw[0], rw[1], rw[2], rw[3]};
+}
+
+// V = blocks per thread per iteration (loads of all V blocks issued first); NT = non-temporal stores.
+template <int V, bool NT>
+__global__ __launch_bounds__(256) void k_fdct_quant_t(const v4u* __restrict__ src, const v4u* __restrict__ pred,
+                                                      size_t n, XformArgs a, v4u* __restrict__ levels,
+                                                      v4u* __restrict__ recon)
+{
+    const size_t stride = (size_t)gridDim.x * 256 * V;
+    for (size_t b0 = (size_t)blockIdx.x * 256 * V + threadIdx.x; b0 < n; b0 += stride) {
+        v4u s4[V], p4[V];
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const size_t b = b0 + (size_t)u * 256;
+            if (b < n) {
+                s4[u] = __builtin_nontemporal_load(&src[b]);
+                p4[u] = __builtin_nontemporal_load(&pred[b]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const size_t b = b0 + (size_t)u * 256;
+            if (b < n) {
+                v4u l0, l1, r0;
+                xform_block(s4[u], p4[u], a, l0, l1, r0);
+                if (NT) {
+                    __builtin_nontemporal_store(l0, &levels[2 * b]);
+                    __builtin_nontemporal_store(l1, &levels[2 * b + 1]);
+                    __builtin_nontemporal_store(r0, &recon[b]);
+                } else {
+                    levels[2 * b] = l0;
+                    levels[2 * b + 1] = l1;
+                    recon[b] = r0;
+                }
+            }
+        }
+    }
+}
+
+// Same traffic shape with no arithmetic (calibration of the read:write mix).
+__global__ __launch_bounds__(256) void k_fdct_quant_copy(const v4u* __restrict__ src, const v4u* __restrict__ pred,
+                                                         size_t n, XformArgs a, v4u* __restrict__ levels,
+                                                         v4u* __restrict__ recon)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t b = (size_t)blockIdx.x * 256 + threadIdx.x; b < n; b += stride) {
+        const v4u s4 = __builtin_nontemporal_load(&src[b]), p4 = __builtin_nontemporal_load(&pred[b]);
+        levels[2 * b] = s4 + p4;
+        levels[2 * b + 1] = s4 - p4;
+        recon[b] = s4 ^ p4;
+    }
+}
+
+extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m,
+                                     int first, void* levels, void* recon, int cus)
+{
+    XformArgs a;
+    for (int t = 0; t < 2; t++) {
+        const bool off = t == 0 && first;
+        a.iq[t] = off ? 0 : (int32_t)m->iq[t];
+        a.bp[t] = off ? 0 : (int32_t)m->bias[t];
+        a.bn[t] = off ? 0 : (int32_t)((1u << 17) - 1 - m->bias[t]);
+        a.q[t] = (int32_t)m->q[t];
+    }
+    // Tuning knobs (defaults are the measured best on MI355X: 4 blocks per
+    // thread, non-temporal stores, one pass over the data -- no grid-stride cap).
+    //   ZW_XFORM_VARIANT  0: V1 nt  1: V2 nt  2: V1  3: V2  4: V4  5: V4 nt (default)
+    //                     99: same traffic, no arithmetic (bandwidth calibration only)
+    //   ZW_XFORM_GRID     cap on workgroups, as a multiple of the CU count
+    static const int variant = getenv("ZW_XFORM_VARIANT") ? atoi(getenv("ZW_XFORM_VARIANT")) : 5;
+    static const int gmul = getenv("ZW_XFORM_GRID") ? atoi(getenv("ZW_XFORM_GRID")) : 1 << 20;
+    const int V = variant == 99 ? 1 : (variant >= 4 ? 4 : ((variant & 1) ? 2 : 1));
+    size_t grid = (n + 256 * V - 1) / (256 * V);
+    const size_t cap = (size_t)(cus > 0 ? cus : 256) * gmul;
+    if (grid > cap) grid = cap;
+    if (grid == 0) grid = 1;
+    const dim3 g((unsigned)grid), blk(256);
+    const v4u *sp = (const v4u*)src, *pp = (const v4u*)pred;
+    v4u *lp = (v4u*)levels, *rp = (v4u*)recon;
+    switch (variant) {
+    case 0: hipLaunchKernelGGL((k_fdct_quant_t<1, true>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 1: hipLaunchKernelGGL((k_fdct_quant_t<2, true>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 2: hipLaunchKernelGGL((k_fdct_quant_t<1, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 3: hipLaunchKernelGGL((k_fdct_quant_t<2, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 4: hipLaunchKernelGGL((k_fdct_quant_t<4, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 99: hipLaunchKernelGGL(k_fdct_quant_copy, g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    default: hipLaunchKernelGGL((k_fdct_quant_t<4, true>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    }
+    return hipGetLastError();
+}

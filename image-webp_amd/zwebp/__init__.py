@@ -27,7 +27,7 @@ import numpy as np
 __all__ = [
     "ColorType", "EncoderParams", "WebPEncoder", "ZwError", "EncodingError", "DecodingError", "Context",
     "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
-    "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "library_path", "load_library",
+    "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "transform_quant_blocks", "library_path", "load_library",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -101,6 +101,8 @@ SIGNATURES = [
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
     ("zw_rgb_to_yuv420", _I, [_VP, _VP, _U32, _U32, _I, _VP, _VP, _VP]),
+    ("zw_transform_quant_blocks", _I, [_VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
+    ("zw_transform_quant_blocks_device", _I, [_VP, _VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
     ("zw_quant_blocks", _I, [_VP, _I, _VP, _VP, _I, _I, _I, _U32, _I, _I, _I, _VP, _VP, _VP]),
     ("zw_loop_filter_frame", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I]),
     ("zw_pipe_create", _I, [_VP, _I, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_VP)]),
@@ -348,6 +350,30 @@ def quant_blocks(coeffs, ctx0, ctype, first, use_trellis, lambda_, q_dc, q_ac, m
     _check(c._lib.zw_quant_blocks(c.handle, n, _ptr(co), _ptr(cx), ctype, first, 1 if use_trellis else 0, lambda_,
                                   q_dc, q_ac, matrix_type, _ptr(pr), _ptr(lv), _ptr(dq)), "quant_blocks")
     return lv, dq
+
+
+def transform_quant_blocks(src, pred, q_dc, q_ac, matrix_type=0, first=0, ctx=None):
+    """Streaming DCT+quant pass on (n,16) u8 source/prediction blocks.
+
+    Returns (levels (n,16) int16 zigzag, recon (n,16) uint8)."""
+    c = _ctx(ctx)
+    s = np.ascontiguousarray(src, dtype=np.uint8).reshape(-1, 16)
+    p = np.ascontiguousarray(pred, dtype=np.uint8).reshape(-1, 16)
+    assert s.shape == p.shape
+    n = s.shape[0]
+    lv = np.zeros((n, 16), np.int16)
+    rc = np.zeros((n, 16), np.uint8)
+    _check(c._lib.zw_transform_quant_blocks(c.handle, n, _ptr(s), _ptr(p), q_dc, q_ac, matrix_type, first,
+                                            _ptr(lv), _ptr(rc)), "transform_quant_blocks")
+    return lv, rc
+
+
+def transform_quant_blocks_device(n, d_src, d_pred, q_dc, q_ac, matrix_type, first, d_levels, d_recon, stream=None,
+                                  ctx=None):
+    """Device-pointer form (e.g. torch tensor .data_ptr()); asynchronous on `stream` (int handle or None)."""
+    c = _ctx(ctx)
+    _check(c._lib.zw_transform_quant_blocks_device(c.handle, stream, n, d_src, d_pred, q_dc, q_ac, matrix_type, first,
+                                                   d_levels, d_recon), "transform_quant_blocks_device")
 
 
 def loop_filter_frame(y, u, v, mbw, mbh, mb_flags, filter_type, filter_level, sharpness, segments_enabled=0,

@@ -109,6 +109,20 @@ int zw_rgb_to_yuv420(zw_ctx *ctx, const uint8_t *img, uint32_t width, uint32_t h
 int zw_quant_blocks(zw_ctx *ctx, int n, const int32_t *coeffs, const uint8_t *ctx0, int ctype, int first,
                     int use_trellis, uint32_t lambda, int q_dc, int q_ac, int matrix_type, const uint8_t *probs,
                     int32_t *levels, int32_t *dequant);
+/* Streaming DCT+quant pass ("transform + quant + recon" of transform_luma_block
+ * / transform_chroma_blocks, encoder/vp8.rs:2647-2780 and :3039-3121, with the
+ * prediction materialised): for n 4x4 blocks, block-major u8 source and
+ * prediction (16 B each, raster order in the block) ->
+ *   levels[n][16] int16, zigzag: quantize_coeff(dct4x4(src - pred)) (cost.rs:457;
+ *                 positions < first are 0, first = 1 for I16 AC blocks)
+ *   recon[n][16]  u8: clamp(pred + idct4x4(dequantised levels)).
+ * matrix_type 0 Y1, 1 Y2, 2 UV selects the rounding biases (cost.rs:402-406). */
+int zw_transform_quant_blocks(zw_ctx *ctx, size_t n, const uint8_t *src, const uint8_t *pred, int q_dc, int q_ac,
+                              int matrix_type, int first, int16_t *levels, uint8_t *recon);
+/* Same on device pointers, enqueued on `stream` (a hipStream_t; NULL = the
+ * context's stream), asynchronous. */
+int zw_transform_quant_blocks_device(zw_ctx *ctx, void *stream, size_t n, const void *d_src, const void *d_pred,
+                                     int q_dc, int q_ac, int matrix_type, int first, void *d_levels, void *d_recon);
 /* In-place loop filter of MB-aligned planes; per-MB flags (luma_mode 0..4,
  * segment, skip, non_zero_dct) as 4 bytes per MB, raster order. */
 int zw_loop_filter_frame(zw_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, uint32_t mbw, uint32_t mbh,

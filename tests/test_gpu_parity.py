@@ -341,3 +341,32 @@ def test_quant_blocks(ctx, ctype, first, mtype, trel, qi):
         assert bad.size == 0, f"{bad.size} blocks differ; first {co[bad[0]].tolist()} ctx {ctx0[bad[0]]}: " \
                               f"{g[0][bad[0]].tolist()} vs {o[0][bad[0]].tolist()}"
         assert np.array_equal(g[1], o[1])
+
+
+# --------------------------------------------------------------------------
+# a5/a7/a9/a10: the streaming DCT+quant pass (materialised prediction)
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("q_dc,q_ac,mtype,first", [(24, 30, 0, 0), (24, 30, 0, 1), (48, 46, 1, 0), (24, 30, 2, 0),
+                                                   (4, 4, 0, 0), (157, 284, 2, 0), (13, 13, 0, 1)])
+def test_transform_quant_blocks(ctx, q_dc, q_ac, mtype, first):
+    rng = np.random.default_rng(q_dc * 7 + q_ac + mtype + first)
+    n = 40000
+    base = rng.integers(0, 256, (n, 1))
+    src = np.clip(base + rng.integers(-40, 41, (n, 16)), 0, 255).astype(np.uint8)
+    src[: n // 8] = rng.integers(0, 256, (n // 8, 16)).astype(np.uint8)  # full-range residuals
+    pred = np.clip(base + rng.integers(-20, 21, (n, 16)), 0, 255).astype(np.uint8)
+    # extreme residuals (+-255 patterns): the i16 headroom of the packed butterflies
+    ext = slice(n // 8, n // 4)
+    src[ext] = rng.choice(np.array([0, 255], np.uint8), (n // 8, 16))
+    pred[ext] = np.where(rng.random((n // 8, 16)) < 0.9, 255 - src[ext], src[ext])
+    lv, rc = zwebp.transform_quant_blocks(src, pred, q_dc, q_ac, mtype, first, ctx=ctx)
+    co = O.blocks("or_fdct_c", src.astype(np.int32) - pred.astype(np.int32))
+    olv, odq = O.quant_blocks(co, 0, 3, first, False, 0, q_dc, q_ac, mtype)
+    orc = np.clip(pred.astype(np.int32) + O.blocks("or_idct_c", odq).reshape(n, 16), 0, 255)
+    assert np.array_equal(lv.astype(np.int32), olv)
+    assert np.array_equal(rc.astype(np.int32), orc)
+
+
+def test_transform_quant_blocks_empty(ctx):
+    lv, rc = zwebp.transform_quant_blocks(np.zeros((0, 16), np.uint8), np.zeros((0, 16), np.uint8), 24, 30, ctx=ctx)
+    assert lv.shape == (0, 16)
