@@ -396,8 +396,7 @@ DI int fdct_g(int v, int k)
         const int s = v + r, d = v - r;              // col0: a/8, dd/8  col1: bb/8, c/8  col2: bb/8,-c/8  col3: a/8,-dd/8
         const int X = qnext(s), Y = qprev(d);
         const int ev = csel(j == 0, s + X, X - s) * 8;  // col0: a+bb  col2: a-bb
-        const int sg = csel(j == 1, 1, -1);
-        const int od = (Y * 8 * 5352 + sg * d * 8 * 2217 + csel(j == 1, 14500, 7500)) >> 12;
+        const int od = (m24(Y, 8 * 5352) + m24(d, csel(j == 1, 8 * 2217, -8 * 2217)) + csel(j == 1, 14500, 7500)) >> 12;
         v = csel((j & 1) == 0, ev, od);
     }
     // columns: pair rows i <-> 3-i
@@ -406,8 +405,8 @@ DI int fdct_g(int v, int k)
         const int s = v + r, d = v - r;              // row0: A, D  row1: B, C  row2: B,-C  row3: A,-D
         const int X = ror12(s), Y = ror4(d);          // row i+1 / row i-1
         const int ev = (csel(i == 0, s + X, X - s) + 7) >> 4;
-        const int sg = csel(i == 1, 1, -1);
-        const int od = ((Y * 5352 + sg * d * 2217 + csel(i == 1, 12000, 51000)) >> 16) + (int)(i == 1 && Y != 0);
+        const int od = ((m24(Y, 5352) + m24(d, csel(i == 1, 2217, -2217)) + csel(i == 1, 12000, 51000)) >> 16) +
+                       (int)(i == 1 && Y != 0);
         return csel((i & 1) == 0, ev, od);
     }
 }

@@ -607,6 +607,11 @@ extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
     }
     return 0;
 }
+#elif defined(ZW_ASM_MARKS)
+// ISA inspection builds: phase boundaries as assembly comments
+#define PH_START() asm volatile("; ZWMARK start" ::: "memory")
+#define PH_MARK(k) asm volatile("; ZWMARK " #k ::: "memory")
+#define PH_MARK_L(k, ln, ps) asm volatile("; ZWMARK " #k ::: "memory")
 #else
 #define PH_START() (void)0
 #define PH_MARK(k) (void)0
@@ -646,13 +651,18 @@ __device__ void i4_values(const Ctx& C, int x0, int y0)
     if (l == 0) W->V[38] = (dsum + 4) >> 3;
     wsync();
 }
-__device__ __forceinline__ int i4_pred_px(const WaveLds* W, const LdsTables* T, int mode, int p)
+// V index of pixel p under I4 mode `mode`, with bit 8 set for TrueMotion
+// (pred = clamp(V[ia] + V[5 + col] - V[4])).  Sub-block independent.
+__device__ __forceinline__ int i4_src_index(const LdsTables* T, int mode, int p)
 {
     const int idx = T->i4idx[mode][p];
     const bool tm = idx == 254;
-    const int ia = csel(tm, 3 - (p >> 2), csel(idx == 255, 38, idx));
-    const int va = W->V[ia], vb = W->V[5 + (p & 3)], vc = W->V[4];
-    return csel(tm, clamp255(va + vb - vc), va);
+    return csel(tm, 256 + 3 - (p >> 2), csel(idx == 255, 38, idx));
+}
+__device__ __forceinline__ int i4_pred_at(const WaveLds* W, int sidx, int vbc)
+{
+    const int va = W->V[sidx & 255];
+    return csel(sidx >= 256, clamp255(va + vbc), va);
 }
 
 __device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rate, uint32_t lambda)
@@ -661,8 +671,13 @@ __device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rat
 }
 
 // pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
-// Per sub-block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8),
-// ranking on the scalar unit, top-K candidates 16 lanes each (quirk A12 order).
+// Per sub-block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8);
+// stable ascending SSE rank (quirk A12) computed lane-parallel (lane m ranks
+// mode m against the ten keys sse*16+m held in SGPRs); the top-K candidates
+// are evaluated 16 lanes each and the winner chosen on the scalar unit.
+// Within one sub-block every candidate score sse*256 + u16(rate)*lambda_i4 is
+// below 2^29 (sse <= 16*255^2, lambda_i4 <= 1785), so score*4 + group is a
+// unique 32-bit key whose minimum is the reference's first strict minimum.
 __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
 {
     WaveLds* W = C.W;
@@ -672,52 +687,56 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
     const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
     const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
     const int qk = (int)S.y1.q[k > 0];
+    const uint32_t lam = S.l_i4;
     unsigned long long running = 211ull * S.l_mode;
     uint32_t total_mc = 0;
     unsigned long long mpack = 0;  // chosen sub-modes, 4 bits each
-    int top_nz[4] = {0, 0, 0, 0}, left_nz[4] = {0, 0, 0, 0};
+    uint32_t tnz = 0, lnz = 0;     // nonzero flags of the chosen blocks: bit sbx / bit sby
+    const int si0 = i4_src_index(T, g, k), si1 = i4_src_index(T, g + 4, k), si2 = i4_src_index(T, g < 2 ? g + 8 : 0, k);
     for (int i = 0; i < 16; i++) {
         const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
         const int tctx = sby == 0 ? 0 : (int)((mpack >> (4 * (i - 4))) & 15);
         const int lctx = sbx == 0 ? 0 : (int)((mpack >> (4 * (i - 1))) & 15);
-        const int nzt = sby == 0 ? 0 : top_nz[sbx];
-        const int nzl = sbx == 0 ? 0 : left_nz[sby];
+        const int nzc = (sby == 0 ? 0 : (int)((tnz >> sbx) & 1)) + (sbx == 0 ? 0 : (int)((lnz >> sby) & 1));
         PH_START();
         i4_values(C, x0, y0);
         PH_MARK_L(10, l, 0);
         const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
         int e0, e1, e2;
         {
-            int v = i4_pred_px(W, T, g, k);
+            const int vbc = W->V[5 + (k & 3)] - W->V[4];
+            int v = i4_pred_at(W, si0, vbc);
             W->pred[g][k] = (uint8_t)v;
-            e0 = red16((svk - v) * (svk - v));
-            v = i4_pred_px(W, T, g + 4, k);
+            e0 = red16(m24(svk - v, svk - v));
+            v = i4_pred_at(W, si1, vbc);
             W->pred[g + 4][k] = (uint8_t)v;
-            e1 = red16((svk - v) * (svk - v));
-            v = i4_pred_px(W, T, g < 2 ? g + 8 : 0, k);
+            e1 = red16(m24(svk - v, svk - v));
+            v = i4_pred_at(W, si2, vbc);
             if (g < 2) W->pred[g + 8][k] = (uint8_t)v;
-            e2 = red16((svk - v) * (svk - v));
+            e2 = red16(m24(svk - v, svk - v));
         }
-        // stable ascending rank of the 10 SSEs (ties by mode index), on SGPRs
-        uint32_t se[10];
+        // unique keys sse*16 + m (sse < 2^21) -> rank = #smaller keys
+        uint32_t key[10];
 #pragma unroll
         for (int m = 0; m < 10; m++) {
             const int ev = m < 4 ? e0 : (m < 8 ? e1 : e2);
-            se[m] = (uint32_t)__builtin_amdgcn_readlane(ev, (m & 3) * 16);
+            key[m] = ((uint32_t)__builtin_amdgcn_readlane(ev, (m & 3) * 16) << 4) | (uint32_t)m;
         }
+        uint32_t mykey = 0xffffffffu;
+#pragma unroll
+        for (int m = 0; m < 10; m++) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(mykey) : "s"(key[m]), "i"(m));
+        int rank = 0;
+#pragma unroll
+        for (int m = 0; m < 10; m++) rank += (int)(key[m] < mykey);
         unsigned long long cpack = 0;  // candidate c -> mode, 4 bits each
-#pragma unroll
-        for (int m = 0; m < 10; m++) {
-            int r = 0;
-#pragma unroll
-            for (int o = 0; o < 10; o++) r += (se[o] < se[m]) || (se[o] == se[m] && o < m);
-            cpack |= (unsigned long long)m << (4 * r);
+        for (int c = 0; c < K; c++) {
+            const unsigned long long bm = __ballot(rank == c && l < 10);
+            cpack |= (unsigned long long)__builtin_ctzll(bm) << (4 * c);
         }
         wsync();
         PH_MARK_L(11, l, 0);
-        unsigned long long bsc = ~0ull;
-        uint32_t bsse = 0, brate = 0;
-        int bmode = 0, bnz = 0, bdq = 0, bpk = 0;
+        uint32_t bsc = 0xffffffffu, bsse = 0, brate = 0;
+        int bmode = 0, bnz = 0, brv = 0;
         for (int base = 0; base < K; base += 4) {
             const int c = base + g;
             const bool act = c < K;
@@ -726,44 +745,38 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
             const int r = fdct_g(svk - pk, k);
             const int qv = quantz(r, iqk, biask);
             const unsigned nzm = gmask(qv != 0);
-            const uint32_t cc = rcost_g<0>(qv, k, nzt + nzl, 3, T);
-            const int dq = idct_g(qv * qk, k);
-            const int d = svk - clamp255(pk + dq);
+            const uint32_t cc = rcost_g<0>(qv, k, nzc, 3, T);
+            const int dq = idct_g(m24(qv, qk), k);
+            const int rv = clamp255(pk + dq);
+            const int d = svk - rv;
             const uint32_t sse = (uint32_t)red16(d * d);
             const uint32_t rate = (uint32_t)T->fci4[tctx][lctx][mm] + cc;
-            const unsigned long long sc = rdscore(sse, rate, S.l_i4);
-            // best of this round's groups in rank order (strict <), all in VGPRs
-            const unsigned slo = (unsigned)sc, shi = (unsigned)(sc >> 32);
-            int bg = -1;
-#pragma unroll
-            for (int gg = 0; gg < 4; gg++) {
-                const unsigned long long sg =
-                    ((unsigned long long)(unsigned)__shfl((int)shi, gg * 16) << 32) | (unsigned)__shfl((int)slo, gg * 16);
-                if (base + gg < K && sg < bsc) {
-                    bsc = sg;
-                    bg = gg;
-                }
-            }
-            if (bg >= 0) {
-                const int src = bg * 16;
-                bsse = (uint32_t)__shfl((int)sse, src);
-                brate = (uint32_t)__shfl((int)rate, src);
-                bnz = __shfl((int)(nzm != 0), src);
+            const uint32_t sc = sse * 256u + (rate & 0xffffu) * lam;
+            const uint32_t kv = act ? sc * 4u + (uint32_t)g : 0xffffffffu;
+            uint32_t kmin = (uint32_t)__builtin_amdgcn_readlane((int)kv, 0);
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 16));
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 32));
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 48));
+            if ((kmin >> 2) < bsc) {  // strict: earlier rounds keep ties
+                const int bg = (int)(kmin & 3u), src = bg * 16;
+                bsc = kmin >> 2;
+                bsse = (uint32_t)__builtin_amdgcn_readlane((int)sse, src);
+                brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, src);
+                bnz = __builtin_amdgcn_readlane((int)(nzm != 0), src);
                 bmode = (int)((cpack >> (4 * (base + bg))) & 15);
-                bdq = __shfl(dq, src + k);
-                bpk = __shfl(pk, src + k);
+                brv = __shfl(rv, src + k);
             }
         }
         PH_MARK_L(12, l, 0);
-        top_nz[sbx] = bnz;
-        left_nz[sby] = bnz;
+        tnz = (tnz & ~(1u << sbx)) | ((uint32_t)bnz << sbx);
+        lnz = (lnz & ~(1u << sby)) | ((uint32_t)bnz << sby);
         total_mc += T->fci4[tctx][lctx][bmode];
         running += rdscore(bsse, brate, S.l_mode);
         mpack |= (unsigned long long)bmode << (4 * i);
         if (l == 0) W->modes[i] = (uint8_t)bmode;
         if (running >= i16_score) { wsync(); return false; }
         if (total_mc > 256u * 16u * 16u / 4u) { wsync(); return false; }
-        if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(bpk + bdq);
+        if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)brv;
         wsync();
         PH_MARK_L(13, l, 0);
     }
@@ -992,7 +1005,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             i4_values(C, x0, y0);
             // 16-lane group form: every group computes the same block; group 0 stores
             const int k = l & 15;
-            const int pk = i4_pred_px(W, C.T, bm, k);
+            const int pk = i4_pred_at(W, i4_src_index(C.T, bm, k), W->V[5 + (k & 3)] - W->V[4]);
             const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
             const int ck = fdct_g(svk - pk, k);
             const int ctx0 = min(left_nz[sby] + top_nz[sbx], 2);
