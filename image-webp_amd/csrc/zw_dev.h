@@ -82,13 +82,6 @@ DI int wave_sum(int v)
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
-DI int red8(int v)
-{
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 1);
-    return v;
-}
 DI long long shfl64(long long v, int src)
 {
     int lo = __shfl((int)(v & 0xffffffff), src);
@@ -581,4 +574,127 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
         }
     }
     return nz;
+}
+
+// ---------------------------------------------------------------------------
+// Full-block lane forms: one lane holds a whole 4x4 block (16 values).
+// ---------------------------------------------------------------------------
+DI int red8(int v)  // sum within aligned 8-lane groups (DPP), result in every lane
+{
+    v += DPP(v, 0xB1);   // quad xor 1
+    v += DPP(v, 0x4E);   // quad xor 2
+    v += DPP(v, 0x141);  // row half mirror (lane i <-> 7-i)
+    return v;
+}
+
+typedef short zs2 __attribute__((ext_vector_type(2)));
+DI zs2 as_zs2(uint32_t v) { return __builtin_bit_cast(zs2, v); }
+DI uint32_t as_zu(zs2 v) { return __builtin_bit_cast(uint32_t, v); }
+// (lo16(a), lo16(b)) packed
+DI uint32_t pack_lo(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+// VOP3P v_dot2_i32_i16, accumulator from an SGPR (the builtin selects the VOP2
+// dot2c form, which costs a v_mov of the accumulator every time)
+DI int dot2(zs2 a, zs2 b, int c)
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+
+// dct4x4 (transform.rs:176) of one block of residuals r[16] (|r| <= 255) in
+// packed-i16 form: rows as pairs (r0,r1),(r3,r2), butterflies v_pk_add/sub,
+// rotations v_dot2 with the rounding folded in (see zw_xform_kernels.hip).
+DI void fdct16_pk(const int* r, int* c)
+{
+    const zs2 k8p = {8, 8}, k8m = {8, -8}, k1a = {10704, 4434}, k1b = {4434, -10704};
+    int o[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const zs2 R01 = as_zs2(pack_lo(r[4 * i], r[4 * i + 1])), R32 = as_zs2(pack_lo(r[4 * i + 3], r[4 * i + 2]));
+        const zs2 A = R01 + R32, D = R01 - R32;
+        o[4 * i] = dot2(A, k8p, 0);
+        o[4 * i + 2] = dot2(A, k8m, 0);
+        o[4 * i + 1] = dot2(D, k1a, 3625) >> 10;
+        o[4 * i + 3] = dot2(D, k1b, 1875) >> 10;
+    }
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const zs2 X01 = as_zs2(pack_lo(o[i], o[4 + i])), X32 = as_zs2(pack_lo(o[12 + i], o[8 + i]));
+        const zs2 A = X01 + X32, D = X01 - X32;
+        c[i] = dot2(A, k1p, 7) >> 4;
+        c[8 + i] = dot2(A, k1m, 7) >> 4;
+        c[4 + i] = (dot2(D, k2a, 12000) >> 16) + ((as_zu(D) & 0xffffu) != 0u ? 1 : 0);
+        c[12 + i] = dot2(D, k2b, 51000) >> 16;
+    }
+}
+
+// rcost<FIRST> (get_residual_cost, cost.rs:1670) without branches: every
+// table lookup is issued, terms past the last nonzero are masked.  v[n] is
+// indexed by position n exactly as rcost (quirk A1); av[n] = |v[n]|.
+template <int FIRST>
+DI uint32_t rcost_bf(const int* av, int ctx0, int ctype, const LdsTables* T)
+{
+    uint32_t nzm = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) nzm |= (uint32_t)min(av[n], 1) << n;
+    const int last = 31 - __clz((int)nzm);  // -1 when nzm == 0 (clz(0) == 32)
+    const int p0 = T->probs[ctype][kBand(FIRST)][ctx0][0];
+    uint32_t cost = 0;
+#pragma unroll
+    for (int n = FIRST; n < 16; n++) {
+        const int ctx = n == FIRST ? ctx0 : min(av[n - 1], 2);
+        const int t = T->lfc[min(av[n], 2047)] + T->lc[ctype][kBand(n)][ctx][min(av[n], 67)];
+        cost += (uint32_t)(t & -(int)(n <= last));
+    }
+    int lastv = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) lastv = n == last ? av[n] : lastv;
+    const int ctx_t = last >= FIRST ? min(lastv, 2) : ctx0;  // the loop's final ctx
+    const uint32_t tail =
+        bitcost(T, 0, T->probs[ctype][band_of(min(last + 1, 15))][ctx_t][0]) & -(uint32_t)(last < 15);
+    const uint32_t head = ctx0 == 0 ? bitcost(T, 1, p0) : 0u;
+    return last < 0 ? bitcost(T, 0, p0) : head + cost + tail;
+}
+
+DI int dot2sv(zs2 a, zs2 b_uniform, int acc)  // v_dot2_i32_i16 with the multiplier pair in an SGPR
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b_uniform), "v"(acc));
+    return d;
+}
+
+// sum_k kWY(k) * (|T(a)_k| - |T(b)_k|) for the TDisto 4x4 Hadamard T
+// (ttransform) of two blocks at once: a in the low and b in the high i16 half
+// of every register, so each butterfly is one packed op and each weighted
+// |coefficient| difference one v_dot2 against (w, -w).  |T(.)| <= 4080.
+DI int ttransform_diff_pk(const int* a, const int* b)
+{
+    zs2 t[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const zs2 r0 = as_zs2(pack_lo(a[4 * i], b[4 * i])), r1 = as_zs2(pack_lo(a[4 * i + 1], b[4 * i + 1]));
+        const zs2 r2 = as_zs2(pack_lo(a[4 * i + 2], b[4 * i + 2])), r3 = as_zs2(pack_lo(a[4 * i + 3], b[4 * i + 3]));
+        const zs2 a0 = r0 + r2, a1 = r1 + r3, a2 = r1 - r3, a3 = r0 - r2;
+        t[4 * i] = a0 + a1;
+        t[4 * i + 1] = a3 + a2;
+        t[4 * i + 2] = a3 - a2;
+        t[4 * i + 3] = a0 - a1;
+    }
+    int acc = 0;
+    const zs2 z = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const zs2 a0 = t[i] + t[8 + i], a1 = t[4 + i] + t[12 + i];
+        const zs2 a2 = t[4 + i] - t[12 + i], a3 = t[i] - t[8 + i];
+        const zs2 o[4] = {a0 + a1, a3 + a2, a3 - a2, a0 - a1};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const zs2 ab = __builtin_elementwise_max(o[r], z - o[r]);
+            const short w = (short)kWY(4 * r + i);
+            const zs2 wp = {w, (short)-w};
+            acc = dot2sv(ab, wp, acc);
+        }
+    }
+    return acc;
 }

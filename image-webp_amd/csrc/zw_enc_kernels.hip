@@ -16,7 +16,10 @@
 // and runs on wave 0 while waves 1..NW-1 do the luma wavefront.
 #include "zw_dev.h"
 
-#define NW 8
+#ifndef ZW_NW
+#define ZW_NW 8
+#endif
+#define NW ZW_NW
 #define WG (NW * 64)
 
 // ---------------------------------------------------------------------------
@@ -488,59 +491,72 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     WaveLds* W = C.W;
     const uint8_t* ws = W->ws;
     const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
     const int above = C.mby != 0, left = C.mbx != 0;
-    int s = 0;
-    if (lane < 16) s = above ? ws[1 + lane] : 0;
-    else if (lane < 32) s = left ? ws[(lane - 15) * ZW_BPS] : 0;
-    s = wave_sum(s);
-    const int shf = 3 + above + left;
-    const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
-    int src[16], pr[16], r[16];
-    const int P0 = ws[0];
+    int dcv;
+    {  // DC predictor: lanes 0..15 top row, 16..31 left column
+        const int top = lane < 16;
+        const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(lane < 32 && (top ? above : left));
+        const int sum = red16(v);
+        const int s = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
+        const int shf = 3 + above + left;
+        dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
+    }
+    int src[16], pr[16], r[16], c[16];
+    {
+        const int P0 = ws[0];
+        int L[4], Tp[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int y = by * 4 + i, x = bx * 4 + j;
-            const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
-            int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - P0)));
-            const int sv = C.sY[y * 16 + x];
-            src[i * 4 + j] = sv;
-            pr[i * 4 + j] = p;
-            r[i * 4 + j] = sv - p;
+        for (int i = 0; i < 4; i++) {
+            L[i] = ws[(by * 4 + i + 1) * ZW_BPS];
+            Tp[i] = ws[1 + bx * 4 + i];
         }
-    fdct16(r);
-    W->dc[m * 16 + b] = r[0];
-    int q[16];
-    q[0] = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t srow = *(const uint32_t*)(C.sY + (by * 4 + i) * 16 + bx * 4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int p = sel4(m, dcv, Tp[j], L[i], clamp255(L[i] + Tp[j] - P0));
+                const int sv = (int)((srow >> (8 * j)) & 255u);
+                src[i * 4 + j] = sv;
+                pr[i * 4 + j] = p;
+                r[i * 4 + j] = sv - p;
+            }
+        }
+    }
+    fdct16_pk(r, c);
+    W->dc[m * 16 + b] = c[0];
+    int aq[16], dq[16];
+    aq[0] = 0;
     int nzac = 0;
 #pragma unroll
     for (int k = 1; k < 16; k++) {
-        q[k] = quantz(r[k], S.y1.iq[1], S.y1.bias[1]);
-        nzac |= q[k] != 0;
+        aq[k] = (int)((__umul24((uint32_t)iabs(c[k]), S.y1.iq[1]) + S.y1.bias[1]) >> 17);
+        nzac |= aq[k];
+        dq[k] = m24(c[k] < 0 ? -aq[k] : aq[k], (int)S.y1.q[1]);
     }
-    int cost = (int)rcost<1>(q, 0, 0, C.T);
+    nzac = nzac != 0;
+    int cost = (int)rcost_bf<1>(aq, 0, 0, T);
     wsync();
     if (b == 0) {
         int d[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) d[k] = W->dc[m * 16 + k];
         wht16(d);
-        int y2q[16];
+        int ay[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) y2q[k] = quantz(d[k], S.y2.iq[k > 0], S.y2.bias[k > 0]);
-        W->y2cost[m] = (int)rcost<0>(y2q, 0, 1, C.T);
-#pragma unroll
-        for (int k = 0; k < 16; k++) d[k] = m24(y2q[k], (int)S.y2.q[k > 0]);
+        for (int k = 0; k < 16; k++) {
+            const int t = k > 0;
+            ay[k] = (int)((__umul24((uint32_t)iabs(d[k]), S.y2.iq[t]) + S.y2.bias[t]) >> 17);
+            d[k] = m24(d[k] < 0 ? -ay[k] : ay[k], (int)S.y2.q[t]);
+        }
+        W->y2cost[m] = (int)rcost_bf<0>(ay, 0, 1, T);
         iwht16(d);
 #pragma unroll
         for (int k = 0; k < 16; k++) W->y2d[m * 16 + k] = d[k];
     }
     wsync();
-    int dq[16];
     dq[0] = W->y2d[m * 16 + b];
-#pragma unroll
-    for (int k = 1; k < 16; k++) dq[k] = m24(q[k], (int)S.y1.q[1]);
     idct16(dq);
     int rec[16], sse = 0, flat = 1;
     const int s00 = C.sY[0];
@@ -548,17 +564,17 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     for (int k = 0; k < 16; k++) {
         rec[k] = clamp255(pr[k] + dq[k]);
         const int d = src[k] - rec[k];
-        sse += d * d;
+        sse += m24(d, d);
         flat &= src[k] == s00;
     }
-    int td = iabs(ttransform(rec) - ttransform(src)) >> 5;
+    int td = iabs(ttransform_diff_pk(rec, src)) >> 5;
     sse = red16(sse);
     td = red16(td);
     cost = red16(cost);
     nzac = red16(nzac);
     flat = red16(flat);
-    // per mode (uniform within the 16-lane group)
-    const int srcflat = __shfl(flat, 0) == 16;  // mode-0 group covers all 256 pixels
+    // per mode (uniform within the 16-lane group), decided on the scalar unit
+    const int srcflat = __builtin_amdgcn_readlane(flat, 0) == 16;  // mode-0 group covers all 256 pixels
     cost += W->y2cost[m];
     int sd = S.tlambda > 0 ? ((int)S.tlambda * td + 128) >> 8 : 0;
     int dfin = sse;
@@ -566,15 +582,16 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
         dfin = sse * 2;
         sd = sd * 2;
     }
-    const long long mc = d_FIXED_COSTS_I16[m];
-    const long long rd = (mc + cost) * (long long)S.l_i16 + 256LL * ((long long)dfin + sd);
-    const long long fin = (mc + cost) * (long long)S.l_mode + 256LL * ((long long)dfin + sd);
+    const int mcost = sel4(m, d_FIXED_COSTS_I16[0], d_FIXED_COSTS_I16[1], d_FIXED_COSTS_I16[2], d_FIXED_COSTS_I16[3]) + cost;
+    const int dist = dfin + sd;
     long long brd = 0x7fffffffffffffffLL, bfin = 0;
     int bm = 0;
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
-        const long long r_m = shfl64(rd, mm * 16);
-        const long long f_m = shfl64(fin, mm * 16);
+        const long long mc = __builtin_amdgcn_readlane(mcost, mm * 16);
+        const long long dd = 256LL * __builtin_amdgcn_readlane(dist, mm * 16);
+        const long long r_m = mc * (long long)S.l_i16 + dd;
+        const long long f_m = mc * (long long)S.l_mode + dd;
         const int avail = mm == 0 || (mm == 1 && above) || (mm == 2 && left) || (mm == 3 && above && left);
         if (avail && r_m < brd) {
             brd = r_m;
@@ -783,73 +800,95 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
     return true;
 }
 
-// pick_best_uv (vp8.rs:2050-2200): lane = mode*8 + block (U 0..3, V 4..7).
-__device__ int pick_uv(const Ctx& C)
+// Chroma DC predictors of both planes (uniform values): lanes 0..15 sum U,
+// 16..31 V; lane i < 8 reads left pixel i, i >= 8 top pixel i - 8.
+__device__ __forceinline__ void uv_dc_preds(const Ctx& C, int& dcU, int& dcV)
+{
+    const int l = C.lane, pl = (l >> 4) & 1, i = l & 15;
+    const uint8_t* w = pl ? C.W->cv : C.W->cu;
+    const int above = C.mby != 0, left = C.mbx != 0;
+    const int v = (int)w[csel(i < 8, (i + 1) * ZW_BPS, i - 7)] & -(int)(i < 8 ? left : above);
+    const int sum = red16(v);
+    const int su = __builtin_amdgcn_readlane(sum, 0), sv = __builtin_amdgcn_readlane(sum, 16);
+    const int shf = 2 + left + above;
+    dcU = (above | left) ? (su + (1 << (shf - 1))) >> shf : 128;
+    dcV = (above | left) ? (sv + (1 << (shf - 1))) >> shf : 128;
+}
+
+// One chroma 4x4 block per lane: prediction (mode 0 DC, 1 TM... per
+// pick_best_uv's order: 0 DC, 1 V(top), 2 H(left), 3 TM), source pixels and
+// the forward transform.  b = block 0..7 (U 0..3, V 4..7).
+__device__ __forceinline__ void uv_block(const Ctx& C, int b, int mode, int dcU, int dcV, int* pr, int* sv, int* c)
 {
     WaveLds* W = C.W;
+    const int pl = b >> 2, bb = b & 3, bx = bb & 1, by = bb >> 1;
+    const uint8_t* w = pl ? W->cv : W->cu;
+    const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
+    const int dcp = pl ? dcV : dcU, corner = w[0];
+    int L[4], Tp[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        L[i] = w[(by * 4 + i + 1) * ZW_BPS];
+        Tp[i] = w[1 + bx * 4 + i];
+    }
+    int r[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t srow = *(const uint32_t*)(sp + i * 8);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int p = sel4(mode, dcp, Tp[j], L[i], clamp255(L[i] + Tp[j] - corner));
+            const int x = (int)((srow >> (8 * j)) & 255u);
+            pr[i * 4 + j] = p;
+            sv[i * 4 + j] = x;
+            r[i * 4 + j] = x - p;
+        }
+    }
+    fdct16_pk(r, c);
+}
+
+// pick_best_uv (vp8.rs:2050-2200): lane = mode*8 + block (U 0..3, V 4..7),
+// one whole block per lane; lanes 32..63 shadow 0..31 (results unused).
+__device__ int pick_uv(const Ctx& C)
+{
     const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
     const int l = C.lane;
     const int above = C.mby != 0, left = C.mbx != 0;
-    long long rd = 0x7fffffffffffffffLL;
-    if (l < 32) {
-        const int m = l >> 3, b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
-        const uint8_t* w = pl ? W->cv : W->cu;
-        const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
-        int dcv = 128;
-        {
-            uint32_t s = 0;
-            int shf = 2;
-            if (left) {
-                for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
-                shf++;
-            }
-            if (above) {
-                for (int x = 1; x <= 8; x++) s += w[x];
-                shf++;
-            }
-            if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
-        }
-        int src[16], pr[16], r[16], q[16];
+    int dcU, dcV;
+    uv_dc_preds(C, dcU, dcV);
+    const int m = (l >> 3) & 3, b = l & 7;
+    int pr[16], sv[16], c[16];
+    uv_block(C, b, m, dcU, dcV, pr, sv, c);
+    int aq[16], rr[16], nzac = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int y = by * 4 + i, x = bx * 4 + j;
-                const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
-                const int p = m == 0 ? dcv : (m == 1 ? T : (m == 2 ? L : clamp255(L + T - w[0])));
-                const int sv = sp[i * 8 + j];
-                src[i * 4 + j] = sv;
-                pr[i * 4 + j] = p;
-                r[i * 4 + j] = sv - p;
-            }
-        fdct16(r);
-        int nzac = 0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            q[k] = quantz(r[k], S.uv.iq[k > 0], S.uv.bias[k > 0]);
-            if (k > 0) nzac += q[k] != 0;
-        }
-        int cost = (int)rcost<0>(q, 0, 2, C.T);
-#pragma unroll
-        for (int k = 0; k < 16; k++) r[k] = m24(q[k], (int)S.uv.q[k > 0]);
-        idct16(r);
-        int sse = 0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int d = src[k] - clamp255(pr[k] + r[k]);
-            sse += d * d;
-        }
-        sse = red8(sse);
-        cost = red8(cost);
-        nzac = red8(nzac);
-        const int pen = (m > 0 && nzac <= 2) ? 140 * 8 : 0;
-        rd = ((long long)d_FIXED_COSTS_UV[m] + cost + pen) * (long long)S.l_uv + 256LL * sse;
+    for (int k = 0; k < 16; k++) {
+        const int t = k > 0;
+        aq[k] = (int)((__umul24((uint32_t)iabs(c[k]), S.uv.iq[t]) + S.uv.bias[t]) >> 17);
+        if (k > 0) nzac += min(aq[k], 1);
+        rr[k] = m24(c[k] < 0 ? -aq[k] : aq[k], (int)S.uv.q[t]);
     }
+    int cost = (int)rcost_bf<0>(aq, 0, 2, T);
+    idct16(rr);
+    int sse = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int d = sv[k] - clamp255(pr[k] + rr[k]);
+        sse += m24(d, d);
+    }
+    sse = red8(sse);
+    cost = red8(cost);
+    nzac = red8(nzac);
+    const int fixed = sel4(m, d_FIXED_COSTS_UV[0], d_FIXED_COSTS_UV[1], d_FIXED_COSTS_UV[2], d_FIXED_COSTS_UV[3]);
+    const int pen = (m > 0 && nzac <= 2) ? 140 * 8 : 0;
+    const int csum = fixed + cost + pen;
+    // per-mode RD on the scalar unit: rd = (fixed + cost + pen) * lambda_uv + 256 * sse
     long long brd = 0x7fffffffffffffffLL;
     int bm = 0;
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
-        const long long r_m = shfl64(rd, mm * 8);
+        const long long r_m = (long long)__builtin_amdgcn_readlane(csum, mm * 8) * (long long)S.l_uv +
+                              256LL * (long long)__builtin_amdgcn_readlane(sse, mm * 8);
         const int avail = mm == 0 || (mm == 1 && above) || (mm == 2 && left) || (mm == 3 && above && left);
         if (avail && r_m < brd) {
             brd = r_m;
@@ -1073,85 +1112,70 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
     WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const int l = C.lane;
-    const int above = C.mby != 0, left = C.mbx != 0;
-    int c[16], pr[16];
-    const int b = l & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
-    if (l < 8) {
-        const uint8_t* w = pl ? W->cv : W->cu;
-        const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
-        int dcv = 128;
-        {
-            uint32_t s = 0;
-            int shf = 2;
-            if (left) {
-                for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
-                shf++;
-            }
-            if (above) {
-                for (int x = 1; x <= 8; x++) s += w[x];
-                shf++;
-            }
-            if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int y = by * 4 + i, x = bx * 4 + j;
-                const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
-                const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - w[0])));
-                pr[i * 4 + j] = p;
-                c[i * 4 + j] = (int)sp[i * 8 + j] - p;
-            }
-        fdct16(c);
-        W->dc[b] = c[0];
-    }
-    wsync();
-    if (l == 0 || l == 4) {
-        const int ch = l >> 2;
+    const int b = l & 7, pl = b >> 2, bb = b & 3, bx = bb & 1, by = bb >> 1;
+    int dcU, dcV;
+    uv_dc_preds(C, dcU, dcV);
+    int pr[16], sv[16], c[16];
+    uv_block(C, b, mode, dcU, dcV, pr, sv, c);
+    // DC error diffusion (vp8.rs chroma quirk, per plane: blocks 0,1,2,3 in
+    // order), on the scalar unit; the adjusted DCs go back to their lanes.
+    {
         const int q = (int)S.uv.q[0];
         const uint32_t iq = S.uv.iq[0], bias = S.uv.bias[0];
         const uint32_t zt = ((1u << 17) - 1 - bias) / iq;
-        int8_t* top = top_derr + ch * 2;
-        int8_t* lft = W->left_derr + ch * 2;
-        auto diffuse = [&](int k, int te, int le) -> int {
-            int dc = W->dc[ch * 4 + k] + ((7 * te + 8 * le) >> 3);
-            W->dc[ch * 4 + k] = dc;
+        int dcs[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) dcs[k] = __builtin_amdgcn_readlane(c[0], k);
+        auto diffuse = [&](int& dc, int te, int le) -> int {
+            dc += (7 * te + 8 * le) >> 3;
             const int sign = dc < 0;
             const uint32_t a = (uint32_t)(sign ? -dc : dc);
             const int level = a > zt ? (int)((a * iq + bias) >> 17) : 0;
             const int err = (int)a - level * q;
             const int se = sign ? -err : err;
-            int v = se >> 1;
-            return v < -127 ? -127 : (v > 127 ? 127 : v);
+            const int v = se >> 1;
+            return (int)(int8_t)(v < -127 ? -127 : (v > 127 ? 127 : v));
         };
-        const int e0 = (int8_t)diffuse(0, top[0], lft[0]);
-        const int e1 = (int8_t)diffuse(1, top[1], e0);
-        const int e2 = (int8_t)diffuse(2, e0, lft[1]);
-        const int e3 = (int8_t)diffuse(3, e1, e2);
-        lft[0] = (int8_t)e1;
-        lft[1] = (int8_t)((3 * e3) >> 2);
-        top[0] = (int8_t)e2;
-        top[1] = (int8_t)(e3 - lft[1]);
+#pragma unroll
+        for (int ch = 0; ch < 2; ch++) {
+            int8_t* top = top_derr + ch * 2;
+            int8_t* lft = W->left_derr + ch * 2;
+            const int t0 = __builtin_amdgcn_readfirstlane((int)top[0]), t1 = __builtin_amdgcn_readfirstlane((int)top[1]);
+            const int l0 = __builtin_amdgcn_readfirstlane((int)lft[0]), l1 = __builtin_amdgcn_readfirstlane((int)lft[1]);
+            int* d = dcs + ch * 4;
+            const int e0 = diffuse(d[0], t0, l0);
+            const int e1 = diffuse(d[1], t1, e0);
+            const int e2 = diffuse(d[2], e0, l1);
+            const int e3 = diffuse(d[3], e1, e2);
+            const int nl1 = (int)(int8_t)((3 * e3) >> 2);
+            wsync();
+            if (l == 0) {
+                lft[0] = (int8_t)e1;
+                lft[1] = (int8_t)nl1;
+                top[0] = (int8_t)e2;
+                top[1] = (int8_t)(e3 - nl1);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(c[0]) : "s"(__builtin_amdgcn_readfirstlane(dcs[k])), "i"(k));
     }
-    wsync();
-    int snz = 0, nzb = 0;
+    int nzb = 0;
+    int lv[16];
+#pragma unroll
+    for (int n = 0; n < 16; n++) {
+        const int j = kZZ(n);
+        lv[n] = quantz(c[j], S.uv.iq[j > 0], S.uv.bias[j > 0]);
+        nzb |= lv[n];
+    }
+    nzb = nzb != 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) c[kZZ(n)] = m24(lv[n], (int)S.uv.q[kZZ(n) > 0]);
+    idct16(c);
     if (l < 8) {
-        c[0] = W->dc[b];
-        int lv[16];
+        uint32_t* lw = (uint32_t*)&W->lev[17 + b][0];
 #pragma unroll
-        for (int n = 0; n < 16; n++) {
-            const int j = kZZ(n);
-            lv[n] = quantz(c[j], S.uv.iq[j > 0], S.uv.bias[j > 0]);
-            nzb |= lv[n] != 0;
-        }
-        snz = nzb;
-#pragma unroll
-        for (int n = 0; n < 16; n++) {
-            W->lev[17 + b][n] = (int16_t)lv[n];
-            c[kZZ(n)] = m24(lv[n], (int)S.uv.q[kZZ(n) > 0]);
-        }
-        idct16(c);
+        for (int n = 0; n < 8; n++) lw[n] = pack_lo(lv[2 * n], lv[2 * n + 1]);
         uint8_t* w = pl ? W->cv : W->cu;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
@@ -1159,9 +1183,12 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
             w[(y + 1) * ZW_BPS + 1 + x] = (uint8_t)clamp255(pr[k] + c[k]);
         }
     }
-    for (int k = 0; k < 8; k++) uv_nz[k] = __shfl(nzb, k);
     int any = 0;
-    for (int k = 0; k < 8; k++) any |= __shfl(snz, k);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uv_nz[k] = __builtin_amdgcn_readlane(nzb, k);
+        any |= uv_nz[k];
+    }
     wsync();
     return any;
 }
@@ -1353,6 +1380,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         return;
     }
 
+    // Pass 1: the luma wavefront couples every wave to the slowest row, and the
+    // luma wave sharing a SIMD with the chroma chain would be that row: give
+    // the luma waves issue priority (the chain has slack and uses the gaps).
+    if (PASS == 1) __builtin_amdgcn_s_setprio(2);
     const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
     const int rw = PASS == 1 ? wv - 1 : wv;
     for (int mby = rw; mby < mbh; mby += nrw) {

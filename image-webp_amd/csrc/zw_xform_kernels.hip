@@ -22,19 +22,10 @@ struct XformArgs {
     int32_t iq[2], bp[2], bn[2], q[2];
 };
 
-typedef short s2 __attribute__((ext_vector_type(2)));
-DI s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
-DI uint32_t as_u(s2 v) { return __builtin_bit_cast(uint32_t, v); }
-// VOP3P v_dot2_i32_i16 with the accumulator from an SGPR (the builtin selects
-// the VOP2 dot2c form, which needs a v_mov of the accumulator every time).
-DI int dot2(s2 a, s2 b, int c)
-{
-    int d;
-    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-    return d;
-}
-// (lo16(a), lo16(b)) packed
-DI uint32_t pack_lo(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+// packed-i16 helpers (dot2, pack_lo) live in zw_dev.h
+typedef zs2 s2;
+DI s2 as_s2(uint32_t v) { return as_zs2(v); }
+DI uint32_t as_u(s2 v) { return as_zu(v); }
 
 // One 4x4 block, packed-i16 form.  Residual rows are held as i16 pairs
 // (r0,r1),(r3,r2) so both butterfly stages are one v_pk_add/v_pk_sub each and

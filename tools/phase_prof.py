@@ -14,7 +14,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["ZWEBP_LIB"] = os.path.join(ROOT, "image-webp_amd", "zwebp", "libzwebp_prof.so")
+os.environ.setdefault("ZWEBP_LIB", os.path.join(ROOT, "image-webp_amd", "zwebp", "libzwebp_prof.so"))
 sys.path.insert(0, os.path.join(ROOT, "image-webp_amd"))
 import zwebp  # noqa: E402
 from zwebp.synth import synth_rgba  # noqa: E402
