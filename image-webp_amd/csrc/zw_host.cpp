@@ -78,6 +78,72 @@ extern "C" int zw_ctx_create(int device, zw_ctx** out)
     return ZW_OK;
 }
 
+// ---- HSA agents of the context's device (PCI location match) and SDMA copies
+struct AgentFind {
+    uint32_t bdf, domain;
+    hsa_agent_t gpu{}, cpu{};
+    bool gpu_ok = false, cpu_ok = false;
+};
+static hsa_status_t find_agents_cb(hsa_agent_t a, void* data)
+{
+    AgentFind* F = (AgentFind*)data;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !F->cpu_ok) {
+        F->cpu = a;
+        F->cpu_ok = true;
+    } else if (t == HSA_DEVICE_TYPE_GPU) {
+        uint32_t bdf = 0, dom = 0;
+        (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+        (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+        if (bdf == F->bdf && dom == F->domain) {
+            F->gpu = a;
+            F->gpu_ok = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+static bool sdma_probe(zw_ctx* c)
+{
+    if (c->sdma >= 0) return c->sdma == 1;
+    c->sdma = 0;
+    if (getenv("ZW_NO_SDMA")) return false;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return false;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return false;  // reference-counted; HIP holds one
+    AgentFind F;
+    F.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
+    F.domain = (uint32_t)prop.pciDomainID;
+    (void)hsa_iterate_agents(find_agents_cb, &F);
+    if (!F.gpu_ok || !F.cpu_ok) return false;
+    c->gpu_agent = F.gpu;
+    c->cpu_agent = F.cpu;
+    c->sdma = 1;
+    return true;
+}
+
+int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (bytes == 0) return ZW_OK;
+    if (sdma_probe(c)) {
+        hsa_signal_t sig;
+        if (hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS) {
+            const hsa_status_t st =
+                hsa_amd_memory_async_copy(dst, c->cpu_agent, src, c->gpu_agent, bytes, 0, nullptr, sig);
+            hsa_signal_value_t v = 1;
+            if (st == HSA_STATUS_SUCCESS)
+                v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            (void)hsa_signal_destroy(sig);
+            if (st == HSA_STATUS_SUCCESS && v == 0) return ZW_OK;
+            if (st == HSA_STATUS_SUCCESS) return ZW_EDEVICE;  // the copy itself failed
+        }
+        c->sdma = 0;  // HSA path unusable: fall back for good
+    }
+    HIPOK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return ZW_OK;
+}
+
 extern "C" void zw_ctx_destroy(zw_ctx* c)
 {
     if (!c) return;
@@ -380,14 +446,11 @@ static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_
 // `ready` (recorded after chunk_pack) has fired.  h_finfo[2*i] = offset of frame fa+i.
 static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEvent_t ready)
 {
-    hipStream_t s = L.stream2;
     const size_t F = (size_t)fa;
-    HIPOK(hipStreamWaitEvent(s, ready, 0));
-    HIPOK(hipMemcpyAsync(L.h_total.data() + slot, L.d_ctr + slot, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                         s));
-    HIPOK(hipMemcpyAsync(L.h_finfo.data(), p->d_finfo + 2 * F, 2 * (size_t)na * sizeof(unsigned long long),
-                         hipMemcpyDeviceToHost, s));
-    HIPOK(hipStreamSynchronize(s));
+    HIPOK(hipEventSynchronize(ready));
+    int r = ctx_d2h(p->ctx, L.h_total.data() + slot, L.d_ctr + slot, sizeof(unsigned long long));
+    if (!r) r = ctx_d2h(p->ctx, L.h_finfo.data(), p->d_finfo + 2 * F, 2 * (size_t)na * sizeof(unsigned long long));
+    if (r) return r;
     const unsigned long long total = L.h_total[slot];
     if (total > L.h_pack_cap) {
         if (L.h_pack) (void)hipHostFree(L.h_pack);
@@ -397,9 +460,7 @@ static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEve
         if (hipHostMalloc((void**)&L.h_pack, cap, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
         L.h_pack_cap = cap;
     }
-    HIPOK(hipMemcpyAsync(L.h_pack, p->d_pack + F * p->pack_stride, total, hipMemcpyDeviceToHost, s));
-    HIPOK(hipStreamSynchronize(s));
-    return ZW_OK;
+    return ctx_d2h(p->ctx, L.h_pack, p->d_pack + F * p->pack_stride, total);
 }
 
 static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
@@ -407,9 +468,10 @@ static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa, n = (size_t)na;
     // segment params of the chunk (written by k_segments before pass 1)
-    HIPOK(hipMemcpyAsync(p->h_params.data() + F, p->d_params + F, n * sizeof(ZwFrameParams), hipMemcpyDeviceToHost,
-                         L.stream2));
-    HIPOK(hipStreamSynchronize(L.stream2));
+    {
+        const int r = ctx_d2h(p->ctx, p->h_params.data() + F, p->d_params + F, n * sizeof(ZwFrameParams));
+        if (r) return r;
+    }
     parallel_for(na, [&](int i) {
         const size_t f = F + i;
         zwh::Stats st;

@@ -1,6 +1,8 @@
 // zw_host_internal.h -- state shared by the host translation units.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -14,6 +16,11 @@ struct zw_ctx {
     // grow-only device scratch for the single-call decode / filter entry points
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
+    // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
+    // D2H runs as a blit kernel, which cannot be dispatched while an encode
+    // kernel holds every CU; the DMA engines need no CU.
+    int sdma = -1;  // -1 unprobed, 0 unavailable, 1 ready
+    hsa_agent_t gpu_agent{}, cpu_agent{};
 };
 
 #define HIPOK(x)                                  \
@@ -80,3 +87,8 @@ static inline hipStream_t ctx_stream(zw_ctx* c)
     if (!c->stream_) (void)hipStreamCreateWithFlags(&c->stream_, hipStreamNonBlocking);
     return c->stream_;
 }
+
+// Blocking device->host copy on a DMA engine (falls back to hipMemcpy when the
+// HSA agents cannot be resolved).  `src` must have been released by the
+// producing kernel (event-complete) before the call.
+int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
