@@ -68,25 +68,11 @@ struct BoolEncoder {
     {
         for (int b = nbits - 1; b >= 0; b--) put(((1 << b) & v) > 0, 128);
     }
-    void tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start = 0)
+    void tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start = 0);
+    // a precomputed tree path: n bits, MSB-first bits / probability indices
+    inline void path(const uint8_t* bits, const uint8_t* pidx, int n, const uint8_t* probs)
     {
-        int cur = -1;
-        for (int i = 0; i < tlen; i++)
-            if (t[i] == -value) { cur = i; break; }
-        int enc[16], pr[16], cnt = 0;
-        for (;;) {
-            if (cur == start) { enc[cnt] = 0; pr[cnt++] = probs[cur / 2]; break; }
-            if (cur == start + 1) { enc[cnt] = 1; pr[cnt++] = probs[cur / 2]; break; }
-            int ev = 0;
-            if (cur % 2) { cur -= 1; ev = 1; }
-            enc[cnt] = ev;
-            pr[cnt++] = probs[cur / 2];
-            int pi = -1;
-            for (int i = 0; i < tlen; i++)
-                if (t[i] == cur) { pi = i; break; }
-            cur = pi;
-        }
-        for (int i = cnt - 1; i >= 0; i--) put(enc[i], pr[i]);
+        for (int i = 0; i < n; i++) put(bits[i], probs[pidx[i]]);
     }
     void flush()
     {
@@ -100,7 +86,89 @@ struct BoolEncoder {
     }
 };
 
+// Path of `value` through a VP8 tree (write_with_tree_start_index,
+// arithmetic.rs:120): bits root-first and the probability index of each.
+inline int tree_path(const int8_t* t, int tlen, int value, int start, uint8_t* bits, uint8_t* pidx)
+{
+    int cur = -1;
+    for (int i = 0; i < tlen; i++)
+        if (t[i] == -value) { cur = i; break; }
+    int enc[16], pr[16], cnt = 0;
+    for (;;) {
+        if (cur == start) { enc[cnt] = 0; pr[cnt++] = cur / 2; break; }
+        if (cur == start + 1) { enc[cnt] = 1; pr[cnt++] = cur / 2; break; }
+        int ev = 0;
+        if (cur % 2) { cur -= 1; ev = 1; }
+        enc[cnt] = ev;
+        pr[cnt++] = cur / 2;
+        int pi = -1;
+        for (int i = 0; i < tlen; i++)
+            if (t[i] == cur) { pi = i; break; }
+        cur = pi;
+    }
+    for (int i = 0; i < cnt; i++) {
+        bits[i] = (uint8_t)enc[cnt - 1 - i];
+        pidx[i] = (uint8_t)pr[cnt - 1 - i];
+    }
+    return cnt;
+}
+
+inline void BoolEncoder::tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start)
+{
+    uint8_t bits[16], pidx[16];
+    const int n = tree_path(t, tlen, value, start, bits, pidx);
+    path(bits, pidx, n, probs);
+}
+
+// TOKEN_TREE paths for tokens 0..11 from start index 0 / 2 (after a zero token)
+struct TokenPaths {
+    uint8_t n[2][12], bits[2][12][12], pidx[2][12][12];
+    TokenPaths()
+    {
+        for (int s = 0; s < 2; s++)
+            for (int v = 0; v < 12; v++) n[s][v] = (uint8_t)tree_path(TOKEN_TREE, 22, v, 2 * s, bits[s][v], pidx[s][v]);
+    }
+};
+inline const TokenPaths& token_paths()
+{
+    static const TokenPaths P;
+    return P;
+}
+
 inline uint16_t bitcost(int bit, int p) { return bit ? VP8_ENTROPY_COST[255 - p] : VP8_ENTROPY_COST[p]; }
+
+// Packed MB record view (zw_pack_kernels.hip): header, sub-modes, eobs and a
+// pointer to each block's zigzag levels (little-endian i16, eob of them).
+struct PackedMb {
+    int luma, skip, segment, chroma;
+    uint8_t bpred[16];
+    const uint8_t* eob;
+    const uint8_t* lv[25];
+};
+inline const uint8_t* view_mb(const uint8_t* p, PackedMb& m)
+{
+    const uint8_t h = p[0];
+    m.luma = h & 7;
+    m.skip = (h >> 3) & 1;
+    m.segment = (h >> 4) & 3;
+    m.chroma = h >> 6;
+    p++;
+    if (m.luma == 4) {
+        for (int i = 0; i < 8; i++) {
+            m.bpred[2 * i] = p[i] & 15;
+            m.bpred[2 * i + 1] = p[i] >> 4;
+        }
+        p += 8;
+    }
+    m.eob = p;
+    p += 25;
+    for (int b = 0; b < 25; b++) {
+        m.lv[b] = p;
+        p += 2 * m.eob[b];
+    }
+    return p;
+}
+inline int lv_at(const uint8_t* lv, int n) { return (int)(int16_t)(uint16_t)(lv[2 * n] | (lv[2 * n + 1] << 8)); }
 
 // LevelCosts::calculate (cost.rs:1500)
 inline void level_costs(ZwLevelCosts& L, const uint8_t probs[4][8][3][11])
@@ -128,37 +196,6 @@ inline void level_costs(ZwLevelCosts& L, const uint8_t probs[4][8][3][11])
             }
 }
 
-// Packed MB record (zw_pack_kernels.hip) -> ZwMbOut (levels beyond each
-// block's eob are zero).  Returns the pointer past the record.
-inline const uint8_t* unpack_mb(const uint8_t* p, ZwMbOut& m)
-{
-    const uint8_t h = p[0];
-    m.luma_mode = h & 7;
-    m.skip = (h >> 3) & 1;
-    m.segment = (h >> 4) & 3;
-    m.chroma_mode = h >> 6;
-    p++;
-    if (m.luma_mode == 4) {
-        for (int i = 0; i < 8; i++) {
-            m.bpred[2 * i] = p[i] & 15;
-            m.bpred[2 * i + 1] = p[i] >> 4;
-        }
-        p += 8;
-    } else {
-        memset(m.bpred, 0, 16);
-    }
-    const uint8_t* eob = p;
-    p += 25;
-    for (int b = 0; b < 25; b++) {
-        const int e = eob[b];
-        int16_t* d = m.levels[b];
-        int n = 0;
-        for (; n < e; n++, p += 2) d[n] = (int16_t)(uint16_t)(p[0] | (p[1] << 8));
-        for (; n < 16; n++) d[n] = 0;
-    }
-    return p;
-}
-
 struct Stats {
     uint32_t s[4][8][3][11];
 };
@@ -169,13 +206,10 @@ inline void rec_stat(uint32_t& s, int bit)
     s += 0x00010000u + (bit ? 1u : 0u);
 }
 
-// record_coeffs (cost.rs:1297); c = zigzag levels
-inline void record_coeffs(Stats& S, const int16_t* c, int t, int first, int ctx)
+// record_coeffs (cost.rs:1297) over a packed block: eob = last nonzero + 1,
+// lv = its zigzag levels.
+inline void record_coeffs(Stats& S, const uint8_t* lv, int eob, int t, int first, int ctx)
 {
-    int last = -1;
-    for (int i = 15; i >= 0; i--)
-        if (c[i] != 0) { last = i; break; }
-    int eob = last >= 0 ? last + 1 : 0;
     if (eob <= first) {
         rec_stat(S.s[t][VP8_ENC_BANDS[first]][ctx][0], 0);
         return;
@@ -183,7 +217,8 @@ inline void record_coeffs(Stats& S, const int16_t* c, int t, int first, int ctx)
     int n = first, skip_eob = 0;
     while (n < eob) {
         uint32_t* st = S.s[t][VP8_ENC_BANDS[n]][ctx];
-        int v = c[n] < 0 ? -c[n] : c[n];
+        const int c = lv_at(lv, n);
+        int v = c < 0 ? -c : c;
         n++;
         if (!skip_eob) rec_stat(st[0], 1);
         if (v == 0) {
@@ -238,22 +273,17 @@ struct Cplx {
     }
 };
 
-inline bool any_nz(const int16_t* c, int first)
+// check_all_coeffs_zero on pass-1 (simple-quant) levels: a block has a
+// nonzero at index >= first exactly when its eob > first.
+inline bool mb_all_zero_p1(const PackedMb& m)
 {
-    for (int i = first; i < 16; i++)
-        if (c[i]) return true;
-    return false;
-}
-
-// check_all_coeffs_zero on pass-1 (simple-quant) levels.
-inline bool mb_all_zero_p1(const ZwMbOut& m)
-{
-    const bool i4 = m.luma_mode == 4;
-    if (!i4 && any_nz(m.levels[16], 0)) return false;
+    const bool i4 = m.luma == 4;
+    if (!i4 && m.eob[16] > 0) return false;
+    const int first = i4 ? 0 : 1;
     for (int b = 0; b < 16; b++)
-        if (any_nz(m.levels[b], i4 ? 0 : 1)) return false;
+        if (m.eob[b] > first) return false;
     for (int b = 17; b < 25; b++)
-        if (any_nz(m.levels[b], 0)) return false;
+        if (m.eob[b] > 0) return false;
     return true;
 }
 
@@ -261,7 +291,7 @@ inline bool mb_all_zero_p1(const ZwMbOut& m)
 // Returns the skip probability.
 inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
 {
-    ZwMbOut m;
+    PackedMb m;
     memset(&S, 0, sizeof S);
     std::vector<Cplx> top(mbw);
     memset(top.data(), 0, sizeof(Cplx) * mbw);
@@ -270,9 +300,9 @@ inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
         Cplx left;
         memset(&left, 0, sizeof left);
         for (int x = 0; x < mbw; x++) {
-            packed = unpack_mb(packed, m);
+            packed = view_mb(packed, m);
             total++;
-            const bool i4 = m.luma_mode == 4;
+            const bool i4 = m.luma == 4;
             if (mb_all_zero_p1(m)) {
                 skipped++;
                 left.clear(!i4);
@@ -281,17 +311,17 @@ inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
             }
             if (!i4) {
                 int cx = left.y2 + top[x].y2;
-                record_coeffs(S, m.levels[16], 1, 0, cx < 2 ? cx : 2);
-                left.y2 = top[x].y2 = any_nz(m.levels[16], 0);
+                record_coeffs(S, m.lv[16], m.eob[16], 1, 0, cx < 2 ? cx : 2);
+                left.y2 = top[x].y2 = m.eob[16] > 0;
             }
             const int tt = i4 ? 3 : 0, first = i4 ? 0 : 1;
             for (int by = 0; by < 4; by++) {
                 int l = left.y[by];
                 for (int bx = 0; bx < 4; bx++) {
                     int cx = l + top[x].y[bx];
-                    const int16_t* c = m.levels[by * 4 + bx];
-                    record_coeffs(S, c, tt, first, cx < 2 ? cx : 2);
-                    l = any_nz(c, first);
+                    const int b = by * 4 + bx;
+                    record_coeffs(S, m.lv[b], m.eob[b], tt, first, cx < 2 ? cx : 2);
+                    l = m.eob[b] > first;
                     top[x].y[bx] = (uint8_t)l;
                 }
                 left.y[by] = (uint8_t)l;
@@ -303,9 +333,9 @@ inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
                     int l = lc[by];
                     for (int bx = 0; bx < 2; bx++) {
                         int cx = l + tc[bx];
-                        const int16_t* c = m.levels[17 + 4 * pl + by * 2 + bx];
-                        record_coeffs(S, c, 2, 0, cx < 2 ? cx : 2);
-                        l = any_nz(c, 0);
+                        const int b = 17 + 4 * pl + by * 2 + bx;
+                        record_coeffs(S, m.lv[b], m.eob[b], 2, 0, cx < 2 ? cx : 2);
+                        l = m.eob[b] > 0;
                         tc[bx] = (uint8_t)l;
                     }
                     lc[by] = (uint8_t)l;
@@ -351,30 +381,27 @@ inline bool updated_probs(const Stats& S, uint8_t out[4][8][3][11])
     return true;
 }
 
-// encode_coefficients token part (vp8.rs:845-958) for already-quantized zigzag levels.
-inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const int16_t* zz, int first, int ctx)
+// encode_coefficients token part (vp8.rs:845-958) for an already-quantized
+// packed block (eob = last nonzero + 1).
+inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first, int ctx)
 {
-    int eobi = 0;
-    for (int i = 15; i >= 0; i--)
-        if (zz[i] != 0) { eobi = i + 1; break; }
+    const TokenPaths& TP = token_paths();
     int skip_eob = 0;
     for (int idx = first; idx < eobi; idx++) {
-        const int coeff = zz[idx];
+        const int coeff = lv_at(lv, idx);
         const uint8_t* pr = P[COEFF_BANDS[idx]][ctx];
-        const int start = skip_eob ? 2 : 0;
         const int a = coeff < 0 ? -coeff : coeff;
         int token;
         if (a == 0) {
-            E.tree(TOKEN_TREE, 22, pr, 0, start);
-            skip_eob = 1;
             token = 0;
         } else if (a <= 4) {
-            E.tree(TOKEN_TREE, 22, pr, a, start);
-            skip_eob = 0;
             token = a;
         } else {
-            int cat = a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10;
-            E.tree(TOKEN_TREE, 22, pr, cat, start);
+            token = a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10;
+        }
+        E.path(TP.bits[skip_eob][token], TP.pidx[skip_eob][token], TP.n[skip_eob][token], pr);
+        if (token >= 5) {
+            const int cat = token;
             const uint8_t* cp = PROB_DCT_CAT[cat - 5];
             int extra = a - DCT_CAT_BASE[cat - 5];
             int mask = cat == 10 ? 1 << 10 : 1 << (cat - 5);
@@ -382,15 +409,14 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const int16_t* 
                 E.put((extra & mask) > 0, cp[k]);
                 mask >>= 1;
             }
-            skip_eob = 0;
-            token = cat;
         }
+        skip_eob = token == 0;
         if (token != 0) E.flag(!(coeff > 0));
         ctx = token == 0 ? 0 : (token == 1 ? 1 : 2);
     }
     if (eobi < 16) {
         int bi = first > eobi ? first : eobi;
-        E.tree(TOKEN_TREE, 22, P[COEFF_BANDS[bi]][ctx], 11, 0);
+        E.path(TP.bits[0][11], TP.pidx[0][11], TP.n[0][11], P[COEFF_BANDS[bi]][ctx]);
     }
     return eobi > 0;
 }
@@ -400,9 +426,10 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const int16_t* 
 inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const uint8_t* packed, int width,
                        int height, bool have_updated, const uint8_t upd[4][8][3][11])
 {
-    ZwMbOut m;
+    PackedMb m;
     const int mbw = P.mbw, mbh = P.mbh;
     BoolEncoder H, T;
+    T.buf.reserve((size_t)mbw * mbh * 16 + 4096);
     uint8_t probs[4][8][3][11];
     memcpy(probs, COEFF_PROBS, sizeof probs);
     H.literal(1, 0);
@@ -459,11 +486,11 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
         memset(&left, 0, sizeof left);
         uint8_t left_bp[4] = {0, 0, 0, 0};
         for (int x = 0; x < mbw; x++) {
-            packed = unpack_mb(packed, m);
+            packed = view_mb(packed, m);
             if (P.seg_enabled && P.seg_update_map) H.tree(SEGMENT_ID_TREE, 6, P.seg_probs, m.segment);
             H.put(m.skip, P.skip_prob);
-            H.tree(YMODE_TREE, 8, KEYFRAME_YMODE_PROBS, m.luma_mode);
-            if (m.luma_mode == 4) {
+            H.tree(YMODE_TREE, 8, KEYFRAME_YMODE_PROBS, m.luma);
+            if (m.luma == 4) {
                 for (int by = 0; by < 4; by++) {
                     int l = left_bp[by];
                     for (int bx = 0; bx < 4; bx++) {
@@ -476,10 +503,10 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
                 }
             } else {
                 static const int intra_of[4] = {0, 2, 3, 1};
-                for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma_mode];
+                for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma];
             }
-            H.tree(UVMODE_TREE, 6, KEYFRAME_UV_MODE_PROBS, m.chroma_mode);
-            const bool i4 = m.luma_mode == 4;
+            H.tree(UVMODE_TREE, 6, KEYFRAME_UV_MODE_PROBS, m.chroma);
+            const bool i4 = m.luma == 4;
             if (m.skip) {
                 left.clear(!i4);
                 top[x].clear(!i4);
@@ -487,14 +514,15 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
             }
             int plane = i4 ? 3 : 0;
             if (!i4) {
-                int hc = emit_block(T, probs[1], m.levels[16], 0, left.y2 + top[x].y2);
+                int hc = emit_block(T, probs[1], m.lv[16], m.eob[16], 0, left.y2 + top[x].y2);
                 left.y2 = top[x].y2 = (uint8_t)hc;
             }
             const int first = i4 ? 0 : 1;
             for (int by = 0; by < 4; by++) {
                 int l = left.y[by];
                 for (int bx = 0; bx < 4; bx++) {
-                    int hc = emit_block(T, probs[plane], m.levels[by * 4 + bx], first, l + top[x].y[bx]);
+                    const int b = by * 4 + bx;
+                    int hc = emit_block(T, probs[plane], m.lv[b], m.eob[b], first, l + top[x].y[bx]);
                     l = hc;
                     top[x].y[bx] = (uint8_t)hc;
                 }
@@ -506,7 +534,8 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
                 for (int by = 0; by < 2; by++) {
                     int l = lc[by];
                     for (int bx = 0; bx < 2; bx++) {
-                        int hc = emit_block(T, probs[2], m.levels[17 + 4 * pl + by * 2 + bx], 0, l + tc[bx]);
+                        const int b = 17 + 4 * pl + by * 2 + bx;
+                        int hc = emit_block(T, probs[2], m.lv[b], m.eob[b], 0, l + tc[bx]);
                         l = hc;
                         tc[bx] = (uint8_t)hc;
                     }
