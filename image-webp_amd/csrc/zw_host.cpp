@@ -235,8 +235,8 @@ struct zw_pipe {
     // packed MB streams (zw_pack_kernels.hip)
     uint8_t* d_eobs = nullptr;
     uint32_t* d_sizes = nullptr;
-    unsigned long long* d_finfo = nullptr;
-    uint8_t* d_pack = nullptr;
+    unsigned long long *d_finfo = nullptr, *d_finfo2 = nullptr;  // pass-1 / pass-2 packed streams
+    uint8_t *d_pack = nullptr, *d_pack2 = nullptr;
     size_t pack_stride = 0;  // worst-case packed bytes per frame
     Pinned<ZwFrameParams> h_params;
     Pinned<ZwLevelCosts> h_lcost;
@@ -252,7 +252,7 @@ static void pipe_free(zw_pipe* p)
     if (!p) return;
     void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
                     p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg,
-                    p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack};
+                    p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack, p->d_finfo2, p->d_pack2};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     for (PipeLane& L : p->lanes) {
@@ -340,7 +340,9 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
               hipMalloc(&p->d_eobs, N * p->nmb * 25) == hipSuccess &&
               hipMalloc(&p->d_sizes, N * p->nmb * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&p->d_finfo, N * 2 * sizeof(unsigned long long)) == hipSuccess &&
-              hipMalloc(&p->d_pack, N * p->pack_stride) == hipSuccess;
+              hipMalloc(&p->d_pack, N * p->pack_stride) == hipSuccess &&
+              hipMalloc(&p->d_finfo2, N * 2 * sizeof(unsigned long long)) == hipSuccess &&
+              hipMalloc(&p->d_pack2, N * p->pack_stride) == hipSuccess;
     const int G = pipe_lanes_for(n);
     p->lanes.resize(G);
     for (int g = 0; ok && g < G; g++) {
@@ -437,8 +439,11 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
 static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_out, int slot)
 {
     const size_t F = (size_t)fa;
+    const bool p2 = slot & 1;  // pass-2 streams have their own buffers (a later batch's pass 1 may overwrite
+                               // the pass-1 buffers while the host is still fetching pass-2 data)
     HIPOK(zwk_pack(L.stream, d_out + F * p->nmb, p->nmb, na, p->d_eobs + F * p->nmb * 25, p->d_sizes + F * p->nmb,
-                   L.d_ctr + slot, p->d_finfo + 2 * F, p->d_pack + F * p->pack_stride));
+                   L.d_ctr + slot, (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
+                   (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride));
     return ZW_OK;
 }
 
@@ -449,7 +454,10 @@ static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEve
     const size_t F = (size_t)fa;
     HIPOK(hipEventSynchronize(ready));
     int r = ctx_d2h(p->ctx, L.h_total.data() + slot, L.d_ctr + slot, sizeof(unsigned long long));
-    if (!r) r = ctx_d2h(p->ctx, L.h_finfo.data(), p->d_finfo + 2 * F, 2 * (size_t)na * sizeof(unsigned long long));
+    const bool p2 = slot & 1;
+    if (!r)
+        r = ctx_d2h(p->ctx, L.h_finfo.data(), (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
+                    2 * (size_t)na * sizeof(unsigned long long));
     if (r) return r;
     const unsigned long long total = L.h_total[slot];
     if (total > L.h_pack_cap) {
@@ -460,7 +468,7 @@ static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEve
         if (hipHostMalloc((void**)&L.h_pack, cap, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
         L.h_pack_cap = cap;
     }
-    return ctx_d2h(p->ctx, L.h_pack, p->d_pack + F * p->pack_stride, total);
+    return ctx_d2h(p->ctx, L.h_pack, (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, total);
 }
 
 static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
@@ -527,50 +535,67 @@ static void lane_times(PipeLane& L)
 //   host:                 S(0)   S(1) ..          E(0)   E(1) .. E(C-1)
 static double g_trace_t0 = 0;
 static bool g_trace = false;
-static int lane_encode(zw_pipe* p, PipeLane& L, bool emit)
+// Encode the lane's frames `nb` times back to back (nb = 1: one batch).  Per
+// batch: pass 1 of every chunk is queued up front; then per chunk fetch the
+// pass-1 records, replay statistics, queue pass 2; then per chunk fetch the
+// pass-2 records and emit.  With nb > 1 the next batch's pass 1 is queued
+// before this batch's emit loop, so the GPU runs it while the host emits.
+static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
 {
     const int nch = (L.n + L.chunk - 1) / L.chunk;
     auto ca = [&](int c) { return L.f0 + c * L.chunk; };
     auto cn = [&](int c) { return std::min(L.chunk, L.n - c * L.chunk); };
-    for (int c = 0; c < nch; c++) {
-        int r = chunk_pass1(p, L, ca(c), cn(c), c == 0);
-        if (!r) r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
-        if (r) return r;
-        HIPOK(hipEventRecord(L.cev[2 * c], L.stream));
-    }
+    auto queue_pass1 = [&]() -> int {
+        for (int c = 0; c < nch; c++) {
+            int r = chunk_pass1(p, L, ca(c), cn(c), c == 0);
+            if (!r) r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
+            if (r) return r;
+            HIPOK(hipEventRecord(L.cev[2 * c], L.stream));
+        }
+        return ZW_OK;
+    };
     double fetch = 0, stats = 0, fetch2 = 0, tok = 0;
-    for (int c = 0; c < nch; c++) {
-        double t0 = now_ms();
-        int r = chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c]);
-        if (r) return r;
-        double t1 = now_ms();
-        r = chunk_stats(p, L, ca(c), cn(c));
-        if (r) return r;
-        stats += now_ms() - t1;
-        fetch += t1 - t0;
-        if (g_trace) fprintf(stderr, "  lane %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, c, t1 - g_trace_t0, now_ms() - g_trace_t0);
-        r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
-        if (!r && emit) r = chunk_pack(p, L, ca(c), cn(c), p->d_out2, 2 * c + 1);
-        if (r) return r;
-        HIPOK(hipEventRecord(L.cev[2 * c + 1], L.stream));
-    }
-    if (emit) {
+    int r = queue_pass1();
+    if (r) return r;
+    for (int b = 0; b < nb; b++) {
         for (int c = 0; c < nch; c++) {
             double t0 = now_ms();
-            int r = chunk_fetch(p, L, ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
+            r = chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c]);
             if (r) return r;
             double t1 = now_ms();
-            chunk_emit(p, L, ca(c), cn(c));
-            tok += now_ms() - t1;
-            fetch2 += t1 - t0;
-            if (g_trace) fprintf(stderr, "  lane %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, c, t1 - g_trace_t0, now_ms() - g_trace_t0);
+            r = chunk_stats(p, L, ca(c), cn(c));
+            if (r) return r;
+            stats += now_ms() - t1;
+            fetch += t1 - t0;
+            if (g_trace)
+                fprintf(stderr, "  lane %d batch %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, b, c,
+                        t1 - g_trace_t0, now_ms() - g_trace_t0);
+            r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
+            if (!r && emit) r = chunk_pack(p, L, ca(c), cn(c), p->d_out2, 2 * c + 1);
+            if (r) return r;
+            HIPOK(hipEventRecord(L.cev[2 * c + 1], L.stream));
+        }
+        if (b + 1 < nb && (r = queue_pass1())) return r;
+        if (emit) {
+            for (int c = 0; c < nch; c++) {
+                double t0 = now_ms();
+                r = chunk_fetch(p, L, ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
+                if (r) return r;
+                double t1 = now_ms();
+                chunk_emit(p, L, ca(c), cn(c));
+                tok += now_ms() - t1;
+                fetch2 += t1 - t0;
+                if (g_trace)
+                    fprintf(stderr, "  lane %d batch %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, b, c,
+                            t1 - g_trace_t0, now_ms() - g_trace_t0);
+            }
         }
     }
     HIPOK(hipStreamSynchronize(L.stream));
-    L.hms[0] = fetch;
-    L.hms[1] = stats;
-    L.hms[2] = fetch2;
-    L.hms[3] = tok;
+    L.hms[0] = fetch / nb;
+    L.hms[1] = stats / nb;
+    L.hms[2] = fetch2 / nb;
+    L.hms[3] = tok / nb;
     lane_times(L);
     return ZW_OK;
 }
@@ -627,26 +652,30 @@ extern "C" int zw_pipe_run_device(zw_pipe* p)
     return r;
 }
 
-extern "C" int zw_pipe_encode(zw_pipe* p)
+static int pipe_encode(zw_pipe* p, int nb)
 {
-    if (!p) return ZW_EINVAL;
+    if (!p || nb < 1) return ZW_EINVAL;
     HIPOK(hipSetDevice(p->ctx->device));
     static const bool trace = getenv("ZW_PIPE_TRACE") != nullptr;
     const double T0 = now_ms();
     g_trace = trace;
     g_trace_t0 = T0;
     int r = run_lanes(p, [&](PipeLane& L) -> int {
-        const int q = lane_encode(p, L, true);
+        const int q = lane_encode(p, L, true, nb);
         if (trace)
-            fprintf(stderr, "lane f0=%d n=%d chunk=%d: done %.1f ms (fetch %.1f stats %.1f fetch2 %.1f emit %.1f) "
-                            "k: %.1f %.1f %.1f %.1f\n",
-                    L.f0, L.n, L.chunk, now_ms() - T0, L.hms[0], L.hms[1], L.hms[2], L.hms[3], L.kms[0], L.kms[1],
+            fprintf(stderr, "lane f0=%d n=%d chunk=%d x%d: done %.1f ms (per batch: fetch %.1f stats %.1f fetch2 %.1f "
+                            "emit %.1f) k: %.1f %.1f %.1f %.1f\n",
+                    L.f0, L.n, L.chunk, nb, now_ms() - T0, L.hms[0], L.hms[1], L.hms[2], L.hms[3], L.kms[0], L.kms[1],
                     L.kms[2], L.kms[3]);
         return q;
     });
     pipe_collect_times(p);
     return r;
 }
+
+extern "C" int zw_pipe_encode(zw_pipe* p) { return pipe_encode(p, 1); }
+
+extern "C" int zw_pipe_encode_repeat(zw_pipe* p, int n) { return pipe_encode(p, n); }
 
 extern "C" int zw_pipe_launch_frames(zw_pipe* p) { return p && !p->lanes.empty() ? p->lanes[0].chunk : 0; }
 

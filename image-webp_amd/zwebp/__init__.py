@@ -110,6 +110,7 @@ SIGNATURES = [
     ("zw_pipe_input_device_ptr", _VP, [_VP]),
     ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
     ("zw_pipe_encode", _I, [_VP]),
+    ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_run_pass1", _I, [_VP, _I]),
     ("zw_pipe_run_device", _I, [_VP]),
     ("zw_pipe_output", _I, [_VP, _I, ctypes.POINTER(_Bytes)]),
@@ -417,6 +418,11 @@ class Pipeline:
 
     def encode(self):
         _check(self._lib.zw_pipe_encode(self._h), "zw_pipe_encode", EncodingError)
+
+    def encode_repeat(self, n):
+        """Encode the batch n times back to back with batch k+1's GPU passes
+        overlapping batch k's host token emission (streaming throughput)."""
+        _check(self._lib.zw_pipe_encode_repeat(self._h, int(n)), "zw_pipe_encode_repeat", EncodingError)
 
     def run_pass1(self, write_recon=True):
         _check(self._lib.zw_pipe_run_pass1(self._h, 1 if write_recon else 0), "zw_pipe_run_pass1", EncodingError)

@@ -142,6 +142,11 @@ void *zw_pipe_input_device_ptr(zw_pipe *p);
 int zw_pipe_upload(zw_pipe *p, int frame, const uint8_t *data, size_t len);
 /* Runs the full encode of all frames; bitstreams retrievable afterwards. */
 int zw_pipe_encode(zw_pipe *p);
+/* Encodes the uploaded batch n times back to back, streaming-style: batch k+1's
+ * pass-1 kernels are queued before batch k's host token emission, so the GPU
+ * and the host entropy stage overlap across batches.  Outputs afterwards are
+ * those of the last batch (identical to zw_pipe_encode's). */
+int zw_pipe_encode_repeat(zw_pipe *p, int n);
 /* Device-only passes (rgb2yuv, analysis, segments, pass 1, stats, pass 2) without
  * token emission, for kernel timing.  Returns 0 or an error. */
 int zw_pipe_run_device(zw_pipe *p);

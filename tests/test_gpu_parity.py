@@ -193,6 +193,25 @@ def test_encode_batch_independent_frames(ctx):
         assert outs[i] == ref, f"frame {i}"
 
 
+def test_encode_repeat_streaming(ctx, monkeypatch):
+    """encode_repeat: batch k+1's pass 1 overlaps batch k's emission (separate
+    pass-1 / pass-2 pack buffers); several chunks per lane; every batch's
+    output must equal the reference's."""
+    monkeypatch.setenv("ZW_PIPE_CHUNK", "2")
+    w, h = 160, 128
+    imgs = [synth_rgba(w, h, 0x5EED1000 + i, "natural" if i % 2 else "noise") for i in range(5)]
+    p = zwebp.Pipeline(5, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    try:
+        for i, img in enumerate(imgs):
+            p.upload(i, img)
+        p.encode_repeat(3)
+        for i, img in enumerate(imgs):
+            rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
+            assert p.output(i) == ref, f"frame {i}"
+    finally:
+        p.close()
+
+
 def test_encode_api_errors(ctx):
     img = synth_rgba(16, 16)
     with pytest.raises(zwebp.EncodingError) as e:
