@@ -698,3 +698,153 @@ DI int ttransform_diff_pk(const int* a, const int* b)
     }
     return acc;
 }
+
+// kWTrellis[j] for a lane-varying j (two 64-bit immediates, 8 bits per entry)
+DI int wtrellis_of(int j)
+{
+    const unsigned long long lo = 0x0a11181b0b131b1eull, hi = 0x06080a0b080c1113ull;
+    return (int)(((j < 8 ? lo : hi) >> (8 * (j & 7))) & 255ull);
+}
+
+DI long long llmin(long long a, long long b) { return a < b ? a : b; }
+// Materialise a cross-lane result at this point of the program: a DPP whose
+// value feeds only a lane-dependent select may otherwise be sunk into a
+// branch, where it would read inactive source lanes.
+DI int pin(int v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+DI long long pin(long long v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+template <int CTRL>
+DI long long dpp_ll(long long v, long long old)  // 64-bit DPP row op; lanes without a source get `old`
+{
+    const int lo = __builtin_amdgcn_update_dpp((int)(old & 0xffffffff), (int)(v & 0xffffffff), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(old >> 32), (int)(v >> 32), CTRL, 0xf, 0xf, false);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// one step of the inclusive min-plus scan of 2x2 matrices (row_shr CTRL)
+template <int CTRL>
+DI void mp_scan_step(long long& P00, long long& P01, long long& P10, long long& P11, long long INF)
+{
+    const long long Q00 = dpp_ll<CTRL>(P00, 0), Q01 = dpp_ll<CTRL>(P01, INF);
+    const long long Q10 = dpp_ll<CTRL>(P10, INF), Q11 = dpp_ll<CTRL>(P11, 0);
+    const long long R00 = llmin(P00 + Q00, P01 + Q10), R01 = llmin(P00 + Q01, P01 + Q11);
+    const long long R10 = llmin(P10 + Q00, P11 + Q10), R11 = llmin(P10 + Q01, P11 + Q11);
+    P00 = R00;
+    P01 = R01;
+    P10 = R10;
+    P11 = R11;
+}
+// group min of (t, i) with the smallest i on ties, one xor-butterfly step
+template <int CTRL>
+DI void argmin_step(long long& t, int& i)
+{
+    const long long ot = dpp_ll<CTRL>(t, 0);
+    const int oi = DPP(i, CTRL);
+    const bool take = ot < t || (ot == t && oi < i);
+    t = take ? ot : t;
+    i = take ? oi : i;
+}
+
+// trellis_quantize_block (cost.rs:788-1006) in 16-lane group form: lane n =
+// zigzag position n, cn = the coefficient at that position.  The per-position
+// node costs do not depend on the path (a node's context is fixed by its own
+// level), so the Viterbi recurrence over positions is a min-plus product of
+// 2x2 transition matrices: an inclusive scan of them (4 DPP row_shr steps)
+// gives every position's node scores at once.  Ties and the early-stop rule
+// are the serial version's: argmin strict (sc1 < sc0), best term the first
+// strict minimum in (n, d) order.  Returns the group's any-nonzero flag and
+// the signed level at position n in lvl.
+template <int FIRST>
+DI int trellis_g(int cn, int n, const ZwMatrix& m, const uint16_t* sharpen, uint32_t lambda, const LdsTables* T,
+                 int ctype, int ctx0, int& lvl)
+{
+    const long long INF = 1LL << 57;
+    const int j = zz_of(n);
+    const int qac = (int)m.q[1];
+    const int thresh = (qac * qac) / 4;
+    const long long lam = lambda;
+    // last position processed: highest n >= FIRST with c^2 > thresh (or FIRST - 1), plus one
+    const unsigned big = gmask(n >= FIRST && cn * cn > thresh);
+    int last = big ? 31 - __clz((int)big) : FIRST - 1;
+    if (last < 15) last++;
+    const bool inpos = n >= FIRST && n <= last;
+    const int q = j == 0 ? (int)m.q[0] : qac;
+    const uint32_t iq = j == 0 ? m.iq[0] : m.iq[1];
+    const int sign = cn < 0;
+    const int cws = iabs(cn) + sharpen[j];
+    const int l0 = min((int)(((uint32_t)cws * iq) >> 17), 2047);
+    const int thr = min((int)(((uint32_t)cws * iq + 65536u) >> 17), 2047);
+    const int band = kBand(n);
+    const int w = wtrellis_of(j);
+    // predecessor contexts (position n - 1's node levels), ctx0 at FIRST
+    const int l0p = pin(shr1(l0));
+    const int cp0 = n == FIRST ? ctx0 : min(l0p, 2), cp1 = n == FIRST ? ctx0 : min(l0p + 1, 2);
+    long long M[2][2], base[2], eobc[2];
+    int valid[2];
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+        const int level = l0 + d;
+        valid[d] = inpos && level <= thr;
+        const int ne = cws - level * q;
+        base[d] = 256LL * ((long long)w * ((long long)(ne * ne) - (long long)(cws * cws)));
+        const int lv = min(level, 67);
+        const int fixed = T->lfc[min(level, 2047)] + (level > 0 ? 256 : 0);
+        const long long c0 = (long long)(fixed + T->lc[ctype][band][cp0][lv]) * lam;
+        const long long c1 = (long long)(fixed + T->lc[ctype][band][cp1][lv]) * lam;
+        M[d][0] = valid[d] ? c0 + base[d] : INF;
+        M[d][1] = valid[d] ? c1 + base[d] : INF;
+        eobc[d] = n < 15 ? (long long)T->eob[ctype][kBand(n + 1)][min(level, 2)] * lam : 0;
+    }
+    if (!inpos) {  // positions outside FIRST..last leave the scores unchanged
+        M[0][0] = 0;
+        M[0][1] = INF;
+        M[1][0] = INF;
+        M[1][1] = 0;
+    }
+    // inclusive min-plus scan: P_n = M_n (x) M_{n-1} (x) ... (x) M_0
+    long long P00 = M[0][0], P01 = M[0][1], P10 = M[1][0], P11 = M[1][1];
+    mp_scan_step<0x111>(P00, P01, P10, P11, INF);  // row_shr:1
+    mp_scan_step<0x112>(P00, P01, P10, P11, INF);  // row_shr:2
+    mp_scan_step<0x114>(P00, P01, P10, P11, INF);  // row_shr:4
+    mp_scan_step<0x118>(P00, P01, P10, P11, INF);  // row_shr:8
+    const long long init = ctx0 == 0 ? (long long)T->init[ctype][kBand(FIRST)][ctx0] * lam : 0;
+    const long long s0 = init + llmin(P00, P01), s1 = init + llmin(P10, P11);  // node scores after position n
+    // predecessor scores -> the serial version's argmin bits
+    const long long q0 = pin(dpp_ll<0x111>(s0, init)), q1 = pin(dpp_ll<0x111>(s1, init));
+    const long long p0 = n == FIRST ? init : q0, p1 = n == FIRST ? init : q1;
+    int pb[2];
+#pragma unroll
+    for (int d = 0; d < 2; d++) pb[d] = (p1 + (M[d][1] - base[d])) < (p0 + (M[d][0] - base[d]));
+    // best terminating node: first strict minimum of s_d + eob_d over (n, d), against the empty block
+    const long long best0 = (long long)T->eob[ctype][kBand(FIRST)][ctx0] * lam;
+    const long long t0 = (valid[0] && l0 != 0) ? s0 + eobc[0] : INF;
+    const long long t1 = valid[1] ? s1 + eobc[1] : INF;
+    long long bt = t1 < t0 ? t1 : t0;
+    int bi = 2 * n + (t1 < t0 ? 1 : 0);
+    argmin_step<0xB1>(bt, bi);   // quad xor 1
+    argmin_step<0x4E>(bt, bi);   // quad xor 2
+    argmin_step<0x141>(bt, bi);  // row half mirror
+    argmin_step<0x140>(bt, bi);  // row mirror
+    lvl = 0;
+    if (!(bt < best0)) return 0;  // the empty block wins (bn = -1)
+    const int bn = bi >> 1, bd = bi & 1;
+    // backtrack: cd_{n-1} = pb_n[cd_n], from (bn, bd)
+    const unsigned long long ball = __ballot(pb[0] != 0), ball1 = __ballot(pb[1] != 0);
+    const int gsh = __lane_id() & 48;
+    const unsigned pbm0 = (unsigned)(ball >> gsh) & 0xffffu, pbm1 = (unsigned)(ball1 >> gsh) & 0xffffu;
+    unsigned cdm = 0;
+    int cd = bd;
+    for (int k = bn; k >= FIRST; k--) {
+        cdm |= (unsigned)cd << k;
+        cd = (int)(((cd ? pbm1 : pbm0) >> k) & 1u);
+    }
+    const int level = (n >= FIRST && n <= bn) ? l0 + (int)((cdm >> n) & 1u) : 0;
+    lvl = sign ? -level : level;
+    return gmask(level != 0) != 0;
+}

@@ -1061,22 +1061,12 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             const int snz = gmask(qs != 0) != 0;
             int dqk, nzq;
             if (trel) {
-                if (l < 16) W->cres[0][5 + k] = ck;
-                wsync();
-                if (l == 0) {
-                    int c[16], lv[16];
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) c[kk] = W->cres[0][5 + kk];
-                    const int tnz = trellis<0>(c, lv, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0);
-#pragma unroll
-                    for (int n = 0; n < 16; n++) W->lev[i][n] = (int16_t)lv[n];
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) W->cres[0][5 + kk] = c[kk];
-                    W->misc[1] = tnz;
-                }
-                wsync();
-                dqk = W->cres[0][5 + k];
-                nzq = W->misc[1];
+                // lane-parallel trellis: lane n = zigzag position n
+                const int cn = gget(ck, zz_of(k));
+                int lvn;
+                nzq = trellis_g<0>(cn, k, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0, lvn);
+                if (l < 16) W->lev[i][k] = (int16_t)lvn;
+                dqk = m24(gget(lvn, izz_of(k)), (int)S.y1.q[k > 0]);
             } else {
                 if (l < 16) W->lev[i][izz_of(k)] = (int16_t)qs;
                 nzq = snz;
@@ -1536,12 +1526,48 @@ extern "C" __global__ __launch_bounds__(256) void k_quant_blocks(const int* __re
     }
 }
 
+// The lane-parallel trellis (trellis_g, used by the final I4 pass): 16 lanes
+// per block, lane = zigzag position.
+extern "C" __global__ __launch_bounds__(256) void k_quant_blocks_g(const int* __restrict__ coeffs,
+                                                                  const uint8_t* __restrict__ ctx0s,
+                                                                  const ZwLevelCosts* __restrict__ lcost,
+                                                                  const uint8_t* __restrict__ probs, QuantBlocksArgs a,
+                                                                  int* __restrict__ levels, int* __restrict__ dq)
+{
+    __shared__ LdsTables T;
+    for (int i = threadIdx.x; i < (int)(sizeof(T.lc) / 2); i += 256) (&T.lc[0][0][0][0])[i] = (&lcost->lc[0][0][0][0])[i];
+    for (int i = threadIdx.x; i < 96; i += 256) {
+        (&T.eob[0][0][0])[i] = (&lcost->eob[0][0][0])[i];
+        (&T.init[0][0][0])[i] = (&lcost->init[0][0][0])[i];
+    }
+    for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += 256) (&T.probs[0][0][0][0])[i] = probs[i];
+    load_static_tables(&T, threadIdx.x, 256, probs);
+    __syncthreads();
+    const int b = (int)((blockIdx.x * 256 + threadIdx.x) >> 4), n = threadIdx.x & 15;
+    const int bb = min(b, a.n - 1);  // whole groups stay active (DPP/ballot need every lane)
+    const int cn = coeffs[(size_t)bb * 16 + zz_of(n)];
+    const int ctx0 = ctx0s[bb];
+    int lvl;
+    if (a.first) (void)trellis_g<1>(cn, n, a.m, a.sharpen, a.lambda, &T, a.ctype, ctx0, lvl);
+    else (void)trellis_g<0>(cn, n, a.m, a.sharpen, a.lambda, &T, a.ctype, ctx0, lvl);
+    if (b < a.n) {
+        const int j = zz_of(n);
+        levels[(size_t)b * 16 + n] = lvl;
+        // positions before `first` keep their input coefficient (as trellis<1> leaves coeffs[0])
+        dq[(size_t)b * 16 + j] = n < a.first ? cn : lvl * (int)(j == 0 ? a.m.q[0] : a.m.q[1]);
+    }
+}
+
 extern "C" hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
                                        const uint8_t* probs, const void* args, int* levels, int* dq)
 {
     const QuantBlocksArgs& a = *(const QuantBlocksArgs*)args;
-    hipLaunchKernelGGL(k_quant_blocks, dim3((a.n + 255) / 256), dim3(256), 0, s, coeffs, ctx0s, lcost, probs, a, levels,
-                       dq);
+    if (a.trel == 2)
+        hipLaunchKernelGGL(k_quant_blocks_g, dim3((a.n * 16 + 255) / 256), dim3(256), 0, s, coeffs, ctx0s, lcost, probs,
+                           a, levels, dq);
+    else
+        hipLaunchKernelGGL(k_quant_blocks, dim3((a.n + 255) / 256), dim3(256), 0, s, coeffs, ctx0s, lcost, probs, a,
+                           levels, dq);
     return hipGetLastError();
 }
 

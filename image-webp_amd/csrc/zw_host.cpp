@@ -915,7 +915,7 @@ extern "C" int zw_quant_blocks(zw_ctx* ctx, int n, const int32_t* coeffs, const 
     a.lambda = lambda;
     a.ctype = ctype;
     a.first = first;
-    a.trel = use_trellis != 0;
+    a.trel = use_trellis == 2 ? 2 : use_trellis != 0;  // 2: the lane-parallel trellis
     a.n = n;
     uint8_t P[4][8][3][11];
     memcpy(P, probs ? probs : &zwh::COEFF_PROBS[0][0][0][0], sizeof P);

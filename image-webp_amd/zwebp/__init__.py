@@ -348,7 +348,8 @@ def quant_blocks(coeffs, ctx0, ctype, first, use_trellis, lambda_, q_dc, q_ac, m
     pr = None if probs is None else np.ascontiguousarray(probs, dtype=np.uint8).reshape(-1)
     lv = np.zeros((n, 16), np.int32)
     dq = np.zeros((n, 16), np.int32)
-    _check(c._lib.zw_quant_blocks(c.handle, n, _ptr(co), _ptr(cx), ctype, first, 1 if use_trellis else 0, lambda_,
+    ut = 2 if use_trellis == 2 else (1 if use_trellis else 0)  # 2: lane-parallel trellis kernel
+    _check(c._lib.zw_quant_blocks(c.handle, n, _ptr(co), _ptr(cx), ctype, first, ut, lambda_,
                                   q_dc, q_ac, matrix_type, _ptr(pr), _ptr(lv), _ptr(dq)), "quant_blocks")
     return lv, dq
 

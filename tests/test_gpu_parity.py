@@ -341,7 +341,7 @@ def test_1080p_encode_decode_roundtrip(ctx):
 # a7/a8: quantisation and trellis on independent blocks
 # --------------------------------------------------------------------------
 @pytest.mark.parametrize("ctype,first,mtype", [(3, 0, 0), (0, 1, 0), (2, 0, 2), (1, 0, 1)])
-@pytest.mark.parametrize("trel", [False, True])
+@pytest.mark.parametrize("trel", [False, True, 2])  # 2: lane-parallel trellis (trellis_g)
 @pytest.mark.parametrize("qi", [0, 10, 26, 60, 127])
 def test_quant_blocks(ctx, ctype, first, mtype, trel, qi):
     rng = np.random.default_rng(qi * 31 + ctype * 7 + first + trel)
@@ -355,7 +355,7 @@ def test_quant_blocks(ctx, ctype, first, mtype, trel, qi):
     lam = int(rng.integers(1, 5000))
     for pr in (None, probs):
         g = zwebp.quant_blocks(co, ctx0, ctype, first, trel, lam, dc_q, ac_q, mtype, pr, ctx=ctx)
-        o = O.quant_blocks(co, ctx0, ctype, first, trel, lam, dc_q, ac_q, mtype, pr)
+        o = O.quant_blocks(co, ctx0, ctype, first, bool(trel), lam, dc_q, ac_q, mtype, pr)
         bad = np.nonzero((g[0] != o[0]).any(axis=1))[0]
         assert bad.size == 0, f"{bad.size} blocks differ; first {co[bad[0]].tolist()} ctx {ctx0[bad[0]]}: " \
                               f"{g[0][bad[0]].tolist()} vs {o[0][bad[0]].tolist()}"
