@@ -848,3 +848,31 @@ DI int trellis_g(int cn, int n, const ZwMatrix& m, const uint16_t* sharpen, uint
     lvl = sign ? -level : level;
     return gmask(level != 0) != 0;
 }
+
+// 4-point Walsh-Hadamard butterflies in 16-lane group form (lane k = element k
+// of a 4x4 block, row k >> 2, column k & 3).  Row pass: out0 = a + b, out1 =
+// c + d, out2 = a - b, out3 = d - c with a = x0 + x3, b = x1 + x2, c = x1 - x2,
+// d = x0 - x3 (the pass shared by wht16's rows and iwht16's rows); column
+// pass: the same on the rows of a column.
+DI int hrow_g(int x, int j)
+{
+    const int r = qrev(x);
+    const int s = x + r, df = x - r;  // col0: a, d  col1: b, c  col2: b, -c  col3: a, -d
+    const int X = pin(qnext(s)), Y = pin(qprev(df));
+    return sel4(j, s + X, df + Y, X - s, Y - df);
+}
+DI int hcol_g(int x, int i)
+{
+    const int r = pin(rrev(x));
+    const int s = x + r, df = x - r;
+    const int X = pin(ror12(s)), Y = pin(ror4(df));  // row i + 1 / row i - 1
+    return sel4(i, s + X, df + Y, X - s, Y - df);
+}
+// wht16 (transform.rs:58): rows, then columns with (v + (v > 0)) / 2
+DI int wht_g(int x, int k)
+{
+    const int v = hcol_g(hrow_g(x, k & 3), k >> 2);
+    return (v + (v > 0 ? 1 : 0)) / 2;
+}
+// iwht16 (transform.rs:82): columns, then rows with (v + 3) >> 3
+DI int iwht_g(int x, int k) { return (hrow_g(hcol_g(x, k >> 2), k & 3) + 3) >> 3; }

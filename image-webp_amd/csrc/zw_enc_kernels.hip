@@ -418,7 +418,7 @@ struct WaveLds {
     int16_t lev[25][16];
     int misc[16];
 #ifdef ZW_PHASE_PROF
-    unsigned long long ph[16];
+    unsigned long long ph[24];
 #endif
 };
 
@@ -605,7 +605,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
 
 #ifdef ZW_PHASE_PROF
 // Per-phase cycle counters (profiling builds only): [pass-1][phase].
-__device__ unsigned long long zw_phase_cycles_dev[2][16];
+__device__ unsigned long long zw_phase_cycles_dev[2][24];
 #define PH_START() long long ph_t_ = clock64()
 #define PH_MARK(k) PH_MARK_L(k, lane, PASS)
 // accumulate in the wave's LDS slot; flushed once per kernel (ph_flush)
@@ -619,17 +619,23 @@ extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_phase_cycles_dev), sizeof(zw_phase_cycles_dev)) != hipSuccess) return -1;
     if (reset) {
-        static unsigned long long z[2][16];
+        static unsigned long long z[2][24];
         if (hipMemcpyToSymbol(HIP_SYMBOL(zw_phase_cycles_dev), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
 }
+#define PH_COUNT(k) \
+    do {                \
+        if (C.lane == 0) C.W->ph[k] += 1; \
+    } while (0)
 #elif defined(ZW_ASM_MARKS)
+#define PH_COUNT(k) (void)0
 // ISA inspection builds: phase boundaries as assembly comments
 #define PH_START() asm volatile("; ZWMARK start" ::: "memory")
 #define PH_MARK(k) asm volatile("; ZWMARK " #k ::: "memory")
 #define PH_MARK_L(k, ln, ps) asm volatile("; ZWMARK " #k ::: "memory")
 #else
+#define PH_COUNT(k) (void)0
 #define PH_START() (void)0
 #define PH_MARK(k) (void)0
 #define PH_MARK_L(k, ln, ps) (void)0
@@ -907,58 +913,55 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
     const ZwSegment& S = *C.S;
     const int l = C.lane;
     int anynz = 0;
+    PH_START();
     if (mode != 4) {
         build_luma_border(C);
         const uint8_t* ws = W->ws;
         const int above = C.mby != 0, left = C.mbx != 0;
-        int s = 0;
-        if (l < 16) s = above ? ws[1 + l] : 0;
-        else if (l < 32) s = left ? ws[(l - 15) * ZW_BPS] : 0;
-        s = wave_sum(s);
-        const int shf = 3 + above + left;
-        const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
-        int c[16], pr[16];
         const int b = l & 15, bx = b & 3, by = b >> 2;
-        // lanes 16..47 recompute their block's coefficients for the ctx-parallel trellis
-        if (l < (trel ? 48 : 16)) {
-            const int P0 = ws[0];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int y = by * 4 + i, x = bx * 4 + j;
-                    const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
-                    const int p = mode == 0 ? dcv : (mode == 1 ? T : (mode == 2 ? L : clamp255(L + T - P0)));
-                    pr[i * 4 + j] = p;
-                    c[i * 4 + j] = (int)C.sY[y * 16 + x] - p;
-                }
-            fdct16(c);
-            if (l < 16) W->dc[b] = c[0];
+        int dcv;
+        {  // DC predictor: lanes 0..15 top row, 16..31 left column
+            const int top = l < 16;
+            const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(l < 32 && (top ? above : left));
+            const int sum = red16(v);
+            const int su = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
+            const int shf = 3 + above + left;
+            dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
         }
-        wsync();
-        if (l == 0) {
-            int d[16];
+        int c[16], pr[16];
+        {
+            // every 16-lane group computes its block's coefficients (lanes 16..47
+            // feed the ctx-parallel trellis)
+            const int P0 = ws[0];
+            int L[4], Tp[4], r[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) d[k] = W->dc[k];
-            wht16(d);
-            int y2q[16];
-            int nz = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                y2q[k] = quantz(d[k], S.y2.iq[k > 0], S.y2.bias[k > 0]);
-                nz |= y2q[k] != 0;
+            for (int i = 0; i < 4; i++) {
+                L[i] = ws[(by * 4 + i + 1) * ZW_BPS];
+                Tp[i] = ws[1 + bx * 4 + i];
             }
 #pragma unroll
-            for (int n = 0; n < 16; n++) W->lev[16][n] = (int16_t)y2q[kZZ(n)];
+            for (int i = 0; i < 4; i++) {
+                const uint32_t srow = *(const uint32_t*)(C.sY + (by * 4 + i) * 16 + bx * 4);
 #pragma unroll
-            for (int k = 0; k < 16; k++) d[k] = m24(y2q[k], (int)S.y2.q[k > 0]);
-            iwht16(d);
-#pragma unroll
-            for (int k = 0; k < 16; k++) W->y2d[k] = d[k];
-            W->misc[0] = nz;
+                for (int j = 0; j < 4; j++) {
+                    const int p = sel4(mode, dcv, Tp[j], L[i], clamp255(L[i] + Tp[j] - P0));
+                    pr[i * 4 + j] = p;
+                    r[i * 4 + j] = (int)((srow >> (8 * j)) & 255u) - p;
+                }
+            }
+            fdct16_pk(r, c);
         }
-        wsync();
-        anynz = W->misc[0];
+        // Y2 (the 16 DCs) in group form: lane b holds block b's DC
+        int y2dq;
+        {
+            const int d = wht_g(c[0], b);
+            const int t = b > 0;
+            const int y2q = quantz(d, S.y2.iq[t], S.y2.bias[t]);
+            if (l < 16) W->lev[16][izz_of(b)] = (int16_t)y2q;
+            if (gmask(y2q != 0)) anynz = 1;
+            y2dq = iwht_g(m24(y2q, (int)S.y2.q[t]), b);
+        }
+        PH_MARK_L(16, l, 0);
         int dq[16], lv[16];
         int nzb = 0;
         {
@@ -980,6 +983,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                 for (int k = 0; k < 16; k++) dq[k] = c[k];
                 tnz = trellis<1>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, l >> 4);
             }
+            PH_MARK_L(17, l, 0);
             const unsigned long long nzm = __ballot(l < 48 && tnz);
             int nt[4], nl[4];
 #pragma unroll
@@ -1004,6 +1008,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
                 dq[k] = __shfl(dq[k], srcl);
             }
             nzb = (nzbits >> b) & 1u;
+            PH_MARK_L(18, l, 0);
         } else if (l < 16) {
 #pragma unroll
             for (int n = 1; n < 16; n++) {
@@ -1020,7 +1025,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             lv[0] = 0;
 #pragma unroll
             for (int n = 0; n < 16; n++) W->lev[b][n] = (int16_t)lv[n];
-            dq[0] = W->y2d[b];
+            dq[0] = y2dq;
             idct16(dq);
             uint8_t* wsp = W->ws;
 #pragma unroll
@@ -1031,6 +1036,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
         }
         for (int k = 0; k < 16; k++) y_nz_out[k] = __shfl(nzb, k);
         wsync();
+        PH_MARK_L(14, l, 0);
     } else {
         build_luma_border(C);
         int top_nz[4], left_nz[4];
@@ -1089,6 +1095,8 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
         }
         if (l < 16) W->lev[16][l] = 0;
         wsync();
+        PH_MARK_L(15, l, 0);
+        PH_COUNT(7);
     }
     return anynz;
 }
@@ -1331,10 +1339,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     const bool trel = PASS == 2 && P->do_trellis;
     const size_t nmb = (size_t)mbw * mbh;
 #ifdef ZW_PHASE_PROF
-    if (lane < 16) W->ph[lane] = 0;
+    if (lane < 24) W->ph[lane] = 0;
     wsync();
     auto ph_flush = [&]() {
-        if (lane < 16) atomicAdd(&zw_phase_cycles_dev[PASS - 1][lane], W->ph[lane]);
+        if (lane < 24) atomicAdd(&zw_phase_cycles_dev[PASS - 1][lane], W->ph[lane]);
     };
 #else
     auto ph_flush = []() {};

@@ -21,7 +21,9 @@ from zwebp.synth import synth_rgba  # noqa: E402
 
 NAMES = {0: "wait(row above)", 1: "border+pick_i16", 2: "pick_i4", 3: "pick_uv", 4: "final_luma",
          5: "final_chroma", 6: "store/levels/publish", 8: "p1 chroma pick_uv", 9: "p1 chroma final",
-         10: "  i4: values", 11: "  i4: preds+sse+rank", 12: "  i4: candidates", 13: "  i4: select+recon"}
+         10: "  i4: values", 11: "  i4: preds+sse+rank", 12: "  i4: candidates", 13: "  i4: select+recon",
+         7: "  (count of I4 MBs)", 14: "  final: I16 MBs", 15: "  final: I4 MBs",
+         16: "    i16: fdct+y2", 17: "    i16: quant check+trellis", 18: "    i16: ctx resolve+gather"}
 
 
 def main():
@@ -31,7 +33,7 @@ def main():
     m = int(sys.argv[4]) if len(sys.argv) > 4 else 4
     L = zwebp.load_library()
     L.zw_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 48)()
     p = zwebp.Pipeline(F, w, h, zwebp.ColorType.Rgba8, 75, m)
     imgs = [synth_rgba(w, h, 0x5EED0000 + i) for i in range(4)]
     for i in range(F):
@@ -47,10 +49,10 @@ def main():
     print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt[:4]]} "
           f"host(ms) fetch1/stats/fetch2/emit {[round(x, 2) for x in kt[4:8]]}")
     for ps in (0, 1):
-        tot = sum(buf[ps * 16 + k] for k in range(10)) or 1
+        tot = sum(buf[ps * 24 + k] for k in range(10) if k != 7) or 1
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
-        for k in range(16):
-            v = buf[ps * 16 + k]
+        for k in range(24):
+            v = buf[ps * 24 + k]
             if v:
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.0f} cyc/MB  {100 * v / tot:5.1f}%")
 
