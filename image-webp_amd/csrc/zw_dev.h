@@ -474,10 +474,18 @@ DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
 
 // trellis_quantize_block (cost.rs:788-1006).  coeffs (natural order) become the
 // dequantized values; out (zigzag) the levels.  Returns has_nz.
-template <int FIRST>
+// SMALL: every product is formed with full-rate 24-bit multiplies, exact for
+// the encoder's operands (|coeff| + sharpening < 2^12, lambda < 2^16, level
+// cost < 2^16); the general form (any int32 input) uses 32/64-bit multiplies.
+template <int FIRST, bool SMALL = false>
 DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen, uint32_t lambda,
                const LdsTables* T, int ctype, int ctx0)
 {
+    auto mul = [](int a, int b) -> int { return SMALL ? m24(a, b) : a * b; };
+    auto umul = [](uint32_t a, uint32_t b) -> uint32_t { return SMALL ? __umul24(a, b) : a * b; };
+    auto rate = [&](int r) -> long long {
+        return SMALL ? (long long)__umul24((uint32_t)r, lambda) : (long long)r * lambda;
+    };
     const long long MAXC = 0x3fffffffffffffffLL;
     const int qac = (int)m.q[1];
     const int thresh = (qac * qac) / 4;
@@ -485,12 +493,12 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
         int j = kZZ(n);
-        if (coeffs[j] * coeffs[j] > thresh) last = n;
+        if (mul(coeffs[j], coeffs[j]) > thresh) last = n;
     }
     if (last < 15) last++;
     const int bfirst = kBand(FIRST);
-    long long best = (long long)T->eob[ctype][bfirst][ctx0] * lambda;
-    long long init = ctx0 == 0 ? (long long)T->init[ctype][bfirst][ctx0] * lambda : 0;
+    long long best = rate(T->eob[ctype][bfirst][ctx0]);
+    long long init = ctx0 == 0 ? rate(T->init[ctype][bfirst][ctx0]) : 0;
     long long s0 = init, s1 = init;
     int c0 = ctx0, c1 = ctx0;  // ctx selecting the predecessor's cost table
     int bn = -1, bd = 0, bp = 0;
@@ -507,9 +515,10 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
             const uint32_t iq = j == 0 ? m.iq[0] : m.iq[1];
             const int sign = coeffs[j] < 0;
             const int cws = iabs(coeffs[j]) + sharpen[j];
-            int l0 = (int)(((uint32_t)cws * iq + nbias) >> 17);
+            const uint32_t prod = umul((uint32_t)cws, iq);
+            int l0 = (int)((prod + nbias) >> 17);
             l0 = l0 < 2047 ? l0 : 2047;
-            int thr = (int)(((uint32_t)cws * iq + tbias) >> 17);
+            int thr = (int)((prod + tbias) >> 17);
             thr = thr < 2047 ? thr : 2047;
             const int band = kBand(n);
             long long ns0 = MAXC, ns1 = MAXC;
@@ -521,13 +530,14 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
                 if (d == 0) nc0 = ctx;
                 else nc1 = ctx;
                 if (level <= thr) {
-                    const int ne = cws - level * q;
-                    const long long dd = (long long)kWTrellis(j) * ((long long)(ne * ne) - (long long)(cws * cws));
+                    const int ne = cws - mul(level, q);
+                    const long long dd = SMALL ? (long long)m24(kWTrellis(j), m24(ne, ne) - m24(cws, cws))
+                                               : (long long)kWTrellis(j) * ((long long)(ne * ne) - (long long)(cws * cws));
                     const long long base = 256 * dd;
                     const int lv = level < 67 ? level : 67;
                     const int fixed = T->lfc[level] + (level > 0 ? 256 : 0);
-                    long long sc0 = s0 + (long long)(fixed + T->lc[ctype][band][c0][lv]) * lambda;
-                    long long sc1 = s1 + (long long)(fixed + T->lc[ctype][band][c1][lv]) * lambda;
+                    long long sc0 = s0 + rate(fixed + T->lc[ctype][band][c0][lv]);
+                    long long sc1 = s1 + rate(fixed + T->lc[ctype][band][c1][lv]);
                     int pb = sc1 < sc0;
                     long long cur = (pb ? sc1 : sc0) + base;
                     prevbits |= (unsigned)pb << (2 * n + d);
@@ -535,7 +545,7 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
                     else ns1 = cur;
                     if (level != 0 && cur < best) {
                         long long eob = 0;
-                        if (n < 15) eob = (long long)T->eob[ctype][kBand(n + 1)][ctx] * lambda;
+                        if (n < 15) eob = rate(T->eob[ctype][kBand(n + 1)][ctx]);
                         long long term = cur + eob;
                         if (term < best) {
                             best = term;
@@ -568,7 +578,7 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
             const int level = lv0[n] + cd;
             const int v = sg[n] ? -level : level;
             out[n] = v;
-            coeffs[j] = v * (int)(j == 0 ? m.q[0] : m.q[1]);
+            coeffs[j] = mul(v, (int)(j == 0 ? m.q[0] : m.q[1]));
             nz |= v != 0;
             cd = (n == bn) ? bp : (int)((prevbits >> (2 * n + cd)) & 1);
         }

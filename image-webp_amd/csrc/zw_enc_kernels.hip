@@ -981,7 +981,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             if (l < 48) {
 #pragma unroll
                 for (int k = 0; k < 16; k++) dq[k] = c[k];
-                tnz = trellis<1>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, l >> 4);
+                tnz = trellis<1, true>(dq, lv, S.y1, S.sharpen, S.lt_i16, C.T, 0, l >> 4);
             }
             PH_MARK_L(17, l, 0);
             const unsigned long long nzm = __ballot(l < 48 && tnz);

@@ -53,7 +53,9 @@ def main():
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
         for k in range(24):
             v = buf[ps * 24 + k]
-            if v:
+            if v and k == 7:
+                print(f"   {NAMES.get(k, k):24s} {v / nmb:12.3f} of MBs")
+            elif v:
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.0f} cyc/MB  {100 * v / tot:5.1f}%")
 
 
