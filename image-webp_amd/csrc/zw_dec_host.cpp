@@ -457,9 +457,14 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     HIPOK(hipMemcpyAsync(d + o_mbs, mbs.data(), mbs.size() * sizeof(ZwDecMb), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
+    for (int e = 0; e < 3; e++)
+        if (!ctx->dev_ev[e]) HIPOK(hipEventCreate(&ctx->dev_ev[e]));
+    HIPOK(hipEventRecord(ctx->dev_ev[0], s));
     HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_mbs), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
                         csz, n));
+    HIPOK(hipEventRecord(ctx->dev_ev[1], s));
     HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
+    HIPOK(hipEventRecord(ctx->dev_ev[2], s));
     for (int i = 0; i < n; i++) {
         uint8_t* buf = (uint8_t*)malloc(ysz + 2 * csz);
         if (!buf) return ZW_ENOMEM;
@@ -480,6 +485,16 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         HIPOK(hipMemcpyAsync(o.v, d + o_v + (size_t)i * csz, csz, hipMemcpyDeviceToHost, s));
     }
     HIPOK(hipStreamSynchronize(s));
+    (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
+    (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
+    return ZW_OK;
+}
+
+extern "C" int zw_decode_kernel_times(zw_ctx* ctx, float* ms)
+{
+    if (!ctx || !ms) return ZW_EINVAL;
+    ms[0] = ctx->dec_ms[0];
+    ms[1] = ctx->dec_ms[1];
     return ZW_OK;
 }
 

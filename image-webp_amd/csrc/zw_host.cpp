@@ -149,6 +149,8 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->dscratch) (void)hipFree(c->dscratch);
+    for (hipEvent_t e : c->dev_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream_) (void)hipStreamDestroy(c->stream_);
     delete c;
 }

@@ -21,6 +21,9 @@ struct zw_ctx {
     // kernel holds every CU; the DMA engines need no CU.
     int sdma = -1;  // -1 unprobed, 0 unavailable, 1 ready
     hsa_agent_t gpu_agent{}, cpu_agent{};
+    // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter (ms)
+    hipEvent_t dev_ev[3] = {nullptr, nullptr, nullptr};
+    float dec_ms[2] = {0.f, 0.f};
 };
 
 #define HIPOK(x)                                  \

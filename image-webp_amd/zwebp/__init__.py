@@ -109,6 +109,7 @@ SIGNATURES = [
     ("zw_pipe_destroy", None, [_VP]),
     ("zw_pipe_input_device_ptr", _VP, [_VP]),
     ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
+    ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_run_pass1", _I, [_VP, _I]),
@@ -320,6 +321,14 @@ def decode_batch(frames, ctx=None):
     outs = (_Frame * n)()
     _check(L.zw_vp8_decode_batch(c.handle, n, ptrs, lens, outs), "decode_batch", DecodingError)
     return [_take_frame(L, outs[i]) for i in range(n)]
+
+
+def decode_kernel_times(ctx=None):
+    """Device ms of the last decode batch on `ctx`: (k_dec_recon, k_loopfilter)."""
+    c = _ctx(ctx)
+    ms = (ctypes.c_float * 2)()
+    _check(c._lib.zw_decode_kernel_times(c.handle, ms), "decode_kernel_times")
+    return float(ms[0]), float(ms[1])
 
 
 def rgb_to_yuv420(img, width, height, bpp, ctx=None):

@@ -97,6 +97,9 @@ int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, u
 int zw_vp8_decode_frame(zw_ctx *ctx, const uint8_t *vp8, size_t len, zw_frame *out);
 /* n independent decode_frame calls on frames of identical dimensions (new: batch). */
 int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, zw_frame *outs);
+/* Device time (HIP events on the context stream) of the last decode batch:
+ * ms[0] = k_dec_recon (dequant + iWHT/iDCT + prediction), ms[1] = k_loopfilter. */
+int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
 
 /* Kernel-level entry points (host buffers in/out) for parity testing. */
 int zw_rgb_to_yuv420(zw_ctx *ctx, const uint8_t *img, uint32_t width, uint32_t height, int bpp, uint8_t *y,
