@@ -71,6 +71,7 @@ struct ZwDecMb {
     uint32_t nz_mask;          // bit b: block b's token run was non-empty (0..15 Y, 16..19 U, 20..23 V)
     int16_t y2[16];            // Y2 levels, natural order (luma_mode != 4 && !skip)
     int16_t coeffs[24][16];    // levels, natural order; dequantised on the device
+    uint32_t pad[2];           // 832 B: whole 16-byte lines (one coalesced load per lane)
 };
 
 // Loop-filter parameters per segment x {i16, i4} (calculate_filter_parameters,

@@ -22,6 +22,8 @@ struct ZwDecQuant {
 };
 
 struct DecLds {
+    uint4 rec[52];  // the current MB's ZwDecMb record (832 B), prefetched one MB ahead
+    uint8_t i4idx[10][16];
     uint8_t ws[17 * ZW_BPS];
     uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
     uint8_t left_y[20], left_u[12], left_v[12];
@@ -67,7 +69,7 @@ __device__ void dec_i4_values(DecLds* W, int lane, int x0, int y0)
 }
 __device__ __forceinline__ int dec_i4_px(const DecLds* W, int mode, int p)
 {
-    const int idx = d_I4_IDX[mode][p];
+    const int idx = W->i4idx[mode][p];
     if (idx == 255) return W->V[38];
     if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
     return W->V[idx];
@@ -85,7 +87,7 @@ __device__ __forceinline__ void dec_block_residual(int* c, int nz)
     }
 }
 
-extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
+extern "C" __global__ __launch_bounds__(WGD, 2) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
                                                               size_t csz)
@@ -103,19 +105,27 @@ extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __r
     off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
     uint8_t* top_v = smem + off;
     DecLds* W = (DecLds*)((uint8_t*)Wall + ((sizeof(DecLds) + 15) & ~(size_t)15) * wv);
+    for (int i = lane; i < 160; i += 64) (&W->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WGD) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WGD) top_u[i] = top_v[i] = 127;
     if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
     __syncthreads();
     const int ys = mbw * 16, cs = mbw * 8;
     const size_t nmb = (size_t)mbw * mbh;
+    const uint4* recs = (const uint4*)mbs;  // 52 lines per record
     for (int mby = wv; mby < mbh; mby += NWD) {
         if (lane < 20) W->left_y[lane] = 129;
         if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
         wsync();
+        uint4 nxt = {0u, 0u, 0u, 0u};
+        if (lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw) * 52 + lane];
         for (int mbx = 0; mbx < mbw; mbx++) {
+            const uint4 cur = nxt;
+            if (mbx + 1 < mbw && lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 52 + lane];
             if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            const ZwDecMb& M = mbs[(size_t)f * nmb + (size_t)mby * mbw + mbx];
+            if (lane < 52) W->rec[lane] = cur;
+            wsync();
+            const ZwDecMb& M = *(const ZwDecMb*)W->rec;
             const ZwDecQuant& Q = quant[(size_t)f * 4 + M.segment];
             const int lm = M.luma_mode;
             // --- luma border (create_border_luma) ---
@@ -135,32 +145,25 @@ extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __r
             wsync();
             int nzdct = 0;
             if (lm != 4) {
-                if (lane == 0) {
-                    int d[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) d[k] = 0;
-                    if (!M.skip) {
-#pragma unroll
-                        for (int k = 0; k < 16; k++) d[k] = (int)M.y2[k] * (k ? Q.y2ac : Q.y2dc);
-                        iwht16(d);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 16; k++) W->dc[k] = d[k];
-                }
-                wsync();
-                // DC predictor sum
+                // Y2 in group form: lane b holds block b's DC after the iWHT (zero when skipped)
+                const int b = lane & 15, bx = b & 3, by = b >> 2;
+                const int y2v = M.skip ? 0 : (int)M.y2[b] * (b ? Q.y2ac : Q.y2dc);
+                const int dcb = iwht_g(y2v, b);
+                // DC predictor sum: lanes 0..15 top row, 16..31 left column
                 const int above = mby != 0, left = mbx != 0;
-                int s = 0;
-                if (lane < 16) s = above ? ws[1 + lane] : 0;
-                else if (lane < 32) s = left ? ws[(lane - 15) * ZW_BPS] : 0;
-                s = wave_sum(s);
-                const int shf = 3 + above + left;
-                const int dcv = (!above && !left) ? 128 : ((s + (1 << (shf - 1))) >> shf);
+                int dcv;
+                {
+                    const int top = lane < 16;
+                    const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(lane < 32 && (top ? above : left));
+                    const int sum = red16(v);
+                    const int su = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
+                    const int shf = 3 + above + left;
+                    dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
+                }
                 int blocknz = 0;
                 if (lane < 16) {
-                    const int b = lane, bx = b & 3, by = b >> 2;
                     int c[16];
-                    c[0] = W->dc[b];
+                    c[0] = dcb;
 #pragma unroll
                     for (int k = 1; k < 16; k++) c[k] = (int)M.coeffs[b][k] * Q.yac;
                     const int nz = (M.nz_mask >> b) & 1;
@@ -184,25 +187,19 @@ extern "C" __global__ __launch_bounds__(WGD) void k_dec_recon(const ZwDecMb* __r
                 nzdct |= __any(blocknz) ? 1 : 0;
                 wsync();
             } else {
+                // group form: lane k = coefficient k of the sub-block (all four groups alike)
+                const int k = lane & 15;
                 for (int i = 0; i < 16; i++) {
                     const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
                     dec_i4_values(W, lane, x0, y0);
-                    if (lane == 0) {
-                        int c[16];
-#pragma unroll
-                        for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
-                        const int nz = (M.nz_mask >> i) & 1;
-                        W->misc[0] = (c[0] != 0) || nz;
-                        dec_block_residual(c, nz);
-#pragma unroll
-                        for (int k = 0; k < 16; k++) W->res[k] = c[k];
-                    }
-                    wsync();
-                    nzdct |= W->misc[0];
-                    if (lane < 16) {
-                        const int v = clamp255(dec_i4_px(W, M.bpred[i], lane) + W->res[lane]);
-                        ws[(y0 + (lane >> 2)) * ZW_BPS + x0 + (lane & 3)] = (uint8_t)v;
-                    }
+                    const int c = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
+                    const int nz = (M.nz_mask >> i) & 1;
+                    const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
+                    const int full = idct_g_exact(c, k);
+                    const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
+                    nzdct |= nz || c0 != 0;
+                    const int v = clamp255(dec_i4_px(W, M.bpred[i], k) + r);
+                    if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
                     wsync();
                 }
             }
@@ -364,12 +361,17 @@ struct LfLds {
     uint8_t u[LFC * LFC], v[LFC * LFC];
 };
 
+// Per wave, row by row: the MB's 16x16 / 8x8 interiors only change when the
+// MB itself is filtered, so they are prefetched into registers one MB ahead;
+// the left 4 columns (with the corner) are carried over in LDS from the
+// previous MB's tile; only the 4 rows above come from global memory after the
+// wait on the row above.  Every tile is written back whole.
 extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8_t* U, uint8_t* V,
                                                                const uint8_t* __restrict__ flags,
                                                                const ZwFilterParams* __restrict__ fp, size_t ysz,
                                                                size_t csz)
 {
-    __shared__ LfLds lds[NWD];
+    __shared__ __attribute__((aligned(16))) LfLds lds[NWD];
     __shared__ int progress[NWD];
     const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const ZwFilterParams& F = fp[f];
@@ -381,31 +383,56 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
     uint8_t* Yf = Y + (size_t)f * ysz;
     uint8_t* Uf = U + (size_t)f * csz;
     uint8_t* Vf = V + (size_t)f * csz;
+    const bool chroma = !F.filter_type;
+    // interior lanes: luma row lane>>2, word lane&3; chroma (lanes 0..31) plane lane>>4, row (lane>>1)&7, word lane&1
+    const int iy_r = lane >> 2, iy_w = lane & 3;
+    const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
+    auto load_interior = [&](int mby, int mbx, uint32_t& py, uint32_t& pc) {
+        py = *(const uint32_t*)(Yf + (size_t)(mby * 16 + iy_r) * ys + mbx * 16 + 4 * iy_w);
+        pc = 0;
+        if (chroma && lane < 32)
+            pc = *(const uint32_t*)((ic_p ? Vf : Uf) + (size_t)(mby * 8 + ic_r) * cs + mbx * 8 + 4 * ic_w);
+    };
     for (int mby = wv; mby < mbh; mby += NWD) {
+        uint32_t ny, nc;
+        load_interior(mby, 0, ny, nc);
+        uint32_t nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw) * 4);
         for (int mbx = 0; mbx < mbw; mbx++) {
+            const uint32_t cy = ny, cc = nc, fl = nfl;
+            if (mbx + 1 < mbw) {
+                load_interior(mby, mbx + 1, ny, nc);
+                nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 4);
+            }
             if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            const uint8_t* fl = flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4;
-            const int i4 = fl[0] == 4, seg = fl[1], skip = fl[2], nzd = fl[3];
+            const int i4 = (fl & 255) == 4, seg = (fl >> 8) & 255, skip = (fl >> 16) & 255, nzd = fl >> 24;
             const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
+            const int x0 = mbx * 16, y0 = mby * 16;
+            // ---- assemble the tile ----
+            if (mbx > 0) {  // left 4 columns (rows -4..15) from the previous tile's columns 12..15
+                if (lane < LFY) {
+                    uint32_t* row = (uint32_t*)(L->y + lane * LFY);
+                    row[0] = row[4];
+                }
+                if (chroma && lane >= 32 && lane < 32 + 2 * LFC) {
+                    const int pl = (lane - 32) / LFC, r = (lane - 32) % LFC;
+                    uint32_t* row = (uint32_t*)((pl ? L->v : L->u) + r * LFC);
+                    row[0] = row[2];
+                }
+            }
+            ((uint32_t*)(L->y + (4 + iy_r) * LFY + 4))[iy_w] = cy;
+            if (chroma && lane < 32) ((uint32_t*)((ic_p ? L->v : L->u) + (4 + ic_r) * LFC + 4))[ic_w] = cc;
+            if (mby > 0) {  // the 4 rows above: luma lanes 0..15 (row lane>>2), chroma lanes 32..47
+                if (lane < 16) {
+                    const int r = lane >> 2, w = lane & 3;
+                    ((uint32_t*)(L->y + r * LFY + 4))[w] = *(const uint32_t*)(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
+                } else if (chroma && lane >= 32 && lane < 48) {
+                    const int t = lane - 32, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
+                    ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] =
+                        *(const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
+                }
+            }
+            wsync();
             if (lvl != 0) {
-                const int x0 = mbx * 16, y0 = mby * 16;
-                // stage (rows/cols outside the frame are never touched by the filters)
-                for (int k = lane; k < LFY * LFY; k += 64) {
-                    const int r = k / LFY - 4, c = k % LFY - 4;
-                    const int gy = y0 + r, gx = x0 + c;
-                    if (gy >= 0 && gx >= 0) L->y[k] = Yf[(size_t)gy * ys + gx];
-                }
-                if (!F.filter_type) {
-                    for (int k = lane; k < LFC * LFC; k += 64) {
-                        const int r = k / LFC - 4, c = k % LFC - 4;
-                        const int gy = mby * 8 + r, gx = mbx * 8 + c;
-                        if (gy >= 0 && gx >= 0) {
-                            L->u[k] = Uf[(size_t)gy * cs + gx];
-                            L->v[k] = Vf[(size_t)gy * cs + gx];
-                        }
-                    }
-                }
-                wsync();
                 const int mbe = (lvl + 2) * 2 + il, sube = lvl * 2 + il;
                 const int inner = i4 || (!skip && nzd);
                 // lane roles: 0..15 luma line, 16..23 U line, 24..31 V line
@@ -413,7 +440,7 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
                 const int li = isy ? lane : (lane - 16) & 7;
                 uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
                 const int W_ = isy ? LFY : LFC;
-                const bool act = isy || (!F.filter_type && (isu || isv));
+                const bool act = isy || (chroma && (isu || isv));
                 // left MB edge (vertical edge, filter along rows)
                 if (mbx > 0 && act) {
                     uint8_t* p = buf + (li + 4) * W_ + 4;
@@ -451,20 +478,18 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
                         wsync();
                     }
                 }
-                // write back
-                for (int k = lane; k < LFY * LFY; k += 64) {
-                    const int r = k / LFY - 4, c = k % LFY - 4;
-                    const int gy = y0 + r, gx = x0 + c;
-                    if (gy >= 0 && gx >= 0) Yf[(size_t)gy * ys + gx] = L->y[k];
+                // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame)
+                for (int t = lane; t < LFY * 5; t += 64) {
+                    const int r = t / 5 - 4, w = t % 5 - 1;
+                    if (y0 + r >= 0 && x0 + 4 * w >= 0)
+                        *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1];
                 }
-                if (!F.filter_type) {
-                    for (int k = lane; k < LFC * LFC; k += 64) {
-                        const int r = k / LFC - 4, c = k % LFC - 4;
-                        const int gy = mby * 8 + r, gx = mbx * 8 + c;
-                        if (gy >= 0 && gx >= 0) {
-                            Uf[(size_t)gy * cs + gx] = L->u[k];
-                            Vf[(size_t)gy * cs + gx] = L->v[k];
-                        }
+                if (chroma) {
+                    for (int t = lane; t < 2 * LFC * 3; t += 64) {
+                        const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+                        if (mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
+                            *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) =
+                                ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1];
                     }
                 }
             }

@@ -886,3 +886,41 @@ DI int wht_g(int x, int k)
 }
 // iwht16 (transform.rs:82): columns, then rows with (v + 3) >> 3
 DI int iwht_g(int x, int k) { return (hrow_g(hcol_g(x, k >> 2), k & 3) + 3) >> 3; }
+
+// idct16_exact (SSE2 i16 semantics, transform_simd_intrinsics.rs:478) in
+// 16-lane group form: the butterfly of idct_g with every intermediate wrapped
+// to i16, the multiplies as _mm_mulhi_epi16 and the input saturated.
+DI int idct_g_exact(int x, int k)
+{
+    const int i = k >> 2, j = k & 3;
+    x = sat16(x);
+    {
+        const int o = pin(ror8(x));  // row i+2
+        const bool even = (i & 1) == 0;
+        const int x0 = csel(i == 0, x, o), x2 = csel(i == 0, o, x);
+        const int x1 = csel(i == 1, x, o), x3 = csel(i == 1, o, x);
+        const int a = w16(x0 + x2), bb = w16(x0 - x2);
+        const int c = w16(w16(x1 - x3) + w16(mulhi16(x1, -30068) - mulhi16(x3, 20091)));
+        const int d = w16(w16(x1 + x3) + w16(mulhi16(x1, 20091) + mulhi16(x3, -30068)));
+        const int p = csel(even, a, d), q = csel(even, bb, c);
+        const int send = csel(i == 0 || i == 3, q, p);
+        const int nb = csel(even, pin(ror12(send)), pin(ror4(send)));
+        const int base = csel(i == 0 || i == 3, p, q);
+        x = w16(csel(i == 3, -base, base) + csel(i == 2, -nb, nb));
+    }
+    {
+        x = csel(j == 0, w16(x + 4), x);  // dc = y0 + 4
+        const int o = pin(qxor2(x));
+        const bool even = (j & 1) == 0;
+        const int y0 = csel(j == 0, x, o), y2 = csel(j == 0, o, x);
+        const int y1 = csel(j == 1, x, o), y3 = csel(j == 1, o, x);
+        const int a = w16(y0 + y2), bb = w16(y0 - y2);
+        const int c = w16(w16(y1 - y3) + w16(mulhi16(y1, -30068) - mulhi16(y3, 20091)));
+        const int d = w16(w16(y1 + y3) + w16(mulhi16(y1, 20091) + mulhi16(y3, -30068)));
+        const int p = csel(even, a, d), q = csel(even, bb, c);
+        const int send = csel(j == 0 || j == 3, q, p);
+        const int nb = csel(even, pin(qnext(send)), pin(qprev(send)));
+        const int base = csel(j == 0 || j == 3, p, q);
+        return w16(csel(j == 3, -base, base) + csel(j == 2, -nb, nb)) >> 3;
+    }
+}
