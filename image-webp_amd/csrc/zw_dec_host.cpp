@@ -431,7 +431,11 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     if (mbw == 0 || mbh == 0) return ZW_EINVALID_DIMENSIONS;
     const size_t nmb = (size_t)mbw * mbh;
     const size_t ysz = nmb * 256, csz = nmb * 64;
-    std::vector<ZwDecMb> mbs((size_t)n * nmb);
+    // MB records land in pinned memory (parse_mbs writes every record; no
+    // value-initialisation of the whole batch) for a DMA upload
+    const size_t rec_bytes = (size_t)n * nmb * sizeof(ZwDecMb);
+    ZwDecMb* mbs = (ZwDecMb*)ctx_pinned(ctx, 0, rec_bytes);
+    if (!mbs) return ZW_ENOMEM;
     std::vector<DecQuant> quant((size_t)n * 4);
     std::vector<ZwFilterParams> fps(n);
     parallel_for(n, [&](int i) {
@@ -445,7 +449,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         if (rc[i] != ZW_OK) return rc[i];
 
     HIPOK(hipSetDevice(ctx->device));
-    const size_t o_mbs = 0, o_q = al256(o_mbs + mbs.size() * sizeof(ZwDecMb));
+    const size_t o_mbs = 0, o_q = al256(o_mbs + rec_bytes);
     const size_t o_fp = al256(o_q + quant.size() * sizeof(DecQuant));
     const size_t o_fl = al256(o_fp + fps.size() * sizeof(ZwFilterParams));
     const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
@@ -454,7 +458,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
     hipStream_t s = ctx_stream(ctx);
-    HIPOK(hipMemcpyAsync(d + o_mbs, mbs.data(), mbs.size() * sizeof(ZwDecMb), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_mbs, mbs, rec_bytes, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
     for (int e = 0; e < 3; e++)
@@ -465,9 +469,35 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     HIPOK(hipEventRecord(ctx->dev_ev[1], s));
     HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
     HIPOK(hipEventRecord(ctx->dev_ev[2], s));
+    // planes down through pinned staging (one DMA per plane set), then fanned out
+    const size_t fsz = ysz + 2 * csz;
+    uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fsz);
+    if (!hout) return ZW_ENOMEM;
+    HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
+    {
+        int r = ctx_d2h(ctx, hout, d + o_y, (size_t)n * ysz);
+        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * ysz, d + o_u, (size_t)n * csz);
+        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * (ysz + csz), d + o_v, (size_t)n * csz);
+        if (r) return r;
+    }
+    std::vector<int> oom(n, 0);
+    parallel_for(n, [&](int i) {
+        uint8_t* buf = (uint8_t*)malloc(fsz);
+        if (!buf) {
+            oom[i] = 1;
+            return;
+        }
+        memcpy(buf, hout + (size_t)i * ysz, ysz);
+        memcpy(buf + ysz, hout + (size_t)n * ysz + (size_t)i * csz, csz);
+        memcpy(buf + ysz + csz, hout + (size_t)n * (ysz + csz) + (size_t)i * csz, csz);
+        outs[i].y = buf;
+    });
     for (int i = 0; i < n; i++) {
-        uint8_t* buf = (uint8_t*)malloc(ysz + 2 * csz);
-        if (!buf) return ZW_ENOMEM;
+        if (oom[i]) {
+            for (int k = 0; k < n; k++) zw_frame_free(&outs[k]);
+            return ZW_ENOMEM;
+        }
+        uint8_t* buf = outs[i].y;
         zw_frame& o = outs[i];
         o.width = (uint16_t)F[i].width;
         o.height = (uint16_t)F[i].height;
@@ -480,11 +510,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         o.filter_type = (uint8_t)F[i].filter_type;
         o.filter_level = (uint8_t)F[i].filter_level;
         o.sharpness_level = (uint8_t)F[i].sharpness;
-        HIPOK(hipMemcpyAsync(o.y, d + o_y + (size_t)i * ysz, ysz, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(o.u, d + o_u + (size_t)i * csz, csz, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(o.v, d + o_v + (size_t)i * csz, csz, hipMemcpyDeviceToHost, s));
     }
-    HIPOK(hipStreamSynchronize(s));
     (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
     (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
     return ZW_OK;

@@ -151,6 +151,8 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (c->dscratch) (void)hipFree(c->dscratch);
     for (hipEvent_t e : c->dev_ev)
         if (e) (void)hipEventDestroy(e);
+    for (void* h : c->hpin)
+        if (h) (void)hipHostFree(h);
     if (c->stream_) (void)hipStreamDestroy(c->stream_);
     delete c;
 }

@@ -21,6 +21,9 @@ struct zw_ctx {
     // kernel holds every CU; the DMA engines need no CU.
     int sdma = -1;  // -1 unprobed, 0 unavailable, 1 ready
     hsa_agent_t gpu_agent{}, cpu_agent{};
+    // grow-only pinned host staging (decode batch: MB records up, planes down)
+    void* hpin[2] = {nullptr, nullptr};
+    size_t hpin_cap[2] = {0, 0};
     // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter (ms)
     hipEvent_t dev_ev[3] = {nullptr, nullptr, nullptr};
     float dec_ms[2] = {0.f, 0.f};
@@ -95,3 +98,16 @@ static inline hipStream_t ctx_stream(zw_ctx* c)
 // HSA agents cannot be resolved).  `src` must have been released by the
 // producing kernel (event-complete) before the call.
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
+
+// Pinned host staging buffer `which` of at least `bytes` owned by the context.
+static inline void* ctx_pinned(zw_ctx* c, int which, size_t bytes)
+{
+    if (c->hpin_cap[which] < bytes) {
+        if (c->hpin[which]) (void)hipHostFree(c->hpin[which]);
+        c->hpin[which] = nullptr;
+        c->hpin_cap[which] = 0;
+        if (hipHostMalloc(&c->hpin[which], bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+        c->hpin_cap[which] = bytes;
+    }
+    return c->hpin[which];
+}

@@ -34,6 +34,25 @@ def main():
     el, rk, lf = best
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * F
     gbs = DEC_BYTES_PER_MB * nmb / ((rk + lf) * 1e-3) / 1e9
+    # single frame (SURVEY config 3): end to end, and the oracle's CPU decode of the same stream
+    one = [vp8[0]]
+    zwebp.decode_batch(one, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        zwebp.decode_batch(one, ctx=ctx)
+    el1 = (time.perf_counter() - t0) / 5
+    rk1, lf1 = zwebp.decode_kernel_times(ctx=ctx)
+    cpu = None
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        t0 = time.perf_counter()
+        O.decode(bytes(one[0]))
+        cpu = time.perf_counter() - t0
+    except Exception as e:  # noqa: BLE001 - the oracle is optional here
+        print("oracle decode unavailable:", e)
+    print(f"single frame: {el1 * 1e3:.2f} ms end to end (kernels {rk1:.2f} + {lf1:.2f} ms)"
+          + (f"; oracle CPU decode {cpu * 1e3:.1f} ms (1 thread)" if cpu else ""))
     print(f"{F} frames: wall {el * 1e3:.1f} ms = {F / el:.0f} decodes/s (host parse + PCIe both ways); "
           f"kernels recon {rk:.2f} ms + loopfilter {lf:.2f} ms = {F / ((rk + lf) * 1e-3):.0f} frames/s, "
           f"{gbs:.0f} GB/s ({gbs / 8000:.3f} of HBM peak)")
