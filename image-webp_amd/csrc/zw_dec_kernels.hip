@@ -14,7 +14,10 @@
 // overlapping access happen in raster order, as in the reference.
 #include "zw_dev.h"
 
-#define NWD 8
+#ifndef ZW_NWD
+#define ZW_NWD 16  // 16 rows of the x+2y wavefront in flight per frame
+#endif
+#define NWD ZW_NWD
 #define WGD (NWD * 64)
 
 struct ZwDecQuant {
@@ -87,7 +90,7 @@ __device__ __forceinline__ void dec_block_residual(int* c, int nz)
     }
 }
 
-extern "C" __global__ __launch_bounds__(WGD, 2) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
+extern "C" __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
                                                               size_t csz)
