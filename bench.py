@@ -132,6 +132,43 @@ def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
             "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": byts}
 
 
+def decode_path(ctx, streams, frames, w, h, with_cpu):
+    """SURVEY config 3: the decode path on this GPU.  Host bool decoding + MB
+    records up, k_dec_recon (dequant, iWHT/iDCT, prediction) + k_loopfilter,
+    planes down.  Single frame end to end, plus a batch for the kernels'
+    throughput; algorithmic bytes 1208 B/MB (levels 800 + side info 24 + YUV 384)."""
+    import zwebp
+    one = [streams[0]]
+    zwebp.decode_batch(one, ctx=ctx)
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        zwebp.decode_batch(one, ctx=ctx)
+    single_ms = (time.perf_counter() - t0) / reps * 1e3
+    rk1, lf1 = zwebp.decode_kernel_times(ctx=ctx)
+    batch = [streams[i % len(streams)] for i in range(frames)]
+    zwebp.decode_batch(batch, ctx=ctx)  # warm-up: grows the pinned staging buffers
+    t0 = time.perf_counter()
+    zwebp.decode_batch(batch, ctx=ctx)
+    el = time.perf_counter() - t0
+    rk, lf = zwebp.decode_kernel_times(ctx=ctx)
+    nmb = ((w + 15) // 16) * ((h + 15) // 16) * frames
+    ach = 1208 * nmb / ((rk + lf) * 1e-3) / 1e9
+    out = {"single_frame_ms": single_ms, "single_frame_kernel_ms": {"k_dec_recon": rk1, "k_loopfilter": lf1},
+           "batch_frames": frames, "batch_decodes_per_s": frames / el,
+           "batch_kernel_ms": {"k_dec_recon": rk, "k_loopfilter": lf},
+           "kernel_frames_per_s": frames / ((rk + lf) * 1e-3),
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                        "alg_bytes_per_mb": 1208}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        t0 = time.perf_counter()
+        O.decode(bytes(one[0]))
+        out["cpu_baseline_single_frame_ms"] = (time.perf_counter() - t0) * 1e3
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,6 +227,8 @@ def main():
         per_launch = pipe.launch_frames  # frames covered by one k_encode_pass2 launch (one lane chunk)
         achieved = ALG_BYTES_PER_MB * nmb * per_launch / (p2_ms * 1e-3) / 1e9 if p2_ms > 0 else 0.0
         dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
+        dec = decode_path(ctx, [bytes(pipe.output(i)) for i in range(min(F, 4))], 256, w, h,
+                          not a.no_cpu_baseline)
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
@@ -216,6 +255,7 @@ def main():
                          "alg_bytes_per_launch": dq["alg_bytes_per_launch"], "ms_per_launch": dq["ms_per_launch"],
                          "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"},
             "cpu_baseline": cpu,
+            "decode_path": dec,
             "encode_kernel": {"kernel": "k_encode_pass2", "bound": "valu", "hbm_achieved": achieved,
                               "hbm_frac": achieved / HBM_PEAK_GBS, "unit": "GB/s",
                               "alg_bytes_per_launch": ALG_BYTES_PER_MB * nmb * per_launch,
