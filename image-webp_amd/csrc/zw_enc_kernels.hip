@@ -525,7 +525,6 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
         }
     }
     fdct16_pk(r, c);
-    W->dc[m * 16 + b] = c[0];
     int aq[16], dq[16];
     aq[0] = 0;
     int nzac = 0;
@@ -537,26 +536,16 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     }
     nzac = nzac != 0;
     int cost = (int)rcost_bf<1>(aq, 0, 0, T);
-    wsync();
-    if (b == 0) {
-        int d[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) d[k] = W->dc[m * 16 + k];
-        wht16(d);
-        int ay[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int t = k > 0;
-            ay[k] = (int)((__umul24((uint32_t)iabs(d[k]), S.y2.iq[t]) + S.y2.bias[t]) >> 17);
-            d[k] = m24(d[k] < 0 ? -ay[k] : ay[k], (int)S.y2.q[t]);
-        }
-        W->y2cost[m] = (int)rcost_bf<0>(ay, 0, 1, T);
-        iwht16(d);
-#pragma unroll
-        for (int k = 0; k < 16; k++) W->y2d[m * 16 + k] = d[k];
+    // Y2 in group form: lane (m, b) holds block b's DC under mode m
+    int y2cost;
+    {
+        const int d = wht_g(c[0], b);
+        const int t = b > 0;
+        const int ay = (int)((__umul24((uint32_t)iabs(d), S.y2.iq[t]) + S.y2.bias[t]) >> 17);
+        const int qy = d < 0 ? -ay : ay;
+        y2cost = (int)rcost_g<0>(qy, b, 0, 1, T);  // uniform within the mode's group
+        dq[0] = iwht_g(m24(qy, (int)S.y2.q[t]), b);
     }
-    wsync();
-    dq[0] = W->y2d[m * 16 + b];
     idct16(dq);
     int rec[16], sse = 0, flat = 1;
     const int s00 = C.sY[0];
@@ -575,7 +564,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
     flat = red16(flat);
     // per mode (uniform within the 16-lane group), decided on the scalar unit
     const int srcflat = __builtin_amdgcn_readlane(flat, 0) == 16;  // mode-0 group covers all 256 pixels
-    cost += W->y2cost[m];
+    cost += y2cost;
     int sd = S.tlambda > 0 ? ((int)S.tlambda * td + 128) >> 8 : 0;
     int dfin = sse;
     if (srcflat && nzac == 0) {
