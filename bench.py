@@ -181,11 +181,16 @@ def main():
     from zwebp.shard import frame_seed, reduce_max
     from zwebp.synth import synth_rgba
 
+    # ZW_BENCH_BACKEND / ZW_BENCH_DEVICE: rehearsal of the N>1 path on fewer GPUs
+    # (e.g. gloo with every rank on device 0); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("ZW_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("ZW_BENCH_DEVICE", str(local)))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    red_dev = dev if backend == "nccl" else None
 
     w, h, F = a.width, a.height, a.frames
     ctx = zwebp.Context(local)
@@ -197,6 +202,7 @@ def main():
     nmb = pipe.mbw * pipe.mbh
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -217,7 +223,7 @@ def main():
         kt += np.array(pipe.kernel_times()) * a.steps
     barrier()
     el = time.perf_counter() - t0
-    el = reduce_max(el, dev)
+    el = reduce_max(el, red_dev)
     total_frames = F * a.steps * world
     bytes_out = sum(len(pipe.output(i)) for i in range(min(F, 4)))
 
