@@ -83,28 +83,14 @@ extern "C" __global__ void k_rgb2yuv(const uint8_t* __restrict__ img, int w, int
 // pixels; on the MB-padded planes libwebp's import/replicate rules reduce to
 // direct reads (analysis.rs:520-745).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void fdct_analysis(int* d, int16_t* out)
-{
-    int tmp[16];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        int d0 = d[i * 4], d1 = d[i * 4 + 1], d2 = d[i * 4 + 2], d3 = d[i * 4 + 3];
-        int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
-        tmp[0 + i * 4] = (a0 + a1) * 8;
-        tmp[2 + i * 4] = (a0 - a1) * 8;
-        tmp[1 + i * 4] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
-        tmp[3 + i * 4] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        int a0 = tmp[i] + tmp[12 + i], a1 = tmp[4 + i] + tmp[8 + i];
-        int a2 = tmp[4 + i] - tmp[8 + i], a3 = tmp[i] - tmp[12 + i];
-        out[i] = (int16_t)((a0 + a1 + 7) >> 4);
-        out[8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
-        out[4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0 ? 1 : 0));
-        out[12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
-    }
-}
+// One wave per MB: the MB and its edge pixels staged in LDS.
+struct AnalysisTile {
+    uint32_t y[16][4];     // luma rows, 4 packed pixels per word
+    uint32_t c[2][8][2];   // U, V rows
+    uint32_t ytop[4], ctop[2][2];
+    uint8_t yleft[16], cleft[2][8];
+    uint8_t corner[4];     // Y, U, V
+};
 
 extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
                                                              const uint8_t* __restrict__ V, int mbw, int mbh,
@@ -112,6 +98,7 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
                                                              uint32_t* __restrict__ histo)
 {
     __shared__ uint32_t hist[4][4][32];  // [wave][histogram][bin]
+    __shared__ AnalysisTile tile[4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int mb = blockIdx.x * 4 + wv;
@@ -124,57 +111,91 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
         const uint8_t* Yf = Y + (size_t)f * ysz;
         const uint8_t* Uf = U + (size_t)f * csz;
         const uint8_t* Vf = V + (size_t)f * csz;
+        // ---- stage the MB and its edges in LDS (coalesced u32 loads) ----
+        // tiles: [plane][row][col] with interior rows 0..15 / 0..7, top row, left column, corner
+        AnalysisTile* A = &tile[wv];
+        const bool ht = mby > 0, hl = mbx > 0;
+        {
+            const uint32_t* y32 = (const uint32_t*)(Yf + (size_t)(mby * 16 + (lane >> 2)) * ys + mbx * 16);
+            A->y[lane >> 2][lane & 3] = y32[lane & 3];
+            if (lane < 32) {
+                const int pl = lane >> 4, r = (lane >> 1) & 7, w = lane & 1;
+                const uint8_t* P = pl ? Vf : Uf;
+                A->c[pl][r][w] = ((const uint32_t*)(P + (size_t)(mby * 8 + r) * cs + mbx * 8))[w];
+            } else if (lane < 36) {
+                A->ytop[lane - 32] = ht ? ((const uint32_t*)(Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16))[lane - 32] : 0u;
+            } else if (lane < 40) {
+                const int pl = (lane - 36) >> 1, w = lane & 1;
+                const uint8_t* P = pl ? Vf : Uf;
+                A->ctop[pl][w] = ht ? ((const uint32_t*)(P + (size_t)(mby * 8 - 1) * cs + mbx * 8))[w] : 0u;
+            } else if (lane < 56) {
+                const int r = lane - 40;
+                A->yleft[r] = hl ? Yf[(size_t)(mby * 16 + r) * ys + mbx * 16 - 1] : (uint8_t)0;
+            } else {
+                const int r = lane - 56;  // 0..7: U and V left columns
+                A->cleft[0][r] = hl ? Uf[(size_t)(mby * 8 + r) * cs + mbx * 8 - 1] : (uint8_t)0;
+                A->cleft[1][r] = hl ? Vf[(size_t)(mby * 8 + r) * cs + mbx * 8 - 1] : (uint8_t)0;
+            }
+            if (lane < 3) {
+                const uint8_t* P = lane == 0 ? Yf : (lane == 1 ? Uf : Vf);
+                const int st = lane == 0 ? ys : cs, sz = lane == 0 ? 16 : 8;
+                A->corner[lane] = (ht && hl) ? P[(size_t)(mby * sz - 1) * st + mbx * sz - 1] : (uint8_t)0;
+            }
+        }
+        wsync();
         if (lane < 48) {
+            // libwebp analysis predictors on source pixels (analysis.rs:259-490, quirk A21):
+            // lane 0..31 luma (mode = lane >> 4: DC, TM; block lane & 15), 32..47 chroma
+            // (mode (lane-32) >> 3, block (lane-32) & 7: U 0..3, V 4..7)
             const bool luma = lane < 32;
             const int mode = luma ? (lane >> 4) : ((lane - 32) >> 3);
             const int b = luma ? (lane & 15) : ((lane - 32) & 7);
-            const int size = luma ? 16 : 8;
-            const uint8_t* P = luma ? Yf : (b < 4 ? Uf : Vf);
-            const int st = luma ? ys : cs;
+            const int pl = b >> 2;  // chroma plane
             const int bb = luma ? b : (b & 3);
             const int bx = luma ? (bb & 3) : (bb & 1), by = luma ? (bb >> 2) : (bb >> 1);
-            const int ox = mbx * size, oy = mby * size;
-            const bool ht = mby > 0, hl = mbx > 0;
-            // predictor value at (r, c) of the MB
-            int dcv = 0x80;
-            {
-                uint32_t s = 0;
-                if (ht && hl) {
-                    for (int i = 0; i < size; i++) s += P[(size_t)(oy - 1) * st + ox + i] + P[(size_t)(oy + i) * st + ox - 1];
-                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
-                } else if (ht) {
-                    for (int i = 0; i < size; i++) s += P[(size_t)(oy - 1) * st + ox + i];
-                    s += s;
-                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
-                } else if (hl) {
-                    for (int i = 0; i < size; i++) s += P[(size_t)(oy + i) * st + ox - 1];
-                    s += s;
-                    dcv = luma ? (int)((s + 16) >> 5) : (int)((s + 8) >> 4);
+            // edge sums (v_sad_u8 over 4 packed bytes)
+            uint32_t st = 0, sl = 0;
+            if (luma) {
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    st = __builtin_amdgcn_sad_u8(A->ytop[w], 0u, st);
+                    sl = __builtin_amdgcn_sad_u8(((const uint32_t*)A->yleft)[w], 0u, sl);
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 2; w++) {
+                    st = __builtin_amdgcn_sad_u8(A->ctop[pl][w], 0u, st);
+                    sl = __builtin_amdgcn_sad_u8(((const uint32_t*)A->cleft[pl])[w], 0u, sl);
                 }
             }
-            const int corner = (ht && hl) ? P[(size_t)(oy - 1) * st + ox - 1] : 0;
+            const uint32_t s2 = ht && hl ? st + sl : (ht ? 2 * st : 2 * sl);
+            const int dcv = (ht || hl) ? (luma ? (int)((s2 + 16) >> 5) : (int)((s2 + 8) >> 4)) : 0x80;
+            const int corner = A->corner[luma ? 0 : 1 + pl];
             int d[16];
 #pragma unroll
-            for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 4; i++) {
+                const int r = by * 4 + i;
+                const uint32_t srow = luma ? A->y[r][bx] : A->c[pl][r][bx];
+                const int L = luma ? A->yleft[r] : A->cleft[pl][r];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const int r = by * 4 + i, c = bx * 4 + j;
-                    const int s = P[(size_t)(oy + r) * st + ox + c];
-                    int p;
-                    if (mode == 0) p = dcv;
-                    else if (ht && hl) p = clamp255(P[(size_t)(oy + r) * st + ox - 1] + P[(size_t)(oy - 1) * st + ox + c] - corner);
-                    else if (hl) p = P[(size_t)(oy + r) * st + ox - 1];
-                    else if (ht) p = P[(size_t)(oy - 1) * st + ox + c];
-                    else p = 129;
-                    d[i * 4 + j] = s - p;
+                    const int cidx = bx * 4 + j;
+                    const uint32_t tw = luma ? A->ytop[cidx >> 2] : A->ctop[pl][cidx >> 2];
+                    const int T = (int)((tw >> (8 * (cidx & 3))) & 255u);
+                    const int tm = (ht && hl) ? clamp255(L + T - corner) : (hl ? L : (ht ? T : 129));
+                    const int p = mode == 0 ? dcv : tm;
+                    d[i * 4 + j] = (int)((srow >> (8 * j)) & 255u) - p;
                 }
-            int16_t o[16];
-            fdct_analysis(d, o);
+            }
+            // forward_dct_4x4 (analysis.rs:172) == dct4x4 for residuals in [-255, 255]:
+            // (X + 1812) >> 9 == (8X + 14500) >> 12 and (X + 937) >> 9 == (8X + 7500) >> 12
+            int o[16];
+            fdct16_pk(d, o);
             const int hidx = luma ? mode : 2 + mode;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                int v = iabs(o[k]) >> 3;
-                atomicAdd(&hist[wv][hidx][v < 31 ? v : 31], 1u);
+                const int v = min(iabs(o[k]) >> 3, 31);
+                atomicAdd(&hist[wv][hidx][v], 1u);
             }
         }
         wsync();
