@@ -429,11 +429,8 @@ struct WaveLds {
     int dc[64];
     int y2d[64];
     int y2cost[4];
-    int V[40];
-    uint8_t pred[10][16];
-    uint32_t msse[12];
-    int cand[12];
-    int cres[10][24];             // per I4 candidate: score lo/hi, sse, rate, hnz, q[16]
+    int V[2][40];                 // I4 value vectors of the (up to) two sub-blocks of a search step
+    uint8_t pred[2][10][16];
     int nzt[4], nzl[4];
     uint8_t modes[16];
     int16_t lev[25][16];
@@ -651,12 +648,14 @@ extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
 #define PH_MARK_L(k, ln, ps) (void)0
 #endif
 
-// Fill the I4 value vector V for sub-block (x0, y0) of W->ws (branch-free:
-// every lane reads up to three edge pixels and forms an avg2/avg3/copy).
+// Fill the I4 value vectors V[h] for the NB sub-blocks (x0[h], y0[h]) of
+// W->ws (branch-free: every lane reads up to three edge pixels and forms an
+// avg2/avg3/copy; the lane -> (edge indices, weights) map is block invariant).
 //   V[0..12]  E = [L3 L2 L1 L0 P A0..A7]      V[13..23] avg3(E[k], E[k+1], E[k+2])
 //   V[24..35] avg2(E[k], E[k+1])              V[36] avg3(A6,A7,A7)  V[37] avg3(L2,L3,L3)
 //   V[38] DC = (4 + L0..L3 + A0..A3) >> 3
-__device__ void i4_values(const Ctx& C, int x0, int y0)
+template <int NB>
+__device__ __forceinline__ void i4_values_n(const Ctx& C, const int* x0, const int* y0)
 {
     WaveLds* W = C.W;
     const uint8_t* ws = W->ws;
@@ -669,21 +668,32 @@ __device__ void i4_values(const Ctx& C, int x0, int y0)
     const int ka = k + t3 * (11 - k) + t4 * (1 - k);
     const int kb = k + t12 + t3 * (12 - k) - t4 * k;
     const int kc = min(k + 2 * (int)(t == 1), 12);
-    const int rowL = (y0 + 3) * ZW_BPS + x0 - 1, rowT = (y0 - 1) * ZW_BPS + x0 - 5;
-    const int aa = csel(ka < 4, rowL - ka * ZW_BPS, rowT + ka);
-    const int ab = csel(kb < 4, rowL - kb * ZW_BPS, rowT + kb);
-    const int ac = csel(kc < 4, rowL - kc * ZW_BPS, rowT + kc);
-    const int ea = ws[aa], eb = ws[ab], ec = ws[ac];
     // v = (ea + wb*eb + wc*ec + rnd) >> sh
     const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
     const int wc = (int)(t == 1);
     const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
-    const int v = (ea + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh;
-    const int dsum = red16((l < 4 || (l >= 5 && l < 9)) ? ea : 0);
-    if (l < 38) W->V[l] = v;
-    if (l == 0) W->V[38] = (dsum + 4) >> 3;
+    const int oa = csel(ka < 4, -ka * ZW_BPS, ka - 4 - 4 * ZW_BPS);  // offsets from rowL = (y0+3)*BPS + x0-1
+    const int ob = csel(kb < 4, -kb * ZW_BPS, kb - 4 - 4 * ZW_BPS);
+    const int oc = csel(kc < 4, -kc * ZW_BPS, kc - 4 - 4 * ZW_BPS);
+    const bool dcl = l < 4 || (l >= 5 && l < 9);
+    int v[NB], ea[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int rowL = (y0[h] + 3) * ZW_BPS + x0[h] - 1;
+        ea[h] = ws[rowL + oa];
+        const int eb = ws[rowL + ob], ec = ws[rowL + oc];
+        v[h] = (ea[h] + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh;
+    }
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int dsum = red16(dcl ? ea[h] : 0);
+        if (l < 38) W->V[h][l] = v[h];
+        if (l == 0) W->V[h][38] = (dsum + 4) >> 3;
+    }
     wsync();
 }
+__device__ __forceinline__ void i4_values(const Ctx& C, int x0, int y0) { i4_values_n<1>(C, &x0, &y0); }
+
 // V index of pixel p under I4 mode `mode`, with bit 8 set for TrueMotion
 // (pred = clamp(V[ia] + V[5 + col] - V[4])).  Sub-block independent.
 __device__ __forceinline__ int i4_src_index(const LdsTables* T, int mode, int p)
@@ -692,9 +702,9 @@ __device__ __forceinline__ int i4_src_index(const LdsTables* T, int mode, int p)
     const bool tm = idx == 254;
     return csel(tm, 256 + 3 - (p >> 2), csel(idx == 255, 38, idx));
 }
-__device__ __forceinline__ int i4_pred_at(const WaveLds* W, int sidx, int vbc)
+__device__ __forceinline__ int i4_pred_at(const int* V, int sidx, int vbc)
 {
-    const int va = W->V[sidx & 255];
+    const int va = V[sidx & 255];
     return csel(sidx >= 256, clamp255(va + vbc), va);
 }
 
@@ -703,56 +713,76 @@ __device__ __forceinline__ unsigned long long rdscore(uint32_t sse, uint32_t rat
     return (unsigned long long)sse * 256ull + (unsigned long long)(uint16_t)rate * lambda;
 }
 
-// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
-// Per sub-block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8);
+// Running state of the I4 search (pick_best_intra4, vp8.rs:1790-2040).
+struct I4State {
+    unsigned long long running;  // sum of the chosen blocks' rd scores (+ 211 * lambda_mode)
+    uint32_t total_mc;           // header-bit cap accumulator (vp8.rs:1839)
+    unsigned long long mpack;    // chosen sub-modes, 4 bits each (raster index)
+    uint32_t tnz, lnz;           // nonzero flags of the chosen blocks: bit sbx / bit sby
+};
+
+// One x+2y anti-diagonal step of the I4 search: the NB (1 or 2) sub-blocks
+// (sbx[h], sby[h]) share no pixels and no contexts, so they are searched
+// together -- every dependent chain of the single-block search (predictions,
+// SSE reductions, rank, candidate DCT/quant/cost/iDCT) runs twice,
+// interleaved, for instruction-level parallelism inside the wave.
+// Per block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8);
 // stable ascending SSE rank (quirk A12) computed lane-parallel (lane m ranks
 // mode m against the ten keys sse*16+m held in SGPRs); the top-K candidates
 // are evaluated 16 lanes each and the winner chosen on the scalar unit.
 // Within one sub-block every candidate score sse*256 + u16(rate)*lambda_i4 is
 // below 2^29 (sse <= 16*255^2, lambda_i4 <= 1785), so score*4 + group is a
 // unique 32-bit key whose minimum is the reference's first strict minimum.
-__device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
+template <int NB>
+__device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, int si0, int si1, int si2,
+                                        uint32_t iqk, uint32_t biask, int qk, I4State& st)
 {
     WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
     const int l = C.lane, g = l >> 4, k = l & 15;
-    const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
-    const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
-    const int qk = (int)S.y1.q[k > 0];
     const uint32_t lam = S.l_i4;
-    unsigned long long running = 211ull * S.l_mode;
-    uint32_t total_mc = 0;
-    unsigned long long mpack = 0;  // chosen sub-modes, 4 bits each
-    uint32_t tnz = 0, lnz = 0;     // nonzero flags of the chosen blocks: bit sbx / bit sby
-    const int si0 = i4_src_index(T, g, k), si1 = i4_src_index(T, g + 4, k), si2 = i4_src_index(T, g < 2 ? g + 8 : 0, k);
-    for (int i = 0; i < 16; i++) {
-        const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
-        const int tctx = sby == 0 ? 0 : (int)((mpack >> (4 * (i - 4))) & 15);
-        const int lctx = sbx == 0 ? 0 : (int)((mpack >> (4 * (i - 1))) & 15);
-        const int nzc = (sby == 0 ? 0 : (int)((tnz >> sbx) & 1)) + (sbx == 0 ? 0 : (int)((lnz >> sby) & 1));
-        PH_START();
-        i4_values(C, x0, y0);
-        PH_MARK_L(10, l, 0);
-        const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
-        int e0, e1, e2;
-        {
-            const int vbc = W->V[5 + (k & 3)] - W->V[4];
-            int v = i4_pred_at(W, si0, vbc);
-            W->pred[g][k] = (uint8_t)v;
-            e0 = red16(m24(svk - v, svk - v));
-            v = i4_pred_at(W, si1, vbc);
-            W->pred[g + 4][k] = (uint8_t)v;
-            e1 = red16(m24(svk - v, svk - v));
-            v = i4_pred_at(W, si2, vbc);
-            if (g < 2) W->pred[g + 8][k] = (uint8_t)v;
-            e2 = red16(m24(svk - v, svk - v));
-        }
-        // unique keys sse*16 + m (sse < 2^21) -> rank = #smaller keys
+    int x0[NB], y0[NB], tctx[NB], lctx[NB], nzc[NB], svk[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int i = sby[h] * 4 + sbx[h];
+        x0[h] = sbx[h] * 4 + 1;
+        y0[h] = sby[h] * 4 + 1;
+        tctx[h] = sby[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 4))) & 15);
+        lctx[h] = sbx[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 1))) & 15);
+        nzc[h] = (sby[h] == 0 ? 0 : (int)((st.tnz >> sbx[h]) & 1)) + (sbx[h] == 0 ? 0 : (int)((st.lnz >> sby[h]) & 1));
+        svk[h] = C.sY[(sby[h] * 4 + (k >> 2)) * 16 + sbx[h] * 4 + (k & 3)];
+    }
+    PH_START();
+    i4_values_n<NB>(C, x0, y0);
+    PH_MARK_L(10, l, 0);
+    int e0[NB], e1[NB], e2[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int* V = W->V[h];
+        const int vbc = V[5 + (k & 3)] - V[4];
+        const int v0 = i4_pred_at(V, si0, vbc), v1 = i4_pred_at(V, si1, vbc), v2 = i4_pred_at(V, si2, vbc);
+        W->pred[h][g][k] = (uint8_t)v0;
+        W->pred[h][g + 4][k] = (uint8_t)v1;
+        if (g < 2) W->pred[h][g + 8][k] = (uint8_t)v2;
+        e0[h] = m24(svk[h] - v0, svk[h] - v0);
+        e1[h] = m24(svk[h] - v1, svk[h] - v1);
+        e2[h] = m24(svk[h] - v2, svk[h] - v2);
+    }
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        e0[h] = red16(e0[h]);
+        e1[h] = red16(e1[h]);
+        e2[h] = red16(e2[h]);
+    }
+    // unique keys sse*16 + m (sse < 2^21) -> rank = #smaller keys
+    unsigned long long cpack[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
         uint32_t key[10];
 #pragma unroll
         for (int m = 0; m < 10; m++) {
-            const int ev = m < 4 ? e0 : (m < 8 ? e1 : e2);
+            const int ev = m < 4 ? e0[h] : (m < 8 ? e1[h] : e2[h]);
             key[m] = ((uint32_t)__builtin_amdgcn_readlane(ev, (m & 3) * 16) << 4) | (uint32_t)m;
         }
         uint32_t mykey = 0xffffffffu;
@@ -761,57 +791,132 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         int rank = 0;
 #pragma unroll
         for (int m = 0; m < 10; m++) rank += (int)(key[m] < mykey);
-        unsigned long long cpack = 0;  // candidate c -> mode, 4 bits each
+        cpack[h] = 0;  // candidate c -> mode, 4 bits each
         for (int c = 0; c < K; c++) {
             const unsigned long long bm = __ballot(rank == c && l < 10);
-            cpack |= (unsigned long long)__builtin_ctzll(bm) << (4 * c);
+            cpack[h] |= (unsigned long long)__builtin_ctzll(bm) << (4 * c);
         }
-        wsync();
-        PH_MARK_L(11, l, 0);
-        uint32_t bsc = 0xffffffffu, bsse = 0, brate = 0;
-        int bmode = 0, bnz = 0, brv = 0;
-        for (int base = 0; base < K; base += 4) {
-            const int c = base + g;
-            const bool act = c < K;
-            const int mm = act ? (int)((cpack >> (4 * c)) & 15) : 0;
-            const int pk = W->pred[mm][k];
-            const int r = fdct_g(svk - pk, k);
-            const int qv = quantz(r, iqk, biask);
-            const unsigned nzm = gmask(qv != 0);
-            const uint32_t cc = rcost_g<0>(qv, k, nzc, 3, T);
-            const int dq = idct_g(m24(qv, qk), k);
-            const int rv = clamp255(pk + dq);
-            const int d = svk - rv;
-            const uint32_t sse = (uint32_t)red16(d * d);
-            const uint32_t rate = (uint32_t)T->fci4[tctx][lctx][mm] + cc;
-            const uint32_t sc = sse * 256u + (rate & 0xffffu) * lam;
-            const uint32_t kv = act ? sc * 4u + (uint32_t)g : 0xffffffffu;
-            uint32_t kmin = (uint32_t)__builtin_amdgcn_readlane((int)kv, 0);
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 16));
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 32));
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv, 48));
-            if ((kmin >> 2) < bsc) {  // strict: earlier rounds keep ties
+    }
+    wsync();
+    PH_MARK_L(11, l, 0);
+    uint32_t bsc[NB], bsse[NB], brate[NB];
+    int bmode[NB], bnz[NB], brv[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        bsc[h] = 0xffffffffu;
+        bsse[h] = brate[h] = 0;
+        bmode[h] = bnz[h] = brv[h] = 0;
+    }
+    for (int base = 0; base < K; base += 4) {
+        const int c = base + g;
+        const bool act = c < K;
+        int mm[NB], pk[NB], r[NB], qv[NB], dq[NB], rv[NB];
+        unsigned nzm[NB];
+        uint32_t cc[NB], sse[NB], rate[NB], kv[NB];
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            mm[h] = act ? (int)((cpack[h] >> (4 * c)) & 15) : 0;
+            pk[h] = W->pred[h][mm[h]][k];
+        }
+#pragma unroll
+        for (int h = 0; h < NB; h++) r[h] = fdct_g(svk[h] - pk[h], k);
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            qv[h] = quantz(r[h], iqk, biask);
+            nzm[h] = gmask(qv[h] != 0);
+        }
+#pragma unroll
+        for (int h = 0; h < NB; h++) cc[h] = rcost_g<0>(qv[h], k, nzc[h], 3, T);
+#pragma unroll
+        for (int h = 0; h < NB; h++) dq[h] = idct_g(m24(qv[h], qk), k);
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            rv[h] = clamp255(pk[h] + dq[h]);
+            const int d = svk[h] - rv[h];
+            sse[h] = (uint32_t)red16(d * d);
+        }
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            rate[h] = (uint32_t)T->fci4[tctx[h]][lctx[h]][mm[h]] + cc[h];
+            const uint32_t sc = sse[h] * 256u + (rate[h] & 0xffffu) * lam;
+            kv[h] = act ? sc * 4u + (uint32_t)g : 0xffffffffu;
+        }
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            uint32_t kmin = (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 0);
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 16));
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 32));
+            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 48));
+            if ((kmin >> 2) < bsc[h]) {  // strict: earlier rounds keep ties
                 const int bg = (int)(kmin & 3u), src = bg * 16;
-                bsc = kmin >> 2;
-                bsse = (uint32_t)__builtin_amdgcn_readlane((int)sse, src);
-                brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, src);
-                bnz = __builtin_amdgcn_readlane((int)(nzm != 0), src);
-                bmode = (int)((cpack >> (4 * (base + bg))) & 15);
-                brv = __shfl(rv, src + k);
+                bsc[h] = kmin >> 2;
+                bsse[h] = (uint32_t)__builtin_amdgcn_readlane((int)sse[h], src);
+                brate[h] = (uint32_t)__builtin_amdgcn_readlane((int)rate[h], src);
+                bnz[h] = __builtin_amdgcn_readlane((int)(nzm[h] != 0), src);
+                bmode[h] = (int)((cpack[h] >> (4 * (base + bg))) & 15);
+                brv[h] = __shfl(rv[h], src + k);
             }
         }
-        PH_MARK_L(12, l, 0);
-        tnz = (tnz & ~(1u << sbx)) | ((uint32_t)bnz << sbx);
-        lnz = (lnz & ~(1u << sby)) | ((uint32_t)bnz << sby);
-        total_mc += T->fci4[tctx][lctx][bmode];
-        running += rdscore(bsse, brate, S.l_mode);
-        mpack |= (unsigned long long)bmode << (4 * i);
-        if (l == 0) W->modes[i] = (uint8_t)bmode;
-        if (running >= i16_score) { wsync(); return false; }
-        if (total_mc > 256u * 16u * 16u / 4u) { wsync(); return false; }
-        if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)brv;
-        wsync();
-        PH_MARK_L(13, l, 0);
+    }
+    PH_MARK_L(12, l, 0);
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int i = sby[h] * 4 + sbx[h];
+        st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz[h] << sbx[h]);
+        st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz[h] << sby[h]);
+        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode[h]];
+        st.running += rdscore(bsse[h], brate[h], S.l_mode);
+        st.mpack |= (unsigned long long)bmode[h] << (4 * i);
+        if (l == h) W->modes[i] = (uint8_t)bmode[h];
+    }
+    // recon pixels: lanes 16h..16h+15 write block h
+    {
+        const int hh = NB == 2 ? (l >> 4) & 1 : 0;
+        const int xo = NB == 2 ? csel(hh, x0[NB - 1], x0[0]) : x0[0];
+        const int yo = NB == 2 ? csel(hh, y0[NB - 1], y0[0]) : y0[0];
+        const int pv = NB == 2 ? csel(hh, brv[NB - 1], brv[0]) : brv[0];
+        if (l < 16 * NB) W->ws[(yo + (k >> 2)) * ZW_BPS + xo + (k & 3)] = (uint8_t)pv;
+    }
+    wsync();
+    PH_MARK_L(13, l, 0);
+}
+
+// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
+// The sub-blocks are visited along x+2y anti-diagonals (10 steps, 6 of them with
+// two independent blocks) instead of raster order.  Each block's choice depends
+// only on its left / top / top-right neighbours, which every earlier
+// anti-diagonal holds, so every choice equals the raster-order one.  The
+// reference's early exits (running score >= the I16 score, vp8.rs:2018; mode
+// cost cap, :1839) test sums of non-negative terms, which grow with every
+// block: "some raster prefix crossed the bound" is "the sum over every block
+// crossed it", so testing the sum of the blocks searched so far after each
+// step decides exactly as the reference does.
+__device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
+{
+    const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
+    const int l = C.lane, g = l >> 4, k = l & 15;
+    const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
+    const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
+    const int qk = (int)S.y1.q[k > 0];
+    I4State st;
+    st.running = 211ull * S.l_mode;
+    st.total_mc = 0;
+    st.mpack = 0;
+    st.tnz = st.lnz = 0;
+    const int si0 = i4_src_index(T, g, k), si1 = i4_src_index(T, g + 4, k), si2 = i4_src_index(T, g < 2 ? g + 8 : 0, k);
+    for (int s = 0; s < 10; s++) {
+        // anti-diagonal s: A = (sbx, sby) with the smallest sby, B = (sbx - 2, sby + 1)
+        const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
+        const int sbxA = s - 2 * sbyA;
+        if (s >= 2 && s <= 7) {
+            const int bx[2] = {sbxA, sbxA - 2}, by[2] = {sbyA, sbyA + 1};
+            i4_step<2>(C, bx, by, K, si0, si1, si2, iqk, biask, qk, st);
+        } else {
+            i4_step<1>(C, &sbxA, &sbyA, K, si0, si1, si2, iqk, biask, qk, st);
+        }
+        if (st.running >= i16_score) return false;
+        if (st.total_mc > 256u * 16u * 16u / 4u) return false;
     }
     return true;
 }
@@ -1060,7 +1165,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
             i4_values(C, x0, y0);
             // 16-lane group form: every group computes the same block; group 0 stores
             const int k = l & 15;
-            const int pk = i4_pred_at(W, i4_src_index(C.T, bm, k), W->V[5 + (k & 3)] - W->V[4]);
+            const int pk = i4_pred_at(W->V[0], i4_src_index(C.T, bm, k), W->V[0][5 + (k & 3)] - W->V[0][4]);
             const int svk = C.sY[(sby * 4 + (k >> 2)) * 16 + sbx * 4 + (k & 3)];
             const int ck = fdct_g(svk - pk, k);
             const int ctx0 = min(left_nz[sby] + top_nz[sbx], 2);

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Iteration check: GPU parity tests, then the phase-cycle profile (profiling build).
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+fatal() { case $1 in 124|137|134|139|135|132) return 0;; *) return 1;; esac; }
+tools/gpu_step.sh pytest_gpu 500 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread; rc=$?
+[ $rc -ne 0 ] && exit $rc
+tools/gpu_step.sh phase 200 python tools/phase_prof.py ${PHASE_FRAMES:-256}; rc=$?
+exit $rc
