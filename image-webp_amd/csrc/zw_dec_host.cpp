@@ -20,6 +20,8 @@
 extern "C" {
 hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
                          uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
+hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
+                       int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
                           const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes);
 }
@@ -415,12 +417,24 @@ extern "C" void zw_frame_free(zw_frame* f)
     }
 }
 
-// Vp8Decoder::decode_frame for n frames of identical dimensions, one device pass.
-extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
+// Decoded planes of a batch, resident in the context's device scratch.
+struct DecBatch {
+    std::vector<DecFrame> F;
+    uint8_t* d = nullptr;  // device scratch base
+    size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
+    int mbw = 0, mbh = 0;
+};
+
+// Vp8Decoder::decode_frame for n frames of identical dimensions, one device
+// pass: host header/token parse (parallel over frames) -> k_dec_recon ->
+// k_loopfilter.  Leaves the filtered planes in device scratch (plus
+// `extra_bytes` of scratch at B.o_extra for the caller) with the kernel
+// stream's work queued; dev_ev[2] marks the end of the loop filter.
+static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
+                            size_t extra_bytes, DecBatch& B)
 {
-    if (!ctx || n <= 0 || !data || !lens || !outs) return ZW_EINVAL;
-    for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
-    std::vector<DecFrame> F(n);
+    B.F.assign(n, DecFrame());
+    std::vector<DecFrame>& F = B.F;
     std::vector<int> rc(n, ZW_OK);
     parallel_for(n, [&](int i) { rc[i] = parse_header(F[i], data[i], lens[i]); });
     for (int i = 0; i < n; i++)
@@ -454,14 +468,15 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     const size_t o_fl = al256(o_fp + fps.size() * sizeof(ZwFilterParams));
     const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
     const size_t o_u = al256(o_y + (size_t)n * ysz), o_v = al256(o_u + (size_t)n * csz);
-    const size_t total = al256(o_v + (size_t)n * csz);
+    const size_t o_extra = al256(o_v + (size_t)n * csz);
+    const size_t total = al256(o_extra + extra_bytes);
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
     hipStream_t s = ctx_stream(ctx);
     HIPOK(hipMemcpyAsync(d + o_mbs, mbs, rec_bytes, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
-    for (int e = 0; e < 3; e++)
+    for (int e = 0; e < 4; e++)
         if (!ctx->dev_ev[e]) HIPOK(hipEventCreate(&ctx->dev_ev[e]));
     HIPOK(hipEventRecord(ctx->dev_ev[0], s));
     HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_mbs), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
@@ -469,15 +484,37 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     HIPOK(hipEventRecord(ctx->dev_ev[1], s));
     HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
     HIPOK(hipEventRecord(ctx->dev_ev[2], s));
+    B.d = d;
+    B.o_y = o_y;
+    B.o_u = o_u;
+    B.o_v = o_v;
+    B.o_extra = o_extra;
+    B.ysz = ysz;
+    B.csz = csz;
+    B.mbw = mbw;
+    B.mbh = mbh;
+    return ZW_OK;
+}
+
+extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
+{
+    if (!ctx || n <= 0 || !data || !lens || !outs) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
+    DecBatch B;
+    int r0 = decode_to_device(ctx, n, data, lens, 0, B);
+    if (r0) return r0;
+    const std::vector<DecFrame>& F = B.F;
+    const size_t ysz = B.ysz, csz = B.csz;
+    uint8_t* d = B.d;
     // planes down through pinned staging (one DMA per plane set), then fanned out
     const size_t fsz = ysz + 2 * csz;
     uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fsz);
     if (!hout) return ZW_ENOMEM;
     HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
     {
-        int r = ctx_d2h(ctx, hout, d + o_y, (size_t)n * ysz);
-        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * ysz, d + o_u, (size_t)n * csz);
-        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * (ysz + csz), d + o_v, (size_t)n * csz);
+        int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)n * ysz);
+        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * ysz, d + B.o_u, (size_t)n * csz);
+        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * (ysz + csz), d + B.o_v, (size_t)n * csz);
         if (r) return r;
     }
     std::vector<int> oom(n, 0);
@@ -501,9 +538,9 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         zw_frame& o = outs[i];
         o.width = (uint16_t)F[i].width;
         o.height = (uint16_t)F[i].height;
-        o.y_stride = (uint32_t)mbw * 16;
-        o.uv_stride = (uint32_t)mbw * 8;
-        o.mb_rows = (uint32_t)mbh;
+        o.y_stride = (uint32_t)B.mbw * 16;
+        o.uv_stride = (uint32_t)B.mbw * 8;
+        o.mb_rows = (uint32_t)B.mbh;
         o.y = buf;
         o.u = buf + ysz;
         o.v = buf + ysz + csz;
@@ -513,6 +550,105 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     }
     (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
     (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
+    ctx->dec_ms[2] = 0.f;
+    return ZW_OK;
+}
+
+// Frame::fill_rgb / fill_rgba (decoder/vp8.rs:200-258) after decode_frame, on
+// the device: decode -> k_yuv2rgb -> packed RGB(A) down.  Every frame of the
+// batch must have the same dimensions (their packed images are contiguous).
+extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int bpp,
+                                       int upsampling, zw_bytes* outs, uint32_t* widths, uint32_t* heights)
+{
+    if (!ctx || n <= 0 || !data || !lens || !outs || (bpp != 3 && bpp != 4) ||
+        (upsampling != ZW_UPSAMPLE_BILINEAR && upsampling != ZW_UPSAMPLE_SIMPLE))
+        return ZW_EINVAL;
+    for (int i = 0; i < n; i++) outs[i].data = nullptr, outs[i].len = 0;
+    // dimensions first (they size the device output)
+    size_t w = 0, h = 0;
+    {
+        DecFrame f0;
+        const int r = parse_header(f0, data[0], lens[0]);
+        if (r) return r;
+        w = f0.width;
+        h = f0.height;
+    }
+    const size_t fbytes = w * h * (size_t)bpp;
+    DecBatch B;
+    int r0 = decode_to_device(ctx, n, data, lens, (size_t)n * fbytes, B);
+    if (r0) return r0;
+    for (int i = 0; i < n; i++)
+        if ((size_t)B.F[i].width != w || (size_t)B.F[i].height != h) return ZW_EINVAL;
+    hipStream_t s = ctx_stream(ctx);
+    uint8_t* drgb = B.d + B.o_extra;
+    HIPOK(zwk_yuv2rgb(s, B.d + B.o_y, B.d + B.o_u, B.d + B.o_v, B.ysz, B.csz, (int)w, (int)h, B.mbw * 16, B.mbw * 8,
+                      bpp, upsampling == ZW_UPSAMPLE_BILINEAR, drgb, n));
+    HIPOK(hipEventRecord(ctx->dev_ev[3], s));
+    uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fbytes);
+    if (!hout) return ZW_ENOMEM;
+    HIPOK(hipEventSynchronize(ctx->dev_ev[3]));
+    if (int r = ctx_d2h(ctx, hout, drgb, (size_t)n * fbytes)) return r;
+    std::vector<int> oom(n, 0);
+    parallel_for(n, [&](int i) {
+        uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
+        if (!buf) {
+            oom[i] = 1;
+            return;
+        }
+        memcpy(buf, hout + (size_t)i * fbytes, fbytes);
+        outs[i].data = buf;
+        outs[i].len = fbytes;
+    });
+    for (int i = 0; i < n; i++)
+        if (oom[i]) {
+            for (int k = 0; k < n; k++) zw_bytes_free(&outs[k]);
+            return ZW_ENOMEM;
+        }
+    for (int i = 0; i < n; i++) {
+        if (widths) widths[i] = (uint32_t)w;
+        if (heights) heights[i] = (uint32_t)h;
+    }
+    (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
+    (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
+    (void)hipEventElapsedTime(&ctx->dec_ms[2], ctx->dev_ev[2], ctx->dev_ev[3]);
+    return ZW_OK;
+}
+
+extern "C" int zw_vp8_decode_rgb(zw_ctx* ctx, const uint8_t* vp8, size_t len, int bpp, int upsampling, zw_bytes* out,
+                                 uint32_t* width, uint32_t* height)
+{
+    if (!vp8 && len) return ZW_EINVAL;
+    const uint8_t* d[1] = {vp8};
+    size_t l[1] = {len};
+    return zw_vp8_decode_rgb_batch(ctx, 1, d, l, bpp, upsampling, out, width, height);
+}
+
+// Kernel-level entry: fill_rgb_buffer_fancy / _simple (decoder/yuv.rs:82, :402)
+// of one image's planes (host buffers; rows of y_stride / uv_stride bytes,
+// ceil(h/2) chroma rows) into out (w*h*bpp bytes, packed).
+extern "C" int zw_yuv_to_rgb(zw_ctx* ctx, const uint8_t* y, const uint8_t* u, const uint8_t* v, uint32_t width,
+                             uint32_t height, uint32_t y_stride, uint32_t uv_stride, int bpp, int upsampling,
+                             uint8_t* out)
+{
+    if (!ctx || !y || !u || !v || !out || width == 0 || height == 0 || y_stride < width ||
+        uv_stride < (width + 1) / 2 || (bpp != 3 && bpp != 4) ||
+        (upsampling != ZW_UPSAMPLE_BILINEAR && upsampling != ZW_UPSAMPLE_SIMPLE))
+        return ZW_EINVAL;
+    const size_t ch = (height + 1) / 2;
+    const size_t ysz = (size_t)y_stride * height, csz = (size_t)uv_stride * ch;
+    const size_t obytes = (size_t)width * height * bpp;
+    const size_t o_y = 0, o_u = al256(ysz), o_v = al256(o_u + csz), o_o = al256(o_v + csz);
+    HIPOK(hipSetDevice(ctx->device));
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, al256(o_o + obytes));
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx_stream(ctx);
+    HIPOK(hipMemcpyAsync(d + o_y, y, ysz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_u, u, csz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_v, v, csz, hipMemcpyHostToDevice, s));
+    HIPOK(zwk_yuv2rgb(s, d + o_y, d + o_u, d + o_v, ysz, csz, (int)width, (int)height, (int)y_stride, (int)uv_stride,
+                      bpp, upsampling == ZW_UPSAMPLE_BILINEAR, d + o_o, 1));
+    HIPOK(hipMemcpyAsync(out, d + o_o, obytes, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
     return ZW_OK;
 }
 
@@ -521,6 +657,13 @@ extern "C" int zw_decode_kernel_times(zw_ctx* ctx, float* ms)
     if (!ctx || !ms) return ZW_EINVAL;
     ms[0] = ctx->dec_ms[0];
     ms[1] = ctx->dec_ms[1];
+    return ZW_OK;
+}
+
+extern "C" int zw_decode_rgb_kernel_ms(zw_ctx* ctx, float* ms)
+{
+    if (!ctx || !ms) return ZW_EINVAL;
+    *ms = ctx->dec_ms[2];
     return ZW_OK;
 }
 
@@ -559,5 +702,101 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(v, d + o_v, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// WebP container, lossy subset: WebPDecoder::new -> read_data
+// (decoder/api.rs:334-510) for a simple "VP8 " file or a VP8X file whose image
+// is a VP8 chunk, then read_image (:640-700) + decode_rgb / decode_rgba
+// (:938-993).  Lossless (VP8L), alpha (ALPH) and animation are outside the
+// lossy block-transform path: ZW_EUNSUPPORTED.
+// ---------------------------------------------------------------------------
+namespace {
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+uint32_t rd24(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16); }
+bool fourcc_is(const uint8_t* p, const char* s) { return memcmp(p, s, 4) == 0; }
+}  // namespace
+
+extern "C" int zw_webp_parse(const uint8_t* data, size_t len, zw_webp_info* info)
+{
+    if (!info || (!data && len)) return ZW_EINVAL;
+    memset(info, 0, sizeof *info);
+    if (len < 8) return ZW_EBITSTREAM;
+    if (!fourcc_is(data, "RIFF")) return ZW_ECHUNK_HEADER;  // ChunkHeaderInvalid(b"RIFF")
+    const uint64_t riff_size = rd32(data + 4);
+    if (len < 12) return ZW_EBITSTREAM;
+    if (!fourcc_is(data + 8, "WEBP")) return ZW_EWEBP_SIGNATURE;
+    if (len < 20) return ZW_EBITSTREAM;
+    const uint8_t* ch = data + 12;
+    const uint64_t csize = rd32(ch + 4), crounded = csize + (csize & 1);
+    const uint64_t start = 20;
+    if (fourcc_is(ch, "VP8 ")) {
+        if (len < start + 10) return ZW_EBITSTREAM;
+        const uint32_t tag = rd24(data + start);
+        if (tag & 1) return ZW_EUNSUPPORTED_FEATURE;  // non-keyframe
+        const uint8_t* m = data + start + 3;
+        if (m[0] != 0x9d || m[1] != 0x01 || m[2] != 0x2a) return ZW_EVP8_MAGIC;
+        info->width = (data[start + 6] | (data[start + 7] << 8)) & 0x3fff;
+        info->height = (data[start + 8] | (data[start + 9] << 8)) & 0x3fff;
+        if (info->width == 0 || info->height == 0) return ZW_EINCONSISTENT_SIZES;
+        info->is_lossy = 1;
+        info->vp8_offset = start;
+        info->vp8_len = csize;
+    } else if (fourcc_is(ch, "VP8L")) {
+        info->is_lossless = 1;
+        return ZW_EUNSUPPORTED;
+    } else if (fourcc_is(ch, "VP8X")) {
+        if (len < start + 10) return ZW_EBITSTREAM;
+        const uint8_t flags = data[start];
+        info->has_alpha = (flags & 0x10) != 0;
+        info->is_animated = (flags & 0x02) != 0;
+        info->width = rd24(data + start + 4) + 1;
+        info->height = rd24(data + start + 7) + 1;
+        if ((uint64_t)info->width * info->height > 0xffffffffull) return ZW_EIMAGE_TOO_LARGE;
+        uint64_t pos = start + crounded;
+        const uint64_t max_pos = pos + (riff_size > 12 ? riff_size - 12 : 0);
+        int have_vp8 = 0, have_vp8l = 0;
+        while (pos < max_pos) {
+            if (pos + 8 > len) break;  // read_chunk_header hits the end: BitStreamError -> stop scanning
+            const uint8_t* c = data + pos;
+            const uint64_t sz = rd32(c + 4), rsz = sz + (sz & 1);
+            if (fourcc_is(c, "VP8 ") && !have_vp8) {
+                have_vp8 = 1;
+                info->vp8_offset = pos + 8;
+                info->vp8_len = sz;
+            } else if (fourcc_is(c, "VP8L")) {
+                have_vp8l = 1;
+            }
+            pos += 8 + rsz;
+        }
+        info->is_lossy = have_vp8;
+        info->is_lossless = have_vp8l && !have_vp8;
+        if (info->is_animated || have_vp8l || info->has_alpha) return ZW_EUNSUPPORTED;
+        if (!have_vp8) return ZW_ECHUNK_MISSING;
+    } else {
+        return ZW_ECHUNK_HEADER;
+    }
+    if (info->vp8_offset + info->vp8_len > len) return ZW_EBITSTREAM;
+    return ZW_OK;
+}
+
+extern "C" int zw_webp_decode(zw_ctx* ctx, const uint8_t* data, size_t len, int bpp, int upsampling, zw_bytes* out,
+                              uint32_t* width, uint32_t* height)
+{
+    if (!ctx || !out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    zw_webp_info info;
+    if (int r = zw_webp_parse(data, len, &info)) return r;
+    uint32_t w = 0, h = 0;
+    if (int r = zw_vp8_decode_rgb(ctx, data + info.vp8_offset, (size_t)info.vp8_len, bpp, upsampling, out, &w, &h))
+        return r;
+    if (w != info.width || h != info.height) {  // read_image: InconsistentImageSizes
+        zw_bytes_free(out);
+        return ZW_EINCONSISTENT_SIZES;
+    }
+    if (width) *width = w;
+    if (height) *height = h;
     return ZW_OK;
 }

@@ -529,3 +529,113 @@ extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint
     hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), 0, s, Y, U, V, flags, fp, ysz, csz);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// k_yuv2rgb: decoded YUV 4:2:0 planes -> packed RGB / RGBA (decoder/yuv.rs).
+//
+// FANCY: fill_rgb_buffer_fancy (yuv.rs:82-160) with its row helpers
+// fill_row_fancy_with_2_uv_rows / _1_uv_row (:162-395).  Written per output
+// pixel: chroma sample (main row mr, secondary row sr) x (main column mc,
+// secondary column sc) and U = (9 m + 3 s1 + 3 s2 + t + 8) >> 4
+// (get_fancy_chroma_value, :397).  Row r >= 1 pairs with chroma rows
+// (r-1)/2 and (r+1)/2 (main = the nearer one); row 0 and the final row of an
+// even-height image use one chroma row (sr = mr); columns likewise, with the
+// first pixel and the final pixel of an even-width row on one chroma column.
+// Every one of those special cases is the general formula with sr / sc
+// clamped to the image's chroma extent.
+// !FANCY: fill_rgb_buffer_simple (yuv.rs:402-515): U = u[r/2][x/2].
+// yuv_to_r/g/b (:63-78): mulhi(v, c) = (v * c) >> 8, clip = clamp(v >> 6).
+// BPP 4 writes alpha 255 (decode_rgba, decoder/api.rs:938-960).
+//
+// One thread per 4 consecutive pixels of the packed output (flat index, so
+// the 12 / 16-byte stores stay 4-byte aligned for any width); frames on
+// blockIdx.y.  Algorithmic bytes per pixel: 1 (Y) + 0.5 (U, V) read,
+// BPP written.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int yuv_clip(int v)
+{
+    v >>= 6;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+__device__ __forceinline__ uint32_t yuv_px(int y, int u, int v)
+{
+    const int yy = (y * 19077) >> 8;
+    const int r = yuv_clip(yy + ((v * 26149) >> 8) - 14234);
+    const int g = yuv_clip(yy - ((u * 6419) >> 8) - ((v * 13320) >> 8) + 8708);
+    const int b = yuv_clip(yy + ((u * 33050) >> 8) - 17685);
+    return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16) | 0xff000000u;
+}
+
+template <int BPP, bool FANCY>
+__global__ __launch_bounds__(256) void k_yuv2rgb(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
+                                                 const uint8_t* __restrict__ V, size_t ysz, size_t csz, int w, int h,
+                                                 int ys, int cs, uint8_t* __restrict__ out)
+{
+    const int f = blockIdx.y;
+    Y += (size_t)f * ysz;
+    U += (size_t)f * csz;
+    V += (size_t)f * csz;
+    const uint32_t npx = (uint32_t)w * (uint32_t)h;
+    uint8_t* o = out + (size_t)f * npx * BPP;
+    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 4u;
+    if (p0 >= npx) return;
+    int r = (int)(p0 / (uint32_t)w), x = (int)(p0 - (uint32_t)r * (uint32_t)w);
+    const int cw1 = ((w + 1) >> 1) - 1, ch1 = ((h + 1) >> 1) - 1;
+    uint32_t px[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int yv = Y[(size_t)r * ys + x];
+        int u, v;
+        if (FANCY) {
+            const int k = (r + 1) >> 1;
+            const int mr = (r & 1) ? k - 1 : k, sr = min((r & 1) ? k : k - 1, ch1);
+            const int q = (x - 1) >> 1;  // x = 0: q = -1 -> mc = sc = 0
+            const int mc = (x & 1) ? q : q + 1, sc = min(max((x & 1) ? q + 1 : q, 0), cw1);
+            const int srr = max(sr, 0);
+            const uint8_t *um = U + (size_t)mr * cs, *us = U + (size_t)srr * cs;
+            const uint8_t *vm = V + (size_t)mr * cs, *vs = V + (size_t)srr * cs;
+            u = (9 * um[mc] + 3 * um[sc] + 3 * us[mc] + us[sc] + 8) >> 4;
+            v = (9 * vm[mc] + 3 * vm[sc] + 3 * vs[mc] + vs[sc] + 8) >> 4;
+        } else {
+            u = U[(size_t)(r >> 1) * cs + (x >> 1)];
+            v = V[(size_t)(r >> 1) * cs + (x >> 1)];
+        }
+        px[j] = yuv_px(yv, u, v);
+        if (++x == w) {
+            x = 0;
+            r = min(r + 1, h - 1);  // past the last pixel: clamp (the store below drops it)
+        }
+    }
+    if (p0 + 4 <= npx) {
+        if (BPP == 4) {
+            *(uint4*)(o + (size_t)p0 * 4) = make_uint4(px[0], px[1], px[2], px[3]);
+        } else {
+            const uint32_t a = (px[0] & 0xffffffu) | (px[1] << 24);
+            const uint32_t b = ((px[1] >> 8) & 0xffffu) | (px[2] << 16);
+            const uint32_t c = ((px[2] >> 16) & 0xffu) | ((px[3] & 0xffffffu) << 8);
+            uint32_t* d = (uint32_t*)(o + (size_t)p0 * 3);
+            d[0] = a;
+            d[1] = b;
+            d[2] = c;
+        }
+    } else {
+        for (uint32_t j = 0; j < 4 && p0 + j < npx; j++)
+            for (int c = 0; c < BPP; c++) o[(size_t)(p0 + j) * BPP + c] = (uint8_t)(px[j] >> (8 * c));
+    }
+}
+
+extern "C" hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz,
+                                  size_t csz, int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out,
+                                  int nframes)
+{
+    const uint32_t npx = (uint32_t)w * (uint32_t)h;
+    const dim3 grid((npx + 1023) / 1024, nframes);
+    if (bpp == 4) {
+        if (fancy) hipLaunchKernelGGL((k_yuv2rgb<4, true>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
+        else hipLaunchKernelGGL((k_yuv2rgb<4, false>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
+    } else {
+        if (fancy) hipLaunchKernelGGL((k_yuv2rgb<3, true>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
+        else hipLaunchKernelGGL((k_yuv2rgb<3, false>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
+    }
+    return hipGetLastError();
+}

@@ -60,6 +60,11 @@ extern "C" const char* zw_strerror(int code)
     case ZW_EBITSTREAM: return "bitstream error";
     case ZW_EUNSUPPORTED_FEATURE: return "unsupported feature";
     case ZW_ENOT_ENOUGH_INIT_DATA: return "not enough VP8 init data";
+    case ZW_ECHUNK_HEADER: return "invalid chunk header";
+    case ZW_EWEBP_SIGNATURE: return "invalid WEBP signature";
+    case ZW_ECHUNK_MISSING: return "an expected chunk was missing";
+    case ZW_EINCONSISTENT_SIZES: return "inconsistent image sizes";
+    case ZW_EIMAGE_TOO_LARGE: return "image too large";
     default: return "unknown error";
     }
 }

@@ -24,9 +24,10 @@ struct zw_ctx {
     // grow-only pinned host staging (decode batch: MB records up, planes down)
     void* hpin[2] = {nullptr, nullptr};
     size_t hpin_cap[2] = {0, 0};
-    // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter (ms)
-    hipEvent_t dev_ev[3] = {nullptr, nullptr, nullptr};
-    float dec_ms[2] = {0.f, 0.f};
+    // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter,
+    // [2] k_yuv2rgb (0 when the batch returned planes) (ms)
+    hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float dec_ms[3] = {0.f, 0.f, 0.f};
 };
 
 #define HIPOK(x)                                  \

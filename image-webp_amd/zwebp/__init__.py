@@ -11,6 +11,10 @@ public surface for the lossy path:
   ``EncoderParams.lossy``          ``encoder/api.rs:445`` EncoderParams::lossy
   ``WebPEncoder.encode``           ``encoder/api.rs:1291`` WebPEncoder::encode
   ``vp8_decode_frame``             ``decoder/vp8.rs:1526`` Vp8Decoder::decode_frame
+  ``WebPDecoder``                  ``decoder/api.rs:306-906`` WebPDecoder (lossy)
+  ``decode_rgb/decode_rgba``       ``decoder/api.rs:938-993``
+  ``UpsamplingMethod``             ``decoder/api.rs:268``
+  ``yuv_to_rgb``                   ``decoder/yuv.rs:82/:402`` fill_rgb_buffer_*
   ``rgb_to_yuv420``                ``decoder/yuv.rs:656`` convert_image_yuv
   ``loop_filter_frame``            ``decoder/vp8.rs:1172`` filter_row_in_cache
   ``EncodingError/DecodingError``  ``encoder/api.rs:35``, ``decoder/api.rs:79``
@@ -28,6 +32,8 @@ __all__ = [
     "ColorType", "EncoderParams", "WebPEncoder", "ZwError", "EncodingError", "DecodingError", "Context",
     "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
     "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "transform_quant_blocks", "library_path", "load_library",
+    "UpsamplingMethod", "WebPDecoder", "decode_rgb", "decode_rgba", "vp8_decode_rgb", "decode_rgb_batch",
+    "yuv_to_rgb", "webp_parse",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +93,12 @@ class _Image(ctypes.Structure):
                 ("height", ctypes.c_uint32), ("color", ctypes.c_int)]
 
 
+class _WebpInfo(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("has_alpha", ctypes.c_int),
+                ("is_lossy", ctypes.c_int), ("is_lossless", ctypes.c_int), ("is_animated", ctypes.c_int),
+                ("vp8_offset", ctypes.c_uint64), ("vp8_len", ctypes.c_uint64)]
+
+
 # (name, restype, argtypes) for every symbol in include/zwebp.h
 _VP, _SZ, _U32, _I, _U8 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint8
 SIGNATURES = [
@@ -100,6 +112,15 @@ SIGNATURES = [
     ("zw_encode_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
+    ("zw_vp8_decode_rgb", _I, [_VP, _VP, _SZ, _I, _I, ctypes.POINTER(_Bytes), ctypes.POINTER(_U32),
+                               ctypes.POINTER(_U32)]),
+    ("zw_vp8_decode_rgb_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _I,
+                                     ctypes.POINTER(_Bytes), _VP, _VP]),
+    ("zw_webp_parse", _I, [_VP, _SZ, ctypes.POINTER(_WebpInfo)]),
+    ("zw_webp_decode", _I, [_VP, _VP, _SZ, _I, _I, ctypes.POINTER(_Bytes), ctypes.POINTER(_U32),
+                            ctypes.POINTER(_U32)]),
+    ("zw_decode_rgb_kernel_ms", _I, [_VP, ctypes.POINTER(ctypes.c_float)]),
+    ("zw_yuv_to_rgb", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _U32, _U32, _I, _I, _VP]),
     ("zw_rgb_to_yuv420", _I, [_VP, _VP, _U32, _U32, _I, _VP, _VP, _VP]),
     ("zw_transform_quant_blocks", _I, [_VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
     ("zw_transform_quant_blocks_device", _I, [_VP, _VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
@@ -329,6 +350,135 @@ def decode_kernel_times(ctx=None):
     ms = (ctypes.c_float * 2)()
     _check(c._lib.zw_decode_kernel_times(c.handle, ms), "decode_kernel_times")
     return float(ms[0]), float(ms[1])
+
+
+class UpsamplingMethod:
+    """UpsamplingMethod (decoder/api.rs:268-279): Bilinear (fancy, default) / Simple."""
+    Bilinear = 0
+    Simple = 1
+
+
+def _take_image(L, b, w, h, bpp):
+    img = np.ctypeslib.as_array((ctypes.c_uint8 * b.len).from_address(b.data)).copy() if b.len else \
+        np.zeros(0, np.uint8)
+    L.zw_bytes_free(ctypes.byref(b))
+    return img.reshape(h, w, bpp)
+
+
+def vp8_decode_rgb(data, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
+    """decode_frame + Frame::fill_rgb / fill_rgba (decoder/vp8.rs:200-258) on the device: (h, w, bpp) u8."""
+    c = _ctx(ctx)
+    L = c._lib
+    a = _as_u8(data)
+    out, w, h = _Bytes(), ctypes.c_uint32(), ctypes.c_uint32()
+    _check(L.zw_vp8_decode_rgb(c.handle, _ptr(a) if a.size else None, a.size, bpp, upsampling, ctypes.byref(out),
+                               ctypes.byref(w), ctypes.byref(h)), "decode_rgb", DecodingError)
+    return _take_image(L, out, w.value, h.value, bpp)
+
+
+def decode_rgb_batch(frames, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
+    """vp8_decode_rgb over frames of identical dimensions, one device pass."""
+    c = _ctx(ctx)
+    L = c._lib
+    arrs = [_as_u8(d) for d in frames]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    lens = (ctypes.c_size_t * n)(*[a.size for a in arrs])
+    outs = (_Bytes * n)()
+    ws, hs = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+    _check(L.zw_vp8_decode_rgb_batch(c.handle, n, ptrs, lens, bpp, upsampling, outs, ws, hs), "decode_rgb_batch",
+           DecodingError)
+    return [_take_image(L, outs[i], ws[i], hs[i], bpp) for i in range(n)]
+
+
+def decode_rgb_kernel_ms(ctx=None):
+    """Device ms of the last RGB decode batch's k_yuv2rgb launch."""
+    c = _ctx(ctx)
+    ms = ctypes.c_float()
+    _check(c._lib.zw_decode_rgb_kernel_ms(c.handle, ctypes.byref(ms)), "decode_rgb_kernel_ms")
+    return float(ms.value)
+
+
+def webp_parse(data):
+    """WebPDecoder::new's container parse (decoder/api.rs:334-510): dict of the header facts."""
+    L = load_library()
+    a = _as_u8(data)
+    info = _WebpInfo()
+    rc = L.zw_webp_parse(_ptr(a) if a.size else None, a.size, ctypes.byref(info))
+    _check(rc, "WebPDecoder::new", DecodingError)
+    return {f: getattr(info, f) for f, _ in _WebpInfo._fields_}
+
+
+def _webp_decode(data, bpp, upsampling, ctx):
+    c = _ctx(ctx)
+    L = c._lib
+    a = _as_u8(data)
+    out, w, h = _Bytes(), ctypes.c_uint32(), ctypes.c_uint32()
+    _check(L.zw_webp_decode(c.handle, _ptr(a) if a.size else None, a.size, bpp, upsampling, ctypes.byref(out),
+                            ctypes.byref(w), ctypes.byref(h)), "decode", DecodingError)
+    return _take_image(L, out, w.value, h.value, bpp), w.value, h.value
+
+
+def decode_rgba(data, ctx=None):
+    """decode_rgba (decoder/api.rs:938): (flat RGBA bytes, width, height); lossy files."""
+    img, w, h = _webp_decode(data, 4, UpsamplingMethod.Bilinear, ctx)
+    return img.reshape(-1), w, h
+
+
+def decode_rgb(data, ctx=None):
+    """decode_rgb (decoder/api.rs:973): (flat RGB bytes, width, height); lossy files."""
+    img, w, h = _webp_decode(data, 3, UpsamplingMethod.Bilinear, ctx)
+    return img.reshape(-1), w, h
+
+
+class WebPDecoder:
+    """WebPDecoder (decoder/api.rs:306-906), lossy subset: new / dimensions / has_alpha /
+    is_lossy / output_buffer_size / set_lossy_upsampling / read_image."""
+
+    def __init__(self, data, ctx=None):
+        self._data = _as_u8(data)
+        self._ctx = ctx
+        self._info = webp_parse(self._data)
+        self._up = UpsamplingMethod.Bilinear
+
+    def dimensions(self):
+        return self._info["width"], self._info["height"]
+
+    def has_alpha(self):
+        return bool(self._info["has_alpha"])
+
+    def is_lossy(self):
+        return bool(self._info["is_lossy"])
+
+    def output_buffer_size(self):
+        w, h = self.dimensions()
+        return w * h * (4 if self.has_alpha() else 3)
+
+    def set_lossy_upsampling(self, method):
+        self._up = method
+
+    def read_image(self, buf=None):
+        """Decodes into `buf` (a writable u8 buffer of output_buffer_size()) or returns a new array."""
+        bpp = 4 if self.has_alpha() else 3
+        img, _, _ = _webp_decode(self._data, bpp, self._up, self._ctx)
+        flat = img.reshape(-1)
+        if buf is None:
+            return flat
+        dst = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf.reshape(-1)
+        if dst.size != flat.size:
+            raise DecodingError(3, "read_image: buffer size")  # ImageTooLarge / InvalidParameter in the reference
+        dst[:] = flat
+        return dst
+
+
+def yuv_to_rgb(y, u, v, width, height, y_stride, uv_stride, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
+    """fill_rgb_buffer_fancy / _simple (decoder/yuv.rs:82 / :402) on the device: (h, w, bpp) u8."""
+    c = _ctx(ctx)
+    y, u, v = _as_u8(y), _as_u8(u), _as_u8(v)
+    out = np.zeros(width * height * bpp, np.uint8)
+    _check(c._lib.zw_yuv_to_rgb(c.handle, _ptr(y), _ptr(u), _ptr(v), width, height, y_stride, uv_stride, bpp,
+                                upsampling, _ptr(out)), "yuv_to_rgb")
+    return out.reshape(height, width, bpp)
 
 
 def rgb_to_yuv420(img, width, height, bpp, ctx=None):

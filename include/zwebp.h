@@ -10,6 +10,10 @@
  *                            the ALPH/VP8L lossless encoder is out of scope)
  *   zw_encode_batch         many independent encode_frame_lossy calls (new: batch)
  *   zw_vp8_decode_frame     Vp8Decoder::decode_frame  src/decoder/vp8.rs:1526
+ *   zw_vp8_decode_rgb       decode_frame + Frame::fill_rgb/fill_rgba  src/decoder/vp8.rs:200-258
+ *   zw_webp_parse           WebPDecoder::new (read_data)  src/decoder/api.rs:334-510
+ *   zw_webp_decode          decode_rgb / decode_rgba   src/decoder/api.rs:938-993
+ *   zw_yuv_to_rgb           fill_rgb_buffer_fancy/_simple  src/decoder/yuv.rs:82 / :402
  *   zw_rgb_to_yuv420        convert_image_yuv/_y      src/decoder/yuv.rs:656 / :806
  *   zw_loop_filter_frame    filter_row_in_cache       src/decoder/vp8.rs:1172-1345
  *
@@ -47,8 +51,17 @@ enum {
     ZW_ECHROMA_MODE = 14,
     ZW_EBITSTREAM = 15,
     ZW_EUNSUPPORTED_FEATURE = 16,
-    ZW_ENOT_ENOUGH_INIT_DATA = 17
+    ZW_ENOT_ENOUGH_INIT_DATA = 17,
+    /* container (WebPDecoder::new / read_image, decoder/api.rs:334-700) */
+    ZW_ECHUNK_HEADER = 18,       /* ChunkHeaderInvalid */
+    ZW_EWEBP_SIGNATURE = 19,     /* WebpSignatureInvalid */
+    ZW_ECHUNK_MISSING = 20,      /* ChunkMissing */
+    ZW_EINCONSISTENT_SIZES = 21, /* InconsistentImageSizes */
+    ZW_EIMAGE_TOO_LARGE = 22     /* ImageTooLarge */
 };
+
+/* UpsamplingMethod (decoder/api.rs:268-279), same order; Bilinear is the default. */
+enum { ZW_UPSAMPLE_BILINEAR = 0, ZW_UPSAMPLE_SIMPLE = 1 };
 
 /* ColorType (api.rs:83-92), same order. */
 enum { ZW_COLOR_L8 = 0, ZW_COLOR_LA8 = 1, ZW_COLOR_RGB8 = 2, ZW_COLOR_RGBA8 = 3 };
@@ -68,6 +81,13 @@ typedef struct {
     uint8_t *y, *u, *v;
     uint8_t filter_type, filter_level, sharpness_level, pad;
 } zw_frame;
+
+/* What WebPDecoder::new learns from the container (decoder/api.rs:334-510). */
+typedef struct {
+    uint32_t width, height; /* canvas */
+    int has_alpha, is_lossy, is_lossless, is_animated;
+    uint64_t vp8_offset, vp8_len; /* the "VP8 " chunk payload inside the file */
+} zw_webp_info;
 
 typedef struct {
     const uint8_t *data; /* host pointer, w*h*bpp bytes */
@@ -97,13 +117,36 @@ int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, u
 int zw_vp8_decode_frame(zw_ctx *ctx, const uint8_t *vp8, size_t len, zw_frame *out);
 /* n independent decode_frame calls on frames of identical dimensions (new: batch). */
 int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, zw_frame *outs);
+/* decode_frame + Frame::fill_rgb (bpp 3) / fill_rgba (bpp 4, alpha 255 as
+ * decode_rgba) (decoder/vp8.rs:200-258, yuv.rs:82 / :402) on the device: the
+ * packed w*h*bpp image is returned in out (free with zw_bytes_free).
+ * upsampling: ZW_UPSAMPLE_BILINEAR (fancy) or ZW_UPSAMPLE_SIMPLE. */
+int zw_vp8_decode_rgb(zw_ctx *ctx, const uint8_t *vp8, size_t len, int bpp, int upsampling, zw_bytes *out,
+                      uint32_t *width, uint32_t *height);
+/* n frames of identical dimensions (new: batch); widths/heights may be NULL. */
+int zw_vp8_decode_rgb_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, int bpp,
+                            int upsampling, zw_bytes *outs, uint32_t *widths, uint32_t *heights);
+/* WebPDecoder::new (container parse, no decoding; lossy subset: ALPH, VP8L and
+ * animation return ZW_EUNSUPPORTED with info filled as far as parsed). */
+int zw_webp_parse(const uint8_t *data, size_t len, zw_webp_info *info);
+/* decode_rgb (bpp 3) / decode_rgba (bpp 4) (decoder/api.rs:938-993) of a lossy
+ * WebP file; WebPDecoder::set_lossy_upsampling via `upsampling`. */
+int zw_webp_decode(zw_ctx *ctx, const uint8_t *data, size_t len, int bpp, int upsampling, zw_bytes *out,
+                   uint32_t *width, uint32_t *height);
 /* Device time (HIP events on the context stream) of the last decode batch:
  * ms[0] = k_dec_recon (dequant + iWHT/iDCT + prediction), ms[1] = k_loopfilter. */
 int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
+/* ... and of its k_yuv2rgb launch (0 when the batch returned planes). */
+int zw_decode_rgb_kernel_ms(zw_ctx *ctx, float *ms);
 
 /* Kernel-level entry points (host buffers in/out) for parity testing. */
 int zw_rgb_to_yuv420(zw_ctx *ctx, const uint8_t *img, uint32_t width, uint32_t height, int bpp, uint8_t *y,
                      uint8_t *u, uint8_t *v);
+/* fill_rgb_buffer_fancy (upsampling 0) / fill_rgb_buffer_simple (1) of one
+ * image's planes (rows of y_stride / uv_stride bytes, ceil(h/2) chroma rows)
+ * into out: w*h*bpp bytes, packed; bpp 4 writes alpha 255. */
+int zw_yuv_to_rgb(zw_ctx *ctx, const uint8_t *y, const uint8_t *u, const uint8_t *v, uint32_t width,
+                  uint32_t height, uint32_t y_stride, uint32_t uv_stride, int bpp, int upsampling, uint8_t *out);
 /* Quantisation of n 4x4 coefficient blocks (natural order in, zigzag levels and
  * natural-order dequantised values out): VP8Matrix::quantize_coeff
  * (encoder/cost.rs:457) or trellis_quantize_block (cost.rs:788-1006) with level

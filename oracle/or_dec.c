@@ -534,6 +534,13 @@ void or_yuv_to_rgb_fancy_c(const uint8_t *y, const uint8_t *u, const uint8_t *v,
     if (bpp == 4)
         for (size_t i = 0; i < (size_t)w * h; i++) out[i * 4 + 3] = 255;
 }
+void or_yuv_to_rgb_simple_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out)
+{
+    int mbw = (w + 15) / 16;
+    or_yuv_to_rgb_simple(y, u, v, w, h, mbw * 16, bpp, out);
+    if (bpp == 4)
+        for (size_t i = 0; i < (size_t)w * h; i++) out[i * 4 + 3] = 255;
+}
 size_t or_debug_struct_size(void) { return sizeof(or_enc_debug); }
 /* all ten I4 predictions for a 13-pixel edge (L3,L2,L1,L0,P,A0..A7) */
 void or_i4_preds_edge_c(const uint8_t e[13], uint8_t out[160])

@@ -570,6 +570,21 @@ void or_yuv_to_rgb_fancy(const uint8_t *Y, const uint8_t *U, const uint8_t *V, i
     }
 }
 
+/* fill_rgb_buffer_simple + fill_rgba_row_simple_scalar, yuv.rs:402-515: every
+ * chroma row serves two luma rows, every chroma sample two pixels; the odd
+ * final pixel of a row takes the next chroma sample.  For BPP 4 the caller
+ * fills alpha. */
+void or_yuv_to_rgb_simple(const uint8_t *Y, const uint8_t *U, const uint8_t *V, int w, int h,
+                          int bw, int bpp, uint8_t *out)
+{
+    int cbw = bw / 2;
+    for (int r = 0; r < h; r++) {
+        const uint8_t *yr = Y + (size_t)r * bw, *ur = U + (size_t)(r / 2) * cbw, *vr = V + (size_t)(r / 2) * cbw;
+        uint8_t *o = out + (size_t)r * w * bpp;
+        for (int x = 0; x < w; x++) set_px(o + (size_t)x * bpp, yr[x], ur[x / 2], vr[x / 2]);
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* Loop filter (decoder/loop_filter.rs; order decoder/vp8.rs:1172-1345)      */
 /* ------------------------------------------------------------------------ */

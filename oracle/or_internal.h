@@ -47,6 +47,8 @@ void or_i4_preds(const uint8_t *src, int x0, int y0, int stride, uint8_t out[10]
 
 /* ---- colour (decoder/yuv.rs) ---- */
 void or_rgb_to_yuv420(const uint8_t *img, int w, int h, int bpp, uint8_t *y, uint8_t *u, uint8_t *v);
+void or_yuv_to_rgb_simple(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bw, int bpp,
+                          uint8_t *out);
 void or_yuv_to_rgb_fancy(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h,
                          int buffer_width, int bpp, uint8_t *out);
 

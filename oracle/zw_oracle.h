@@ -94,6 +94,7 @@ void or_iwht_c(int32_t *blk, int n);
 void or_loop_filter_c(uint8_t *y, uint8_t *u, uint8_t *v, int mbw, int mbh, const or_mb_info *mbs,
                       const or_frame_hdr *hdr);
 void or_yuv_to_rgb_fancy_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
+void or_yuv_to_rgb_simple_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
 void or_analyze(const uint8_t *Y, const uint8_t *U, const uint8_t *V, int width, int height,
                 uint8_t *mb_alphas, uint32_t histo[256]);
 int or_quality_to_quant_index(int quality);

@@ -61,6 +61,7 @@ def lib():
         L.or_rgb_to_yuv420_c.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3
         L.or_loop_filter_c.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.or_yuv_to_rgb_fancy_c.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+        L.or_yuv_to_rgb_simple_c.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
         L.or_analyze.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.or_bool_encoder_kat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         L.or_trellis_kat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -193,6 +194,16 @@ def yuv_to_rgb_fancy(y, u, v, w, h, bpp=3):
     y, u, v = (np.ascontiguousarray(a, dtype=np.uint8) for a in (y, u, v))
     out = np.zeros(w * h * bpp, np.uint8)
     lib().or_yuv_to_rgb_fancy_c(_p(y), _p(u), _p(v), w, h, bpp, _p(out))
+    return out
+
+
+def yuv_to_rgb_simple(y, u, v, w, h, bpp=3):
+    """fill_rgb_buffer_simple (decoder/yuv.rs:402); planes MB-padded (stride mbw*16 / mbw*8)."""
+    y = np.ascontiguousarray(y, np.uint8)
+    u = np.ascontiguousarray(u, np.uint8)
+    v = np.ascontiguousarray(v, np.uint8)
+    out = np.zeros(w * h * bpp, np.uint8)
+    lib().or_yuv_to_rgb_simple_c(_p(y), _p(u), _p(v), w, h, bpp, _p(out))
     return out
 
 

@@ -1,0 +1,76 @@
+"""Host logic, no GPU: the WebP container parse (WebPDecoder::new -> read_data,
+decoder/api.rs:334-510) behind zw_webp_parse, on the reference's gallery1
+streams (tests/golden/*.vp8, wrapped in the RIFF forms the reference reads)
+and on malformed files, with the DecodingError variant each one maps to."""
+import os
+import struct
+
+import pytest
+
+import zwebp
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _vp8(name="gallery1_1"):
+    return open(os.path.join(GOLD, name + ".vp8"), "rb").read()
+
+
+def _chunk(tag, payload):
+    return tag + struct.pack("<I", len(payload)) + payload + (b"\0" if len(payload) & 1 else b"")
+
+
+def _riff(*chunks):
+    body = b"WEBP" + b"".join(chunks)
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def _vp8x(w, h, flags=0):
+    return _chunk(b"VP8X", bytes([flags, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little"))
+
+
+def test_simple_lossy():
+    vp8 = _vp8()
+    info = zwebp.webp_parse(_riff(_chunk(b"VP8 ", vp8)))
+    assert (info["width"], info["height"]) == (550, 368)
+    assert info["is_lossy"] and not info["has_alpha"] and not info["is_animated"]
+    assert info["vp8_offset"] == 20 and info["vp8_len"] == len(vp8)
+
+
+def test_extended_lossy_with_metadata_chunks():
+    vp8 = _vp8()
+    f = _riff(_vp8x(550, 368, flags=0x08), _chunk(b"EXIF", b"x" * 7), _chunk(b"VP8 ", vp8))
+    info = zwebp.webp_parse(f)
+    assert info["is_lossy"] and (info["width"], info["height"]) == (550, 368)
+    assert f[info["vp8_offset"]:info["vp8_offset"] + info["vp8_len"]] == vp8
+
+
+@pytest.mark.parametrize("mutate,code", [
+    (lambda f: b"RIFX" + f[4:], 18),                       # ChunkHeaderInvalid(RIFF)
+    (lambda f: f[:8] + b"WEBQ" + f[12:], 19),              # WebpSignatureInvalid
+    (lambda f: f[:12] + b"ABCD" + f[16:], 18),             # ChunkHeaderInvalid(first chunk)
+    (lambda f: f[:23] + b"\0\0\0" + f[26:], 10),            # Vp8MagicInvalid
+    (lambda f: f[:20] + bytes([f[20] | 1]) + f[21:], 16),  # non-keyframe: UnsupportedFeature
+    (lambda f: f[:26] + b"\0\0" + f[28:], 21),              # width 0: InconsistentImageSizes
+    (lambda f: f[:10], 15),                                 # truncated: BitStreamError
+])
+def test_malformed(mutate, code):
+    f = _riff(_chunk(b"VP8 ", _vp8()))
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.webp_parse(mutate(f))
+    assert e.value.code == code
+
+
+def test_out_of_scope_forms():
+    vp8 = _vp8()
+    # VP8L (lossless), ALPH-carrying VP8X, animation: outside the lossy block-transform path
+    for f in (_riff(_chunk(b"VP8L", b"\x2f" + b"\0" * 8)),
+              _riff(_vp8x(550, 368, flags=0x10), _chunk(b"ALPH", b"\0" * 9), _chunk(b"VP8 ", vp8)),
+              _riff(_vp8x(550, 368, flags=0x02), _chunk(b"ANIM", b"\0" * 6))):
+        with pytest.raises(zwebp.DecodingError) as e:
+            zwebp.webp_parse(f)
+        assert e.value.code == 5
+    # VP8X with no image chunk: ChunkMissing
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.webp_parse(_riff(_vp8x(8, 8)))
+    assert e.value.code == 20

@@ -1,0 +1,152 @@
+"""GPU parity of the decoder's YUV -> RGB(A) stage (SURVEY §8(f) row 2:
+fill_rgb_buffer_fancy / fill_rgb_buffer_simple, decoder/yuv.rs:82-515) and the
+lossy WebP decode entry points built on it (decode_rgb / decode_rgba /
+WebPDecoder::read_image, decoder/api.rs:640-993).
+
+Pinned against the reference's own RGB goldens (tests/reference/gallery1 and
+gallery1_nofancy PNG digests in tests/golden/decode_golden.json, i.e. the
+reference's tests/decode.rs reftests) and bit-exact against the oracle
+(oracle/or_dsp.c) on random planes of every parity of width and height."""
+import hashlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import zwebp
+from zwebp.synth import synth_rgba
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+BIL, SIMPLE = zwebp.UpsamplingMethod.Bilinear, zwebp.UpsamplingMethod.Simple
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return zwebp.Context(0)
+
+
+def _manifest():
+    with open(os.path.join(GOLD, "decode_golden.json")) as f:
+        return json.load(f)["streams"]
+
+
+def _oracle_rgb(y, u, v, w, h, bpp, up):
+    fn = O.yuv_to_rgb_fancy if up == BIL else O.yuv_to_rgb_simple
+    return fn(y, u, v, w, h, bpp)
+
+
+def _riff(vp8):
+    body = b"WEBP" + b"VP8 " + struct.pack("<I", len(vp8)) + vp8 + (b"\0" if len(vp8) & 1 else b"")
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (1, 2), (2, 1), (2, 2), (3, 3), (5, 4), (4, 5), (17, 9), (16, 16),
+                                 (33, 31), (250, 31), (1920, 1080)])
+@pytest.mark.parametrize("bpp", [3, 4])
+@pytest.mark.parametrize("up", [BIL, SIMPLE])
+def test_yuv_to_rgb_kernel(ctx, w, h, bpp, up):
+    rng = np.random.default_rng(w * 7919 + h * 31 + bpp + 5 * up)
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    y = rng.integers(0, 256, mbw * 16 * mbh * 16, dtype=np.uint8)
+    u = rng.integers(0, 256, mbw * 8 * mbh * 8, dtype=np.uint8)
+    v = rng.integers(0, 256, mbw * 8 * mbh * 8, dtype=np.uint8)
+    got = zwebp.yuv_to_rgb(y, u, v, w, h, mbw * 16, mbw * 8, bpp, up, ctx=ctx)
+    exp = _oracle_rgb(y, u, v, w, h, bpp, up)
+    assert np.array_equal(got.reshape(-1), exp)
+
+
+def test_yuv_to_rgb_extremes(ctx):
+    # clip both ends: every (y, u, v) corner of the cube
+    w, h = 16, 16
+    y = np.zeros(256, np.uint8)
+    u = np.zeros(64, np.uint8)
+    v = np.zeros(64, np.uint8)
+    for i, (a, b, c) in enumerate([(0, 0, 0), (255, 255, 255), (0, 255, 0), (255, 0, 255), (0, 0, 255),
+                                   (255, 255, 0), (128, 0, 255), (16, 240, 16)]):
+        y[i * 32:(i + 1) * 32] = a
+        u[i * 8:(i + 1) * 8] = b
+        v[i * 8:(i + 1) * 8] = c
+    for up in (BIL, SIMPLE):
+        got = zwebp.yuv_to_rgb(y, u, v, w, h, 16, 8, 3, up, ctx=ctx)
+        assert np.array_equal(got.reshape(-1), _oracle_rgb(y, u, v, w, h, 3, up))
+
+
+@pytest.mark.parametrize("entry", [e for e in _manifest() if "rgb_sha256" in e], ids=lambda e: e["name"])
+def test_decode_rgb_reference_goldens(ctx, entry):
+    """The reference's own reftests: gallery1 fancy and nofancy PNG pixels."""
+    vp8 = open(os.path.join(GOLD, entry["name"] + ".vp8"), "rb").read()
+    w, h = entry["width"], entry["height"]
+    rgb = zwebp.vp8_decode_rgb(vp8, 3, BIL, ctx=ctx)
+    assert rgb.shape == (h, w, 3)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == entry["rgb_sha256"]
+    rgb = zwebp.vp8_decode_rgb(vp8, 3, SIMPLE, ctx=ctx)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == entry["rgb_nofancy_sha256"]
+    # the container path: decode_rgb / decode_rgba / WebPDecoder
+    riff = _riff(vp8)
+    flat, ww, hh = zwebp.decode_rgb(riff, ctx=ctx)
+    assert (ww, hh) == (w, h) and hashlib.sha256(flat.tobytes()).hexdigest() == entry["rgb_sha256"]
+    rgba, ww, hh = zwebp.decode_rgba(riff, ctx=ctx)
+    rgba = rgba.reshape(h, w, 4)
+    assert (rgba[..., 3] == 255).all()
+    assert hashlib.sha256(np.ascontiguousarray(rgba[..., :3]).tobytes()).hexdigest() == entry["rgb_sha256"]
+    dec = zwebp.WebPDecoder(riff, ctx=ctx)
+    assert dec.dimensions() == (w, h) and dec.is_lossy() and not dec.has_alpha()
+    assert dec.output_buffer_size() == w * h * 3
+    dec.set_lossy_upsampling(SIMPLE)
+    buf = bytearray(dec.output_buffer_size())
+    dec.read_image(buf)
+    assert hashlib.sha256(bytes(buf)).hexdigest() == entry["rgb_nofancy_sha256"]
+
+
+@pytest.mark.parametrize("entry", _manifest(), ids=lambda e: e["name"])
+def test_decode_rgb_matches_oracle(ctx, entry):
+    vp8 = open(os.path.join(GOLD, entry["name"] + ".vp8"), "rb").read()
+    rc, r = O.decode(vp8)
+    assert rc == 0
+    w, h = entry["width"], entry["height"]
+    for bpp in (3, 4):
+        for up in (BIL, SIMPLE):
+            got = zwebp.vp8_decode_rgb(vp8, bpp, up, ctx=ctx)
+            exp = _oracle_rgb(r["y"], r["u"], r["v"], w, h, bpp, up)
+            assert np.array_equal(got.reshape(-1), exp), (bpp, up)
+
+
+def test_decode_rgb_batch(ctx):
+    w, h = 161, 97
+    streams = [O.encode(synth_rgba(w, h, 0x5EED0000 + i), w, h, 3, 20 + 15 * i, 4)[1] for i in range(5)]
+    imgs = zwebp.decode_rgb_batch(streams, 4, BIL, ctx=ctx)
+    assert zwebp.decode_rgb_kernel_ms(ctx=ctx) > 0
+    for s, img in zip(streams, imgs):
+        rc, r = O.decode(s)
+        assert np.array_equal(img.reshape(-1), _oracle_rgb(r["y"], r["u"], r["v"], w, h, 4, BIL))
+
+
+def test_encode_decode_rgb_roundtrip(ctx):
+    """Our encoder -> RIFF -> our RGB decoder == oracle decode + oracle upsampling."""
+    w, h = 333, 211
+    img = np.ascontiguousarray(synth_rgba(w, h, 0x5EED0042)[..., :3])
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    riff = bytes(enc.encode(img, w, h, zwebp.ColorType.Rgb8))
+    flat, ww, hh = zwebp.decode_rgb(riff, ctx=ctx)
+    rc, r = O.decode(O.riff_vp8_chunk(riff))
+    assert (ww, hh) == (w, h)
+    assert np.array_equal(flat, _oracle_rgb(r["y"], r["u"], r["v"], w, h, 3, BIL))
+    # lossy at Q75: close to the source
+    assert np.abs(flat.reshape(h, w, 3).astype(int) - img.astype(int)).mean() < 8
+
+
+def test_decode_rgb_errors(ctx):
+    vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
+    with pytest.raises(zwebp.DecodingError):
+        zwebp.vp8_decode_rgb(vp8[:20], 3, BIL, ctx=ctx)
+    with pytest.raises(zwebp.ZwError) as e:
+        zwebp.vp8_decode_rgb(vp8, 2, BIL, ctx=ctx)
+    assert e.value.code == 3
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.decode_rgb(b"RIFF\0\0\0\0WEBQ", ctx=ctx)
+    assert e.value.code == 19

@@ -144,6 +144,10 @@ def test_oracle_decoder_matches_goldens(entry):
         Yc, Uc, Vc = planes
         rgb = O.yuv_to_rgb_fancy(Yc.reshape(-1), Uc.reshape(-1), Vc.reshape(-1), w, h)
         assert hashlib.sha256(rgb.tobytes()).hexdigest() == entry["rgb_sha256"]
+    if "rgb_nofancy_sha256" in entry:
+        # UpsamplingMethod::Simple goldens (tests/decode.rs:168-190, reference/gallery1_nofancy)
+        rgb = O.yuv_to_rgb_simple(r["y"], r["u"], r["v"], w, h)
+        assert hashlib.sha256(rgb.tobytes()).hexdigest() == entry["rgb_nofancy_sha256"]
 
 
 def test_oracle_decoder_errors():

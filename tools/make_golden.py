@@ -8,6 +8,8 @@ Inputs and expected outputs only -- no reference source is copied:
   * Expected results:
       - rgb_sha256: SHA-256 of the reference's golden PNG pixels
         (tests/reference/gallery1/*.png, fancy upsampling), RGB rows, for gallery1;
+      - rgb_nofancy_sha256: the same for tests/reference/gallery1_nofancy/*.png
+        (UpsamplingMethod::Simple), gallery1;
       - yuv_sha256: SHA-256 of the cropped Y, U, V planes decoded by the system
         libwebp (WebPDecodeYUV), the independent decoder the survey pins on.
   * libwebp-encoded synthetic streams (WebPEncodeRGB at several qualities) with
@@ -90,8 +92,12 @@ def main():
         W, H, d = libwebp_yuv_digests(riff)
         png = np.asarray(Image.open(f"{REF}/reference/gallery1/{i}.png").convert("RGB"))
         assert png.shape == (H, W, 3)
+        # UpsamplingMethod::Simple goldens (tests/decode.rs:168-190 reftest_nofancy)
+        png_nf = np.asarray(Image.open(f"{REF}/reference/gallery1_nofancy/{i}.png").convert("RGB"))
+        assert png_nf.shape == (H, W, 3)
         manifest["streams"].append(dict(name=name, source=f"tests/images/gallery1/{i}.webp", width=W, height=H,
-                                        yuv_sha256=d, rgb_sha256=hashlib.sha256(png.tobytes()).hexdigest()))
+                                        yuv_sha256=d, rgb_sha256=hashlib.sha256(png.tobytes()).hexdigest(),
+                                        rgb_nofancy_sha256=hashlib.sha256(png_nf.tobytes()).hexdigest()))
     for i in range(1, 6):
         riff = open(f"{REF}/images/gallery2/{i}_webp_a.webp", "rb").read()
         vp8 = riff_vp8(riff)
