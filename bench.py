@@ -160,12 +160,27 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
            "kernel_frames_per_s": frames / ((rk + lf) * 1e-3),
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                         "alg_bytes_per_mb": 1208}}
+    # decode to packed RGBA (decode_rgba: fancy upsampling on the device, k_yuv2rgb);
+    # k_yuv2rgb algorithmic bytes per pixel: Y 1 + U,V 0.5 read, RGBA 4 written
+    zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    t0 = time.perf_counter()
+    zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    el_rgb = time.perf_counter() - t0
+    yk = zwebp.decode_rgb_kernel_ms(ctx=ctx)
+    yb = 5.5 * w * h * frames
+    out["rgba"] = {"batch_decodes_per_s": frames / el_rgb, "k_yuv2rgb_ms": yk,
+                   "roofline": {"bound": "hbm", "achieved": yb / (yk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": yb / (yk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                "alg_bytes_per_px": 5.5}}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         t0 = time.perf_counter()
-        O.decode(bytes(one[0]))
+        rc, r = O.decode(bytes(one[0]))
         out["cpu_baseline_single_frame_ms"] = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        O.yuv_to_rgb_fancy(r["y"], r["u"], r["v"], w, h, 4)
+        out["rgba"]["cpu_baseline_fancy_upsample_ms"] = (time.perf_counter() - t0) * 1e3
     return out
 
 

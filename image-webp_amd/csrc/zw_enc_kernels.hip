@@ -447,7 +447,8 @@ struct SharedHdr {
 struct Ctx {
     const EncArgs* a;
     const ZwFrameParams* P;
-    const ZwSegment* S;
+    const ZwSegment* S;   // the MB's segment, in LDS
+    const ZwSegment* Sl;  // the frame's 4 segments, in LDS
     const LdsTables* T;
     WaveLds* W;
     uint8_t *top_y, *top_u, *top_v, *top_c;
@@ -1376,8 +1377,11 @@ __device__ void setup_ctx(Ctx& C, const EncArgs* a, const ZwFrameParams* P, cons
     wsync();
     int seg = 0;
     if (P->seg_enabled) seg = P->seg_map_lut[a->alpha[(size_t)f * a->mbw * a->mbh + (size_t)mby * a->mbw + mbx]];
+    // wave-uniform: the segment's matrices / lambdas / sharpening then come in
+    // through the scalar cache (s_load into SGPRs) instead of per-lane loads
+    seg = __builtin_amdgcn_readfirstlane(seg);
     C.seg = seg;
-    C.S = &P->seg[seg];
+    C.S = C.Sl + seg;
     (void)shared_base;
 }
 
@@ -1406,6 +1410,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     size_t off = 0;
     LdsTables* T = (LdsTables*)(smem + off);
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
+    ZwSegment* Sl = (ZwSegment*)(smem + off);  // the frame's 4 segments (matrices, lambdas, sharpening)
+    off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
     WaveLds* Wall = (WaveLds*)(smem + off);
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
     int* progress = (int*)(smem + off);
@@ -1429,6 +1435,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         (&T->init[0][0][0])[i] = a.lcost ? (&a.lcost[f].init[0][0][0])[i] : 0;
     }
     for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&T->probs[0][0][0][0])[i] = (&P->probs[0][0][0][0])[i];
+    static_assert(sizeof(ZwSegment) % 4 == 0, "segment copy by dwords");
+    for (int i = threadIdx.x; i < (int)(4 * sizeof(ZwSegment) / 4); i += WG)
+        ((uint32_t*)Sl)[i] = ((const uint32_t*)P->seg)[i];
     load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
@@ -1446,6 +1455,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.T = T;
     C.W = W;
     C.lane = lane;
+    C.Sl = Sl;
     C.top_y = top_y;
     C.top_u = top_u;
     C.top_v = top_v;
@@ -1698,6 +1708,7 @@ extern "C" size_t zw_encode_lds_bytes(int mbw)
 {
     size_t off = 0;
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
+    off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
     off += 64;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;

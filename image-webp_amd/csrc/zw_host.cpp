@@ -831,36 +831,9 @@ extern "C" int zw_encode_webp(zw_ctx* ctx, const uint8_t* data, size_t len, uint
                               int color, uint8_t quality, uint8_t method, zw_bytes* out)
 {
     if (!ctx || !out) return ZW_EINVAL;
-    out->data = nullptr;
-    out->len = 0;
-    if (color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8) return ZW_EUNSUPPORTED; /* VP8X+ALPH needs VP8L */
-    zw_bytes frame = {nullptr, 0};
-    int r = zw_encode_frame_lossy(ctx, data, len, width, height, color, quality, method, &frame);
-    if (r) return r;
-    // simple container: RIFF size = 4 + chunk (8 + payload + pad)  (api.rs:1325-1330)
-    const size_t pad = frame.len & 1;
-    const size_t total = 12 + 8 + frame.len + pad;
-    out->data = (uint8_t*)malloc(total);
-    if (!out->data) {
-        zw_bytes_free(&frame);
-        return ZW_ENOMEM;
-    }
-    uint8_t* o = out->data;
-    auto le32 = [](uint8_t* d, uint32_t v) {
-        d[0] = (uint8_t)v;
-        d[1] = (uint8_t)(v >> 8);
-        d[2] = (uint8_t)(v >> 16);
-        d[3] = (uint8_t)(v >> 24);
-    };
-    memcpy(o, "RIFF", 4);
-    le32(o + 4, (uint32_t)(total - 8));
-    memcpy(o + 8, "WEBPVP8 ", 8);
-    le32(o + 16, (uint32_t)frame.len);
-    memcpy(o + 20, frame.data, frame.len);
-    if (pad) o[20 + frame.len] = 0;
-    out->len = total;
-    zw_bytes_free(&frame);
-    return ZW_OK;
+    // EncoderParams::lossy(quality) with the method set (api.rs:451-458)
+    const zw_encoder_params p = {1, quality, method, 1};
+    return zw_encode_webp_ex(ctx, data, len, width, height, color, &p, nullptr, out);
 }
 
 extern "C" int zw_rgb_to_yuv420(zw_ctx* ctx, const uint8_t* img, uint32_t width, uint32_t height, int bpp, uint8_t* y,

@@ -1,0 +1,521 @@
+// zw_host_lossless.cpp -- host VP8L coder and the extended (VP8X) container.
+//
+// The lossless side of WebPEncoder::encode (encoder/api.rs:1291-1398):
+//   * encode_frame_lossless (:945-1173): subtract-green + left/top predictor
+//     transform, a single Huffman group (green+length 280 symbols, red, blue,
+//     alpha, distance), no colour cache, no backward references other than
+//     runs of the previous pixel (count_run / write_run, :366-417);
+//   * encode_alpha_lossless (:1175-1222): the ALPH chunk every lossy RGBA / LA
+//     encode carries -- the alpha plane as an L8 VP8L image with implicit
+//     dimensions behind a one-byte header;
+//   * the VP8X container with ICCP / ALPH / EXIF / XMP chunks (:1319-1395).
+// Like the VP8 bool coder this is sequential entropy coding and stays on the
+// host.  The Huffman builder reproduces build_huffman_tree (:163-287) including
+// Rust's BinaryHeap tie behaviour (heapify, pop = sift to the bottom then up,
+// peek_mut write-back = sift down), so equal frequencies resolve as in the
+// reference.  Over-long trees (> 15 bits, > 7 for the code-length code) are
+// re-balanced as the reference does; among equal frequencies the reference's
+// sort_unstable order is Rust's ipnsort's and here a stable order (see DESIGN).
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "../../include/zwebp.h"
+#include "zw_host_internal.h"
+
+namespace {
+
+class BitSink {
+  public:
+    explicit BitSink(std::vector<uint8_t>& o) : out_(o) {}
+    // BitWriter::write_bits (:125-137): LSB-first into a 64-bit accumulator
+    void put(uint64_t bits, unsigned n)
+    {
+        acc_ |= bits << fill_;
+        fill_ += n;
+        if (fill_ >= 64) {
+            emit8();
+            fill_ -= 64;
+            const unsigned used = n - fill_;
+            acc_ = used >= 64 ? 0 : bits >> used;
+        }
+    }
+    void finish()  // BitWriter::flush (:139-148)
+    {
+        if (fill_ & 7) put(0, 8 - (fill_ & 7));
+        for (unsigned i = 0; i < fill_ / 8; i++) out_.push_back((uint8_t)(acc_ >> (8 * i)));
+        acc_ = 0;
+        fill_ = 0;
+    }
+
+  private:
+    void emit8()
+    {
+        for (int i = 0; i < 8; i++) out_.push_back((uint8_t)(acc_ >> (8 * i)));
+    }
+    std::vector<uint8_t>& out_;
+    uint64_t acc_ = 0;
+    unsigned fill_ = 0;
+};
+
+void put_single_symbol_code(BitSink& w, unsigned sym)  // write_single_entry_huffman_tree (:152-161)
+{
+    w.put(1, 2);
+    if (sym <= 1) {
+        w.put(0, 1);
+        w.put(sym, 1);
+    } else {
+        w.put(1, 1);
+        w.put(sym, 8);
+    }
+}
+
+// Rust BinaryHeap<Item> where Item's Ord is the REVERSED frequency: the root is
+// the smallest frequency.  `below(a, b)` is Ord's a < b, i.e. a.freq > b.freq.
+struct Node {
+    uint32_t freq;
+    uint16_t id;
+};
+struct RustMinHeap {
+    std::vector<Node> d;
+    static bool below(const Node& a, const Node& b) { return a.freq > b.freq; }
+    static bool not_above(const Node& a, const Node& b) { return a.freq >= b.freq; }  // a <= b
+    void sift_down(size_t pos, size_t end)
+    {
+        const Node el = d[pos];
+        size_t hole = pos, c = 2 * pos + 1;
+        while (c + 2 <= end) {
+            if (not_above(d[c], d[c + 1])) c++;
+            if (!below(el, d[c])) {  // el >= child: in order
+                d[hole] = el;
+                return;
+            }
+            d[hole] = d[c];
+            hole = c;
+            c = 2 * hole + 1;
+        }
+        if (end && c == end - 1 && below(el, d[c])) {
+            d[hole] = d[c];
+            hole = c;
+        }
+        d[hole] = el;
+    }
+    void heapify()
+    {
+        for (size_t k = d.size() / 2; k-- > 0;) sift_down(k, d.size());
+    }
+    Node pop()
+    {
+        Node last = d.back();
+        d.pop_back();
+        if (d.empty()) return last;
+        std::swap(last, d[0]);
+        // sift_down_to_bottom(0) + sift_up(0, hole)
+        const size_t n = d.size();
+        const Node el = d[0];
+        size_t hole = 0, c = 1;
+        while (c + 2 <= n) {
+            if (not_above(d[c], d[c + 1])) c++;
+            d[hole] = d[c];
+            hole = c;
+            c = 2 * hole + 1;
+        }
+        if (c == n - 1) {
+            d[hole] = d[c];
+            hole = c;
+        }
+        while (hole > 0) {
+            const size_t parent = (hole - 1) / 2;
+            if (not_above(el, d[parent])) break;
+            d[hole] = d[parent];
+            hole = parent;
+        }
+        d[hole] = el;
+        return last;
+    }
+};
+
+// build_huffman_tree (:163-287): returns false for <= 1 used symbol.
+bool huffman_lengths_codes(const uint32_t* freq, int n, uint8_t* len, uint16_t* code, int limit)
+{
+    std::fill(len, len + n, 0);
+    std::fill(code, code + n, 0);
+    RustMinHeap h;
+    for (int i = 0; i < n; i++)
+        if (freq[i]) h.d.push_back({freq[i], (uint16_t)i});
+    if (h.d.size() <= 1) return false;
+    h.heapify();
+    std::vector<std::pair<uint16_t, uint16_t>> inner;  // (popped, root) children of node n + k
+    inner.reserve(h.d.size());
+    while (h.d.size() > 1) {
+        const Node a = h.pop();
+        inner.emplace_back(a.id, h.d[0].id);
+        h.d[0] = {a.freq + h.d[0].freq, (uint16_t)(inner.size() + (size_t)n - 1)};
+        h.sift_down(0, h.d.size());
+    }
+    // depths (the walk order does not matter for lengths)
+    std::vector<std::pair<int, int>> todo{{h.d[0].id, 0}};
+    while (!todo.empty()) {
+        auto [node, depth] = todo.back();
+        todo.pop_back();
+        if (node < n) {
+            len[node] = (uint8_t)depth;
+        } else {
+            todo.emplace_back(inner[node - n].first, depth + 1);
+            todo.emplace_back(inner[node - n].second, depth + 1);
+        }
+    }
+    if (*std::max_element(len, len + n) > limit) {
+        uint32_t cnt[16] = {0};
+        for (int i = 0; i < n; i++) cnt[std::min<int>(len[i], limit)]++;
+        uint32_t kraft = 0;
+        for (int l = 1; l <= limit; l++) kraft += cnt[l] << (limit - l);
+        while (kraft > (1u << limit)) {
+            int l = limit - 1;
+            while (!cnt[l]) l--;
+            cnt[l]--;
+            cnt[limit]--;
+            cnt[l + 1] += 2;
+            kraft--;
+        }
+        std::vector<int> order(n);
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return freq[a] < freq[b]; });
+        int l = limit;
+        for (int i : order) {
+            if (!freq[i]) continue;
+            while (!cnt[l]) l--;
+            len[i] = (uint8_t)l;
+            cnt[l]--;
+        }
+    }
+    uint32_t next = 0;  // canonical codes, stored bit-reversed (LSB-first stream)
+    for (int l = 1; l <= limit; l++) {
+        for (int i = 0; i < n; i++) {
+            if (len[i] != l) continue;
+            uint32_t r = 0;
+            for (int b = 0; b < l; b++) r |= ((next >> b) & 1u) << (l - 1 - b);
+            code[i] = (uint16_t)r;
+            next++;
+        }
+        next <<= 1;
+    }
+    return true;
+}
+
+// write_huffman_tree (:289-364)
+void put_huffman_code(BitSink& w, const uint32_t* freq, int n, uint8_t* len, uint16_t* code)
+{
+    if (!huffman_lengths_codes(freq, n, len, code, 15)) {
+        int sym = 0;
+        while (sym < n && !freq[sym]) sym++;
+        put_single_symbol_code(w, (unsigned)(uint8_t)(sym == n ? 0 : sym));
+        return;
+    }
+    uint32_t clf[16] = {0};
+    for (int i = 0; i < n; i++) clf[len[i]]++;
+    uint8_t cll[16];
+    uint16_t clc[16];
+    const bool one_length = !huffman_lengths_codes(clf, 16, cll, clc, 7);
+    static const int kOrder[19] = {17, 18, 0, 1, 2, 3, 4, 5, 16, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+    w.put(0, 1);
+    w.put(15, 4);
+    for (int k = 0; k < 19; k++) {
+        const int i = kOrder[k];
+        w.put(i > 15 || !clf[i] ? 0 : (one_length ? 1 : cll[i]), 3);
+    }
+    if (n == 256) {
+        w.put(1, 1);
+        w.put(3, 3);
+        w.put(254, 8);
+    } else {
+        w.put(0, 1);
+    }
+    if (!one_length)
+        for (int i = 0; i < n; i++) w.put(clc[len[i]], cll[len[i]]);
+}
+
+// length_to_symbol (:355-362) for runs 5..4096
+inline void run_symbol(uint32_t run, uint32_t& sym, uint32_t& extra)
+{
+    const uint32_t v = run - 1, hb = 31 - (uint32_t)__builtin_clz(v);
+    extra = hb - 1;
+    sym = 2 * hb + ((v >> (hb - 1)) & 1u);
+}
+
+}  // namespace
+
+// encode_frame_lossless (:945-1173) into `out` (appended).
+int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color, bool predictor,
+                   bool implicit_dims, std::vector<uint8_t>& out)
+{
+    if (color < ZW_COLOR_L8 || color > ZW_COLOR_RGBA8) return ZW_EINVAL;
+    const int bpp = color + 1;
+    const bool rgb = color >= ZW_COLOR_RGB8, alpha = color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8;
+    if (!data && len) return ZW_EINVAL;
+    if ((uint64_t)width * height * (uint64_t)bpp != (uint64_t)len) return ZW_EINVALID_BUFFER_SIZE;
+    if (width == 0 || width > 16384 || height == 0 || height > 16384) return ZW_EINVALID_DIMENSIONS;
+    BitSink w(out);
+    if (!implicit_dims) {
+        w.put(0x2f, 8);
+        w.put(width - 1, 14);
+        w.put(height - 1, 14);
+        w.put(alpha ? 1 : 0, 1);
+        w.put(0, 3);
+    }
+    w.put(5, 3);  // subtract-green transform
+    if (predictor) {
+        w.put(0x39, 6);  // predictor transform, size bits, no colour cache, mode-2 sub-image
+        w.put(0, 1);
+        put_single_symbol_code(w, 2);
+        for (int i = 0; i < 4; i++) put_single_symbol_code(w, 0);
+    }
+    w.put(0, 1);  // no more transforms
+    w.put(0, 1);  // no colour cache
+    w.put(0, 1);  // no meta Huffman codes
+
+    // ARGB residuals, one uint32 per pixel (bytes r, g, b, a): expand, subtract
+    // green, then the predictor's "pixel minus the pixel above (row 0: left)"
+    const size_t npx = (size_t)width * height;
+    std::vector<uint32_t> px(npx);
+    auto pack = [](uint32_t r, uint32_t g, uint32_t b, uint32_t a) { return r | (g << 8) | (b << 16) | (a << 24); };
+    parallel_for((int)height, [&](int y) {
+        for (size_t x = 0; x < width; x++) {
+            const size_t i = (size_t)y * width + x;
+            const uint8_t* s = data + i * bpp;
+            uint32_t r, g, b, a;
+            switch (color) {
+            case ZW_COLOR_L8: r = g = b = s[0]; a = 255; break;
+            case ZW_COLOR_LA8: r = g = b = s[0]; a = s[1]; break;
+            case ZW_COLOR_RGB8: r = s[0]; g = s[1]; b = s[2]; a = 255; break;
+            default: r = s[0]; g = s[1]; b = s[2]; a = s[3]; break;
+            }
+            px[i] = pack((r - g) & 255, g, (b - g) & 255, a);
+        }
+    });
+    auto bytesub = [](uint32_t c, uint32_t p) {  // per-byte wrapping subtraction
+        return ((c | 0x80808080u) - (p & 0x7f7f7f7fu)) ^ ((c ^ ~p) & 0x80808080u);
+    };
+    if (predictor) {
+        std::vector<uint32_t> up(px);  // rows are differenced against the ORIGINAL row above
+        parallel_for((int)height - 1, [&](int yy) {
+            const size_t y = (size_t)yy + 1;
+            for (size_t x = 0; x < width; x++) px[y * width + x] = bytesub(up[y * width + x], up[(y - 1) * width + x]);
+        });
+        for (size_t x = width - 1; x >= 1; x--) px[x] = bytesub(up[x], up[x - 1]);
+        px[0] = bytesub(up[0], pack(0, 0, 0, 255));
+    }
+
+    // symbol statistics: every pixel codes green (+ red/blue/alpha), then an
+    // optional run of up to 4096 repeats of that pixel
+    uint32_t fr[256] = {0}, fg[280] = {0}, fb[256] = {0}, fa[256] = {0};
+    if (!rgb) fr[0] = fb[0] = 1;
+    if (!alpha) fa[0] = 1;
+    std::vector<uint16_t> runs;  // run after each coded pixel
+    runs.reserve(npx / 2 + 1);
+    for (size_t p = 0; p < npx;) {
+        const uint32_t c = px[p];
+        fg[(c >> 8) & 255]++;
+        if (rgb) {
+            fr[c & 255]++;
+            fb[(c >> 16) & 255]++;
+        }
+        if (alpha) fa[c >> 24]++;
+        uint32_t run = 0;
+        while (run < 4096 && p + 1 + run < npx && px[p + 1 + run] == c) run++;
+        if (run) {
+            if (run <= 4) {
+                fg[256 + run - 1]++;
+            } else {
+                uint32_t s, e;
+                run_symbol(run, s, e);
+                fg[256 + s]++;
+            }
+        }
+        runs.push_back((uint16_t)run);
+        p += 1 + run;
+    }
+    uint8_t lr[256], lg[280], lb[256], la[256];
+    uint16_t cr[256], cg[280], cb[256], ca[256];
+    memset(lr, 0, sizeof lr);
+    memset(lb, 0, sizeof lb);
+    memset(la, 0, sizeof la);
+    memset(cr, 0, sizeof cr);
+    memset(cb, 0, sizeof cb);
+    memset(ca, 0, sizeof ca);
+    put_huffman_code(w, fg, 280, lg, cg);
+    if (rgb) {
+        put_huffman_code(w, fr, 256, lr, cr);
+        put_huffman_code(w, fb, 256, lb, cb);
+    } else {
+        put_single_symbol_code(w, 0);
+        put_single_symbol_code(w, 0);
+    }
+    if (alpha) put_huffman_code(w, fa, 256, la, ca);
+    else put_single_symbol_code(w, predictor ? 0 : 255);
+    put_single_symbol_code(w, 1);  // distance code (unused)
+
+    size_t k = 0;
+    for (size_t p = 0; p < npx; k++) {
+        const uint32_t c = px[p];
+        const uint32_t g = (c >> 8) & 255, r = c & 255, b = (c >> 16) & 255, a = c >> 24;
+        uint64_t bits = cg[g];
+        unsigned nb = lg[g];
+        if (rgb) {
+            bits |= (uint64_t)cr[r] << nb;
+            nb += lr[r];
+            bits |= (uint64_t)cb[b] << nb;
+            nb += lb[b];
+        }
+        if (alpha) {
+            bits |= (uint64_t)ca[a] << nb;
+            nb += la[a];
+        }
+        w.put(bits, nb);
+        const uint32_t run = runs[k];
+        if (run) {
+            if (run <= 4) {
+                w.put(cg[256 + run - 1], lg[256 + run - 1]);
+            } else {
+                uint32_t s, e;
+                run_symbol(run, s, e);
+                w.put(cg[256 + s], lg[256 + s]);
+                w.put((uint64_t)(run - 1) & ((1ull << e) - 1), e);
+            }
+        }
+        p += 1 + run;
+    }
+    w.finish();
+    return ZW_OK;
+}
+
+// encode_alpha_lossless (:1175-1222)
+int zw_alph_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                   std::vector<uint8_t>& out)
+{
+    if (color != ZW_COLOR_LA8 && color != ZW_COLOR_RGBA8) return ZW_EINVAL;
+    if (width == 0 || width > 16384 || height == 0 || height > 16384) return ZW_EINVALID_DIMENSIONS;
+    const int bpp = color == ZW_COLOR_LA8 ? 2 : 4;
+    const size_t npx = (size_t)width * height;
+    if (len != npx * bpp) return ZW_EINVALID_BUFFER_SIZE;
+    std::vector<uint8_t> a(npx);
+    for (size_t i = 0; i < npx; i++) a[i] = data[i * bpp + bpp - 1];
+    out.push_back(1);  // no preprocessing, no filtering, lossless compression
+    return zw_vp8l_encode(a.data(), npx, width, height, ZW_COLOR_L8, true, true, out);
+}
+
+static int to_bytes(const std::vector<uint8_t>& v, zw_bytes* out)
+{
+    out->data = (uint8_t*)malloc(v.size() ? v.size() : 1);
+    if (!out->data) return ZW_ENOMEM;
+    memcpy(out->data, v.data(), v.size());
+    out->len = v.size();
+    return ZW_OK;
+}
+
+extern "C" int zw_encode_frame_lossless(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                                        int use_predictor, zw_bytes* out)
+{
+    if (!out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    std::vector<uint8_t> v;
+    if (int r = zw_vp8l_encode(data, len, width, height, color, use_predictor != 0, false, v)) return r;
+    return to_bytes(v, out);
+}
+
+extern "C" int zw_encode_alpha(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                               zw_bytes* out)
+{
+    if (!out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    std::vector<uint8_t> v;
+    if (int r = zw_alph_encode(data, len, width, height, color, v)) return r;
+    return to_bytes(v, out);
+}
+
+namespace {
+void put_le32(std::vector<uint8_t>& o, uint32_t v)
+{
+    for (int i = 0; i < 4; i++) o.push_back((uint8_t)(v >> (8 * i)));
+}
+uint32_t chunk_bytes(size_t payload) { return (uint32_t)(payload + (payload & 1) + 8); }  // chunk_size (:1224)
+void put_chunk(std::vector<uint8_t>& o, const char* tag, const uint8_t* p, size_t n)  // write_chunk (:1232)
+{
+    o.insert(o.end(), tag, tag + 4);
+    put_le32(o, (uint32_t)n);
+    if (n) o.insert(o.end(), p, p + n);
+    if (n & 1) o.push_back(0);
+}
+}  // namespace
+
+// WebPEncoder::encode (:1291-1398) with EncoderParams and metadata.
+extern "C" int zw_encode_webp_ex(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
+                                 int color, const zw_encoder_params* params, const zw_metadata* meta, zw_bytes* out)
+{
+    if (!out) return ZW_EINVAL;
+    out->data = nullptr;
+    out->len = 0;
+    zw_encoder_params prm = {0, 95, 4, 1};  // EncoderParams::default(): lossless, predictor on
+    if (params) prm = *params;
+    zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
+    if (meta) md = *meta;
+    if (color < ZW_COLOR_L8 || color > ZW_COLOR_RGBA8) return ZW_EINVAL;
+    const bool has_alpha = color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8;
+    const bool lossy_alpha = prm.use_lossy && has_alpha;
+
+    std::vector<uint8_t> frame;
+    const char* tag;
+    if (prm.use_lossy) {
+        if (!ctx) return ZW_EINVAL;
+        zw_bytes f = {nullptr, 0};
+        if (int r = zw_encode_frame_lossy(ctx, data, len, width, height, color, prm.lossy_quality, prm.method, &f))
+            return r;
+        frame.assign(f.data, f.data + f.len);
+        zw_bytes_free(&f);
+        tag = "VP8 ";
+    } else {
+        if (int r = zw_vp8l_encode(data, len, width, height, color, prm.use_predictor_transform != 0, false, frame))
+            return r;
+        tag = "VP8L";
+    }
+    std::vector<uint8_t> o;
+    const bool simple = !md.icc_len && !md.exif_len && !md.xmp_len && !lossy_alpha;
+    if (simple) {
+        o.insert(o.end(), {'R', 'I', 'F', 'F'});
+        put_le32(o, chunk_bytes(frame.size()) + 4);
+        o.insert(o.end(), {'W', 'E', 'B', 'P'});
+        put_chunk(o, tag, frame.data(), frame.size());
+        return to_bytes(o, out);
+    }
+    std::vector<uint8_t> alph;
+    uint32_t total = 22 + chunk_bytes(frame.size());
+    if (md.icc_len) total += chunk_bytes(md.icc_len);
+    if (md.exif_len) total += chunk_bytes(md.exif_len);
+    if (md.xmp_len) total += chunk_bytes(md.xmp_len);
+    if (lossy_alpha) {
+        if (int r = zw_alph_encode(data, len, width, height, color, alph)) return r;
+        total += chunk_bytes(alph.size());
+    }
+    uint8_t flags = 0;
+    if (md.xmp_len) flags |= 1 << 2;
+    if (md.exif_len) flags |= 1 << 3;
+    if (has_alpha) flags |= 1 << 4;
+    if (md.icc_len) flags |= 1 << 5;
+    o.insert(o.end(), {'R', 'I', 'F', 'F'});
+    put_le32(o, total);
+    o.insert(o.end(), {'W', 'E', 'B', 'P'});
+    uint8_t x[10] = {flags, 0, 0, 0};
+    for (int i = 0; i < 3; i++) {
+        x[4 + i] = (uint8_t)((width - 1) >> (8 * i));
+        x[7 + i] = (uint8_t)((height - 1) >> (8 * i));
+    }
+    put_chunk(o, "VP8X", x, 10);
+    if (md.icc_len) put_chunk(o, "ICCP", md.icc, md.icc_len);
+    if (lossy_alpha) put_chunk(o, "ALPH", alph.data(), alph.size());
+    put_chunk(o, tag, frame.data(), frame.size());
+    if (md.exif_len) put_chunk(o, "EXIF", md.exif, md.exif_len);
+    if (md.xmp_len) put_chunk(o, "XMP ", md.xmp, md.xmp_len);
+    return to_bytes(o, out);
+}

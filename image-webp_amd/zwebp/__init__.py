@@ -33,7 +33,7 @@ __all__ = [
     "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
     "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "transform_quant_blocks", "library_path", "load_library",
     "UpsamplingMethod", "WebPDecoder", "decode_rgb", "decode_rgba", "vp8_decode_rgb", "decode_rgb_batch",
-    "yuv_to_rgb", "webp_parse",
+    "yuv_to_rgb", "webp_parse", "encode_frame_lossless", "encode_alpha",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -93,6 +93,16 @@ class _Image(ctypes.Structure):
                 ("height", ctypes.c_uint32), ("color", ctypes.c_int)]
 
 
+class _EncParams(ctypes.Structure):
+    _fields_ = [("use_lossy", ctypes.c_int), ("lossy_quality", ctypes.c_uint8), ("method", ctypes.c_uint8),
+                ("use_predictor_transform", ctypes.c_int)]
+
+
+class _Metadata(ctypes.Structure):
+    _fields_ = [("icc", ctypes.c_void_p), ("icc_len", ctypes.c_size_t), ("exif", ctypes.c_void_p),
+                ("exif_len", ctypes.c_size_t), ("xmp", ctypes.c_void_p), ("xmp_len", ctypes.c_size_t)]
+
+
 class _WebpInfo(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("has_alpha", ctypes.c_int),
                 ("is_lossy", ctypes.c_int), ("is_lossless", ctypes.c_int), ("is_animated", ctypes.c_int),
@@ -109,6 +119,10 @@ SIGNATURES = [
     ("zw_frame_free", None, [ctypes.POINTER(_Frame)]),
     ("zw_encode_frame_lossy", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_encode_webp", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_webp_ex", _I, [_VP, _VP, _SZ, _U32, _U32, _I, ctypes.POINTER(_EncParams), ctypes.POINTER(_Metadata),
+                               ctypes.POINTER(_Bytes)]),
+    ("zw_encode_frame_lossless", _I, [_VP, _SZ, _U32, _U32, _I, _I, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_alpha", _I, [_VP, _SZ, _U32, _U32, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
@@ -254,48 +268,89 @@ def encode_batch(images, width, height, color, quality=75, method=4, ctx=None):
 
 
 class EncoderParams:
-    """EncoderParams (encoder/api.rs:430-460); only the lossy variant is on this path."""
+    """EncoderParams (encoder/api.rs:415-458).  The default is lossless (VP8L),
+    quality 95, method 4, predictor transform on, as in the reference."""
 
-    def __init__(self, quality=75, method=4, lossless=False):
-        self.quality = quality
+    def __init__(self, use_predictor_transform=True, use_lossy=False, lossy_quality=95, method=4):
+        self.use_predictor_transform = use_predictor_transform
+        self.use_lossy = use_lossy
+        self.lossy_quality = lossy_quality
         self.method = method
-        self.lossless = lossless
 
     @classmethod
     def lossy(cls, quality, method=4):
-        return cls(quality, method, False)
+        return cls(True, True, quality, method)
 
     @classmethod
     def lossless(cls):
-        return cls(100, 4, True)
+        return cls()
 
     @classmethod
     def default(cls):
         return cls()
 
+    def _c(self):
+        return _EncParams(int(self.use_lossy), self.lossy_quality, self.method, int(self.use_predictor_transform))
+
 
 class WebPEncoder:
-    """WebPEncoder (encoder/api.rs:1244-1398) writing to a bytearray-like sink."""
+    """WebPEncoder (encoder/api.rs:1244-1398) writing to a bytearray-like sink:
+    new / set_params / set_icc_profile / set_exif_metadata / set_xmp_metadata / encode."""
 
     def __init__(self, writer=None, ctx=None):
         self.writer = writer if writer is not None else bytearray()
         self.params = EncoderParams.default()
         self.ctx = ctx
+        self.icc = self.exif = self.xmp = b""
 
     def set_params(self, params):
         self.params = params
 
+    def set_icc_profile(self, icc):
+        self.icc = bytes(icc)
+
+    def set_exif_metadata(self, exif):
+        self.exif = bytes(exif)
+
+    def set_xmp_metadata(self, xmp):
+        self.xmp = bytes(xmp)
+
     def encode(self, data, width, height, color):
-        if self.params.lossless:
-            raise EncodingError(5, "lossless (VP8L) encoding is outside the accelerated path")
-        c = _ctx(self.ctx)
-        L = c._lib
+        # lossless encodes are host entropy coding and need no device
+        c = _ctx(self.ctx) if self.params.use_lossy else None
+        L = c._lib if c is not None else load_library()
         a = _as_u8(data)
+        bufs = [np.frombuffer(m, np.uint8) if m else None for m in (self.icc, self.exif, self.xmp)]
+        md = _Metadata(*[x for b in bufs for x in ((b.ctypes.data if b is not None else None),
+                                                   (b.size if b is not None else 0))])
         out = _Bytes()
-        _check(L.zw_encode_webp(c.handle, _ptr(a), a.size, width, height, color, self.params.quality,
-                                self.params.method, ctypes.byref(out)), "WebPEncoder.encode", EncodingError)
+        prm = self.params._c()
+        _check(L.zw_encode_webp_ex(c.handle if c is not None else None, _ptr(a) if a.size else None, a.size, width,
+                                   height, color, ctypes.byref(prm), ctypes.byref(md), ctypes.byref(out)),
+               "WebPEncoder.encode", EncodingError)
         self.writer += _take_bytes(L, out)
         return self.writer
+
+
+def encode_frame_lossless(data, width, height, color, use_predictor_transform=True):
+    """encode_frame_lossless (encoder/api.rs:945): the VP8L bitstream (host coder, no device)."""
+    L = load_library()
+    a = _as_u8(data)
+    out = _Bytes()
+    _check(L.zw_encode_frame_lossless(_ptr(a) if a.size else None, a.size, width, height, color,
+                                      int(use_predictor_transform), ctypes.byref(out)), "encode_frame_lossless",
+           EncodingError)
+    return _take_bytes(L, out)
+
+
+def encode_alpha(data, width, height, color):
+    """encode_alpha_lossless (encoder/api.rs:1175): the ALPH chunk payload (host coder, no device)."""
+    L = load_library()
+    a = _as_u8(data)
+    out = _Bytes()
+    _check(L.zw_encode_alpha(_ptr(a) if a.size else None, a.size, width, height, color, ctypes.byref(out)),
+           "encode_alpha_lossless", EncodingError)
+    return _take_bytes(L, out)
 
 
 class Frame:

@@ -6,8 +6,11 @@
  *
  *   zw_encode_frame_lossy   encode_frame_lossy        src/encoder/vp8.rs:3132-3153
  *   zw_encode_webp          WebPEncoder::encode       src/encoder/api.rs:1291-1398
- *                           (simple RIFF container; alpha inputs -> ZW_EUNSUPPORTED,
- *                            the ALPH/VP8L lossless encoder is out of scope)
+ *                           (EncoderParams::lossy(q, m); RGBA / LA inputs get VP8X + ALPH)
+ *   zw_encode_webp_ex       WebPEncoder::{set_params, set_icc_profile, set_exif_metadata,
+ *                           set_xmp_metadata, encode}  src/encoder/api.rs:1244-1398
+ *   zw_encode_frame_lossless  encode_frame_lossless  src/encoder/api.rs:945-1173
+ *   zw_encode_alpha         encode_alpha_lossless     src/encoder/api.rs:1175-1222
  *   zw_encode_batch         many independent encode_frame_lossy calls (new: batch)
  *   zw_vp8_decode_frame     Vp8Decoder::decode_frame  src/decoder/vp8.rs:1526
  *   zw_vp8_decode_rgb       decode_frame + Frame::fill_rgb/fill_rgba  src/decoder/vp8.rs:200-258
@@ -102,13 +105,43 @@ const char *zw_strerror(int code);
 void zw_bytes_free(zw_bytes *b);
 void zw_frame_free(zw_frame *f);
 
+/* EncoderParams (encoder/api.rs:415-458).  Default: lossless, quality 95,
+ * method 4, predictor transform on. */
+typedef struct {
+    int use_lossy;
+    uint8_t lossy_quality, method;
+    int use_predictor_transform;
+} zw_encoder_params;
+
+/* WebPEncoder metadata (set_icc_profile / set_exif_metadata / set_xmp_metadata,
+ * encoder/api.rs:1262-1287); empty = absent. */
+typedef struct {
+    const uint8_t *icc;
+    size_t icc_len;
+    const uint8_t *exif;
+    size_t exif_len;
+    const uint8_t *xmp;
+    size_t xmp_len;
+} zw_metadata;
+
 /* encode_frame_lossy: raw VP8 frame bytes ("VP8 " chunk payload). */
 int zw_encode_frame_lossy(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
                           int color, uint8_t quality, uint8_t method, zw_bytes *out);
 
-/* WebPEncoder::encode with EncoderParams::lossy(quality, method): RIFF container. */
+/* WebPEncoder::encode with EncoderParams::lossy(quality, method): RIFF container
+ * ("VP8 " simple form; VP8X + ALPH + "VP8 " for LA8 / RGBA8 inputs). */
 int zw_encode_webp(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
                    uint8_t quality, uint8_t method, zw_bytes *out);
+/* WebPEncoder::encode with any EncoderParams and metadata (params / meta may be
+ * NULL: defaults / none).  Lossless encodes need no device (ctx may be NULL). */
+int zw_encode_webp_ex(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
+                      const zw_encoder_params *params, const zw_metadata *meta, zw_bytes *out);
+/* encode_frame_lossless (VP8L bitstream incl. its 5-byte header, the "VP8L"
+ * chunk payload).  Host entropy coder (like the VP8 bool coder): no device. */
+int zw_encode_frame_lossless(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
+                             int use_predictor_transform, zw_bytes *out);
+/* encode_alpha_lossless: the ALPH chunk payload of an LA8 / RGBA8 image.  Host. */
+int zw_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, zw_bytes *out);
 
 /* n independent frames of identical size/color; outs[i] receives frame i. */
 int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method, zw_bytes *outs);

@@ -94,6 +94,12 @@ void or_iwht_c(int32_t *blk, int n);
 void or_loop_filter_c(uint8_t *y, uint8_t *u, uint8_t *v, int mbw, int mbh, const or_mb_info *mbs,
                       const or_frame_hdr *hdr);
 void or_yuv_to_rgb_fancy_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
+/* encode_frame_lossless (encoder/api.rs:945-1173) and encode_alpha_lossless
+ * (:1175-1222); *out is malloc'd (free with or_free). */
+int or_encode_frame_lossless(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
+                             int use_predictor, int implicit_dims, uint8_t **out, size_t *out_len);
+int or_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, uint8_t **out,
+                    size_t *out_len);
 void or_yuv_to_rgb_simple_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
 void or_analyze(const uint8_t *Y, const uint8_t *U, const uint8_t *V, int width, int height,
                 uint8_t *mb_alphas, uint32_t histo[256]);

@@ -207,6 +207,36 @@ def yuv_to_rgb_simple(y, u, v, w, h, bpp=3):
     return out
 
 
+def _bytes_out(fn, *args):
+    L = lib()
+    out, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = fn(*args, ctypes.byref(out), ctypes.byref(n))
+    data = ctypes.string_at(out.value, n.value) if rc == 0 and out.value else b""
+    if out.value:
+        L.or_free(out)
+    return rc, data
+
+
+def encode_lossless(img, w, h, color, use_predictor=True, implicit_dims=False):
+    """encode_frame_lossless (encoder/api.rs:945): (rc, VP8L bitstream bytes)."""
+    L = lib()
+    L.or_encode_frame_lossless.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+    a = np.ascontiguousarray(img, dtype=np.uint8).reshape(-1)
+    return _bytes_out(L.or_encode_frame_lossless, _p(a) if a.size else None, a.size, w, h, color,
+                      int(use_predictor), int(implicit_dims))
+
+
+def encode_alpha(img, w, h, color):
+    """encode_alpha_lossless (encoder/api.rs:1175): (rc, ALPH chunk payload)."""
+    L = lib()
+    L.or_encode_alpha.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p]
+    a = np.ascontiguousarray(img, dtype=np.uint8).reshape(-1)
+    return _bytes_out(L.or_encode_alpha, _p(a) if a.size else None, a.size, w, h, color)
+
+
 def riff_vp8_chunk(data):
     """Extract the 'VP8 ' chunk payload from a RIFF WebP file."""
     assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"

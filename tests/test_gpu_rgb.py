@@ -150,3 +150,37 @@ def test_decode_rgb_errors(ctx):
     with pytest.raises(zwebp.DecodingError) as e:
         zwebp.decode_rgb(b"RIFF\0\0\0\0WEBQ", ctx=ctx)
     assert e.value.code == 19
+
+
+# --------------------------------------------------------------------------
+# WebPEncoder::encode, lossy with alpha (encoder/api.rs:1291-1398):
+# VP8X + ALPH (encode_alpha_lossless) + "VP8 " (the GPU encoder)
+# --------------------------------------------------------------------------
+def _chunk(tag, payload):
+    return tag + struct.pack("<I", len(payload)) + payload + (b"\0" if len(payload) & 1 else b"")
+
+
+def _riff_chunks(*chunks):
+    body = b"WEBP" + b"".join(chunks)
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+@pytest.mark.parametrize("w,h,color", [(96, 80, 3), (33, 17, 3), (64, 48, 1)])
+def test_webp_encoder_lossy_with_alpha(ctx, w, h, color):
+    rgba = synth_rgba(w, h, 0x5EED0100 + w, "natural").copy()
+    rgba[..., 3] = (np.arange(w)[None, :] * 4 + np.arange(h)[:, None]) % 256  # non-trivial alpha
+    img = rgba if color == 3 else np.ascontiguousarray(rgba[..., [1, 3]])
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    enc.set_exif_metadata(b"exif")
+    riff = bytes(enc.encode(img, w, h, color))
+    rc, vp8, _ = O.encode(img, w, h, color, 75, 4)
+    rc2, alph = O.encode_alpha(img, w, h, color)
+    assert rc == 0 and rc2 == 0
+    vp8x = bytes([0x18, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little")
+    assert riff == _riff_chunks(_chunk(b"VP8X", vp8x), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8),
+                                _chunk(b"EXIF", b"exif"))
+    # the decoder side reads the container (ALPH decoding is outside the lossy path)
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.decode_rgba(riff, ctx=ctx)
+    assert e.value.code == 5

@@ -1,0 +1,173 @@
+"""The lossless side of the container: encode_frame_lossless
+(encoder/api.rs:945-1173, the VP8L coder behind EncoderParams::lossless) and
+encode_alpha_lossless (:1175-1222, the ALPH chunk of every RGBA / LA lossy
+encode).  CPU tests: the oracle restatement round-trips through the system
+libwebp decoder exactly as the reference's own roundtrip_libwebp tests do
+(api.rs tests: random 256x256 images, every color type, predictor on and off),
+and the product's host coder (libzwebp.so, no device needed) is byte-identical
+to the oracle."""
+import ctypes
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from zwebp.synth import synth_rgba
+
+try:
+    _W = ctypes.CDLL("libwebp.so.7")
+    _W.WebPDecodeRGBA.restype = ctypes.c_void_p
+    _W.WebPDecodeRGBA.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    _W.WebPFree.argtypes = [ctypes.c_void_p]
+except OSError:  # pragma: no cover - the GPU box image may lack it
+    _W = None
+
+BPP = {0: 1, 1: 2, 2: 3, 3: 4}
+
+
+def _chunk(tag, payload):
+    return tag + struct.pack("<I", len(payload)) + payload + (b"\0" if len(payload) & 1 else b"")
+
+
+def _riff(*chunks):
+    body = b"WEBP" + b"".join(chunks)
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def _libwebp_rgba(riff):
+    w, h = ctypes.c_int(), ctypes.c_int()
+    p = _W.WebPDecodeRGBA(riff, len(riff), ctypes.byref(w), ctypes.byref(h))
+    assert p, "libwebp refused the stream"
+    out = np.ctypeslib.as_array((ctypes.c_uint8 * (w.value * h.value * 4)).from_address(p)).copy()
+    _W.WebPFree(p)
+    return out.reshape(h.value, w.value, 4)
+
+
+def _to_rgba(img, color):
+    a = img.reshape(-1, BPP[color])
+    if color == 0:
+        return np.stack([a[:, 0], a[:, 0], a[:, 0], np.full(len(a), 255, np.uint8)], 1)
+    if color == 1:
+        return np.stack([a[:, 0], a[:, 0], a[:, 0], a[:, 1]], 1)
+    if color == 2:
+        return np.concatenate([a, np.full((len(a), 1), 255, np.uint8)], 1)
+    return a
+
+
+def _images():
+    rng = np.random.default_rng(7)
+    yield "random256", 256, 256, rng.integers(0, 256, (256, 256, 4), dtype=np.uint8)
+    yield "natural333x211", 333, 211, synth_rgba(333, 211, 0x5EED0001, "natural")
+    yield "flat17x9", 17, 9, np.full((9, 17, 4), 77, np.uint8)
+    yield "runs", 300, 40, np.repeat(rng.integers(0, 3, (40, 300 // 50, 4), dtype=np.uint8) * 100, 50, axis=1)
+    yield "tiny1x1", 1, 1, np.array([[[1, 2, 3, 4]]], np.uint8)
+    # skewed histogram: deep Huffman trees (length limiting at 15)
+    fib = np.concatenate([np.full(int(1.6 ** k), k, np.uint8) for k in range(24)])
+    n = 512 * 64
+    g = np.resize(fib, n)
+    rng.shuffle(g)
+    sk = np.stack([g, g, g, g], 1).reshape(64, 512, 4)
+    yield "skewed512x64", 512, 64, sk
+
+
+IMAGES = list(_images())
+
+
+@pytest.mark.skipif(_W is None, reason="system libwebp not available")
+@pytest.mark.parametrize("name,w,h,img", IMAGES, ids=[i[0] for i in IMAGES])
+@pytest.mark.parametrize("color", [0, 1, 2, 3])
+@pytest.mark.parametrize("pred", [True, False])
+def test_oracle_lossless_roundtrip_libwebp(name, w, h, img, color, pred):
+    src = np.ascontiguousarray(img[..., :BPP[color]]) if color >= 2 else \
+        np.ascontiguousarray(img[..., [1, 3]][..., :BPP[color]])
+    rc, vp8l = O.encode_lossless(src, w, h, color, pred)
+    assert rc == 0 and vp8l[0] == 0x2F
+    dec = _libwebp_rgba(_riff(_chunk(b"VP8L", vp8l)))
+    assert np.array_equal(dec.reshape(-1, 4), _to_rgba(src, color))
+
+
+@pytest.mark.skipif(_W is None, reason="system libwebp not available")
+@pytest.mark.parametrize("name,w,h,img", IMAGES[:4], ids=[i[0] for i in IMAGES[:4]])
+def test_oracle_alpha_chunk_roundtrip_libwebp(name, w, h, img):
+    """VP8X + ALPH + VP8: libwebp recovers the alpha plane exactly."""
+    rgba = np.ascontiguousarray(img)
+    rc, alph = O.encode_alpha(rgba, w, h, 3)
+    assert rc == 0 and alph[0] == 1
+    rc, vp8, _ = O.encode(rgba, w, h, 3, 75, 4)
+    assert rc == 0
+    vp8x = bytes([0x10, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little")
+    dec = _libwebp_rgba(_riff(_chunk(b"VP8X", vp8x), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8)))
+    assert np.array_equal(dec[..., 3], rgba[..., 3])
+
+
+def test_oracle_lossless_errors():
+    img = np.zeros((4, 4, 4), np.uint8)
+    assert O.encode_lossless(img, 4, 4, 3)[0] == 0
+    assert O.encode_lossless(img, 4, 5, 3)[0] == 2          # length mismatch (the reference asserts)
+    assert O.encode_lossless(np.zeros(0, np.uint8), 0, 4, 3)[0] != 0
+    big = np.zeros(16385 * 4, np.uint8)
+    assert O.encode_lossless(big, 16385, 1, 3)[0] == 1      # InvalidDimensions
+
+
+# --------------------------------------------------------------------------
+# the product's host coder (libzwebp.so; no device needed) == the oracle
+# --------------------------------------------------------------------------
+import zwebp  # noqa: E402
+
+
+def _src(img, color):
+    return np.ascontiguousarray(img[..., :BPP[color]]) if color >= 2 else \
+        np.ascontiguousarray(img[..., [1, 3]][..., :BPP[color]])
+
+
+@pytest.mark.parametrize("name,w,h,img", IMAGES, ids=[i[0] for i in IMAGES])
+@pytest.mark.parametrize("color", [0, 1, 2, 3])
+@pytest.mark.parametrize("pred", [True, False])
+def test_product_lossless_matches_oracle(name, w, h, img, color, pred):
+    src = _src(img, color)
+    rc, ref = O.encode_lossless(src, w, h, color, pred)
+    assert rc == 0
+    assert zwebp.encode_frame_lossless(src, w, h, color, pred) == ref
+
+
+@pytest.mark.parametrize("name,w,h,img", IMAGES, ids=[i[0] for i in IMAGES])
+@pytest.mark.parametrize("color", [1, 3])
+def test_product_alpha_matches_oracle(name, w, h, img, color):
+    src = _src(img, color)
+    rc, ref = O.encode_alpha(src, w, h, color)
+    assert rc == 0
+    assert zwebp.encode_alpha(src, w, h, color) == ref
+
+
+def test_product_lossless_container():
+    """WebPEncoder with default (lossless) params: simple VP8L container, and VP8X
+    with ICCP / EXIF / XMP chunks in the reference's order and flags."""
+    w, h = 64, 48
+    img = synth_rgba(w, h, 0x5EED0007, "natural")
+    rc, vp8l = O.encode_lossless(img, w, h, 3, True)
+    enc = zwebp.WebPEncoder()
+    riff = bytes(enc.encode(img, w, h, zwebp.ColorType.Rgba8))
+    assert riff == _riff(_chunk(b"VP8L", vp8l))
+    enc = zwebp.WebPEncoder()
+    enc.set_icc_profile(b"icc-profile")
+    enc.set_exif_metadata(b"exif!")
+    enc.set_xmp_metadata(b"<xmp/>")
+    riff = bytes(enc.encode(img, w, h, zwebp.ColorType.Rgba8))
+    vp8x = bytes([0x3C, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little")
+    assert riff == _riff(_chunk(b"VP8X", vp8x), _chunk(b"ICCP", b"icc-profile"), _chunk(b"VP8L", vp8l),
+                         _chunk(b"EXIF", b"exif!"), _chunk(b"XMP ", b"<xmp/>"))
+    if _W is not None:
+        assert np.array_equal(_libwebp_rgba(riff), img)
+
+
+def test_product_lossless_errors():
+    img = np.zeros((4, 4, 4), np.uint8)
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossless(img, 4, 5, 3)
+    assert e.value.code == 2
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossless(np.zeros(16385 * 4, np.uint8), 16385, 1, 3)
+    assert e.value.code == 1
+    with pytest.raises(zwebp.EncodingError):
+        zwebp.encode_alpha(img, 4, 4, 2)  # no alpha channel
