@@ -65,6 +65,17 @@ struct ZwMbOut {
 // decoder/vp8.rs:681-734 modes, :1060-1168 residual tokens).  Levels stay
 // quantised; the device dequantises, runs the iWHT and picks full / DC-only
 // iDCT per block from nz_mask and the DC value.
+// Packed decode record (what crosses PCIe): 16-byte aligned, per MB
+//   [0] luma_mode | chroma_mode << 3 | skip << 5   [1] segment   [2..3] pad
+//   [4..7] nz_mask   [8..15] bpred, 4 bits each
+//   [16..67] start[26] (u16): block b's levels are entries start[b] ..
+//            start[b+1]-1 of the level array (its zigzag prefix up to the last
+//            nonzero); blocks 0..23, then 24 = Y2   [68..79] pad
+//   [80..] int16 levels, zigzag order; pad to 16.
+// The device expands it into a ZwDecMb in LDS.
+#define ZW_DREC_HDR 80
+#define ZW_DREC_MAX (ZW_DREC_HDR + 25 * 16 * 2)  // 880 B = 55 lines
+
 struct ZwDecMb {
     uint8_t luma_mode, chroma_mode, segment, skip;
     uint8_t bpred[16];

@@ -9,6 +9,7 @@
 //   device: k_dec_recon (dequant, iWHT, iDCT, prediction) and k_loopfilter.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -18,6 +19,8 @@
 #include "zw_host_internal.h"
 
 extern "C" {
+hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
+                          ZwDecMb* mbs, int nmb, int nframes);
 hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
                          uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
@@ -241,10 +244,43 @@ static int parse_header(DecFrame& F, const uint8_t* data, size_t len)
     return ZW_OK;
 }
 
-// read_coefficients decoder/vp8.rs:872-1058: levels (not dequantised) into blk
-// at natural positions.  Returns -1 on eof, else whether the run was non-empty.
-static int read_levels(BitReader& r, const uint8_t P[8][3][11], int16_t* blk, int first, int ctx)
+// Packed-record builder for one MB (zw_common.h ZW_DREC_*).
+struct PackedMb {
+    uint8_t hdr[ZW_DREC_HDR];
+    int16_t lv[25 * 16];
+    int nlv;
+    uint16_t* start() { return (uint16_t*)(hdr + 16); }
+    void reset()
+    {
+        memset(hdr, 0, sizeof hdr);
+        nlv = 0;
+    }
+    // the next block's levels: zigzag prefix zz[0..eob)
+    void add_block(int b, const int16_t* zz, int eob)
+    {
+        start()[b] = (uint16_t)nlv;
+        memcpy(lv + nlv, zz, (size_t)eob * 2);
+        nlv += eob;
+        start()[b + 1] = (uint16_t)nlv;
+    }
+    // writes the record at out; returns its padded size (<= ZW_DREC_MAX)
+    size_t emit(uint8_t* out)
+    {
+        const size_t bytes = ZW_DREC_HDR + (size_t)nlv * 2, padded = (bytes + 15) & ~(size_t)15;
+        memcpy(out, hdr, ZW_DREC_HDR);
+        memcpy(out + ZW_DREC_HDR, lv, (size_t)nlv * 2);
+        memset(out + bytes, 0, padded - bytes);
+        return padded;
+    }
+};
+
+// read_coefficients decoder/vp8.rs:872-1058: levels (not dequantised) in
+// zigzag order into zz[16] (zeroed here); *eob = last nonzero position + 1.
+// Returns -1 on eof, else whether the run was non-empty.
+static int read_levels_zz(BitReader& r, const uint8_t P[8][3][11], int16_t* zz, int first, int ctx, int* eob)
 {
+    memset(zz, 0, 32);
+    *eob = 0;
     int n = first;
     const uint8_t* p = P[COEFF_BANDS[n]][ctx];
     while (n < 16) {
@@ -279,26 +315,32 @@ static int read_levels(BitReader& r, const uint8_t P[8][3][11], int16_t* blk, in
             }
             nctx = 2;
         }
-        blk[ZIGZAG[n]] = (int16_t)(r.bit(128) ? -v : v);
+        zz[n] = (int16_t)(r.bit(128) ? -v : v);
         n++;
+        *eob = n;
         if (n < 16) p = P[COEFF_BANDS[n]][nctx];
     }
     if (r.eof) return -1;
     return n > first;
 }
 
-// MB headers + tokens for the whole frame (decoder/vp8.rs:681-734, :1060-1168).
-static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
+// MB headers + tokens for the whole frame (decoder/vp8.rs:681-734, :1060-1168),
+// as packed records in raster order into recs (room for nmb * ZW_DREC_MAX
+// bytes); moff[i] = byte offset of MB i's record (moff[nmb] = total).
+static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
 {
+    size_t used = 0;
     const int mbw = F.mbw, mbh = F.mbh;
     std::vector<uint8_t> top_cx((size_t)mbw * 9, 0), top_bp((size_t)mbw * 4, 0);
     BitReader& b = F.hdr;
+    PackedMb M;
+    int16_t zz[16];
     for (int mby = 0; mby < mbh; mby++) {
         BitReader& pr = F.part[mby % F.nparts];
         uint8_t left_cx[9] = {0}, left_bp[4] = {0};
         for (int mbx = 0; mbx < mbw; mbx++) {
-            ZwDecMb& M = mbs[(size_t)mby * mbw + mbx];
-            memset(&M, 0, sizeof M);
+            moff[(size_t)mby * mbw + mbx] = (uint32_t)used;
+            M.reset();
             uint8_t* tcx = &top_cx[(size_t)mbx * 9];
             uint8_t* tbp = &top_bp[(size_t)mbx * 4];
             int seg = 0;
@@ -309,7 +351,7 @@ static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
                 for (int y = 0; y < 4; y++)
                     for (int x = 0; x < 4; x++) {
                         const int m = b.tree(BMODE_TREE, KEYFRAME_BPRED_MODE_PROBS[tbp[x]][left_bp[y]]);
-                        M.bpred[x + y * 4] = (uint8_t)m;
+                        M.hdr[8 + ((x + y * 4) >> 1)] |= (uint8_t)(m << (4 * ((x + y * 4) & 1)));
                         tbp[x] = (uint8_t)m;
                         left_bp[y] = (uint8_t)m;
                     }
@@ -319,19 +361,20 @@ static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
             }
             const int cm = b.tree(UVMODE_TREE, KEYFRAME_UV_MODE_PROBS);
             if (b.eof) return ZW_EBITSTREAM;
-            M.luma_mode = (uint8_t)lm;
-            M.chroma_mode = (uint8_t)cm;
-            M.segment = (uint8_t)seg;
-            M.skip = (uint8_t)skip;
+            M.hdr[0] = (uint8_t)(lm | (cm << 3) | (skip << 5));
+            M.hdr[1] = (uint8_t)seg;
             if (skip) {
                 if (lm != 4) left_cx[0] = tcx[0] = 0;
                 for (int i = 1; i < 9; i++) left_cx[i] = tcx[i] = 0;
+                used += M.emit(recs + used);
                 continue;
             }
             uint32_t nzm = 0;
-            int first = 0;
+            int first = 0, eob;
+            int16_t y2zz[16];
+            int y2eob = 0;
             if (lm != 4) {
-                const int nz = read_levels(pr, F.probs[1], M.y2, 0, tcx[0] + left_cx[0]);
+                const int nz = read_levels_zz(pr, F.probs[1], y2zz, 0, tcx[0] + left_cx[0], &y2eob);
                 if (nz < 0) return ZW_EBITSTREAM;
                 left_cx[0] = tcx[0] = (uint8_t)nz;
                 first = 1;
@@ -341,8 +384,9 @@ static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
                 int left = left_cx[y + 1];
                 for (int x = 0; x < 4; x++) {
                     const int i = x + y * 4;
-                    const int nz = read_levels(pr, F.probs[plane], M.coeffs[i], first, tcx[x + 1] + left);
+                    const int nz = read_levels_zz(pr, F.probs[plane], zz, first, tcx[x + 1] + left, &eob);
                     if (nz < 0) return ZW_EBITSTREAM;
+                    M.add_block(i, zz, eob);
                     nzm |= (uint32_t)nz << i;
                     left = nz;
                     tcx[x + 1] = (uint8_t)nz;
@@ -354,8 +398,9 @@ static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
                     int left = left_cx[y + j];
                     for (int x = 0; x < 2; x++) {
                         const int i = x + y * 2 + (j == 5 ? 16 : 20);
-                        const int nz = read_levels(pr, F.probs[2], M.coeffs[i], 0, tcx[x + j] + left);
+                        const int nz = read_levels_zz(pr, F.probs[2], zz, 0, tcx[x + j] + left, &eob);
                         if (nz < 0) return ZW_EBITSTREAM;
+                        M.add_block(i, zz, eob);
                         nzm |= (uint32_t)nz << i;
                         left = nz;
                         tcx[x + j] = (uint8_t)nz;
@@ -363,9 +408,12 @@ static int parse_mbs(DecFrame& F, ZwDecMb* mbs)
                     left_cx[y + j] = (uint8_t)left;
                 }
             }
-            M.nz_mask = nzm;
+            M.add_block(24, y2zz, y2eob);
+            memcpy(M.hdr + 4, &nzm, 4);
+            used += M.emit(recs + used);
         }
     }
+    moff[(size_t)mbw * mbh] = (uint32_t)used;
     return ZW_OK;
 }
 
@@ -430,9 +478,16 @@ struct DecBatch {
 // k_loopfilter.  Leaves the filtered planes in device scratch (plus
 // `extra_bytes` of scratch at B.o_extra for the caller) with the kernel
 // stream's work queued; dev_ev[2] marks the end of the loop filter.
+static double dec_now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool dec_timing() { static const bool on = getenv("ZW_DEC_TIMING") != nullptr; return on; }
+
 static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
                             size_t extra_bytes, DecBatch& B)
 {
+    const double t0 = dec_now_ms();
     B.F.assign(n, DecFrame());
     std::vector<DecFrame>& F = B.F;
     std::vector<int> rc(n, ZW_OK);
@@ -445,15 +500,20 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     if (mbw == 0 || mbh == 0) return ZW_EINVALID_DIMENSIONS;
     const size_t nmb = (size_t)mbw * mbh;
     const size_t ysz = nmb * 256, csz = nmb * 64;
-    // MB records land in pinned memory (parse_mbs writes every record; no
-    // value-initialisation of the whole batch) for a DMA upload
-    const size_t rec_bytes = (size_t)n * nmb * sizeof(ZwDecMb);
-    ZwDecMb* mbs = (ZwDecMb*)ctx_pinned(ctx, 0, rec_bytes);
-    if (!mbs) return ZW_ENOMEM;
+    // packed MB records (zw_common.h ZW_DREC_*) straight into pinned staging,
+    // one worst-case slot per frame (only the used prefix crosses PCIe); the MB
+    // offsets and frame bases follow the slots
+    const size_t slot = al256(nmb * ZW_DREC_MAX);
+    const size_t off_bytes = (size_t)n * (nmb + 1) * 4, base_bytes = (size_t)n * 8;
+    const size_t o_moff = (size_t)n * slot, o_base = o_moff + al256(off_bytes);
+    const size_t up_bytes = o_base + base_bytes;
+    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, 0, up_bytes);
+    if (!stage) return ZW_ENOMEM;
+    uint32_t* moff = (uint32_t*)(stage + o_moff);
     std::vector<DecQuant> quant((size_t)n * 4);
     std::vector<ZwFilterParams> fps(n);
     parallel_for(n, [&](int i) {
-        rc[i] = parse_mbs(F[i], &mbs[(size_t)i * nmb]);
+        rc[i] = parse_mbs(F[i], stage + (size_t)i * slot, moff + (size_t)i * (nmb + 1));
         for (int s = 0; s < 4; s++) quant[(size_t)i * 4 + s] = F[i].q[s];
         filter_table(fps[i], F[i].filter_type, F[i].filter_level, F[i].sharpness, F[i].segments_enabled,
                      F[i].seg_delta_values, F[i].seg_lf, F[i].lf_adj_enabled, F[i].ref_delta0, F[i].mode_delta0, mbw,
@@ -461,11 +521,19 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     });
     for (int i = 0; i < n; i++)
         if (rc[i] != ZW_OK) return rc[i];
+    uint64_t* fbase = (uint64_t*)(stage + o_base);
+    size_t rec_bytes = 0;
+    for (int i = 0; i < n; i++) {
+        fbase[i] = (uint64_t)i * slot;
+        rec_bytes += moff[(size_t)i * (nmb + 1) + nmb];
+    }
+    const double t1 = dec_now_ms();
 
     HIPOK(hipSetDevice(ctx->device));
-    const size_t o_mbs = 0, o_q = al256(o_mbs + rec_bytes);
+    const size_t o_mbs = 0, o_q = al256(o_mbs + up_bytes);
     const size_t o_fp = al256(o_q + quant.size() * sizeof(DecQuant));
-    const size_t o_fl = al256(o_fp + fps.size() * sizeof(ZwFilterParams));
+    const size_t o_full = al256(o_fp + fps.size() * sizeof(ZwFilterParams));  // expanded ZwDecMb records
+    const size_t o_fl = al256(o_full + (size_t)n * nmb * sizeof(ZwDecMb));
     const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
     const size_t o_u = al256(o_y + (size_t)n * ysz), o_v = al256(o_u + (size_t)n * csz);
     const size_t o_extra = al256(o_v + (size_t)n * csz);
@@ -473,17 +541,27 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
     hipStream_t s = ctx_stream(ctx);
-    HIPOK(hipMemcpyAsync(d + o_mbs, mbs, rec_bytes, hipMemcpyHostToDevice, s));
+    for (int i = 0; i < n; i++)  // each frame's used prefix
+        HIPOK(hipMemcpyAsync(d + o_mbs + (size_t)i * slot, stage + (size_t)i * slot, moff[(size_t)i * (nmb + 1) + nmb],
+                             hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_mbs + o_moff, stage + o_moff, up_bytes - o_moff, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
     for (int e = 0; e < 4; e++)
         if (!ctx->dev_ev[e]) HIPOK(hipEventCreate(&ctx->dev_ev[e]));
     HIPOK(hipEventRecord(ctx->dev_ev[0], s));
-    HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_mbs), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
+    HIPOK(zwk_dec_expand(s, d + o_mbs, (const uint32_t*)(d + o_mbs + o_moff), (const uint64_t*)(d + o_mbs + o_base),
+                         (ZwDecMb*)(d + o_full), (int)nmb, n));
+    HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
                         csz, n));
     HIPOK(hipEventRecord(ctx->dev_ev[1], s));
     HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
     HIPOK(hipEventRecord(ctx->dev_ev[2], s));
+    if (dec_timing()) {
+        HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
+        fprintf(stderr, "[dec] n=%d parse %.2f ms, upload+kernels %.2f ms (records %.1f MB)\n", n, t1 - t0,
+                dec_now_ms() - t1, rec_bytes / 1e6);
+    }
     B.d = d;
     B.o_y = o_y;
     B.o_u = o_u;
@@ -511,6 +589,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
     uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fsz);
     if (!hout) return ZW_ENOMEM;
     HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
+    const double td = dec_now_ms();
     {
         int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)n * ysz);
         if (!r) r = ctx_d2h(ctx, hout + (size_t)n * ysz, d + B.o_u, (size_t)n * csz);
@@ -529,6 +608,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         memcpy(buf + ysz + csz, hout + (size_t)n * (ysz + csz) + (size_t)i * csz, csz);
         outs[i].y = buf;
     });
+    if (dec_timing()) fprintf(stderr, "[dec] download+fanout %.2f ms\n", dec_now_ms() - td);
     for (int i = 0; i < n; i++) {
         if (oom[i]) {
             for (int k = 0; k < n; k++) zw_frame_free(&outs[k]);

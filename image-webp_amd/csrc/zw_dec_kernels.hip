@@ -510,6 +510,64 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
     return off;
 }
 
+// k_dec_expand: packed MB records (what crossed PCIe, zw_common.h ZW_DREC_*)
+// -> full ZwDecMb records for k_dec_recon.  One wave per MB, fully parallel
+// over the batch: the wavefront kernel keeps its one-MB-ahead prefetch of
+// fixed-size records.  Slot sl = block (sl >> 4, 24 = Y2) x zigzag position.
+extern "C" __global__ __launch_bounds__(256) void k_dec_expand(const uint8_t* __restrict__ recs,
+                                                                 const uint32_t* __restrict__ moff,
+                                                                 const uint64_t* __restrict__ fbase, ZwDecMb* mbs,
+                                                                 int nmb)
+{
+    __shared__ uint4 raw[4][55];
+    const int f = blockIdx.y, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wv;
+    if (i >= nmb) return;
+    const uint32_t* fo = moff + (size_t)f * (nmb + 1);
+    const uint32_t a = fo[i], e = fo[i + 1];
+    if (a + 16u * (uint32_t)lane < e && lane < 55) raw[wv][lane] = *(const uint4*)(recs + fbase[f] + a + 16u * lane);
+    wsync();
+    const uint8_t* rb = (const uint8_t*)raw[wv];
+    const uint16_t* st = (const uint16_t*)(rb + 16);
+    const int16_t* lv = (const int16_t*)(rb + ZW_DREC_HDR);
+    // the 832-byte record as 52 16-byte lines: lane l < 52 assembles line l
+    // from 8 halfwords (line 0: header bytes and bpred, line 1..: y2/coeffs)
+    uint4* out = (uint4*)(mbs + (size_t)f * nmb + i);
+    if (lane < 52) {
+        uint16_t h[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int byte = lane * 16 + q * 2;  // offset in ZwDecMb
+            int v = 0;
+            if (byte >= 24 && byte < 824) {  // y2[16] at 24, coeffs[24][16] at 56
+                const int c = (byte - 24) >> 1, b = c < 16 ? 24 : (c - 16) >> 4, nat = c & 15;
+                const int k = izz_of(nat), s0 = st[b], s1 = st[b + 1];
+                v = s0 + k < s1 ? (int)(uint16_t)lv[s0 + k] : 0;
+            } else if (byte < 24) {
+                auto hb = [&](int o) -> int {
+                    if (o == 0) return rb[0] & 7;
+                    if (o == 1) return (rb[0] >> 3) & 3;
+                    if (o == 2) return rb[1];
+                    if (o == 3) return (rb[0] >> 5) & 1;
+                    if (o < 20) return (rb[8 + ((o - 4) >> 1)] >> (4 * ((o - 4) & 1))) & 15;
+                    return rb[4 + (o - 20)];  // nz_mask
+                };
+                v = hb(byte) | (hb(byte + 1) << 8);
+            }
+            h[q] = (uint16_t)v;
+        }
+        out[lane] = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16), h[4] | ((uint32_t)h[5] << 16),
+                               h[6] | ((uint32_t)h[7] << 16));
+    }
+}
+
+extern "C" hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
+                                     ZwDecMb* mbs, int nmb, int nframes)
+{
+    hipLaunchKernelGGL(k_dec_expand, dim3((nmb + 3) / 4, nframes), dim3(256), 0, s, recs, moff, fbase, mbs, nmb);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
                                     uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
 {

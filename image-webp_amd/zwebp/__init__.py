@@ -25,6 +25,7 @@ built, or no HIP device is visible, the first call raises.
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -365,15 +366,17 @@ class Frame:
 
 
 def _take_frame(L, f):
+    """Zero-copy: the planes are numpy views of the library's buffer, freed
+    (zw_frame_free) when the last view goes away."""
     ysz = f.y_stride * f.mb_rows * 16
     csz = f.uv_stride * f.mb_rows * 8
-    y = np.ctypeslib.as_array((ctypes.c_uint8 * ysz).from_address(f.y)).copy()
-    u = np.ctypeslib.as_array((ctypes.c_uint8 * csz).from_address(f.u)).copy()
-    v = np.ctypeslib.as_array((ctypes.c_uint8 * csz).from_address(f.v)).copy()
-    fr = Frame(f.width, f.height, y, u, v, f.y_stride, f.uv_stride, f.filter_type, f.filter_level,
-               f.sharpness_level)
-    L.zw_frame_free(ctypes.byref(f))
-    return fr
+    buf = (ctypes.c_uint8 * (ysz + 2 * csz)).from_address(f.y)
+    owner = _Frame()
+    ctypes.pointer(owner)[0] = f
+    weakref.finalize(buf, L.zw_frame_free, owner)
+    a = np.ctypeslib.as_array(buf)
+    return Frame(f.width, f.height, a[:ysz], a[ysz:ysz + csz], a[ysz + csz:], f.y_stride, f.uv_stride,
+                 f.filter_type, f.filter_level, f.sharpness_level)
 
 
 def vp8_decode_frame(data, ctx=None):
@@ -414,10 +417,14 @@ class UpsamplingMethod:
 
 
 def _take_image(L, b, w, h, bpp):
-    img = np.ctypeslib.as_array((ctypes.c_uint8 * b.len).from_address(b.data)).copy() if b.len else \
-        np.zeros(0, np.uint8)
-    L.zw_bytes_free(ctypes.byref(b))
-    return img.reshape(h, w, bpp)
+    """Zero-copy view of the library's image buffer (zw_bytes_free when unreferenced)."""
+    if not b.len:
+        L.zw_bytes_free(ctypes.byref(b))
+        return np.zeros((h, w, bpp), np.uint8)
+    buf = (ctypes.c_uint8 * b.len).from_address(b.data)
+    owner = _Bytes(b.data, b.len)
+    weakref.finalize(buf, L.zw_bytes_free, owner)
+    return np.ctypeslib.as_array(buf).reshape(h, w, bpp)
 
 
 def vp8_decode_rgb(data, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
