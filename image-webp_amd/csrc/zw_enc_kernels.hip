@@ -430,7 +430,6 @@ struct WaveLds {
     int y2d[64];
     int y2cost[4];
     int V[2][40];                 // I4 value vectors of the (up to) two sub-blocks of a search step
-    uint8_t pred[2][10][16];
     int nzt[4], nzl[4];
     uint8_t modes[16];
     int16_t lev[25][16];
@@ -695,6 +694,42 @@ __device__ __forceinline__ void i4_values_n(const Ctx& C, const int* x0, const i
 }
 __device__ __forceinline__ void i4_values(const Ctx& C, int x0, int y0) { i4_values_n<1>(C, &x0, &y0); }
 
+// Register form of i4_values_n for the search: lane l < 39 returns V[l] of
+// each block (no LDS round trip; consumers gather with ds_bpermute).
+template <int NB>
+__device__ __forceinline__ void i4_values_reg(const Ctx& C, const int* x0, const int* y0, int* vreg)
+{
+    const uint8_t* ws = C.W->ws;
+    const int l = C.lane;
+    const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
+    const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
+    const int t3 = (int)(t == 3), t4 = (int)(t >= 4), t12 = (int)(t == 1 || t == 2);
+    const int ka = k + t3 * (11 - k) + t4 * (1 - k);
+    const int kb = k + t12 + t3 * (12 - k) - t4 * k;
+    const int kc = min(k + 2 * (int)(t == 1), 12);
+    const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
+    const int wc = (int)(t == 1);
+    const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
+    const int oa = csel(ka < 4, -ka * ZW_BPS, ka - 4 - 4 * ZW_BPS);
+    const int ob = csel(kb < 4, -kb * ZW_BPS, kb - 4 - 4 * ZW_BPS);
+    const int oc = csel(kc < 4, -kc * ZW_BPS, kc - 4 - 4 * ZW_BPS);
+    const bool dcl = l < 4 || (l >= 5 && l < 9);
+    int ea[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int rowL = (y0[h] + 3) * ZW_BPS + x0[h] - 1;
+        ea[h] = ws[rowL + oa];
+        const int eb = ws[rowL + ob], ec = ws[rowL + oc];
+        vreg[h] = (ea[h] + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh;
+    }
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int dsum = __builtin_amdgcn_readfirstlane(red16(dcl ? ea[h] : 0));
+        vreg[h] = csel(l == 38, (dsum + 4) >> 3, vreg[h]);
+    }
+}
+__device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
+
 // V index of pixel p under I4 mode `mode`, with bit 8 set for TrueMotion
 // (pred = clamp(V[ia] + V[5 + col] - V[4])).  Sub-block independent.
 __device__ __forceinline__ int i4_src_index(const LdsTables* T, int mode, int p)
@@ -755,20 +790,23 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
         svk[h] = C.sY[(sby[h] * 4 + (k >> 2)) * 16 + sbx[h] * 4 + (k & 3)];
     }
     PH_START();
-    i4_values_n<NB>(C, x0, y0);
+    int vreg[NB];
+    i4_values_reg<NB>(C, x0, y0, vreg);
     PH_MARK_L(10, l, 0);
-    int e0[NB], e1[NB], e2[NB];
+    // lane (g, k): predictions of modes g, g+4, g+8 at pixel k, gathered from
+    // the V vectors held in lanes 0..38 (TrueMotion: V[3-row] + V[5+col] - V[4])
+    int e0[NB], e1[NB], e2[NB], p0[NB], p1[NB], p2[NB];
 #pragma unroll
     for (int h = 0; h < NB; h++) {
-        const int* V = W->V[h];
-        const int vbc = V[5 + (k & 3)] - V[4];
-        const int v0 = i4_pred_at(V, si0, vbc), v1 = i4_pred_at(V, si1, vbc), v2 = i4_pred_at(V, si2, vbc);
-        W->pred[h][g][k] = (uint8_t)v0;
-        W->pred[h][g + 4][k] = (uint8_t)v1;
-        if (g < 2) W->pred[h][g + 8][k] = (uint8_t)v2;
-        e0[h] = m24(svk[h] - v0, svk[h] - v0);
-        e1[h] = m24(svk[h] - v1, svk[h] - v1);
-        e2[h] = m24(svk[h] - v2, svk[h] - v2);
+        const int a0 = bperm(vreg[h], si0 & 255), a1 = bperm(vreg[h], si1 & 255), a2 = bperm(vreg[h], si2 & 255);
+        const int c5 = bperm(vreg[h], 5 + (k & 3));
+        const int vbc = c5 - __builtin_amdgcn_readlane(vreg[h], 4);
+        p0[h] = csel(si0 >= 256, clamp255(a0 + vbc), a0);
+        p1[h] = csel(si1 >= 256, clamp255(a1 + vbc), a1);
+        p2[h] = csel(si2 >= 256, clamp255(a2 + vbc), a2);
+        e0[h] = m24(svk[h] - p0[h], svk[h] - p0[h]);
+        e1[h] = m24(svk[h] - p1[h], svk[h] - p1[h]);
+        e2[h] = m24(svk[h] - p2[h], svk[h] - p2[h]);
     }
 #pragma unroll
     for (int h = 0; h < NB; h++) {
@@ -817,7 +855,10 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
 #pragma unroll
         for (int h = 0; h < NB; h++) {
             mm[h] = act ? (int)((cpack[h] >> (4 * c)) & 15) : 0;
-            pk[h] = W->pred[h][mm[h]][k];
+            // mode mm's prediction at pixel k lives in lane (mm & 3) * 16 + k, value mm >> 2
+            const int src = (mm[h] & 3) * 16 + k;
+            const int q0 = bperm(p0[h], src), q1 = bperm(p1[h], src), q2 = bperm(p2[h], src);
+            pk[h] = sel4(mm[h] >> 2, q0, q1, q2, 0);
         }
 #pragma unroll
         for (int h = 0; h < NB; h++) r[h] = fdct_g(svk[h] - pk[h], k);
