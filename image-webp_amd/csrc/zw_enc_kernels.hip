@@ -1516,6 +1516,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 
     if (PASS == 1 && wv == 0) {
         // ---- pass-1 chroma raster chain ----
+#ifdef ZW_CHAIN_PRIO
+        __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
+#endif
         if (lane < 4) W->left_derr[lane] = 0;
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
@@ -1547,7 +1550,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     // Pass 1: the luma wavefront couples every wave to the slowest row, and the
     // luma wave sharing a SIMD with the chroma chain would be that row: give
     // the luma waves issue priority (the chain has slack and uses the gaps).
-    if (PASS == 1) __builtin_amdgcn_s_setprio(2);
+#ifndef ZW_LUMA_PRIO
+#define ZW_LUMA_PRIO 2
+#endif
+    if (PASS == 1) __builtin_amdgcn_s_setprio(ZW_LUMA_PRIO);
     const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
     const int rw = PASS == 1 ? wv - 1 : wv;
     for (int mby = rw; mby < mbh; mby += nrw) {
