@@ -22,7 +22,8 @@ extern "C" {
 hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
                           ZwDecMb* mbs, int nmb, int nframes);
 hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
-                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
+                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes,
+                         const ZwFilterParams* fused_fp);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
                        int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
@@ -552,10 +553,14 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     HIPOK(hipEventRecord(ctx->dev_ev[0], s));
     HIPOK(zwk_dec_expand(s, d + o_mbs, (const uint32_t*)(d + o_mbs + o_moff), (const uint64_t*)(d + o_mbs + o_base),
                          (ZwDecMb*)(d + o_full), (int)nmb, n));
+    // two wavefront kernels (ZW_DEC_FUSE=1: one fused wavefront; measured slower on
+    // a 1080p frame, 8.2 vs 4.6 + 3.0 ms: the per-MB latencies add up in one chain)
+    static const bool split = getenv("ZW_DEC_FUSE") == nullptr;
     HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
-                        csz, n));
+                        csz, n, split ? nullptr : (const ZwFilterParams*)(d + o_fp)));
     HIPOK(hipEventRecord(ctx->dev_ev[1], s));
-    HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
+    if (split)
+        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
     HIPOK(hipEventRecord(ctx->dev_ev[2], s));
     if (dec_timing()) {
         HIPOK(hipEventSynchronize(ctx->dev_ev[2]));

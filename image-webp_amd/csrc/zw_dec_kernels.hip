@@ -90,10 +90,200 @@ __device__ __forceinline__ void dec_block_residual(int* c, int nz)
     }
 }
 
-extern "C" __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
+// ---------------------------------------------------------------------------
+// Loop filter (decoder/loop_filter.rs) on LDS-staged neighbourhoods.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int c8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+__device__ __forceinline__ int u2s(int v) { return v - 128; }
+__device__ __forceinline__ uint8_t s2u(int v) { return (uint8_t)(c8(v) + 128); }
+
+// p points at q0; s = step across the edge.
+__device__ __forceinline__ int lf_common(int outer, uint8_t* p, int s)
+{
+    const int p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]), q0 = u2s(p[0]), q1 = u2s(p[s]);
+    const int o = outer ? c8(p1 - q1) : 0;
+    int a = c8(o + 3 * (q0 - p0));
+    const int b = c8(a + 3) >> 3;
+    a = c8(a + 4) >> 3;
+    p[0] = s2u(q0 - a);
+    p[-s] = s2u(p0 + b);
+    return a;
+}
+__device__ __forceinline__ bool lf_simple_th(int lim, const uint8_t* p, int s)
+{
+    return iabs(p[-s] - p[0]) * 2 + iabs(p[-2 * s] - p[s]) / 2 <= lim;
+}
+__device__ __forceinline__ bool lf_should(int il, int el, const uint8_t* p, int s)
+{
+    return lf_simple_th(el, p, s) && iabs(p[-4 * s] - p[-3 * s]) <= il && iabs(p[-3 * s] - p[-2 * s]) <= il &&
+           iabs(p[-2 * s] - p[-s]) <= il && iabs(p[3 * s] - p[2 * s]) <= il && iabs(p[2 * s] - p[s]) <= il &&
+           iabs(p[s] - p[0]) <= il;
+}
+__device__ __forceinline__ bool lf_hev(int t, const uint8_t* p, int s) { return iabs(p[-2 * s] - p[-s]) > t || iabs(p[s] - p[0]) > t; }
+
+__device__ void lf_simple(int el, uint8_t* p, int s)
+{
+    if (lf_simple_th(el, p, s)) lf_common(1, p, s);
+}
+__device__ void lf_inner(int ht, int il, int el, uint8_t* p, int s)
+{
+    if (lf_should(il, el, p, s)) {
+        const bool hv = lf_hev(ht, p, s);
+        const int a = (lf_common(hv, p, s) + 1) >> 1;
+        if (!hv) {
+            p[s] = s2u(u2s(p[s]) - a);
+            p[-2 * s] = s2u(u2s(p[-2 * s]) + a);
+        }
+    }
+}
+__device__ void lf_mb(int ht, int il, int el, uint8_t* p, int s)
+{
+    if (lf_should(il, el, p, s)) {
+        if (!lf_hev(ht, p, s)) {
+            const int p2 = u2s(p[-3 * s]), p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]);
+            const int q0 = u2s(p[0]), q1 = u2s(p[s]), q2 = u2s(p[2 * s]);
+            const int w = c8(c8(p1 - q1) + 3 * (q0 - p0));
+            int a = c8((27 * w + 63) >> 7);
+            p[0] = s2u(q0 - a);
+            p[-s] = s2u(p0 + a);
+            a = c8((18 * w + 63) >> 7);
+            p[s] = s2u(q1 - a);
+            p[-2 * s] = s2u(p1 + a);
+            a = c8((9 * w + 63) >> 7);
+            p[2 * s] = s2u(q2 - a);
+            p[-3 * s] = s2u(p2 + a);
+        } else {
+            lf_common(1, p, s);
+        }
+    }
+}
+
+#define LFY 20   // luma staging: rows/cols -4..15 around the MB
+#define LFC 12   // chroma staging: -4..7
+
+struct LfLds {
+    uint8_t y[LFY * LFY];
+    uint8_t u[LFC * LFC], v[LFC * LFC];
+};
+
+// Filter one MB (filter_row_in_cache's per-MB edge order, decoder/vp8.rs:1172-1345)
+// on its LDS tile and write the tile back.  The lane holds the MB's interior
+// word cy (luma row lane>>2, word lane&3) and, for lanes < 32, cc (chroma plane
+// lane>>4, row (lane>>1)&7, word lane&1).  The tile's left 4 columns (with the
+// corner rows) are carried over in L from the previous MB of the row; the 4
+// rows above come from global memory, so the caller has waited for the row
+// above to finish MB mbx+1.  Lanes write back the whole tile (the interior
+// even when the level is 0: the fused kernel has not stored it yet).
+__device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
+                                        uint8_t* Vf, int ys, int cs, int mbx, int mby, int i4, int seg, int skip,
+                                        int nzd, uint32_t cy, uint32_t cc, bool write_interior_always)
+{
+    const bool chroma = !F.filter_type;
+    const int iy_r = lane >> 2, iy_w = lane & 3;
+    const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
+    const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
+    const int x0 = mbx * 16, y0 = mby * 16;
+    // ---- assemble the tile ----
+    if (mbx > 0) {  // left 4 columns (rows -4..15) from the previous tile's columns 12..15
+        if (lane < LFY) {
+            uint32_t* row = (uint32_t*)(L->y + lane * LFY);
+            row[0] = row[4];
+        }
+        if (chroma && lane >= 32 && lane < 32 + 2 * LFC) {
+            const int pl = (lane - 32) / LFC, r = (lane - 32) % LFC;
+            uint32_t* row = (uint32_t*)((pl ? L->v : L->u) + r * LFC);
+            row[0] = row[2];
+        }
+    }
+    ((uint32_t*)(L->y + (4 + iy_r) * LFY + 4))[iy_w] = cy;
+    if (chroma && lane < 32) ((uint32_t*)((ic_p ? L->v : L->u) + (4 + ic_r) * LFC + 4))[ic_w] = cc;
+    if (mby > 0) {  // the 4 rows above: luma lanes 0..15 (row lane>>2), chroma lanes 32..47
+        if (lane < 16) {
+            const int r = lane >> 2, w = lane & 3;
+            ((uint32_t*)(L->y + r * LFY + 4))[w] = *(const uint32_t*)(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
+        } else if (chroma && lane >= 32 && lane < 48) {
+            const int t = lane - 32, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
+            ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] =
+                *(const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
+        }
+    }
+    wsync();
+    if (lvl != 0) {
+        const int mbe = (lvl + 2) * 2 + il, sube = lvl * 2 + il;
+        const int inner = i4 || (!skip && nzd);
+        // lane roles: 0..15 luma line, 16..23 U line, 24..31 V line
+        const bool isy = lane < 16, isu = lane >= 16 && lane < 24, isv = lane >= 24 && lane < 32;
+        const int li = isy ? lane : (lane - 16) & 7;
+        uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
+        const int W_ = isy ? LFY : LFC;
+        const bool act = isy || (chroma && (isu || isv));
+        // left MB edge (vertical edge, filter along rows)
+        if (mbx > 0 && act) {
+            uint8_t* p = buf + (li + 4) * W_ + 4;
+            if (F.filter_type) lf_simple(mbe, p, 1);
+            else lf_mb(ht, il, mbe, p, 1);
+        }
+        wsync();
+        if (inner) {
+            for (int x = 4; x < 16; x += 4) {
+                if (isy) {
+                    uint8_t* p = buf + (li + 4) * W_ + 4 + x;
+                    if (F.filter_type) lf_simple(sube, p, 1);
+                    else lf_inner(ht, il, sube, p, 1);
+                } else if (act && x == 4) {
+                    lf_inner(ht, il, sube, buf + (li + 4) * W_ + 4 + 4, 1);
+                }
+                wsync();
+            }
+        }
+        if (mby > 0 && act) {
+            uint8_t* p = buf + 4 * W_ + 4 + li;
+            if (F.filter_type) lf_simple(mbe, p, W_);
+            else lf_mb(ht, il, mbe, p, W_);
+        }
+        wsync();
+        if (inner) {
+            for (int y = 4; y < 16; y += 4) {
+                if (isy) {
+                    uint8_t* p = buf + (4 + y) * W_ + 4 + li;
+                    if (F.filter_type) lf_simple(sube, p, W_);
+                    else lf_inner(ht, il, sube, p, W_);
+                } else if (act && y == 4) {
+                    lf_inner(ht, il, sube, buf + (4 + 4) * W_ + 4 + li, W_);
+                }
+                wsync();
+            }
+        }
+    }
+    if (lvl != 0 || write_interior_always) {
+        // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame)
+        for (int t = lane; t < LFY * 5; t += 64) {
+            const int r = t / 5 - 4, w = t % 5 - 1;
+            if (y0 + r >= 0 && x0 + 4 * w >= 0)
+                *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1];
+        }
+        if (chroma) {  // (the simple filter leaves chroma alone: the caller stores it)
+            for (int t = lane; t < 2 * LFC * 3; t += 64) {
+                const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+                if (mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
+                    *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) =
+                        ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1];
+            }
+        }
+    }
+    wsync();
+}
+
+// FUSE: the loop filter runs in the same wavefront right after each MB's
+// reconstruction (the prediction of later MBs reads the unfiltered borders kept
+// in LDS, vp8.rs:791-797; the filter reads and writes the planes in the same
+// raster-consistent order as k_loopfilter), so a frame pays one wavefront
+// instead of two.
+template <bool FUSE>
+__global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
-                                                              size_t csz)
+                                                              size_t csz, const ZwFilterParams* __restrict__ fp)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -107,6 +297,8 @@ extern "C" __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(
     uint8_t* top_u = smem + off;
     off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
     uint8_t* top_v = smem + off;
+    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    LfLds* LF = (LfLds*)(smem + off) + wv;  // FUSE only
     DecLds* W = (DecLds*)((uint8_t*)Wall + ((sizeof(DecLds) + 15) & ~(size_t)15) * wv);
     for (int i = lane; i < 160; i += 64) (&W->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WGD) top_y[i] = 127;
@@ -272,103 +464,40 @@ extern "C" __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(
                 top_u[mbx * 8 + lane - 40] = W->cu[8 * ZW_BPS + lane - 40 + 1];
                 top_v[mbx * 8 + lane - 40] = W->cv[8 * ZW_BPS + lane - 40 + 1];
             }
-            uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
-            for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
             uint8_t* uo = U + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
             uint8_t* vo = V + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
-            uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-            vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-            if (lane < 4) {
-                const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
-                flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
+            if (FUSE) {
+                const ZwFilterParams& F = fp[f];
+                // interior words: luma row lane>>2 word lane&3; chroma plane lane>>4, row (lane>>1)&7, word lane&1
+                const int iy_r = lane >> 2, iy_w = lane & 3;
+                const uint8_t* py = ws + (iy_r + 1) * ZW_BPS + 1 + 4 * iy_w;
+                const uint32_t cy = (uint32_t)py[0] | ((uint32_t)py[1] << 8) | ((uint32_t)py[2] << 16) | ((uint32_t)py[3] << 24);
+                const uint8_t* pc = ((lane >> 4) & 1 ? W->cv : W->cu) + (((lane >> 1) & 7) + 1) * ZW_BPS + 1 + 4 * (lane & 1);
+                const uint32_t cc = (uint32_t)pc[0] | ((uint32_t)pc[1] << 8) | ((uint32_t)pc[2] << 16) | ((uint32_t)pc[3] << 24);
+                if (F.filter_type) {  // simple filter: chroma is final as reconstructed
+                    uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+                    vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+                }
+                lf_tile(LF, lane, F, Y + (size_t)f * ysz, U + (size_t)f * csz, V + (size_t)f * csz, ys, cs, mbx, mby,
+                        lm == 4, M.segment, M.skip, nzdct, cy, cc, true);
+            } else {
+                uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
+                for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
+                uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+                vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+                if (lane < 4) {
+                    const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
+                    flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
+                }
+                wsync();
             }
-            wsync();
             dec_publish(progress, wv, mby * 65536 + mbx + 1);
         }
     }
 }
 
-// ---------------------------------------------------------------------------
-// Loop filter (decoder/loop_filter.rs) on LDS-staged neighbourhoods.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int c8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
-__device__ __forceinline__ int u2s(int v) { return v - 128; }
-__device__ __forceinline__ uint8_t s2u(int v) { return (uint8_t)(c8(v) + 128); }
-
-// p points at q0; s = step across the edge.
-__device__ __forceinline__ int lf_common(int outer, uint8_t* p, int s)
-{
-    const int p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]), q0 = u2s(p[0]), q1 = u2s(p[s]);
-    const int o = outer ? c8(p1 - q1) : 0;
-    int a = c8(o + 3 * (q0 - p0));
-    const int b = c8(a + 3) >> 3;
-    a = c8(a + 4) >> 3;
-    p[0] = s2u(q0 - a);
-    p[-s] = s2u(p0 + b);
-    return a;
-}
-__device__ __forceinline__ bool lf_simple_th(int lim, const uint8_t* p, int s)
-{
-    return iabs(p[-s] - p[0]) * 2 + iabs(p[-2 * s] - p[s]) / 2 <= lim;
-}
-__device__ __forceinline__ bool lf_should(int il, int el, const uint8_t* p, int s)
-{
-    return lf_simple_th(el, p, s) && iabs(p[-4 * s] - p[-3 * s]) <= il && iabs(p[-3 * s] - p[-2 * s]) <= il &&
-           iabs(p[-2 * s] - p[-s]) <= il && iabs(p[3 * s] - p[2 * s]) <= il && iabs(p[2 * s] - p[s]) <= il &&
-           iabs(p[s] - p[0]) <= il;
-}
-__device__ __forceinline__ bool lf_hev(int t, const uint8_t* p, int s) { return iabs(p[-2 * s] - p[-s]) > t || iabs(p[s] - p[0]) > t; }
-
-__device__ void lf_simple(int el, uint8_t* p, int s)
-{
-    if (lf_simple_th(el, p, s)) lf_common(1, p, s);
-}
-__device__ void lf_inner(int ht, int il, int el, uint8_t* p, int s)
-{
-    if (lf_should(il, el, p, s)) {
-        const bool hv = lf_hev(ht, p, s);
-        const int a = (lf_common(hv, p, s) + 1) >> 1;
-        if (!hv) {
-            p[s] = s2u(u2s(p[s]) - a);
-            p[-2 * s] = s2u(u2s(p[-2 * s]) + a);
-        }
-    }
-}
-__device__ void lf_mb(int ht, int il, int el, uint8_t* p, int s)
-{
-    if (lf_should(il, el, p, s)) {
-        if (!lf_hev(ht, p, s)) {
-            const int p2 = u2s(p[-3 * s]), p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]);
-            const int q0 = u2s(p[0]), q1 = u2s(p[s]), q2 = u2s(p[2 * s]);
-            const int w = c8(c8(p1 - q1) + 3 * (q0 - p0));
-            int a = c8((27 * w + 63) >> 7);
-            p[0] = s2u(q0 - a);
-            p[-s] = s2u(p0 + a);
-            a = c8((18 * w + 63) >> 7);
-            p[s] = s2u(q1 - a);
-            p[-2 * s] = s2u(p1 + a);
-            a = c8((9 * w + 63) >> 7);
-            p[2 * s] = s2u(q2 - a);
-            p[-3 * s] = s2u(p2 + a);
-        } else {
-            lf_common(1, p, s);
-        }
-    }
-}
-
-#define LFY 20   // luma staging: rows/cols -4..15 around the MB
-#define LFC 12   // chroma staging: -4..7
-
-struct LfLds {
-    uint8_t y[LFY * LFY];
-    uint8_t u[LFC * LFC], v[LFC * LFC];
-};
-
 // Per wave, row by row: the MB's 16x16 / 8x8 interiors only change when the
-// MB itself is filtered, so they are prefetched into registers one MB ahead;
-// the left 4 columns (with the corner) are carried over in LDS from the
-// previous MB's tile; only the 4 rows above come from global memory after the
-// wait on the row above.  Every tile is written back whole.
+// MB itself is filtered, so they are prefetched into registers one MB ahead.
 extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8_t* U, uint8_t* V,
                                                                const uint8_t* __restrict__ flags,
                                                                const ZwFilterParams* __restrict__ fp, size_t ysz,
@@ -387,7 +516,6 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
     uint8_t* Uf = U + (size_t)f * csz;
     uint8_t* Vf = V + (size_t)f * csz;
     const bool chroma = !F.filter_type;
-    // interior lanes: luma row lane>>2, word lane&3; chroma (lanes 0..31) plane lane>>4, row (lane>>1)&7, word lane&1
     const int iy_r = lane >> 2, iy_w = lane & 3;
     const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
     auto load_interior = [&](int mby, int mbx, uint32_t& py, uint32_t& pc) {
@@ -407,96 +535,8 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
                 nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 4);
             }
             if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            const int i4 = (fl & 255) == 4, seg = (fl >> 8) & 255, skip = (fl >> 16) & 255, nzd = fl >> 24;
-            const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
-            const int x0 = mbx * 16, y0 = mby * 16;
-            // ---- assemble the tile ----
-            if (mbx > 0) {  // left 4 columns (rows -4..15) from the previous tile's columns 12..15
-                if (lane < LFY) {
-                    uint32_t* row = (uint32_t*)(L->y + lane * LFY);
-                    row[0] = row[4];
-                }
-                if (chroma && lane >= 32 && lane < 32 + 2 * LFC) {
-                    const int pl = (lane - 32) / LFC, r = (lane - 32) % LFC;
-                    uint32_t* row = (uint32_t*)((pl ? L->v : L->u) + r * LFC);
-                    row[0] = row[2];
-                }
-            }
-            ((uint32_t*)(L->y + (4 + iy_r) * LFY + 4))[iy_w] = cy;
-            if (chroma && lane < 32) ((uint32_t*)((ic_p ? L->v : L->u) + (4 + ic_r) * LFC + 4))[ic_w] = cc;
-            if (mby > 0) {  // the 4 rows above: luma lanes 0..15 (row lane>>2), chroma lanes 32..47
-                if (lane < 16) {
-                    const int r = lane >> 2, w = lane & 3;
-                    ((uint32_t*)(L->y + r * LFY + 4))[w] = *(const uint32_t*)(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
-                } else if (chroma && lane >= 32 && lane < 48) {
-                    const int t = lane - 32, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
-                    ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] =
-                        *(const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
-                }
-            }
-            wsync();
-            if (lvl != 0) {
-                const int mbe = (lvl + 2) * 2 + il, sube = lvl * 2 + il;
-                const int inner = i4 || (!skip && nzd);
-                // lane roles: 0..15 luma line, 16..23 U line, 24..31 V line
-                const bool isy = lane < 16, isu = lane >= 16 && lane < 24, isv = lane >= 24 && lane < 32;
-                const int li = isy ? lane : (lane - 16) & 7;
-                uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
-                const int W_ = isy ? LFY : LFC;
-                const bool act = isy || (chroma && (isu || isv));
-                // left MB edge (vertical edge, filter along rows)
-                if (mbx > 0 && act) {
-                    uint8_t* p = buf + (li + 4) * W_ + 4;
-                    if (F.filter_type) lf_simple(mbe, p, 1);
-                    else lf_mb(ht, il, mbe, p, 1);
-                }
-                wsync();
-                if (inner) {
-                    for (int x = 4; x < 16; x += 4) {
-                        if (isy) {
-                            uint8_t* p = buf + (li + 4) * W_ + 4 + x;
-                            if (F.filter_type) lf_simple(sube, p, 1);
-                            else lf_inner(ht, il, sube, p, 1);
-                        } else if (act && x == 4) {
-                            lf_inner(ht, il, sube, buf + (li + 4) * W_ + 4 + 4, 1);
-                        }
-                        wsync();
-                    }
-                }
-                if (mby > 0 && act) {
-                    uint8_t* p = buf + 4 * W_ + 4 + li;
-                    if (F.filter_type) lf_simple(mbe, p, W_);
-                    else lf_mb(ht, il, mbe, p, W_);
-                }
-                wsync();
-                if (inner) {
-                    for (int y = 4; y < 16; y += 4) {
-                        if (isy) {
-                            uint8_t* p = buf + (4 + y) * W_ + 4 + li;
-                            if (F.filter_type) lf_simple(sube, p, W_);
-                            else lf_inner(ht, il, sube, p, W_);
-                        } else if (act && y == 4) {
-                            lf_inner(ht, il, sube, buf + (4 + 4) * W_ + 4 + li, W_);
-                        }
-                        wsync();
-                    }
-                }
-                // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame)
-                for (int t = lane; t < LFY * 5; t += 64) {
-                    const int r = t / 5 - 4, w = t % 5 - 1;
-                    if (y0 + r >= 0 && x0 + 4 * w >= 0)
-                        *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1];
-                }
-                if (chroma) {
-                    for (int t = lane; t < 2 * LFC * 3; t += 64) {
-                        const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
-                        if (mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
-                            *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) =
-                                ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1];
-                    }
-                }
-            }
-            wsync();
+            lf_tile(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255, (fl >> 16) & 255,
+                    fl >> 24, cy, cc, false);
             dec_publish(progress, wv, mby * 65536 + mbx + 1);
         }
     }
@@ -507,6 +547,7 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
     size_t off = ((sizeof(DecLds) + 15) & ~(size_t)15) * NWD + 64;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
     off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
+    off += sizeof(LfLds) * NWD;
     return off;
 }
 
@@ -568,16 +609,23 @@ extern "C" hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const u
     return hipGetLastError();
 }
 
+// fp == nullptr: reconstruction only (k_loopfilter follows); else the fused kernel.
 extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
-                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
+                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes,
+                                    const ZwFilterParams* fp)
 {
     static const bool attr = []() {
-        (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_dec_recon<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_dec_recon<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs, (const ZwDecQuant*)quant,
-                       Y, U, V, flags, mbw, mbh, ysz, csz);
+    if (fp)
+        hipLaunchKernelGGL(k_dec_recon<true>, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs,
+                           (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, fp);
+    else
+        hipLaunchKernelGGL(k_dec_recon<false>, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs,
+                           (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, fp);
     return hipGetLastError();
 }
 
