@@ -1390,8 +1390,32 @@ __device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
     for (int k = C.lane; k < nblk * 16; k += 64) dst[first_blk * 16 + k] = zero ? (int16_t)0 : srcl[first_blk * 16 + k];
 }
 
-__device__ void setup_ctx(Ctx& C, const EncArgs* a, const ZwFrameParams* P, const LdsTables* T, WaveLds* W,
-                          uint8_t* shared_base, int mbx, int mby)
+// What an MB needs from global memory, fetched one MB ahead (the loads are in
+// flight while the previous MB is encoded): the lane's word of the source MB
+// (luma: row lane>>2, word lane&3; chroma lanes < 32: plane lane>>4, row
+// (lane>>1)&7, word lane&1) and the MB's alpha (segment lookup).
+struct MbFetch {
+    uint32_t y, c;
+    int alpha;
+};
+__device__ __forceinline__ MbFetch fetch_mb(const EncArgs* a, int lane, int mbx, int mby)
+{
+    const int f = blockIdx.x, ys = a->mbw * 16, cs = a->mbw * 8;
+    const uint8_t* sy = a->Y + (size_t)f * a->ysz + (size_t)mby * 16 * ys + mbx * 16;
+    MbFetch r;
+    r.y = *(const uint32_t*)(sy + (size_t)(lane >> 2) * ys + (lane & 3) * 4);
+    r.c = 0;
+    if (lane < 32) {
+        const int pl = lane >> 4, k = lane & 15;
+        const uint8_t* sp = (pl ? a->V : a->U) + (size_t)f * a->csz + (size_t)mby * 8 * cs + mbx * 8;
+        r.c = *(const uint32_t*)(sp + (size_t)(k >> 1) * cs + (k & 1) * 4);
+    }
+    r.alpha = a->alpha[(size_t)f * a->mbw * a->mbh + (size_t)mby * a->mbw + mbx];
+    return r;
+}
+
+__device__ void setup_ctx(Ctx& C, const EncArgs* a, const uint8_t* seg_lut, WaveLds* W, int mbx, int mby,
+                          const MbFetch& m)
 {
     C.mbx = mbx;
     C.mby = mby;
@@ -1404,26 +1428,18 @@ __device__ void setup_ctx(Ctx& C, const EncArgs* a, const ZwFrameParams* P, cons
     // stage the source MB in LDS: 64 lanes x 4 B luma, 32 lanes x 4 B chroma
     {
         const int l = C.lane;
-        uint32_t* sy = (uint32_t*)W->sy;
-        sy[l] = *(const uint32_t*)(C.srcY + (size_t)(l >> 2) * C.ys + (l & 3) * 4);
-        if (l < 32) {
-            const int pl = l >> 4, k = l & 15;
-            const uint8_t* sp = pl ? C.srcV : C.srcU;
-            ((uint32_t*)(pl ? W->sv : W->su))[k] = *(const uint32_t*)(sp + (size_t)(k >> 1) * C.cs + (k & 1) * 4);
-        }
+        ((uint32_t*)W->sy)[l] = m.y;
+        if (l < 32) ((uint32_t*)((l >> 4) ? W->sv : W->su))[l & 15] = m.c;
         C.sY = W->sy;
         C.sU = W->su;
         C.sV = W->sv;
     }
     wsync();
-    int seg = 0;
-    if (P->seg_enabled) seg = P->seg_map_lut[a->alpha[(size_t)f * a->mbw * a->mbh + (size_t)mby * a->mbw + mbx]];
-    // wave-uniform: the segment's matrices / lambdas / sharpening then come in
-    // through the scalar cache (s_load into SGPRs) instead of per-lane loads
-    seg = __builtin_amdgcn_readfirstlane(seg);
+    // wave-uniform: the segment's matrices / lambdas / sharpening come from LDS;
+    // seg_lut is the k-means alpha -> segment map (all zero without segments)
+    const int seg = __builtin_amdgcn_readfirstlane((int)seg_lut[m.alpha]);
     C.seg = seg;
     C.S = C.Sl + seg;
-    (void)shared_base;
 }
 
 __device__ void wait_row(const int* progress, int wave_of_prev, int need)
@@ -1453,6 +1469,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
     ZwSegment* Sl = (ZwSegment*)(smem + off);  // the frame's 4 segments (matrices, lambdas, sharpening)
     off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
+    uint8_t* seg_lut = smem + off;  // alpha -> segment (zeros when segmentation is off)
+    off += 256;
     WaveLds* Wall = (WaveLds*)(smem + off);
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
     int* progress = (int*)(smem + off);
@@ -1479,6 +1497,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     static_assert(sizeof(ZwSegment) % 4 == 0, "segment copy by dwords");
     for (int i = threadIdx.x; i < (int)(4 * sizeof(ZwSegment) / 4); i += WG)
         ((uint32_t*)Sl)[i] = ((const uint32_t*)P->seg)[i];
+    for (int i = threadIdx.x; i < 256; i += WG) seg_lut[i] = P->seg_enabled ? P->seg_map_lut[i] : 0;
     load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
@@ -1520,6 +1539,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
 #endif
         if (lane < 4) W->left_derr[lane] = 0;
+        MbFetch nx = fetch_mb(&a, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
                 W->left_u[lane] = 129;
@@ -1528,7 +1548,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             wsync();
             for (int mbx = 0; mbx < mbw; mbx++) {
                 PH_START();
-                setup_ctx(C, &a, P, T, W, smem, mbx, mby);
+                const MbFetch cur = nx;
+                if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
+                else if (mby + 1 < mbh) nx = fetch_mb(&a, lane, 0, mby + 1);
+                setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
                 build_chroma_border(C);
                 const int cm = pick_uv(C);
                 PH_MARK(8);
@@ -1566,11 +1589,14 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         if (lane < 4) W->left_derr[lane] = 0;
         wsync();
         const int prevw = mby > 0 ? ((mby - 1) % nrw) + (PASS == 1 ? 1 : 0) : 0;
+        MbFetch nx = fetch_mb(&a, lane, 0, mby);
         for (int mbx = 0; mbx < mbw; mbx++) {
             PH_START();
+            const MbFetch cur = nx;
+            if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
             if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
             PH_MARK(0);
-            setup_ctx(C, &a, P, T, W, smem, mbx, mby);
+            setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
             build_luma_border(C);
             int lm;
             unsigned long long i16s;
@@ -1756,6 +1782,7 @@ extern "C" size_t zw_encode_lds_bytes(int mbw)
     size_t off = 0;
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
     off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
+    off += 256;
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
     off += 64;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
