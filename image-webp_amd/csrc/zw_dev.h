@@ -30,27 +30,23 @@ __constant__ uint8_t d_I4_IDX[10][16] = {
 
 #define DI __device__ __forceinline__
 
-// Compile-time copies of the small position tables: indexed with constants
-// inside unrolled loops they fold into immediates.
-DI int kZZ(int n)
+// Small position tables as 64-bit immediates: with a constant index they fold,
+// with a dynamic one (a loop the compiler kept rolled) they are a shift -- never
+// a load from constant memory.
+DI int kZZ(int n) { return (int)((0xfeb7adc963258410ull >> (4 * n)) & 15); }  // ZIGZAG
+DI int kBand(int n)  // VP8_ENC_BANDS[n], n in 0..16
 {
-    constexpr uint8_t t[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
-    return t[n];
+    return n >= 16 ? 0 : (int)((0x7666666665463210ull >> (4 * n)) & 15);
 }
-DI int kBand(int n)
+DI int kWTrellis(int j)  // VP8_WEIGHT_TRELLIS {30,27,19,11,27,24,17,10,19,17,12,8,11,10,8,6}
 {
-    constexpr uint8_t t[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
-    return t[n];
+    const unsigned long long lo = 0x0a11181b0b131b1eull, hi = 0x06080a0b080c1113ull;
+    return (int)(((j < 8 ? lo : hi) >> (8 * (j & 7))) & 255);
 }
-DI int kWTrellis(int j)
+DI int kWY(int j)  // kWeightY {38,32,20,9,32,28,17,7,20,17,10,4,9,7,4,2}
 {
-    constexpr uint16_t t[16] = {30, 27, 19, 11, 27, 24, 17, 10, 19, 17, 12, 8, 11, 10, 8, 6};
-    return t[j];
-}
-DI int kWY(int j)
-{
-    constexpr uint16_t t[16] = {38, 32, 20, 9, 32, 28, 17, 7, 20, 17, 10, 4, 9, 7, 4, 2};
-    return t[j];
+    const unsigned long long lo = 0x07111c2009142026ull, hi = 0x02040709040a1114ull;
+    return (int)(((j < 8 ? lo : hi) >> (8 * (j & 7))) & 255);
 }
 
 // Small position tables packed 4 bits per entry into 64-bit immediates: a

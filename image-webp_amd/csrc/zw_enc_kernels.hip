@@ -446,6 +446,7 @@ struct SharedHdr {
 struct Ctx {
     const EncArgs* a;
     const ZwFrameParams* P;
+    int method;           // EncoderParams method (wave-uniform, read once)
     const ZwSegment* S;   // the MB's segment, in LDS
     const ZwSegment* Sl;  // the frame's 4 segments, in LDS
     const LdsTables* T;
@@ -938,7 +939,7 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
     const int l = C.lane, g = l >> 4, k = l & 15;
-    const int K = C.P->method <= 3 ? 3 : (C.P->method == 4 ? 4 : 10);
+    const int K = C.method <= 3 ? 3 : (C.method == 4 ? 4 : 10);
     const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
     const int qk = (int)S.y1.q[k > 0];
     I4State st;
@@ -1516,12 +1517,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.W = W;
     C.lane = lane;
     C.Sl = Sl;
+    C.method = __builtin_amdgcn_readfirstlane(P->method);
     C.top_y = top_y;
     C.top_u = top_u;
     C.top_v = top_v;
     C.top_c = top_c;
     C.top_derr = top_derr;
-    const bool trel = PASS == 2 && P->do_trellis;
+    const bool trel = PASS == 2 && __builtin_amdgcn_readfirstlane(P->do_trellis);
     const size_t nmb = (size_t)mbw * mbh;
 #ifdef ZW_PHASE_PROF
     if (lane < 24) W->ph[lane] = 0;
@@ -1603,9 +1605,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             pick_i16(C, lm, i16s);
             wsync();
             PH_MARK(1);
-            if (P->method > 1) {
+            if (C.method > 1) {
                 const unsigned long long thr = 211ull * C.S->l_mode;
-                if (P->method >= 5 || i16s > thr || lm != 0) {
+                if (C.method >= 5 || i16s > thr || lm != 0) {
                     if (pick_i4(C, i16s)) lm = 4;
                 }
             }
