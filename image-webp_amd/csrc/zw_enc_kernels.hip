@@ -460,13 +460,19 @@ struct Ctx {
 };
 
 // create_border_luma (prediction.rs:15) into W->ws
-__device__ void build_luma_border(const Ctx& C)
+// part 0: corner, top and left (everything the I16 search reads: available once
+// the MB above is done); part 1: the top-right pixels (row 0 columns 17..31 and
+// their copies at rows 4, 8, 12; the I4 search needs the MB above-right);
+// part 2: both.
+__device__ void build_luma_border(const Ctx& C, int part = 2)
 {
     uint8_t* ws = C.W->ws;
     const int l = C.lane;
     const int mbw = C.a->mbw;
+    const bool want = part == 2 || (part == 0 ? (l < 17 || l >= 32) : (l >= 17 && l < 32));
     // row 0 entries 0..31
-    if (l < 32) {
+    if (!want) {
+    } else if (l < 32) {
         int v;
         if (l == 0) v = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : C.W->left_y[0]);
         else if (C.mby == 0) v = 127;
@@ -1596,28 +1602,33 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             PH_START();
             const MbFetch cur = nx;
             if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
-            if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
+            // the I16 and chroma searches need only the MB above (x, y-1); the
+            // I4 search also reads the above-right MB's bottom row: wait for
+            // (x+1, y-1) only then, so the wait overlaps the first searches
+            if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 1, mbw));
             PH_MARK(0);
             setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
-            build_luma_border(C);
+            build_luma_border(C, 0);
             int lm;
             unsigned long long i16s;
             pick_i16(C, lm, i16s);
             wsync();
             PH_MARK(1);
-            if (C.method > 1) {
-                const unsigned long long thr = 211ull * C.S->l_mode;
-                if (C.method >= 5 || i16s > thr || lm != 0) {
-                    if (pick_i4(C, i16s)) lm = 4;
-                }
-            }
-            PH_MARK(2);
             int cm = 0;
             if (PASS == 2) {
                 build_chroma_border(C);
                 cm = pick_uv(C);
             }
             PH_MARK(3);
+            if (C.method > 1) {
+                const unsigned long long thr = 211ull * C.S->l_mode;
+                if (C.method >= 5 || i16s > thr || lm != 0) {
+                    if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
+                    build_luma_border(C, 1);
+                    if (pick_i4(C, i16s)) lm = 4;
+                }
+            }
+            PH_MARK(2);
             int ynz[16];
             const int lnz = final_luma(C, lm, trel, ynz);
             PH_MARK(4);
