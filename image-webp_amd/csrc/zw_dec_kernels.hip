@@ -658,10 +658,16 @@ extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint
 // blockIdx.y.  Algorithmic bytes per pixel: 1 (Y) + 0.5 (U, V) read,
 // BPP written.
 // ---------------------------------------------------------------------------
+// clip (yuv.rs:57-61).  Written as inline v_med3_i32: otherwise the gfx950
+// backend fuses two neighbouring clips of the packed pixel into
+// v_ashr_pk_u8_i32 and then ORs the third channel over bits 16-31 it assumes
+// are zero; they are not (measured: blue read back as 255 whenever green
+// clipped to 0).
 __device__ __forceinline__ int yuv_clip(int v)
 {
-    v >>= 6;
-    return v < 0 ? 0 : (v > 255 ? 255 : v);
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v >> 6), "v"(255));
+    return r;
 }
 __device__ __forceinline__ uint32_t yuv_px(int y, int u, int v)
 {
@@ -672,61 +678,127 @@ __device__ __forceinline__ uint32_t yuv_px(int y, int u, int v)
     return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16) | 0xff000000u;
 }
 
+// General per-pixel form (edges, odd widths): the chroma sample indices with
+// their clamps, one byte load per sample.
+template <bool FANCY>
+__device__ __forceinline__ uint32_t yuv2rgb_px(const uint8_t* Y, const uint8_t* U, const uint8_t* V, int ys, int cs,
+                                               int cw1, int ch1, int r, int x)
+{
+    const int yv = Y[(size_t)r * ys + x];
+    int u, v;
+    if (FANCY) {
+        const int k = (r + 1) >> 1;
+        const int mr = (r & 1) ? k - 1 : k, sr = max(min((r & 1) ? k : k - 1, ch1), 0);
+        const int q = (x - 1) >> 1;  // x = 0: q = -1 -> mc = sc = 0
+        const int mc = (x & 1) ? q : q + 1, sc = min(max((x & 1) ? q + 1 : q, 0), cw1);
+        const uint8_t *um = U + (size_t)mr * cs, *us = U + (size_t)sr * cs;
+        const uint8_t *vm = V + (size_t)mr * cs, *vs = V + (size_t)sr * cs;
+        u = (9 * um[mc] + 3 * um[sc] + 3 * us[mc] + us[sc] + 8) >> 4;
+        v = (9 * vm[mc] + 3 * vm[sc] + 3 * vs[mc] + vs[sc] + 8) >> 4;
+    } else {
+        u = U[(size_t)(r >> 1) * cs + (x >> 1)];
+        v = V[(size_t)(r >> 1) * cs + (x >> 1)];
+    }
+    return yuv_px(yv, u, v);
+}
+
+__device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int i)  // i constant after unrolling
+{
+    const uint32_t w = i < 4 ? w0 : (i < 8 ? w1 : w2);
+    return (int)((w >> (8 * (i & 3))) & 255u);
+}
+
+// One thread per 8 horizontally adjacent pixels of one output row (x = 8 *
+// thread): Y as one 8-byte load, each chroma row as three aligned words
+// covering columns x/2-4 .. x/2+7, so the interior does two vector loads per
+// plane row and no per-sample addressing; the 8 pixels leave as two 16-byte
+// (RGBA) or six 4-byte (RGB) stores.  Threads at the image edges, or whose
+// row start is not 4-byte aligned in the packed RGB output, take the
+// per-pixel form.
 template <int BPP, bool FANCY>
 __global__ __launch_bounds__(256) void k_yuv2rgb(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
                                                  const uint8_t* __restrict__ V, size_t ysz, size_t csz, int w, int h,
                                                  int ys, int cs, uint8_t* __restrict__ out)
 {
-    const int f = blockIdx.y;
+    const int f = blockIdx.z, r = blockIdx.y;
+    const int x = (int)(blockIdx.x * 256u + threadIdx.x) * 8;
+    if (x >= w) return;
     Y += (size_t)f * ysz;
     U += (size_t)f * csz;
     V += (size_t)f * csz;
-    const uint32_t npx = (uint32_t)w * (uint32_t)h;
-    uint8_t* o = out + (size_t)f * npx * BPP;
-    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 4u;
-    if (p0 >= npx) return;
-    int r = (int)(p0 / (uint32_t)w), x = (int)(p0 - (uint32_t)r * (uint32_t)w);
+    uint8_t* o = out + ((size_t)f * h + r) * (size_t)w * BPP + (size_t)x * BPP;
     const int cw1 = ((w + 1) >> 1) - 1, ch1 = ((h + 1) >> 1) - 1;
-    uint32_t px[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int yv = Y[(size_t)r * ys + x];
-        int u, v;
+    const bool fast = x >= 8 && x + 8 <= w && (x >> 1) + 5 <= cw1 + 1 && (x >> 1) + 8 <= cs && (ys & 7) == 0 &&
+                      (cs & 3) == 0 && ((uintptr_t)o & (BPP == 4 ? 15 : 3)) == 0;
+    uint32_t px[8];
+    if (fast) {
+        const uint2 yy = *(const uint2*)(Y + (size_t)r * ys + x);
+        const int cb = (x >> 1) - 4;
+        int mr, sr;
         if (FANCY) {
             const int k = (r + 1) >> 1;
-            const int mr = (r & 1) ? k - 1 : k, sr = min((r & 1) ? k : k - 1, ch1);
-            const int q = (x - 1) >> 1;  // x = 0: q = -1 -> mc = sc = 0
-            const int mc = (x & 1) ? q : q + 1, sc = min(max((x & 1) ? q + 1 : q, 0), cw1);
-            const int srr = max(sr, 0);
-            const uint8_t *um = U + (size_t)mr * cs, *us = U + (size_t)srr * cs;
-            const uint8_t *vm = V + (size_t)mr * cs, *vs = V + (size_t)srr * cs;
-            u = (9 * um[mc] + 3 * um[sc] + 3 * us[mc] + us[sc] + 8) >> 4;
-            v = (9 * vm[mc] + 3 * vm[sc] + 3 * vs[mc] + vs[sc] + 8) >> 4;
+            mr = (r & 1) ? k - 1 : k;
+            sr = max(min((r & 1) ? k : k - 1, ch1), 0);
         } else {
-            u = U[(size_t)(r >> 1) * cs + (x >> 1)];
-            v = V[(size_t)(r >> 1) * cs + (x >> 1)];
+            mr = sr = r >> 1;
         }
-        px[j] = yuv_px(yv, u, v);
-        if (++x == w) {
-            x = 0;
-            r = min(r + 1, h - 1);  // past the last pixel: clamp (the store below drops it)
+        const uint32_t* um = (const uint32_t*)(U + (size_t)mr * cs + cb);
+        const uint32_t* vm = (const uint32_t*)(V + (size_t)mr * cs + cb);
+        const uint32_t um0 = um[0], um1 = um[1], um2 = um[2], vm0 = vm[0], vm1 = vm[1], vm2 = vm[2];
+        uint32_t us0 = um0, us1 = um1, us2 = um2, vs0 = vm0, vs1 = vm1, vs2 = vm2;
+        if (FANCY) {
+            const uint32_t* us = (const uint32_t*)(U + (size_t)sr * cs + cb);
+            const uint32_t* vs = (const uint32_t*)(V + (size_t)sr * cs + cb);
+            us0 = us[0], us1 = us[1], us2 = us[2], vs0 = vs[0], vs1 = vs[1], vs2 = vs[2];
         }
-    }
-    if (p0 + 4 <= npx) {
+        // fancy: 9 m + 3 s1 + 3 s2 + t = 3 (3 um + us)[mc] + (3 um + us)[sc], so
+        // blend the two chroma rows once per column (local columns 3..8)
+        int tu[6], tv[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const int c = 3 + j;
+            if (FANCY) {
+                tu[j] = 3 * byte_of(um0, um1, um2, c) + byte_of(us0, us1, us2, c);
+                tv[j] = 3 * byte_of(vm0, vm1, vm2, c) + byte_of(vs0, vs1, vs2, c);
+            } else {
+                tu[j] = byte_of(um0, um1, um2, c);
+                tv[j] = byte_of(vm0, vm1, vm2, c);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int yv = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 255u);
+            const int jm = 1 + (i >> 1);  // local chroma column (x + i) / 2 - 3
+            int u, v;
+            if (FANCY) {
+                const int js = (i & 1) ? jm + 1 : jm - 1;
+                u = (3 * tu[jm] + tu[js] + 8) >> 4;
+                v = (3 * tv[jm] + tv[js] + 8) >> 4;
+            } else {
+                u = tu[jm];
+                v = tv[jm];
+            }
+            px[i] = yuv_px(yv, u, v);
+        }
         if (BPP == 4) {
-            *(uint4*)(o + (size_t)p0 * 4) = make_uint4(px[0], px[1], px[2], px[3]);
+            ((uint4*)o)[0] = make_uint4(px[0], px[1], px[2], px[3]);
+            ((uint4*)o)[1] = make_uint4(px[4], px[5], px[6], px[7]);
         } else {
-            const uint32_t a = (px[0] & 0xffffffu) | (px[1] << 24);
-            const uint32_t b = ((px[1] >> 8) & 0xffffu) | (px[2] << 16);
-            const uint32_t c = ((px[2] >> 16) & 0xffu) | ((px[3] & 0xffffffu) << 8);
-            uint32_t* d = (uint32_t*)(o + (size_t)p0 * 3);
-            d[0] = a;
-            d[1] = b;
-            d[2] = c;
+            uint32_t* d = (uint32_t*)o;
+#pragma unroll
+            for (int g = 0; g < 2; g++) {
+                const uint32_t p0 = px[4 * g], p1 = px[4 * g + 1], p2 = px[4 * g + 2], p3 = px[4 * g + 3];
+                d[3 * g + 0] = (p0 & 0xffffffu) | (p1 << 24);
+                d[3 * g + 1] = ((p1 >> 8) & 0xffffu) | (p2 << 16);
+                d[3 * g + 2] = ((p2 >> 16) & 0xffu) | ((p3 & 0xffffffu) << 8);
+            }
         }
     } else {
-        for (uint32_t j = 0; j < 4 && p0 + j < npx; j++)
-            for (int c = 0; c < BPP; c++) o[(size_t)(p0 + j) * BPP + c] = (uint8_t)(px[j] >> (8 * c));
+        const int n = min(8, w - x);
+        for (int i = 0; i < n; i++) {
+            const uint32_t p = yuv2rgb_px<FANCY>(Y, U, V, ys, cs, cw1, ch1, r, x + i);
+            for (int c = 0; c < BPP; c++) o[(size_t)i * BPP + c] = (uint8_t)(p >> (8 * c));
+        }
     }
 }
 
@@ -734,8 +806,7 @@ extern "C" hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t
                                   size_t csz, int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out,
                                   int nframes)
 {
-    const uint32_t npx = (uint32_t)w * (uint32_t)h;
-    const dim3 grid((npx + 1023) / 1024, nframes);
+    const dim3 grid(((unsigned)w + 2047) / 2048, (unsigned)h, (unsigned)nframes);
     if (bpp == 4) {
         if (fancy) hipLaunchKernelGGL((k_yuv2rgb<4, true>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
         else hipLaunchKernelGGL((k_yuv2rgb<4, false>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
