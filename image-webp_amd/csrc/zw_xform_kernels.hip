@@ -143,6 +143,21 @@ __global__ __launch_bounds__(256) void k_fdct_quant_copy(const v4u* __restrict__
     }
 }
 
+// Calibration: the same bytes with every store instruction fully contiguous
+// (levels written as two planes; not the API layout).
+__global__ __launch_bounds__(256) void k_fdct_quant_copy_planar(const v4u* __restrict__ src, const v4u* __restrict__ pred,
+                                                                size_t n, XformArgs a, v4u* __restrict__ levels,
+                                                                v4u* __restrict__ recon)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t b = (size_t)blockIdx.x * 256 + threadIdx.x; b < n; b += stride) {
+        const v4u s4 = __builtin_nontemporal_load(&src[b]), p4 = __builtin_nontemporal_load(&pred[b]);
+        __builtin_nontemporal_store(s4 + p4, &levels[b]);
+        __builtin_nontemporal_store(s4 - p4, &levels[n + b]);
+        __builtin_nontemporal_store(s4 ^ p4, &recon[b]);
+    }
+}
+
 extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m,
                                      int first, void* levels, void* recon, int cus)
 {
@@ -161,7 +176,7 @@ extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void*
     //   ZW_XFORM_GRID     cap on workgroups, as a multiple of the CU count
     static const int variant = getenv("ZW_XFORM_VARIANT") ? atoi(getenv("ZW_XFORM_VARIANT")) : 5;
     static const int gmul = getenv("ZW_XFORM_GRID") ? atoi(getenv("ZW_XFORM_GRID")) : 1 << 20;
-    const int V = variant == 99 ? 1 : (variant >= 4 ? 4 : ((variant & 1) ? 2 : 1));
+    const int V = variant >= 98 ? 1 : (variant >= 4 ? 4 : ((variant & 1) ? 2 : 1));
     size_t grid = (n + 256 * V - 1) / (256 * V);
     const size_t cap = (size_t)(cus > 0 ? cus : 256) * gmul;
     if (grid > cap) grid = cap;
@@ -176,6 +191,7 @@ extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void*
     case 3: hipLaunchKernelGGL((k_fdct_quant_t<2, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 4: hipLaunchKernelGGL((k_fdct_quant_t<4, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 99: hipLaunchKernelGGL(k_fdct_quant_copy, g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 98: hipLaunchKernelGGL(k_fdct_quant_copy_planar, g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     default: hipLaunchKernelGGL((k_fdct_quant_t<4, true>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     }
     return hipGetLastError();
