@@ -25,11 +25,18 @@ static const int8_t UVMODE_TREE[6] = {-0, 2, -1, 4, -2, -3};
 static const int8_t TOKEN_TREE[22] = {-11, 2, -0, 4, -1, 6, 8, 12, -2, 10, -3, -4,
                                       14, 16, -5, -6, 18, 20, -7, -8, -9, -10};
 
+// ArithmeticEncoder (arithmetic.rs:7-196).  The reference renormalises one bit
+// per loop iteration; here all `shift` bits of one renormalisation are taken
+// at once (the same arithmetic in libvpx's batched form: `count` = -bit_num,
+// `low` = bottom), with the carry into already-written bytes propagated as the
+// reference's add_one does.  Byte-identical output (tests/test_host_entropy.py
+// drives both forms over random decision streams).
 struct BoolEncoder {
     std::vector<uint8_t> buf;
-    uint32_t bottom = 0, range = 255;
-    int bit_num = 24;
+    uint32_t low = 0, range = 255;
+    int count = -24;  // = -bit_num
 
+    BoolEncoder() { buf.reserve(1 << 16); }
     void add_one()
     {
         size_t i = buf.size();
@@ -44,6 +51,76 @@ struct BoolEncoder {
         buf.insert(buf.begin(), 1);
     }
     inline void put(int bit, int prob)
+    {
+        const uint32_t split = 1 + (((range - 1) * (uint32_t)prob) >> 8);
+        // branch-free: the coded bits are by construction unpredictable
+        const uint32_t m = 0u - (uint32_t)(bit != 0);
+        low += split & m;
+        const uint32_t r = split ^ ((split ^ (range - split)) & m);
+        // renormalise: range back to [128, 255]
+        const int shift = __builtin_clz(r) - 24;
+        range = r << shift;
+        count += shift;
+        if (count >= 0) {  // a byte is complete after `offset` of the shifts
+            const int offset = shift - count;
+            if ((low << (offset - 1)) & 0x80000000u) add_one();
+            buf.push_back((uint8_t)(low >> (24 - offset)));
+            low = (low << offset) & 0xffffffu;
+            low <<= count;
+            count -= 8;
+        } else {
+            low <<= shift;
+        }
+    }
+    void flag(int f) { put(f, 128); }
+    void literal(int nbits, int v)
+    {
+        for (int b = nbits - 1; b >= 0; b--) put(((1 << b) & v) > 0, 128);
+    }
+    void tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start = 0);
+    // a precomputed tree path: n bits, MSB-first bits / probability indices
+    inline void path(const uint8_t* bits, const uint8_t* pidx, int n, const uint8_t* probs)
+    {
+        for (int i = 0; i < n; i++) put(bits[i], probs[pidx[i]]);
+    }
+    void flush()  // the reference's flush (arithmetic.rs:176-196) on its state (bottom, bit_num)
+    {
+        const int bit_num = -count;
+        int c = bit_num;
+        uint32_t v = low;
+        if (low & (1u << (32 - bit_num))) add_one();
+        v <<= (c & 7);
+        c = (c >> 3) - 1;
+        while (c >= 0) {
+            v <<= 8;
+            c--;
+        }
+        for (c = 3; c >= 0; c--) {
+            buf.push_back((uint8_t)(v >> 24));
+            v <<= 8;
+        }
+    }
+};
+
+// The reference's bit-at-a-time form, kept for the equivalence test only.
+struct BoolEncoderRef {
+    std::vector<uint8_t> buf;
+    uint32_t bottom = 0, range = 255;
+    int bit_num = 24;
+    void add_one()
+    {
+        size_t i = buf.size();
+        while (i > 0) {
+            i--;
+            if (buf[i] < 255) {
+                buf[i]++;
+                return;
+            }
+            buf[i] = 0;
+        }
+        buf.insert(buf.begin(), 1);
+    }
+    void put(int bit, int prob)
     {
         uint32_t split = 1 + (((range - 1) * (uint32_t)prob) >> 8);
         if (bit) {
@@ -62,17 +139,6 @@ struct BoolEncoder {
                 bit_num = 8;
             }
         }
-    }
-    void flag(int f) { put(f, 128); }
-    void literal(int nbits, int v)
-    {
-        for (int b = nbits - 1; b >= 0; b--) put(((1 << b) & v) > 0, 128);
-    }
-    void tree(const int8_t* t, int tlen, const uint8_t* probs, int value, int start = 0);
-    // a precomputed tree path: n bits, MSB-first bits / probability indices
-    inline void path(const uint8_t* bits, const uint8_t* pidx, int n, const uint8_t* probs)
-    {
-        for (int i = 0; i < n; i++) put(bits[i], probs[pidx[i]]);
     }
     void flush()
     {
@@ -119,6 +185,16 @@ inline void BoolEncoder::tree(const int8_t* t, int tlen, const uint8_t* probs, i
     const int n = tree_path(t, tlen, value, start, bits, pidx);
     path(bits, pidx, n, probs);
 }
+
+// Precomputed paths of the mode trees (the per-MB header symbols).
+struct TreePaths {
+    uint8_t n[10], bits[10][16], pidx[10][16];
+    TreePaths(const int8_t* t, int tlen, int nsym)
+    {
+        for (int v = 0; v < nsym; v++) n[v] = (uint8_t)tree_path(t, tlen, v, 0, bits[v], pidx[v]);
+    }
+    void put(BoolEncoder& E, const uint8_t* probs, int v) const { E.path(bits[v], pidx[v], n[v], probs); }
+};
 
 // TOKEN_TREE paths for tokens 0..11 from start index 0 / 2 (after a zero token)
 struct TokenPaths {
@@ -206,8 +282,15 @@ inline void rec_stat(uint32_t& s, int bit)
     s += 0x00010000u + (bit ? 1u : 0u);
 }
 
+inline int token_of(int a)  // |level| -> token (0..10)
+{
+    return a <= 4 ? a : (a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10);
+}
+
 // record_coeffs (cost.rs:1297) over a packed block: eob = last nonzero + 1,
-// lv = its zigzag levels.
+// lv = its zigzag levels.  (The branchy form measured faster than walking the
+// token paths: most tokens are 0 / 1 and predict well.)  Quirk
+// (cost.rs:1325-1342): skip_eob is never cleared once a zero token was seen.
 inline void record_coeffs(Stats& S, const uint8_t* lv, int eob, int t, int first, int ctx)
 {
     if (eob <= first) {
@@ -391,14 +474,7 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* 
         const int coeff = lv_at(lv, idx);
         const uint8_t* pr = P[COEFF_BANDS[idx]][ctx];
         const int a = coeff < 0 ? -coeff : coeff;
-        int token;
-        if (a == 0) {
-            token = 0;
-        } else if (a <= 4) {
-            token = a;
-        } else {
-            token = a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10;
-        }
+        const int token = token_of(a);
         E.path(TP.bits[skip_eob][token], TP.pidx[skip_eob][token], TP.n[skip_eob][token], pr);
         if (token >= 5) {
             const int cat = token;
@@ -478,6 +554,8 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
     H.literal(1, 1);
     H.literal(8, P.skip_prob);
 
+    static const TreePaths seg_t(SEGMENT_ID_TREE, 6, 4), ymode_t(YMODE_TREE, 8, 5), bmode_t(BMODE_TREE, 18, 10),
+        uvmode_t(UVMODE_TREE, 6, 4);
     std::vector<Cplx> top(mbw);
     memset(top.data(), 0, sizeof(Cplx) * mbw);
     std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
@@ -487,15 +565,15 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
         uint8_t left_bp[4] = {0, 0, 0, 0};
         for (int x = 0; x < mbw; x++) {
             packed = view_mb(packed, m);
-            if (P.seg_enabled && P.seg_update_map) H.tree(SEGMENT_ID_TREE, 6, P.seg_probs, m.segment);
+            if (P.seg_enabled && P.seg_update_map) seg_t.put(H, P.seg_probs, m.segment);
             H.put(m.skip, P.skip_prob);
-            H.tree(YMODE_TREE, 8, KEYFRAME_YMODE_PROBS, m.luma);
+            ymode_t.put(H, KEYFRAME_YMODE_PROBS, m.luma);
             if (m.luma == 4) {
                 for (int by = 0; by < 4; by++) {
                     int l = left_bp[by];
                     for (int bx = 0; bx < 4; bx++) {
                         int t = top_bp[x * 4 + bx], md = m.bpred[by * 4 + bx];
-                        H.tree(BMODE_TREE, 18, KEYFRAME_BPRED_MODE_PROBS[t][l], md);
+                        bmode_t.put(H, KEYFRAME_BPRED_MODE_PROBS[t][l], md);
                         l = md;
                         top_bp[x * 4 + bx] = (uint8_t)md;
                     }
@@ -505,7 +583,7 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
                 static const int intra_of[4] = {0, 2, 3, 1};
                 for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma];
             }
-            H.tree(UVMODE_TREE, 6, KEYFRAME_UV_MODE_PROBS, m.chroma);
+            uvmode_t.put(H, KEYFRAME_UV_MODE_PROBS, m.chroma);
             const bool i4 = m.luma == 4;
             if (m.skip) {
                 left.clear(!i4);
