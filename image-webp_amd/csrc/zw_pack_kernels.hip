@@ -20,6 +20,22 @@
 
 __device__ __forceinline__ int pk_mb_size(int luma, int eobsum) { return 1 + (luma == 4 ? 8 : 0) + 25 + 2 * eobsum; }
 
+// The 800 B of levels of an MB as 200 aligned words (ZwMbOut is 4-byte
+// aligned): round r, lane l holds word j = l + 64 r = zigzag positions
+// 2 (j & 7), +1 of block j >> 3; the 8 lanes of a block reduce with DPP.
+__device__ __forceinline__ int pk_word_eob(uint32_t v, int j)
+{
+    const int n0 = 2 * (j & 7);
+    return (v >> 16) ? n0 + 2 : ((v & 0xffffu) ? n0 + 1 : 0);
+}
+__device__ __forceinline__ int max8(int e)  // max within aligned 8-lane groups, result in every lane
+{
+    e = max(e, __builtin_amdgcn_mov_dpp(e, 0xB1, 0xf, 0xf, false));  // quad xor 1
+    e = max(e, __builtin_amdgcn_mov_dpp(e, 0x4E, 0xf, 0xf, false));  // quad xor 2
+    e = max(e, __builtin_amdgcn_mov_dpp(e, 0x141, 0xf, 0xf, false)); // row half mirror: lane i <-> 7-i
+    return e;
+}
+
 extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_size(const ZwMbOut* __restrict__ mbs, int nmb,
                                                                       int nframes, uint8_t* __restrict__ eobs,
                                                                       uint32_t* __restrict__ sizes)
@@ -28,19 +44,21 @@ extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_size(const Zw
     const int lane = threadIdx.x & 63;
     if (mb >= (size_t)nmb * nframes) return;
     const ZwMbOut& M = mbs[mb];
-    int eob = 0;
-    if (lane < 25) {
-        const uint32_t* p = (const uint32_t*)&M.levels[lane][0];
+    const uint32_t* W = (const uint32_t*)&M.levels[0][0];
+    uint32_t w[4];
 #pragma unroll
-        for (int w = 0; w < 8; w++) {
-            const uint32_t v = p[w];
-            if (v & 0xffffu) eob = 2 * w + 1;
-            if (v >> 16) eob = 2 * w + 2;
+    for (int r = 0; r < 4; r++) w[r] = lane + 64 * r < 200 ? W[lane + 64 * r] : 0u;
+    const int skip = M.skip;
+    int s = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int j = lane + 64 * r;
+        const int eob = skip ? 0 : max8(pk_word_eob(w[r], j));
+        if ((j & 7) == 0 && j < 200) {
+            eobs[mb * 25 + (j >> 3)] = (uint8_t)eob;
+            s += eob;
         }
-        if (M.skip) eob = 0;
-        eobs[mb * 25 + lane] = (uint8_t)eob;
     }
-    int s = eob;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
     if (lane == 0) sizes[mb] = (uint32_t)pk_mb_size(M.luma_mode, s);
@@ -82,6 +100,8 @@ extern "C" __global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restr
     }
 }
 
+// MB sizes are even (header 26 or 34 bytes + 2 per level) and so are the
+// frame slices, so every level lands on a 2-byte aligned address.
 extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
     const ZwMbOut* __restrict__ mbs, int nmb, int nframes, const uint8_t* __restrict__ eobs,
     const uint32_t* __restrict__ offs, const unsigned long long* __restrict__ frame_info, uint8_t* __restrict__ out)
@@ -106,12 +126,17 @@ extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
         if (lane >= d) pre += v;
     }
     pre -= eob;
-    if (lane < 25) {
-        uint8_t* lv = o + hdr + 25 + 2 * pre;  // byte stream: i16 little-endian, unaligned
-        for (int n = 0; n < eob; n++) {
-            const int16_t v = M.levels[lane][n];
-            lv[2 * n] = (uint8_t)(v & 0xff);
-            lv[2 * n + 1] = (uint8_t)((uint16_t)v >> 8);
+    int16_t* lv = (int16_t*)(o + hdr + 25);
+    const uint32_t* W = (const uint32_t*)&M.levels[0][0];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int j = lane + 64 * r;
+        const int b = min(j >> 3, 24), n0 = 2 * (j & 7);
+        const int eb = __shfl(eob, b), st = __shfl(pre, b);
+        if (j < 200 && n0 < eb) {
+            const uint32_t v = W[j];
+            lv[st + n0] = (int16_t)(v & 0xffffu);
+            if (n0 + 1 < eb) lv[st + n0 + 1] = (int16_t)(v >> 16);
         }
     }
 }
