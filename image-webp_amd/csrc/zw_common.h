@@ -42,6 +42,14 @@ struct ZwFrameParams {
     uint8_t probs[4][8][3][11];            // token probabilities in effect
 };
 
+// Pass-1 token statistics of one frame from k_stats (zw_stats_kernels.hip):
+// ProbaStats counters [type][band][ctx][node] exactly as the reference holds
+// them, and the MB counts for the skip probability.
+struct ZwStatsOut {
+    uint32_t s[4 * 8 * 3 * 11];
+    uint32_t nonzero_mbs, total_mbs;
+};
+
 // LevelCosts (encoder/cost.rs:1452-1545) for one frame.
 struct ZwLevelCosts {
     uint16_t lc[4][8][3][68];

@@ -30,6 +30,8 @@ hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const
                         size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes);
 hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
                         int nframes);
+hipError_t zwk_stats(hipStream_t s, const ZwMbOut* mbs, int mbw, int mbh, void* scratch, void* out, int nframes);
+size_t zw_stats_scratch_bytes(int nmb, int nframes);
 hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
                      unsigned long long* counter, unsigned long long* frame_info, uint8_t* out);
 hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m, int first,
@@ -224,6 +226,7 @@ struct PipeLane {
     size_t h_pack_cap = 0;
     Pinned<unsigned long long> h_finfo;  // [2*n] offset, bytes of each frame's packed stream
     Pinned<unsigned long long> h_total;
+    Pinned<ZwStatsOut> h_stats;          // [chunk] pass-1 statistics from k_stats
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
     int rc = 0;
@@ -241,6 +244,9 @@ struct zw_pipe {
     int8_t* d_derr = nullptr;
     ZwMbOut *d_out1 = nullptr, *d_out2 = nullptr;
     int* d_dbg = nullptr;  // optional pass-2 I4 dump
+    ZwStatsOut* d_stats = nullptr;  // pass-1 statistics (zwk_stats)
+    void* d_stats_tmp = nullptr;    // zwk_stats scratch (flags, stripe partials)
+    bool host_stats = false;        // ZW_HOST_STATS=1: replay the statistics on the host instead
     // packed MB streams (zw_pack_kernels.hip)
     uint8_t* d_eobs = nullptr;
     uint32_t* d_sizes = nullptr;
@@ -261,7 +267,7 @@ static void pipe_free(zw_pipe* p)
     if (!p) return;
     void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
                     p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg,
-                    p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack, p->d_finfo2, p->d_pack2};
+                    p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack, p->d_finfo2, p->d_pack2, p->d_stats, p->d_stats_tmp};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     for (PipeLane& L : p->lanes) {
@@ -352,13 +358,18 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
               hipMalloc(&p->d_pack, N * p->pack_stride) == hipSuccess &&
               hipMalloc(&p->d_finfo2, N * 2 * sizeof(unsigned long long)) == hipSuccess &&
               hipMalloc(&p->d_pack2, N * p->pack_stride) == hipSuccess;
+    // Pass-1 statistics are pre-aggregated on the device (zwk_stats) unless
+    // ZW_HOST_STATS asks for the host replay of the packed records.
+    p->host_stats = getenv("ZW_HOST_STATS") != nullptr;
+    ok = ok && (p->host_stats || (hipMalloc(&p->d_stats, N * sizeof(ZwStatsOut)) == hipSuccess &&
+                                  hipMalloc(&p->d_stats_tmp, zw_stats_scratch_bytes(p->nmb, n)) == hipSuccess));
     const int G = pipe_lanes_for(n);
     p->lanes.resize(G);
     for (int g = 0; ok && g < G; g++) {
         PipeLane& L = p->lanes[g];
         L.f0 = (int)((long long)n * g / G);
         L.n = (int)((long long)n * (g + 1) / G) - L.f0;
-        ok = L.h_finfo.alloc(2 * (size_t)L.n);
+        ok = L.h_finfo.alloc(2 * (size_t)L.n) && (p->host_stats || L.h_stats.alloc((size_t)L.n));
         L.chunk = pipe_chunk_for(L.n, ctx->device);
         const int nch = (L.n + L.chunk - 1) / L.chunk;
         L.cev.assign(2 * (size_t)nch, nullptr);
@@ -480,6 +491,14 @@ static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEve
     return ctx_d2h(p->ctx, L.h_pack, (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, total);
 }
 
+// Fetch the chunk's k_stats output (device pre-aggregated ProbaStats) once
+// `ready` (recorded after zwk_stats) has fired.  h_stats[i] = frame fa+i.
+static int chunk_fetch_stats(zw_pipe* p, PipeLane& L, int fa, int na, hipEvent_t ready)
+{
+    HIPOK(hipEventSynchronize(ready));
+    return ctx_d2h(p->ctx, L.h_stats.data() + (fa - L.f0), p->d_stats + fa, (size_t)na * sizeof(ZwStatsOut));
+}
+
 static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
 {
     hipStream_t s = L.stream;
@@ -492,7 +511,14 @@ static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
     parallel_for(na, [&](int i) {
         const size_t f = F + i;
         zwh::Stats st;
-        int sp = zwh::replay_stats(st, L.h_pack + L.h_finfo[2 * i], p->mbw, p->mbh);
+        int sp;
+        if (p->host_stats) {
+            sp = zwh::replay_stats(st, L.h_pack + L.h_finfo[2 * i], p->mbw, p->mbh);
+        } else {
+            const ZwStatsOut& so = L.h_stats[f - L.f0];
+            memcpy(st.s, so.s, sizeof st.s);
+            sp = zwh::skip_prob(so.total_mbs, so.nonzero_mbs);
+        }
         uint8_t* upd = p->h_upd.data() + f * 4 * 8 * 3 * 11;
         bool have = zwh::updated_probs(st, (uint8_t(*)[8][3][11])upd);
         p->h_have_upd[f] = have;
@@ -557,7 +583,16 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     auto queue_pass1 = [&]() -> int {
         for (int c = 0; c < nch; c++) {
             int r = chunk_pass1(p, L, ca(c), cn(c), c == 0);
-            if (!r) r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
+            if (!r) {
+                if (p->host_stats) {
+                    r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
+                } else {
+                    const size_t F = (size_t)ca(c);
+                    HIPOK(zwk_stats(L.stream, p->d_out1 + F * p->nmb, p->mbw, p->mbh,
+                                    (uint8_t*)p->d_stats_tmp + zw_stats_scratch_bytes(p->nmb, (int)F),
+                                    p->d_stats + F, cn(c)));
+                }
+            }
             if (r) return r;
             HIPOK(hipEventRecord(L.cev[2 * c], L.stream));
         }
@@ -569,7 +604,8 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     for (int b = 0; b < nb; b++) {
         for (int c = 0; c < nch; c++) {
             double t0 = now_ms();
-            r = chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c]);
+            r = p->host_stats ? chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c])
+                              : chunk_fetch_stats(p, L, ca(c), cn(c), L.cev[2 * c]);
             if (r) return r;
             double t1 = now_ms();
             r = chunk_stats(p, L, ca(c), cn(c));

@@ -370,6 +370,15 @@ inline bool mb_all_zero_p1(const PackedMb& m)
     return true;
 }
 
+// Skip probability from the MB counts (vp8.rs:1387-1394).
+inline int skip_prob(uint32_t total, uint32_t ns)
+{
+    uint32_t p = (255 * ns + total / 2) / total;
+    if (p > 255) p = 255;
+    int sp = (int)(uint8_t)p;
+    return sp < 1 ? 1 : (sp > 254 ? 254 : sp);
+}
+
 // Pass-1 statistics replay in raster order (vp8.rs:1337-1385 + record_residual_stats :1027).
 // Returns the skip probability.
 inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
@@ -426,11 +435,7 @@ inline int replay_stats(Stats& S, const uint8_t* packed, int mbw, int mbh)
             }
         }
     }
-    uint32_t ns = total - skipped;
-    uint32_t p = (255 * ns + total / 2) / total;
-    if (p > 255) p = 255;
-    int sp = (int)(uint8_t)p;
-    return sp < 1 ? 1 : (sp > 254 ? 254 : sp);
+    return skip_prob(total, total - skipped);
 }
 
 // compute_updated_probabilities (vp8.rs:1202); returns whether any update applies.

@@ -337,6 +337,21 @@ def test_1080p_encode_decode_roundtrip(ctx):
     assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
 
 
+@pytest.mark.parametrize("w,h,kind,q", [(1920, 1080, "natural", 75), (1920, 1080, "noise", 95),
+                                         (2048, 2048, "noise", 100), (1920, 1080, "flat", 75)])
+def test_device_stats_equal_host_replay(ctx, monkeypatch, w, h, kind, q):
+    """k_stats (device ProbaStats pre-aggregation, including the exact replay of
+    counters that pass 0xfffe decisions and halve) gives the same bitstreams as
+    the host's raster replay of the pass-1 records (ZW_HOST_STATS=1), which the
+    oracle-parity tests pin to the reference."""
+    imgs = [synth_rgba(w, h, 0x5EED2000 + i, kind) for i in range(2)]
+    dev = zwebp.encode_batch(imgs, w, h, zwebp.ColorType.Rgba8, q, 4, ctx=ctx)
+    monkeypatch.setenv("ZW_HOST_STATS", "1")
+    host = zwebp.encode_batch(imgs, w, h, zwebp.ColorType.Rgba8, q, 4, ctx=ctx)
+    for i in range(len(imgs)):
+        assert dev[i] == host[i], f"frame {i}"
+
+
 # --------------------------------------------------------------------------
 # a7/a8: quantisation and trellis on independent blocks
 # --------------------------------------------------------------------------
