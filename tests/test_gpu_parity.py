@@ -337,8 +337,15 @@ def test_1080p_encode_decode_roundtrip(ctx):
     assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
 
 
+def test_4k_encode_matches_oracle(ctx):
+    """BASELINE config 5 frame size (3840x2160, 240x135 MBs) Q75 m4: every stage
+    and the bitstream equal the oracle's."""
+    _check_encode(ctx, 3840, 2160, "natural", 75, 4, 3, 0x5EED4000)
+
+
 @pytest.mark.parametrize("w,h,kind,q", [(1920, 1080, "natural", 75), (1920, 1080, "noise", 95),
-                                         (2048, 2048, "noise", 100), (1920, 1080, "flat", 75)])
+                                         (2048, 2048, "noise", 100), (1920, 1080, "flat", 75),
+                                         (3840, 2160, "noise", 90)])
 def test_device_stats_equal_host_replay(ctx, monkeypatch, w, h, kind, q):
     """k_stats (device ProbaStats pre-aggregation, including the exact replay of
     counters that pass 0xfffe decisions and halve) gives the same bitstreams as
