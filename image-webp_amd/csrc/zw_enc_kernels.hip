@@ -954,7 +954,9 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
     st.mpack = 0;
     st.tnz = st.lnz = 0;
     const int si0 = i4_src_index(T, g, k), si1 = i4_src_index(T, g + 4, k), si2 = i4_src_index(T, g < 2 ? g + 8 : 0, k);
+    PH_COUNT(20);
     for (int s = 0; s < 10; s++) {
+        PH_COUNT(19);
         // anti-diagonal s: A = (sbx, sby) with the smallest sby, B = (sbx - 2, sby + 1)
         const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
         const int sbxA = s - 2 * sbyA;

@@ -23,7 +23,8 @@ NAMES = {0: "wait(row above)", 1: "border+pick_i16", 2: "pick_i4", 3: "pick_uv",
          5: "final_chroma", 6: "store/levels/publish", 8: "p1 chroma pick_uv", 9: "p1 chroma final",
          10: "  i4: values", 11: "  i4: preds+sse+rank", 12: "  i4: candidates", 13: "  i4: select+recon",
          7: "  (count of I4 MBs)", 14: "  final: I16 MBs", 15: "  final: I4 MBs",
-         16: "    i16: fdct+y2", 17: "    i16: quant check+trellis", 18: "    i16: ctx resolve+gather"}
+         16: "    i16: fdct+y2", 17: "    i16: quant check+trellis", 18: "    i16: ctx resolve+gather",
+         19: "  (I4 search steps run)", 20: "  (I4 searches)"}
 
 
 def main():
@@ -49,11 +50,11 @@ def main():
     print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt[:4]]} "
           f"host(ms) fetch1/stats/fetch2/emit {[round(x, 2) for x in kt[4:8]]}")
     for ps in (0, 1):
-        tot = sum(buf[ps * 24 + k] for k in range(10) if k != 7) or 1
+        tot = sum(buf[ps * 24 + k] for k in range(10) if k not in (7, 19, 20)) or 1
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
         for k in range(24):
             v = buf[ps * 24 + k]
-            if v and k == 7:
+            if v and k in (7, 19, 20):
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.3f} of MBs")
             elif v:
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.0f} cyc/MB  {100 * v / tot:5.1f}%")
