@@ -26,6 +26,12 @@ hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, u
                          const ZwFilterParams* fused_fp);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
                        int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
+hipError_t zwk_dec_rows(hipStream_t s, int phase, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
+                        uint8_t* V, uint8_t* flags, const ZwFilterParams* fp, int mbw, int mbh, size_t ysz, size_t csz,
+                        int nframes, int* rowsync, uint8_t* borders, int rows);
+hipError_t zwk_dec_rows_init(hipStream_t s, int* rowsync, int mbh, int nframes);
+size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
+size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
                           const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes);
 }
@@ -537,7 +543,14 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     const size_t o_fl = al256(o_full + (size_t)n * nmb * sizeof(ZwDecMb));
     const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
     const size_t o_u = al256(o_y + (size_t)n * ysz), o_v = al256(o_u + (size_t)n * csz);
-    const size_t o_extra = al256(o_v + (size_t)n * csz);
+    // Small batches run the row-parallel kernels (one wave per MB row, the x+2y
+    // wavefront spread over up to mbh CUs); large ones fill the GPU with one
+    // workgroup per frame.  ZW_DEC_ROWS=0/1 forces either.
+    const int rows_env = getenv("ZW_DEC_ROWS") ? atoi(getenv("ZW_DEC_ROWS")) : -1;
+    const bool rows = rows_env >= 0 ? rows_env != 0 : n < 128;  // measured: rows faster up to 64, slower at 256
+    const size_t o_rs = al256(o_v + (size_t)n * csz);
+    const size_t o_bd = al256(o_rs + (rows ? zw_dec_rows_sync_bytes(mbh, n) : 0));
+    const size_t o_extra = al256(o_bd + (rows ? zw_dec_rows_border_bytes(mbw, n) : 0));
     const size_t total = al256(o_extra + extra_bytes);
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
@@ -556,11 +569,22 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     // two wavefront kernels (ZW_DEC_FUSE=1: one fused wavefront; measured slower on
     // a 1080p frame, 8.2 vs 4.6 + 3.0 ms: the per-MB latencies add up in one chain)
     static const bool split = getenv("ZW_DEC_FUSE") == nullptr;
-    HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz,
-                        csz, n, split ? nullptr : (const ZwFilterParams*)(d + o_fp)));
-    HIPOK(hipEventRecord(ctx->dev_ev[1], s));
-    if (split)
-        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n));
+    if (rows) {
+        int* rs = (int*)(d + o_rs);
+        HIPOK(zwk_dec_rows_init(s, rs, mbh, n));
+        HIPOK(zwk_dec_rows(s, 1, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
+                           (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
+        HIPOK(hipEventRecord(ctx->dev_ev[1], s));
+        HIPOK(zwk_dec_rows(s, 2, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
+                           (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
+    } else {
+        HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh,
+                            ysz, csz, n, split ? nullptr : (const ZwFilterParams*)(d + o_fp)));
+        HIPOK(hipEventRecord(ctx->dev_ev[1], s));
+        if (split)
+            HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz,
+                                 n));
+    }
     HIPOK(hipEventRecord(ctx->dev_ev[2], s));
     if (dec_timing()) {
         HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
@@ -772,7 +796,9 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
                  seg_lf_level ? seg_lf_level : zero, lf_adj_enabled, ref_delta0, mode_delta0, (int)mbw, (int)mbh);
     const size_t nmb = (size_t)mbw * mbh, ysz = nmb * 256, csz = nmb * 64;
     const size_t o_fp = 0, o_fl = 256, o_y = al256(o_fl + nmb * 4), o_u = al256(o_y + ysz), o_v = al256(o_u + csz);
-    const size_t total = al256(o_v + csz);
+    const size_t o_rs = al256(o_v + csz);
+    const size_t total = al256(o_rs + zw_dec_rows_sync_bytes((int)mbh, 1));
+    const int rows_env = getenv("ZW_DEC_ROWS") ? atoi(getenv("ZW_DEC_ROWS")) : -1;  // as decode_to_device, n = 1
     HIPOK(hipSetDevice(ctx->device));
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
     if (!d) return ZW_ENOMEM;
@@ -782,7 +808,13 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipMemcpyAsync(d + o_y, y, ysz, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_u, u, csz, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_v, v, csz, hipMemcpyHostToDevice, s));
-    HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1));
+    if (rows_env != 0) {
+        HIPOK(zwk_dec_rows_init(s, (int*)(d + o_rs), (int)mbh, 1));
+        HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp),
+                           (int)mbw, (int)mbh, ysz, csz, 1, (int*)(d + o_rs), nullptr, (int)mbh));
+    } else {
+        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1));
+    }
     HIPOK(hipMemcpyAsync(y, d + o_y, ysz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(v, d + o_v, csz, hipMemcpyDeviceToHost, s));

@@ -34,6 +34,8 @@ struct DecLds {
     int dc[16];
     int res[16];
     int misc[4];
+    uint32_t twy[8], twu[2], twv[2];  // row-parallel kernel: the row above's bottom pixels around this MB
+    ZwDecQuant q[4];                  // row-parallel kernel: the frame's segment quantisers
 };
 
 __device__ __forceinline__ void dec_wait(const int* progress, int w, int need)
@@ -174,10 +176,29 @@ struct LfLds {
 // rows above come from global memory, so the caller has waited for the row
 // above to finish MB mbx+1.  Lanes write back the whole tile (the interior
 // even when the level is 0: the fused kernel has not stored it yet).
+// XCU: the rows above were written by another workgroup (any CU, any XCD), so
+// they are read with sc1 loads, and every store is an sc1 (write-through) store
+// (MI355X_MICROARCH.md, inter-workgroup hand-off, first table row).
+__device__ __forceinline__ uint32_t ld_sc1(const uint8_t* p)
+{
+    return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint8_t* p, uint32_t v)
+{
+    __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// pub() runs once the rows the MB row below reads (luma 12..15, chroma 4..7 of
+// this tile) are stored; the rest of the write-back follows it.
+template <bool XCU, class PUB>
 __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
                                         uint8_t* Vf, int ys, int cs, int mbx, int mby, int i4, int seg, int skip,
-                                        int nzd, uint32_t cy, uint32_t cc, bool write_interior_always)
+                                        int nzd, uint32_t cy, uint32_t cc, bool write_interior_always, PUB&& pub)
 {
+    auto ld = [](const uint8_t* p) -> uint32_t { return XCU ? ld_sc1(p) : *(const uint32_t*)p; };
+    auto st = [](uint8_t* p, uint32_t v) {
+        if (XCU) st_sc1(p, v);
+        else *(uint32_t*)p = v;
+    };
     const bool chroma = !F.filter_type;
     const int iy_r = lane >> 2, iy_w = lane & 3;
     const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
@@ -200,11 +221,11 @@ __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams
     if (mby > 0) {  // the 4 rows above: luma lanes 0..15 (row lane>>2), chroma lanes 32..47
         if (lane < 16) {
             const int r = lane >> 2, w = lane & 3;
-            ((uint32_t*)(L->y + r * LFY + 4))[w] = *(const uint32_t*)(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
+            ((uint32_t*)(L->y + r * LFY + 4))[w] = ld(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
         } else if (chroma && lane >= 32 && lane < 48) {
             const int t = lane - 32, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
             ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] =
-                *(const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
+                ld((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
         }
     }
     wsync();
@@ -255,23 +276,247 @@ __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams
             }
         }
     }
-    if (lvl != 0 || write_interior_always) {
-        // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame)
-        for (int t = lane; t < LFY * 5; t += 64) {
-            const int r = t / 5 - 4, w = t % 5 - 1;
-            if (y0 + r >= 0 && x0 + 4 * w >= 0)
-                *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1];
-        }
-        if (chroma) {  // (the simple filter leaves chroma alone: the caller stores it)
-            for (int t = lane; t < 2 * LFC * 3; t += 64) {
-                const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
-                if (mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
-                    *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) =
-                        ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1];
+    const bool wb = lvl != 0 || write_interior_always;
+    // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame);
+    // part 0: the rows the MB row below reads, part 1: the others
+    for (int part = 0; part < 2; part++) {
+        if (wb) {
+            for (int t = lane; t < LFY * 5; t += 64) {
+                const int r = t / 5 - 4, w = t % 5 - 1;
+                if ((r >= 12) == (part == 0) && y0 + r >= 0 && x0 + 4 * w >= 0)
+                    st(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w, ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]);
+            }
+            if (chroma) {  // (the simple filter leaves chroma alone: the caller stores it)
+                for (int t = lane; t < 2 * LFC * 3; t += 64) {
+                    const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+                    if ((r >= 4) == (part == 0) && mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
+                        st((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w,
+                           ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]);
+                }
             }
         }
+        if (part == 0) pub();
     }
     wsync();
+}
+
+// One MB row of the reconstruction (shared by the one-workgroup-per-frame
+// kernel and the row-parallel one).  wait(n): block until the row above has
+// finished n MBs; pub(n): this row has finished n MBs.  XCU: the row above may
+// run on another CU / XCD, so its bottom pixels are exchanged through the
+// global border rows gty/gtu/gtv with sc1 stores and loads; otherwise
+// gty/gtu/gtv are the workgroup's LDS border rows.
+template <bool FUSE, bool XCU, class WAIT, class PUB>
+__device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuant* __restrict__ quant, uint8_t* Y,
+                                              uint8_t* U, uint8_t* V, uint8_t* flags,
+                                              const ZwFilterParams* __restrict__ fp, int f, int mbw, int mbh,
+                                              size_t ysz, size_t csz, int mby, DecLds* W, LfLds* LF, uint8_t* gty,
+                                              uint8_t* gtu, uint8_t* gtv, WAIT&& wait, PUB&& pub)
+{
+    const int lane = threadIdx.x & 63;
+    const int ys = mbw * 16, cs = mbw * 8;
+    const size_t nmb = (size_t)mbw * mbh;
+    if (lane < 20) W->left_y[lane] = 129;
+    if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
+    wsync();
+    uint4 nxt = {0u, 0u, 0u, 0u};
+    if (lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw) * 52 + lane];
+    for (int mbx = 0; mbx < mbw; mbx++) {
+        const uint4 cur = nxt;
+        if (mbx + 1 < mbw && lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 52 + lane];
+        if (mby > 0) wait(min(mbx + 2, mbw));
+        if (XCU && mby > 0) {  // the row above's bottom pixels (written by another workgroup)
+            if (lane < 8) W->twy[lane] = ld_sc1(gty + mbx * 16 + 4 * lane);
+            else if (lane < 10) W->twu[lane - 8] = ld_sc1(gtu + mbx * 8 + 4 * (lane - 8));
+            else if (lane < 12) W->twv[lane - 10] = ld_sc1(gtv + mbx * 8 + 4 * (lane - 10));
+        }
+        const uint8_t* top_y = XCU ? (const uint8_t*)W->twy - mbx * 16 : gty;
+        const uint8_t* top_u = XCU ? (const uint8_t*)W->twu - mbx * 8 : gtu;
+        const uint8_t* top_v = XCU ? (const uint8_t*)W->twv - mbx * 8 : gtv;
+        if (lane < 52) W->rec[lane] = cur;
+        wsync();
+        const ZwDecMb& M = *(const ZwDecMb*)W->rec;
+        const ZwDecQuant& Q = quant[(XCU ? 0 : (size_t)f * 4) + M.segment];  // XCU: quant is the frame's LDS copy
+        const int lm = M.luma_mode;
+        // --- luma border (create_border_luma) ---
+        uint8_t* ws = W->ws;
+        if (lane < 32) {
+            int v;
+            if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
+            else if (mby == 0) v = 127;
+            else if (lane <= 16) v = top_y[mbx * 16 + lane - 1];
+            else if (mbx == mbw - 1) v = top_y[mbx * 16 + 15];
+            else v = top_y[mbx * 16 + lane - 1];
+            ws[lane] = (uint8_t)v;
+            if (lane >= 17 && lane < 21) ws[4 * ZW_BPS + lane] = ws[8 * ZW_BPS + lane] = ws[12 * ZW_BPS + lane] = (uint8_t)v;
+        } else if (lane < 48) {
+            ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
+        }
+        wsync();
+        int nzdct = 0;
+        if (lm != 4) {
+            // Y2 in group form: lane b holds block b's DC after the iWHT (zero when skipped)
+            const int b = lane & 15, bx = b & 3, by = b >> 2;
+            const int y2v = M.skip ? 0 : (int)M.y2[b] * (b ? Q.y2ac : Q.y2dc);
+            const int dcb = iwht_g(y2v, b);
+            // DC predictor sum: lanes 0..15 top row, 16..31 left column
+            const int above = mby != 0, left = mbx != 0;
+            int dcv;
+            {
+                const int top = lane < 16;
+                const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(lane < 32 && (top ? above : left));
+                const int sum = red16(v);
+                const int su = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
+                const int shf = 3 + above + left;
+                dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
+            }
+            int blocknz = 0;
+            if (lane < 16) {
+                int c[16];
+                c[0] = dcb;
+#pragma unroll
+                for (int k = 1; k < 16; k++) c[k] = (int)M.coeffs[b][k] * Q.yac;
+                const int nz = (M.nz_mask >> b) & 1;
+                blocknz = (c[0] != 0) || nz;
+                dec_block_residual(c, nz);
+                const int P0 = ws[0];
+                int px[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+                    const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
+                    const int p = lm == 0 ? dcv : (lm == 1 ? T : (lm == 2 ? L : clamp255(L + T - P0)));
+                    px[k] = clamp255(p + c[k]);
+                }
+                wsync();
+#pragma unroll
+                for (int k = 0; k < 16; k++) ws[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
+            } else {
+                wsync();
+            }
+            nzdct |= __any(blocknz) ? 1 : 0;
+            wsync();
+        } else {
+            // group form: lane k = coefficient k of the sub-block (all four groups alike)
+            const int k = lane & 15;
+            for (int i = 0; i < 16; i++) {
+                const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
+                dec_i4_values(W, lane, x0, y0);
+                const int c = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
+                const int nz = (M.nz_mask >> i) & 1;
+                const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
+                const int full = idct_g_exact(c, k);
+                const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
+                nzdct |= nz || c0 != 0;
+                const int v = clamp255(dec_i4_px(W, M.bpred[i], k) + r);
+                if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
+                wsync();
+            }
+        }
+        // --- chroma ---
+        if (lane < 34) {  // per plane: corner, 8 top, 8 left
+            const int pl = lane >= 17;
+            const int i = pl ? lane - 17 : lane;
+            uint8_t* w = pl ? W->cv : W->cu;
+            const uint8_t* top = pl ? top_v : top_u;
+            const uint8_t* lft = pl ? W->left_v : W->left_u;
+            if (i == 0) w[0] = mby == 0 ? 127 : (mbx == 0 ? 129 : lft[0]);
+            else if (i <= 8) w[i] = mby == 0 ? 127 : top[mbx * 8 + i - 1];
+            else w[(i - 8) * ZW_BPS] = mbx == 0 ? 129 : lft[i - 8];
+        }
+        wsync();
+        {
+            int blocknz = 0;
+            int px[16];
+            const int b = lane & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
+            uint8_t* w = pl ? W->cv : W->cu;
+            if (lane < 8) {
+                const int cm = M.chroma_mode;
+                const int above = mby != 0, left = mbx != 0;
+                int dcv = 128;
+                {
+                    uint32_t s = 0;
+                    int shf = 2;
+                    if (left) {
+                        for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
+                        shf++;
+                    }
+                    if (above) {
+                        for (int x = 1; x <= 8; x++) s += w[x];
+                        shf++;
+                    }
+                    if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
+                }
+                int c[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[16 + b][k] * (k ? Q.uvac : Q.uvdc);
+                const int nz = (M.nz_mask >> (16 + b)) & 1;
+                blocknz = (c[0] != 0) || nz;
+                dec_block_residual(c, nz);
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
+                    const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
+                    const int p = cm == 0 ? dcv : (cm == 1 ? T : (cm == 2 ? L : clamp255(L + T - w[0])));
+                    px[k] = clamp255(p + c[k]);
+                }
+            }
+            wsync();
+            if (lane < 8) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) w[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
+            }
+            nzdct |= __any(blocknz) ? 1 : 0;
+            wsync();
+        }
+        // --- borders, output ---
+        if (lane < 17) W->left_y[lane] = ws[lane * ZW_BPS + 16];
+        else if (!XCU && lane < 33) gty[mbx * 16 + lane - 17] = ws[16 * ZW_BPS + lane - 17 + 1];
+        if (lane < 9) {
+            W->left_u[lane] = W->cu[lane * ZW_BPS + 8];
+            W->left_v[lane] = W->cv[lane * ZW_BPS + 8];
+        } else if (!XCU && lane >= 40 && lane < 48) {
+            gtu[mbx * 8 + lane - 40] = W->cu[8 * ZW_BPS + lane - 40 + 1];
+            gtv[mbx * 8 + lane - 40] = W->cv[8 * ZW_BPS + lane - 40 + 1];
+        }
+        if (XCU && lane >= 48 && lane < 56) {  // bottom row for the row below: 4 + 2 + 2 words, sc1
+            const int t = lane - 48;
+            const uint8_t* src =
+                t < 4 ? ws + 16 * ZW_BPS + 1 + 4 * t : (t < 6 ? W->cu : W->cv) + 8 * ZW_BPS + 1 + 4 * (t & 1);
+            const uint32_t w =
+                (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
+            st_sc1(t < 4 ? gty + mbx * 16 + 4 * t : (t < 6 ? gtu : gtv) + mbx * 8 + 4 * (t & 1), w);
+        }
+        if (XCU) pub(mbx + 1);  // the row below needs only the border: publish before the plane stores
+        uint8_t* uo = U + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
+        uint8_t* vo = V + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
+        if (FUSE) {
+            const ZwFilterParams& F = fp[f];
+            // interior words: luma row lane>>2 word lane&3; chroma plane lane>>4, row (lane>>1)&7, word lane&1
+            const int iy_r = lane >> 2, iy_w = lane & 3;
+            const uint8_t* py = ws + (iy_r + 1) * ZW_BPS + 1 + 4 * iy_w;
+            const uint32_t cy = (uint32_t)py[0] | ((uint32_t)py[1] << 8) | ((uint32_t)py[2] << 16) | ((uint32_t)py[3] << 24);
+            const uint8_t* pc = ((lane >> 4) & 1 ? W->cv : W->cu) + (((lane >> 1) & 7) + 1) * ZW_BPS + 1 + 4 * (lane & 1);
+            const uint32_t cc = (uint32_t)pc[0] | ((uint32_t)pc[1] << 8) | ((uint32_t)pc[2] << 16) | ((uint32_t)pc[3] << 24);
+            if (F.filter_type) {  // simple filter: chroma is final as reconstructed
+                uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+                vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+            }
+            lf_tile<false>(LF, lane, F, Y + (size_t)f * ysz, U + (size_t)f * csz, V + (size_t)f * csz, ys, cs, mbx, mby,
+                    lm == 4, M.segment, M.skip, nzdct, cy, cc, true, [] {});
+        } else {
+            uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
+            for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
+            uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+            vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
+            if (lane < 4) {
+                const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
+                flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
+            }
+            wsync();
+        }
+            if (!XCU) pub(mbx + 1);
+        }
 }
 
 // FUSE: the loop filter runs in the same wavefront right after each MB's
@@ -305,194 +550,83 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WGD) top_u[i] = top_v[i] = 127;
     if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
     __syncthreads();
-    const int ys = mbw * 16, cs = mbw * 8;
-    const size_t nmb = (size_t)mbw * mbh;
     const uint4* recs = (const uint4*)mbs;  // 52 lines per record
     for (int mby = wv; mby < mbh; mby += NWD) {
-        if (lane < 20) W->left_y[lane] = 129;
-        if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
-        wsync();
-        uint4 nxt = {0u, 0u, 0u, 0u};
-        if (lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw) * 52 + lane];
-        for (int mbx = 0; mbx < mbw; mbx++) {
-            const uint4 cur = nxt;
-            if (mbx + 1 < mbw && lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 52 + lane];
-            if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            if (lane < 52) W->rec[lane] = cur;
-            wsync();
-            const ZwDecMb& M = *(const ZwDecMb*)W->rec;
-            const ZwDecQuant& Q = quant[(size_t)f * 4 + M.segment];
-            const int lm = M.luma_mode;
-            // --- luma border (create_border_luma) ---
-            uint8_t* ws = W->ws;
-            if (lane < 32) {
-                int v;
-                if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
-                else if (mby == 0) v = 127;
-                else if (lane <= 16) v = top_y[mbx * 16 + lane - 1];
-                else if (mbx == mbw - 1) v = top_y[mbx * 16 + 15];
-                else v = top_y[mbx * 16 + lane - 1];
-                ws[lane] = (uint8_t)v;
-                if (lane >= 17 && lane < 21) ws[4 * ZW_BPS + lane] = ws[8 * ZW_BPS + lane] = ws[12 * ZW_BPS + lane] = (uint8_t)v;
-            } else if (lane < 48) {
-                ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
-            }
-            wsync();
-            int nzdct = 0;
-            if (lm != 4) {
-                // Y2 in group form: lane b holds block b's DC after the iWHT (zero when skipped)
-                const int b = lane & 15, bx = b & 3, by = b >> 2;
-                const int y2v = M.skip ? 0 : (int)M.y2[b] * (b ? Q.y2ac : Q.y2dc);
-                const int dcb = iwht_g(y2v, b);
-                // DC predictor sum: lanes 0..15 top row, 16..31 left column
-                const int above = mby != 0, left = mbx != 0;
-                int dcv;
-                {
-                    const int top = lane < 16;
-                    const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(lane < 32 && (top ? above : left));
-                    const int sum = red16(v);
-                    const int su = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
-                    const int shf = 3 + above + left;
-                    dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
-                }
-                int blocknz = 0;
-                if (lane < 16) {
-                    int c[16];
-                    c[0] = dcb;
-#pragma unroll
-                    for (int k = 1; k < 16; k++) c[k] = (int)M.coeffs[b][k] * Q.yac;
-                    const int nz = (M.nz_mask >> b) & 1;
-                    blocknz = (c[0] != 0) || nz;
-                    dec_block_residual(c, nz);
-                    const int P0 = ws[0];
-                    int px[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
-                        const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
-                        const int p = lm == 0 ? dcv : (lm == 1 ? T : (lm == 2 ? L : clamp255(L + T - P0)));
-                        px[k] = clamp255(p + c[k]);
-                    }
-                    wsync();
-#pragma unroll
-                    for (int k = 0; k < 16; k++) ws[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
-                } else {
-                    wsync();
-                }
-                nzdct |= __any(blocknz) ? 1 : 0;
-                wsync();
-            } else {
-                // group form: lane k = coefficient k of the sub-block (all four groups alike)
-                const int k = lane & 15;
-                for (int i = 0; i < 16; i++) {
-                    const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
-                    dec_i4_values(W, lane, x0, y0);
-                    const int c = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
-                    const int nz = (M.nz_mask >> i) & 1;
-                    const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
-                    const int full = idct_g_exact(c, k);
-                    const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
-                    nzdct |= nz || c0 != 0;
-                    const int v = clamp255(dec_i4_px(W, M.bpred[i], k) + r);
-                    if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
-                    wsync();
-                }
-            }
-            // --- chroma ---
-            if (lane < 34) {  // per plane: corner, 8 top, 8 left
-                const int pl = lane >= 17;
-                const int i = pl ? lane - 17 : lane;
-                uint8_t* w = pl ? W->cv : W->cu;
-                const uint8_t* top = pl ? top_v : top_u;
-                const uint8_t* lft = pl ? W->left_v : W->left_u;
-                if (i == 0) w[0] = mby == 0 ? 127 : (mbx == 0 ? 129 : lft[0]);
-                else if (i <= 8) w[i] = mby == 0 ? 127 : top[mbx * 8 + i - 1];
-                else w[(i - 8) * ZW_BPS] = mbx == 0 ? 129 : lft[i - 8];
-            }
-            wsync();
-            {
-                int blocknz = 0;
-                int px[16];
-                const int b = lane & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
-                uint8_t* w = pl ? W->cv : W->cu;
-                if (lane < 8) {
-                    const int cm = M.chroma_mode;
-                    const int above = mby != 0, left = mbx != 0;
-                    int dcv = 128;
-                    {
-                        uint32_t s = 0;
-                        int shf = 2;
-                        if (left) {
-                            for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
-                            shf++;
-                        }
-                        if (above) {
-                            for (int x = 1; x <= 8; x++) s += w[x];
-                            shf++;
-                        }
-                        if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
-                    }
-                    int c[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[16 + b][k] * (k ? Q.uvac : Q.uvdc);
-                    const int nz = (M.nz_mask >> (16 + b)) & 1;
-                    blocknz = (c[0] != 0) || nz;
-                    dec_block_residual(c, nz);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
-                        const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
-                        const int p = cm == 0 ? dcv : (cm == 1 ? T : (cm == 2 ? L : clamp255(L + T - w[0])));
-                        px[k] = clamp255(p + c[k]);
-                    }
-                }
-                wsync();
-                if (lane < 8) {
-#pragma unroll
-                    for (int k = 0; k < 16; k++) w[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
-                }
-                nzdct |= __any(blocknz) ? 1 : 0;
-                wsync();
-            }
-            // --- borders, output ---
-            if (lane < 17) W->left_y[lane] = ws[lane * ZW_BPS + 16];
-            else if (lane < 33) top_y[mbx * 16 + lane - 17] = ws[16 * ZW_BPS + lane - 17 + 1];
-            if (lane < 9) {
-                W->left_u[lane] = W->cu[lane * ZW_BPS + 8];
-                W->left_v[lane] = W->cv[lane * ZW_BPS + 8];
-            } else if (lane >= 40 && lane < 48) {
-                top_u[mbx * 8 + lane - 40] = W->cu[8 * ZW_BPS + lane - 40 + 1];
-                top_v[mbx * 8 + lane - 40] = W->cv[8 * ZW_BPS + lane - 40 + 1];
-            }
-            uint8_t* uo = U + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
-            uint8_t* vo = V + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
-            if (FUSE) {
-                const ZwFilterParams& F = fp[f];
-                // interior words: luma row lane>>2 word lane&3; chroma plane lane>>4, row (lane>>1)&7, word lane&1
-                const int iy_r = lane >> 2, iy_w = lane & 3;
-                const uint8_t* py = ws + (iy_r + 1) * ZW_BPS + 1 + 4 * iy_w;
-                const uint32_t cy = (uint32_t)py[0] | ((uint32_t)py[1] << 8) | ((uint32_t)py[2] << 16) | ((uint32_t)py[3] << 24);
-                const uint8_t* pc = ((lane >> 4) & 1 ? W->cv : W->cu) + (((lane >> 1) & 7) + 1) * ZW_BPS + 1 + 4 * (lane & 1);
-                const uint32_t cc = (uint32_t)pc[0] | ((uint32_t)pc[1] << 8) | ((uint32_t)pc[2] << 16) | ((uint32_t)pc[3] << 24);
-                if (F.filter_type) {  // simple filter: chroma is final as reconstructed
-                    uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-                    vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-                }
-                lf_tile(LF, lane, F, Y + (size_t)f * ysz, U + (size_t)f * csz, V + (size_t)f * csz, ys, cs, mbx, mby,
-                        lm == 4, M.segment, M.skip, nzdct, cy, cc, true);
-            } else {
-                uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
-                for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
-                uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-                vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-                if (lane < 4) {
-                    const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
-                    flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
-                }
-                wsync();
-            }
-            dec_publish(progress, wv, mby * 65536 + mbx + 1);
+        dec_recon_row<FUSE, false>(
+            recs, quant, Y, U, V, flags, fp, f, mbw, mbh, ysz, csz, mby, W, LF, top_y, top_u, top_v,
+            [&](int need) { dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + need); },
+            [&](int done) { dec_publish(progress, wv, mby * 65536 + done); });
+    }
+}
+
+// Row-parallel reconstruction: one wave per workgroup, rows handed out by a
+// per-frame ticket (a wave only ever waits for a row whose ticket an already
+// running wave holds, so the grid cannot deadlock whatever the residency), the
+// row-to-row hand-off through global memory (progress flags and the bottom
+// pixel rows, sc1 both ways).  For one frame or a few, this spreads the x+2y
+// wavefront over up to mbh CUs instead of one.
+#define ZW_SPIN_MAX (1 << 22)
+__device__ __forceinline__ int row_ticket(int* ticket)
+{
+    int t = 0;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(ticket, 1);
+    return __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+}
+// Wait until *prog >= need.  seen caches the last value read: the row above
+// usually runs ahead, so most waits cost no memory round trip.
+__device__ __forceinline__ void row_wait(const int* prog, int need, int* err, int& seen)
+{
+    if (seen >= need) return;
+    int it = 0;
+    for (;;) {
+        seen = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (seen >= need) break;
+        __builtin_amdgcn_s_sleep(2);
+        // never expected: after ZW_SPIN_MAX polls (or once any wave of the frame
+        // gave up) report through *err instead of hanging the GPU
+        if (++it > ZW_SPIN_MAX || ((it & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            if ((threadIdx.x & 63) == 0) atomicOr(err, 1);
+            seen = 1 << 30;
+            break;
         }
+    }
+}
+__device__ __forceinline__ void row_publish(int* prog, int val)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are out
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(prog, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// rowsync per frame: [0] recon ticket, [1] filter ticket, [2] error, [3] pad,
+// then progress[2][mbh] (recon, filter), initialised to -1.
+__device__ __forceinline__ int* rs_frame(int* rowsync, int f, int mbh) { return rowsync + (size_t)f * (4 + 2 * mbh); }
+
+__global__ __launch_bounds__(64) void k_dec_recon_rows(const ZwDecMb* __restrict__ mbs,
+                                                       const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
+                                                       uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
+                                                       size_t csz, int* rowsync, uint8_t* borders)
+{
+    __shared__ __attribute__((aligned(16))) DecLds Wl;
+    DecLds* W = &Wl;
+    const int f = blockIdx.y, lane = threadIdx.x;
+    for (int i = lane; i < 160; i += 64) (&W->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
+    if (lane < 24) ((int32_t*)W->q)[lane] = ((const int32_t*)(quant + (size_t)f * 4))[lane];
+    int* rs = rs_frame(rowsync, f, mbh);
+    int* prog = rs + 4;
+    const size_t bsz = (size_t)mbw * 16 + 48 + 2 * ((size_t)mbw * 8 + 48);
+    uint8_t* gty = borders + (size_t)f * bsz;
+    uint8_t* gtu = gty + (size_t)mbw * 16 + 48;
+    uint8_t* gtv = gtu + (size_t)mbw * 8 + 48;
+    wsync();
+    for (;;) {
+        const int mby = row_ticket(&rs[0]);
+        if (mby >= mbh) break;
+        int seen = -1;
+        dec_recon_row<false, true>(
+            (const uint4*)mbs, W->q, Y, U, V, flags, nullptr, f, mbw, mbh, ysz, csz, mby, W, nullptr, gty, gtu, gtv,
+            [&](int need) { row_wait(&prog[mby - 1], need, &rs[2], seen); },
+            [&](int done) { row_publish(&prog[mby], done); });
     }
 }
 
@@ -535,11 +669,95 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
                 nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 4);
             }
             if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            lf_tile(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255, (fl >> 16) & 255,
-                    fl >> 24, cy, cc, false);
+            lf_tile<false>(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255,
+                           (fl >> 16) & 255, fl >> 24, cy, cc, false, [] {});
             dec_publish(progress, wv, mby * 65536 + mbx + 1);
         }
     }
+}
+
+// Row-parallel loop filter (see k_dec_recon_rows): every load and store of
+// pixels another row hands over is sc1, including this row's own interior
+// loads (MI355X_MICROARCH.md: every load of handed-off bytes must be one).
+__global__ __launch_bounds__(64) void k_loopfilter_rows(uint8_t* Y, uint8_t* U, uint8_t* V,
+                                                        const uint8_t* __restrict__ flags,
+                                                        const ZwFilterParams* __restrict__ fp, size_t ysz, size_t csz,
+                                                        int* rowsync)
+{
+    __shared__ __attribute__((aligned(16))) LfLds Ll;
+    LfLds* L = &Ll;
+    const int f = blockIdx.y, lane = threadIdx.x;
+    const ZwFilterParams& F = fp[f];
+    const int mbw = F.mbw, mbh = F.mbh, ys = mbw * 16, cs = mbw * 8;
+    const size_t nmb = (size_t)mbw * mbh;
+    int* rs = rs_frame(rowsync, f, mbh);
+    int* prog = rs + 4 + mbh;
+    uint8_t* Yf = Y + (size_t)f * ysz;
+    uint8_t* Uf = U + (size_t)f * csz;
+    uint8_t* Vf = V + (size_t)f * csz;
+    const bool chroma = !F.filter_type;
+    const int iy_r = lane >> 2, iy_w = lane & 3;
+    const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
+    auto load_interior = [&](int mby, int mbx, uint32_t& py, uint32_t& pc) {
+        py = ld_sc1(Yf + (size_t)(mby * 16 + iy_r) * ys + mbx * 16 + 4 * iy_w);
+        pc = 0;
+        if (chroma && lane < 32) pc = ld_sc1((ic_p ? Vf : Uf) + (size_t)(mby * 8 + ic_r) * cs + mbx * 8 + 4 * ic_w);
+    };
+    for (;;) {
+        const int mby = row_ticket(&rs[1]);
+        if (mby >= mbh) break;
+        uint32_t ny, nc;
+        load_interior(mby, 0, ny, nc);
+        uint32_t nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw) * 4);
+        int seen = -1;
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            const uint32_t cy = ny, cc = nc, fl = nfl;
+            if (mbx + 1 < mbw) {
+                load_interior(mby, mbx + 1, ny, nc);
+                nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 4);
+            }
+            if (mby > 0) row_wait(&prog[mby - 1], min(mbx + 2, mbw), &rs[2], seen);
+            lf_tile<true>(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255,
+                          (fl >> 16) & 255, fl >> 24, cy, cc, false, [&] { row_publish(&prog[mby], mbx + 1); });
+        }
+    }
+}
+
+// Row-parallel path scratch: rowsync ints and border rows for nframes frames.
+extern "C" size_t zw_dec_rows_sync_bytes(int mbh, int nframes) { return (size_t)nframes * (4 + 2 * mbh) * 4; }
+extern "C" size_t zw_dec_rows_border_bytes(int mbw, int nframes)
+{
+    return (size_t)nframes * ((size_t)mbw * 16 + 48 + 2 * ((size_t)mbw * 8 + 48));
+}
+
+// rowsync must hold zeros in [0..3] and -1 in the progress words of every
+// frame (zw_dec_rows_sync_init); rows = workgroups (waves) per frame.
+// phase 1: reconstruction, 2: loop filter.
+extern "C" hipError_t zwk_dec_rows(hipStream_t s, int phase, const ZwDecMb* mbs, const void* quant, uint8_t* Y,
+                                   uint8_t* U, uint8_t* V, uint8_t* flags, const ZwFilterParams* fp, int mbw, int mbh,
+                                   size_t ysz, size_t csz, int nframes, int* rowsync, uint8_t* borders, int rows)
+{
+    const int R = rows < 1 ? 1 : (rows > mbh ? mbh : rows);
+    if (phase == 1)
+        hipLaunchKernelGGL(k_dec_recon_rows, dim3(R, nframes), dim3(64), 0, s, mbs, (const ZwDecQuant*)quant, Y, U,
+                           V, flags, mbw, mbh, ysz, csz, rowsync, borders);
+    else
+        hipLaunchKernelGGL(k_loopfilter_rows, dim3(R, nframes), dim3(64), 0, s, Y, U, V, flags, fp, ysz, csz,
+                           rowsync);
+    return hipGetLastError();
+}
+
+// Sets the rowsync words: tickets / error 0, progress -1.
+__global__ void k_dec_rows_init(int* rowsync, int mbh, int total)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < total) rowsync[i] = (i % (4 + 2 * mbh)) < 4 ? 0 : -1;
+}
+extern "C" hipError_t zwk_dec_rows_init(hipStream_t s, int* rowsync, int mbh, int nframes)
+{
+    const int total = nframes * (4 + 2 * mbh);
+    hipLaunchKernelGGL(k_dec_rows_init, dim3((total + 255) / 256), dim3(256), 0, s, rowsync, mbh, total);
+    return hipGetLastError();
 }
 
 extern "C" size_t zw_dec_lds_bytes(int mbw)

@@ -278,6 +278,21 @@ def test_decode_batch(ctx):
         assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"])
 
 
+@pytest.mark.parametrize("rows", ["1", "0"])
+def test_decode_rows_and_frame_kernels(ctx, monkeypatch, rows):
+    """Both reconstruction / loop-filter kernel families on the same 1080p streams
+    (ZW_DEC_ROWS=1: one wave per MB row spread over the CUs, rows handed over
+    through global memory; 0: one workgroup per frame) equal the oracle."""
+    monkeypatch.setenv("ZW_DEC_ROWS", rows)
+    w, h = 1920, 1080
+    streams = [O.encode(synth_rgba(w, h, 0x5EED3000 + i, "natural" if i else "noise"), w, h, 3, q, 4)[1]
+               for i, q in enumerate((20, 75, 95))]
+    frames = zwebp.decode_batch(streams, ctx=ctx)
+    for s, fr in zip(streams, frames):
+        rc, r = O.decode(s)
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+
+
 def test_decode_errors(ctx):
     vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
     bad = bytearray(vp8)
@@ -293,7 +308,10 @@ def test_decode_errors(ctx):
 
 @pytest.mark.parametrize("ftype,level,sharp,seg", [(0, 6, 0, 0), (0, 40, 3, 1), (1, 20, 0, 0), (0, 63, 7, 1),
                                                    (1, 63, 5, 1), (0, 15, 1, 0)])
-def test_loop_filter_frame(ctx, ftype, level, sharp, seg):
+@pytest.mark.parametrize("rows", ["1", "0"])
+def test_loop_filter_frame(ctx, monkeypatch, ftype, level, sharp, seg, rows):
+    """rows=1: the row-parallel kernel (one wave per MB row, cross-CU hand-off); 0: one workgroup per frame."""
+    monkeypatch.setenv("ZW_DEC_ROWS", rows)
     rng = np.random.default_rng(level * 10 + sharp)
     mbw, mbh = 23, 17
     nmb = mbw * mbh
