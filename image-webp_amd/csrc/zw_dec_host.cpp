@@ -475,6 +475,7 @@ extern "C" void zw_frame_free(zw_frame* f)
 // Decoded planes of a batch, resident in the context's device scratch.
 struct DecBatch {
     std::vector<DecFrame> F;
+    hipEvent_t* ev = nullptr;  // [0] expand done / recon start, [1] recon done, [2] filter done, [3] caller's
     uint8_t* d = nullptr;  // device scratch base
     size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
     int mbw = 0, mbh = 0;
@@ -491,8 +492,10 @@ static double dec_now_ms()
 }
 static bool dec_timing() { static const bool on = getenv("ZW_DEC_TIMING") != nullptr; return on; }
 
+// bi: which of the context's two staging / scratch / event sets (the
+// pipelined batches alternate between them).
 static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
-                            size_t extra_bytes, DecBatch& B)
+                            size_t extra_bytes, DecBatch& B, int bi = 0)
 {
     const double t0 = dec_now_ms();
     B.F.assign(n, DecFrame());
@@ -514,7 +517,7 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     const size_t off_bytes = (size_t)n * (nmb + 1) * 4, base_bytes = (size_t)n * 8;
     const size_t o_moff = (size_t)n * slot, o_base = o_moff + al256(off_bytes);
     const size_t up_bytes = o_base + base_bytes;
-    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, 0, up_bytes);
+    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, bi ? 2 : 0, up_bytes);
     if (!stage) return ZW_ENOMEM;
     uint32_t* moff = (uint32_t*)(stage + o_moff);
     std::vector<DecQuant> quant((size_t)n * 4);
@@ -552,9 +555,11 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     const size_t o_bd = al256(o_rs + (rows ? zw_dec_rows_sync_bytes(mbh, n) : 0));
     const size_t o_extra = al256(o_bd + (rows ? zw_dec_rows_border_bytes(mbw, n) : 0));
     const size_t total = al256(o_extra + extra_bytes);
-    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total, bi);
     if (!d) return ZW_ENOMEM;
     hipStream_t s = ctx_stream(ctx);
+    hipEvent_t* ev = bi ? ctx->dev_ev1 : ctx->dev_ev;
+    B.ev = ev;
     for (int i = 0; i < n; i++)  // each frame's used prefix
         HIPOK(hipMemcpyAsync(d + o_mbs + (size_t)i * slot, stage + (size_t)i * slot, moff[(size_t)i * (nmb + 1) + nmb],
                              hipMemcpyHostToDevice, s));
@@ -562,8 +567,8 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
     for (int e = 0; e < 4; e++)
-        if (!ctx->dev_ev[e]) HIPOK(hipEventCreate(&ctx->dev_ev[e]));
-    HIPOK(hipEventRecord(ctx->dev_ev[0], s));
+        if (!ev[e]) HIPOK(hipEventCreate(&ev[e]));
+    HIPOK(hipEventRecord(ev[0], s));
     HIPOK(zwk_dec_expand(s, d + o_mbs, (const uint32_t*)(d + o_mbs + o_moff), (const uint64_t*)(d + o_mbs + o_base),
                          (ZwDecMb*)(d + o_full), (int)nmb, n));
     // two wavefront kernels (ZW_DEC_FUSE=1: one fused wavefront; measured slower on
@@ -574,20 +579,20 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
         HIPOK(zwk_dec_rows_init(s, rs, mbh, n));
         HIPOK(zwk_dec_rows(s, 1, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
-        HIPOK(hipEventRecord(ctx->dev_ev[1], s));
+        HIPOK(hipEventRecord(ev[1], s));
         HIPOK(zwk_dec_rows(s, 2, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
     } else {
         HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh,
                             ysz, csz, n, split ? nullptr : (const ZwFilterParams*)(d + o_fp)));
-        HIPOK(hipEventRecord(ctx->dev_ev[1], s));
+        HIPOK(hipEventRecord(ev[1], s));
         if (split)
             HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz,
                                  n));
     }
-    HIPOK(hipEventRecord(ctx->dev_ev[2], s));
+    HIPOK(hipEventRecord(ev[2], s));
     if (dec_timing()) {
-        HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
+        HIPOK(hipEventSynchronize(ev[2]));
         fprintf(stderr, "[dec] n=%d parse %.2f ms, upload+kernels %.2f ms (records %.1f MB)\n", n, t1 - t0,
                 dec_now_ms() - t1, rec_bytes / 1e6);
     }
@@ -603,64 +608,113 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     return ZW_OK;
 }
 
+// Frames per pipelined chunk: chunk c+1 is parsed on the host while chunk c
+// runs on the device, and chunk c is downloaded and fanned out while chunk c+1
+// runs.  ZW_DEC_CHUNK overrides.
+static int dec_chunk_frames()
+{
+    const char* e = getenv("ZW_DEC_CHUNK");
+    const int c = e ? atoi(e) : 128;  // measured on 256 1080p frames: 32 / 64 / 128 / 256 -> 3198 / 3559 / 3771 / 3267 per s
+    return c > 0 ? c : 128;
+}
+
+// Runs the batch through decode_to_device in chunks, alternating the two buffer
+// sets.  enqueue(B, first, count) queues caller work after the filter (or does
+// nothing); finish(B, first, count) waits for it, downloads and fans out.  Device
+// times of all chunks add up in ctx->dec_ms.
+template <class ENQ, class FIN>
+static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, size_t extra_per_frame,
+                        ENQ&& enqueue, FIN&& finish)
+{
+    const int C = dec_chunk_frames(), nch = (n + C - 1) / C;
+    DecBatch B[2];
+    ctx->dec_ms[0] = ctx->dec_ms[1] = ctx->dec_ms[2] = 0.f;
+    auto first = [&](int c) { return c * C; };
+    auto count = [&](int c) { return std::min(C, n - c * C); };
+    int err = ZW_OK;
+    for (int c = 0; c <= nch && !err; c++) {
+        if (c < nch) {
+            DecBatch& b = B[c & 1];
+            err = decode_to_device(ctx, count(c), data + first(c), lens + first(c), extra_per_frame * count(c), b,
+                                   c & 1);
+            if (!err) err = enqueue(b, first(c), count(c));
+        }
+        if (c >= 1 && !err) {
+            DecBatch& b = B[(c - 1) & 1];
+            err = finish(b, first(c - 1), count(c - 1));
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, b.ev[0], b.ev[1]) == hipSuccess) ctx->dec_ms[0] += ms;
+            if (hipEventElapsedTime(&ms, b.ev[1], b.ev[2]) == hipSuccess) ctx->dec_ms[1] += ms;
+        }
+    }
+    if (err) (void)hipStreamSynchronize(ctx_stream(ctx));  // nothing queued may outlive the call
+    return err;
+}
+
 extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
 {
     if (!ctx || n <= 0 || !data || !lens || !outs) return ZW_EINVAL;
     for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
-    DecBatch B;
-    int r0 = decode_to_device(ctx, n, data, lens, 0, B);
-    if (r0) return r0;
-    const std::vector<DecFrame>& F = B.F;
-    const size_t ysz = B.ysz, csz = B.csz;
-    uint8_t* d = B.d;
-    // planes down through pinned staging (one DMA per plane set), then fanned out
-    const size_t fsz = ysz + 2 * csz;
-    uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fsz);
-    if (!hout) return ZW_ENOMEM;
-    HIPOK(hipEventSynchronize(ctx->dev_ev[2]));
-    const double td = dec_now_ms();
-    {
-        int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)n * ysz);
-        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * ysz, d + B.o_u, (size_t)n * csz);
-        if (!r) r = ctx_d2h(ctx, hout + (size_t)n * (ysz + csz), d + B.o_v, (size_t)n * csz);
-        if (r) return r;
-    }
-    std::vector<int> oom(n, 0);
-    parallel_for(n, [&](int i) {
-        uint8_t* buf = (uint8_t*)malloc(fsz);
-        if (!buf) {
-            oom[i] = 1;
-            return;
+    int mbw0 = -1, mbh0 = -1;
+    auto enqueue = [&](DecBatch& B, int, int) -> int {
+        if (mbw0 < 0) mbw0 = B.mbw, mbh0 = B.mbh;
+        return B.mbw == mbw0 && B.mbh == mbh0 ? ZW_OK : ZW_EINVAL;  // one size per batch, as in one chunk
+    };
+    auto finish = [&](DecBatch& B, int f0, int cn) -> int {
+        const std::vector<DecFrame>& F = B.F;
+        const size_t ysz = B.ysz, csz = B.csz;
+        uint8_t* d = B.d;
+        // planes down through pinned staging (one DMA per plane set), then fanned out
+        const size_t fsz = ysz + 2 * csz;
+        uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fsz);
+        if (!hout) return ZW_ENOMEM;
+        HIPOK(hipEventSynchronize(B.ev[2]));
+        const double td = dec_now_ms();
+        {
+            int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)cn * ysz);
+            if (!r) r = ctx_d2h(ctx, hout + (size_t)cn * ysz, d + B.o_u, (size_t)cn * csz);
+            if (!r) r = ctx_d2h(ctx, hout + (size_t)cn * (ysz + csz), d + B.o_v, (size_t)cn * csz);
+            if (r) return r;
         }
-        memcpy(buf, hout + (size_t)i * ysz, ysz);
-        memcpy(buf + ysz, hout + (size_t)n * ysz + (size_t)i * csz, csz);
-        memcpy(buf + ysz + csz, hout + (size_t)n * (ysz + csz) + (size_t)i * csz, csz);
-        outs[i].y = buf;
-    });
-    if (dec_timing()) fprintf(stderr, "[dec] download+fanout %.2f ms\n", dec_now_ms() - td);
-    for (int i = 0; i < n; i++) {
-        if (oom[i]) {
-            for (int k = 0; k < n; k++) zw_frame_free(&outs[k]);
-            return ZW_ENOMEM;
+        std::vector<int> oom(cn, 0);
+        parallel_for(cn, [&](int i) {
+            uint8_t* buf = (uint8_t*)malloc(fsz);
+            if (!buf) {
+                oom[i] = 1;
+                return;
+            }
+            memcpy(buf, hout + (size_t)i * ysz, ysz);
+            memcpy(buf + ysz, hout + (size_t)cn * ysz + (size_t)i * csz, csz);
+            memcpy(buf + ysz + csz, hout + (size_t)cn * (ysz + csz) + (size_t)i * csz, csz);
+            outs[f0 + i].y = buf;
+        });
+        if (dec_timing()) fprintf(stderr, "[dec] download+fanout %.2f ms\n", dec_now_ms() - td);
+        int r = ZW_OK;
+        for (int i = 0; i < cn; i++) {
+            zw_frame& o = outs[f0 + i];
+            if (oom[i]) {
+                r = ZW_ENOMEM;
+                continue;
+            }
+            uint8_t* buf = o.y;
+            o.width = (uint16_t)F[i].width;
+            o.height = (uint16_t)F[i].height;
+            o.y_stride = (uint32_t)B.mbw * 16;
+            o.uv_stride = (uint32_t)B.mbw * 8;
+            o.mb_rows = (uint32_t)B.mbh;
+            o.y = buf;
+            o.u = buf + ysz;
+            o.v = buf + ysz + csz;
+            o.filter_type = (uint8_t)F[i].filter_type;
+            o.filter_level = (uint8_t)F[i].filter_level;
+            o.sharpness_level = (uint8_t)F[i].sharpness;
         }
-        uint8_t* buf = outs[i].y;
-        zw_frame& o = outs[i];
-        o.width = (uint16_t)F[i].width;
-        o.height = (uint16_t)F[i].height;
-        o.y_stride = (uint32_t)B.mbw * 16;
-        o.uv_stride = (uint32_t)B.mbw * 8;
-        o.mb_rows = (uint32_t)B.mbh;
-        o.y = buf;
-        o.u = buf + ysz;
-        o.v = buf + ysz + csz;
-        o.filter_type = (uint8_t)F[i].filter_type;
-        o.filter_level = (uint8_t)F[i].filter_level;
-        o.sharpness_level = (uint8_t)F[i].sharpness;
-    }
-    (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
-    (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
-    ctx->dec_ms[2] = 0.f;
-    return ZW_OK;
+        return r;
+    };
+    const int r = dec_pipeline(ctx, n, data, lens, 0, enqueue, finish);
+    if (r)
+        for (int k = 0; k < n; k++) zw_frame_free(&outs[k]);
+    return r;
 }
 
 // Frame::fill_rgb / fill_rgba (decoder/vp8.rs:200-258) after decode_frame, on
@@ -683,43 +737,46 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
         h = f0.height;
     }
     const size_t fbytes = w * h * (size_t)bpp;
-    DecBatch B;
-    int r0 = decode_to_device(ctx, n, data, lens, (size_t)n * fbytes, B);
-    if (r0) return r0;
-    for (int i = 0; i < n; i++)
-        if ((size_t)B.F[i].width != w || (size_t)B.F[i].height != h) return ZW_EINVAL;
     hipStream_t s = ctx_stream(ctx);
-    uint8_t* drgb = B.d + B.o_extra;
-    HIPOK(zwk_yuv2rgb(s, B.d + B.o_y, B.d + B.o_u, B.d + B.o_v, B.ysz, B.csz, (int)w, (int)h, B.mbw * 16, B.mbw * 8,
-                      bpp, upsampling == ZW_UPSAMPLE_BILINEAR, drgb, n));
-    HIPOK(hipEventRecord(ctx->dev_ev[3], s));
-    uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)n * fbytes);
-    if (!hout) return ZW_ENOMEM;
-    HIPOK(hipEventSynchronize(ctx->dev_ev[3]));
-    if (int r = ctx_d2h(ctx, hout, drgb, (size_t)n * fbytes)) return r;
-    std::vector<int> oom(n, 0);
-    parallel_for(n, [&](int i) {
-        uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
-        if (!buf) {
-            oom[i] = 1;
-            return;
-        }
-        memcpy(buf, hout + (size_t)i * fbytes, fbytes);
-        outs[i].data = buf;
-        outs[i].len = fbytes;
-    });
-    for (int i = 0; i < n; i++)
-        if (oom[i]) {
-            for (int k = 0; k < n; k++) zw_bytes_free(&outs[k]);
-            return ZW_ENOMEM;
-        }
+    auto enqueue = [&](DecBatch& B, int, int cn) -> int {
+        for (int i = 0; i < cn; i++)
+            if ((size_t)B.F[i].width != w || (size_t)B.F[i].height != h) return ZW_EINVAL;
+        HIPOK(zwk_yuv2rgb(s, B.d + B.o_y, B.d + B.o_u, B.d + B.o_v, B.ysz, B.csz, (int)w, (int)h, B.mbw * 16,
+                          B.mbw * 8, bpp, upsampling == ZW_UPSAMPLE_BILINEAR, B.d + B.o_extra, cn));
+        HIPOK(hipEventRecord(B.ev[3], s));
+        return ZW_OK;
+    };
+    auto finish = [&](DecBatch& B, int f0, int cn) -> int {
+        uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fbytes);
+        if (!hout) return ZW_ENOMEM;
+        HIPOK(hipEventSynchronize(B.ev[3]));
+        if (int r = ctx_d2h(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
+        std::vector<int> oom(cn, 0);
+        parallel_for(cn, [&](int i) {
+            uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
+            if (!buf) {
+                oom[i] = 1;
+                return;
+            }
+            memcpy(buf, hout + (size_t)i * fbytes, fbytes);
+            outs[f0 + i].data = buf;
+            outs[f0 + i].len = fbytes;
+        });
+        for (int i = 0; i < cn; i++)
+            if (oom[i]) return ZW_ENOMEM;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, B.ev[2], B.ev[3]) == hipSuccess) ctx->dec_ms[2] += ms;
+        return ZW_OK;
+    };
+    const int r = dec_pipeline(ctx, n, data, lens, fbytes, enqueue, finish);
+    if (r) {
+        for (int k = 0; k < n; k++) zw_bytes_free(&outs[k]);
+        return r;
+    }
     for (int i = 0; i < n; i++) {
         if (widths) widths[i] = (uint32_t)w;
         if (heights) heights[i] = (uint32_t)h;
     }
-    (void)hipEventElapsedTime(&ctx->dec_ms[0], ctx->dev_ev[0], ctx->dev_ev[1]);
-    (void)hipEventElapsedTime(&ctx->dec_ms[1], ctx->dev_ev[1], ctx->dev_ev[2]);
-    (void)hipEventElapsedTime(&ctx->dec_ms[2], ctx->dev_ev[2], ctx->dev_ev[3]);
     return ZW_OK;
 }
 

@@ -156,7 +156,10 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->dscratch) (void)hipFree(c->dscratch);
+    if (c->dscratch1) (void)hipFree(c->dscratch1);
     for (hipEvent_t e : c->dev_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->dev_ev1)
         if (e) (void)hipEventDestroy(e);
     for (void* h : c->hpin)
         if (h) (void)hipHostFree(h);

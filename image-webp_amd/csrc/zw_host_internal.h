@@ -16,17 +16,21 @@ struct zw_ctx {
     // grow-only device scratch for the single-call decode / filter entry points
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
+    void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
+    size_t dscratch1_cap = 0;
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
     // D2H runs as a blit kernel, which cannot be dispatched while an encode
     // kernel holds every CU; the DMA engines need no CU.
     int sdma = -1;  // -1 unprobed, 0 unavailable, 1 ready
     hsa_agent_t gpu_agent{}, cpu_agent{};
     // grow-only pinned host staging (decode batch: MB records up, planes down)
-    void* hpin[2] = {nullptr, nullptr};
-    size_t hpin_cap[2] = {0, 0};
+    // [0] / [2]: the two upload buffers of the pipelined decode, [1] downloads
+    void* hpin[3] = {nullptr, nullptr, nullptr};
+    size_t hpin_cap[3] = {0, 0, 0};
     // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter,
     // [2] k_yuv2rgb (0 when the batch returned planes) (ms)
     hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t dev_ev1[4] = {nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
 };
 
@@ -74,17 +78,19 @@ static inline void parallel_for(int n, F fn)
 }
 
 
-// Device scratch of at least `bytes` owned by the context.
-static inline void* ctx_scratch(zw_ctx* c, size_t bytes)
+// Device scratch `which` (0 or 1) of at least `bytes` owned by the context.
+static inline void* ctx_scratch(zw_ctx* c, size_t bytes, int which = 0)
 {
-    if (c->dscratch_cap < bytes) {
-        if (c->dscratch) (void)hipFree(c->dscratch);
-        c->dscratch = nullptr;
-        c->dscratch_cap = 0;
-        if (hipMalloc(&c->dscratch, bytes) != hipSuccess) return nullptr;
-        c->dscratch_cap = bytes;
+    void*& p = which ? c->dscratch1 : c->dscratch;
+    size_t& cap = which ? c->dscratch1_cap : c->dscratch_cap;
+    if (cap < bytes) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        cap = bytes;
     }
-    return c->dscratch;
+    return p;
 }
 
 // The context's own stream (single-call entry points); created lazily so a
