@@ -192,27 +192,34 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
             int o[16];
             fdct16_pk(d, o);
             const int hidx = luma ? mode : 2 + mode;
+            // bin 0 holds most coefficients: count it in the lane, add the rest
+            // with (far less contended) LDS atomics
+            uint32_t z = 0;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const int v = min(iabs(o[k]) >> 3, 31);
-                atomicAdd(&hist[wv][hidx][v], 1u);
+                if (v == 0) z++;
+                else atomicAdd(&hist[wv][hidx][v], 1u);
             }
+            if (z) atomicAdd(&hist[wv][hidx][0], z);
         }
         wsync();
-        int a = 0;
-        if (lane < 4) {
-            uint32_t mx = 0;
-            int lnz = 1;
-            for (int k = 0; k < 32; k++) {
-                uint32_t c = hist[wv][lane][k];
-                if (c > 0) {
-                    if (c > mx) mx = c;
-                    lnz = k;
-                }
-            }
-            a = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
+        // per histogram: max count and last non-empty bin (get_alpha,
+        // analysis.rs:160), two histograms per pass, lane = (histogram, bin)
+        int av[4];
+#pragma unroll
+        for (int ps = 0; ps < 2; ps++) {
+            const uint32_t c = hist[wv][2 * ps + (lane >> 5)][lane & 31];
+            uint32_t mx = c;
+#pragma unroll
+            for (int o2 = 16; o2 >= 1; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o2));
+            const uint32_t half = (uint32_t)(__ballot(c > 0) >> (lane & 32));
+            const int lnz = half ? 31 - __clz((int)half) : 1;
+            const int ah = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
+            av[2 * ps] = __builtin_amdgcn_readlane(ah, 0);
+            av[2 * ps + 1] = __builtin_amdgcn_readlane(ah, 32);
         }
-        const int a0 = __shfl(a, 0), a1 = __shfl(a, 1), a2 = __shfl(a, 2), a3 = __shfl(a, 3);
+        const int a0 = av[0], a1 = av[1], a2 = av[2], a3 = av[3];
         if (lane == 0) {
             int best = max(-1, max(a0, a1));
             int buv = max(-1, max(a2, a3));
