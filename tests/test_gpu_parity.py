@@ -278,6 +278,36 @@ def test_decode_batch(ctx):
         assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"])
 
 
+@pytest.mark.parametrize("chunk", ["1", "2", "4"])
+def test_decode_batch_chunked(ctx, monkeypatch, chunk):
+    """The double-buffered chunk pipeline (ZW_DEC_CHUNK frames per chunk; the
+    host parses chunk c+1 while chunk c runs): several chunks, a ragged last
+    chunk, both buffer sets reused, every frame equal to the oracle."""
+    monkeypatch.setenv("ZW_DEC_CHUNK", chunk)
+    w, h = 160, 112
+    streams = [O.encode(synth_rgba(w, h, 0x5EED4000 + i, ("natural", "noise", "flat")[i % 3]), w, h, 3,
+                        20 + 15 * i, 4)[1] for i in range(5)]
+    frames = zwebp.decode_batch(streams, ctx=ctx)
+    assert len(frames) == len(streams)
+    for s, fr in zip(streams, frames):
+        rc, r = O.decode(s)
+        assert rc == 0
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+
+
+def test_decode_batch_chunked_size_mismatch(ctx, monkeypatch):
+    """A batch holds one frame size: a second size in a later chunk is an error
+    (after the first chunk already ran), and the context stays usable."""
+    monkeypatch.setenv("ZW_DEC_CHUNK", "2")
+    a = O.encode(synth_rgba(64, 48, 1), 64, 48, 3, 75, 4)[1]
+    b = O.encode(synth_rgba(96, 48, 2), 96, 48, 3, 75, 4)[1]
+    with pytest.raises(zwebp.ZwError):
+        zwebp.decode_batch([a, a, b], ctx=ctx)
+    fr = zwebp.decode_batch([a, a, a], ctx=ctx)
+    rc, r = O.decode(a)
+    assert all(np.array_equal(f.ybuf, r["y"]) for f in fr)
+
+
 @pytest.mark.parametrize("rows", ["1", "0"])
 def test_decode_rows_and_frame_kernels(ctx, monkeypatch, rows):
     """Both reconstruction / loop-filter kernel families on the same 1080p streams

@@ -115,7 +115,11 @@ def test_decode_rgb_matches_oracle(ctx, entry):
             assert np.array_equal(got.reshape(-1), exp), (bpp, up)
 
 
-def test_decode_rgb_batch(ctx):
+@pytest.mark.parametrize("chunk", [None, "2"])
+def test_decode_rgb_batch(ctx, monkeypatch, chunk):
+    """chunk "2": the double-buffered chunk pipeline over 3 chunks (ragged last)."""
+    if chunk:
+        monkeypatch.setenv("ZW_DEC_CHUNK", chunk)
     w, h = 161, 97
     streams = [O.encode(synth_rgba(w, h, 0x5EED0000 + i), w, h, 3, 20 + 15 * i, 4)[1] for i in range(5)]
     imgs = zwebp.decode_rgb_batch(streams, 4, BIL, ctx=ctx)
