@@ -2,33 +2,48 @@
 """Benchmark: 1080p lossy VP8 encodes/s at Q75 method 4 (BASELINE.json metric).
 
 One step = one full encode of a batch of `--frames` synthetic 1920x1080 RGBA
-frames already resident in HBM: rgb->yuv, analysis, segments, pass 1, host
-statistics/probabilities, pass 2 (mode search + DCT/quant/trellis + recon) and
-host token emission to finished VP8 bitstreams.  value = frames encoded by all
-ranks / max-over-ranks wall time of the K timed steps.  The K steps run as a
-stream (Pipeline.encode_repeat): step k+1's GPU passes are queued before step
-k's host token emission, as a serving deployment would run consecutive
-batches; every step's bitstreams are complete inside the timed region.
---sequential times K independent encode() calls instead.
+frames already resident in HBM: rgb->yuv, analysis, segments, pass 1, device
+statistics + host probabilities, pass 2 (mode search + DCT/quant/trellis +
+recon) and host token emission to finished VP8 bitstreams.  value = frames
+encoded by all ranks / max-over-ranks wall time of the K timed steps.  The K
+steps run as a stream (Pipeline.encode_repeat): step k+1's GPU passes are
+queued before step k's host token emission, as a serving deployment would run
+consecutive batches; every step's bitstreams are complete inside the timed
+region.  --sequential times K independent encode() calls instead.
+
+Output check: after the timed region every bitstream of the batch is hashed
+and compared with tests/golden/bench_digests.json (SHA-256 of the oracle's
+bitstream for each synthetic frame, tools/make_bench_digests.py); the line
+carries "verified": true only if every frame matched.
 
 Multi-GPU: one process per GPU (torch.distributed.run); frames are sharded by
 rank (independent frames, no data-path collective); a barrier brackets the
 timed region and the max time is taken with an all-reduce.
+  default          weak scaling: every rank encodes its own `--frames` frames
+                   per step (global frames [rank*F, (rank+1)*F)).
+  --total-frames T strong scaling (BASELINE config 5: 4096 x 3840x2160 over N
+                   GPUs): a step encodes T frames in total, rank r the block
+                   shard_range(T, r, N), in device batches of `--batch` frames.
 
-The `roofline` object is SURVEY.md 8(d)'s designated HBM-bound kernel, the
-streaming DCT+quant pass k_fdct_quant: 80 algorithmic bytes per 4x4 block
-(16 src + 16 pred + 32 levels + 16 recon) x blocks per launch / average launch
-time from HIP events on the launch stream, over 256 frames' worth of blocks
-(24 per MB) resident in HBM; `traffic` is the PMC-measured HBM bytes per launch
-from profiles/ (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_pmc_xform.sh), scaled to
-this launch size.  `encode_kernel` reports the step's dominant kernel
-(k_encode pass 2, whose final DCT+quant is fused with the RD mode search)
-against the same HBM peak using 8(d)'s 1568 B/MB -- it is VALU-latency bound,
-not HBM bound.
-cpu_baseline times the C restatement of the reference encoder (oracle/, 1
-thread) on a bounded sample of the same frames.
+`roofline`: SURVEY.md 8(d)'s designated HBM-bound kernel, the streaming
+DCT+quant pass k_fdct_quant, over 256 frames' worth of 4x4 blocks (24 per MB)
+resident in HBM: ALGORITHMIC bytes 64 per block (16 src + 32 levels + 16
+recon; 1568 B/MB) / the average launch time from HIP events on the launch
+stream.  The materialised prediction (16 B per block) is traffic the kernel
+moves but 8(d) does not count; it is reported separately
+(achieved_incl_pred).  `copy_ceiling` times a kernel with the same read:write
+mix and no arithmetic on the same buffers (ZW_XFORM_VARIANT=99).  `traffic`
+is the PMC-measured HBM bytes per launch from profiles/ scaled to this launch.
+`encode_roofline`: the step's dominant kernel, k_encode_pass2 (RD mode search
+fused with the final DCT+quant+recon), against the VALU issue peak: its VALU
+instructions per launch (rocprofv3 SQ_INSTS_VALU, profiles/) over the live
+launch time, against 2 wave-instructions per CU-cycle (4 SIMD32, a wave64 VALU
+op every 2 cycles per SIMD).
+cpu_baseline times the C restatement of the reference encoder (oracle/, -O3)
+on a bounded sample of the same frames.
 """
 import argparse
+import hashlib
 import json
 import os
 
@@ -41,9 +56,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "image-webp_amd"))
 
-ALG_BYTES_PER_MB = 1568
+ALG_BYTES_PER_MB = 1568           # src YUV 384 + levels 800 + recon 384
+ALG_BYTES_PER_BLOCK = 64          # the same per 4x4 block: src 16 + levels 32 + recon 16
+PRED_BYTES_PER_BLOCK = 16         # materialised prediction: moved, not counted (8(d))
 HBM_PEAK_GBS = 8000.0
+VALU_PEAK_PER_CU_CYCLE = 2.0      # wave64 VALU instructions: 4 SIMD32 x 1 per 2 cycles
+CLOCK_GHZ = 2.4
 XFORM_PMC = os.path.join(ROOT, "profiles", "r01_xform_pmc_traffic.json")
+ENCODE_PMC = os.path.join(ROOT, "profiles", "r02_encode_pmc.json")
+DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
 
 
 def xform_traffic(blocks):
@@ -62,7 +83,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--frames", type=int, default=int(os.environ.get("ZW_BENCH_FRAMES", "1024")))
+    ap.add_argument("--frames", type=int, default=int(os.environ.get("ZW_BENCH_FRAMES", "1024")),
+                    help="frames per rank per step (weak scaling)")
+    ap.add_argument("--total-frames", type=int, default=0,
+                    help="strong scaling: frames per step over all ranks (BASELINE config 5: 4096)")
+    ap.add_argument("--batch", type=int, default=256, help="device batch in --total-frames mode")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--quality", type=int, default=75)
@@ -70,15 +95,37 @@ def parse():
     ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic frames per rank")
     ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("ZW_BENCH_CPU_SECONDS", "12")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="only the timed encode (no roofline / decode / single-frame side measurements)")
     ap.add_argument("--sequential", action="store_true",
                     help="time K separate encode() calls (no overlap between consecutive batches)")
     return ap.parse_args()
 
 
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        share = min(share, omp)
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cpu_share": share}
+
+
 def cpu_baseline(imgs, w, h, q, m, budget_s):
-    """Oracle (C port of the reference CPU encoder), 1 thread, bounded sample."""
+    """Oracle (C restatement of the reference CPU encoder, -O3), bounded sample:
+    (i) one frame on one thread, (ii) one frame per thread over the job's CPU share."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
+    info = cpu_info()
     n = 0
     t0 = time.perf_counter()
     while True:
@@ -89,10 +136,12 @@ def cpu_baseline(imgs, w, h, q, m, budget_s):
         if el >= budget_s or n >= 64:
             break
     out = {"value": n / el, "unit": "encodes/s", "cores": 1, "kind": "port",
-           "sample": f"{n} synthetic {w}x{h} RGBA frames, Q{q} m{m}, oracle/ C restatement, 1 thread, {el:.1f} s"}
-    # a batch over the host cores, one frame per thread (ctypes
-    # releases the GIL; the oracle keeps no global state).  16 = the box's CPU share.
-    nt = min(16, len(os.sched_getaffinity(0)))
+           "sample": f"{n} synthetic {w}x{h} RGBA frames, Q{q} m{m}, oracle/ C restatement (-O3), 1 thread, {el:.1f} s",
+           **info}
+    # a batch over the visible cores, one frame per thread (ctypes
+    # releases the GIL; the oracle keeps no global state), capped at the job's
+    # per-process CPU share (OMP_NUM_THREADS on the GPU box: 16 of the machine's cores)
+    nt = info["cpu_share"]
     if nt > 1:
         from concurrent.futures import ThreadPoolExecutor
         stop = time.perf_counter() + budget_s * 0.75
@@ -111,14 +160,30 @@ def cpu_baseline(imgs, w, h, q, m, budget_s):
             list(ex.map(worker, range(nt)))
         el = time.perf_counter() - t0
         out["batch_all_cores"] = {"value": sum(counts) / el, "unit": "encodes/s", "cores": nt,
-                                  "sample": f"{sum(counts)} frames, one frame per thread, {nt} threads, {el:.1f} s"}
+                                  "sample": f"{sum(counts)} frames, one frame per thread, {nt} threads "
+                                            f"(job CPU share of {info['affinity_cpus']} visible), {el:.1f} s"}
     return out
+
+
+def timed_launches(torch, dev, stream, fn, reps):
+    """Average ms of fn() over reps launches, HIP events on `stream` (the launch stream)."""
+    fn()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / reps
 
 
 def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
     """Streaming DCT+quant pass (k_fdct_quant) over `frames` frames' worth of 4x4
     blocks (24 per MB), device-resident synthetic src/pred; HIP events on the
-    launch stream.  Algorithmic bytes per block: 16 src + 16 pred + 32 levels + 16 recon."""
+    launch stream.  Algorithmic bytes per block: 16 src + 32 levels + 16 recon
+    (the 16 B of materialised prediction are reported, not counted).  The copy
+    ceiling is variant 99 (same loads and stores, no arithmetic) on the same buffers."""
     import zwebp
     n = frames * nmb * 24
     g = torch.Generator(device=dev)
@@ -131,28 +196,35 @@ def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
     rc = torch.empty((n, 16), dtype=torch.uint8, device=dev)
     stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the kernel and the events share it
     sh = stream.cuda_stream
-    torch.cuda.synchronize(dev)
 
     def run():
         zwebp.transform_quant_blocks_device(n, src.data_ptr(), pred.data_ptr(), 24, 30, 0, 0, lv.data_ptr(),
                                             rc.data_ptr(), stream=sh, ctx=ctx)
 
-    run()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        run()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
-    byts = n * 80
-    ach = byts / (ms * 1e-3) / 1e9
+    ms = timed_launches(torch, dev, stream, run, reps)
+    prev = os.environ.get("ZW_XFORM_VARIANT")
+    os.environ["ZW_XFORM_VARIANT"] = "99"
+    try:
+        ms_copy = timed_launches(torch, dev, stream, run, reps)
+    finally:
+        if prev is None:
+            os.environ.pop("ZW_XFORM_VARIANT", None)
+        else:
+            os.environ["ZW_XFORM_VARIANT"] = prev
     del src, pred, lv, rc
     torch.cuda.empty_cache()
+    alg = n * ALG_BYTES_PER_BLOCK
+    moved = n * (ALG_BYTES_PER_BLOCK + PRED_BYTES_PER_BLOCK)
+    ach = alg / (ms * 1e-3) / 1e9
+    ach_moved = moved / (ms * 1e-3) / 1e9
+    copy_gbs = moved / (ms_copy * 1e-3) / 1e9
     return {"kernel": "k_fdct_quant", "workload": f"{frames} frames x {nmb} MBs x 24 4x4 blocks, Q75 Y1 matrix",
-            "blocks": n, "ms_per_launch": ms, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": byts}
+            "blocks": n, "ms_per_launch": ms, "achieved": ach, "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+            "achieved_incl_pred": ach_moved, "frac_incl_pred": ach_moved / HBM_PEAK_GBS,
+            "copy_ceiling": {"kernel": "k_fdct_quant_copy (ZW_XFORM_VARIANT=99: same 32 B read + 48 B written "
+                                       "per block, no arithmetic)", "ms_per_launch": ms_copy,
+                             "achieved": copy_gbs, "frac": copy_gbs / HBM_PEAK_GBS,
+                             "pass_over_copy": ms_copy / ms}}
 
 
 def decode_path(ctx, streams, frames, w, h, with_cpu):
@@ -215,7 +287,79 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
         t0 = time.perf_counter()
         O.yuv_to_rgb_fancy(r["y"], r["u"], r["v"], w, h, 4)
         out["rgba"]["cpu_baseline_fancy_upsample_ms"] = (time.perf_counter() - t0) * 1e3
+    ctx.release_buffers()
     return out
+
+
+def single_frame(ctx, img, w, h, q, m, reps=3):
+    """Latency of one frame through the drop-in seam (zw_encode_frame_lossy:
+    buffers allocated per call, as encode_frame_lossy would) and through a
+    persistent one-frame pipeline (encode + output, buffers reused)."""
+    import zwebp
+    zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    seam_ms = (time.perf_counter() - t0) / reps * 1e3
+    p = zwebp.Pipeline(1, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    p.upload(0, img)
+    p.encode()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        p.encode()
+        p.output(0)
+    pipe_ms = (time.perf_counter() - t0) / reps * 1e3
+    k = p.kernel_times()
+    p.close()
+    return {"encode_frame_lossy_ms": seam_ms, "pipeline_1_frame_ms": pipe_ms,
+            "kernel_ms": {"rgb2yuv": k[0], "analysis_segments": k[1], "encode_pass1": k[2], "encode_pass2": k[3]},
+            "note": "one frame = one workgroup (one CU) per encode pass"}
+
+
+def encode_roofline(p2_ms, launch_frames, nmb):
+    """k_encode_pass2 against the VALU issue peak: SQ_INSTS_VALU per MB from the
+    committed rocprofv3 --pmc summary x MBs per launch / the live launch time."""
+    try:
+        with open(ENCODE_PMC) as f:
+            d = json.load(f)["k_encode_pass2"]
+    except (OSError, KeyError, ValueError):
+        return None
+    mbs = launch_frames * nmb
+    insts = d["valu_insts_per_mb"] * mbs
+    cus = 256
+    achieved = insts / (p2_ms * 1e-3) / 1e9  # G wave-instructions / s
+    peak = VALU_PEAK_PER_CU_CYCLE * cus * CLOCK_GHZ
+    return {"kernel": "k_encode_pass2", "bound": "valu", "achieved": achieved, "peak": peak,
+            "unit": "G wave64-VALU-instructions/s", "frac": achieved / peak,
+            "valu_insts_per_mb": d["valu_insts_per_mb"], "ms_per_launch": p2_ms, "mbs_per_launch": mbs,
+            "pmc_frac": d.get("valu_issue_frac"), "hbm_achieved": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9,
+            "hbm_frac": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "source": "profiles/r02_encode_pmc.json (rocprofv3 --pmc SQ_INSTS_VALU, GRBM_GUI_ACTIVE)"}
+
+
+def load_digests():
+    try:
+        with open(DIGESTS) as f:
+            return json.load(f)["digests"]
+    except (OSError, KeyError, ValueError):
+        return {}
+
+
+def verify(pipe, nframes, seeds, w, h, q, m, digests):
+    """Hash every output bitstream of the batch; frame i was uploaded from the
+    synthetic frame seeds[i % len(seeds)].  Returns (matched, mismatched, missing)."""
+    ok = bad = missing = 0
+    for i in range(nframes):
+        key = f"{w}x{h}/q{q}m{m}/{seeds[i % len(seeds)]:#010x}"
+        want = digests.get(key)
+        if want is None:
+            missing += 1
+            continue
+        if hashlib.sha256(pipe.output(i)).hexdigest() == want:
+            ok += 1
+        else:
+            bad += 1
+    return ok, bad, missing
 
 
 def main():
@@ -227,7 +371,7 @@ def main():
     import torch
     import torch.distributed as dist
     import zwebp
-    from zwebp.shard import frame_seed, reduce_max
+    from zwebp.shard import frame_seed, gather_counts, rank_frames, reduce_max
     from zwebp.synth import synth_rgba
 
     # ZW_BENCH_BACKEND / ZW_BENCH_DEVICE: rehearsal of the N>1 path on fewer GPUs
@@ -241,14 +385,29 @@ def main():
     torch.cuda.set_device(dev)
     red_dev = dev if backend == "nccl" else None
 
-    w, h, F = a.width, a.height, a.frames
+    w, h = a.width, a.height
+    # frames of this rank per step: its own F (weak) or its block of the T total (strong, config 5)
+    first, n_rank = rank_frames(rank, world, a.frames, a.total_frames)
+    if a.total_frames > 0:
+        B = max(1, min(a.batch, n_rank))
+        nbatch, rem = divmod(n_rank, B)
+        scaling = "strong"
+    else:
+        B, nbatch, rem = a.frames, 1, 0
+        scaling = "weak"
     ctx = zwebp.Context(local)
-    pipe = zwebp.Pipeline(F, w, h, zwebp.ColorType.Rgba8, a.quality, a.method, ctx=ctx)
-    # weak scaling: rank r owns global frames [r*F, (r+1)*F); `distinct` of them are generated
-    imgs = [synth_rgba(w, h, frame_seed(rank * F + i)) for i in range(min(a.distinct, F))]
-    for i in range(F):
-        pipe.upload(i, imgs[i % len(imgs)])
-    nmb = pipe.mbw * pipe.mbh
+    D = max(1, min(a.distinct, B))
+    seeds = [frame_seed(first + i) for i in range(D)]
+    imgs = [synth_rgba(w, h, sd) for sd in seeds]
+    pipes = []
+    if n_rank > 0:
+        pipes.append((zwebp.Pipeline(B, w, h, zwebp.ColorType.Rgba8, a.quality, a.method, ctx=ctx), nbatch))
+    if rem:
+        pipes.append((zwebp.Pipeline(rem, w, h, zwebp.ColorType.Rgba8, a.quality, a.method, ctx=ctx), 1))
+    for pipe, _ in pipes:
+        for i in range(pipe.n):
+            pipe.upload(i, imgs[i % D])
+    nmb = ((w + 15) // 16) * ((h + 15) // 16)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -257,36 +416,46 @@ def main():
         torch.cuda.synchronize(dev)
 
     for _ in range(a.warmup):
-        pipe.encode()
+        for pipe, nb in pipes:
+            pipe.encode_repeat(nb)
     barrier()
     kt = np.zeros(8)
     t0 = time.perf_counter()
     if a.sequential:
         for _ in range(a.steps):
-            pipe.encode()
-            kt += np.array(pipe.kernel_times())
+            for pipe, nb in pipes:
+                for _ in range(nb):
+                    pipe.encode()
+            kt += np.array(pipes[0][0].kernel_times()) if pipes else 0
     else:
-        # streaming: step k+1's GPU passes overlap step k's host token emission;
-        # all K batches are complete (bitstreams emitted) when this returns
-        pipe.encode_repeat(a.steps)
-        kt += np.array(pipe.kernel_times()) * a.steps
+        # streaming: batch k+1's GPU passes overlap batch k's host token emission;
+        # every batch is complete (bitstreams emitted) when this returns
+        for pipe, nb in pipes:
+            pipe.encode_repeat(nb * a.steps)
+        if pipes:
+            kt += np.array(pipes[0][0].kernel_times()) * a.steps
     barrier()
     el = time.perf_counter() - t0
     el = reduce_max(el, red_dev)
-    total_frames = F * a.steps * world
-    bytes_out = sum(len(pipe.output(i)) for i in range(min(F, 4)))
+    frames_done = n_rank * a.steps
+    total_frames = int(sum(c[0] for c in gather_counts([frames_done], red_dev)))
+
+    # output check (outside the timed region): every bitstream of every pipe
+    digests = load_digests()
+    vok = vbad = vmiss = 0
+    for pipe, _ in pipes:
+        r = verify(pipe, pipe.n, seeds, w, h, a.quality, a.method, digests)
+        vok, vbad, vmiss = vok + r[0], vbad + r[1], vmiss + r[2]
+    vc = gather_counts([vok, vbad, vmiss], red_dev)
+    vok, vbad, vmiss = (sum(c[i] for c in vc) for i in range(3))
+    bytes_out = sum(len(pipes[0][0].output(i)) for i in range(min(B, D))) if pipes else 0
 
     if rank == 0:
         k = kt / max(a.steps, 1)  # ms per launch: rgb2yuv, analysis+segments, pass1, pass2
         p2_ms = float(k[3])
-        per_launch = pipe.launch_frames  # frames covered by one k_encode_pass2 launch (one lane chunk)
-        achieved = ALG_BYTES_PER_MB * nmb * per_launch / (p2_ms * 1e-3) / 1e9 if p2_ms > 0 else 0.0
-        dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
-        dec = decode_path(ctx, [bytes(pipe.output(i)) for i in range(min(F, 4))], 256, w, h,
-                          not a.no_cpu_baseline)
-        cpu = None
-        if not a.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
+        per_launch = pipes[0][0].launch_frames
+        threads = zwebp.host_threads()
+        emit_s = float(k[7]) * 1e-3
         line = {
             "metric": f"{w}x{h} lossy encodes/s (Q{a.quality}, method {a.method})",
             "value": total_frames / el,
@@ -296,34 +465,47 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": el / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
+            "verified": vbad == 0 and vmiss == 0 and vok > 0,
+            "verification": {"frames_checked": vok + vbad + vmiss, "matched": vok, "mismatched": vbad,
+                             "no_digest": vmiss, "against": "tests/golden/bench_digests.json (oracle SHA-256)"},
             "config": {"workload": f"encode_frame_lossy {w}x{h} RGBA Q{a.quality} m{a.method}",
-                       "frames_per_step_per_gpu": F, "distinct_frames": len(imgs), "mbs_per_frame": nmb,
-                       "parallelism": f"frames sharded over {world} GPU(s)",
-                       "steps_pipelined": not a.sequential},
-            "roofline": {"bound": "hbm", "achieved": dq["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": dq["frac"], "traffic": xform_traffic(dq["blocks"]),
-                         "kernel": "k_fdct_quant", "workload": dq["workload"], "blocks_per_launch": dq["blocks"],
-                         "alg_bytes_per_launch": dq["alg_bytes_per_launch"], "ms_per_launch": dq["ms_per_launch"],
-                         "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"},
-            "cpu_baseline": cpu,
-            "decode_path": dec,
-            "encode_kernel": {"kernel": "k_encode_pass2", "bound": "valu", "hbm_achieved": achieved,
-                              "hbm_frac": achieved / HBM_PEAK_GBS, "unit": "GB/s",
-                              "alg_bytes_per_launch": ALG_BYTES_PER_MB * nmb * per_launch,
-                              "launch_frames": per_launch, "ms_per_launch": p2_ms},
+                       "frames_per_step": total_frames // max(a.steps, 1),
+                       "frames_per_step_per_gpu": n_rank, "device_batch": B, "distinct_frames": D,
+                       "mbs_per_frame": nmb, "parallelism": f"frames sharded over {world} GPU(s)",
+                       "steps_pipelined": not a.sequential,
+                       **({"total_frames": a.total_frames} if a.total_frames else {})},
             "kernel_ms_per_step": {"rgb2yuv": float(k[0]), "analysis_segments": float(k[1]),
-                                   "encode_pass1": float(k[2]), "encode_pass2": p2_ms},
+                                   "encode_pass1": float(k[2]), "encode_pass2": p2_ms, "launch_frames": per_launch},
             "host_ms_per_step": {"fetch_pass1": float(k[4]), "stats_probs": float(k[5]),
-                                 "fetch_pass2": float(k[6]), "emit": float(k[7])},
-            "avg_frame_bytes": bytes_out / min(F, 4),
+                                 "fetch_pass2": float(k[6]), "emit": float(k[7]), "threads": threads},
+            "host_emit_frames_per_s_per_core": B / (emit_s * threads) if emit_s > 0 else None,
+            "avg_frame_bytes": bytes_out / max(1, min(B, D)),
         }
+        if not a.no_extras:
+            dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
+            line["roofline"] = {"bound": "hbm", "achieved": dq["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": dq["frac"], "traffic": xform_traffic(dq["blocks"]),
+                                "kernel": "k_fdct_quant", "workload": dq["workload"],
+                                "blocks_per_launch": dq["blocks"], "alg_bytes_per_block": ALG_BYTES_PER_BLOCK,
+                                "alg_bytes_per_launch": dq["alg_bytes_per_launch"],
+                                "ms_per_launch": dq["ms_per_launch"],
+                                "achieved_incl_pred": dq["achieved_incl_pred"], "frac_incl_pred": dq["frac_incl_pred"],
+                                "copy_ceiling": dq["copy_ceiling"],
+                                "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"}
+            line["encode_roofline"] = encode_roofline(p2_ms, per_launch, nmb)
+            line["single_frame"] = single_frame(ctx, imgs[0], w, h, a.quality, a.method)
+            line["decode_path"] = decode_path(ctx, [bytes(pipes[0][0].output(i)) for i in range(min(B, D))], 256, w, h,
+                                              not a.no_cpu_baseline)
+        line["cpu_baseline"] = None
+        if not a.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
         print(json.dumps(line), flush=True)
-    lanes = pipe.lanes
-    pipe.close()
+    for pipe, _ in pipes:
+        pipe.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -11,6 +11,8 @@
 
 #include <chrono>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <vector>
 
 #include "../../include/zwebp.h"
@@ -479,7 +481,33 @@ struct DecBatch {
     uint8_t* d = nullptr;  // device scratch base
     size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
     int mbw = 0, mbh = 0;
+    const int* d_rs = nullptr;  // row-parallel kernels' per-frame sync words (null: workgroup-per-frame kernels)
+    int n = 0;
 };
+
+// Test hook (ZW_DEC_FORCE_ERROR=1): pre-set frame 0's row-sync error word, as a
+// wave that gave up waiting would, so the host-side check below is exercised.
+static bool dec_force_error() { return getenv("ZW_DEC_FORCE_ERROR") != nullptr; }
+
+// A row-parallel wave that gives up waiting (k_dec_recon_rows / k_loopfilter_rows
+// bounded spins) reports through its frame's error word rowsync[f][2] instead of
+// hanging the GPU; the planes of such a frame are incomplete.  Read the words
+// after the kernels completed (SDMA: the kernel stream may already run the next
+// chunk) and fail the call with ZW_EDEVICE.
+static int rows_error(zw_ctx* ctx, const int* d_rs, int n, int mbh)
+{
+    if (!d_rs) return ZW_OK;
+    const size_t words = (size_t)n * (4 + 2 * mbh);
+    int* rs = (int*)ctx_pinned(ctx, 3, words * sizeof(int));
+    if (!rs) return ZW_ENOMEM;
+    if (int r = ctx_d2h(ctx, rs, d_rs, words * sizeof(int))) return r;
+    for (int f = 0; f < n; f++)
+        if (rs[(size_t)f * (4 + 2 * mbh) + 2]) {
+            fprintf(stderr, "zwebp: row-parallel decode gave up waiting on frame %d of %d\n", f, n);
+            return ZW_EDEVICE;
+        }
+    return ZW_OK;
+}
 
 // Vp8Decoder::decode_frame for n frames of identical dimensions, one device
 // pass: host header/token parse (parallel over frames) -> k_dec_recon ->
@@ -510,20 +538,24 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     if (mbw == 0 || mbh == 0) return ZW_EINVALID_DIMENSIONS;
     const size_t nmb = (size_t)mbw * mbh;
     const size_t ysz = nmb * 256, csz = nmb * 64;
-    // packed MB records (zw_common.h ZW_DREC_*) straight into pinned staging,
-    // one worst-case slot per frame (only the used prefix crosses PCIe); the MB
-    // offsets and frame bases follow the slots
-    const size_t slot = al256(nmb * ZW_DREC_MAX);
-    const size_t off_bytes = (size_t)n * (nmb + 1) * 4, base_bytes = (size_t)n * 8;
-    const size_t o_moff = (size_t)n * slot, o_base = o_moff + al256(off_bytes);
-    const size_t up_bytes = o_base + base_bytes;
-    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, bi ? 2 : 0, up_bytes);
-    if (!stage) return ZW_ENOMEM;
-    uint32_t* moff = (uint32_t*)(stage + o_moff);
+    // packed MB records (zw_common.h ZW_DREC_*): each frame is parsed into its
+    // own worst-case pageable buffer (only the pages written are touched), then
+    // the used prefixes are packed back to back (256-B aligned frame bases) into
+    // pinned staging sized by the measured bytes -- ~1 MB per 1080p frame at
+    // Q75 instead of the 7 MB worst case -- followed by the MB offsets and the
+    // frame bases; one upload carries all of it.
+    const size_t slot = nmb * ZW_DREC_MAX;
+    std::vector<uint32_t> moffv((size_t)n * (nmb + 1));
+    std::vector<std::unique_ptr<uint8_t[]>> recs(n);
     std::vector<DecQuant> quant((size_t)n * 4);
     std::vector<ZwFilterParams> fps(n);
     parallel_for(n, [&](int i) {
-        rc[i] = parse_mbs(F[i], stage + (size_t)i * slot, moff + (size_t)i * (nmb + 1));
+        recs[i].reset(new (std::nothrow) uint8_t[slot]);
+        if (!recs[i]) {
+            rc[i] = ZW_ENOMEM;
+            return;
+        }
+        rc[i] = parse_mbs(F[i], recs[i].get(), moffv.data() + (size_t)i * (nmb + 1));
         for (int s = 0; s < 4; s++) quant[(size_t)i * 4 + s] = F[i].q[s];
         filter_table(fps[i], F[i].filter_type, F[i].filter_level, F[i].sharpness, F[i].segments_enabled,
                      F[i].seg_delta_values, F[i].seg_lf, F[i].lf_adj_enabled, F[i].ref_delta0, F[i].mode_delta0, mbw,
@@ -531,12 +563,25 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     });
     for (int i = 0; i < n; i++)
         if (rc[i] != ZW_OK) return rc[i];
-    uint64_t* fbase = (uint64_t*)(stage + o_base);
-    size_t rec_bytes = 0;
+    std::vector<uint64_t> fb(n);
+    size_t rec_bytes = 0, rec_span = 0;
     for (int i = 0; i < n; i++) {
-        fbase[i] = (uint64_t)i * slot;
-        rec_bytes += moff[(size_t)i * (nmb + 1) + nmb];
+        fb[i] = rec_span;
+        const size_t used = moffv[(size_t)i * (nmb + 1) + nmb];
+        rec_bytes += used;
+        rec_span = al256(rec_span + used);
     }
+    const size_t off_bytes = (size_t)n * (nmb + 1) * 4, base_bytes = (size_t)n * 8;
+    const size_t o_moff = rec_span, o_base = o_moff + al256(off_bytes);
+    const size_t up_bytes = o_base + base_bytes;
+    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, bi ? 2 : 0, up_bytes);
+    if (!stage) return ZW_ENOMEM;
+    parallel_for(n, [&](int i) {
+        memcpy(stage + fb[i], recs[i].get(), moffv[(size_t)i * (nmb + 1) + nmb]);
+        recs[i].reset();
+    });
+    memcpy(stage + o_moff, moffv.data(), off_bytes);
+    memcpy(stage + o_base, fb.data(), base_bytes);
     const double t1 = dec_now_ms();
 
     HIPOK(hipSetDevice(ctx->device));
@@ -560,10 +605,7 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     hipStream_t s = ctx_stream(ctx);
     hipEvent_t* ev = bi ? ctx->dev_ev1 : ctx->dev_ev;
     B.ev = ev;
-    for (int i = 0; i < n; i++)  // each frame's used prefix
-        HIPOK(hipMemcpyAsync(d + o_mbs + (size_t)i * slot, stage + (size_t)i * slot, moff[(size_t)i * (nmb + 1) + nmb],
-                             hipMemcpyHostToDevice, s));
-    HIPOK(hipMemcpyAsync(d + o_mbs + o_moff, stage + o_moff, up_bytes - o_moff, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_mbs, stage, up_bytes, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
     for (int e = 0; e < 4; e++)
@@ -577,6 +619,7 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     if (rows) {
         int* rs = (int*)(d + o_rs);
         HIPOK(zwk_dec_rows_init(s, rs, mbh, n));
+        if (dec_force_error()) HIPOK(hipMemsetAsync(rs + 2, 1, sizeof(int), s));
         HIPOK(zwk_dec_rows(s, 1, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
         HIPOK(hipEventRecord(ev[1], s));
@@ -605,6 +648,8 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     B.csz = csz;
     B.mbw = mbw;
     B.mbh = mbh;
+    B.d_rs = rows ? (const int*)(d + o_rs) : nullptr;
+    B.n = n;
     return ZW_OK;
 }
 
@@ -669,6 +714,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fsz);
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[2]));
+        if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         const double td = dec_now_ms();
         {
             int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)cn * ysz);
@@ -750,6 +796,7 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
         uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fbytes);
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[3]));
+        if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         if (int r = ctx_d2h(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
         std::vector<int> oom(cn, 0);
         parallel_for(cn, [&](int i) {
@@ -867,6 +914,7 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipMemcpyAsync(d + o_v, v, csz, hipMemcpyHostToDevice, s));
     if (rows_env != 0) {
         HIPOK(zwk_dec_rows_init(s, (int*)(d + o_rs), (int)mbh, 1));
+        if (dec_force_error()) HIPOK(hipMemsetAsync(d + o_rs + 2 * sizeof(int), 1, sizeof(int), s));
         HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp),
                            (int)mbw, (int)mbh, ysz, csz, 1, (int*)(d + o_rs), nullptr, (int)mbh));
     } else {
@@ -876,7 +924,7 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(v, d + o_v, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
-    return ZW_OK;
+    return rows_env != 0 ? rows_error(ctx, (const int*)(d + o_rs), 1, (int)mbh) : ZW_OK;
 }
 
 // ---------------------------------------------------------------------------

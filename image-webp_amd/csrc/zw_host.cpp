@@ -111,23 +111,36 @@ static hsa_status_t find_agents_cb(hsa_agent_t a, void* data)
     return HSA_STATUS_SUCCESS;
 }
 
-static bool sdma_probe(zw_ctx* c)
+static int sdma_probe_locked(zw_ctx* c)
 {
-    if (c->sdma >= 0) return c->sdma == 1;
-    c->sdma = 0;
-    if (getenv("ZW_NO_SDMA")) return false;
+    if (getenv("ZW_NO_SDMA")) return 0;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return false;
-    if (hsa_init() != HSA_STATUS_SUCCESS) return false;  // reference-counted; HIP holds one
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return 0;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return 0;  // reference-counted; HIP holds one
     AgentFind F;
     F.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
     F.domain = (uint32_t)prop.pciDomainID;
     (void)hsa_iterate_agents(find_agents_cb, &F);
-    if (!F.gpu_ok || !F.cpu_ok) return false;
+    if (!F.gpu_ok || !F.cpu_ok) return 0;
     c->gpu_agent = F.gpu;
     c->cpu_agent = F.cpu;
-    c->sdma = 1;
-    return true;
+    return 1;
+}
+
+// Resolved once per context: the first caller probes under sdma_mu, later and
+// concurrent callers (pipe lanes) wait for it and then read the published agents.
+static bool sdma_probe(zw_ctx* c)
+{
+    int st = c->sdma.load(std::memory_order_acquire);
+    if (st < 0) {
+        std::lock_guard<std::mutex> lk(c->sdma_mu);
+        st = c->sdma.load(std::memory_order_relaxed);
+        if (st < 0) {
+            st = sdma_probe_locked(c);
+            c->sdma.store(st, std::memory_order_release);  // publishes gpu_agent / cpu_agent
+        }
+    }
+    return st == 1;
 }
 
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
@@ -139,16 +152,36 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
             const hsa_status_t st =
                 hsa_amd_memory_async_copy(dst, c->cpu_agent, src, c->gpu_agent, bytes, 0, nullptr, sig);
             hsa_signal_value_t v = 1;
-            if (st == HSA_STATUS_SUCCESS)
-                v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            // bounded wait: a copy that never completes fails the call instead of hanging it
+            const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+            while (st == HSA_STATUS_SUCCESS) {
+                v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 100000000ull, HSA_WAIT_STATE_BLOCKED);
+                if (v == 0 || std::chrono::steady_clock::now() > deadline) break;
+            }
             (void)hsa_signal_destroy(sig);
             if (st == HSA_STATUS_SUCCESS && v == 0) return ZW_OK;
             if (st == HSA_STATUS_SUCCESS) return ZW_EDEVICE;  // the copy itself failed
         }
-        c->sdma = 0;  // HSA path unusable: fall back for good
+        c->sdma.store(0, std::memory_order_release);  // HSA path unusable: fall back for good
     }
     HIPOK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return ZW_OK;
+}
+
+extern "C" void zw_ctx_release_buffers(zw_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream_) (void)hipStreamSynchronize(c->stream_);  // nothing queued may still use them
+    if (c->dscratch) (void)hipFree(c->dscratch);
+    if (c->dscratch1) (void)hipFree(c->dscratch1);
+    c->dscratch = c->dscratch1 = nullptr;
+    c->dscratch_cap = c->dscratch1_cap = 0;
+    for (int i = 0; i < 4; i++) {
+        if (c->hpin[i]) (void)hipHostFree(c->hpin[i]);
+        c->hpin[i] = nullptr;
+        c->hpin_cap[i] = 0;
+    }
 }
 
 extern "C" void zw_ctx_destroy(zw_ctx* c)
@@ -407,7 +440,10 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
     t.filter_level = p->filter;
     t.skip_prob = 200;
     memcpy(t.probs, zwh::COEFF_PROBS, sizeof t.probs);
-    HIPOK(hipMemcpy(p->d_tmpl, &t, sizeof t, hipMemcpyHostToDevice));
+    if (hipMemcpy(p->d_tmpl, &t, sizeof t, hipMemcpyHostToDevice) != hipSuccess) {
+        pipe_free(p);
+        return ZW_EDEVICE;
+    }
     *out = p;
     return ZW_OK;
 }
@@ -724,6 +760,8 @@ static int pipe_encode(zw_pipe* p, int nb)
 extern "C" int zw_pipe_encode(zw_pipe* p) { return pipe_encode(p, 1); }
 
 extern "C" int zw_pipe_encode_repeat(zw_pipe* p, int n) { return pipe_encode(p, n); }
+
+extern "C" int zw_host_threads(void) { return host_threads(); }
 
 extern "C" int zw_pipe_launch_frames(zw_pipe* p) { return p && !p->lanes.empty() ? p->lanes[0].chunk : 0; }
 

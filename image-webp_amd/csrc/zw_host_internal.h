@@ -3,10 +3,12 @@
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <sched.h>
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -21,12 +23,15 @@ struct zw_ctx {
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
     // D2H runs as a blit kernel, which cannot be dispatched while an encode
     // kernel holds every CU; the DMA engines need no CU.
-    int sdma = -1;  // -1 unprobed, 0 unavailable, 1 ready
+    // Probed once under sdma_mu (pipe lanes call ctx_d2h from several threads).
+    std::atomic<int> sdma{-1};  // -1 unprobed, 0 unavailable, 1 ready
+    std::mutex sdma_mu;
     hsa_agent_t gpu_agent{}, cpu_agent{};
     // grow-only pinned host staging (decode batch: MB records up, planes down)
-    // [0] / [2]: the two upload buffers of the pipelined decode, [1] downloads
-    void* hpin[3] = {nullptr, nullptr, nullptr};
-    size_t hpin_cap[3] = {0, 0, 0};
+    // [0] / [2]: the two upload buffers of the pipelined decode, [1] downloads,
+    // [3] the row-parallel kernels' sync / error words
+    void* hpin[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t hpin_cap[4] = {0, 0, 0, 0};
     // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter,
     // [2] k_yuv2rgb (0 when the batch returned planes) (ms)
     hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -44,14 +49,30 @@ struct zw_ctx {
     } while (0)
 
 
+// Host worker threads per process (entropy coding, stats, decode parsing).
+// ZW_HOST_THREADS overrides.  Default: this process's share of the CPUs it may
+// run on -- the affinity mask divided by the ranks on this node
+// (LOCAL_WORLD_SIZE, set by torch.distributed.run), capped by the job's
+// per-process CPU share when one is declared (OMP_NUM_THREADS).
+static inline int host_threads_default()
+{
+    cpu_set_t set;
+    int cpus = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 0;
+    if (cpus <= 0) cpus = (int)std::thread::hardware_concurrency();
+    const char* lw = getenv("LOCAL_WORLD_SIZE");
+    const int ranks = lw && atoi(lw) > 0 ? atoi(lw) : 1;
+    int n = cpus / ranks;
+    const char* omp = getenv("OMP_NUM_THREADS");
+    if (omp && atoi(omp) > 0 && atoi(omp) < n) n = atoi(omp);
+    return n < 1 ? 1 : n;
+}
 static inline int host_threads()
 {
     const char* e = getenv("ZW_HOST_THREADS");
     int n = e ? atoi(e) : 0;
     if (n <= 0) {
-        n = (int)std::thread::hardware_concurrency();
-        if (n > 16) n = 16;
-        if (n < 1) n = 1;
+        static const int dflt = host_threads_default();
+        n = dflt;
     }
     return n;
 }
@@ -103,7 +124,8 @@ static inline hipStream_t ctx_stream(zw_ctx* c)
 
 // Blocking device->host copy on a DMA engine (falls back to hipMemcpy when the
 // HSA agents cannot be resolved).  `src` must have been released by the
-// producing kernel (event-complete) before the call.
+// producing kernel (event-complete) before the call, and `dst` must be pinned
+// (hipHostMalloc): the DMA engine cannot reach pageable memory.
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
 
 // Pinned host staging buffer `which` of at least `bytes` owned by the context.

@@ -461,6 +461,7 @@ extern "C" int zw_encode_webp_ex(zw_ctx* ctx, const uint8_t* data, size_t len, u
     if (params) prm = *params;
     zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
     if (meta) md = *meta;
+    if ((!md.icc && md.icc_len) || (!md.exif && md.exif_len) || (!md.xmp && md.xmp_len)) return ZW_EINVAL;
     if (color < ZW_COLOR_L8 || color > ZW_COLOR_RGBA8) return ZW_EINVAL;
     const bool has_alpha = color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8;
     const bool lossy_alpha = prm.use_lossy && has_alpha;

@@ -115,6 +115,7 @@ _VP, _SZ, _U32, _I, _U8 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, cty
 SIGNATURES = [
     ("zw_ctx_create", _I, [_I, ctypes.POINTER(_VP)]),
     ("zw_ctx_destroy", None, [_VP]),
+    ("zw_ctx_release_buffers", None, [_VP]),
     ("zw_strerror", ctypes.c_char_p, [_I]),
     ("zw_bytes_free", None, [ctypes.POINTER(_Bytes)]),
     ("zw_frame_free", None, [ctypes.POINTER(_Frame)]),
@@ -160,6 +161,7 @@ SIGNATURES = [
     ("zw_pipe_kernel_times", _I, [_VP, ctypes.POINTER(ctypes.c_float), _I]),
     ("zw_pipe_lanes", _I, [_VP]),
     ("zw_pipe_launch_frames", _I, [_VP]),
+    ("zw_host_threads", _I, []),
 ]
 
 _LIB = None
@@ -190,6 +192,11 @@ def _check(rc, what, cls=ZwError):
         raise cls(rc, what)
 
 
+def host_threads():
+    """Host worker threads per process (zw_host_threads)."""
+    return load_library().zw_host_threads()
+
+
 class Context:
     """One HIP device + stream (zw_ctx).  Not thread-safe; one per thread."""
 
@@ -204,6 +211,11 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def release_buffers(self):
+        """Free the grow-only device scratch / pinned staging (zw_ctx_release_buffers)."""
+        if self._h:
+            self._lib.zw_ctx_release_buffers(self._h)
 
     def close(self):
         if self._h:

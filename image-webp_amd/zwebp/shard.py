@@ -16,6 +16,19 @@ def shard_range(n_total, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
+def rank_frames(rank, world, frames_per_rank=0, total_frames=0):
+    """Global frame indices [first, first + n) a rank encodes per bench step.
+
+    total_frames > 0: strong scaling (BASELINE config 5, a fixed batch split
+    over the ranks): the contiguous block shard_range(total_frames, rank, world).
+    Otherwise weak scaling: every rank owns frames_per_rank frames of its own,
+    [rank * frames_per_rank, (rank + 1) * frames_per_rank)."""
+    if total_frames > 0:
+        s, e = shard_range(total_frames, rank, world)
+        return s, e - s
+    return rank * frames_per_rank, frames_per_rank
+
+
 def frame_seed(global_index, base=0x5EED0000):
     """Seed convention of the synthetic inputs: base + frame index."""
     return base + global_index

@@ -101,6 +101,10 @@ typedef struct {
 
 int zw_ctx_create(int device, zw_ctx **out);
 void zw_ctx_destroy(zw_ctx *ctx);
+/* Frees the context's grow-only device scratch and pinned host staging (the
+ * single-call and batch decode / filter entry points keep them between calls);
+ * the next call reallocates what it needs. */
+void zw_ctx_release_buffers(zw_ctx *ctx);
 const char *zw_strerror(int code);
 void zw_bytes_free(zw_bytes *b);
 void zw_frame_free(zw_frame *f);
@@ -253,6 +257,10 @@ int zw_pipe_lanes(zw_pipe *p);
 /* frames covered by one encode-kernel launch (a lane's chunk) */
 int zw_pipe_launch_frames(zw_pipe *p);
 int zw_pipe_kernel_times(zw_pipe *p, float *ms, int n);
+/* Host worker threads the library uses per process for entropy coding and
+ * decode parsing: ZW_HOST_THREADS, else the process's affinity mask divided by
+ * LOCAL_WORLD_SIZE, capped by OMP_NUM_THREADS when set. */
+int zw_host_threads(void);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,167 @@
+"""GPU: the encoder at the shapes the benchmark times (BASELINE configs 4 and 5),
+the full WebP container for alpha inputs, and failure reporting of the
+row-parallel decode.
+
+* A 512-frame 1080p batch through zwebp.Pipeline at the default lane and chunk
+  shape (256-frame launches, multi-chunk, streaming repeat) -- every output is
+  compared with the oracle's bitstream of its source frame.
+* A 256-frame 4K batch (one default launch of 3840x2160 frames).
+* WebPEncoder::encode for RGBA8 / LA8 (api.rs:1291-1398): VP8X + ALPH + VP8
+  (+ ICCP / EXIF / XMP) byte-equal to the oracle's pieces in the reference's
+  chunk order; libwebp round trip when the system library is present.
+"""
+import ctypes
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import zwebp
+from zwebp.shard import frame_seed
+from zwebp.synth import synth_rgba
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return zwebp.Context(0)
+
+
+def _batch_check(ctx, n, w, h, distinct, repeat):
+    imgs = [synth_rgba(w, h, frame_seed(i)) for i in range(distinct)]
+    refs = []
+    for im in imgs:
+        rc, ref, _ = O.encode(im, w, h, 3, 75, 4)
+        assert rc == 0
+        refs.append(ref)
+    p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    try:
+        for i in range(n):
+            p.upload(i, imgs[i % distinct])
+        assert p.launch_frames == min(n, 256)  # default chunk = one frame per CU
+        for run in range(2):
+            if run == 0:
+                p.encode()
+            else:
+                p.encode_repeat(repeat)
+            bad = [i for i in range(n) if p.output(i) != refs[i % distinct]]
+            assert not bad, f"run {run}: {len(bad)} of {n} frames differ, first {bad[0]}"
+    finally:
+        p.close()
+
+
+def test_default_shape_1080p_batch_512(ctx):
+    """BASELINE config 4 shape: 512 x 1920x1080, default lanes/chunks (2 launches
+    of 256 frames per pass), single encode and a 2-batch streaming repeat."""
+    _batch_check(ctx, 512, 1920, 1080, 4, 2)
+
+
+def test_4k_batch_default_launch(ctx):
+    """BASELINE config 5 frame size: one default launch of 256 x 3840x2160."""
+    _batch_check(ctx, 256, 3840, 2160, 2, 1)
+
+
+# --------------------------------------------------------------------------
+# full container for alpha inputs
+# --------------------------------------------------------------------------
+def _chunk(tag, payload):
+    return tag + struct.pack("<I", len(payload)) + payload + (b"\0" if len(payload) & 1 else b"")
+
+
+def _riff(*chunks):
+    body = b"WEBP" + b"".join(chunks)
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def _vp8x(w, h, flags):
+    return _chunk(b"VP8X", bytes([flags, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little"))
+
+
+try:
+    _W = ctypes.CDLL("libwebp.so.7")
+    _W.WebPDecodeRGBA.restype = ctypes.c_void_p
+    _W.WebPDecodeRGBA.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    _W.WebPFree.argtypes = [ctypes.c_void_p]
+except OSError:  # the GPU box image may lack it
+    _W = None
+
+
+def _alpha_img(w, h, color):
+    rgba = synth_rgba(w, h, 0x5EED0042)
+    yy, xx = np.mgrid[0:h, 0:w]
+    rgba[..., 3] = np.where((xx // 7 + yy // 5) % 3 == 0, 255, (xx * 3 + yy) & 255).astype(np.uint8)
+    if color == zwebp.ColorType.La8:
+        return np.ascontiguousarray(rgba[..., [0, 3]])
+    return rgba
+
+
+@pytest.mark.parametrize("color", [zwebp.ColorType.Rgba8, zwebp.ColorType.La8])
+@pytest.mark.parametrize("w,h", [(160, 96), (333, 211), (1920, 1080)])
+def test_webp_container_alpha(ctx, color, w, h):
+    img = _alpha_img(w, h, color)
+    rc, vp8, _ = O.encode(img, w, h, color, 75, 4)
+    assert rc == 0
+    rc, alph = O.encode_alpha(img, w, h, color)
+    assert rc == 0
+    want = _riff(_vp8x(w, h, 0x10), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8))
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    got = bytes(enc.encode(img, w, h, color))
+    assert got == want
+    # with metadata: VP8X flags ICC|alpha|EXIF|XMP, ICCP before ALPH, EXIF/XMP after VP8
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    enc.set_icc_profile(b"icc!")
+    enc.set_exif_metadata(b"exif-data")
+    enc.set_xmp_metadata(b"<x/>")
+    got = bytes(enc.encode(img, w, h, color))
+    assert got == _riff(_vp8x(w, h, 0x3C), _chunk(b"ICCP", b"icc!"), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8),
+                        _chunk(b"EXIF", b"exif-data"), _chunk(b"XMP ", b"<x/>"))
+    if _W is not None:
+        ww, hh = ctypes.c_int(), ctypes.c_int()
+        p = _W.WebPDecodeRGBA(got, len(got), ctypes.byref(ww), ctypes.byref(hh))
+        assert p and (ww.value, hh.value) == (w, h)
+        dec = np.ctypeslib.as_array((ctypes.c_uint8 * (w * h * 4)).from_address(p)).copy().reshape(h, w, 4)
+        _W.WebPFree(p)
+        assert np.array_equal(dec[..., 3], img[..., -1])
+
+
+def test_encode_webp_rgba_entry(ctx):
+    """zw_encode_webp (EncoderParams::lossy) for RGBA8 equals the _ex form."""
+    w, h = 200, 120
+    img = _alpha_img(w, h, zwebp.ColorType.Rgba8)
+    L = zwebp.load_library()
+    a = np.ascontiguousarray(img).reshape(-1)
+    out = zwebp._Bytes()
+    rc = L.zw_encode_webp(ctx.handle, a.ctypes.data, a.size, w, h, 3, 75, 4, ctypes.byref(out))
+    assert rc == 0
+    got = zwebp._take_bytes(L, out)
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    assert got == bytes(enc.encode(img, w, h, zwebp.ColorType.Rgba8))
+
+
+# --------------------------------------------------------------------------
+# row-parallel decode: a wave that gives up waiting fails the call
+# --------------------------------------------------------------------------
+def test_rows_decode_error_reported(ctx, monkeypatch):
+    w, h = 320, 240
+    img = synth_rgba(w, h, 0x5EED0050)
+    vp8 = zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    zwebp.vp8_decode_frame(vp8, ctx=ctx)  # fine without the hook
+    monkeypatch.setenv("ZW_DEC_FORCE_ERROR", "1")
+    monkeypatch.setenv("ZW_DEC_ROWS", "1")
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.vp8_decode_frame(vp8, ctx=ctx)
+    assert e.value.code == 4
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    y = np.zeros(mbw * mbh * 256, np.uint8)
+    u = np.zeros(mbw * mbh * 64, np.uint8)
+    v = np.zeros(mbw * mbh * 64, np.uint8)
+    with pytest.raises(zwebp.ZwError) as e:
+        zwebp.loop_filter_frame(y, u, v, mbw, mbh, np.zeros((mbw * mbh, 4), np.uint8), 0, 6, 0, ctx=ctx)
+    assert e.value.code == 4
+    monkeypatch.delenv("ZW_DEC_FORCE_ERROR")
+    zwebp.vp8_decode_frame(vp8, ctx=ctx)
