@@ -447,7 +447,9 @@ DI unsigned gmask(bool pred)
 // rcost<FIRST> with lane k holding c[k] (position n = k, quirk A1).  Result is
 // uniform across the group.  T->beob / T->binit are bitcost(0/1, p[0]) of the
 // current probabilities.
-template <int FIRST>
+// LC = false: the LevelCosts tables are all zero (pass 1, quirk A2), so their
+// lookups are skipped (the sum is the same).
+template <int FIRST, bool LC = true>
 DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
 {
     const unsigned m = gmask(v != 0);
@@ -456,7 +458,7 @@ DI uint32_t rcost_g(int v, int k, int ctx0, int ctype, const LdsTables* T)
     const int pav = shr1(av);
     const int ctx = k == FIRST ? ctx0 : min(pav, 2);
     // unconditional lookups with clamped indices, masked arithmetic (no branches)
-    const int tl = T->lfc[min(av, 2047)] + T->lc[ctype][band_of(k)][ctx][min(av, 67)];
+    const int tl = T->lfc[min(av, 2047)] + (LC ? (int)T->lc[ctype][band_of(k)][ctx][min(av, 67)] : 0);
     const int term = tl & -(int)(k >= FIRST && k <= last);
     const int lastc = max(last, 0);
     const int lastv = gget(av, lastc);
@@ -638,7 +640,7 @@ DI void fdct16_pk(const int* r, int* c)
 // rcost<FIRST> (get_residual_cost, cost.rs:1670) without branches: every
 // table lookup is issued, terms past the last nonzero are masked.  v[n] is
 // indexed by position n exactly as rcost (quirk A1); av[n] = |v[n]|.
-template <int FIRST>
+template <int FIRST, bool LC = true>
 DI uint32_t rcost_bf(const int* av, int ctx0, int ctype, const LdsTables* T)
 {
     uint32_t nzm = 0;
@@ -650,7 +652,7 @@ DI uint32_t rcost_bf(const int* av, int ctx0, int ctype, const LdsTables* T)
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
         const int ctx = n == FIRST ? ctx0 : min(av[n - 1], 2);
-        const int t = T->lfc[min(av[n], 2047)] + T->lc[ctype][kBand(n)][ctx][min(av[n], 67)];
+        const int t = T->lfc[min(av[n], 2047)] + (LC ? (int)T->lc[ctype][kBand(n)][ctx][min(av[n], 67)] : 0);
         cost += (uint32_t)(t & -(int)(n <= last));
     }
     int lastv = 0;

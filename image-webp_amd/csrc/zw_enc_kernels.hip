@@ -433,6 +433,7 @@ struct WaveLds {
     uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
     uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
     int8_t left_derr[4];
+    uint32_t uvc[32][12];         // pick_uv -> final_chroma: per (mode, block) coeffs (i16 pairs) + pred (u8 x4)
     int dc[64];
     int y2d[64];
     int y2cost[4];
@@ -517,6 +518,7 @@ __device__ void build_chroma_border(const Ctx& C)
 }
 
 // pick_best_intra16 (vp8.rs:1504-1687).  lane = mode*16 + block.
+template <int PASS>
 __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_score)
 {
     const int lane = C.lane, m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
@@ -567,7 +569,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
         dq[k] = m24(c[k] < 0 ? -aq[k] : aq[k], (int)S.y1.q[1]);
     }
     nzac = nzac != 0;
-    int cost = (int)rcost_bf<1>(aq, 0, 0, T);
+    int cost = (int)rcost_bf<1, PASS == 2>(aq, 0, 0, T);
     // Y2 in group form: lane (m, b) holds block b's DC under mode m
     int y2cost;
     {
@@ -575,7 +577,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
         const int t = b > 0;
         const int ay = (int)((__umul24((uint32_t)iabs(d), S.y2.iq[t]) + S.y2.bias[t]) >> 17);
         const int qy = d < 0 ? -ay : ay;
-        y2cost = (int)rcost_g<0>(qy, b, 0, 1, T);  // uniform within the mode's group
+        y2cost = (int)rcost_g<0, PASS == 2>(qy, b, 0, 1, T);  // uniform within the mode's group
         dq[0] = iwht_g(m24(qy, (int)S.y2.q[t]), b);
     }
     idct16(dq);
@@ -783,7 +785,7 @@ struct I4State {
 // Within one sub-block every candidate score sse*256 + u16(rate)*lambda_i4 is
 // below 2^29 (sse <= 16*255^2, lambda_i4 <= 1785), so score*4 + group is a
 // unique 32-bit key whose minimum is the reference's first strict minimum.
-template <int NB>
+template <int PASS, int NB>
 __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, int si0, int si1, int si2,
                                         uint32_t iqk, uint32_t biask, int qk, I4State& st)
 {
@@ -882,7 +884,7 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
             nzm[h] = gmask(qv[h] != 0);
         }
 #pragma unroll
-        for (int h = 0; h < NB; h++) cc[h] = rcost_g<0>(qv[h], k, nzc[h], 3, T);
+        for (int h = 0; h < NB; h++) cc[h] = rcost_g<0, PASS == 2>(qv[h], k, nzc[h], 3, T);
 #pragma unroll
         for (int h = 0; h < NB; h++) dq[h] = idct_g(m24(qv[h], qk), k);
 #pragma unroll
@@ -947,6 +949,7 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
 // block: "some raster prefix crossed the bound" is "the sum over every block
 // crossed it", so testing the sum of the blocks searched so far after each
 // step decides exactly as the reference does.
+template <int PASS>
 __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
 {
     const ZwSegment& S = *C.S;
@@ -969,9 +972,9 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
         const int sbxA = s - 2 * sbyA;
         if (s >= 2 && s <= 7) {
             const int bx[2] = {sbxA, sbxA - 2}, by[2] = {sbyA, sbyA + 1};
-            i4_step<2>(C, bx, by, K, si0, si1, si2, iqk, biask, qk, st);
+            i4_step<PASS, 2>(C, bx, by, K, si0, si1, si2, iqk, biask, qk, st);
         } else {
-            i4_step<1>(C, &sbxA, &sbyA, K, si0, si1, si2, iqk, biask, qk, st);
+            i4_step<PASS, 1>(C, &sbxA, &sbyA, K, si0, si1, si2, iqk, biask, qk, st);
         }
         if (st.running >= i16_score) return false;
         if (st.total_mc > 256u * 16u * 16u / 4u) return false;
@@ -1028,6 +1031,10 @@ __device__ __forceinline__ void uv_block(const Ctx& C, int b, int mode, int dcU,
 
 // pick_best_uv (vp8.rs:2050-2200): lane = mode*8 + block (U 0..3, V 4..7),
 // one whole block per lane; lanes 32..63 shadow 0..31 (results unused).
+// Lane l < 32 leaves its block's coefficients (i16 pairs) and prediction
+// (packed u8) in W->uvc[l], so final_chroma starts from the chosen mode's
+// transform instead of recomputing it.
+template <int PASS>
 __device__ int pick_uv(const Ctx& C)
 {
     const ZwSegment& S = *C.S;
@@ -1039,6 +1046,15 @@ __device__ int pick_uv(const Ctx& C)
     const int m = (l >> 3) & 3, b = l & 7;
     int pr[16], sv[16], c[16];
     uv_block(C, b, m, dcU, dcV, pr, sv, c);
+    if (l < 32) {
+        uint32_t* e = C.W->uvc[l];
+#pragma unroll
+        for (int k = 0; k < 8; k++) e[k] = pack_lo(c[2 * k], c[2 * k + 1]);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            e[8 + k] = (uint32_t)pr[4 * k] | ((uint32_t)pr[4 * k + 1] << 8) | ((uint32_t)pr[4 * k + 2] << 16) |
+                       ((uint32_t)pr[4 * k + 3] << 24);
+    }
     int aq[16], rr[16], nzac = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -1047,7 +1063,7 @@ __device__ int pick_uv(const Ctx& C)
         if (k > 0) nzac += min(aq[k], 1);
         rr[k] = m24(c[k] < 0 ? -aq[k] : aq[k], (int)S.uv.q[t]);
     }
-    int cost = (int)rcost_bf<0>(aq, 0, 2, T);
+    int cost = (int)rcost_bf<0, PASS == 2>(aq, 0, 2, T);
     idct16(rr);
     int sse = 0;
 #pragma unroll
@@ -1284,16 +1300,25 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
     const ZwSegment& S = *C.S;
     const int l = C.lane;
     const int b = l & 7, pl = b >> 2, bb = b & 3, bx = bb & 1, by = bb >> 1;
-    int dcU, dcV;
-    uv_dc_preds(C, dcU, dcV);
-    int pr[16], sv[16], c[16];
-    uv_block(C, b, mode, dcU, dcV, pr, sv, c);
+    // the chosen mode's prediction and coefficients, left by pick_uv
+    int pr[16], c[16];
+    {
+        const uint32_t* e = W->uvc[mode * 8 + b];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t v = e[k];
+            c[2 * k] = (int)(int16_t)(v & 0xffffu);
+            c[2 * k + 1] = (int)(int16_t)(v >> 16);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) pr[k] = (int)((e[8 + (k >> 2)] >> (8 * (k & 3))) & 255u);
+    }
     // DC error diffusion (vp8.rs chroma quirk, per plane: blocks 0,1,2,3 in
     // order), on the scalar unit; the adjusted DCs go back to their lanes.
     {
         const int q = (int)S.uv.q[0];
         const uint32_t iq = S.uv.iq[0], bias = S.uv.bias[0];
-        const uint32_t zt = ((1u << 17) - 1 - bias) / iq;
+        const uint32_t zt = S.uv.zthresh[0];  // ((1 << 17) - 1 - bias) / iq, matrix_init
         int dcs[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) dcs[k] = __builtin_amdgcn_readlane(c[0], k);
@@ -1570,7 +1595,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 else if (mby + 1 < mbh) nx = fetch_mb(&a, lane, 0, mby + 1);
                 setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
                 build_chroma_border(C);
-                const int cm = pick_uv(C);
+                const int cm = pick_uv<PASS>(C);
                 PH_MARK(8);
                 int uvnz[8];
                 final_chroma(C, cm, top_derr + mbx * 4, uvnz);
@@ -1620,13 +1645,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             build_luma_border(C, 0);
             int lm;
             unsigned long long i16s;
-            pick_i16(C, lm, i16s);
+            pick_i16<PASS>(C, lm, i16s);
             wsync();
             PH_MARK(1);
             int cm = 0;
             if (PASS == 2) {
                 build_chroma_border(C);
-                cm = pick_uv(C);
+                cm = pick_uv<PASS>(C);
             }
             PH_MARK(3);
             if (C.method > 1) {
@@ -1634,7 +1659,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 if (C.method >= 5 || i16s > thr || lm != 0) {
                     if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
                     build_luma_border(C, 1);
-                    if (pick_i4(C, i16s)) lm = 4;
+                    if (pick_i4<PASS>(C, i16s)) lm = 4;
                 }
             }
             PH_MARK(2);

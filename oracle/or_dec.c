@@ -553,3 +553,15 @@ void or_i4_preds_edge_c(const uint8_t e[13], uint8_t out[160])
     for (int i = 0; i < 4; i++) ws[(y0 + i) * OR_BPS + x0 - 1] = e[3 - i];
     or_i4_preds(ws, x0, y0, OR_BPS, (uint8_t(*)[16])out);
 }
+
+/* Known-answer-test entry point for the bool decoder (bit_reader.rs /
+ * arithmetic.rs tests): ops[i] > 0 reads a bool with that probability,
+ * ops[i] < 0 a literal of -ops[i] bits; out[i] receives the value.  Returns the
+ * reader's eof flag after the reads. */
+int or_bool_read_kat(const uint8_t *data, size_t len, const int *ops, int nops, int *out)
+{
+    br_t b;
+    br_init(&b, data, len);
+    for (int i = 0; i < nops; i++) out[i] = ops[i] > 0 ? br_bit(&b, ops[i]) : br_lit(&b, -ops[i]);
+    return b.eof;
+}

@@ -1985,3 +1985,27 @@ void or_quant_blocks_c(int n, const int32_t *coeffs, const uint8_t *ctx0, int ct
 uint32_t or_fixed_cost_i16(int mode) { return FIXED_COSTS_I16[mode]; }
 uint32_t or_fixed_cost_uv(int mode) { return FIXED_COSTS_UV[mode]; }
 int or_filter_level_for_quality(int quality) { return compute_filter_level(or_quality_to_quant_index(quality), 0, 50); }
+
+/* ======================================================================== */
+/* Known-answer-test entry points (tests/test_oracle.py pins these against  */
+/* the reference's own in-crate tests).                                     */
+/* ======================================================================== */
+float or_fm_roundf(float x) { return (float)(int32_t)(x + 0.5f); } /* fast_math.rs:8 */
+double or_fm_round(double x) { return fm_round(x); }
+double or_fm_cbrt(double x) { return fm_cbrt(x); }
+double or_fm_pow(double x, double n) { return fm_pow(x, n); }
+uint64_t or_rd_score(uint32_t sse, uint32_t rate, uint32_t lambda) { return rd_score(sse, (uint16_t)rate, lambda); }
+int or_t_transform(const uint8_t *in, int stride, const uint16_t w[16]) { return t_xform(in, stride, w); }
+/* Segment::init_matrices with every quantizer = q (so qi4 = qi16 = quv = q):
+ * out = {l_i4, l_i16, l_uv, l_mode, lt_i4, lt_i16, lt_uv, tlambda} */
+void or_seg_lambdas(uint32_t q, uint32_t out[8])
+{
+    seg_t s;
+    memset(&s, 0, sizeof s);
+    s.ydc = s.yac = s.y2dc = s.y2ac = s.uvdc = s.uvac = (int16_t)q;
+    seg_init(&s);
+    const uint32_t v[8] = {s.l_i4, s.l_i16, s.l_uv, s.l_mode, s.lt_i4, s.lt_i16, s.lt_uv, s.tlambda};
+    memcpy(out, v, sizeof v);
+}
+/* add_residue (prediction.rs:138) on a 4x4 block of stride 4 */
+void or_add_residue_kat(uint8_t pblock[16], const int32_t r[16]) { or_add_residue(pblock, r, 0, 0, 4); }

@@ -115,6 +115,16 @@ void or_quant_blocks_c(int n, const int32_t *coeffs, const uint8_t *ctx0, int ct
 uint32_t or_fixed_cost_i16(int mode);
 uint32_t or_fixed_cost_uv(int mode);
 size_t or_debug_struct_size(void);
+/* known-answer-test entry points (fast_math.rs, cost.rs, prediction.rs, bit_reader.rs) */
+float or_fm_roundf(float x);
+double or_fm_round(double x);
+double or_fm_cbrt(double x);
+double or_fm_pow(double x, double n);
+uint64_t or_rd_score(uint32_t sse, uint32_t rate, uint32_t lambda);
+int or_t_transform(const uint8_t *in, int stride, const uint16_t w[16]);
+void or_seg_lambdas(uint32_t q, uint32_t out[8]);
+void or_add_residue_kat(uint8_t pblock[16], const int32_t r[16]);
+int or_bool_read_kat(const uint8_t *data, size_t len, const int *ops, int nops, int *out);
 void or_i4_preds_edge_c(const uint8_t e[13], uint8_t out[160]);
 
 #ifdef __cplusplus

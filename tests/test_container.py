@@ -74,3 +74,26 @@ def test_out_of_scope_forms():
     with pytest.raises(zwebp.DecodingError) as e:
         zwebp.webp_parse(_riff(_vp8x(8, 8)))
     assert e.value.code == 20
+
+
+def test_add_with_overflow_size():
+    """decoder/api.rs:1153 add_with_overflow_size: a RIFF file whose chunk sizes
+    overflow when added must be rejected with an error, not crash."""
+    b = bytes([0x52, 0x49, 0x46, 0x46, 0xaf, 0x37, 0x80, 0x47, 0x57, 0x45, 0x42, 0x50, 0x6c, 0x64, 0x00, 0x00, 0xff,
+               0xff, 0xff, 0xff, 0xfb, 0x7e, 0x73, 0x00, 0x06, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x05, 0x00,
+               0x00, 0x00, 0x65, 0x65, 0x65, 0x65, 0x65, 0x65, 0x40, 0xfb, 0xff, 0xff, 0x65, 0x65, 0x65, 0x65, 0x65,
+               0x65, 0x65, 0x65, 0x65, 0x65, 0x00, 0x00, 0x00, 0x00, 0x62, 0x00, 0x10, 0x00, 0x00, 0x00, 0x00, 0x00,
+               0x00, 0x49, 0x49, 0x54, 0x55, 0x50, 0x4c, 0x54, 0x59, 0x50, 0x45, 0x33, 0x37, 0x44, 0x4d, 0x46])
+    with pytest.raises(zwebp.DecodingError):
+        zwebp.webp_parse(b)
+    for cut in range(0, len(b), 7):  # and every truncation of it
+        with pytest.raises(zwebp.DecodingError):
+            zwebp.webp_parse(b[:cut])
+
+
+def test_single_colour_files_parse():
+    """decoder/api.rs:1166-1212 imagemagick 2x2 / 3x3 red files: WebPDecoder::new facts."""
+    from test_oracle import imagemagick_red
+    for n in (2, 3):
+        info = zwebp.webp_parse(imagemagick_red(n))
+        assert (info["width"], info["height"]) == (n, n) and info["is_lossy"] and not info["has_alpha"]

@@ -165,3 +165,26 @@ def test_rows_decode_error_reported(ctx, monkeypatch):
     assert e.value.code == 4
     monkeypatch.delenv("ZW_DEC_FORCE_ERROR")
     zwebp.vp8_decode_frame(vp8, ctx=ctx)
+
+
+# --------------------------------------------------------------------------
+# decoder/api.rs:1166-1212: the reference's single-colour imagemagick files
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [2, 3])
+def test_single_colour_files_decode(ctx, n):
+    """WebPDecoder::read_image on the 2x2 / 3x3 red files: every pixel equal
+    (the odd tail included) and equal to the oracle's decode."""
+    from test_oracle import imagemagick_red
+    f = imagemagick_red(n)
+    dec = zwebp.WebPDecoder(f, ctx=ctx)
+    assert dec.dimensions() == (n, n)
+    rgb = dec.read_image().reshape(-1, 3)
+    assert (rgb == rgb[0]).all()
+    vp8 = f[20:20 + int.from_bytes(f[16:20], "little")]
+    rc, r = O.decode(vp8)
+    assert rc == 0
+    ys, cs = r["mbw"] * 16, r["mbw"] * 8
+    c = (n + 1) // 2
+    ref = O.yuv_to_rgb_fancy(r["y"].reshape(-1, ys)[:n, :n].reshape(-1), r["u"].reshape(-1, cs)[:c, :c].reshape(-1),
+                             r["v"].reshape(-1, cs)[:c, :c].reshape(-1), n, n).reshape(-1, 3)
+    assert np.array_equal(rgb, ref)

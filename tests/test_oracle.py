@@ -8,6 +8,14 @@ Reference KATs restated (values are the reference tests' own data):
   encoder/cost.rs:2046-2069   fixed mode costs
   decoder/yuv.rs:905-971      fancy upsampling grid + yuv_to_rgb
   tests/decode.rs             gallery goldens (tests/golden/decode_golden.json)
+  common/prediction.rs:959-1091  add_residue, bhepred / brdpred / bldpred / bvepred
+  encoder/fast_math.rs:129-190   roundf, round, cbrt, pow
+  encoder/cost.rs:2088-2135      lambda formulas, i4 penalty, rd_score
+  encoder/cost.rs t_transform    (common/simd_sse.rs:879-918 scalar basic / uniform)
+  decoder/arithmetic.rs:673-709  bool decoder "hel" / "hello world" literals
+  decoder/bit_reader.rs:678-777  EOF behaviour; flag / bool reads equal to a second,
+                                 independent (RFC 6386) bool decoder
+  decoder/api.rs:1153-1212       imagemagick 2x2 / 3x3 single-colour lossy files
 """
 import ctypes
 import hashlib
@@ -50,11 +58,20 @@ def test_idct_sse2_saturation_differs_only_out_of_i16():
     assert not np.array_equal(O.blocks("or_idct_c", b), O.blocks("or_idct_scalar_c", b))
 
 
-def test_wht_roundtrip_dc_only():
+def test_wht_kat_and_roundtrip():
+    """wht4x4 (transform.rs:116) of a lone DC of 16 spreads 8 to every output
+    (rows 16,16,16,16; columns (16 + 1) / 2); iwht4x4 (:82) inverts wht4x4
+    exactly on even inputs (the encoder's DCs are sums of 16 residuals x 8)
+    and within 1 on odd ones."""
+    one = np.zeros(16, np.int32)
+    one[0] = 16
+    assert np.array_equal(O.blocks("or_wht_c", one).reshape(-1), np.full(16, 8, np.int32))
     rng = np.random.default_rng(3)
-    dc = rng.integers(-2000, 2000, size=(1000, 16)).astype(np.int32) * 8
-    w = O.blocks("or_wht_c", dc)
-    assert w.shape == dc.shape
+    dc = rng.integers(-2000, 2000, size=(1000, 16)).astype(np.int32)
+    back = O.blocks("or_iwht_c", O.blocks("or_wht_c", dc * 2))
+    assert np.array_equal(back, dc * 2)
+    back = O.blocks("or_iwht_c", O.blocks("or_wht_c", dc))
+    assert np.abs(back - dc).max() <= 1
 
 
 def _bool_kat(ops):
@@ -199,3 +216,231 @@ def test_oracle_encoder_errors():
     assert O.encode(img, 0, 16, 3)[0] != 0
     assert O.encode(img[:8], 16, 16, 3)[0] != 0
     assert O.encode(img, 16, 16, 3, quality=101)[0] != 0
+
+
+# --------------------------------------------------------------------------
+# common/prediction.rs:959-1091
+# --------------------------------------------------------------------------
+def test_add_residue_kat():
+    """test_add_residue: pred + residual clamped to [0, 255]."""
+    p = np.arange(1, 17, dtype=np.uint8)
+    r = np.array([-1, -2, -3, -4, 250, 249, 248, 250, -10, -18, -192, -17, -3, 15, 18, 9], np.int32)
+    O.lib().or_add_residue_kat(O._p(p), O._p(r))
+    assert list(p) == [0, 0, 0, 0, 255, 255, 255, 255, 0, 0, 0, 0, 10, 29, 33, 25]
+
+
+def _i4_preds(L=(0, 0, 0, 0), P=0, A=(0,) * 8):
+    """All 10 I4 predictions (I4Predictions::compute, prediction.rs:568) from the
+    edge E = [L3 L2 L1 L0 P A0..A7]; mode order DC TM VE HE LD RD VR VL HD HU."""
+    e = np.array([L[3], L[2], L[1], L[0], P] + list(A), np.uint8)
+    out = np.zeros(160, np.uint8)
+    O.lib().or_i4_preds_edge_c(O._p(e), O._p(out))
+    return out.reshape(10, 4, 4)
+
+
+def test_predict_bhepred_kat():
+    """test_predict_bhepred: corner 5, left column 4,3,2,1 -> rows 4,3,2,1."""
+    got = _i4_preds(L=(4, 3, 2, 1), P=5)[3]
+    assert got.tolist() == [[4] * 4, [3] * 4, [2] * 4, [1] * 4]
+
+
+def test_predict_brdpred_kat():
+    """test_predict_brdpred: a linear ramp stays a ramp (rows 5..8, 4..7, 3..6, 2..5)."""
+    got = _i4_preds(L=(4, 3, 2, 1), P=5, A=(6, 7, 8, 9, 0, 0, 0, 0))[5]
+    assert got.tolist() == [[5, 6, 7, 8], [4, 5, 6, 7], [3, 4, 5, 6], [2, 3, 4, 5]]
+
+
+def test_predict_bldpred_kat():
+    """test_predict_bldpred: top row 1..8 -> avg3 diagonals 2..8."""
+    got = _i4_preds(A=(1, 2, 3, 4, 5, 6, 7, 8))[4]
+    assert got.tolist() == [[2, 3, 4, 5], [3, 4, 5, 6], [4, 5, 6, 7], [5, 6, 7, 8]]
+
+
+def test_predict_bvepred_kat():
+    """test_predict_bvepred: corner 1, top row 2..9 -> every row avg3 = 2,3,4,5."""
+    got = _i4_preds(P=1, A=(2, 3, 4, 5, 6, 7, 8, 9))[2]
+    assert got.tolist() == [[2, 3, 4, 5]] * 4
+
+
+# --------------------------------------------------------------------------
+# encoder/fast_math.rs:129-190
+# --------------------------------------------------------------------------
+def _fm():
+    L = O.lib()
+    L.or_fm_roundf.restype, L.or_fm_roundf.argtypes = ctypes.c_float, [ctypes.c_float]
+    for n in ("or_fm_round", "or_fm_cbrt"):
+        getattr(L, n).restype, getattr(L, n).argtypes = ctypes.c_double, [ctypes.c_double]
+    L.or_fm_pow.restype, L.or_fm_pow.argtypes = ctypes.c_double, [ctypes.c_double, ctypes.c_double]
+    return L
+
+
+def test_fast_math_round_kat():
+    L = _fm()
+    for x, e in [(0.0, 0.0), (0.4, 0.0), (0.5, 1.0), (0.6, 1.0), (1.5, 2.0), (75.4, 75.0), (75.5, 76.0)]:
+        assert L.or_fm_roundf(x) == e
+    for x, e in [(0.0, 0.0), (0.4, 0.0), (0.5, 1.0), (127.0 * 0.5, 64.0)]:
+        assert L.or_fm_round(x) == e
+
+
+def test_fast_math_cbrt_kat():
+    L = _fm()
+    for x, e in [(0.0, 0.0), (1.0, 1.0), (8.0, 2.0), (27.0, 3.0), (0.125, 0.5), (0.001, 0.1)]:
+        assert abs(L.or_fm_cbrt(x) - e) < 1e-10
+
+
+def test_fast_math_pow_kat():
+    L = _fm()
+    assert L.or_fm_pow(0.0, 2.0) == 0.0 and L.or_fm_pow(1.0, 5.0) == 1.0
+    assert L.or_fm_pow(2.0, 0.0) == 1.0 and L.or_fm_pow(2.0, 1.0) == 2.0
+    for x, n, e in [(0.5, 1.0, 0.5), (0.5, 2.0, 0.25), (0.5, 0.5, 0.707_106_781), (0.8, 0.9, 0.821_871_788),
+                    (0.3, 1.1, 0.268_269_580)]:
+        assert abs(L.or_fm_pow(x, n) - e) / max(abs(e), 1e-10) < 0.01  # the reference's 1 % bound
+
+
+# --------------------------------------------------------------------------
+# encoder/cost.rs:2088-2135 (lambdas, rd_score) and t_transform
+# --------------------------------------------------------------------------
+def test_lambda_formulas_kat():
+    """test_lambda_calculation / test_i4_penalty at q = 64, through the oracle's
+    Segment::init_matrices (every quantizer 64, so qi4 = qi16 = quv = 64)."""
+    out = np.zeros(8, np.uint32)
+    O.lib().or_seg_lambdas(64, O._p(out))
+    l_i4, l_i16, l_uv, l_mode, lt_i4, lt_i16, lt_uv, tl = (int(v) for v in out)
+    assert l_i4 == (3 * 64 * 64) >> 7 and l_i16 == 3 * 64 * 64 and l_uv == (3 * 64 * 64) >> 6
+    assert l_i16 > l_i4 * 50 and l_i4 < l_uv < l_i16
+    assert l_mode == (64 * 64) >> 7 and lt_i4 == (7 * 64 * 64) >> 3 and lt_i16 == (64 * 64) >> 2
+    assert lt_uv == (64 * 64) << 1 and tl == (50 * 64) >> 5
+    O.lib().or_seg_lambdas(1, O._p(out))
+    assert list(out[:4]) == [1, 3, 1, 1]  # .max(1) floors
+
+
+def test_rd_score_kat():
+    """test_rd_score with LAMBDA_I16 = 106 and FIXED_COSTS_I16[0] = 663."""
+    L = O.lib()
+    L.or_rd_score.restype = ctypes.c_uint64
+    L.or_rd_score.argtypes = [ctypes.c_uint32] * 3
+    assert L.or_rd_score(0, 0, 106) == 0
+    assert L.or_rd_score(100, 0, 106) == 100 * 256
+    assert L.or_rd_score(0, 663, 106) == 663 * 106
+    assert L.or_rd_score(1000, 663, 106) == 1000 * 256 + 663 * 106
+    assert L.or_rd_score(0, 0x1_0005, 1) == 5  # the rate is a u16 (quirk A13)
+
+
+def test_t_transform_kat():
+    """simd_sse.rs:879-918: a gradient block gives a positive weighted Hadamard
+    magnitude; a uniform block only its DC term (16 x 100 with unit weights)."""
+    L = O.lib()
+    w = np.ones(16, np.uint16)
+    g = np.zeros(64, np.uint8)
+    for y in range(4):
+        for x in range(4):
+            g[y * 16 + x] = (y * 4 + x) * 10
+    assert L.or_t_transform(O._p(g), 16, O._p(w)) > 0
+    u = np.full(64, 128, np.uint8)
+    for y in range(4):
+        u[y * 16:y * 16 + 4] = 100
+    assert L.or_t_transform(O._p(u), 16, O._p(w)) == 1600
+
+
+# --------------------------------------------------------------------------
+# decoder/arithmetic.rs:673-712, decoder/bit_reader.rs:678-777
+# --------------------------------------------------------------------------
+def _bool_read(data, ops):
+    d = np.frombuffer(bytes(data), np.uint8)
+    o = np.array(ops, np.int32)
+    out = np.zeros(len(ops), np.int32)
+    eof = O.lib().or_bool_read_kat(O._p(d), d.size, O._p(o), len(ops), O._p(out))
+    return list(out), eof
+
+
+def test_bool_decoder_hello_kat():
+    """test_arithmetic_decoder_hello_short / _long (the values; the EOF rule is
+    ArithmeticDecoder::check's, not VP8BitReader's, and is covered below)."""
+    ops = [128, 10, 250, -1, -3, -8, -8]
+    assert _bool_read(b"hel", ops)[0] == [0, 1, 0, 1, 5, 64, 185]
+    got, eof = _bool_read(b"hello world", ops + [-8])
+    assert got == [0, 1, 0, 1, 5, 64, 185, 31] and not eof
+
+
+def test_bool_decoder_eof_kat():
+    """test_basic_reading: 50 flags of a 30-byte stream stay inside it;
+    test_short_data: 100 flags of 3 bytes run past the end."""
+    assert not _bool_read(b"hello world and some more text", [128] * 50)[1]
+    assert _bool_read(bytes([0x55, 0xAA, 0x55]), [128] * 100)[1]
+
+
+def _rfc6386_bools(data, probs):
+    """Independent bool decoder (RFC 6386 section 7.3, the ArithmeticDecoder the
+    reference compares VP8BitReader with): 2-byte window, bit-at-a-time shifts."""
+    value = (data[0] << 8) | data[1] if len(data) > 1 else data[0] << 8
+    pos, rng, bit_count, out = 2, 255, 0, []
+    for p in probs:
+        split = 1 + (((rng - 1) * p) >> 8)
+        big = split << 8
+        if value >= big:
+            b, rng, value = 1, rng - split, value - big
+        else:
+            b, rng = 0, split
+        while rng < 128:
+            value <<= 1
+            rng <<= 1
+            bit_count += 1
+            if bit_count == 8:
+                bit_count = 0
+                if pos < len(data):
+                    value |= data[pos]
+                pos += 1
+        out.append(b)
+    return out
+
+
+def test_bool_decoder_matches_rfc_decoder():
+    """test_compare_with_arithmetic_decoder / test_compare_various_probs."""
+    d = bytes((i * 17 + 31) & 255 for i in range(256))
+    assert _bool_read(d, [128] * 100)[0] == _rfc6386_bools(d, [128] * 100)
+    d = bytes((i * 13 + 7) & 255 for i in range(512))
+    probs = [p for p in (1, 10, 50, 100, 128, 150, 200, 240, 254) for _ in range(20)]
+    assert _bool_read(d, probs)[0] == _rfc6386_bools(d, probs)
+
+
+# --------------------------------------------------------------------------
+# decoder/api.rs:1153-1212: single-colour imagemagick files
+# --------------------------------------------------------------------------
+IM_RED = [0x52, 0x49, 0x46, 0x46, 0x3c, 0x00, 0x00, 0x00, 0x57, 0x45, 0x42, 0x50, 0x56, 0x50, 0x38, 0x20, 0x30, 0x00,
+          0x00, 0x00, 0xd0, 0x01, 0x00, 0x9d, 0x01, 0x2a, None, 0x00, None, 0x00, 0x02, 0x00, 0x34, 0x25, 0xa0, 0x02,
+          0x74, 0xba, 0x01, 0xf8, 0x00, 0x03, 0xb0, 0x00, 0xfe, 0xf0, 0xc4, 0x0b, 0xff, 0x20, 0xb9, 0x61, 0x75, 0xc8,
+          0xd7, 0xff, 0x20, 0x3f, 0xe4, 0x07, 0xfc, 0x80, 0xff, 0xf8, 0xf2, 0x00, 0x00, 0x00]
+
+
+def imagemagick_red(n):
+    """`convert -size NxN xc:#f00 red.webp` bytes from the reference's tests (N = 2, 3)."""
+    return bytes(n if b is None else b for b in IM_RED)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_single_colour_file_kat(n):
+    """decode_2x2/3x3_single_color_image: every decoded RGB pixel is the same
+    (the odd 3x3 tail included); libwebp decodes the same pixels."""
+    f = imagemagick_red(n)
+    vp8 = f[20:20 + int.from_bytes(f[16:20], "little")]
+    rc, r = O.decode(vp8)
+    assert rc == 0
+    ys, cs = r["mbw"] * 16, r["mbw"] * 8
+    Y = _crop(r["y"], ys, n, n).reshape(-1)
+    U = _crop(r["u"], cs, (n + 1) // 2, (n + 1) // 2).reshape(-1)
+    V = _crop(r["v"], cs, (n + 1) // 2, (n + 1) // 2).reshape(-1)
+    rgb = O.yuv_to_rgb_fancy(Y, U, V, n, n).reshape(-1, 3)
+    assert (rgb == rgb[0]).all()
+    try:
+        W = ctypes.CDLL("libwebp.so.7")
+    except OSError:
+        return
+    W.WebPDecodeRGB.restype = ctypes.c_void_p
+    W.WebPDecodeRGB.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    ww, hh = ctypes.c_int(), ctypes.c_int()
+    p = W.WebPDecodeRGB(f, len(f), ctypes.byref(ww), ctypes.byref(hh))
+    assert p
+    lw = np.ctypeslib.as_array((ctypes.c_uint8 * (n * n * 3)).from_address(p)).copy().reshape(-1, 3)
+    W.WebPFree.argtypes = [ctypes.c_void_p]
+    W.WebPFree(p)
+    assert np.array_equal(lw, rgb)
