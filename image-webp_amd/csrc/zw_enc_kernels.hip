@@ -16,11 +16,23 @@
 // and runs on wave 0 while waves 1..NW-1 do the luma wavefront.
 #include "zw_dev.h"
 
-#ifndef ZW_NW
-#define ZW_NW 8
+// Waves per workgroup of each encode pass.  Both kernels stay within 168
+// VGPRs, so three waves share each SIMD (12 per CU); ZW_NW sets both.
+#ifdef ZW_NW
+#define ZW_NW1 ZW_NW
+#define ZW_NW2 ZW_NW
 #endif
-#define NW ZW_NW
-#define WG (NW * 64)
+#ifndef ZW_NW1
+#define ZW_NW1 12
+#endif
+#ifndef ZW_NW2
+#define ZW_NW2 12
+#endif
+#define NW_MAX (ZW_NW1 > ZW_NW2 ? ZW_NW1 : ZW_NW2)
+template <int PASS> struct PassShape {
+    static constexpr int NW = PASS == 1 ? ZW_NW1 : ZW_NW2;
+    static constexpr int WG = NW * 64;
+};
 
 // ---------------------------------------------------------------------------
 // RGB(A)/L(A) -> padded YUV420.  One thread per chroma sample; it produces the
@@ -433,7 +445,7 @@ struct WaveLds {
     uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
     uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
     int8_t left_derr[4];
-    uint32_t uvc[32][12];         // pick_uv -> final_chroma: per (mode, block) coeffs (i16 pairs) + pred (u8 x4)
+    uint32_t uvc[64][8];          // pick_uv -> final_chroma, per lane: its coefficients (i16 pairs) + rows' pred
     int dc[64];
     int y2d[64];
     int y2cost[4];
@@ -447,9 +459,6 @@ struct WaveLds {
 #endif
 };
 
-struct SharedHdr {
-    int progress[NW];
-};
 
 struct Ctx {
     const EncArgs* a;
@@ -982,6 +991,145 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Chroma in lane-pair form.  A 4x4 chroma block is worked by two lanes, l and
+// l ^ 32 (half h = l >> 5): the pixel rows 2h, 2h+1 for prediction, residual,
+// the fDCT row pass, the iDCT row pass and the reconstruction, the coefficient
+// columns 2h, 2h+1 for the fDCT column pass, quantisation, rate and the iDCT
+// column pass.  The halves trade intermediate values with v_permlane32_swap
+// (four swaps per transform), so each lane does half of a block's arithmetic
+// and the search over 4 modes x 8 blocks fills all 64 lanes.  Pixel rows are
+// held as i16 pairs (x0, x1), (x3, x2) (the fdct16_pk layout).
+// ---------------------------------------------------------------------------
+// Both halves' copies of v: r[0] holds the lower half's value in every lane of
+// the upper half, r[1] the upper half's in every lane of the lower half.
+__device__ __forceinline__ int hx_partner(int v)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (__lane_id() < 32) ? (int)r[1] : (int)r[0];
+}
+__device__ __forceinline__ int hx_sum(int v)  // v(l) + v(l ^ 32), in both lanes
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (int)r[0] + (int)r[1];
+}
+DI uint32_t clamp_pk(uint32_t v)  // per i16 half: clamp to [0, 255]
+{
+    const zs2 z = {0, 0}, m = {255, 255};
+    return as_zu(__builtin_elementwise_min(__builtin_elementwise_max(as_zs2(v), z), m));
+}
+DI uint32_t add_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) + as_zs2(b)); }
+DI uint32_t sub_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) - as_zs2(b)); }
+DI int dot2v(uint32_t a, uint32_t b, int acc)  // v_dot2_i32_i16, both operands in VGPRs
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(acc));
+    return d;
+}
+DI int lo16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
+DI int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
+
+// The lane's two pixel rows of chroma block (bx, by) under 8x8 mode m (0 DC,
+// 1 V, 2 H, 3 TM; predict_dcpred / vpred / hpred / tmpred): pred(i, j) =
+// clamp(rowv(i) + colv(j)) with (rowv, colv) = (dc, 0) / (0, T[j]) / (L[i], 0)
+// / (L[i] - P, T[j]); source and prediction as i16 pairs.
+DI void uv_rows_pk(const uint8_t* w, const uint8_t* sblk, int bx, int by, int h, int m, int dc, uint32_t s01[2],
+                   uint32_t s32[2], uint32_t p01[2], uint32_t p32[2])
+{
+    const int cm = -(int)(m & 1), rm = -(int)(m >= 2);
+    const int P = w[0];
+    const int ro = csel(m == 0, dc, csel(m == 3, -P, 0));
+    const uint8_t* tp = w + 1 + bx * 4;
+    const uint32_t c01 = pack_lo(tp[0] & cm, tp[1] & cm), c32 = pack_lo(tp[3] & cm, tp[2] & cm);
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int y = 2 * h + r;
+        const int rv = (w[(by * 4 + y + 1) * ZW_BPS] & rm) + ro;
+        const uint32_t rvv = pack_lo(rv, rv);
+        p01[r] = clamp_pk(add_pk(c01, rvv));
+        p32[r] = clamp_pk(add_pk(c32, rvv));
+        const uint32_t sw = *(const uint32_t*)(sblk + y * 8);
+        s01[r] = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
+        s32[r] = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
+    }
+}
+
+// dct4x4 (transform.rs:176) of the pair's block: this lane's coefficients of
+// columns 2h, 2h+1, cf[col][row] = coefficient (row, 2h + col).
+DI void fdct_pair(const uint32_t s01[2], const uint32_t s32[2], const uint32_t p01[2], const uint32_t p32[2], int h,
+                  int cf[2][4])
+{
+    // row pass (fdct16_pk first stage), outputs of this lane's columns (own*)
+    // and of the partner's columns (oth*)
+    const zs2 k8p = {8, 8}, k8m = {8, -8}, k1a = {10704, 4434}, k1b = {4434, -10704};
+    const uint32_t kA0 = h ? as_zu(k8m) : as_zu(k8p), kA1 = h ? as_zu(k8p) : as_zu(k8m);
+    const uint32_t kD0 = h ? as_zu(k1b) : as_zu(k1a), kD1 = h ? as_zu(k1a) : as_zu(k1b);
+    const int rD0 = h ? 1875 : 3625, rD1 = h ? 3625 : 1875;
+    int own0[2], own1[2], oth0[2], oth1[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t R01 = sub_pk(s01[r], p01[r]), R32 = sub_pk(s32[r], p32[r]);
+        const uint32_t A = add_pk(R01, R32), D = sub_pk(R01, R32);
+        own0[r] = dot2v(A, kA0, 0);
+        oth0[r] = dot2v(A, kA1, 0);
+        own1[r] = dot2v(D, kD0, rD0) >> 10;
+        oth1[r] = dot2v(D, kD1, rD1) >> 10;
+    }
+    // the partner's rows of this lane's columns
+    const uint32_t g0 = (uint32_t)hx_partner((int)pack_lo(oth0[0], oth0[1]));
+    const uint32_t g1 = (uint32_t)hx_partner((int)pack_lo(oth1[0], oth1[1]));
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int* ow = c ? own1 : own0;
+        const uint32_t g = c ? g1 : g0;
+        // column = rows (0, 1) and (3, 2): own rows are 2h, 2h+1, the partner's the others
+        const uint32_t fwd = pack_lo(ow[0], ow[1]), rev = pack_lo(ow[1], ow[0]);
+        const uint32_t grev = __builtin_amdgcn_alignbit(g, g, 16);
+        const uint32_t X01 = h ? g : fwd, X32 = h ? rev : grev;
+        const zs2 A = as_zs2(X01) + as_zs2(X32), D = as_zs2(X01) - as_zs2(X32);
+        cf[c][0] = dot2(A, k1p, 7) >> 4;
+        cf[c][2] = dot2(A, k1m, 7) >> 4;
+        cf[c][1] = (dot2(D, k2a, 12000) >> 16) + ((as_zu(D) & 0xffffu) != 0u ? 1 : 0);
+        cf[c][3] = dot2(D, k2b, 51000) >> 16;
+    }
+}
+
+// idct4x4 (transform.rs:19, i32 form of idct16) of the pair's dequantised
+// coefficients dq[col][row] (columns 2h, 2h+1), then the reconstruction
+// clamp(pred + residual) of this lane's two rows as i16 pairs (x0,x1),(x3,x2).
+DI void idct_recon_pair(const int dq[2][4], const uint32_t p01[2], const uint32_t p32[2], int h, uint32_t r01[2],
+                        uint32_t r32[2])
+{
+    uint32_t lo[2], hi[2];  // vertical pass of this lane's columns: rows (0,1), (2,3)
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int x0 = dq[c][0], x1 = dq[c][1], x2 = dq[c][2], x3 = dq[c][3];
+        const int a1 = x0 + x2, b1 = x0 - x2;
+        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
+        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
+        lo[c] = pack_lo(a1 + d1, b1 + c1);
+        hi[c] = pack_lo(b1 - c1, a1 - d1);
+    }
+    // the partner needs these columns at its rows, this lane the partner's columns at its own
+    const uint32_t g0 = (uint32_t)hx_partner((int)(h ? lo[0] : hi[0]));
+    const uint32_t g1 = (uint32_t)hx_partner((int)(h ? lo[1] : hi[1]));
+    const uint32_t m0 = h ? hi[0] : lo[0], m1 = h ? hi[1] : lo[1];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        // values of row 2h + r at columns 0..3
+        const int e0 = r ? hi16(m0) : lo16(m0), e1 = r ? hi16(m1) : lo16(m1);
+        const int f0 = r ? hi16(g0) : lo16(g0), f1 = r ? hi16(g1) : lo16(g1);
+        const int y0 = h ? f0 : e0, y1 = h ? f1 : e1, y2 = h ? e0 : f0, y3 = h ? e1 : f1;
+        const int a1 = y0 + y2, b1 = y0 - y2;
+        const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
+        const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
+        const int o0 = (a1 + d1 + 4) >> 3, o1 = (b1 + c1 + 4) >> 3, o2 = (b1 - c1 + 4) >> 3, o3 = (a1 - d1 + 4) >> 3;
+        r01[r] = clamp_pk(add_pk(pack_lo(o0, o1), p01[r]));
+        r32[r] = clamp_pk(add_pk(pack_lo(o3, o2), p32[r]));
+    }
+}
+
 // Chroma DC predictors of both planes (uniform values): lanes 0..15 sum U,
 // 16..31 V; lane i < 8 reads left pixel i, i >= 8 top pixel i - 8.
 __device__ __forceinline__ void uv_dc_preds(const Ctx& C, int& dcU, int& dcV)
@@ -997,83 +1145,113 @@ __device__ __forceinline__ void uv_dc_preds(const Ctx& C, int& dcU, int& dcV)
     dcV = (above | left) ? (sv + (1 << (shf - 1))) >> shf : 128;
 }
 
-// One chroma 4x4 block per lane: prediction (mode 0 DC, 1 TM... per
-// pick_best_uv's order: 0 DC, 1 V(top), 2 H(left), 3 TM), source pixels and
-// the forward transform.  b = block 0..7 (U 0..3, V 4..7).
-__device__ __forceinline__ void uv_block(const Ctx& C, int b, int mode, int dcU, int dcV, int* pr, int* sv, int* c)
-{
-    WaveLds* W = C.W;
-    const int pl = b >> 2, bb = b & 3, bx = bb & 1, by = bb >> 1;
-    const uint8_t* w = pl ? W->cv : W->cu;
-    const uint8_t* sp = (pl ? C.sV : C.sU) + (by * 4) * 8 + bx * 4;
-    const int dcp = pl ? dcV : dcU, corner = w[0];
-    int L[4], Tp[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        L[i] = w[(by * 4 + i + 1) * ZW_BPS];
-        Tp[i] = w[1 + bx * 4 + i];
-    }
-    int r[16];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t srow = *(const uint32_t*)(sp + i * 8);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int p = sel4(mode, dcp, Tp[j], L[i], clamp255(L[i] + Tp[j] - corner));
-            const int x = (int)((srow >> (8 * j)) & 255u);
-            pr[i * 4 + j] = p;
-            sv[i * 4 + j] = x;
-            r[i * 4 + j] = x - p;
-        }
-    }
-    fdct16_pk(r, c);
-}
-
-// pick_best_uv (vp8.rs:2050-2200): lane = mode*8 + block (U 0..3, V 4..7),
-// one whole block per lane; lanes 32..63 shadow 0..31 (results unused).
-// Lane l < 32 leaves its block's coefficients (i16 pairs) and prediction
-// (packed u8) in W->uvc[l], so final_chroma starts from the chosen mode's
-// transform instead of recomputing it.
+// pick_best_uv (vp8.rs:2050-2200): lane pair (l, l ^ 32) = mode * 8 + block
+// (U blocks 0..3, V 4..7).  Each lane leaves its coefficients (i16 pairs) and
+// its rows' prediction in W->uvc[lane], so final_chroma starts from the chosen
+// mode's transform instead of recomputing it.
 template <int PASS>
 __device__ int pick_uv(const Ctx& C)
 {
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
+    WaveLds* W = C.W;
     const int l = C.lane;
     const int above = C.mby != 0, left = C.mbx != 0;
     int dcU, dcV;
     uv_dc_preds(C, dcU, dcV);
-    const int m = (l >> 3) & 3, b = l & 7;
-    int pr[16], sv[16], c[16];
-    uv_block(C, b, m, dcU, dcV, pr, sv, c);
-    if (l < 32) {
-        uint32_t* e = C.W->uvc[l];
+    const int h = l >> 5, q = l & 31, m = q >> 3, b = q & 7;
+    const int pl = b >> 2, bx = b & 1, by = (b >> 1) & 1;
+    uint32_t s01[2], s32[2], p01[2], p32[2];
+    uv_rows_pk(pl ? W->cv : W->cu, (pl ? C.sV : C.sU) + by * 32 + bx * 4, bx, by, h, m, pl ? dcV : dcU, s01, s32, p01,
+               p32);
+    int cf[2][4];
+    fdct_pair(s01, s32, p01, p32, h, cf);
+    {
+        uint32_t* e = W->uvc[l];
 #pragma unroll
-        for (int k = 0; k < 8; k++) e[k] = pack_lo(c[2 * k], c[2 * k + 1]);
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            e[8 + k] = (uint32_t)pr[4 * k] | ((uint32_t)pr[4 * k + 1] << 8) | ((uint32_t)pr[4 * k + 2] << 16) |
-                       ((uint32_t)pr[4 * k + 3] << 24);
+        for (int c = 0; c < 2; c++) {
+            e[2 * c] = pack_lo(cf[c][0], cf[c][1]);
+            e[2 * c + 1] = pack_lo(cf[c][2], cf[c][3]);
+        }
+        e[4] = p01[0];
+        e[5] = p32[0];
+        e[6] = p01[1];
+        e[7] = p32[1];
     }
-    int aq[16], rr[16], nzac = 0;
+    // quantize_coeff (no sharpening, cost.rs:457); natural index n = 4 row + 2h + col
+    int dq[2][4], av[2][4];
+    unsigned nzbits = 0, big = 0;
+    int nzac = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int t = k > 0;
-        aq[k] = (int)((__umul24((uint32_t)iabs(c[k]), S.uv.iq[t]) + S.uv.bias[t]) >> 17);
-        if (k > 0) nzac += min(aq[k], 1);
-        rr[k] = m24(c[k] < 0 ? -aq[k] : aq[k], (int)S.uv.q[t]);
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool dcs = c == 0 && r == 0;  // natural index 2h: the DC when h == 0
+            const int t = dcs ? (int)(h != 0) : 1;
+            const uint32_t iq = dcs ? (h ? S.uv.iq[1] : S.uv.iq[0]) : S.uv.iq[1];
+            const uint32_t bias = dcs ? (h ? S.uv.bias[1] : S.uv.bias[0]) : S.uv.bias[1];
+            const int q_ = dcs ? (int)(h ? S.uv.q[1] : S.uv.q[0]) : (int)S.uv.q[1];
+            const int v = cf[c][r];
+            const int a = (int)((__umul24((uint32_t)iabs(v), iq) + bias) >> 17);
+            av[c][r] = a;
+            dq[c][r] = m24(v < 0 ? -a : a, q_);
+            const int n = 4 * r + 2 * h + c;
+            nzbits |= (unsigned)min(a, 1) << n;
+            big |= (unsigned)(a >= 2) << n;
+            nzac += t ? min(a, 1) : 0;
+        }
+    // get_residual_cost (cost.rs:1670), ctype 2, first 0, ctx0 0: terms of this
+    // lane's positions, then the pair's sum; head / tail from the pair's masks
+    nzbits |= (unsigned)hx_partner((int)nzbits);
+    big |= (unsigned)hx_partner((int)big);
+    const int last = 31 - __clz((int)nzbits);
+    int part = 0;
+    if (PASS == 2) {
+        // predecessor contexts from the partner's second column (2(1-h)+1), 2 bits per row
+        unsigned sc = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) sc |= (unsigned)min(av[1][r], 2) << (2 * r);
+        const unsigned rc = (unsigned)hx_partner((int)sc);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int n = 4 * r + 2 * h + c;
+                int ctx;
+                if (c == 1) ctx = min(av[0][r], 2);
+                else if (r == 0) ctx = h ? (int)(rc & 3u) : 0;  // n = 2: column 1 of row 0; n = 0: ctx0
+                else ctx = h ? (int)((rc >> (2 * r)) & 3u) : (int)((rc >> (2 * r - 2)) & 3u);
+                const int a = av[c][r];
+                const int tl = T->lfc[min(a, 2047)] + T->lc[2][band_of(n)][ctx][min(a, 67)];
+                part += tl & -(int)(n <= last);
+            }
+    } else {
+        // pass 1: the LevelCosts tables are zero (quirk A2) and lfc[0] == 0, so
+        // positions past the last nonzero level add nothing: no masks
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) part += T->lfc[min(av[c][r], 2047)];
     }
-    int cost = (int)rcost_bf<0, PASS == 2>(aq, 0, 2, T);
-    idct16(rr);
+    int cost;
+    {
+        const int ctx_t = last >= 0 ? (((big >> max(last, 0)) & 1u) ? 2 : 1) : 0;
+        const int tail = (int)T->beob[2][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
+        cost = last < 0 ? (int)T->beob[2][0][0] : (int)T->binit[2][0][0] + hx_sum(part) + tail;
+    }
+    // reconstruction and SSE of this lane's rows
+    uint32_t r01[2], r32[2];
+    idct_recon_pair(dq, p01, p32, h, r01, r32);
     int sse = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int d = sv[k] - clamp255(pr[k] + rr[k]);
-        sse += m24(d, d);
+    for (int r = 0; r < 2; r++) {
+        const uint32_t d01 = sub_pk(s01[r], r01[r]), d32 = sub_pk(s32[r], r32[r]);
+        sse = dot2v(d01, d01, sse);
+        sse = dot2v(d32, d32, sse);
     }
-    sse = red8(sse);
+    sse = red8(hx_sum(sse));
     cost = red8(cost);
-    nzac = red8(nzac);
+    nzac = red8(hx_sum(nzac));
     const int fixed = sel4(m, d_FIXED_COSTS_UV[0], d_FIXED_COSTS_UV[1], d_FIXED_COSTS_UV[2], d_FIXED_COSTS_UV[3]);
     const int pen = (m > 0 && nzac <= 2) ? 140 * 8 : 0;
     const int csum = fixed + cost + pen;
@@ -1291,37 +1469,42 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
 }
 
 // Final chroma transform with error diffusion (transform_chroma_blocks
-// vp8.rs:3039, apply_chroma_error_diffusion :572).  Levels to W->lev[17..24],
-// recon into cu/cv.  Returns the simple-quant "any nonzero" flag; uv_nz[8]
-// receives per-block has-coefficients.
+// vp8.rs:3039, apply_chroma_error_diffusion :572), lane-pair form: lanes b and
+// 32 + b work block b (U 0..3, V 4..7) from the coefficients pick_uv left for
+// the chosen mode.  Levels to W->lev[17..24], recon into cu / cv.  Returns the
+// simple-quant "any nonzero" flag; uv_nz[8] receives per-block has-coefficients.
 __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[8])
 {
     WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const int l = C.lane;
-    const int b = l & 7, pl = b >> 2, bb = b & 3, bx = bb & 1, by = bb >> 1;
-    // the chosen mode's prediction and coefficients, left by pick_uv
-    int pr[16], c[16];
+    const int h = l >> 5, b = l & 7, pl = b >> 2, bx = b & 1, by = (b >> 1) & 1;
+    const bool act = (l & 31) < 8;
+    int cf[2][4];
+    uint32_t p01[2], p32[2];
     {
-        const uint32_t* e = W->uvc[mode * 8 + b];
+        const uint32_t* e = W->uvc[h * 32 + mode * 8 + b];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t v = e[k];
-            c[2 * k] = (int)(int16_t)(v & 0xffffu);
-            c[2 * k + 1] = (int)(int16_t)(v >> 16);
+        for (int c = 0; c < 2; c++) {
+            cf[c][0] = lo16(e[2 * c]);
+            cf[c][1] = hi16(e[2 * c]);
+            cf[c][2] = lo16(e[2 * c + 1]);
+            cf[c][3] = hi16(e[2 * c + 1]);
         }
-#pragma unroll
-        for (int k = 0; k < 16; k++) pr[k] = (int)((e[8 + (k >> 2)] >> (8 * (k & 3))) & 255u);
+        p01[0] = e[4];
+        p32[0] = e[5];
+        p01[1] = e[6];
+        p32[1] = e[7];
     }
     // DC error diffusion (vp8.rs chroma quirk, per plane: blocks 0,1,2,3 in
-    // order), on the scalar unit; the adjusted DCs go back to their lanes.
+    // order), on the scalar unit; block k's DC is cf[0][0] of lane k.
     {
         const int q = (int)S.uv.q[0];
         const uint32_t iq = S.uv.iq[0], bias = S.uv.bias[0];
         const uint32_t zt = S.uv.zthresh[0];  // ((1 << 17) - 1 - bias) / iq, matrix_init
         int dcs[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) dcs[k] = __builtin_amdgcn_readlane(c[0], k);
+        for (int k = 0; k < 8; k++) dcs[k] = __builtin_amdgcn_readlane(cf[0][0], k);
         auto diffuse = [&](int& dc, int te, int le) -> int {
             dc += (7 * te + 8 * le) >> 3;
             const int sign = dc < 0;
@@ -1354,31 +1537,38 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
         }
 #pragma unroll
         for (int k = 0; k < 8; k++)
-            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(c[0]) : "s"(__builtin_amdgcn_readfirstlane(dcs[k])), "i"(k));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(cf[0][0]) : "s"(__builtin_amdgcn_readfirstlane(dcs[k])), "i"(k));
     }
-    int nzb = 0;
-    int lv[16];
+    // quantize_coeff of this lane's 8 coefficients (natural index n = 4 row + 2h + col)
+    int dq[2][4];
+    int nz = 0;
 #pragma unroll
-    for (int n = 0; n < 16; n++) {
-        const int j = kZZ(n);
-        lv[n] = quantz(c[j], S.uv.iq[j > 0], S.uv.bias[j > 0]);
-        nzb |= lv[n];
-    }
-    nzb = nzb != 0;
+    for (int c = 0; c < 2; c++)
 #pragma unroll
-    for (int n = 0; n < 16; n++) c[kZZ(n)] = m24(lv[n], (int)S.uv.q[kZZ(n) > 0]);
-    idct16(c);
-    if (l < 8) {
-        uint32_t* lw = (uint32_t*)&W->lev[17 + b][0];
-#pragma unroll
-        for (int n = 0; n < 8; n++) lw[n] = pack_lo(lv[2 * n], lv[2 * n + 1]);
+        for (int r = 0; r < 4; r++) {
+            const bool dcs = c == 0 && r == 0;
+            const uint32_t iq = dcs ? (h ? S.uv.iq[1] : S.uv.iq[0]) : S.uv.iq[1];
+            const uint32_t bias = dcs ? (h ? S.uv.bias[1] : S.uv.bias[0]) : S.uv.bias[1];
+            const int q_ = dcs ? (int)(h ? S.uv.q[1] : S.uv.q[0]) : (int)S.uv.q[1];
+            const int lv = quantz(cf[c][r], iq, bias);
+            nz |= lv;
+            if (act) W->lev[17 + b][izz_of(4 * r + 2 * h + c)] = (int16_t)lv;
+            dq[c][r] = m24(lv, q_);
+        }
+    uint32_t r01[2], r32[2];
+    idct_recon_pair(dq, p01, p32, h, r01, r32);
+    if (act) {
         uint8_t* w = pl ? W->cv : W->cu;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
-            w[(y + 1) * ZW_BPS + 1 + x] = (uint8_t)clamp255(pr[k] + c[k]);
+        for (int r = 0; r < 2; r++) {
+            uint8_t* row = w + (by * 4 + 2 * h + r + 1) * ZW_BPS + 1 + bx * 4;
+            row[0] = (uint8_t)(r01[r] & 255u);
+            row[1] = (uint8_t)(r01[r] >> 16);
+            row[2] = (uint8_t)(r32[r] >> 16);
+            row[3] = (uint8_t)(r32[r] & 255u);
         }
     }
+    const int nzb = (nz | hx_partner(nz)) != 0;
     int any = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -1496,12 +1686,24 @@ __device__ void publish(int* progress, int wave, int val)
 }
 
 
+// The lane id as a value the compiler cannot prove loop-invariant.  Taken at
+// the top of every MB iteration, it keeps lane-derived constants (per-lane
+// offsets, 64-bit source pointers, table indices) from being hoisted out of
+// the MB loops and held -- or spilled -- across them: they are cheap to
+// recompute and the registers go to the search stages.
+__device__ __forceinline__ int opaque_lane(int lane)
+{
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 template <int PASS>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
 {
+    constexpr int NW = PassShape<PASS>::NW, WG = PassShape<PASS>::WG;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int mbw = a.mbw, mbh = a.mbh;
     const ZwFrameParams* P = a.params + f;
     // carve LDS
@@ -1577,9 +1779,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 
     if (PASS == 1 && wv == 0) {
         // ---- pass-1 chroma raster chain ----
-#ifdef ZW_CHAIN_PRIO
-        __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
+        // the chain is pass 1's critical path: it takes issue priority over the
+        // luma waves sharing its SIMD (measured: 47.6 -> 44.3 ms per 256 1080p
+        // frames against luma-first priority at 12 waves)
+#ifndef ZW_CHAIN_PRIO
+#define ZW_CHAIN_PRIO 3
 #endif
+        __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
         if (lane < 4) W->left_derr[lane] = 0;
         MbFetch nx = fetch_mb(&a, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
@@ -1590,6 +1796,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             wsync();
             for (int mbx = 0; mbx < mbw; mbx++) {
                 PH_START();
+                const int lane = opaque_lane(threadIdx.x & 63);
+                C.lane = lane;
                 const MbFetch cur = nx;
                 if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
                 else if (mby + 1 < mbh) nx = fetch_mb(&a, lane, 0, mby + 1);
@@ -1612,11 +1820,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         return;
     }
 
-    // Pass 1: the luma wavefront couples every wave to the slowest row, and the
-    // luma wave sharing a SIMD with the chroma chain would be that row: give
-    // the luma waves issue priority (the chain has slack and uses the gaps).
+    // Pass 1 luma waves: below the chroma chain (ZW_CHAIN_PRIO), which sets the
+    // pass's length once 11 waves share the luma wavefront.
 #ifndef ZW_LUMA_PRIO
-#define ZW_LUMA_PRIO 2
+#define ZW_LUMA_PRIO 0
 #endif
     if (PASS == 1) __builtin_amdgcn_s_setprio(ZW_LUMA_PRIO);
     const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
@@ -1634,6 +1841,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         MbFetch nx = fetch_mb(&a, lane, 0, mby);
         for (int mbx = 0; mbx < mbw; mbx++) {
             PH_START();
+            const int lane = opaque_lane(threadIdx.x & 63);
+            C.lane = lane;
             const MbFetch cur = nx;
             if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
             // the I16 and chroma searches need only the MB above (x, y-1); the
@@ -1719,8 +1928,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     ph_flush();
 }
 
-extern "C" __global__ __launch_bounds__(WG) void k_encode_pass1(EncArgs a) { encode_body<1>(a); }
-extern "C" __global__ __launch_bounds__(WG) void k_encode_pass2(EncArgs a) { encode_body<2>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2>(a); }
 
 // ---------------------------------------------------------------------------
 // Kernel-level entry: quantisation (simple or trellis) of independent 4x4
@@ -1824,13 +2033,13 @@ extern "C" hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const u
     return hipGetLastError();
 }
 
-extern "C" size_t zw_encode_lds_bytes(int mbw)
+static size_t encode_lds_bytes(int mbw, int nw)
 {
     size_t off = 0;
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
     off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
     off += 256;
-    off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
+    off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * nw;
     off += 64;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
     off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
@@ -1838,7 +2047,7 @@ extern "C" size_t zw_encode_lds_bytes(int mbw)
     off += (size_t)mbw * 4;
     return off;
 }
-extern "C" int zw_encode_wg_threads(void) { return WG; }
+
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers (called from zw_host.cpp).
@@ -1878,14 +2087,14 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
     a.dbg = dbg;
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
-    const size_t lds = zw_encode_lds_bytes(mbw);
+    const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW);
     static const bool attr_set = []() {
         (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr_set;
-    if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(WG), lds, s, a);
-    else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(WG), lds, s, a);
+    if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(PassShape<1>::WG), lds, s, a);
+    else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(PassShape<2>::WG), lds, s, a);
     return hipGetLastError();
 }
