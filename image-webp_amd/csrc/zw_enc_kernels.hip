@@ -719,40 +719,6 @@ __device__ __forceinline__ void i4_values_n(const Ctx& C, const int* x0, const i
 }
 __device__ __forceinline__ void i4_values(const Ctx& C, int x0, int y0) { i4_values_n<1>(C, &x0, &y0); }
 
-// Register form of i4_values_n for the search: lane l < 39 returns V[l] of
-// each block (no LDS round trip; consumers gather with ds_bpermute).
-template <int NB>
-__device__ __forceinline__ void i4_values_reg(const Ctx& C, const int* x0, const int* y0, int* vreg)
-{
-    const uint8_t* ws = C.W->ws;
-    const int l = C.lane;
-    const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
-    const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
-    const int t3 = (int)(t == 3), t4 = (int)(t >= 4), t12 = (int)(t == 1 || t == 2);
-    const int ka = k + t3 * (11 - k) + t4 * (1 - k);
-    const int kb = k + t12 + t3 * (12 - k) - t4 * k;
-    const int kc = min(k + 2 * (int)(t == 1), 12);
-    const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
-    const int wc = (int)(t == 1);
-    const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
-    const int oa = csel(ka < 4, -ka * ZW_BPS, ka - 4 - 4 * ZW_BPS);
-    const int ob = csel(kb < 4, -kb * ZW_BPS, kb - 4 - 4 * ZW_BPS);
-    const int oc = csel(kc < 4, -kc * ZW_BPS, kc - 4 - 4 * ZW_BPS);
-    const bool dcl = l < 4 || (l >= 5 && l < 9);
-    int ea[NB];
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int rowL = (y0[h] + 3) * ZW_BPS + x0[h] - 1;
-        ea[h] = ws[rowL + oa];
-        const int eb = ws[rowL + ob], ec = ws[rowL + oc];
-        vreg[h] = (ea[h] + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh;
-    }
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int dsum = __builtin_amdgcn_readfirstlane(red16(dcl ? ea[h] : 0));
-        vreg[h] = csel(l == 38, (dsum + 4) >> 3, vreg[h]);
-    }
-}
 __device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
 
 // V index of pixel p under I4 mode `mode`, with bit 8 set for TrueMotion
@@ -780,215 +746,17 @@ struct I4State {
     uint32_t total_mc;           // header-bit cap accumulator (vp8.rs:1839)
     unsigned long long mpack;    // chosen sub-modes, 4 bits each (raster index)
     uint32_t tnz, lnz;           // nonzero flags of the chosen blocks: bit sbx / bit sby
+    uint32_t nzm;                // nonzero flags of the chosen blocks: bit = raster index
 };
 
-// One x+2y anti-diagonal step of the I4 search: the NB (1 or 2) sub-blocks
-// (sbx[h], sby[h]) share no pixels and no contexts, so they are searched
-// together -- every dependent chain of the single-block search (predictions,
-// SSE reductions, rank, candidate DCT/quant/cost/iDCT) runs twice,
-// interleaved, for instruction-level parallelism inside the wave.
-// Per block: 10 predictions + SSE (lane = group g, pixel k; modes g, g+4, g+8);
-// stable ascending SSE rank (quirk A12) computed lane-parallel (lane m ranks
-// mode m against the ten keys sse*16+m held in SGPRs); the top-K candidates
-// are evaluated 16 lanes each and the winner chosen on the scalar unit.
-// Within one sub-block every candidate score sse*256 + u16(rate)*lambda_i4 is
-// below 2^29 (sse <= 16*255^2, lambda_i4 <= 1785), so score*4 + group is a
-// unique 32-bit key whose minimum is the reference's first strict minimum.
-template <int PASS, int NB>
-__device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, int si0, int si1, int si2,
-                                        uint32_t iqk, uint32_t biask, int qk, I4State& st)
+// Unsigned minimum within aligned 16-lane rows (DPP row rotations), in every lane.
+DI uint32_t min16u(uint32_t v)
 {
-    WaveLds* W = C.W;
-    const ZwSegment& S = *C.S;
-    const LdsTables* T = C.T;
-    const int l = C.lane, g = l >> 4, k = l & 15;
-    const uint32_t lam = S.l_i4;
-    int x0[NB], y0[NB], tctx[NB], lctx[NB], nzc[NB], svk[NB];
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int i = sby[h] * 4 + sbx[h];
-        x0[h] = sbx[h] * 4 + 1;
-        y0[h] = sby[h] * 4 + 1;
-        tctx[h] = sby[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 4))) & 15);
-        lctx[h] = sbx[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 1))) & 15);
-        nzc[h] = (sby[h] == 0 ? 0 : (int)((st.tnz >> sbx[h]) & 1)) + (sbx[h] == 0 ? 0 : (int)((st.lnz >> sby[h]) & 1));
-        svk[h] = C.sY[(sby[h] * 4 + (k >> 2)) * 16 + sbx[h] * 4 + (k & 3)];
-    }
-    PH_START();
-    int vreg[NB];
-    i4_values_reg<NB>(C, x0, y0, vreg);
-    PH_MARK_L(10, l, 0);
-    // lane (g, k): predictions of modes g, g+4, g+8 at pixel k, gathered from
-    // the V vectors held in lanes 0..38 (TrueMotion: V[3-row] + V[5+col] - V[4])
-    int e0[NB], e1[NB], e2[NB], p0[NB], p1[NB], p2[NB];
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int a0 = bperm(vreg[h], si0 & 255), a1 = bperm(vreg[h], si1 & 255), a2 = bperm(vreg[h], si2 & 255);
-        const int c5 = bperm(vreg[h], 5 + (k & 3));
-        const int vbc = c5 - __builtin_amdgcn_readlane(vreg[h], 4);
-        p0[h] = csel(si0 >= 256, clamp255(a0 + vbc), a0);
-        p1[h] = csel(si1 >= 256, clamp255(a1 + vbc), a1);
-        p2[h] = csel(si2 >= 256, clamp255(a2 + vbc), a2);
-        e0[h] = m24(svk[h] - p0[h], svk[h] - p0[h]);
-        e1[h] = m24(svk[h] - p1[h], svk[h] - p1[h]);
-        e2[h] = m24(svk[h] - p2[h], svk[h] - p2[h]);
-    }
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        e0[h] = red16(e0[h]);
-        e1[h] = red16(e1[h]);
-        e2[h] = red16(e2[h]);
-    }
-    // unique keys sse*16 + m (sse < 2^21) -> rank = #smaller keys
-    unsigned long long cpack[NB];
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        uint32_t key[10];
-#pragma unroll
-        for (int m = 0; m < 10; m++) {
-            const int ev = m < 4 ? e0[h] : (m < 8 ? e1[h] : e2[h]);
-            key[m] = ((uint32_t)__builtin_amdgcn_readlane(ev, (m & 3) * 16) << 4) | (uint32_t)m;
-        }
-        uint32_t mykey = 0xffffffffu;
-#pragma unroll
-        for (int m = 0; m < 10; m++) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(mykey) : "s"(key[m]), "i"(m));
-        int rank = 0;
-#pragma unroll
-        for (int m = 0; m < 10; m++) rank += (int)(key[m] < mykey);
-        cpack[h] = 0;  // candidate c -> mode, 4 bits each
-        for (int c = 0; c < K; c++) {
-            const unsigned long long bm = __ballot(rank == c && l < 10);
-            cpack[h] |= (unsigned long long)__builtin_ctzll(bm) << (4 * c);
-        }
-    }
-    wsync();
-    PH_MARK_L(11, l, 0);
-    uint32_t bsc[NB], bsse[NB], brate[NB];
-    int bmode[NB], bnz[NB], brv[NB];
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        bsc[h] = 0xffffffffu;
-        bsse[h] = brate[h] = 0;
-        bmode[h] = bnz[h] = brv[h] = 0;
-    }
-    for (int base = 0; base < K; base += 4) {
-        const int c = base + g;
-        const bool act = c < K;
-        int mm[NB], pk[NB], r[NB], qv[NB], dq[NB], rv[NB];
-        unsigned nzm[NB];
-        uint32_t cc[NB], sse[NB], rate[NB], kv[NB];
-#pragma unroll
-        for (int h = 0; h < NB; h++) {
-            mm[h] = act ? (int)((cpack[h] >> (4 * c)) & 15) : 0;
-            // mode mm's prediction at pixel k lives in lane (mm & 3) * 16 + k, value mm >> 2
-            const int src = (mm[h] & 3) * 16 + k;
-            const int q0 = bperm(p0[h], src), q1 = bperm(p1[h], src), q2 = bperm(p2[h], src);
-            pk[h] = sel4(mm[h] >> 2, q0, q1, q2, 0);
-        }
-#pragma unroll
-        for (int h = 0; h < NB; h++) r[h] = fdct_g(svk[h] - pk[h], k);
-#pragma unroll
-        for (int h = 0; h < NB; h++) {
-            qv[h] = quantz(r[h], iqk, biask);
-            nzm[h] = gmask(qv[h] != 0);
-        }
-#pragma unroll
-        for (int h = 0; h < NB; h++) cc[h] = rcost_g<0, PASS == 2>(qv[h], k, nzc[h], 3, T);
-#pragma unroll
-        for (int h = 0; h < NB; h++) dq[h] = idct_g(m24(qv[h], qk), k);
-#pragma unroll
-        for (int h = 0; h < NB; h++) {
-            rv[h] = clamp255(pk[h] + dq[h]);
-            const int d = svk[h] - rv[h];
-            sse[h] = (uint32_t)red16(d * d);
-        }
-#pragma unroll
-        for (int h = 0; h < NB; h++) {
-            rate[h] = (uint32_t)T->fci4[tctx[h]][lctx[h]][mm[h]] + cc[h];
-            const uint32_t sc = sse[h] * 256u + (rate[h] & 0xffffu) * lam;
-            kv[h] = act ? sc * 4u + (uint32_t)g : 0xffffffffu;
-        }
-#pragma unroll
-        for (int h = 0; h < NB; h++) {
-            uint32_t kmin = (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 0);
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 16));
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 32));
-            kmin = min(kmin, (uint32_t)__builtin_amdgcn_readlane((int)kv[h], 48));
-            if ((kmin >> 2) < bsc[h]) {  // strict: earlier rounds keep ties
-                const int bg = (int)(kmin & 3u), src = bg * 16;
-                bsc[h] = kmin >> 2;
-                bsse[h] = (uint32_t)__builtin_amdgcn_readlane((int)sse[h], src);
-                brate[h] = (uint32_t)__builtin_amdgcn_readlane((int)rate[h], src);
-                bnz[h] = __builtin_amdgcn_readlane((int)(nzm[h] != 0), src);
-                bmode[h] = (int)((cpack[h] >> (4 * (base + bg))) & 15);
-                brv[h] = __shfl(rv[h], src + k);
-            }
-        }
-    }
-    PH_MARK_L(12, l, 0);
-#pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int i = sby[h] * 4 + sbx[h];
-        st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz[h] << sbx[h]);
-        st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz[h] << sby[h]);
-        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode[h]];
-        st.running += rdscore(bsse[h], brate[h], S.l_mode);
-        st.mpack |= (unsigned long long)bmode[h] << (4 * i);
-        if (l == h) W->modes[i] = (uint8_t)bmode[h];
-    }
-    // recon pixels: lanes 16h..16h+15 write block h
-    {
-        const int hh = NB == 2 ? (l >> 4) & 1 : 0;
-        const int xo = NB == 2 ? csel(hh, x0[NB - 1], x0[0]) : x0[0];
-        const int yo = NB == 2 ? csel(hh, y0[NB - 1], y0[0]) : y0[0];
-        const int pv = NB == 2 ? csel(hh, brv[NB - 1], brv[0]) : brv[0];
-        if (l < 16 * NB) W->ws[(yo + (k >> 2)) * ZW_BPS + xo + (k & 3)] = (uint8_t)pv;
-    }
-    wsync();
-    PH_MARK_L(13, l, 0);
-}
-
-// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
-// The sub-blocks are visited along x+2y anti-diagonals (10 steps, 6 of them with
-// two independent blocks) instead of raster order.  Each block's choice depends
-// only on its left / top / top-right neighbours, which every earlier
-// anti-diagonal holds, so every choice equals the raster-order one.  The
-// reference's early exits (running score >= the I16 score, vp8.rs:2018; mode
-// cost cap, :1839) test sums of non-negative terms, which grow with every
-// block: "some raster prefix crossed the bound" is "the sum over every block
-// crossed it", so testing the sum of the blocks searched so far after each
-// step decides exactly as the reference does.
-template <int PASS>
-__device__ bool pick_i4(const Ctx& C, unsigned long long i16_score)
-{
-    const ZwSegment& S = *C.S;
-    const LdsTables* T = C.T;
-    const int l = C.lane, g = l >> 4, k = l & 15;
-    const int K = C.method <= 3 ? 3 : (C.method == 4 ? 4 : 10);
-    const uint32_t iqk = S.y1.iq[k > 0], biask = S.y1.bias[k > 0];
-    const int qk = (int)S.y1.q[k > 0];
-    I4State st;
-    st.running = 211ull * S.l_mode;
-    st.total_mc = 0;
-    st.mpack = 0;
-    st.tnz = st.lnz = 0;
-    const int si0 = i4_src_index(T, g, k), si1 = i4_src_index(T, g + 4, k), si2 = i4_src_index(T, g < 2 ? g + 8 : 0, k);
-    PH_COUNT(20);
-    for (int s = 0; s < 10; s++) {
-        PH_COUNT(19);
-        // anti-diagonal s: A = (sbx, sby) with the smallest sby, B = (sbx - 2, sby + 1)
-        const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
-        const int sbxA = s - 2 * sbyA;
-        if (s >= 2 && s <= 7) {
-            const int bx[2] = {sbxA, sbxA - 2}, by[2] = {sbyA, sbyA + 1};
-            i4_step<PASS, 2>(C, bx, by, K, si0, si1, si2, iqk, biask, qk, st);
-        } else {
-            i4_step<PASS, 1>(C, &sbxA, &sbyA, K, si0, si1, si2, iqk, biask, qk, st);
-        }
-        if (st.running >= i16_score) return false;
-        if (st.total_mc > 256u * 16u * 16u / 4u) return false;
-    }
-    return true;
+    v = min(v, (uint32_t)DPP((int)v, 0x128));
+    v = min(v, (uint32_t)DPP((int)v, 0x124));
+    v = min(v, (uint32_t)DPP((int)v, 0x122));
+    v = min(v, (uint32_t)DPP((int)v, 0x121));
+    return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1130,6 +898,60 @@ DI void idct_recon_pair(const int dq[2][4], const uint32_t p01[2], const uint32_
     }
 }
 
+// get_residual_cost (cost.rs:1670, quirk A1: positions are natural indices) of
+// a lane pair's block, first position 0: av[col][row] = |level| at natural
+// index n = 4 row + 2h + col.  Returns the block's rate in 1/256 bits, uniform
+// in the pair.  LC = false: the LevelCosts tables are zero (pass 1, quirk A2)
+// and lfc[0] == 0, so positions past the last nonzero level add nothing.
+template <bool LC>
+DI int rcost_pair(const int av[2][4], int h, int ctx0, int ctype, const LdsTables* T, int& last_o)
+{
+    unsigned nzbits = 0, big = 0;
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int n = 4 * r + 2 * h + c;
+            nzbits |= (unsigned)min(av[c][r], 1) << n;
+            big |= (unsigned)(av[c][r] >= 2) << n;
+        }
+    nzbits |= (unsigned)hx_partner((int)nzbits);
+    big |= (unsigned)hx_partner((int)big);
+    const int last = 31 - __clz((int)nzbits);
+    last_o = last;
+    int part = 0;
+    if (LC) {
+        // predecessor contexts from the partner's second column (2(1-h)+1), 2 bits per row
+        unsigned sc = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) sc |= (unsigned)min(av[1][r], 2) << (2 * r);
+        const unsigned rc = (unsigned)hx_partner((int)sc);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int n = 4 * r + 2 * h + c;
+                int ctx;
+                if (c == 1) ctx = min(av[0][r], 2);
+                else if (r == 0) ctx = h ? (int)(rc & 3u) : ctx0;  // n = 2: column 1 of row 0; n = 0: ctx0
+                else ctx = h ? (int)((rc >> (2 * r)) & 3u) : (int)((rc >> (2 * r - 2)) & 3u);
+                const int a = av[c][r];
+                const int tl = T->lfc[min(a, 2047)] + T->lc[ctype][band_of(n)][ctx][min(a, 67)];
+                part += tl & -(int)(n <= last);
+            }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) part += T->lfc[min(av[c][r], 2047)];
+    }
+    const int sum = hx_sum(part);
+    const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
+    const int tail = (int)T->beob[ctype][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
+    const int head = (int)T->binit[ctype][0][ctx0] & -(int)(ctx0 == 0);
+    return last < 0 ? (int)T->beob[ctype][0][ctx0] : head + sum + tail;
+}
+
 // Chroma DC predictors of both planes (uniform values): lanes 0..15 sum U,
 // 16..31 V; lane i < 8 reads left pixel i, i >= 8 top pixel i - 8.
 __device__ __forceinline__ void uv_dc_preds(const Ctx& C, int& dcU, int& dcV)
@@ -1180,7 +1002,6 @@ __device__ int pick_uv(const Ctx& C)
     }
     // quantize_coeff (no sharpening, cost.rs:457); natural index n = 4 row + 2h + col
     int dq[2][4], av[2][4];
-    unsigned nzbits = 0, big = 0;
     int nzac = 0;
 #pragma unroll
     for (int c = 0; c < 2; c++)
@@ -1195,50 +1016,11 @@ __device__ int pick_uv(const Ctx& C)
             const int a = (int)((__umul24((uint32_t)iabs(v), iq) + bias) >> 17);
             av[c][r] = a;
             dq[c][r] = m24(v < 0 ? -a : a, q_);
-            const int n = 4 * r + 2 * h + c;
-            nzbits |= (unsigned)min(a, 1) << n;
-            big |= (unsigned)(a >= 2) << n;
             nzac += t ? min(a, 1) : 0;
         }
-    // get_residual_cost (cost.rs:1670), ctype 2, first 0, ctx0 0: terms of this
-    // lane's positions, then the pair's sum; head / tail from the pair's masks
-    nzbits |= (unsigned)hx_partner((int)nzbits);
-    big |= (unsigned)hx_partner((int)big);
-    const int last = 31 - __clz((int)nzbits);
-    int part = 0;
-    if (PASS == 2) {
-        // predecessor contexts from the partner's second column (2(1-h)+1), 2 bits per row
-        unsigned sc = 0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) sc |= (unsigned)min(av[1][r], 2) << (2 * r);
-        const unsigned rc = (unsigned)hx_partner((int)sc);
-#pragma unroll
-        for (int c = 0; c < 2; c++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int n = 4 * r + 2 * h + c;
-                int ctx;
-                if (c == 1) ctx = min(av[0][r], 2);
-                else if (r == 0) ctx = h ? (int)(rc & 3u) : 0;  // n = 2: column 1 of row 0; n = 0: ctx0
-                else ctx = h ? (int)((rc >> (2 * r)) & 3u) : (int)((rc >> (2 * r - 2)) & 3u);
-                const int a = av[c][r];
-                const int tl = T->lfc[min(a, 2047)] + T->lc[2][band_of(n)][ctx][min(a, 67)];
-                part += tl & -(int)(n <= last);
-            }
-    } else {
-        // pass 1: the LevelCosts tables are zero (quirk A2) and lfc[0] == 0, so
-        // positions past the last nonzero level add nothing: no masks
-#pragma unroll
-        for (int c = 0; c < 2; c++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) part += T->lfc[min(av[c][r], 2047)];
-    }
-    int cost;
-    {
-        const int ctx_t = last >= 0 ? (((big >> max(last, 0)) & 1u) ? 2 : 1) : 0;
-        const int tail = (int)T->beob[2][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
-        cost = last < 0 ? (int)T->beob[2][0][0] : (int)T->binit[2][0][0] + hx_sum(part) + tail;
-    }
+    // get_residual_cost (cost.rs:1670), ctype 2, first 0, ctx0 0
+    int last_;
+    int cost = rcost_pair<PASS == 2>(av, h, 0, 2, T, last_);
     // reconstruction and SSE of this lane's rows
     uint32_t r01[2], r32[2];
     idct_recon_pair(dq, p01, p32, h, r01, r32);
@@ -1271,16 +1053,315 @@ __device__ int pick_uv(const Ctx& C)
     return bm;
 }
 
+// ---------------------------------------------------------------------------
+// I4 search (pick_best_intra4, vp8.rs:1790-2040) in lane-pair form.
+// Sub-blocks are visited along x+2y anti-diagonals (10 steps, 6 of them with
+// two independent blocks).  One step evaluates ALL ten modes of both blocks at
+// once: lane l = 32 hf + 16 slot + mode (modes 10..15 idle), the pair (l,
+// l ^ 32) working one (block, mode) in the chroma pair layout (rows 2hf,
+// 2hf+1 / columns 2hf, 2hf+1).  The reference's candidate set -- the K modes
+// of smallest prediction SSE, in that order (K = 3 / 4 / 10 by method) -- is
+// applied afterwards as an eligibility mask: the chosen mode is the eligible
+// one of smallest RD score, ties to the smaller (sse, mode) key, which is the
+// reference's first strict minimum in candidate order.  The full RD of the
+// non-candidates costs nothing extra (the lanes would idle) and the ranking no
+// longer sits in front of the transforms.
+// ---------------------------------------------------------------------------
+// Per-lane constants of the search (fixed for an MB).
+struct I4Lane {
+    uint32_t ia, ib;  // bperm byte addresses (4 x V index) of the lane's pixels in rows 2hf, 2hf+1, one per byte
+    uint32_t psel;    // v_perm selector taking the lane's slot half of two gathered words
+    int tm;           // mode is TrueMotion
+};
+
+// Value vectors of the step's (up to) two sub-blocks, slot 0 in the low and
+// slot 1 in the high 16 bits: lane v < 39 holds V[v] (see i4_values_n).
+template <int NB>
+__device__ __forceinline__ uint32_t i4_values_pk(const Ctx& C, const int* x0, const int* y0)
+{
+    const uint8_t* ws = C.W->ws;
+    const int l = C.lane;
+    const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
+    const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
+    const int t3 = (int)(t == 3), t4 = (int)(t >= 4), t12 = (int)(t == 1 || t == 2);
+    const int ka = k + t3 * (11 - k) + t4 * (1 - k);
+    const int kb = k + t12 + t3 * (12 - k) - t4 * k;
+    const int kc = min(k + 2 * (int)(t == 1), 12);
+    const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
+    const int wc = (int)(t == 1);
+    const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
+    const int oa = csel(ka < 4, -ka * ZW_BPS, ka - 4 - 4 * ZW_BPS);
+    const int ob = csel(kb < 4, -kb * ZW_BPS, kb - 4 - 4 * ZW_BPS);
+    const int oc = csel(kc < 4, -kc * ZW_BPS, kc - 4 - 4 * ZW_BPS);
+    const bool dcl = l < 4 || (l >= 5 && l < 9);
+    uint32_t v = 0, ea = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int hh = NB == 2 ? h : 0;
+        const int rowL = (y0[hh] + 3) * ZW_BPS + x0[hh] - 1;
+        const int a = ws[rowL + oa], eb = ws[rowL + ob], ec = ws[rowL + oc];
+        v |= (uint32_t)((a + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh) << (16 * h);
+        ea |= (uint32_t)a << (16 * h);
+    }
+    // DC = (4 + L0..L3 + A0..A3) >> 3 of both slots at once (sums < 2^16)
+    const uint32_t ds = (uint32_t)__builtin_amdgcn_readfirstlane(red16((int)(dcl ? ea : 0u)));
+    const uint32_t dcv = (((ds & 0xffffu) + 4) >> 3) | ((((ds >> 16) + 4) >> 3) << 16);
+    return l == 38 ? dcv : v;
+}
+
+DI void i4_lane_init(const Ctx& C, I4Lane& L)
+{
+    const int l = C.lane, hf = l >> 5, m = l & 15, mv = m < 10 ? m : 0;
+    L.ia = L.ib = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int sa = i4_src_index(C.T, mv, 8 * hf + j) & 255, sb = i4_src_index(C.T, mv, 8 * hf + 4 + j) & 255;
+        L.ia |= (uint32_t)(4 * sa) << (8 * j);
+        L.ib |= (uint32_t)(4 * sb) << (8 * j);
+    }
+    L.psel = (l & 16) ? 0x0c060c02u : 0x0c040c00u;
+    L.tm = mv == 1;
+}
+
+template <int PASS, int NB>
+__device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, const I4Lane& LC,
+                                        I4State& st, bool keep)
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
+    const int l = C.lane, hf = l >> 5, m = l & 15;
+    const int slot = NB == 2 ? (l >> 4) & 1 : 0;
+    int x0[NB], y0[NB], tctx[NB], lctx[NB], nzc[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int i = sby[h] * 4 + sbx[h];
+        x0[h] = sbx[h] * 4 + 1;
+        y0[h] = sby[h] * 4 + 1;
+        tctx[h] = sby[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 4))) & 15);
+        lctx[h] = sbx[h] == 0 ? 0 : (int)((st.mpack >> (4 * (i - 1))) & 15);
+        nzc[h] = (sby[h] == 0 ? 0 : (int)((st.tnz >> sbx[h]) & 1)) + (sbx[h] == 0 ? 0 : (int)((st.lnz >> sby[h]) & 1));
+    }
+    const int sl = NB == 2 ? 1 : 0;
+    const int bx = csel(slot, sbx[sl], sbx[0]), by = csel(slot, sby[sl], sby[0]);
+    const int ctx0 = csel(slot, nzc[sl], nzc[0]);
+    const int mcost = T->fci4[csel(slot, tctx[sl], tctx[0])][csel(slot, lctx[sl], lctx[0])][m < 10 ? m : 0];
+    PH_START();
+    const uint32_t vp = i4_values_pk<NB>(C, x0, y0);
+    PH_MARK_L(10, l, 0);
+    // TrueMotion offsets V[5 + j] - V[4] of both slots, as (x0, x1), (x3, x2) pairs
+    uint32_t ap01, ap32;
+    {
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)vp, 4);
+        uint32_t a[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) a[j] = (uint32_t)__builtin_amdgcn_readlane((int)vp, 5 + j);
+        const int sh = 16 * slot;
+        const int p_ = (int)((P >> sh) & 255u);
+        const int d0 = (int)((a[0] >> sh) & 255u) - p_, d1 = (int)((a[1] >> sh) & 255u) - p_;
+        const int d2 = (int)((a[2] >> sh) & 255u) - p_, d3 = (int)((a[3] >> sh) & 255u) - p_;
+        ap01 = pack_lo(d0, d1);
+        ap32 = pack_lo(d3, d2);
+    }
+    // this lane's predictions (rows 2hf, 2hf+1) gathered from the value vectors
+    uint32_t p01[2], p32[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t ix = r ? LC.ib : LC.ia;
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ix & 255u), (int)vp);
+        const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ix >> 8) & 255u), (int)vp);
+        const uint32_t v2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ix >> 16) & 255u), (int)vp);
+        const uint32_t v3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ix >> 24), (int)vp);
+        const uint32_t q01 = __builtin_amdgcn_perm(v1, v0, LC.psel), q32 = __builtin_amdgcn_perm(v2, v3, LC.psel);
+        p01[r] = LC.tm ? clamp_pk(add_pk(q01, ap01)) : q01;
+        p32[r] = LC.tm ? clamp_pk(add_pk(q32, ap32)) : q32;
+    }
+    // source rows
+    uint32_t s01[2], s32[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t sw = *(const uint32_t*)(C.sY + (by * 4 + 2 * hf + r) * 16 + bx * 4);
+        s01[r] = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
+        s32[r] = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
+    }
+    // prediction SSE and the candidate set: rank of key = sse * 16 + mode among
+    // the slot's ten modes (the reference's stable ascending sort, quirk A12)
+    int pse = 0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t d01 = sub_pk(s01[r], p01[r]), d32 = sub_pk(s32[r], p32[r]);
+        pse = dot2v(d01, d01, pse);
+        pse = dot2v(d32, d32, pse);
+    }
+    pse = hx_sum(pse);
+    const int key = m < 10 ? (pse << 4) | m : 0x7fffffff;
+    int rank = 0;
+#define ZW_RANK_STEP(R)                                                                      \
+    rank += (int)((uint32_t)(__builtin_amdgcn_update_dpp(0, key, 0x120 + (R), 0xf, 0xf, false) - key) >> 31);
+    ZW_RANK_STEP(1) ZW_RANK_STEP(2) ZW_RANK_STEP(3) ZW_RANK_STEP(4) ZW_RANK_STEP(5)
+    ZW_RANK_STEP(6) ZW_RANK_STEP(7) ZW_RANK_STEP(8) ZW_RANK_STEP(9) ZW_RANK_STEP(10)
+    ZW_RANK_STEP(11) ZW_RANK_STEP(12) ZW_RANK_STEP(13) ZW_RANK_STEP(14) ZW_RANK_STEP(15)
+#undef ZW_RANK_STEP
+    PH_MARK_L(11, l, 0);
+    // transform, quantiser, rate, reconstruction and distortion of every
+    // (block, mode): natural coefficient index n = 4 row + 2 hf + col, the DC
+    // (n = 0) in the lower half's column 0
+    int cf[2][4];
+    fdct_pair(s01, s32, p01, p32, hf, cf);
+    int av[2][4], dq[2][4];
+    unsigned sgn = 0;
+    {
+        const uint32_t iq0 = hf ? S.y1.iq[1] : S.y1.iq[0], bs0 = hf ? S.y1.bias[1] : S.y1.bias[0];
+        const int q0 = hf ? (int)S.y1.q[1] : (int)S.y1.q[0];
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const bool dcs = c == 0 && r == 0;
+                const int v = cf[c][r];
+                const int a = (int)((__umul24((uint32_t)iabs(v), dcs ? iq0 : S.y1.iq[1]) + (dcs ? bs0 : S.y1.bias[1])) >> 17);
+                av[c][r] = a;
+                dq[c][r] = m24(v < 0 ? -a : a, dcs ? q0 : (int)S.y1.q[1]);
+                sgn |= (unsigned)(v < 0) << (4 * c + r);
+            }
+    }
+    int last;
+    const int cost = rcost_pair<PASS == 2>(av, hf, ctx0, 3, T, last);  // get_cost_luma4 (ctype 3, first 0)
+    uint32_t r01[2], r32[2];
+    idct_recon_pair(dq, p01, p32, hf, r01, r32);
+    int sse = 0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t d01 = sub_pk(s01[r], r01[r]), d32 = sub_pk(s32[r], r32[r]);
+        sse = dot2v(d01, d01, sse);
+        sse = dot2v(d32, d32, sse);
+    }
+    sse = hx_sum(sse);
+    const uint32_t rate = (uint32_t)(mcost + cost);
+    // rd_score (cost.rs): sse * 256 + u16(rate) * lambda_i4 < 2^29 (see above)
+    const uint32_t score = (uint32_t)sse * 256u + (rate & 0xffffu) * S.l_i4;
+    const bool elig = m < 10 && rank < K;
+    // the eligible lane of smallest (score, rank) in each slot's row: the
+    // reference's first strict minimum over its candidates in SSE order
+    unsigned long long win;
+    if (K <= 4) {
+        const uint32_t key2 = elig ? (score << 2) | (uint32_t)rank : 0xffffffffu;
+        const uint32_t kmin = min16u(key2);
+        win = __ballot(key2 == kmin);
+    } else {
+        // (DPP reads other lanes: every min16u runs with the whole wave active)
+        const uint32_t sk = elig ? score : 0xffffffffu;
+        const uint32_t smin = min16u(sk);
+        const uint32_t rk = sk == smin ? (uint32_t)rank : 0xffffffffu;
+        const uint32_t rmin = min16u(rk);
+        win = __ballot(rk == rmin && sk == smin);
+    }
+    PH_MARK_L(12, l, 0);
+    int bmode[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        bmode[h] = __builtin_ctz((uint32_t)(win >> (16 * h)) & 0xffffu);
+        const int wl = 16 * h + bmode[h];
+        const uint32_t bsse = (uint32_t)__builtin_amdgcn_readlane(sse, wl);
+        const uint32_t brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, wl);
+        const int bnz = __builtin_amdgcn_readlane((int)(last >= 0), wl);
+        const int i = sby[h] * 4 + sbx[h];
+        st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
+        st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
+        st.nzm |= (uint32_t)bnz << i;
+        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode[h]];
+        st.running += rdscore(bsse, brate, S.l_mode);
+        st.mpack |= (unsigned long long)bmode[h] << (4 * i);
+        if (l == h) W->modes[i] = (uint8_t)bmode[h];
+    }
+    // the winners' two lanes write their rows of the reconstruction (and, when
+    // the final pass reuses them, the levels in zigzag order)
+    const int bms = csel(slot, bmode[sl], bmode[0]);
+    if (m == bms && (NB == 2 || slot == 0)) {
+        const int xo = csel(slot, x0[sl], x0[0]), yo = csel(slot, y0[sl], y0[0]);
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t wd = __builtin_amdgcn_perm(r32[r], r01[r], 0x04060200u);
+            uint8_t* p = W->ws + (yo + 2 * hf + r) * ZW_BPS + xo;
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[j] = (uint8_t)(wd >> (8 * j));
+        }
+        if (keep) {
+            int16_t* lv = W->lev[by * 4 + bx];
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int a = av[c][r];
+                    lv[izz_of(4 * r + 2 * hf + c)] = (int16_t)(((sgn >> (4 * c + r)) & 1u) ? -a : a);
+                }
+        }
+    }
+    wsync();
+    PH_MARK_L(13, l, 0);
+}
+
+// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
+// Each block's choice depends only on its left / top / top-right neighbours,
+// which every earlier anti-diagonal holds, so every choice equals the
+// raster-order one.  The reference's early exits (running score >= the I16
+// score, vp8.rs:2018; mode cost cap, :1839) test sums of non-negative terms,
+// which grow with every block: "some raster prefix crossed the bound" is "the
+// sum over every block crossed it", so testing the sum of the blocks searched
+// so far after each step decides exactly as the reference does.
+template <int PASS>
+__device__ bool pick_i4(const Ctx& C, unsigned long long i16_score, bool keep, uint32_t& nzm)
+{
+    const ZwSegment& S = *C.S;
+    const int K = C.method <= 3 ? 3 : (C.method == 4 ? 4 : 10);
+    I4State st;
+    st.running = 211ull * S.l_mode;
+    st.total_mc = 0;
+    st.mpack = 0;
+    st.tnz = st.lnz = st.nzm = 0;
+    I4Lane LC;
+    i4_lane_init(C, LC);
+    PH_COUNT(20);
+    for (int s = 0; s < 10; s++) {
+        PH_COUNT(19);
+        // anti-diagonal s: A = (sbx, sby) with the smallest sby, B = (sbx - 2, sby + 1)
+        const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
+        const int sbxA = s - 2 * sbyA;
+        if (s >= 2 && s <= 7) {
+            const int bx[2] = {sbxA, sbxA - 2}, by[2] = {sbyA, sbyA + 1};
+            i4_step<PASS, 2>(C, bx, by, K, LC, st, keep);
+        } else {
+            i4_step<PASS, 1>(C, &sbxA, &sbyA, K, LC, st, keep);
+        }
+        if (st.running >= i16_score) return false;
+        if (st.total_mc > 256u * 16u * 16u / 4u) return false;
+    }
+    nzm = st.nzm;
+    return true;
+}
+
 // Final luma transform (transform_luma_block vp8.rs:2647 / _4x4 :2785).
 // Writes zigzag levels to W->lev[0..16], recon into W->ws.  Returns the
 // simple-quant "any nonzero" flag for skip detection (check_all_coeffs_zero).
-__device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16])
+__device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], int i4_nzm)
 {
     WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const int l = C.lane;
     int anynz = 0;
     PH_START();
+    if (mode == 4 && i4_nzm >= 0) {
+        // simple quantisation: the search's winners are the final blocks (same
+        // prediction, transform and quantize_coeff); their levels are in
+        // W->lev, their reconstruction in W->ws
+#pragma unroll
+        for (int i = 0; i < 16; i++) y_nz_out[i] = (i4_nzm >> i) & 1;
+        if (l < 16) W->lev[16][l] = 0;
+        wsync();
+        PH_MARK_L(15, l, 0);
+        PH_COUNT(7);
+        return i4_nzm != 0;
+    }
     if (mode != 4) {
         build_luma_border(C);
         const uint8_t* ws = W->ws;
@@ -1766,6 +1847,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.top_c = top_c;
     C.top_derr = top_derr;
     const bool trel = PASS == 2 && __builtin_amdgcn_readfirstlane(P->do_trellis);
+    // without trellis (and without the pass-2 I4 dump) the final I4 blocks are
+    // the search's winners, which the search leaves in W->lev / W->ws
+    const bool keep_i4 = !trel && (PASS == 1 || a.dbg == nullptr);
     const size_t nmb = (size_t)mbw * mbh;
 #ifdef ZW_PHASE_PROF
     if (lane < 24) W->ph[lane] = 0;
@@ -1858,6 +1942,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             wsync();
             PH_MARK(1);
             int cm = 0;
+            uint32_t i4nz = 0;
+            bool i4reuse = false;
             if (PASS == 2) {
                 build_chroma_border(C);
                 cm = pick_uv<PASS>(C);
@@ -1868,12 +1954,16 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 if (C.method >= 5 || i16s > thr || lm != 0) {
                     if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
                     build_luma_border(C, 1);
-                    if (pick_i4<PASS>(C, i16s)) lm = 4;
+                    PH_MARK(21);
+                    if (pick_i4<PASS>(C, i16s, keep_i4, i4nz)) {
+                        lm = 4;
+                        i4reuse = keep_i4;
+                    }
                 }
             }
             PH_MARK(2);
             int ynz[16];
-            const int lnz = final_luma(C, lm, trel, ynz);
+            const int lnz = final_luma(C, lm, trel, ynz, i4reuse ? (int)i4nz : -1);
             PH_MARK(4);
             int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             int cnz = 0;

@@ -24,7 +24,8 @@ NAMES = {0: "wait(row above)", 1: "border+pick_i16", 2: "pick_i4", 3: "pick_uv",
          10: "  i4: values", 11: "  i4: preds+sse+rank", 12: "  i4: candidates", 13: "  i4: select+recon",
          7: "  (count of I4 MBs)", 14: "  final: I16 MBs", 15: "  final: I4 MBs",
          16: "    i16: fdct+y2", 17: "    i16: quant check+trellis", 18: "    i16: ctx resolve+gather",
-         19: "  (I4 search steps run)", 20: "  (I4 searches)"}
+         19: "  (I4 search steps run)", 20: "  (I4 searches)",
+         21: "wait(above-right)+border"}
 
 
 def main():
@@ -50,7 +51,7 @@ def main():
     print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt[:4]]} "
           f"host(ms) fetch1/stats/fetch2/emit {[round(x, 2) for x in kt[4:8]]}")
     for ps in (0, 1):
-        tot = sum(buf[ps * 24 + k] for k in range(10) if k not in (7, 19, 20)) or 1
+        tot = sum(buf[ps * 24 + k] for k in list(range(10)) + [21] if k not in (7, 19, 20)) or 1
         print(f"pass {ps + 1}: total {tot / 1e9:.2f} G wave-cycles, {tot / nmb:.0f} wave-cycles/MB")
         for k in range(24):
             v = buf[ps * 24 + k]
