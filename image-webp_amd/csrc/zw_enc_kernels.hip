@@ -47,17 +47,12 @@ __device__ __forceinline__ int rgb_y(const uint8_t* p)
 __device__ __forceinline__ int rgb_u(const uint8_t* p) { return -9719 * p[0] - 19081 * p[1] + 28800 * p[2] + (128 << 16); }
 __device__ __forceinline__ int rgb_v(const uint8_t* p) { return 28800 * p[0] - 24116 * p[1] - 4684 * p[2] + (128 << 16); }
 
-extern "C" __global__ void k_rgb2yuv(const uint8_t* __restrict__ img, int w, int h, int bpp, int mbw, int mbh,
-                                     uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V,
-                                     size_t img_stride, size_t ysz, size_t csz)
+// chroma sample (cx, cy) of one frame and its 2x2 luma pixels
+__device__ __forceinline__ void rgb2yuv_sample(const uint8_t* __restrict__ im, int w, int h, int bpp, int mbw, int cx,
+                                               int cy, uint8_t* __restrict__ Yf, uint8_t* __restrict__ Uf,
+                                               uint8_t* __restrict__ Vf)
 {
-    const int cw = mbw * 8, chh = mbh * 8, lw = mbw * 16;
-    const int f = blockIdx.y;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= cw * chh) return;
-    const int cx = idx % cw, cy = idx / cw;
-    const uint8_t* im = img + (size_t)f * img_stride;
-    uint8_t* Yf = Y + (size_t)f * ysz;
+    const int cw = mbw * 8, lw = mbw * 16;
     const int acw = (w + 1) / 2, ach = (h + 1) / 2;
     const int scx = cx < acw ? cx : acw - 1, scy = cy < ach ? cy : ach - 1;
     int xs[2] = {min(2 * scx, w - 1), min(2 * scx + 1, w - 1)};
@@ -85,8 +80,109 @@ extern "C" __global__ void k_rgb2yuv(const uint8_t* __restrict__ img, int w, int
         uo = (uint8_t)((su + (1 << 17)) >> 18);
         vo = (uint8_t)((sv + (1 << 17)) >> 18);
     }
-    U[(size_t)f * csz + (size_t)cy * cw + cx] = uo;
-    V[(size_t)f * csz + (size_t)cy * cw + cx] = vo;
+    Uf[(size_t)cy * cw + cx] = uo;
+    Vf[(size_t)cy * cw + cx] = vo;
+}
+
+extern "C" __global__ void k_rgb2yuv(const uint8_t* __restrict__ img, int w, int h, int bpp, int mbw, int mbh,
+                                     uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V,
+                                     size_t img_stride, size_t ysz, size_t csz)
+{
+    const int cw = mbw * 8, chh = mbh * 8;
+    const int f = blockIdx.y;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= cw * chh) return;
+    rgb2yuv_sample(img + (size_t)f * img_stride, w, h, bpp, mbw, idx % cw, idx / cw, Y + (size_t)f * ysz,
+                   U + (size_t)f * csz, V + (size_t)f * csz);
+}
+
+// Row-coalesced form for 3- and 4-byte pixels: one thread per 8x2 luma pixels
+// (4 chroma samples), so a wave reads 64 consecutive 8-pixel runs of two rows
+// with 16-byte (RGBA) or 8-byte (RGB) loads and writes 8-byte luma and 4-byte
+// chroma words.  Runs that reach the right edge and the padding rows below the
+// image take the per-sample path (edge replication).  The host launches it
+// only when every run is aligned for those loads.
+template <int BPP>
+__device__ __forceinline__ void rgb_run8(const uint8_t* __restrict__ row, uint32_t px[8])  // 0x..BBGGRR
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    if (BPP == 4) {
+        const u32x4 a = __builtin_nontemporal_load((const u32x4*)row);
+        const u32x4 b = __builtin_nontemporal_load((const u32x4*)(row + 16));
+        px[0] = a.x; px[1] = a.y; px[2] = a.z; px[3] = a.w;
+        px[4] = b.x; px[5] = b.y; px[6] = b.z; px[7] = b.w;
+    } else {
+        const u32x2 a = __builtin_nontemporal_load((const u32x2*)row);
+        const u32x2 b = __builtin_nontemporal_load((const u32x2*)(row + 8));
+        const u32x2 c = __builtin_nontemporal_load((const u32x2*)(row + 16));
+        const uint32_t wd[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+#pragma unroll
+        for (int q = 0; q < 2; q++) {  // 4 pixels in 3 words
+            const uint32_t w0 = wd[3 * q], w1 = wd[3 * q + 1], w2 = wd[3 * q + 2];
+            px[4 * q] = w0;
+            px[4 * q + 1] = __builtin_amdgcn_alignbyte(w1, w0, 3);
+            px[4 * q + 2] = __builtin_amdgcn_alignbyte(w2, w1, 2);
+            px[4 * q + 3] = w2 >> 8;
+        }
+    }
+}
+__device__ __forceinline__ int pk_y(uint32_t p)
+{
+    return (16839 * (int)(p & 255u) + 33059 * (int)((p >> 8) & 255u) + 6420 * (int)((p >> 16) & 255u) + (1 << 15) +
+            (16 << 16)) >> 16;
+}
+__device__ __forceinline__ int pk_u(uint32_t p)
+{
+    return -9719 * (int)(p & 255u) - 19081 * (int)((p >> 8) & 255u) + 28800 * (int)((p >> 16) & 255u);
+}
+__device__ __forceinline__ int pk_v(uint32_t p)
+{
+    return 28800 * (int)(p & 255u) - 24116 * (int)((p >> 8) & 255u) - 4684 * (int)((p >> 16) & 255u);
+}
+
+template <int BPP>
+__global__ __launch_bounds__(256) void k_rgb2yuv_rows(const uint8_t* __restrict__ img, int w, int h, int mbw, int mbh,
+                                                      uint8_t* __restrict__ Y, uint8_t* __restrict__ U,
+                                                      uint8_t* __restrict__ V, size_t img_stride, size_t ysz,
+                                                      size_t csz)
+{
+    const int cw = mbw * 8, chh = mbh * 8, lw = mbw * 16, gpr = mbw * 2;  // 4-sample groups per chroma row
+    const int f = blockIdx.y;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= gpr * chh) return;
+    const int g = idx % gpr, cy = idx / gpr;
+    const int cx0 = 4 * g, px0 = 8 * g;
+    const uint8_t* im = img + (size_t)f * img_stride;
+    uint8_t* Yf = Y + (size_t)f * ysz;
+    uint8_t* Uf = U + (size_t)f * csz;
+    uint8_t* Vf = V + (size_t)f * csz;
+    if (px0 + 8 <= w && cy < (h + 1) / 2) {
+        const int r0 = 2 * cy, r1 = min(2 * cy + 1, h - 1);
+        uint32_t a[8], b[8];
+        rgb_run8<BPP>(im + ((size_t)r0 * w + px0) * BPP, a);
+        rgb_run8<BPP>(im + ((size_t)r1 * w + px0) * BPP, b);
+        uint32_t ya[2] = {0, 0}, yb[2] = {0, 0}, uw = 0, vw = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            ya[i >> 2] |= (uint32_t)pk_y(a[i]) << (8 * (i & 3));
+            yb[i >> 2] |= (uint32_t)pk_y(b[i]) << (8 * (i & 3));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int su = pk_u(a[2 * j]) + pk_u(a[2 * j + 1]) + pk_u(b[2 * j]) + pk_u(b[2 * j + 1]) + (512 << 16);
+            const int sv = pk_v(a[2 * j]) + pk_v(a[2 * j + 1]) + pk_v(b[2 * j]) + pk_v(b[2 * j + 1]) + (512 << 16);
+            uw |= (uint32_t)((su + (1 << 17)) >> 18) << (8 * j);
+            vw |= (uint32_t)((sv + (1 << 17)) >> 18) << (8 * j);
+        }
+        *(uint2*)(Yf + (size_t)(2 * cy) * lw + px0) = make_uint2(ya[0], ya[1]);
+        *(uint2*)(Yf + (size_t)(2 * cy + 1) * lw + px0) = make_uint2(yb[0], yb[1]);
+        *(uint32_t*)(Uf + (size_t)cy * cw + cx0) = uw;
+        *(uint32_t*)(Vf + (size_t)cy * cw + cx0) = vw;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) rgb2yuv_sample(im, w, h, BPP, mbw, cx0 + j, cy, Yf, Uf, Vf);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -638,6 +734,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
 #ifdef ZW_PHASE_PROF
 // Per-phase cycle counters (profiling builds only): [pass-1][phase].
 __device__ unsigned long long zw_phase_cycles_dev[2][24];
+__device__ unsigned long long zw_wave_cycles_dev[2][16][24];  // the same per wave index
 #define PH_START() long long ph_t_ = clock64()
 #define PH_MARK(k) PH_MARK_L(k, lane, PASS)
 // accumulate in the wave's LDS slot; flushed once per kernel (ph_flush)
@@ -647,6 +744,15 @@ __device__ unsigned long long zw_phase_cycles_dev[2][24];
         if ((ln) == 0) C.W->ph[k] += (unsigned long long)(n_ - ph_t_);               \
         ph_t_ = n_;                                                                 \
     } while (0)
+extern "C" int zw_wave_cycles(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_wave_cycles_dev), sizeof(zw_wave_cycles_dev)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long z[2][16][24];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(zw_wave_cycles_dev), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
 extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zw_phase_cycles_dev), sizeof(zw_phase_cycles_dev)) != hipSuccess) return -1;
@@ -1759,6 +1865,14 @@ __device__ void wait_row(const int* progress, int wave_of_prev, int need)
     while (__hip_atomic_load(&progress[wave_of_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
         __builtin_amdgcn_s_sleep(1);
 }
+// s_setprio with a wave-uniform level
+DI void set_prio(int p)
+{
+    if (p >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 __device__ void publish(int* progress, int wave, int val)
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1856,6 +1970,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     wsync();
     auto ph_flush = [&]() {
         if (lane < 24) atomicAdd(&zw_phase_cycles_dev[PASS - 1][lane], W->ph[lane]);
+        if (lane < 24) atomicAdd(&zw_wave_cycles_dev[PASS - 1][wv][lane], W->ph[lane]);
     };
 #else
     auto ph_flush = []() {};
@@ -1911,7 +2026,32 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #endif
     if (PASS == 1) __builtin_amdgcn_s_setprio(ZW_LUMA_PRIO);
     const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
-    const int rw = PASS == 1 ? wv - 1 : wv;
+    // Row k of each round of nrw rows goes to wave luma_wave(k).  In pass 1 the
+    // luma waves that share SIMD 0 with the chroma chain (issue priority 3)
+    // run slowest, and every later row of a round waits on a slow row: they
+    // take the last rows of each round, which only the next round's first
+    // row follows, with a round of slack.
+#ifndef ZW_P1_ORDER
+#define ZW_P1_ORDER 1
+#endif
+    auto p1_before = [](int v, int w) {  // wave v takes its row of a round before wave w
+        const bool sv = (v & 3) == 0, sw = (w & 3) == 0;
+        return (ZW_P1_ORDER && sv != sw) ? sw : v < w;
+    };
+    auto luma_rank = [&](int w) {
+        if (PASS == 2) return w;
+        int r = 0;
+        for (int v = 1; v < NW; v++) r += (int)p1_before(v, w);
+        return r;
+    };
+    auto luma_wave = [&](int k) {
+        if (PASS == 2) return k;
+        int w = 1;
+        for (int v = 1; v < NW; v++)
+            if (luma_rank(v) == k) w = v;
+        return w;
+    };
+    const int rw = luma_rank(wv);
     for (int mby = rw; mby < mbh; mby += nrw) {
         if (lane < 20) W->left_y[lane] = 129;
         if (lane < 12) {
@@ -1921,7 +2061,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         }
         if (lane < 4) W->left_derr[lane] = 0;
         wsync();
-        const int prevw = mby > 0 ? ((mby - 1) % nrw) + (PASS == 1 ? 1 : 0) : 0;
+        const int prevw = mby > 0 ? luma_wave((mby - 1) % nrw) : 0;
         MbFetch nx = fetch_mb(&a, lane, 0, mby);
         for (int mbx = 0; mbx < mbw; mbx++) {
             PH_START();
@@ -1933,6 +2073,30 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             // I4 search also reads the above-right MB's bottom row: wait for
             // (x+1, y-1) only then, so the wait overlaps the first searches
             if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 1, mbw));
+#ifndef ZW_DYN_PRIO
+#define ZW_DYN_PRIO 1  // slack (MBs) per priority level; 0: off
+#endif
+#if ZW_DYN_PRIO > 0
+            {
+                // Issue priority from the slack to the row above.  VALU issue is
+                // arbitrated by priority, then wave age: at equal priority the
+                // youngest waves of each SIMD run slowest and every row behind
+                // theirs waits on them (35 % of the oldest waves' time).  A row
+                // that trails the row above by more than the two-MB minimum is
+                // the one later rows wait for, so it issues first.
+                int slack = mbw;
+                if (mby > 0) {
+                    const int v = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&progress[prevw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if ((v >> 16) == mby - 1) slack = (v & 0xffff) - mbx - 1;
+                }
+                const int p = slack >= ZW_DYN_PRIO * 3 ? 3 : (slack >= ZW_DYN_PRIO * 2 ? 2 : (slack >= ZW_DYN_PRIO ? 1 : 0));
+#ifndef ZW_P1_LUMA_MAX
+#define ZW_P1_LUMA_MAX 2  // pass 1: luma waves below the chroma chain
+#endif
+                set_prio(PASS == 1 ? min(p, ZW_P1_LUMA_MAX) : p);
+            }
+#endif
             PH_MARK(0);
             setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
             build_luma_border(C, 0);
@@ -2146,9 +2310,22 @@ extern "C" hipError_t zwk_rgb2yuv(hipStream_t s, const uint8_t* img, int w, int 
                                   uint8_t* Y, uint8_t* U, uint8_t* V, size_t img_stride, size_t ysz, size_t csz,
                                   int nframes)
 {
-    const int n = mbw * 8 * mbh * 8;
-    hipLaunchKernelGGL(k_rgb2yuv, dim3((n + 255) / 256, nframes), dim3(256), 0, s, img, w, h, bpp, mbw, mbh, Y, U, V,
-                       img_stride, ysz, csz);
+    // the row-coalesced kernel needs every 8-pixel run aligned for its loads
+    // (16 B for RGBA, 8 B for RGB) and 8-byte aligned luma rows
+    const uintptr_t base = (uintptr_t)img;
+    const bool planes_ok = ((uintptr_t)Y | (uintptr_t)U | (uintptr_t)V | ysz | csz) % 8 == 0;
+    const int ng = mbw * 2 * mbh * 8;
+    if (planes_ok && bpp == 4 && base % 16 == 0 && img_stride % 16 == 0 && w % 4 == 0) {
+        hipLaunchKernelGGL(k_rgb2yuv_rows<4>, dim3((ng + 255) / 256, nframes), dim3(256), 0, s, img, w, h, mbw, mbh,
+                           Y, U, V, img_stride, ysz, csz);
+    } else if (planes_ok && bpp == 3 && base % 8 == 0 && img_stride % 8 == 0 && w % 8 == 0) {
+        hipLaunchKernelGGL(k_rgb2yuv_rows<3>, dim3((ng + 255) / 256, nframes), dim3(256), 0, s, img, w, h, mbw, mbh,
+                           Y, U, V, img_stride, ysz, csz);
+    } else {
+        const int n = mbw * 8 * mbh * 8;
+        hipLaunchKernelGGL(k_rgb2yuv, dim3((n + 255) / 256, nframes), dim3(256), 0, s, img, w, h, bpp, mbw, mbh, Y, U,
+                           V, img_stride, ysz, csz);
+    }
     return hipGetLastError();
 }
 

@@ -38,9 +38,12 @@ def _img(w, h, kind, seed, color):
 # --------------------------------------------------------------------------
 # a1: RGB -> YUV 4:2:0
 # --------------------------------------------------------------------------
-@pytest.mark.parametrize("w,h", [(1, 1), (17, 9), (64, 48), (333, 211), (250, 31)])
+@pytest.mark.parametrize("w,h", [(1, 1), (17, 9), (64, 48), (333, 211), (250, 31), (120, 67), (200, 75), (1920, 1080)])
 @pytest.mark.parametrize("bpp", [1, 2, 3, 4])
 def test_rgb_to_yuv420(ctx, w, h, bpp):
+    # widths that are multiples of 8 run the row-coalesced kernel for RGB / RGBA
+    # (8-pixel runs; the run at a partial-MB right edge and the padding rows
+    # take the per-sample path)
     img = np.ascontiguousarray(synth_rgba(w, h, 7 + w, "noise")[..., :bpp])
     gy, gu, gv = zwebp.rgb_to_yuv420(img, w, h, bpp, ctx=ctx)
     oy, ou, ov = O.rgb_to_yuv420(img, w, h, bpp)

@@ -46,6 +46,9 @@ def main():
     p.encode()
     el = time.perf_counter() - t
     assert L.zw_phase_cycles(buf, 0) == 0
+    L.zw_wave_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    wbuf = (ctypes.c_ulonglong * (2 * 16 * 24))()
+    assert L.zw_wave_cycles(wbuf, 0) == 0
     kt = p.kernel_times()
     nmb = p.mbw * p.mbh * F
     print(f"{F} frames {w}x{h} m{m}: step {el * 1e3:.1f} ms, kernels(ms) {[round(x, 2) for x in kt[:4]]} "
@@ -59,6 +62,13 @@ def main():
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.3f} of MBs")
             elif v:
                 print(f"   {NAMES.get(k, k):24s} {v / nmb:12.0f} cyc/MB  {100 * v / tot:5.1f}%")
+        print(f"   per wave (pass {ps + 1}): total G cycles / wait G cycles / MBs(approx by I4 searches)")
+        for wv in range(16):
+            b = [wbuf[(ps * 16 + wv) * 24 + k] for k in range(24)]
+            t = sum(b[k] for k in list(range(10)) + [21] if k not in (7,))
+            if t:
+                print(f"     wave {wv:2d}: {t / 1e9:8.2f}  wait {(b[0] + b[21]) / 1e9:7.2f}  ({100 * (b[0] + b[21]) / t:4.1f}%)"
+                      f"  i4 searches {b[20]}")
 
 
 if __name__ == "__main__":
