@@ -532,6 +532,7 @@ struct EncArgs {
     size_t ysz, csz;
     int mbw, mbh, pass;
     int* dbg;                   // optional pass-2 I4 dump (16*34 ints per MB), may be null
+    uint8_t* rows;              // row-parallel kernels: zero-filled ZW_ROWS_HDR + nframes * RowsLayout::frame
 };
 
 // per-wave LDS scratch
@@ -550,6 +551,11 @@ struct WaveLds {
     uint8_t modes[16];
     int16_t lev[25][16];
     int misc[16];
+    // row-parallel kernels: this MB's slice of the row above's state (top_y of
+    // the MB and of the MB above-right, top_u/v, top_c, top_derr), pulled from
+    // and pushed to global memory around each MB
+    uint8_t win_y[32], win_u[8], win_v[8], win_c[12];
+    int8_t win_d[4];
 #ifdef ZW_PHASE_PROF
     unsigned long long ph[24];
 #endif
@@ -570,6 +576,10 @@ struct Ctx {
     const uint8_t *sY, *sU, *sV;        // the same MB staged in LDS (strides 16 / 8)
     int ys, cs;
     int mbx, mby, lane, seg;
+    int f;                  // frame of the launch
+    int oy, oc, ocx, od;    // offsets of this MB in top_y / top_u,v / top_c / top_derr
+                            // (mbx*16, *8, *12, *4; 0 in the row-parallel kernels, whose
+                            // top_* point at the wave's per-MB window)
 };
 
 // create_border_luma (prediction.rs:15) into W->ws
@@ -589,9 +599,9 @@ __device__ void build_luma_border(const Ctx& C, int part = 2)
         int v;
         if (l == 0) v = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : C.W->left_y[0]);
         else if (C.mby == 0) v = 127;
-        else if (l <= 16) v = C.top_y[C.mbx * 16 + l - 1];
-        else if (C.mbx == mbw - 1) v = C.top_y[C.mbx * 16 + 15];
-        else v = C.top_y[C.mbx * 16 + l - 1];
+        else if (l <= 16) v = C.top_y[C.oy + l - 1];
+        else if (C.mbx == mbw - 1) v = C.top_y[C.oy + 15];
+        else v = C.top_y[C.oy + l - 1];
         ws[l] = (uint8_t)v;
         if (l >= 17 && l < 21) {
             ws[4 * ZW_BPS + l] = (uint8_t)v;
@@ -616,7 +626,7 @@ __device__ void build_chroma_border(const Ctx& C)
         const uint8_t* top = pl ? C.top_v : C.top_u;
         const uint8_t* left = pl ? C.W->left_v : C.W->left_u;
         if (i == 0) w[0] = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : left[0]);
-        else if (i <= 8) w[i] = C.mby == 0 ? 127 : top[C.mbx * 8 + i - 1];
+        else if (i <= 8) w[i] = C.mby == 0 ? 127 : top[C.oc + i - 1];
         else w[(i - 8) * ZW_BPS] = C.mbx == 0 ? 129 : left[i - 8];
     }
     wsync();
@@ -1542,7 +1552,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             int nt[4], nl[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                nt[q] = __builtin_amdgcn_readfirstlane(C.top_c[C.mbx * 12 + 1 + q]);
+                nt[q] = __builtin_amdgcn_readfirstlane(C.top_c[C.ocx + 1 + q]);
                 nl[q] = __builtin_amdgcn_readfirstlane(W->left_c[1 + q]);
             }
             unsigned code = 0, nzbits = 0;
@@ -1595,7 +1605,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
         build_luma_border(C);
         int top_nz[4], left_nz[4];
         for (int k = 0; k < 4; k++) {
-            top_nz[k] = C.top_c[C.mbx * 12 + 1 + k];
+            top_nz[k] = C.top_c[C.ocx + 1 + k];
             left_nz[k] = W->left_c[1 + k];
         }
         for (int i = 0; i < 16; i++) {
@@ -1609,7 +1619,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             const int ck = fdct_g(svk - pk, k);
             const int ctx0 = min(left_nz[sby] + top_nz[sbx], 2);
             if (C.a->dbg && C.a->pass == 2 && l < 16) {
-                int* d = C.a->dbg + (((size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx) * 16 + i) * 34;
+                int* d = C.a->dbg + (((size_t)C.f * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx) * 16 + i) * 34;
                 d[k] = ck;
                 d[16 + k] = pk;
                 if (k == 0) {
@@ -1772,9 +1782,9 @@ __device__ void store_luma_borders(const Ctx& C)
     const int l = C.lane;
     WaveLds* W = C.W;
     if (l < 17) W->left_y[l] = W->ws[l * ZW_BPS + 16];
-    else if (l < 33) C.top_y[C.mbx * 16 + (l - 17)] = W->ws[16 * ZW_BPS + (l - 17) + 1];
+    else if (l < 33) C.top_y[C.oy + (l - 17)] = W->ws[16 * ZW_BPS + (l - 17) + 1];
     if (C.a->ry && l < 64) {
-        uint8_t* ry = C.a->ry + (size_t)blockIdx.x * C.a->ysz + (size_t)C.mby * 16 * C.ys + C.mbx * 16;
+        uint8_t* ry = C.a->ry + (size_t)C.f * C.a->ysz + (size_t)C.mby * 16 * C.ys + C.mbx * 16;
         for (int k = l; k < 256; k += 64) ry[(size_t)(k >> 4) * C.ys + (k & 15)] = W->ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
     }
     wsync();
@@ -1787,12 +1797,12 @@ __device__ void store_chroma_borders(const Ctx& C)
         W->left_u[l] = W->cu[l * ZW_BPS + 8];
         W->left_v[l] = W->cv[l * ZW_BPS + 8];
     } else if (l < 17) {
-        C.top_u[C.mbx * 8 + (l - 9)] = W->cu[8 * ZW_BPS + (l - 9) + 1];
-        C.top_v[C.mbx * 8 + (l - 9)] = W->cv[8 * ZW_BPS + (l - 9) + 1];
+        C.top_u[C.oc + (l - 9)] = W->cu[8 * ZW_BPS + (l - 9) + 1];
+        C.top_v[C.oc + (l - 9)] = W->cv[8 * ZW_BPS + (l - 9) + 1];
     }
     if (C.a->ru) {
-        uint8_t* ru = C.a->ru + (size_t)blockIdx.x * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
-        uint8_t* rv = C.a->rv + (size_t)blockIdx.x * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
+        uint8_t* ru = C.a->ru + (size_t)C.f * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
+        uint8_t* rv = C.a->rv + (size_t)C.f * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
         const int k = l;
         ru[(size_t)(k >> 3) * C.cs + (k & 7)] = W->cu[((k >> 3) + 1) * ZW_BPS + 1 + (k & 7)];
         rv[(size_t)(k >> 3) * C.cs + (k & 7)] = W->cv[((k >> 3) + 1) * ZW_BPS + 1 + (k & 7)];
@@ -1802,7 +1812,7 @@ __device__ void store_chroma_borders(const Ctx& C)
 
 __device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
 {
-    ZwMbOut* o = C.a->out + (size_t)blockIdx.x * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx;
+    ZwMbOut* o = C.a->out + (size_t)C.f * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx;
     int16_t* dst = &o->levels[0][0];
     const int16_t* srcl = &C.W->lev[0][0];
     for (int k = C.lane; k < nblk * 16; k += 64) dst[first_blk * 16 + k] = zero ? (int16_t)0 : srcl[first_blk * 16 + k];
@@ -1816,9 +1826,9 @@ struct MbFetch {
     uint32_t y, c;
     int alpha;
 };
-__device__ __forceinline__ MbFetch fetch_mb(const EncArgs* a, int lane, int mbx, int mby)
+__device__ __forceinline__ MbFetch fetch_mb(const EncArgs* a, int f, int lane, int mbx, int mby)
 {
-    const int f = blockIdx.x, ys = a->mbw * 16, cs = a->mbw * 8;
+    const int ys = a->mbw * 16, cs = a->mbw * 8;
     const uint8_t* sy = a->Y + (size_t)f * a->ysz + (size_t)mby * 16 * ys + mbx * 16;
     MbFetch r;
     r.y = *(const uint32_t*)(sy + (size_t)(lane >> 2) * ys + (lane & 3) * 4);
@@ -1837,7 +1847,7 @@ __device__ void setup_ctx(Ctx& C, const EncArgs* a, const uint8_t* seg_lut, Wave
 {
     C.mbx = mbx;
     C.mby = mby;
-    const int f = blockIdx.x;
+    const int f = C.f;
     C.ys = a->mbw * 16;
     C.cs = a->mbw * 8;
     C.srcY = a->Y + (size_t)f * a->ysz + (size_t)mby * 16 * C.ys + mbx * 16;
@@ -1892,12 +1902,73 @@ __device__ __forceinline__ int opaque_lane(int lane)
     return lane;
 }
 
-template <int PASS>
+// ---------------------------------------------------------------------------
+// Row-parallel encode (small batches, single frames): one wave per workgroup,
+// MB rows handed out by a per-frame ticket, the row-to-row state (top_y, and in
+// pass 2 top_u/v, top_c, top_derr) and the progress counters in global memory.
+// A wave only waits for a row whose ticket an already running wave holds, so
+// the grid cannot deadlock whatever the residency.  Hand-off: every byte of the
+// row state is stored sc1 (write-through) and drained (vmcnt(0)) before the
+// sc1 progress store; the consumer polls progress with sc1 loads and reads the
+// bytes with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).
+// Pass 1's chroma raster chain (quirk A5) runs in workgroup 0 of each frame,
+// with its top_u/v/derr in its own LDS, as in the batch kernels.
+// ---------------------------------------------------------------------------
+struct RowsLayout {
+    size_t sync, ty, tu, tv, tc, td, frame;
+    __host__ __device__ RowsLayout(int mbw, int mbh)
+    {
+        auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+        sync = 0;                                  // int [4 + mbh]: ticket, pad x3, done MBs per row
+        ty = a16(4 * (4 + (size_t)mbh));
+        tu = ty + a16((size_t)mbw * 16 + 16);
+        tv = tu + a16((size_t)mbw * 8);
+        tc = tv + a16((size_t)mbw * 8);
+        td = tc + a16((size_t)mbw * 12);
+        frame = td + a16((size_t)mbw * 4);
+    }
+};
+#define ZW_ROWS_HDR 256  // launch header: [0] error word (a wave gave up waiting)
+#define ZW_ENC_SPIN_MAX (1 << 22)
+DI uint32_t ld_sc1(const void* p) { return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DI void st_sc1(void* p, uint32_t v) { __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DI int row_ticket(int* ticket)
+{
+    int t = 0;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(ticket, 1);
+    return __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+}
+// Wait until *prog >= need; seen caches the last value read (the row above
+// usually runs ahead, so most waits cost no memory round trip).  After
+// ZW_ENC_SPIN_MAX polls, or once another wave gave up, report through *err.
+DI void row_wait(const int* prog, int need, int* err, int& seen)
+{
+    if (seen >= need) return;
+    int it = 0;
+    for (;;) {
+        seen = __builtin_amdgcn_readfirstlane((int)ld_sc1(prog));
+        if (seen >= need) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > ZW_ENC_SPIN_MAX || ((it & 1023) == 0 && ld_sc1(err))) {
+            if ((threadIdx.x & 63) == 0) atomicOr(err, 1);
+            seen = 1 << 30;
+            break;
+        }
+    }
+}
+DI void row_publish(int* prog, int val)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are out
+    if ((threadIdx.x & 63) == 0) st_sc1(prog, (uint32_t)val);
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int PASS, bool ROWS>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
 {
-    constexpr int NW = PassShape<PASS>::NW, WG = PassShape<PASS>::WG;
+    constexpr int NW = ROWS ? 1 : PassShape<PASS>::NW, WG = ROWS ? 64 : PassShape<PASS>::WG;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int f = blockIdx.x;
+    const int f = ROWS ? blockIdx.y : blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int mbw = a.mbw, mbh = a.mbh;
     const ZwFrameParams* P = a.params + f;
@@ -1923,6 +1994,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
     int8_t* top_derr = (int8_t*)(smem + off);  // [mbw][4]
     WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
+    // row-parallel: is this workgroup pass 1's chroma chain (it keeps the
+    // frame-wide top_u/v/derr in LDS), and the frame's global row state
+    const bool chain_wg = PASS == 1 && (ROWS ? blockIdx.x == 0 : wv == 0);
+    const RowsLayout RL(mbw, mbh);
+    uint8_t* rb = ROWS ? a.rows + ZW_ROWS_HDR + (size_t)f * RL.frame : nullptr;
+    int* rerr = ROWS ? (int*)a.rows : nullptr;
+    int* rsync = (int*)rb;
 
     // init shared state
     for (int i = threadIdx.x; i < (int)(sizeof(T->lc) / 2); i += WG)
@@ -1937,14 +2015,17 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         ((uint32_t*)Sl)[i] = ((const uint32_t*)P->seg)[i];
     for (int i = threadIdx.x; i < 256; i += WG) seg_lut[i] = P->seg_enabled ? P->seg_map_lut[i] : 0;
     load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
-    for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
-    for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
-        top_u[i] = 127;
-        top_v[i] = 127;
+    if (!ROWS || chain_wg) {
+        for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
+        for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
+            top_u[i] = 127;
+            top_v[i] = 127;
+        }
+        for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
+        for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     }
-    for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
-    for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     if (threadIdx.x < NW) progress[threadIdx.x] = -1;
+    if (ROWS && lane < 12) W->win_c[lane] = 0;  // pass 1: the complexity contexts stay zero
     __syncthreads();
 
     Ctx C;
@@ -1953,6 +2034,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.T = T;
     C.W = W;
     C.lane = lane;
+    C.f = f;
     C.Sl = Sl;
     C.method = __builtin_amdgcn_readfirstlane(P->method);
     C.top_y = top_y;
@@ -1960,6 +2042,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.top_v = top_v;
     C.top_c = top_c;
     C.top_derr = top_derr;
+    C.oy = C.oc = C.ocx = C.od = 0;
     const bool trel = PASS == 2 && __builtin_amdgcn_readfirstlane(P->do_trellis);
     // without trellis (and without the pass-2 I4 dump) the final I4 blocks are
     // the search's winners, which the search leaves in W->lev / W->ws
@@ -1976,7 +2059,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     auto ph_flush = []() {};
 #endif
 
-    if (PASS == 1 && wv == 0) {
+    if (chain_wg) {
         // ---- pass-1 chroma raster chain ----
         // the chain is pass 1's critical path: it takes issue priority over the
         // luma waves sharing its SIMD (measured: 47.6 -> 44.3 ms per 256 1080p
@@ -1986,7 +2069,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #endif
         __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
         if (lane < 4) W->left_derr[lane] = 0;
-        MbFetch nx = fetch_mb(&a, lane, 0, 0);
+        MbFetch nx = fetch_mb(&a, f, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
                 W->left_u[lane] = 129;
@@ -1998,9 +2081,11 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 const int lane = opaque_lane(threadIdx.x & 63);
                 C.lane = lane;
                 const MbFetch cur = nx;
-                if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
-                else if (mby + 1 < mbh) nx = fetch_mb(&a, lane, 0, mby + 1);
+                if (mbx + 1 < mbw) nx = fetch_mb(&a, f, lane, mbx + 1, mby);
+                else if (mby + 1 < mbh) nx = fetch_mb(&a, f, lane, 0, mby + 1);
                 setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
+                C.oc = mbx * 8;
+                C.ocx = mbx * 12;
                 build_chroma_border(C);
                 const int cm = pick_uv<PASS>(C);
                 PH_MARK(8);
@@ -2051,8 +2136,23 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             if (luma_rank(v) == k) w = v;
         return w;
     };
-    const int rw = luma_rank(wv);
-    for (int mby = rw; mby < mbh; mby += nrw) {
+    const int rw = ROWS ? 0 : luma_rank(wv);
+    if (ROWS) {
+        // the wave's window stands in for the frame-wide top arrays (offsets 0)
+        C.top_y = W->win_y;
+        C.top_u = W->win_u;
+        C.top_v = W->win_v;
+        C.top_c = W->win_c;
+        C.top_derr = W->win_d;
+    }
+    uint8_t* const gty = ROWS ? rb + RL.ty : nullptr;
+    uint8_t* const gtu = ROWS ? rb + RL.tu : nullptr;
+    uint8_t* const gtv = ROWS ? rb + RL.tv : nullptr;
+    uint8_t* const gtc = ROWS ? rb + RL.tc : nullptr;
+    uint8_t* const gtd = ROWS ? rb + RL.td : nullptr;
+    for (int it = 0;; it++) {
+        const int mby = ROWS ? row_ticket(&rsync[0]) : rw + it * nrw;
+        if (mby >= mbh) break;
         if (lane < 20) W->left_y[lane] = 129;
         if (lane < 12) {
             W->left_u[lane] = 129;
@@ -2061,23 +2161,58 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         }
         if (lane < 4) W->left_derr[lane] = 0;
         wsync();
-        const int prevw = mby > 0 ? luma_wave((mby - 1) % nrw) : 0;
-        MbFetch nx = fetch_mb(&a, lane, 0, mby);
+        const int prevw = (!ROWS && mby > 0) ? luma_wave((mby - 1) % nrw) : 0;
+        int seen = -1;  // ROWS: last progress value read of the row above
+        int* const prog_above = ROWS ? rsync + 4 + (mby > 0 ? mby - 1 : 0) : nullptr;
+        // the row above has finished `need` MBs
+        auto wait_above = [&](int need) {
+            if (mby == 0) return;
+            if (ROWS) row_wait(prog_above, need, rerr, seen);
+            else wait_row(progress, prevw, (mby - 1) * 65536 + need);
+        };
+        MbFetch nx = fetch_mb(&a, f, lane, 0, mby);
         for (int mbx = 0; mbx < mbw; mbx++) {
             PH_START();
             const int lane = opaque_lane(threadIdx.x & 63);
             C.lane = lane;
             const MbFetch cur = nx;
-            if (mbx + 1 < mbw) nx = fetch_mb(&a, lane, mbx + 1, mby);
+            if (mbx + 1 < mbw) nx = fetch_mb(&a, f, lane, mbx + 1, mby);
             // the I16 and chroma searches need only the MB above (x, y-1); the
             // I4 search also reads the above-right MB's bottom row: wait for
             // (x+1, y-1) only then, so the wait overlaps the first searches
-            if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 1, mbw));
+            wait_above(min(mbx + 1, mbw));
+            if (ROWS) {
+                // pull this MB's slice of the row above's state into the window
+                if (mby > 0) {
+                    uint32_t v = 0;
+                    if (lane < 4) v = ld_sc1(gty + mbx * 16 + 4 * lane);
+                    else if (PASS == 2 && lane < 6) v = ld_sc1(gtu + mbx * 8 + 4 * (lane - 4));
+                    else if (PASS == 2 && lane < 8) v = ld_sc1(gtv + mbx * 8 + 4 * (lane - 6));
+                    else if (PASS == 2 && lane < 11) v = ld_sc1(gtc + mbx * 12 + 4 * (lane - 8));
+                    else if (PASS == 2 && lane < 12) v = ld_sc1(gtd + mbx * 4);
+                    if (lane < 4) ((uint32_t*)W->win_y)[lane] = v;
+                    else if (PASS == 2 && lane < 6) ((uint32_t*)W->win_u)[lane - 4] = v;
+                    else if (PASS == 2 && lane < 8) ((uint32_t*)W->win_v)[lane - 6] = v;
+                    else if (PASS == 2 && lane < 11) ((uint32_t*)W->win_c)[lane - 8] = v;
+                    else if (PASS == 2 && lane < 12) ((uint32_t*)W->win_d)[0] = v;
+                } else if (PASS == 2) {
+                    // row 0: zero contexts; top_derr from pass 1 (quirk A6)
+                    if (lane < 3) ((uint32_t*)W->win_c)[lane] = 0;
+                    else if (lane == 3)
+                        ((uint32_t*)W->win_d)[0] = *(const uint32_t*)(a.derr + (size_t)f * mbw * 4 + mbx * 4);
+                }
+                wsync();
+            } else {
+                C.oy = mbx * 16;
+                C.oc = mbx * 8;
+                C.ocx = mbx * 12;
+                C.od = mbx * 4;
+            }
 #ifndef ZW_DYN_PRIO
 #define ZW_DYN_PRIO 1  // slack (MBs) per priority level; 0: off
 #endif
 #if ZW_DYN_PRIO > 0
-            {
+            if (!ROWS) {
                 // Issue priority from the slack to the row above.  VALU issue is
                 // arbitrated by priority, then wave age: at equal priority the
                 // youngest waves of each SIMD run slowest and every row behind
@@ -2116,7 +2251,14 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             if (C.method > 1) {
                 const unsigned long long thr = 211ull * C.S->l_mode;
                 if (C.method >= 5 || i16s > thr || lm != 0) {
-                    if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + min(mbx + 2, mbw));
+                    wait_above(min(mbx + 2, mbw));
+                    if (ROWS && mby > 0 && mbx + 1 < mbw) {
+                        // the above-right MB's bottom row
+                        uint32_t v = 0;
+                        if (lane < 4) v = ld_sc1(gty + (mbx + 1) * 16 + 4 * lane);
+                        if (lane < 4) ((uint32_t*)W->win_y)[4 + lane] = v;
+                        wsync();
+                    }
                     build_luma_border(C, 1);
                     PH_MARK(21);
                     if (pick_i4<PASS>(C, i16s, keep_i4, i4nz)) {
@@ -2131,14 +2273,14 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             PH_MARK(4);
             int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             int cnz = 0;
-            if (PASS == 2) cnz = final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+            if (PASS == 2) cnz = final_chroma(C, cm, C.top_derr + C.od, uvnz);
             PH_MARK(5);
             ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
             if (PASS == 2) {
                 const int skip = !(lnz | cnz);
                 // complexity (encode_residual_data semantics / skip clearing)
                 if (lane == 0) {
-                    uint8_t* tc = top_c + mbx * 12;
+                    uint8_t* tc = C.top_c + C.ocx;
                     uint8_t* lc = W->left_c;
                     if (skip) {
                         for (int k = 1; k < 9; k++) tc[k] = lc[k] = 0;
@@ -2175,15 +2317,29 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             }
             if (lane < 16) o->bpred[lane] = lm == 4 ? W->modes[lane] : 0;
             store_luma_borders(C);
-            publish(progress, wv, mby * 65536 + mbx + 1);
+            if (ROWS) {
+                // push this MB's state for the row below (sc1), then publish
+                if (mby + 1 < mbh) {
+                    if (lane < 4) st_sc1(gty + mbx * 16 + 4 * lane, ((const uint32_t*)W->win_y)[lane]);
+                    else if (PASS == 2 && lane < 6) st_sc1(gtu + mbx * 8 + 4 * (lane - 4), ((const uint32_t*)W->win_u)[lane - 4]);
+                    else if (PASS == 2 && lane < 8) st_sc1(gtv + mbx * 8 + 4 * (lane - 6), ((const uint32_t*)W->win_v)[lane - 6]);
+                    else if (PASS == 2 && lane < 11) st_sc1(gtc + mbx * 12 + 4 * (lane - 8), ((const uint32_t*)W->win_c)[lane - 8]);
+                    else if (PASS == 2 && lane < 12) st_sc1(gtd + mbx * 4, ((const uint32_t*)W->win_d)[0]);
+                    row_publish(rsync + 4 + mby, mbx + 1);
+                }
+            } else {
+                publish(progress, wv, mby * 65536 + mbx + 1);
+            }
             PH_MARK(6);
         }
     }
     ph_flush();
 }
 
-extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1>(a); }
-extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1, false>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2, false>(a); }
+extern "C" __global__ __launch_bounds__(64) void k_encode_rows_pass1(EncArgs a) { encode_body<1, true>(a); }
+extern "C" __global__ __launch_bounds__(64) void k_encode_rows_pass2(EncArgs a) { encode_body<2, true>(a); }
 
 // ---------------------------------------------------------------------------
 // Kernel-level entry: quantisation (simple or trellis) of independent 4x4
@@ -2345,22 +2501,40 @@ extern "C" hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const Z
     return hipGetLastError();
 }
 
+// Bytes of zero-filled scratch the row-parallel kernels need for nframes frames.
+extern "C" size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes)
+{
+    return ZW_ROWS_HDR + (size_t)nframes * RowsLayout(mbw, mbh).frame;
+}
+
+// rows: null -> one 12-wave workgroup per frame (batches); otherwise the
+// row-parallel kernels with that zero-filled scratch (zwk_encode_rows_bytes).
 extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                                  const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost,
                                  int8_t* derr, ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz,
-                                 size_t csz, int mbw, int mbh, int nframes, int* dbg)
+                                 size_t csz, int mbw, int mbh, int nframes, int* dbg, uint8_t* rows)
 {
     EncArgs a;
     a.dbg = dbg;
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
-    const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW);
+    a.rows = rows;
     static const bool attr_set = []() {
         (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_rows_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_rows_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr_set;
+    if (rows) {
+        // one wave per MB row (+ pass 1's chroma chain in workgroup 0)
+        const size_t lds = encode_lds_bytes(mbw, 1);
+        if (pass == 1) hipLaunchKernelGGL(k_encode_rows_pass1, dim3(mbh + 1, nframes), dim3(64), lds, s, a);
+        else hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), lds, s, a);
+        return hipGetLastError();
+    }
+    const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW);
     if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(PassShape<1>::WG), lds, s, a);
     else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(PassShape<2>::WG), lds, s, a);
     return hipGetLastError();

@@ -41,7 +41,8 @@ hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                       const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost, int8_t* derr,
                       ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
-                      int nframes, int* dbg);
+                      int nframes, int* dbg, uint8_t* rows);
+size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -258,6 +259,7 @@ struct PipeLane {
     std::vector<hipEvent_t> cev;    // per chunk: [p1 done, p2 done]
     hipEvent_t ev[8] = {};
     unsigned long long* d_ctr = nullptr;
+    uint8_t* d_rows = nullptr;  // row-parallel encode scratch (small chunks), else null
     uint8_t* h_pack = nullptr;
     size_t h_pack_cap = 0;
     Pinned<unsigned long long> h_finfo;  // [2*n] offset, bytes of each frame's packed stream
@@ -308,6 +310,7 @@ static void pipe_free(zw_pipe* p)
         if (q) (void)hipFree(q);
     for (PipeLane& L : p->lanes) {
         if (L.d_ctr) (void)hipFree(L.d_ctr);
+        if (L.d_rows) (void)hipFree(L.d_rows);
         if (L.h_pack) (void)hipHostFree(L.h_pack);
         for (int i = 0; i < 8; i++)
             if (L.ev[i]) (void)hipEventDestroy(L.ev[i]);
@@ -345,6 +348,19 @@ static int pipe_chunk_for(int lane_frames, int device)
                 : 256;
     }
     return c > lane_frames ? lane_frames : c;
+}
+// Row-parallel encode kernels (one wave per MB row, spread over the CUs) for
+// chunks too small to fill the device with one 12-wave workgroup per frame.
+// ZW_ENC_ROWS=0/1 forces either shape.
+static bool pipe_rows_for(int chunk, int mbh, int device)
+{
+    const char* e = getenv("ZW_ENC_ROWS");
+    if (e && *e) return atoi(e) != 0;
+    hipDeviceProp_t prop;
+    const int cus = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
+                        ? prop.multiProcessorCount
+                        : 256;
+    return (long long)chunk * (mbh + 1) <= 8LL * cus;  // measured: rows win up to 32 1080p frames
 }
 
 extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t height, int color, uint8_t quality,
@@ -413,6 +429,10 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
              hipStreamCreateWithFlags(&L.stream2, hipStreamNonBlocking) == hipSuccess &&
              hipMalloc(&L.d_ctr, 2 * (size_t)nch * sizeof(unsigned long long)) == hipSuccess &&
              L.h_total.alloc(2 * (size_t)nch);
+        if (ok && pipe_rows_for(L.chunk, p->mbh, ctx->device)) {
+            const size_t rb = zwk_encode_rows_bytes(p->mbw, p->mbh, L.chunk);
+            ok = hipMalloc(&L.d_rows, rb) == hipSuccess && hipMemset(L.d_rows, 0, rb) == hipSuccess;
+        }
         for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
         for (size_t i = 0; ok && i < L.cev.size(); i++)
             ok = hipEventCreateWithFlags(&L.cev[i], hipEventDisableTiming) == hipSuccess;
@@ -469,6 +489,23 @@ static double now_ms()
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Zero the row-parallel kernels' per-frame tickets, progress and row state
+// before a launch of n frames.  The launch header (error word) is not cleared:
+// a wave that gave up waiting leaves it set, and rows_check fails the call.
+static hipError_t rows_reset(zw_pipe* p, PipeLane& L, int n)
+{
+    if (!L.d_rows) return hipSuccess;
+    const size_t hdr = zwk_encode_rows_bytes(p->mbw, p->mbh, 0);
+    return hipMemsetAsync(L.d_rows + hdr, 0, zwk_encode_rows_bytes(p->mbw, p->mbh, n) - hdr, L.stream);
+}
+static int rows_check(zw_pipe* p, PipeLane& L)
+{
+    if (!L.d_rows) return ZW_OK;
+    int err = 0;
+    HIPOK(hipMemcpy(&err, L.d_rows, sizeof err, hipMemcpyDeviceToHost));
+    return err ? ZW_EDEVICE : ZW_OK;
+}
+
 // ---- per-chunk stages (frames [fa, fa + na) of a lane) ----
 static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false)
 {
@@ -484,10 +521,12 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
                        p->csz, p->d_alpha + F * p->nmb, p->d_histo + F * 256, n));
     HIPOK(zwk_segments(s, p->d_histo + F * 256, p->d_tmpl, p->d_params + F, n));
     if (timed) HIPOK(hipEventRecord(L.ev[2], s));
+    HIPOK(rows_reset(p, L, n));
     HIPOK(zwk_encode(s, 1, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
                      p->d_params + F, nullptr, p->d_derr + F * p->mbw * 4, p->d_out1 + F * p->nmb,
                      write_recon ? p->d_ry + F * p->ysz : nullptr, write_recon ? p->d_ru + F * p->csz : nullptr,
-                     write_recon ? p->d_rv + F * p->csz : nullptr, p->ysz, p->csz, p->mbw, p->mbh, n, nullptr));
+                     write_recon ? p->d_rv + F * p->csz : nullptr, p->ysz, p->csz, p->mbw, p->mbh, n, nullptr,
+                     L.d_rows));
     if (timed) HIPOK(hipEventRecord(L.ev[3], s));
     return ZW_OK;
 }
@@ -576,10 +615,11 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa;
     if (timed) HIPOK(hipEventRecord(L.ev[4], s));
+    HIPOK(rows_reset(p, L, na));
     HIPOK(zwk_encode(s, 2, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
                      p->d_params + F, p->d_lcost + F, p->d_derr + F * p->mbw * 4, p->d_out2 + F * p->nmb,
                      p->d_ry + F * p->ysz, p->d_ru + F * p->csz, p->d_rv + F * p->csz, p->ysz, p->csz, p->mbw, p->mbh,
-                     na, p->d_dbg ? p->d_dbg + F * p->nmb * 16 * 34 : nullptr));
+                     na, p->d_dbg ? p->d_dbg + F * p->nmb * 16 * 34 : nullptr, L.d_rows));
     if (timed) HIPOK(hipEventRecord(L.ev[5], s));
     return ZW_OK;
 }
@@ -676,6 +716,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         }
     }
     HIPOK(hipStreamSynchronize(L.stream));
+    if ((r = rows_check(p, L))) return r;
     L.hms[0] = fetch / nb;
     L.hms[1] = stats / nb;
     L.hms[2] = fetch2 / nb;
@@ -723,7 +764,7 @@ extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
             if (r) return r;
         }
         HIPOK(hipStreamSynchronize(L.stream));
-        return ZW_OK;
+        return rows_check(p, L);
     });
 }
 

@@ -182,8 +182,13 @@ def _check_encode(ctx, w, h, kind, q, m, color, seed):
     return ref
 
 
+# rows "1": the row-parallel kernels (one wave per MB row, global-memory row
+# hand-off; the default for single frames), "0": one 12-wave workgroup per frame
+# (the batch kernels)
+@pytest.mark.parametrize("rows", ["1", "0"])
 @pytest.mark.parametrize("w,h,kind,q,m,color", ENC_CASES)
-def test_encode_matches_oracle(ctx, w, h, kind, q, m, color):
+def test_encode_matches_oracle(ctx, monkeypatch, w, h, kind, q, m, color, rows):
+    monkeypatch.setenv("ZW_ENC_ROWS", rows)
     _check_encode(ctx, w, h, kind, q, m, color, 0x5EED0000 + w * 7 + h)
 
 
@@ -194,6 +199,26 @@ def test_encode_batch_independent_frames(ctx):
     for i, img in enumerate(imgs):
         rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
         assert outs[i] == ref, f"frame {i}"
+
+
+@pytest.mark.parametrize("chunk", ["2", "3"])
+def test_encode_rows_multi_frame(ctx, monkeypatch, chunk):
+    """Row-parallel kernels over several frames per launch (grid y = frame) and
+    ragged chunks; the per-frame tickets / progress are reset per launch."""
+    monkeypatch.setenv("ZW_ENC_ROWS", "1")
+    monkeypatch.setenv("ZW_PIPE_CHUNK", chunk)
+    w, h = 208, 144
+    imgs = [synth_rgba(w, h, 0x5EED2000 + i, ("natural", "noise", "flat")[i % 3]) for i in range(5)]
+    p = zwebp.Pipeline(5, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    try:
+        for i, img in enumerate(imgs):
+            p.upload(i, img)
+        p.encode_repeat(2)
+        for i, img in enumerate(imgs):
+            rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
+            assert p.output(i) == ref, f"frame {i}"
+    finally:
+        p.close()
 
 
 def test_encode_repeat_streaming(ctx, monkeypatch):
@@ -380,17 +405,21 @@ def test_loop_filter_frame(ctx, monkeypatch, ftype, level, sharp, seg, rows):
 # --------------------------------------------------------------------------
 # Full-size (BASELINE configs) properties
 # --------------------------------------------------------------------------
-def test_1080p_encode_decode_roundtrip(ctx):
+@pytest.mark.parametrize("rows", ["1", "0"])
+def test_1080p_encode_decode_roundtrip(ctx, monkeypatch, rows):
     """1920x1080 Q75 m4: GPU bitstream == oracle bitstream; GPU decode of it == oracle decode."""
+    monkeypatch.setenv("ZW_ENC_ROWS", rows)
     ref = _check_encode(ctx, 1920, 1080, "natural", 75, 4, 3, 0x5EED0000)
     fr = zwebp.vp8_decode_frame(ref, ctx=ctx)
     rc, r = O.decode(ref)
     assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
 
 
-def test_4k_encode_matches_oracle(ctx):
+@pytest.mark.parametrize("rows", ["1", "0"])
+def test_4k_encode_matches_oracle(ctx, monkeypatch, rows):
     """BASELINE config 5 frame size (3840x2160, 240x135 MBs) Q75 m4: every stage
     and the bitstream equal the oracle's."""
+    monkeypatch.setenv("ZW_ENC_ROWS", rows)
     _check_encode(ctx, 3840, 2160, "natural", 75, 4, 3, 0x5EED4000)
 
 
