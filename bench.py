@@ -313,7 +313,49 @@ def single_frame(ctx, img, w, h, q, m, reps=3):
     p.close()
     return {"encode_frame_lossy_ms": seam_ms, "pipeline_1_frame_ms": pipe_ms,
             "kernel_ms": {"rgb2yuv": k[0], "analysis_segments": k[1], "encode_pass1": k[2], "encode_pass2": k[3]},
-            "note": "one frame = one workgroup (one CU) per encode pass"}
+            "note": "one frame: the row-parallel encode kernels (one wave per MB row, rows handed over through "
+                    "global memory); pass 1 is bounded by the chroma raster chain (quirk A5) on one wave"}
+
+
+def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
+    """Full-container rate (WebPEncoder::encode with EncoderParams::lossy on
+    RGBA input, api.rs:1291-1398): the pipe's container mode adds, per frame on
+    the emission threads, the ALPH chunk (encode_alpha_lossless of the host copy
+    of the frame's alpha plane) and the VP8X container.  Same device-resident
+    inputs as the headline line; the VP8 chunk of every output is checked
+    against the oracle digests."""
+    import struct
+    n = pipe.n
+    pipe.set_container([host_imgs[i % len(host_imgs)] for i in range(n)])
+    try:
+        pipe.encode_repeat(1)
+        t0 = time.perf_counter()
+        pipe.encode_repeat(steps)
+        el = time.perf_counter() - t0
+        ok = bad = 0
+        alph_bytes = 0
+        for i in range(n):
+            c = pipe.output(i)
+            off, vp8 = 12, None
+            while off + 8 <= len(c):
+                tag, ln = c[off:off + 4], struct.unpack("<I", c[off + 4:off + 8])[0]
+                if tag == b"VP8 ":
+                    vp8 = c[off + 8:off + 8 + ln]
+                elif tag == b"ALPH" and i == 0:
+                    alph_bytes = ln
+                off += 8 + ln + (ln & 1)
+            key = f"{w}x{h}/q{q}m{m}/{seeds[i % len(seeds)]:#010x}"
+            if vp8 is not None and hashlib.sha256(vp8).hexdigest() == digests.get(key):
+                ok += 1
+            else:
+                bad += 1
+        k = pipe.kernel_times()
+    finally:
+        pipe.set_container(None, enable=False)
+    return {"container_rgba_encodes_per_s": n * steps / el, "frames": n * steps, "ms_per_batch": el / steps * 1e3,
+            "host_emit_ms_per_batch": float(k[7]), "alph_bytes_frame0": alph_bytes,
+            "verified_vp8_chunks": ok, "mismatched": bad,
+            "note": "RIFF + VP8X + ALPH + VP8 per frame; inputs resident in HBM, alpha planes read from host memory"}
 
 
 def encode_roofline(p2_ms, launch_frames, nmb):
@@ -498,8 +540,9 @@ def main():
                                 "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"}
             line["encode_roofline"] = encode_roofline(p2_ms, per_launch, nmb)
             line["single_frame"] = single_frame(ctx, imgs[0], w, h, a.quality, a.method)
-            line["decode_path"] = decode_path(ctx, [bytes(pipes[0][0].output(i)) for i in range(min(B, D))], 256, w, h,
-                                              not a.no_cpu_baseline)
+            streams = [bytes(pipes[0][0].output(i)) for i in range(min(B, D))]  # VP8 frames, before container mode
+            line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, a.quality, a.method, seeds, digests)
+            line["decode_path"] = decode_path(ctx, streams, 256, w, h, not a.no_cpu_baseline)
         line["cpu_baseline"] = None
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)

@@ -174,6 +174,8 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream_) (void)hipStreamSynchronize(c->stream_);  // nothing queued may still use them
+    zw_pipe_destroy(c->pipe1);
+    c->pipe1 = nullptr;
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     c->dscratch = c->dscratch1 = nullptr;
@@ -189,6 +191,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    zw_pipe_destroy(c->pipe1);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     for (hipEvent_t e : c->dev_ev)
@@ -296,6 +299,10 @@ struct zw_pipe {
     std::vector<uint8_t> h_have_upd;
     std::vector<uint8_t> h_upd;  // [n][4*8*3*11]
     std::vector<std::vector<uint8_t>> bitstreams;
+    // container output (zw_pipe_set_container): RIFF/VP8X per frame, the ALPH
+    // chunk of an LA8 / RGBA8 frame encoded from its host copy
+    bool container = false;
+    std::vector<const uint8_t*> host_frames;
     std::vector<PipeLane> lanes;
     float kms[8];
 };
@@ -360,7 +367,7 @@ static bool pipe_rows_for(int chunk, int mbh, int device)
     const int cus = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
                         ? prop.multiProcessorCount
                         : 256;
-    return (long long)chunk * (mbh + 1) <= 8LL * cus;  // measured: rows win up to 32 1080p frames
+    return (long long)chunk * (mbh + 1) <= 12LL * cus;  // measured: rows win up to ~48 1080p frames
 }
 
 extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t height, int color, uint8_t quality,
@@ -475,6 +482,25 @@ extern "C" void zw_pipe_destroy(zw_pipe* p)
 }
 
 extern "C" void* zw_pipe_input_device_ptr(zw_pipe* p) { return p ? p->d_img : nullptr; }
+
+extern "C" int zw_pipe_set_container(zw_pipe* p, int enable, const uint8_t* const* host_frames)
+{
+    if (!p) return ZW_EINVAL;
+    if (!enable) {
+        p->container = false;
+        p->host_frames.clear();
+        return ZW_OK;
+    }
+    const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
+    if (has_alpha) {
+        if (!host_frames) return ZW_EINVAL;
+        for (int i = 0; i < p->n; i++)
+            if (!host_frames[i]) return ZW_EINVAL;
+        p->host_frames.assign(host_frames, host_frames + p->n);
+    }
+    p->container = true;
+    return ZW_OK;
+}
 
 extern "C" int zw_pipe_upload(zw_pipe* p, int frame, const uint8_t* data, size_t len)
 {
@@ -627,10 +653,27 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
 static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na)
 {
     const size_t F = (size_t)fa;
+    const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
     parallel_for(na, [&](int i) {
         const size_t f = F + i;
-        zwh::emit_frame(p->bitstreams[f], p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h,
-                        p->h_have_upd[f] != 0, (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
+        std::vector<uint8_t>& out = p->bitstreams[f];
+        if (!p->container) {
+            zwh::emit_frame(out, p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h, p->h_have_upd[f] != 0,
+                            (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
+            return;
+        }
+        // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the
+        // VP8 frame, and for alpha inputs the ALPH chunk (encode_alpha_lossless)
+        thread_local std::vector<uint8_t> vp8, alph;
+        vp8.clear();
+        alph.clear();
+        zwh::emit_frame(vp8, p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h, p->h_have_upd[f] != 0,
+                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
+        // the image was validated by zw_pipe_set_container (size, dimensions)
+        if (has_alpha) (void)zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph);
+        const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
+        out.clear();
+        zw_webp_wrap(out, vp8.data(), vp8.size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w, p->h, md);
     });
 }
 
@@ -924,8 +967,49 @@ extern "C" int zw_encode_batch(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t
             return ZW_EINVAL;
     }
     zw_pipe* p = nullptr;
+    int r;
+    const int key[5] = {(int)imgs[0].width, (int)imgs[0].height, imgs[0].color, quality, method};
+    const bool one = n == 1;
+    if (one && ctx->pipe1 && !memcmp(key, ctx->pipe1_key, sizeof key)) {
+        p = ctx->pipe1;  // a one-frame pipeline of this shape from an earlier call
+    } else {
+        r = zw_pipe_create(ctx, n, imgs[0].width, imgs[0].height, imgs[0].color, quality, method, &p);
+        if (r) return r;
+        if (one) {
+            zw_pipe_destroy(ctx->pipe1);
+            ctx->pipe1 = p;
+            memcpy(ctx->pipe1_key, key, sizeof key);
+        }
+    }
+    r = ZW_OK;
+    for (int i = 0; i < n && !r; i++) r = zw_pipe_upload(p, i, imgs[i].data, imgs[i].len);
+    if (!r) r = zw_pipe_encode(p);
+    for (int i = 0; i < n && !r; i++) r = zw_pipe_output(p, i, &outs[i]);
+    if (!one || r) {
+        if (p == ctx->pipe1) ctx->pipe1 = nullptr;  // not reused after a failure
+        zw_pipe_destroy(p);
+    }
+    return r;
+}
+
+extern "C" int zw_encode_webp_batch(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t quality, uint8_t method,
+                                    zw_bytes* outs)
+{
+    if (!ctx || n <= 0 || !imgs || !outs) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) {
+        outs[i].data = nullptr;
+        outs[i].len = 0;
+        int r = check_encode_args(imgs[i].data, imgs[i].len, imgs[i].width, imgs[i].height, imgs[i].color, quality);
+        if (r) return r;
+        if (imgs[i].width != imgs[0].width || imgs[i].height != imgs[0].height || imgs[i].color != imgs[0].color)
+            return ZW_EINVAL;
+    }
+    zw_pipe* p = nullptr;
     int r = zw_pipe_create(ctx, n, imgs[0].width, imgs[0].height, imgs[0].color, quality, method, &p);
     if (r) return r;
+    std::vector<const uint8_t*> host(n);
+    for (int i = 0; i < n; i++) host[i] = imgs[i].data;
+    r = zw_pipe_set_container(p, 1, host.data());
     for (int i = 0; i < n && !r; i++) r = zw_pipe_upload(p, i, imgs[i].data, imgs[i].len);
     if (!r) r = zw_pipe_encode(p);
     for (int i = 0; i < n && !r; i++) r = zw_pipe_output(p, i, &outs[i]);

@@ -37,6 +37,11 @@ struct zw_ctx {
     hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t dev_ev1[4] = {nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
+    // one-frame encode pipeline kept between encode_frame_lossy calls of the
+    // same shape (dimensions, colour type, quality, method): its device buffers
+    // and streams are reused instead of allocated per call
+    struct zw_pipe* pipe1 = nullptr;
+    int pipe1_key[5] = {0, 0, 0, 0, 0};
 };
 
 #define HIPOK(x)                                  \
@@ -140,3 +145,12 @@ static inline void* ctx_pinned(zw_ctx* c, int which, size_t bytes)
     }
     return c->hpin[which];
 }
+
+// Host lossless coder and container writer (zw_host_lossless.cpp).
+int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color, bool predictor,
+                   bool implicit_dims, std::vector<uint8_t>& out);
+int zw_alph_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                   std::vector<uint8_t>& out);
+void zw_webp_wrap(std::vector<uint8_t>& o, const uint8_t* frame, size_t flen, const char* tag,
+                  const std::vector<uint8_t>* alph, bool has_alpha, uint32_t width, uint32_t height,
+                  const zw_metadata& md);

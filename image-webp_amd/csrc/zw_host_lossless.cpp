@@ -16,6 +16,7 @@
 // reference.  Over-long trees (> 15 bits, > 7 for the code-length code) are
 // re-balanced as the reference does; among equal frequencies the reference's
 // sort_unstable order is Rust's ipnsort's and here a stable order (see DESIGN).
+#include <algorithm>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -245,84 +246,73 @@ inline void run_symbol(uint32_t run, uint32_t& sym, uint32_t& extra)
 
 }  // namespace
 
-// encode_frame_lossless (:945-1173) into `out` (appended).
-int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color, bool predictor,
-                   bool implicit_dims, std::vector<uint8_t>& out)
+namespace {
+// Per-pixel residual element: the packed ARGB residual (bytes r, g, b, a), or,
+// for L8 images (the ALPH plane), only the green byte -- red and blue are 0
+// and alpha constant there, so two residuals are equal exactly when their
+// green bytes are.
+template <class T> struct Px;
+template <> struct Px<uint32_t> {
+    static uint32_t g(uint32_t c) { return (c >> 8) & 255; }
+    static uint32_t r(uint32_t c) { return c & 255; }
+    static uint32_t b(uint32_t c) { return (c >> 16) & 255; }
+    static uint32_t a(uint32_t c) { return c >> 24; }
+};
+template <> struct Px<uint8_t> {
+    static uint32_t g(uint8_t c) { return c; }
+    static uint32_t r(uint8_t) { return 0; }
+    static uint32_t b(uint8_t) { return 0; }
+    static uint32_t a(uint8_t) { return 0; }
+};
+// count_run (:366-393): repeats of px[p] after it, at most 4096
+inline uint32_t run_after(const uint32_t* px, size_t p, size_t npx)
 {
-    if (color < ZW_COLOR_L8 || color > ZW_COLOR_RGBA8) return ZW_EINVAL;
-    const int bpp = color + 1;
-    const bool rgb = color >= ZW_COLOR_RGB8, alpha = color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8;
-    if (!data && len) return ZW_EINVAL;
-    if ((uint64_t)width * height * (uint64_t)bpp != (uint64_t)len) return ZW_EINVALID_BUFFER_SIZE;
-    if (width == 0 || width > 16384 || height == 0 || height > 16384) return ZW_EINVALID_DIMENSIONS;
-    BitSink w(out);
-    if (!implicit_dims) {
-        w.put(0x2f, 8);
-        w.put(width - 1, 14);
-        w.put(height - 1, 14);
-        w.put(alpha ? 1 : 0, 1);
-        w.put(0, 3);
-    }
-    w.put(5, 3);  // subtract-green transform
-    if (predictor) {
-        w.put(0x39, 6);  // predictor transform, size bits, no colour cache, mode-2 sub-image
-        w.put(0, 1);
-        put_single_symbol_code(w, 2);
-        for (int i = 0; i < 4; i++) put_single_symbol_code(w, 0);
-    }
-    w.put(0, 1);  // no more transforms
-    w.put(0, 1);  // no colour cache
-    w.put(0, 1);  // no meta Huffman codes
-
-    // ARGB residuals, one uint32 per pixel (bytes r, g, b, a): expand, subtract
-    // green, then the predictor's "pixel minus the pixel above (row 0: left)"
-    const size_t npx = (size_t)width * height;
-    std::vector<uint32_t> px(npx);
-    auto pack = [](uint32_t r, uint32_t g, uint32_t b, uint32_t a) { return r | (g << 8) | (b << 16) | (a << 24); };
-    parallel_for((int)height, [&](int y) {
-        for (size_t x = 0; x < width; x++) {
-            const size_t i = (size_t)y * width + x;
-            const uint8_t* s = data + i * bpp;
-            uint32_t r, g, b, a;
-            switch (color) {
-            case ZW_COLOR_L8: r = g = b = s[0]; a = 255; break;
-            case ZW_COLOR_LA8: r = g = b = s[0]; a = s[1]; break;
-            case ZW_COLOR_RGB8: r = s[0]; g = s[1]; b = s[2]; a = 255; break;
-            default: r = s[0]; g = s[1]; b = s[2]; a = s[3]; break;
-            }
-            px[i] = pack((r - g) & 255, g, (b - g) & 255, a);
+    const uint32_t c = px[p];
+    uint32_t run = 0;
+    while (run < 4096 && p + 1 + run < npx && px[p + 1 + run] == c) run++;
+    return run;
+}
+inline uint32_t run_after(const uint8_t* px, size_t p, size_t npx)
+{
+    const uint8_t c = px[p];
+    const size_t lim = std::min<size_t>(4096, npx - 1 - p);
+    const uint64_t rep = 0x0101010101010101ull * c;
+    size_t run = 0;
+    while (run + 8 <= lim) {  // eight pixels per compare
+        uint64_t v;
+        memcpy(&v, px + p + 1 + run, 8);
+        if (v != rep) {
+            run += (size_t)__builtin_ctzll(v ^ rep) >> 3;
+            return (uint32_t)run;
         }
-    });
-    auto bytesub = [](uint32_t c, uint32_t p) {  // per-byte wrapping subtraction
-        return ((c | 0x80808080u) - (p & 0x7f7f7f7fu)) ^ ((c ^ ~p) & 0x80808080u);
-    };
-    if (predictor) {
-        std::vector<uint32_t> up(px);  // rows are differenced against the ORIGINAL row above
-        parallel_for((int)height - 1, [&](int yy) {
-            const size_t y = (size_t)yy + 1;
-            for (size_t x = 0; x < width; x++) px[y * width + x] = bytesub(up[y * width + x], up[(y - 1) * width + x]);
-        });
-        for (size_t x = width - 1; x >= 1; x--) px[x] = bytesub(up[x], up[x - 1]);
-        px[0] = bytesub(up[0], pack(0, 0, 0, 255));
+        run += 8;
     }
+    while (run < lim && px[p + 1 + run] == c) run++;
+    return (uint32_t)run;
+}
 
+// The Huffman codes and the pixel/run symbols of encode_frame_lossless
+// (:1040-1173) over the residuals px.
+template <class T>
+void code_pixels(const T* px, size_t npx, bool rgb, bool alpha, bool predictor, BitSink& w)
+{
+    using X = Px<T>;
     // symbol statistics: every pixel codes green (+ red/blue/alpha), then an
     // optional run of up to 4096 repeats of that pixel
     uint32_t fr[256] = {0}, fg[280] = {0}, fb[256] = {0}, fa[256] = {0};
     if (!rgb) fr[0] = fb[0] = 1;
     if (!alpha) fa[0] = 1;
     std::vector<uint16_t> runs;  // run after each coded pixel
-    runs.reserve(npx / 2 + 1);
+    runs.reserve(npx / 64 + 16);
     for (size_t p = 0; p < npx;) {
-        const uint32_t c = px[p];
-        fg[(c >> 8) & 255]++;
+        const T c = px[p];
+        fg[X::g(c)]++;
         if (rgb) {
-            fr[c & 255]++;
-            fb[(c >> 16) & 255]++;
+            fr[X::r(c)]++;
+            fb[X::b(c)]++;
         }
-        if (alpha) fa[c >> 24]++;
-        uint32_t run = 0;
-        while (run < 4096 && p + 1 + run < npx && px[p + 1 + run] == c) run++;
+        if (alpha) fa[X::a(c)]++;
+        const uint32_t run = run_after(px, p, npx);
         if (run) {
             if (run <= 4) {
                 fg[256 + run - 1]++;
@@ -357,8 +347,8 @@ int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t hei
 
     size_t k = 0;
     for (size_t p = 0; p < npx; k++) {
-        const uint32_t c = px[p];
-        const uint32_t g = (c >> 8) & 255, r = c & 255, b = (c >> 16) & 255, a = c >> 24;
+        const T c = px[p];
+        const uint32_t g = X::g(c), r = X::r(c), b = X::b(c), a = X::a(c);
         uint64_t bits = cg[g];
         unsigned nb = lg[g];
         if (rgb) {
@@ -386,10 +376,112 @@ int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t hei
         p += 1 + run;
     }
     w.finish();
+}
+
+void put_transforms(BitSink& w, uint32_t width, uint32_t height, bool alpha, bool predictor, bool implicit_dims)
+{
+    if (!implicit_dims) {
+        w.put(0x2f, 8);
+        w.put(width - 1, 14);
+        w.put(height - 1, 14);
+        w.put(alpha ? 1 : 0, 1);
+        w.put(0, 3);
+    }
+    w.put(5, 3);  // subtract-green transform
+    if (predictor) {
+        w.put(0x39, 6);  // predictor transform, size bits, no colour cache, mode-2 sub-image
+        w.put(0, 1);
+        put_single_symbol_code(w, 2);
+        for (int i = 0; i < 4; i++) put_single_symbol_code(w, 0);
+    }
+    w.put(0, 1);  // no more transforms
+    w.put(0, 1);  // no colour cache
+    w.put(0, 1);  // no meta Huffman codes
+}
+
+// An L8 image read from byte `off` of every `bpp`-byte pixel (the grey plane,
+// or the alpha channel of an LA8 / RGBA8 image for ALPH): its green residuals
+// in one pass (subtract-green leaves green; the predictor takes the pixel above,
+// on row 0 the pixel to the left, and 0 for the first pixel).
+void l8_residuals(const uint8_t* data, int bpp, int off, uint32_t width, uint32_t height, bool predictor,
+                  uint8_t* g)
+{
+    const size_t W = width;
+    const uint8_t* s = data + off;
+    if (!predictor) {
+        for (size_t i = 0; i < W * height; i++) g[i] = s[i * bpp];
+        return;
+    }
+    g[0] = s[0];
+    for (size_t x = 1; x < W; x++) g[x] = (uint8_t)(s[x * bpp] - s[(x - 1) * bpp]);
+    for (size_t y = 1; y < height; y++) {
+        const uint8_t* cur = s + y * W * bpp;
+        const uint8_t* up = cur - W * bpp;
+        uint8_t* o = g + y * W;
+        if (bpp == 1) {
+            for (size_t x = 0; x < W; x++) o[x] = (uint8_t)(cur[x] - up[x]);
+        } else {
+            for (size_t x = 0; x < W; x++) o[x] = (uint8_t)(cur[x * bpp] - up[x * bpp]);
+        }
+    }
+}
+}  // namespace
+
+// encode_frame_lossless (:945-1173) into `out` (appended).
+int zw_vp8l_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color, bool predictor,
+                   bool implicit_dims, std::vector<uint8_t>& out)
+{
+    if (color < ZW_COLOR_L8 || color > ZW_COLOR_RGBA8) return ZW_EINVAL;
+    const int bpp = color + 1;
+    const bool rgb = color >= ZW_COLOR_RGB8, alpha = color == ZW_COLOR_LA8 || color == ZW_COLOR_RGBA8;
+    if (!data && len) return ZW_EINVAL;
+    if ((uint64_t)width * height * (uint64_t)bpp != (uint64_t)len) return ZW_EINVALID_BUFFER_SIZE;
+    if (width == 0 || width > 16384 || height == 0 || height > 16384) return ZW_EINVALID_DIMENSIONS;
+    BitSink w(out);
+    put_transforms(w, width, height, alpha, predictor, implicit_dims);
+    const size_t npx = (size_t)width * height;
+    if (color == ZW_COLOR_L8) {
+        std::vector<uint8_t> g(npx);
+        l8_residuals(data, 1, 0, width, height, predictor, g.data());
+        code_pixels(g.data(), npx, false, false, predictor, w);
+        return ZW_OK;
+    }
+
+    // ARGB residuals, one uint32 per pixel (bytes r, g, b, a): expand, subtract
+    // green, then the predictor's "pixel minus the pixel above (row 0: left)"
+    std::vector<uint32_t> px(npx);
+    auto pack = [](uint32_t r, uint32_t g, uint32_t b, uint32_t a) { return r | (g << 8) | (b << 16) | (a << 24); };
+    parallel_for((int)height, [&](int y) {
+        for (size_t x = 0; x < width; x++) {
+            const size_t i = (size_t)y * width + x;
+            const uint8_t* s = data + i * bpp;
+            uint32_t r, g, b, a;
+            switch (color) {
+            case ZW_COLOR_LA8: r = g = b = s[0]; a = s[1]; break;
+            case ZW_COLOR_RGB8: r = s[0]; g = s[1]; b = s[2]; a = 255; break;
+            default: r = s[0]; g = s[1]; b = s[2]; a = s[3]; break;
+            }
+            px[i] = pack((r - g) & 255, g, (b - g) & 255, a);
+        }
+    });
+    auto bytesub = [](uint32_t c, uint32_t p) {  // per-byte wrapping subtraction
+        return ((c | 0x80808080u) - (p & 0x7f7f7f7fu)) ^ ((c ^ ~p) & 0x80808080u);
+    };
+    if (predictor) {
+        std::vector<uint32_t> up(px);  // rows are differenced against the ORIGINAL row above
+        parallel_for((int)height - 1, [&](int yy) {
+            const size_t y = (size_t)yy + 1;
+            for (size_t x = 0; x < width; x++) px[y * width + x] = bytesub(up[y * width + x], up[(y - 1) * width + x]);
+        });
+        for (size_t x = width - 1; x >= 1; x--) px[x] = bytesub(up[x], up[x - 1]);
+        px[0] = bytesub(up[0], pack(0, 0, 0, 255));
+    }
+    code_pixels(px.data(), npx, rgb, alpha, predictor, w);
     return ZW_OK;
 }
 
-// encode_alpha_lossless (:1175-1222)
+// encode_alpha_lossless (:1175-1222): the alpha channel as an L8 image with the
+// predictor on and implicit dimensions, behind a one-byte header.
 int zw_alph_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
                    std::vector<uint8_t>& out)
 {
@@ -397,11 +489,14 @@ int zw_alph_encode(const uint8_t* data, size_t len, uint32_t width, uint32_t hei
     if (width == 0 || width > 16384 || height == 0 || height > 16384) return ZW_EINVALID_DIMENSIONS;
     const int bpp = color == ZW_COLOR_LA8 ? 2 : 4;
     const size_t npx = (size_t)width * height;
-    if (len != npx * bpp) return ZW_EINVALID_BUFFER_SIZE;
-    std::vector<uint8_t> a(npx);
-    for (size_t i = 0; i < npx; i++) a[i] = data[i * bpp + bpp - 1];
+    if (!data || len != npx * bpp) return ZW_EINVALID_BUFFER_SIZE;
     out.push_back(1);  // no preprocessing, no filtering, lossless compression
-    return zw_vp8l_encode(a.data(), npx, width, height, ZW_COLOR_L8, true, true, out);
+    std::vector<uint8_t> g(npx);
+    l8_residuals(data, bpp, bpp - 1, width, height, true, g.data());
+    BitSink w(out);
+    put_transforms(w, width, height, false, true, true);
+    code_pixels(g.data(), npx, false, false, true, w);
+    return ZW_OK;
 }
 
 static int to_bytes(const std::vector<uint8_t>& v, zw_bytes* out)
@@ -450,6 +545,49 @@ void put_chunk(std::vector<uint8_t>& o, const char* tag, const uint8_t* p, size_
 }
 }  // namespace
 
+// The RIFF container of WebPEncoder::encode (:1317-1395): the simple form
+// ("VP8 " / "VP8L" chunk only) without metadata and ALPH, else VP8X with
+// ICCP, ALPH, the frame, EXIF and XMP in that order.  alph: the ALPH payload
+// of a lossy encode with alpha, else null.
+void zw_webp_wrap(std::vector<uint8_t>& o, const uint8_t* frame, size_t flen, const char* tag,
+                  const std::vector<uint8_t>* alph, bool has_alpha, uint32_t width, uint32_t height,
+                  const zw_metadata& md)
+{
+    const bool simple = !md.icc_len && !md.exif_len && !md.xmp_len && !alph;
+    o.reserve(o.size() + flen + (alph ? alph->size() : 0) + md.icc_len + md.exif_len + md.xmp_len + 96);
+    if (simple) {
+        o.insert(o.end(), {'R', 'I', 'F', 'F'});
+        put_le32(o, chunk_bytes(flen) + 4);
+        o.insert(o.end(), {'W', 'E', 'B', 'P'});
+        put_chunk(o, tag, frame, flen);
+        return;
+    }
+    uint32_t total = 22 + chunk_bytes(flen);
+    if (md.icc_len) total += chunk_bytes(md.icc_len);
+    if (md.exif_len) total += chunk_bytes(md.exif_len);
+    if (md.xmp_len) total += chunk_bytes(md.xmp_len);
+    if (alph) total += chunk_bytes(alph->size());
+    uint8_t flags = 0;
+    if (md.xmp_len) flags |= 1 << 2;
+    if (md.exif_len) flags |= 1 << 3;
+    if (has_alpha) flags |= 1 << 4;
+    if (md.icc_len) flags |= 1 << 5;
+    o.insert(o.end(), {'R', 'I', 'F', 'F'});
+    put_le32(o, total);
+    o.insert(o.end(), {'W', 'E', 'B', 'P'});
+    uint8_t x[10] = {flags, 0, 0, 0};
+    for (int i = 0; i < 3; i++) {
+        x[4 + i] = (uint8_t)((width - 1) >> (8 * i));
+        x[7 + i] = (uint8_t)((height - 1) >> (8 * i));
+    }
+    put_chunk(o, "VP8X", x, 10);
+    if (md.icc_len) put_chunk(o, "ICCP", md.icc, md.icc_len);
+    if (alph) put_chunk(o, "ALPH", alph->data(), alph->size());
+    put_chunk(o, tag, frame, flen);
+    if (md.exif_len) put_chunk(o, "EXIF", md.exif, md.exif_len);
+    if (md.xmp_len) put_chunk(o, "XMP ", md.xmp, md.xmp_len);
+}
+
 // WebPEncoder::encode (:1291-1398) with EncoderParams and metadata.
 extern "C" int zw_encode_webp_ex(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
                                  int color, const zw_encoder_params* params, const zw_metadata* meta, zw_bytes* out)
@@ -481,42 +619,10 @@ extern "C" int zw_encode_webp_ex(zw_ctx* ctx, const uint8_t* data, size_t len, u
             return r;
         tag = "VP8L";
     }
-    std::vector<uint8_t> o;
-    const bool simple = !md.icc_len && !md.exif_len && !md.xmp_len && !lossy_alpha;
-    if (simple) {
-        o.insert(o.end(), {'R', 'I', 'F', 'F'});
-        put_le32(o, chunk_bytes(frame.size()) + 4);
-        o.insert(o.end(), {'W', 'E', 'B', 'P'});
-        put_chunk(o, tag, frame.data(), frame.size());
-        return to_bytes(o, out);
-    }
     std::vector<uint8_t> alph;
-    uint32_t total = 22 + chunk_bytes(frame.size());
-    if (md.icc_len) total += chunk_bytes(md.icc_len);
-    if (md.exif_len) total += chunk_bytes(md.exif_len);
-    if (md.xmp_len) total += chunk_bytes(md.xmp_len);
-    if (lossy_alpha) {
+    if (lossy_alpha)
         if (int r = zw_alph_encode(data, len, width, height, color, alph)) return r;
-        total += chunk_bytes(alph.size());
-    }
-    uint8_t flags = 0;
-    if (md.xmp_len) flags |= 1 << 2;
-    if (md.exif_len) flags |= 1 << 3;
-    if (has_alpha) flags |= 1 << 4;
-    if (md.icc_len) flags |= 1 << 5;
-    o.insert(o.end(), {'R', 'I', 'F', 'F'});
-    put_le32(o, total);
-    o.insert(o.end(), {'W', 'E', 'B', 'P'});
-    uint8_t x[10] = {flags, 0, 0, 0};
-    for (int i = 0; i < 3; i++) {
-        x[4 + i] = (uint8_t)((width - 1) >> (8 * i));
-        x[7 + i] = (uint8_t)((height - 1) >> (8 * i));
-    }
-    put_chunk(o, "VP8X", x, 10);
-    if (md.icc_len) put_chunk(o, "ICCP", md.icc, md.icc_len);
-    if (lossy_alpha) put_chunk(o, "ALPH", alph.data(), alph.size());
-    put_chunk(o, tag, frame.data(), frame.size());
-    if (md.exif_len) put_chunk(o, "EXIF", md.exif, md.exif_len);
-    if (md.xmp_len) put_chunk(o, "XMP ", md.xmp, md.xmp_len);
+    std::vector<uint8_t> o;
+    zw_webp_wrap(o, frame.data(), frame.size(), tag, lossy_alpha ? &alph : nullptr, has_alpha, width, height, md);
     return to_bytes(o, out);
 }

@@ -126,6 +126,7 @@ SIGNATURES = [
     ("zw_encode_frame_lossless", _I, [_VP, _SZ, _U32, _U32, _I, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_alpha", _I, [_VP, _SZ, _U32, _U32, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_webp_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_rgb", _I, [_VP, _VP, _SZ, _I, _I, ctypes.POINTER(_Bytes), ctypes.POINTER(_U32),
@@ -146,6 +147,7 @@ SIGNATURES = [
     ("zw_pipe_destroy", None, [_VP]),
     ("zw_pipe_input_device_ptr", _VP, [_VP]),
     ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
+    ("zw_pipe_set_container", _I, [_VP, _I, ctypes.POINTER(_VP)]),
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
@@ -277,6 +279,21 @@ def encode_batch(images, width, height, color, quality=75, method=4, ctx=None):
         imgs[i] = _Image(a.ctypes.data, a.size, width, height, color)
     outs = (_Bytes * n)()
     _check(L.zw_encode_batch(c.handle, n, imgs, quality, method, outs), "encode_batch", EncodingError)
+    return [_take_bytes(L, outs[i]) for i in range(n)]
+
+
+def encode_webp_batch(images, width, height, color, quality=75, method=4, ctx=None):
+    """n WebPEncoder::encode calls with EncoderParams::lossy(quality, method) in
+    one device pass: a RIFF container per frame (VP8X + ALPH for LA8 / RGBA8)."""
+    c = _ctx(ctx)
+    L = c._lib
+    arrs = [_as_u8(im) for im in images]
+    n = len(arrs)
+    imgs = (_Image * n)()
+    for i, a in enumerate(arrs):
+        imgs[i] = _Image(a.ctypes.data, a.size, width, height, color)
+    outs = (_Bytes * n)()
+    _check(L.zw_encode_webp_batch(c.handle, n, imgs, quality, method, outs), "encode_webp_batch", EncodingError)
     return [_take_bytes(L, outs[i]) for i in range(n)]
 
 
@@ -649,6 +666,17 @@ class Pipeline:
     def upload(self, i, img):
         a = _as_u8(img)
         _check(self._lib.zw_pipe_upload(self._h, i, _ptr(a), a.size), "zw_pipe_upload")
+
+    def set_container(self, host_frames=None, enable=True):
+        """Outputs become WebP containers (WebPEncoder::encode, lossy params);
+        for LA8 / RGBA8 the ALPH chunk is encoded from host_frames[i], which the
+        pipeline keeps referenced."""
+        self._host_frames = [_as_u8(f) for f in host_frames] if host_frames is not None else None
+        ptrs = None
+        if self._host_frames is not None:
+            ptrs = (ctypes.c_void_p * len(self._host_frames))(*[f.ctypes.data for f in self._host_frames])
+        _check(self._lib.zw_pipe_set_container(self._h, 1 if enable else 0, ptrs), "zw_pipe_set_container",
+               EncodingError)
 
     def encode(self):
         _check(self._lib.zw_pipe_encode(self._h), "zw_pipe_encode", EncodingError)

@@ -149,6 +149,11 @@ int zw_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t he
 
 /* n independent frames of identical size/color; outs[i] receives frame i. */
 int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method, zw_bytes *outs);
+/* n independent WebPEncoder::encode calls with EncoderParams::lossy(quality,
+ * method) (api.rs:1291-1398; new: batch): outs[i] is frame i's RIFF container,
+ * with VP8X + ALPH for LA8 / RGBA8.  The ALPH chunks are encoded on the host
+ * threads that emit the VP8 tokens, while the device runs later frames. */
+int zw_encode_webp_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method, zw_bytes *outs);
 
 /* Vp8Decoder::decode_frame */
 int zw_vp8_decode_frame(zw_ctx *ctx, const uint8_t *vp8, size_t len, zw_frame *out);
@@ -223,6 +228,12 @@ int zw_pipe_create(zw_ctx *ctx, int nframes, uint32_t width, uint32_t height, in
 void zw_pipe_destroy(zw_pipe *p);
 void *zw_pipe_input_device_ptr(zw_pipe *p);
 int zw_pipe_upload(zw_pipe *p, int frame, const uint8_t *data, size_t len);
+/* Container output: zw_pipe_output then returns WebPEncoder::encode's RIFF
+ * container (EncoderParams::lossy) instead of the bare VP8 frame.  For LA8 /
+ * RGBA8 the ALPH chunk is encoded from host_frames[i] (width*height*bpp bytes,
+ * valid while the pipe encodes); host_frames may be NULL for L8 / RGB8.
+ * enable = 0 switches back to bare frames. */
+int zw_pipe_set_container(zw_pipe *p, int enable, const uint8_t *const *host_frames);
 /* Runs the full encode of all frames; bitstreams retrievable afterwards. */
 int zw_pipe_encode(zw_pipe *p);
 /* Encodes the uploaded batch n times back to back, streaming-style: batch k+1's
@@ -247,10 +258,12 @@ int zw_pipe_enable_debug(zw_pipe *p);
 int zw_pipe_read_debug(zw_pipe *p, int frame, int32_t *out);
 /* Token probabilities (4*8*3*11) and skip probability used by pass 2. */
 int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
-/* The pipe splits its frames into lanes (env ZW_PIPE_LANES, default 2), each with
+/* The pipe splits its frames into lanes (env ZW_PIPE_LANES, default 1), each with
  * a kernel stream and a copy stream, and each lane into chunks (env
- * ZW_PIPE_CHUNK, default 128 frames per launch): the host entropy work on one
- * chunk overlaps the kernels of the next.  zw_pipe_kernel_times: ms[0..3] = mean per-launch device time of
+ * ZW_PIPE_CHUNK, default one frame per CU per launch): the host entropy work on
+ * one chunk overlaps the kernels of the next.  Chunks of at most 12 MB rows per CU
+ * run the row-parallel encode kernels (one wave per MB row; env ZW_ENC_ROWS=0/1
+ * forces either shape).  zw_pipe_kernel_times: ms[0..3] = mean per-launch device time of
  * rgb2yuv, analysis+segments, pass 1, pass 2 (each launch covers one lane's
  * frames); ms[4..7] = host ms of fetch1, stats, fetch2, emit (max over lanes). */
 int zw_pipe_lanes(zw_pipe *p);

@@ -143,6 +143,37 @@ def test_encode_webp_rgba_entry(ctx):
     assert got == bytes(enc.encode(img, w, h, zwebp.ColorType.Rgba8))
 
 
+@pytest.mark.parametrize("color", [zwebp.ColorType.Rgba8, zwebp.ColorType.La8, zwebp.ColorType.Rgb8,
+                                   zwebp.ColorType.L8])
+def test_encode_webp_batch(ctx, color):
+    """zw_encode_webp_batch / the pipe's container mode: per frame the same
+    container as WebPEncoder::encode (VP8X + ALPH for alpha inputs, built from
+    the oracle's VP8 and ALPH payloads; simple RIFF otherwise)."""
+    w, h = 240, 144
+    imgs = []
+    for i in range(5):
+        im = _alpha_img(w, h, zwebp.ColorType.Rgba8) if i % 2 else synth_rgba(w, h, 0x5EED3000 + i, "noise")
+        im = np.ascontiguousarray(im)
+        if color == zwebp.ColorType.La8:
+            im = np.ascontiguousarray(im[..., [0, 3]])
+        elif color == zwebp.ColorType.Rgb8:
+            im = np.ascontiguousarray(im[..., :3])
+        elif color == zwebp.ColorType.L8:
+            im = np.ascontiguousarray(im[..., 0])
+        imgs.append(im)
+    outs = zwebp.encode_webp_batch(imgs, w, h, color, 75, 4, ctx=ctx)
+    for i, im in enumerate(imgs):
+        rc, vp8, _ = O.encode(im, w, h, color, 75, 4)
+        assert rc == 0
+        if color in (zwebp.ColorType.Rgba8, zwebp.ColorType.La8):
+            rc, alph = O.encode_alpha(im, w, h, color)
+            assert rc == 0
+            want = _riff(_vp8x(w, h, 0x10), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8))
+        else:
+            want = _riff(_chunk(b"VP8 ", vp8))
+        assert outs[i] == want, f"frame {i}"
+
+
 # --------------------------------------------------------------------------
 # row-parallel decode: a wave that gives up waiting fails the call
 # --------------------------------------------------------------------------
