@@ -329,13 +329,25 @@ static void pipe_free(zw_pipe* p)
     delete p;
 }
 
-// One lane by default: an encode launch of one frame per CU already fills the
-// GPU, and chunking inside the lane overlaps host and device work.  More lanes
-// (two streams each) only help for batches smaller than two launches.
-static int pipe_lanes_for(int n)
+// Lanes: independent halves of the batch, each with its own kernel and copy
+// streams.  Two lanes by default once each gets at least one full launch (one
+// frame per CU): their launches overlap, so the CUs a launch's early frames
+// free start the other lane's work instead of idling until its slowest frame
+// ends (measured, 1024 1080p frames: 3 015 -> 3 087 encodes/s; three lanes no
+// better).  ZW_PIPE_LANES overrides.
+static int pipe_lanes_for(int n, int device)
 {
     const char* e = getenv("ZW_PIPE_LANES");
-    int g = e ? atoi(e) : 1;
+    int g;
+    if (e && *e) {
+        g = atoi(e);
+    } else {
+        hipDeviceProp_t prop;
+        const int cus = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
+                            ? prop.multiProcessorCount
+                            : 256;
+        g = n >= 2 * cus ? 2 : 1;
+    }
     if (g < 1) g = 1;
     if (g > 16) g = 16;
     while (g > 1 && n / g < 8) g--;  // keep >= 8 frames per lane
@@ -422,7 +434,7 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
     p->host_stats = getenv("ZW_HOST_STATS") != nullptr;
     ok = ok && (p->host_stats || (hipMalloc(&p->d_stats, N * sizeof(ZwStatsOut)) == hipSuccess &&
                                   hipMalloc(&p->d_stats_tmp, zw_stats_scratch_bytes(p->nmb, n)) == hipSuccess));
-    const int G = pipe_lanes_for(n);
+    const int G = pipe_lanes_for(n, ctx->device);
     p->lanes.resize(G);
     for (int g = 0; ok && g < G; g++) {
         PipeLane& L = p->lanes[g];

@@ -258,7 +258,7 @@ int zw_pipe_enable_debug(zw_pipe *p);
 int zw_pipe_read_debug(zw_pipe *p, int frame, int32_t *out);
 /* Token probabilities (4*8*3*11) and skip probability used by pass 2. */
 int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
-/* The pipe splits its frames into lanes (env ZW_PIPE_LANES, default 1), each with
+/* The pipe splits its frames into lanes (env ZW_PIPE_LANES; default 2 from two launches of frames up, else 1), each with
  * a kernel stream and a copy stream, and each lane into chunks (env
  * ZW_PIPE_CHUNK, default one frame per CU per launch): the host entropy work on
  * one chunk overlaps the kernels of the next.  Chunks of at most 12 MB rows per CU
