@@ -451,6 +451,9 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
         if (ok && pipe_rows_for(L.chunk, p->mbh, ctx->device)) {
             const size_t rb = zwk_encode_rows_bytes(p->mbw, p->mbh, L.chunk);
             ok = hipMalloc(&L.d_rows, rb) == hipSuccess && hipMemset(L.d_rows, 0, rb) == hipSuccess;
+            // test hook (ZW_ENC_FORCE_ERROR=1): pre-set the launch error word, as a
+            // wave that gave up waiting would, so the host-side check is exercised
+            if (ok && getenv("ZW_ENC_FORCE_ERROR")) ok = hipMemset(L.d_rows, 1, 1) == hipSuccess;
         }
         for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
         for (size_t i = 0; ok && i < L.cev.size(); i++)

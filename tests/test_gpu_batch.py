@@ -174,6 +174,22 @@ def test_encode_webp_batch(ctx, color):
         assert outs[i] == want, f"frame {i}"
 
 
+def test_rows_encode_error_reported(ctx, monkeypatch):
+    """Row-parallel encode: a set launch error word (a wave that gave up
+    waiting) fails the encode with ZW_EDEVICE instead of returning streams."""
+    w, h = 160, 96
+    img = synth_rgba(w, h, 0x5EED0077)
+    monkeypatch.setenv("ZW_ENC_ROWS", "1")
+    monkeypatch.setenv("ZW_ENC_FORCE_ERROR", "1")
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_batch([img, img], w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    assert e.value.code == 4  # ZW_EDEVICE
+    monkeypatch.delenv("ZW_ENC_FORCE_ERROR")
+    out = zwebp.encode_batch([img, img], w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
+    assert out[0] == ref and out[1] == ref
+
+
 # --------------------------------------------------------------------------
 # row-parallel decode: a wave that gives up waiting fails the call
 # --------------------------------------------------------------------------
