@@ -1818,6 +1818,332 @@ __device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
     for (int k = C.lane; k < nblk * 16; k += 64) dst[first_blk * 16 + k] = zero ? (int16_t)0 : srcl[first_blk * 16 + k];
 }
 
+// ---------------------------------------------------------------------------
+// Pass-1 chroma chain in quad form, one wave per plane (chain wave 0: U,
+// chain wave 1: V).  Lane l = 16 m + 4 b + q works mode m (0 DC, 1 V, 2 H,
+// 3 TM) of 4x4 block b (bx = b & 1, by = b >> 1): pixel row q for the
+// prediction, residual, row transform input and reconstruction; coefficient
+// column q for the column transform, quantisation and rate.  A quad gathers
+// its rows' row-transform inputs with DPP broadcasts and each lane forms its
+// own column, so a lane does a quarter block and the plane's 4 modes x 4
+// blocks fill one wave.  The arithmetic (packing points, rounding) is the pair
+// form's (fdct_pair / idct_recon_pair), so the results are identical.  Only the
+// mode decision couples the planes -- one RD over U + V (pick_best_uv,
+// vp8.rs:2050-2200) -- and the waves trade their per-mode (rate, SSE, AC
+// nonzeros) through LDS; the DC error diffusion (vp8.rs:572-647) runs per
+// channel, so each wave keeps its own.  Halving the chain's instruction stream
+// shortens pass 1, which the chain bounds for single frames (quirk A5 makes it
+// serial across rows) and nearly bounds in batches.
+// ---------------------------------------------------------------------------
+struct UvQ {
+    int pl;             // 0 U, 1 V
+    uint8_t* w;         // the plane's work buffer (create_border_chroma layout, stride ZW_BPS)
+    const uint8_t* sp;  // the MB's staged source plane (8x8, stride 8)
+    uint8_t* top;       // frame-wide top row of the plane
+    uint8_t* left;      // the wave's left column (corner + 8 rows)
+};
+
+// create_border_chroma (prediction.rs:85) of one plane
+DI void uvq_border(const Ctx& C, const UvQ& U)
+{
+    const int l = C.lane;
+    if (l < 17) {
+        if (l == 0) U.w[0] = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : U.left[0]);
+        else if (l <= 8) U.w[l] = C.mby == 0 ? 127 : U.top[C.mbx * 8 + l - 1];
+        else U.w[(l - 8) * ZW_BPS] = C.mbx == 0 ? 129 : U.left[l - 8];
+    }
+    wsync();
+}
+
+// The quad's row-transform inputs broadcast to every lane: lane q forms
+// column q of the row stage (dct4x4 transform.rs:176) for rows 0..3, then the
+// column stage: c[r] = coefficient (r, q), natural index 4 r + q.
+DI void uvq_fdct(uint32_t A, uint32_t D, int q, int c[4])
+{
+    const bool odd = q & 1;
+    const zs2 k0 = {8, 8}, k2 = {8, -8}, k1 = {10704, 4434}, k3 = {4434, -10704};
+    const uint32_t k = q == 0 ? as_zu(k0) : (q == 1 ? as_zu(k1) : (q == 2 ? as_zu(k2) : as_zu(k3)));
+    const int rnd = q == 1 ? 3625 : (q == 3 ? 1875 : 0);
+    const int sh = odd ? 10 : 0;
+    // (csel, not ?: -- a select of two DPP results may be folded into one DPP
+    // of a select, which would take the source lane's choice)
+    int t[4];
+    t[0] = dot2v((uint32_t)csel(odd, qb0((int)D), qb0((int)A)), k, rnd) >> sh;
+    t[1] = dot2v((uint32_t)csel(odd, qb1((int)D), qb1((int)A)), k, rnd) >> sh;
+    t[2] = dot2v((uint32_t)csel(odd, qb2((int)D), qb2((int)A)), k, rnd) >> sh;
+    t[3] = dot2v((uint32_t)csel(odd, qb3((int)D), qb3((int)A)), k, rnd) >> sh;
+    const uint32_t X01 = pack_lo(t[0], t[1]), X32 = pack_lo(t[3], t[2]);
+    const zs2 XA = as_zs2(X01) + as_zs2(X32), XD = as_zs2(X01) - as_zs2(X32);
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+    c[0] = dot2(XA, k1p, 7) >> 4;
+    c[2] = dot2(XA, k1m, 7) >> 4;
+    c[1] = (dot2(XD, k2a, 12000) >> 16) + ((as_zu(XD) & 0xffffu) != 0u ? 1 : 0);
+    c[3] = dot2(XD, k2b, 51000) >> 16;
+}
+
+// idct4x4 (transform.rs:19) of the quad's dequantised columns (lane q holds
+// column q, rows 0..3), then the reconstruction clamp(pred + residual) of row q
+// as i16 pairs (x0, x1), (x3, x2).
+DI void uvq_idct_recon(const int dq[4], uint32_t p01, uint32_t p32, int q, uint32_t& r01, uint32_t& r32)
+{
+    uint32_t lo, hi;
+    {
+        const int x0 = dq[0], x1 = dq[1], x2 = dq[2], x3 = dq[3];
+        const int a1 = x0 + x2, b1 = x0 - x2;
+        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
+        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
+        lo = pack_lo(a1 + d1, b1 + c1);
+        hi = pack_lo(b1 - c1, a1 - d1);
+    }
+    // row q of every column: the lane of column j holds it in lo (rows 0, 1) or hi (rows 2, 3)
+    const bool upper = q >= 2;
+    const uint32_t off = 16u * (uint32_t)(q & 1);
+    const int y0 = __builtin_amdgcn_sbfe(csel(upper, qb0((int)hi), qb0((int)lo)), off, 16);
+    const int y1 = __builtin_amdgcn_sbfe(csel(upper, qb1((int)hi), qb1((int)lo)), off, 16);
+    const int y2 = __builtin_amdgcn_sbfe(csel(upper, qb2((int)hi), qb2((int)lo)), off, 16);
+    const int y3 = __builtin_amdgcn_sbfe(csel(upper, qb3((int)hi), qb3((int)lo)), off, 16);
+    const int a1 = y0 + y2, b1 = y0 - y2;
+    const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
+    const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
+    const int o0 = (a1 + d1 + 4) >> 3, o1 = (b1 + c1 + 4) >> 3, o2 = (b1 - c1 + 4) >> 3, o3 = (a1 - d1 + 4) >> 3;
+    r01 = clamp_pk(add_pk(pack_lo(o0, o1), p01));
+    r32 = clamp_pk(add_pk(pack_lo(o3, o2), p32));
+}
+
+DI int quad_or(int v)
+{
+    v |= DPP(v, 0xB1);
+    return v | DPP(v, 0x4E);
+}
+DI int quad_sum(int v)
+{
+    v += DPP(v, 0xB1);
+    return v + DPP(v, 0x4E);
+}
+
+// get_residual_cost (cost.rs:1670; ctype 2, first 0, ctx0 0; pass 1: the
+// LevelCosts tables are zero, quirk A2) of the quad's block, av[r] = |level|
+// at natural index 4 r + q.  Uniform in the quad.
+DI int uvq_rcost(const int av[4], int q, const LdsTables* T)
+{
+    unsigned nz = 0, big = 0;
+    int part = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int n = 4 * r + q;
+        nz |= (unsigned)min(av[r], 1) << n;
+        big |= (unsigned)(av[r] >= 2) << n;
+        part += T->lfc[min(av[r], 2047)];
+    }
+    nz = (unsigned)quad_or((int)nz);
+    big = (unsigned)quad_or((int)big);
+    const int sum = quad_sum(part);
+    const int last = 31 - __clz((int)nz);
+    const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
+    const int tail = (int)T->beob[2][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
+    const int head = (int)T->binit[2][0][0];
+    return last < 0 ? (int)T->beob[2][0][0] : head + sum + tail;
+}
+
+// pick_best_uv (vp8.rs:2050-2200) with the partner plane's wave: returns the
+// chroma mode.  Leaves each lane's coefficients and prediction row in
+// W->uvc[lane] for uvq_final.  xch: [plane][2][12] exchange words, xflag[2].
+DI int uvq_pick(const Ctx& C, const UvQ& U, int* xch, int* xflag, int seq)
+{
+    const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
+    WaveLds* W = C.W;
+    const int l = C.lane, m = l >> 4, b = (l >> 2) & 3, q = l & 3, bx = b & 1, by = b >> 1;
+    const int above = C.mby != 0, left = C.mbx != 0;
+    // DC predictor (lanes 0..15: i < 8 left pixel i, i >= 8 top pixel i - 8)
+    int dc;
+    {
+        const int i = l & 15;
+        const int v = (int)U.w[csel(i < 8, (i + 1) * ZW_BPS, i - 7)] & -(int)(i < 8 ? left : above);
+        const int su = __builtin_amdgcn_readlane(red16(v), 0);
+        const int shf = 2 + left + above;
+        dc = (above | left) ? (su + (1 << (shf - 1))) >> shf : 128;
+    }
+    // prediction and source of row y = 4 by + q (uv_rows_pk)
+    uint32_t p01, p32, s01, s32;
+    {
+        const int cm = -(int)(m & 1), rm = -(int)(m >= 2);
+        const int P = U.w[0];
+        const int ro = csel(m == 0, dc, csel(m == 3, -P, 0));
+        const uint8_t* tp = U.w + 1 + bx * 4;
+        const uint32_t c01 = pack_lo(tp[0] & cm, tp[1] & cm), c32 = pack_lo(tp[3] & cm, tp[2] & cm);
+        const int y = by * 4 + q;
+        const int rv = (U.w[(y + 1) * ZW_BPS] & rm) + ro;
+        const uint32_t rvv = pack_lo(rv, rv);
+        p01 = clamp_pk(add_pk(c01, rvv));
+        p32 = clamp_pk(add_pk(c32, rvv));
+        const uint32_t sw = *(const uint32_t*)(U.sp + y * 8 + bx * 4);
+        s01 = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
+        s32 = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
+    }
+    const uint32_t R01 = sub_pk(s01, p01), R32 = sub_pk(s32, p32);
+    int cf[4];
+    uvq_fdct(add_pk(R01, R32), sub_pk(R01, R32), q, cf);
+    {
+        uint32_t* e = W->uvc[l];
+        e[0] = pack_lo(cf[0], cf[1]);
+        e[1] = pack_lo(cf[2], cf[3]);
+        e[2] = p01;
+        e[3] = p32;
+    }
+    // quantize_coeff (no sharpening, cost.rs:457): the DC is (r, q) = (0, 0)
+    int av[4], dq[4], nzac = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool dcs = r == 0 && q == 0;
+        const uint32_t iq = dcs ? S.uv.iq[0] : S.uv.iq[1];
+        const uint32_t bias = dcs ? S.uv.bias[0] : S.uv.bias[1];
+        const int q_ = dcs ? (int)S.uv.q[0] : (int)S.uv.q[1];
+        const int v = cf[r];
+        const int a = (int)((__umul24((uint32_t)iabs(v), iq) + bias) >> 17);
+        av[r] = a;
+        dq[r] = m24(v < 0 ? -a : a, q_);
+        nzac += dcs ? 0 : min(a, 1);
+    }
+    const int cost = uvq_rcost(av, q, T);
+    uint32_t r01, r32;
+    uvq_idct_recon(dq, p01, p32, q, r01, r32);
+    int sse = 0;
+    {
+        const uint32_t d01 = sub_pk(s01, r01), d32 = sub_pk(s32, r32);
+        sse = dot2v(d01, d01, sse);
+        sse = dot2v(d32, d32, sse);
+    }
+    // per-mode plane totals (a block's rate once, from its quad's lane 0)
+    const int ct = red16(q == 0 ? cost : 0), st = red16(sse), nt = red16(nzac);
+    int* mine = xch + (U.pl * 2 + (seq & 1)) * 12;
+    const int* theirs = xch + ((1 - U.pl) * 2 + (seq & 1)) * 12;
+    if ((l & 15) == 0) {
+        mine[m * 3 + 0] = ct;
+        mine[m * 3 + 1] = st;
+        mine[m * 3 + 2] = nt;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (l == 0) __hip_atomic_store(&xflag[U.pl], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_wave_barrier();
+    while (__hip_atomic_load(&xflag[1 - U.pl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq)
+        __builtin_amdgcn_s_sleep(1);
+    // the same decision in both waves: rd = (fixed + rate + pen) * lambda_uv + 256 * sse
+    long long brd = 0x7fffffffffffffffLL;
+    int bm = 0;
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++) {
+        const int c_o = __builtin_amdgcn_readfirstlane(theirs[mm * 3 + 0]);
+        const int s_o = __builtin_amdgcn_readfirstlane(theirs[mm * 3 + 1]);
+        const int n_o = __builtin_amdgcn_readfirstlane(theirs[mm * 3 + 2]);
+        const int c_m = __builtin_amdgcn_readlane(ct, mm * 16), s_m = __builtin_amdgcn_readlane(st, mm * 16);
+        const int n_m = __builtin_amdgcn_readlane(nt, mm * 16);
+        const int fixed = sel4(mm, d_FIXED_COSTS_UV[0], d_FIXED_COSTS_UV[1], d_FIXED_COSTS_UV[2], d_FIXED_COSTS_UV[3]);
+        const int pen = (mm > 0 && n_m + n_o <= 2) ? 140 * 8 : 0;
+        const long long r_m = (long long)(fixed + c_m + c_o + pen) * (long long)S.l_uv + 256LL * (long long)(s_m + s_o);
+        const int avail = mm == 0 || (mm == 1 && above) || (mm == 2 && left) || (mm == 3 && above && left);
+        if (avail && r_m < brd) {
+            brd = r_m;
+            bm = mm;
+        }
+    }
+    return bm;
+}
+
+// transform_chroma_blocks (vp8.rs:3039-3121) of one plane under mode cm:
+// the DC error diffusion of channel U.pl (vp8.rs:572-647), quantisation,
+// levels into W->lev[17 + 4 pl + b], reconstruction into the work buffer.
+DI void uvq_final(const Ctx& C, const UvQ& U, int cm, int8_t* top_derr)
+{
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const int l = C.lane, b = (l >> 2) & 3, q = l & 3, bx = b & 1, by = b >> 1;
+    const bool act = l < 16;
+    int cf[4];
+    uint32_t p01, p32;
+    {
+        const uint32_t* e = W->uvc[cm * 16 + (l & 15)];
+        cf[0] = lo16(e[0]);
+        cf[1] = hi16(e[0]);
+        cf[2] = lo16(e[1]);
+        cf[3] = hi16(e[1]);
+        p01 = e[2];
+        p32 = e[3];
+    }
+    {
+        const int qd = (int)S.uv.q[0];
+        const uint32_t iq = S.uv.iq[0], bias = S.uv.bias[0];
+        const uint32_t zt = S.uv.zthresh[0];  // ((1 << 17) - 1 - bias) / iq, matrix_init
+        int d[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = __builtin_amdgcn_readlane(cf[0], 4 * k);
+        auto diffuse = [&](int& dc, int te, int le) -> int {
+            dc += (7 * te + 8 * le) >> 3;
+            const int sign = dc < 0;
+            const uint32_t a = (uint32_t)(sign ? -dc : dc);
+            const int level = a > zt ? (int)((a * iq + bias) >> 17) : 0;
+            const int err = (int)a - level * qd;
+            const int se = sign ? -err : err;
+            const int v = se >> 1;
+            return (int)(int8_t)(v < -127 ? -127 : (v > 127 ? 127 : v));
+        };
+        int8_t* top = top_derr + U.pl * 2;
+        int8_t* lft = W->left_derr;
+        const int t0 = __builtin_amdgcn_readfirstlane((int)top[0]), t1 = __builtin_amdgcn_readfirstlane((int)top[1]);
+        const int l0 = __builtin_amdgcn_readfirstlane((int)lft[0]), l1 = __builtin_amdgcn_readfirstlane((int)lft[1]);
+        const int e0 = diffuse(d[0], t0, l0);
+        const int e1 = diffuse(d[1], t1, e0);
+        const int e2 = diffuse(d[2], e0, l1);
+        const int e3 = diffuse(d[3], e1, e2);
+        const int nl1 = (int)(int8_t)((3 * e3) >> 2);
+        wsync();
+        if (l == 0) {
+            lft[0] = (int8_t)e1;
+            lft[1] = (int8_t)nl1;
+            top[0] = (int8_t)e2;
+            top[1] = (int8_t)(e3 - nl1);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            asm volatile("v_writelane_b32 %0, %1, %2"
+                         : "+v"(cf[0])
+                         : "s"(__builtin_amdgcn_readfirstlane(d[k])), "i"(4 * k));
+    }
+    int dq[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool dcs = r == 0 && q == 0;
+        const int lv = quantz(cf[r], dcs ? S.uv.iq[0] : S.uv.iq[1], dcs ? S.uv.bias[0] : S.uv.bias[1]);
+        if (act) W->lev[17 + 4 * U.pl + b][izz_of(4 * r + q)] = (int16_t)lv;
+        dq[r] = m24(lv, dcs ? (int)S.uv.q[0] : (int)S.uv.q[1]);
+    }
+    uint32_t r01, r32;
+    uvq_idct_recon(dq, p01, p32, q, r01, r32);
+    if (act) {
+        uint8_t* row = U.w + (by * 4 + q + 1) * ZW_BPS + 1 + bx * 4;
+        row[0] = (uint8_t)(r01 & 255u);
+        row[1] = (uint8_t)(r01 >> 16);
+        row[2] = (uint8_t)(r32 >> 16);
+        row[3] = (uint8_t)(r32 & 255u);
+    }
+    wsync();
+}
+
+// Borders of one plane for the next MBs (vp8.rs:3101-3118), and its debug
+// reconstruction when asked for.
+DI void uvq_store_borders(const Ctx& C, const UvQ& U)
+{
+    const int l = C.lane;
+    if (l < 9) U.left[l] = U.w[l * ZW_BPS + 8];
+    else if (l < 17) U.top[C.mbx * 8 + (l - 9)] = U.w[8 * ZW_BPS + (l - 9) + 1];
+    uint8_t* rp = U.pl ? C.a->rv : C.a->ru;
+    if (rp) {
+        rp += (size_t)C.f * C.a->csz + (size_t)C.mby * 8 * C.cs + C.mbx * 8;
+        rp[(size_t)(l >> 3) * C.cs + (l & 7)] = U.w[((l >> 3) + 1) * ZW_BPS + 1 + (l & 7)];
+    }
+    wsync();
+}
+
 // What an MB needs from global memory, fetched one MB ahead (the loads are in
 // flight while the previous MB is encoded): the lane's word of the source MB
 // (luma: row lane>>2, word lane&3; chroma lanes < 32: plane lane>>4, row
@@ -1963,10 +2289,30 @@ DI void row_publish(int* prog, int val)
     __builtin_amdgcn_wave_barrier();
 }
 
+// Pass 1's chroma chain: one wave (pair form) or two (quad form, one wave per
+// plane).  The row-parallel kernels take the two-wave chain: it bounds their
+// pass 1 (one 1080p frame: 27.7 -> 22.1 ms), and their pass-1 workgroups then
+// run two waves (the chain's two planes; two luma rows elsewhere).  The batch
+// kernels keep one chain wave: there a second one costs a luma wave and
+// measured slower (34.4 -> 35.0 ms per 256 1080p frames).
+#ifndef ZW_UVQ_CHAIN_ROWS
+#define ZW_UVQ_CHAIN_ROWS 1
+#endif
+#ifndef ZW_UVQ_CHAIN_BATCH
+#define ZW_UVQ_CHAIN_BATCH 0
+#endif
+template <bool ROWS> struct ChainShape {
+    static constexpr int NCH = (ROWS ? ZW_UVQ_CHAIN_ROWS : ZW_UVQ_CHAIN_BATCH) ? 2 : 1;
+};
+template <int PASS> struct RowsShape {
+    static constexpr int NW = PASS == 1 ? ChainShape<true>::NCH : 1;
+};
+
 template <int PASS, bool ROWS>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
 {
-    constexpr int NW = ROWS ? 1 : PassShape<PASS>::NW, WG = ROWS ? 64 : PassShape<PASS>::WG;
+    constexpr int NW = ROWS ? RowsShape<PASS>::NW : PassShape<PASS>::NW, WG = NW * 64;
+    constexpr int NCH = PASS == 1 ? ChainShape<ROWS>::NCH : 0;  // chain waves (pass 1)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = ROWS ? blockIdx.y : blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1984,6 +2330,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
     int* progress = (int*)(smem + off);
     off += 64;
+    int* xch = (int*)(smem + off);  // two-wave chroma chain: [plane][2][12] exchange words, then 2 flags
+    int* xflag = xch + 48;
+    off += 256;
     uint8_t* top_y = smem + off;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
     uint8_t* top_u = smem + off;
@@ -1996,7 +2345,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
     // row-parallel: is this workgroup pass 1's chroma chain (it keeps the
     // frame-wide top_u/v/derr in LDS), and the frame's global row state
-    const bool chain_wg = PASS == 1 && (ROWS ? blockIdx.x == 0 : wv == 0);
+    const bool chain_wg = PASS == 1 && (ROWS ? blockIdx.x == 0 : wv < NCH);
     const RowsLayout RL(mbw, mbh);
     uint8_t* rb = ROWS ? a.rows + ZW_ROWS_HDR + (size_t)f * RL.frame : nullptr;
     int* rerr = ROWS ? (int*)a.rows : nullptr;
@@ -2025,6 +2374,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     }
     if (threadIdx.x < NW) progress[threadIdx.x] = -1;
+    if (threadIdx.x < 2) xflag[threadIdx.x] = 0;
     if (ROWS && lane < 12) W->win_c[lane] = 0;  // pass 1: the complexity contexts stay zero
     __syncthreads();
 
@@ -2069,6 +2419,65 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #endif
         __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
         if (lane < 4) W->left_derr[lane] = 0;
+        if (NCH == 2) {
+            // quad form: wave 0 the U plane, wave 1 the V plane
+            const int pl = wv;
+            UvQ U;
+            U.pl = pl;
+            U.w = W->cu;
+            U.sp = W->su;
+            U.top = pl ? top_v : top_u;
+            U.left = W->left_u;
+            const uint8_t* const P0 = (pl ? a.V : a.U) + (size_t)f * a.csz;
+            const int cs = mbw * 8;
+            auto fetch_uv = [&](int mbx, int mby) {
+                MbFetch r;
+                r.y = lane < 16 ? *(const uint32_t*)(P0 + (size_t)(mby * 8 + (lane >> 1)) * cs + mbx * 8 + (lane & 1) * 4)
+                                : 0u;
+                r.c = 0;
+                r.alpha = a.alpha[(size_t)f * nmb + (size_t)mby * mbw + mbx];
+                return r;
+            };
+            C.ys = mbw * 16;
+            C.cs = cs;
+            MbFetch nx = fetch_uv(0, 0);
+            int seq = 0;
+            for (int mby = 0; mby < mbh; mby++) {
+                if (lane < 12) W->left_u[lane] = 129;
+                wsync();
+                for (int mbx = 0; mbx < mbw; mbx++) {
+                    PH_START();
+                    const int lane = opaque_lane(threadIdx.x & 63);
+                    C.lane = lane;
+                    const MbFetch cur = nx;
+                    if (mbx + 1 < mbw) nx = fetch_uv(mbx + 1, mby);
+                    else if (mby + 1 < mbh) nx = fetch_uv(0, mby + 1);
+                    C.mbx = mbx;
+                    C.mby = mby;
+                    if (lane < 16) ((uint32_t*)W->su)[lane] = cur.y;
+                    wsync();
+                    const int seg = __builtin_amdgcn_readfirstlane((int)seg_lut[cur.alpha]);
+                    C.seg = seg;
+                    C.S = C.Sl + seg;
+                    uvq_border(C, U);
+                    const int cm = uvq_pick(C, U, xch, xflag, ++seq);
+                    PH_MARK(8);
+                    uvq_final(C, U, cm, top_derr + mbx * 4);
+                    PH_MARK(9);
+                    uvq_store_borders(C, U);
+                    ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
+                    if (pl == 0 && lane == 0) o->chroma_mode = (uint8_t)cm;
+                    write_levels(C, 17 + 4 * pl, 4, false);
+                    wsync();
+                }
+            }
+            for (int i = lane; i < mbw * 2; i += 64) {
+                const int j = (i >> 1) * 4 + pl * 2 + (i & 1);
+                a.derr[(size_t)f * mbw * 4 + j] = top_derr[j];
+            }
+            ph_flush();
+            return;
+        }
         MbFetch nx = fetch_mb(&a, f, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
@@ -2110,7 +2519,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_LUMA_PRIO 0
 #endif
     if (PASS == 1) __builtin_amdgcn_s_setprio(ZW_LUMA_PRIO);
-    const int nrw = PASS == 1 ? NW - 1 : NW;  // waves on the luma wavefront
+    const int nrw = PASS == 1 ? NW - NCH : NW;  // waves on the luma wavefront
     // Row k of each round of nrw rows goes to wave luma_wave(k).  In pass 1 the
     // luma waves that share SIMD 0 with the chroma chain (issue priority 3)
     // run slowest, and every later row of a round waits on a slow row: they
@@ -2120,19 +2529,19 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_P1_ORDER 1
 #endif
     auto p1_before = [](int v, int w) {  // wave v takes its row of a round before wave w
-        const bool sv = (v & 3) == 0, sw = (w & 3) == 0;
+        const bool sv = (v & 3) < NCH, sw = (w & 3) < NCH;
         return (ZW_P1_ORDER && sv != sw) ? sw : v < w;
     };
     auto luma_rank = [&](int w) {
         if (PASS == 2) return w;
         int r = 0;
-        for (int v = 1; v < NW; v++) r += (int)p1_before(v, w);
+        for (int v = NCH; v < NW; v++) r += (int)p1_before(v, w);
         return r;
     };
     auto luma_wave = [&](int k) {
         if (PASS == 2) return k;
-        int w = 1;
-        for (int v = 1; v < NW; v++)
+        int w = NCH;
+        for (int v = NCH; v < NW; v++)
             if (luma_rank(v) == k) w = v;
         return w;
     };
@@ -2338,7 +2747,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 
 extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1, false>(a); }
 extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2, false>(a); }
-extern "C" __global__ __launch_bounds__(64) void k_encode_rows_pass1(EncArgs a) { encode_body<1, true>(a); }
+extern "C" __global__ __launch_bounds__(64 * RowsShape<1>::NW) void k_encode_rows_pass1(EncArgs a) { encode_body<1, true>(a); }
 extern "C" __global__ __launch_bounds__(64) void k_encode_rows_pass2(EncArgs a) { encode_body<2, true>(a); }
 
 // ---------------------------------------------------------------------------
@@ -2451,6 +2860,7 @@ static size_t encode_lds_bytes(int mbw, int nw)
     off += 256;
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * nw;
     off += 64;
+    off += 256;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
     off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
     off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
@@ -2529,9 +2939,13 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
     (void)attr_set;
     if (rows) {
         // one wave per MB row (+ pass 1's chroma chain in workgroup 0)
-        const size_t lds = encode_lds_bytes(mbw, 1);
-        if (pass == 1) hipLaunchKernelGGL(k_encode_rows_pass1, dim3(mbh + 1, nframes), dim3(64), lds, s, a);
-        else hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), lds, s, a);
+        if (pass == 1) {
+            constexpr int nw = RowsShape<1>::NW;
+            hipLaunchKernelGGL(k_encode_rows_pass1, dim3(1 + (mbh + nw - 1) / nw, nframes), dim3(64 * nw),
+                               encode_lds_bytes(mbw, nw), s, a);
+        } else {
+            hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), encode_lds_bytes(mbw, 1), s, a);
+        }
         return hipGetLastError();
     }
     const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW);
