@@ -483,6 +483,12 @@ struct DecBatch {
     int mbw = 0, mbh = 0;
     const int* d_rs = nullptr;  // row-parallel kernels' per-frame sync words (null: workgroup-per-frame kernels)
     int n = 0;
+    // host parse results waiting for dec_launch
+    std::vector<DecQuant> quant;
+    std::vector<ZwFilterParams> fps;
+    uint8_t* stage = nullptr;  // pinned upload staging (records, MB offsets, frame bases)
+    size_t up_bytes = 0, o_moff = 0, o_base = 0, rec_bytes = 0;
+    double parse_ms = 0;
 };
 
 // Test hook (ZW_DEC_FORCE_ERROR=1): pre-set frame 0's row-sync error word, as a
@@ -522,8 +528,9 @@ static bool dec_timing() { static const bool on = getenv("ZW_DEC_TIMING") != nul
 
 // bi: which of the context's two staging / scratch / event sets (the
 // pipelined batches alternate between them).
-static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
-                            size_t extra_bytes, DecBatch& B, int bi = 0)
+// Host half: headers, modes and tokens of n frames into packed MB records in
+// the pinned upload staging of set bi (no device work).
+static int dec_parse(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, DecBatch& B, int bi)
 {
     const double t0 = dec_now_ms();
     B.F.assign(n, DecFrame());
@@ -546,16 +553,22 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     // frame bases; one upload carries all of it.
     const size_t slot = nmb * ZW_DREC_MAX;
     std::vector<uint32_t> moffv((size_t)n * (nmb + 1));
-    std::vector<std::unique_ptr<uint8_t[]>> recs(n);
-    std::vector<DecQuant> quant((size_t)n * 4);
-    std::vector<ZwFilterParams> fps(n);
+    std::vector<zw_ctx::RecBuf>& recs = ctx->dec_recs[bi];
+    if (recs.size() < (size_t)n) recs.resize(n);
+    std::vector<DecQuant>& quant = B.quant;
+    std::vector<ZwFilterParams>& fps = B.fps;
+    quant.assign((size_t)n * 4, DecQuant());
+    fps.assign(n, ZwFilterParams());
     parallel_for(n, [&](int i) {
-        recs[i].reset(new (std::nothrow) uint8_t[slot]);
-        if (!recs[i]) {
-            rc[i] = ZW_ENOMEM;
-            return;
+        if (recs[i].cap < slot) {
+            recs[i].p.reset(new (std::nothrow) uint8_t[slot]);
+            recs[i].cap = recs[i].p ? slot : 0;
+            if (!recs[i].p) {
+                rc[i] = ZW_ENOMEM;
+                return;
+            }
         }
-        rc[i] = parse_mbs(F[i], recs[i].get(), moffv.data() + (size_t)i * (nmb + 1));
+        rc[i] = parse_mbs(F[i], recs[i].p.get(), moffv.data() + (size_t)i * (nmb + 1));
         for (int s = 0; s < 4; s++) quant[(size_t)i * 4 + s] = F[i].q[s];
         filter_table(fps[i], F[i].filter_type, F[i].filter_level, F[i].sharpness, F[i].segments_enabled,
                      F[i].seg_delta_values, F[i].seg_lf, F[i].lf_adj_enabled, F[i].ref_delta0, F[i].mode_delta0, mbw,
@@ -577,13 +590,35 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     uint8_t* stage = (uint8_t*)ctx_pinned(ctx, bi ? 2 : 0, up_bytes);
     if (!stage) return ZW_ENOMEM;
     parallel_for(n, [&](int i) {
-        memcpy(stage + fb[i], recs[i].get(), moffv[(size_t)i * (nmb + 1) + nmb]);
-        recs[i].reset();
+        memcpy(stage + fb[i], recs[i].p.get(), moffv[(size_t)i * (nmb + 1) + nmb]);
     });
     memcpy(stage + o_moff, moffv.data(), off_bytes);
     memcpy(stage + o_base, fb.data(), base_bytes);
-    const double t1 = dec_now_ms();
+    B.stage = stage;
+    B.up_bytes = up_bytes;
+    B.o_moff = o_moff;
+    B.o_base = o_base;
+    B.rec_bytes = rec_bytes;
+    B.mbw = mbw;
+    B.mbh = mbh;
+    B.ysz = ysz;
+    B.csz = csz;
+    B.n = n;
+    B.parse_ms = dec_now_ms() - t0;
+    return ZW_OK;
+}
 
+// Device half: upload set bi's records, expand, reconstruct, filter (leaving
+// `extra_bytes` of scratch at B.o_extra for the caller).
+static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
+{
+    const double t1 = dec_now_ms();
+    const int n = B.n, mbw = B.mbw, mbh = B.mbh;
+    const size_t nmb = (size_t)mbw * mbh, ysz = B.ysz, csz = B.csz;
+    const size_t up_bytes = B.up_bytes, o_moff = B.o_moff, o_base = B.o_base;
+    const std::vector<DecQuant>& quant = B.quant;
+    const std::vector<ZwFilterParams>& fps = B.fps;
+    uint8_t* stage = B.stage;
     HIPOK(hipSetDevice(ctx->device));
     const size_t o_mbs = 0, o_q = al256(o_mbs + up_bytes);
     const size_t o_fp = al256(o_q + quant.size() * sizeof(DecQuant));
@@ -636,26 +671,19 @@ static int decode_to_device(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     HIPOK(hipEventRecord(ev[2], s));
     if (dec_timing()) {
         HIPOK(hipEventSynchronize(ev[2]));
-        fprintf(stderr, "[dec] n=%d parse %.2f ms, upload+kernels %.2f ms (records %.1f MB)\n", n, t1 - t0,
-                dec_now_ms() - t1, rec_bytes / 1e6);
+        fprintf(stderr, "[dec] n=%d parse %.2f ms, upload+kernels %.2f ms (records %.1f MB)\n", n, B.parse_ms,
+                dec_now_ms() - t1, B.rec_bytes / 1e6);
     }
     B.d = d;
     B.o_y = o_y;
     B.o_u = o_u;
     B.o_v = o_v;
     B.o_extra = o_extra;
-    B.ysz = ysz;
-    B.csz = csz;
-    B.mbw = mbw;
-    B.mbh = mbh;
     B.d_rs = rows ? (const int*)(d + o_rs) : nullptr;
-    B.n = n;
     return ZW_OK;
 }
 
-// Frames per pipelined chunk: chunk c+1 is parsed on the host while chunk c
-// runs on the device, and chunk c is downloaded and fanned out while chunk c+1
-// runs.  ZW_DEC_CHUNK overrides.
+// Frames per pipelined chunk.  ZW_DEC_CHUNK overrides.
 static int dec_chunk_frames()
 {
     const char* e = getenv("ZW_DEC_CHUNK");
@@ -663,10 +691,13 @@ static int dec_chunk_frames()
     return c > 0 ? c : 128;
 }
 
-// Runs the batch through decode_to_device in chunks, alternating the two buffer
-// sets.  enqueue(B, first, count) queues caller work after the filter (or does
-// nothing); finish(B, first, count) waits for it, downloads and fans out.  Device
-// times of all chunks add up in ctx->dec_ms.
+// Runs the batch in chunks, alternating the two buffer sets.  Per step c the
+// host parses chunk c while a second thread finishes chunk c-1 (waits for its
+// kernels, downloads and fans out -- mostly a DMA wait), then chunk c is
+// uploaded and launched; the device runs chunk c-1 during both.  enqueue(B,
+// first, count) queues caller work after the filter (or does nothing);
+// finish(B, first, count) waits for it, downloads and fans out.  Device times
+// of all chunks add up in ctx->dec_ms.
 template <class ENQ, class FIN>
 static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, size_t extra_per_frame,
                         ENQ&& enqueue, FIN&& finish)
@@ -678,18 +709,25 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     auto count = [&](int c) { return std::min(C, n - c * C); };
     int err = ZW_OK;
     for (int c = 0; c <= nch && !err; c++) {
-        if (c < nch) {
-            DecBatch& b = B[c & 1];
-            err = decode_to_device(ctx, count(c), data + first(c), lens + first(c), extra_per_frame * count(c), b,
-                                   c & 1);
-            if (!err) err = enqueue(b, first(c), count(c));
+        int err_f = ZW_OK, err_p = ZW_OK;
+        std::thread fin;
+        if (c >= 1) {
+            fin = std::thread([&, c]() {
+                (void)hipSetDevice(ctx->device);
+                DecBatch& b = B[(c - 1) & 1];
+                err_f = finish(b, first(c - 1), count(c - 1));
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, b.ev[0], b.ev[1]) == hipSuccess) ctx->dec_ms[0] += ms;
+                if (hipEventElapsedTime(&ms, b.ev[1], b.ev[2]) == hipSuccess) ctx->dec_ms[1] += ms;
+            });
         }
-        if (c >= 1 && !err) {
-            DecBatch& b = B[(c - 1) & 1];
-            err = finish(b, first(c - 1), count(c - 1));
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, b.ev[0], b.ev[1]) == hipSuccess) ctx->dec_ms[0] += ms;
-            if (hipEventElapsedTime(&ms, b.ev[1], b.ev[2]) == hipSuccess) ctx->dec_ms[1] += ms;
+        if (c < nch) err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+        if (fin.joinable()) fin.join();
+        err = err_f ? err_f : err_p;
+        if (c < nch && !err) {
+            DecBatch& b = B[c & 1];
+            err = dec_launch(ctx, extra_per_frame * count(c), b, c & 1);
+            if (!err) err = enqueue(b, first(c), count(c));
         }
     }
     if (err) (void)hipStreamSynchronize(ctx_stream(ctx));  // nothing queued may outlive the call

@@ -176,6 +176,7 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (c->stream_) (void)hipStreamSynchronize(c->stream_);  // nothing queued may still use them
     zw_pipe_destroy(c->pipe1);
     c->pipe1 = nullptr;
+    for (auto& v : c->dec_recs) std::vector<zw_ctx::RecBuf>().swap(v);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     c->dscratch = c->dscratch1 = nullptr;

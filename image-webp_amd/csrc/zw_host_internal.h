@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -42,6 +43,14 @@ struct zw_ctx {
     // and streams are reused instead of allocated per call
     struct zw_pipe* pipe1 = nullptr;
     int pipe1_key[5] = {0, 0, 0, 0, 0};
+    // decode: per-frame worst-case record buffers of the two pipelined buffer
+    // sets, kept between chunks and calls (a parse touches only the pages it
+    // writes; reallocating them per chunk cost page faults and unmaps)
+    struct RecBuf {
+        std::unique_ptr<uint8_t[]> p;  // uninitialised: untouched pages stay unbacked
+        size_t cap = 0;
+    };
+    std::vector<RecBuf> dec_recs[2];
 };
 
 #define HIPOK(x)                                  \
