@@ -14,8 +14,8 @@
 // Rust's BinaryHeap tie behaviour (heapify, pop = sift to the bottom then up,
 // peek_mut write-back = sift down), so equal frequencies resolve as in the
 // reference.  Over-long trees (> 15 bits, > 7 for the code-length code) are
-// re-balanced as the reference does; among equal frequencies the reference's
-// sort_unstable order is Rust's ipnsort's and here a stable order (see DESIGN).
+// re-balanced as the reference does, in the order of the reference's
+// sort_unstable_by_key (Rust 1.92's ipnsort, restated in RustUnstableSort).
 #include <algorithm>
 #include <cstring>
 #include <numeric>
@@ -136,6 +136,124 @@ struct RustMinHeap {
     }
 };
 
+// `indexes.sort_unstable_by_key(|&(_, f)| f)` (:259-260) on (symbol, freq)
+// pairs.  The order among equal frequencies decides which tied symbols get the
+// longer codes, so the Rust 1.92 standard library's unstable sort
+// (core::slice::sort::unstable) is followed step by step: insertion sort up to
+// 20 elements; a whole-slice leading run is kept (reversed when strictly
+// descending); otherwise introsort-style quicksort with limit 2*ilog2(len|1),
+// stable small sort at <= 32 elements (the 16-byte pair takes
+// small_sort_general, a stable sort), heapsort once the limit is spent,
+// (recursive) median-of-3 pivots, the equal-to-ancestor-pivot shortcut, and
+// the branchless cyclic Lomuto partition.
+class RustUnstableSort {
+  public:
+    struct Pair {
+        uint16_t sym;
+        uint32_t f;
+    };
+    static void sort(Pair* v, size_t n)
+    {
+        if (n < 2) return;
+        if (n <= 20) return insertion(v, n);
+        size_t run = 2;
+        const bool desc = v[1].f < v[0].f;
+        while (run < n && (desc ? v[run].f < v[run - 1].f : !(v[run].f < v[run - 1].f))) run++;
+        if (run == n) {
+            if (desc) std::reverse(v, v + n);
+            return;
+        }
+        unsigned lg = 0;
+        for (size_t x = n | 1; x > 1; x >>= 1) lg++;
+        quick(v, n, nullptr, 2 * lg);
+    }
+
+  private:
+    static void insertion(Pair* v, size_t n)
+    {
+        for (size_t i = 1; i < n; i++)
+            for (size_t j = i; j > 0 && v[j].f < v[j - 1].f; j--) std::swap(v[j], v[j - 1]);
+    }
+    static void heapsort(Pair* v, size_t n)
+    {
+        for (size_t i = n + n / 2; i-- > 0;) {
+            size_t node = i >= n ? i - n : 0;
+            if (i < n) std::swap(v[0], v[i]);
+            const size_t end = std::min(i, n);
+            for (size_t c; (c = 2 * node + 1) < end; node = c) {
+                if (c + 1 < end && v[c].f < v[c + 1].f) c++;
+                if (!(v[node].f < v[c].f)) break;
+                std::swap(v[node], v[c]);
+            }
+        }
+    }
+    static size_t med3(const Pair* v, size_t a, size_t b, size_t c)
+    {
+        const bool ab = v[a].f < v[b].f, ac = v[a].f < v[c].f;
+        if (ab != ac) return a;
+        return ((v[b].f < v[c].f) != ab) ? c : b;
+    }
+    static size_t med3_rec(const Pair* v, size_t a, size_t b, size_t c, size_t n)
+    {
+        if (n >= 8) {  // n * 8 >= 64
+            const size_t s = n / 8;
+            a = med3_rec(v, a, a + 4 * s, a + 7 * s, s);
+            b = med3_rec(v, b, b + 4 * s, b + 7 * s, s);
+            c = med3_rec(v, c, c + 4 * s, c + 7 * s, s);
+        }
+        return med3(v, a, b, c);
+    }
+    static size_t pivot(const Pair* v, size_t n)
+    {
+        const size_t s = n / 8;
+        return n < 64 ? med3(v, 0, 4 * s, 7 * s) : med3_rec(v, 0, 4 * s, 7 * s, s);
+    }
+    // Pivot to the front, cyclic Lomuto over the rest (elements 1..n-1 then
+    // the one first lifted out of the hole), pivot into place.
+    static size_t partition(Pair* v, size_t n, size_t p, bool or_equal)
+    {
+        std::swap(v[0], v[p]);
+        const uint32_t pf = v[0].f;
+        Pair* w = v + 1;
+        const size_t m = n - 1;
+        size_t lt = 0;
+        if (m) {
+            const Pair lifted = w[0];
+            size_t hole = 0;
+            for (size_t r = 1; r <= m; r++) {
+                const Pair e = r < m ? w[r] : lifted;
+                w[hole] = w[lt];
+                w[lt] = e;
+                if (r < m) hole = r;
+                lt += or_equal ? !(pf < e.f) : e.f < pf;
+            }
+        }
+        std::swap(v[0], v[lt]);
+        return lt;
+    }
+    static void quick(Pair* v, size_t n, const Pair* ancestor, unsigned limit)
+    {
+        for (;;) {
+            if (n <= 32) return insertion(v, n);
+            if (!limit) return heapsort(v, n);
+            limit--;
+            const size_t p = pivot(v, n);
+            if (ancestor && !(ancestor->f < v[p].f)) {
+                const size_t le = partition(v, n, p, true);
+                v += le + 1;
+                n -= le + 1;
+                ancestor = nullptr;
+                continue;
+            }
+            const size_t lt = partition(v, n, p, false);
+            quick(v, lt, ancestor, limit);
+            ancestor = v + lt;
+            v += lt + 1;
+            n -= lt + 1;
+        }
+    }
+};
+
 // build_huffman_tree (:163-287): returns false for <= 1 used symbol.
 bool huffman_lengths_codes(const uint32_t* freq, int n, uint8_t* len, uint16_t* code, int limit)
 {
@@ -179,14 +297,14 @@ bool huffman_lengths_codes(const uint32_t* freq, int n, uint8_t* len, uint16_t* 
             cnt[l + 1] += 2;
             kraft--;
         }
-        std::vector<int> order(n);
-        std::iota(order.begin(), order.end(), 0);
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return freq[a] < freq[b]; });
+        std::vector<RustUnstableSort::Pair> order(n);
+        for (int i = 0; i < n; i++) order[i] = {(uint16_t)i, freq[i]};
+        RustUnstableSort::sort(order.data(), order.size());
         int l = limit;
-        for (int i : order) {
-            if (!freq[i]) continue;
+        for (const auto& o : order) {
+            if (!o.f) continue;
             while (!cnt[l]) l--;
-            len[i] = (uint8_t)l;
+            len[o.sym] = (uint8_t)l;
             cnt[l]--;
         }
     }

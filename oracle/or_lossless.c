@@ -9,11 +9,13 @@
  * The Huffman construction follows build_huffman_tree (:163-287) including the
  * tie behaviour of Rust's std BinaryHeap (from_iter = rebuild, pop =
  * sift_down_to_bottom + sift_up, PeekMut write-back = sift_down), restated
- * below.  One case is not pinned: when a tree exceeds the length limit
- * (15, or 7 for the code-length code), the reference re-assigns lengths in
- * the order of `sort_unstable_by_key(frequency)`, whose order among EQUAL
- * frequencies is Rust's ipnsort's; here a stable sort is used (identical
- * whenever the tied symbols end up with the same length).
+ * below.  When a tree exceeds the length limit (15, or 7 for the code-length
+ * code), the reference re-assigns lengths in the order of
+ * `sort_unstable_by_key(frequency)` (:259-260), whose order among EQUAL
+ * frequencies is that of the Rust standard library's unstable sort (ipnsort,
+ * rust-version 1.92 in Cargo.toml); rust_sort_unstable_by_key below restates
+ * it.  No Rust toolchain is available here, so that restatement is checked by
+ * its invariants (tests/test_lossless.py), not against Rust's own output.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -154,11 +156,182 @@ static item_t heap_pop(item_t *d, size_t *n)
     return top;
 }
 
-static int cmp_freq_stable(const void *a, const void *b)
+/* --- Rust 1.92 `<[T]>::sort_unstable_by_key` for T = (usize, u32) keyed by
+ * the u32 (core::slice::sort::unstable).  Only the order among equal keys
+ * matters here, so every step that can move equal keys is restated as is:
+ *   sort():      len <= 20 -> insertion sort (stable); else ipnsort()
+ *   ipnsort():   a leading run covering the whole slice is kept (reversed if
+ *                strictly descending); else quicksort(limit = 2*ilog2(len|1))
+ *   quicksort(): len <= 32 -> small_sort_general (sort4/sort8_stable +
+ *                insert_tail + bidirectional_merge: a stable sort for a total
+ *                order, so insertion sort gives the same result for 16-byte
+ *                T, which has no "efficient in-place swap");
+ *                limit exhausted -> heapsort; pivot = median3 / recursive
+ *                pseudo-median of 3 (shared/pivot.rs); if the ancestor pivot
+ *                is not less than the pivot, partition by <= and drop the
+ *                equal part; partition = swap pivot to 0, branchless cyclic
+ *                Lomuto over v[1..], swap pivot into place.  */
+typedef struct {
+    uint32_t idx, key;
+} kv_t;
+
+static void kv_insertion(kv_t *v, size_t n)
 {
-    const uint32_t *x = (const uint32_t *)a, *y = (const uint32_t *)b; /* (freq, index) */
-    if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
-    return x[1] < y[1] ? -1 : (x[1] > y[1]);
+    for (size_t i = 1; i < n; i++) {
+        kv_t t = v[i];
+        size_t j = i;
+        while (j > 0 && t.key < v[j - 1].key) {
+            v[j] = v[j - 1];
+            j--;
+        }
+        v[j] = t;
+    }
+}
+
+static void kv_sift_down(kv_t *v, size_t n, size_t node)
+{
+    for (;;) {
+        size_t child = 2 * node + 1;
+        if (child >= n) break;
+        if (child + 1 < n) child += v[child].key < v[child + 1].key;
+        if (!(v[node].key < v[child].key)) break;
+        kv_t t = v[node];
+        v[node] = v[child];
+        v[child] = t;
+        node = child;
+    }
+}
+
+static void kv_heapsort(kv_t *v, size_t n)
+{
+    for (size_t i = n + n / 2; i-- > 0;) {
+        size_t sift = 0;
+        if (i >= n) {
+            sift = i - n;
+        } else {
+            kv_t t = v[0];
+            v[0] = v[i];
+            v[i] = t;
+        }
+        kv_sift_down(v, i < n ? i : n, sift);
+    }
+}
+
+static size_t kv_median3(const kv_t *v, size_t a, size_t b, size_t c)
+{
+    int x = v[a].key < v[b].key, y = v[a].key < v[c].key;
+    if (x == y) return ((v[b].key < v[c].key) ^ x) ? c : b;
+    return a;
+}
+
+static size_t kv_median3_rec(const kv_t *v, size_t a, size_t b, size_t c, size_t n)
+{
+    if (n * 8 >= 64) {
+        size_t n8 = n / 8;
+        a = kv_median3_rec(v, a, a + n8 * 4, a + n8 * 7, n8);
+        b = kv_median3_rec(v, b, b + n8 * 4, b + n8 * 7, n8);
+        c = kv_median3_rec(v, c, c + n8 * 4, c + n8 * 7, n8);
+    }
+    return kv_median3(v, a, b, c);
+}
+
+static size_t kv_choose_pivot(const kv_t *v, size_t n)
+{
+    size_t n8 = n / 8;
+    if (n < 64) return kv_median3(v, 0, n8 * 4, n8 * 7);
+    return kv_median3_rec(v, 0, n8 * 4, n8 * 7, n8);
+}
+
+/* partition(): `le` selects the `!is_less(pivot, x)` predicate (x <= pivot) */
+static size_t kv_partition(kv_t *v, size_t n, size_t p, int le)
+{
+    kv_t t = v[0];
+    v[0] = v[p];
+    v[p] = t;
+    const uint32_t pk = v[0].key;
+    kv_t *w = v + 1;
+    const size_t m = n - 1;
+    size_t num_lt = 0;
+    if (m > 0) {
+        /* cyclic Lomuto: the hole starts at w[0] (its value saved) and
+         * every element w[1..m), then the saved one, is placed in turn */
+        const kv_t saved = w[0];
+        size_t gap = 0;
+        for (size_t r = 1; r <= m; r++) {
+            const kv_t e = r < m ? w[r] : saved;
+            const int is_lt = le ? !(pk < e.key) : e.key < pk;
+            w[gap] = w[num_lt];
+            w[num_lt] = e;
+            gap = r < m ? r : gap;
+            num_lt += (size_t)is_lt;
+        }
+    }
+    t = v[0];
+    v[0] = v[num_lt];
+    v[num_lt] = t;
+    return num_lt;
+}
+
+static void kv_quicksort(kv_t *v, size_t n, const kv_t *ancestor, uint32_t limit)
+{
+    for (;;) {
+        if (n <= 32) {
+            kv_insertion(v, n);
+            return;
+        }
+        if (limit == 0) {
+            kv_heapsort(v, n);
+            return;
+        }
+        limit--;
+        size_t p = kv_choose_pivot(v, n);
+        if (ancestor && !(ancestor->key < v[p].key)) {
+            size_t num_le = kv_partition(v, n, p, 1);
+            v += num_le + 1;
+            n -= num_le + 1;
+            ancestor = NULL;
+            continue;
+        }
+        size_t num_lt = kv_partition(v, n, p, 0);
+        kv_quicksort(v, num_lt, ancestor, limit);
+        ancestor = &v[num_lt];
+        v += num_lt + 1;
+        n -= num_lt + 1;
+    }
+}
+
+void or_rust_sort_unstable_by_key(uint32_t *idx, uint32_t *key, size_t n)
+{
+    if (n < 2) return;
+    kv_t *v = (kv_t *)malloc(sizeof(kv_t) * n);
+    for (size_t i = 0; i < n; i++) v[i] = (kv_t){idx[i], key[i]};
+    if (n <= 20) {
+        kv_insertion(v, n);
+    } else {
+        size_t run = 2;
+        const int desc = v[1].key < v[0].key;
+        if (desc)
+            while (run < n && v[run].key < v[run - 1].key) run++;
+        else
+            while (run < n && !(v[run].key < v[run - 1].key)) run++;
+        if (run == n) {
+            if (desc)
+                for (size_t i = 0; i < n / 2; i++) {
+                    kv_t t = v[i];
+                    v[i] = v[n - 1 - i];
+                    v[n - 1 - i] = t;
+                }
+        } else {
+            uint32_t lg = 0;
+            for (size_t x = n | 1; x > 1; x >>= 1) lg++;
+            kv_quicksort(v, n, NULL, 2 * lg);
+        }
+    }
+    for (size_t i = 0; i < n; i++) {
+        idx[i] = v[i].idx;
+        key[i] = v[i].key;
+    }
+    free(v);
 }
 
 /* build_huffman_tree (:163-287) */
@@ -228,21 +401,24 @@ static int build_tree(const uint32_t *freq, int n, uint8_t *len, uint16_t *code,
             counts[i + 1] += 2;
             total--;
         }
-        uint32_t(*idx)[2] = (uint32_t(*)[2])malloc(sizeof(uint32_t) * 2 * (size_t)n);
+        /* indexes = frequencies.enumerate(); sort_unstable_by_key(frequency) */
+        uint32_t *idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)n);
+        uint32_t *key = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)n);
         for (int i = 0; i < n; i++) {
-            idx[i][0] = freq[i];
-            idx[i][1] = (uint32_t)i;
+            idx[i] = (uint32_t)i;
+            key[i] = freq[i];
         }
-        qsort(idx, (size_t)n, sizeof idx[0], cmp_freq_stable);
+        or_rust_sort_unstable_by_key(idx, key, (size_t)n);
         int l = limit;
         for (int k = 0; k < n; k++) {
-            if (idx[k][0] > 0) {
+            if (key[k] > 0) {
                 while (counts[l] == 0) l--;
-                len[idx[k][1]] = (uint8_t)l;
+                len[idx[k]] = (uint8_t)l;
                 counts[l]--;
             }
         }
         free(idx);
+        free(key);
     }
     /* canonical codes, bit-reversed */
     memset(code, 0, (size_t)n * 2);

@@ -100,6 +100,10 @@ int or_encode_frame_lossless(const uint8_t *data, size_t len, uint32_t width, ui
                              int use_predictor, int implicit_dims, uint8_t **out, size_t *out_len);
 int or_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, uint8_t **out,
                     size_t *out_len);
+/* <[(usize, u32)]>::sort_unstable_by_key(|&(_, k)| k) of Rust 1.92 (the
+ * length-limit reassignment order of build_huffman_tree, api.rs:259-260);
+ * sorts the (idx[i], key[i]) pairs in place. */
+void or_rust_sort_unstable_by_key(uint32_t *idx, uint32_t *key, size_t n);
 void or_yuv_to_rgb_simple_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
 void or_analyze(const uint8_t *Y, const uint8_t *U, const uint8_t *V, int width, int height,
                 uint8_t *mb_alphas, uint32_t histo[256]);

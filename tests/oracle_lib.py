@@ -237,6 +237,18 @@ def encode_alpha(img, w, h, color):
     return _bytes_out(L.or_encode_alpha, _p(a) if a.size else None, a.size, w, h, color)
 
 
+def rust_sort_unstable_by_key(keys):
+    """<[(usize, u32)]>::sort_unstable_by_key(|&(_, k)| k) as restated in the
+    oracle (Rust 1.92 ipnsort; api.rs:259-260).  Returns (indexes, keys)."""
+    L = lib()
+    L.or_rust_sort_unstable_by_key.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    k = np.ascontiguousarray(keys, dtype=np.uint32).copy()
+    idx = np.arange(len(k), dtype=np.uint32)
+    if len(k):
+        L.or_rust_sort_unstable_by_key(_p(idx), _p(k), len(k))
+    return idx, k
+
+
 def riff_vp8_chunk(data):
     """Extract the 'VP8 ' chunk payload from a RIFF WebP file."""
     assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"

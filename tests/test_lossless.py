@@ -69,6 +69,15 @@ def _images():
     rng.shuffle(g)
     sk = np.stack([g, g, g, g], 1).reshape(64, 512, 4)
     yield "skewed512x64", 512, 64, sk
+    # length limiting with tie groups split across code lengths: the symbols of
+    # equal frequency that get the longer codes are chosen by the order of the
+    # reference's sort_unstable_by_key (api.rs:259-260), not by symbol order
+    # (checked: with a stable order instead, both predictor settings give other bytes)
+    parts = [np.full(int(1.6 ** k), 100 + k, np.uint8) for k in range(22)]
+    parts += [np.full(c, s, np.uint8) for s, c in zip(range(0, 90), [1, 2, 3] * 30)]
+    g = np.resize(np.concatenate(parts), 640 * 256)
+    rng.shuffle(g)
+    yield "tied640x256", 640, 256, np.stack([g, g[::-1], g, g], 1).reshape(256, 640, 4)
 
 
 IMAGES = list(_images())
@@ -99,6 +108,37 @@ def test_oracle_alpha_chunk_roundtrip_libwebp(name, w, h, img):
     vp8x = bytes([0x10, 0, 0, 0]) + (w - 1).to_bytes(3, "little") + (h - 1).to_bytes(3, "little")
     dec = _libwebp_rgba(_riff(_chunk(b"VP8X", vp8x), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8)))
     assert np.array_equal(dec[..., 3], rgba[..., 3])
+
+
+def _stable_order(keys):
+    return np.argsort(np.asarray(keys, np.int64), kind="stable")
+
+
+@pytest.mark.parametrize("n,seed,span", [(0, 0, 1), (1, 0, 1), (5, 1, 3), (20, 2, 4), (21, 3, 4), (33, 4, 5),
+                                         (40, 5, 2), (64, 6, 9), (280, 7, 6), (280, 8, 1), (256, 9, 40),
+                                         (1000, 10, 3), (2328, 11, 50)])
+def test_rust_sort_unstable_invariants(n, seed, span):
+    """The oracle's ipnsort restatement: a permutation, sorted by key, stable
+    (insertion sort) up to 20 elements, and a sorted / strictly descending
+    whole-slice run is returned as sorted by the run detection alone."""
+    keys = np.random.default_rng(seed).integers(0, span, n).astype(np.uint32)
+    idx, k = O.rust_sort_unstable_by_key(keys)
+    assert sorted(idx.tolist()) == list(range(n))
+    assert np.array_equal(keys[idx], k) and np.all(np.diff(k.astype(np.int64)) >= 0)
+    if n <= 20:
+        assert np.array_equal(idx, _stable_order(keys))
+    asc = np.sort(keys)
+    assert np.array_equal(O.rust_sort_unstable_by_key(asc)[0], np.arange(n))
+    desc = np.arange(n, 0, -1, dtype=np.uint32)
+    assert np.array_equal(O.rust_sort_unstable_by_key(desc)[0], np.arange(n)[::-1])
+
+
+def test_rust_sort_unstable_is_not_stable():
+    """Above the small-sort sizes the partitioning reorders equal keys, which
+    is the case the length-limit reassignment depends on."""
+    keys = np.random.default_rng(12).integers(0, 3, 280).astype(np.uint32)
+    idx, _ = O.rust_sort_unstable_by_key(keys)
+    assert not np.array_equal(idx, _stable_order(keys))
 
 
 def test_oracle_lossless_errors():
