@@ -251,6 +251,9 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
             }
         }
         wsync();
+        uint8_t bins[16];
+        uint32_t z = 0;
+        int vmax = 0, hidx = 0;
         if (lane < 48) {
             // libwebp analysis predictors on source pixels (analysis.rs:259-490, quirk A21):
             // lane 0..31 luma (mode = lane >> 4: DC, TM; block lane & 15), 32..47 chroma
@@ -299,33 +302,68 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
             // (X + 1812) >> 9 == (8X + 14500) >> 12 and (X + 937) >> 9 == (8X + 7500) >> 12
             int o[16];
             fdct16_pk(d, o);
-            const int hidx = luma ? mode : 2 + mode;
-            // bin 0 holds most coefficients: count it in the lane, add the rest
-            // with (far less contended) LDS atomics
-            uint32_t z = 0;
+            hidx = luma ? mode : 2 + mode;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                const int v = min(iabs(o[k]) >> 3, 31);
-                if (v == 0) z++;
-                else atomicAdd(&hist[wv][hidx][v], 1u);
+                bins[k] = (uint8_t)min(iabs(o[k]) >> 3, 31);
+                z += bins[k] == 0;
+                vmax = max(vmax, (int)bins[k]);
             }
-            if (z) atomicAdd(&hist[wv][hidx][0], z);
         }
-        wsync();
+        // Fast path: when bin 0 holds at least half of a histogram's
+        // coefficients (256 luma, 128 chroma), no other bin can exceed it, so
+        // max_value = that count and last_non_zero = the largest bin index.
+        // Sums over the 8-lane groups, then the luma 16-lane groups.
+        uint32_t zs = z;
+        int vm = vmax;
+#pragma unroll
+        for (int o2 = 1; o2 <= 4; o2 <<= 1) {
+            zs += (uint32_t)__shfl_xor((int)zs, o2);
+            vm = max(vm, __shfl_xor(vm, o2));
+        }
+        {
+            const uint32_t zo = (uint32_t)__shfl_xor((int)zs, 8);
+            const int vo = __shfl_xor(vm, 8);
+            if (lane < 32) {
+                zs += zo;
+                vm = max(vm, vo);
+            }
+        }
+        const uint32_t ncoef = lane < 32 ? 256u : 128u;
+        const bool slow = __ballot(lane < 48 && 2 * zs < ncoef) != 0ull;
+        if (slow) {
+            // bin 0 holds most coefficients: count it in the lane, add the rest
+            // with (far less contended) LDS atomics
+            if (lane < 48) {
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (bins[k]) atomicAdd(&hist[wv][hidx][bins[k]], 1u);
+                if (z) atomicAdd(&hist[wv][hidx][0], z);
+            }
+            wsync();
+        }
         // per histogram: max count and last non-empty bin (get_alpha,
         // analysis.rs:160), two histograms per pass, lane = (histogram, bin)
         int av[4];
+        if (!slow) {
+            const int ah = zs > 1 ? (int)(510u * (uint32_t)vm / zs) : 0;
+            av[0] = __builtin_amdgcn_readlane(ah, 0);
+            av[1] = __builtin_amdgcn_readlane(ah, 16);
+            av[2] = __builtin_amdgcn_readlane(ah, 32);
+            av[3] = __builtin_amdgcn_readlane(ah, 40);
+        } else {
 #pragma unroll
-        for (int ps = 0; ps < 2; ps++) {
-            const uint32_t c = hist[wv][2 * ps + (lane >> 5)][lane & 31];
-            uint32_t mx = c;
+            for (int ps = 0; ps < 2; ps++) {
+                const uint32_t c = hist[wv][2 * ps + (lane >> 5)][lane & 31];
+                uint32_t mx = c;
 #pragma unroll
-            for (int o2 = 16; o2 >= 1; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o2));
-            const uint32_t half = (uint32_t)(__ballot(c > 0) >> (lane & 32));
-            const int lnz = half ? 31 - __clz((int)half) : 1;
-            const int ah = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
-            av[2 * ps] = __builtin_amdgcn_readlane(ah, 0);
-            av[2 * ps + 1] = __builtin_amdgcn_readlane(ah, 32);
+                for (int o2 = 16; o2 >= 1; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o2));
+                const uint32_t half = (uint32_t)(__ballot(c > 0) >> (lane & 32));
+                const int lnz = half ? 31 - __clz((int)half) : 1;
+                const int ah = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
+                av[2 * ps] = __builtin_amdgcn_readlane(ah, 0);
+                av[2 * ps + 1] = __builtin_amdgcn_readlane(ah, 32);
+            }
         }
         const int a0 = av[0], a1 = av[1], a2 = av[2], a3 = av[3];
         if (lane == 0) {

@@ -12,9 +12,13 @@
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -251,8 +255,23 @@ struct Pinned {
     }
     T* data() { return p; }
     T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
     size_t size() const { return n; }
     ~Pinned() { free(); }
+};
+
+// Pinned landing buffers of packed MB streams fetched from the device.
+struct FetchBuf {
+    uint8_t* pack = nullptr;
+    size_t cap = 0;
+    Pinned<unsigned long long> finfo;  // [2*chunk] offset, bytes of each frame's packed stream
+    Pinned<unsigned long long> total;  // [1] bytes of the chunk
+    void release()
+    {
+        if (pack) (void)hipHostFree(pack);
+        pack = nullptr;
+        cap = 0;
+    }
 };
 
 struct PipeLane {
@@ -264,14 +283,21 @@ struct PipeLane {
     hipEvent_t ev[8] = {};
     unsigned long long* d_ctr = nullptr;
     uint8_t* d_rows = nullptr;  // row-parallel encode scratch (small chunks), else null
-    uint8_t* h_pack = nullptr;
-    size_t h_pack_cap = 0;
-    Pinned<unsigned long long> h_finfo;  // [2*n] offset, bytes of each frame's packed stream
-    Pinned<unsigned long long> h_total;
+    FetchBuf fb[2];  // [0] pass-1 records (host stats replay), [1] pass-2 records (emission thread)
     Pinned<ZwStatsOut> h_stats;          // [chunk] pass-1 statistics from k_stats
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
     int rc = 0;
+    // Emission runs on its own thread, one batch behind the lane thread.
+    // `fetched` counts the chunks whose pass-2 records it has copied out
+    // (over all batches): pass 2 of the next batch may then reuse the chunk's
+    // device buffers.  fetched = LLONG_MAX once the emitter failed.
+    struct Sync {
+        std::mutex mu;
+        std::condition_variable cv;
+        long long fetched = 0;
+    };
+    std::unique_ptr<Sync> sync = std::make_unique<Sync>();
 };
 
 struct zw_pipe {
@@ -295,10 +321,13 @@ struct zw_pipe {
     unsigned long long *d_finfo = nullptr, *d_finfo2 = nullptr;  // pass-1 / pass-2 packed streams
     uint8_t *d_pack = nullptr, *d_pack2 = nullptr;
     size_t pack_stride = 0;  // worst-case packed bytes per frame
-    Pinned<ZwFrameParams> h_params;
+    // Per-frame header state, two copies by batch parity: the statistics of
+    // batch b+1 are built while batch b is still being emitted.
+    Pinned<ZwFrameParams> h_params;  // [2][n]
     Pinned<ZwLevelCosts> h_lcost;
-    std::vector<uint8_t> h_have_upd;
-    std::vector<uint8_t> h_upd;  // [n][4*8*3*11]
+    std::vector<uint8_t> h_have_upd;  // [2][n]
+    std::vector<uint8_t> h_upd;       // [2][n][4*8*3*11]
+    int out_par = 0;                  // parity of the last emitted batch
     std::vector<std::vector<uint8_t>> bitstreams;
     // container output (zw_pipe_set_container): RIFF/VP8X per frame, the ALPH
     // chunk of an LA8 / RGBA8 frame encoded from its host copy
@@ -319,7 +348,8 @@ static void pipe_free(zw_pipe* p)
     for (PipeLane& L : p->lanes) {
         if (L.d_ctr) (void)hipFree(L.d_ctr);
         if (L.d_rows) (void)hipFree(L.d_rows);
-        if (L.h_pack) (void)hipHostFree(L.h_pack);
+        L.fb[0].release();
+        L.fb[1].release();
         for (int i = 0; i < 8; i++)
             if (L.ev[i]) (void)hipEventDestroy(L.ev[i]);
         for (hipEvent_t e : L.cev)
@@ -441,14 +471,14 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
         PipeLane& L = p->lanes[g];
         L.f0 = (int)((long long)n * g / G);
         L.n = (int)((long long)n * (g + 1) / G) - L.f0;
-        ok = L.h_finfo.alloc(2 * (size_t)L.n) && (p->host_stats || L.h_stats.alloc((size_t)L.n));
         L.chunk = pipe_chunk_for(L.n, ctx->device);
+        ok = L.fb[0].finfo.alloc(2 * (size_t)L.chunk) && L.fb[1].finfo.alloc(2 * (size_t)L.chunk) &&
+             L.fb[0].total.alloc(1) && L.fb[1].total.alloc(1) && (p->host_stats || L.h_stats.alloc((size_t)L.n));
         const int nch = (L.n + L.chunk - 1) / L.chunk;
         L.cev.assign(2 * (size_t)nch, nullptr);
         ok = ok && hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) == hipSuccess &&
              hipStreamCreateWithFlags(&L.stream2, hipStreamNonBlocking) == hipSuccess &&
-             hipMalloc(&L.d_ctr, 2 * (size_t)nch * sizeof(unsigned long long)) == hipSuccess &&
-             L.h_total.alloc(2 * (size_t)nch);
+             hipMalloc(&L.d_ctr, 2 * (size_t)nch * sizeof(unsigned long long)) == hipSuccess;
         if (ok && pipe_rows_for(L.chunk, p->mbh, ctx->device)) {
             const size_t rb = zwk_encode_rows_bytes(p->mbw, p->mbh, L.chunk);
             ok = hipMalloc(&L.d_rows, rb) == hipSuccess && hipMemset(L.d_rows, 0, rb) == hipSuccess;
@@ -464,12 +494,12 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
         pipe_free(p);
         return ZW_ENOMEM;
     }
-    if (!p->h_params.alloc(N) || !p->h_lcost.alloc(N)) {
+    if (!p->h_params.alloc(2 * N) || !p->h_lcost.alloc(N)) {
         pipe_free(p);
         return ZW_ENOMEM;
     }
-    p->h_have_upd.assign(N, 0);
-    p->h_upd.assign(N * 4 * 8 * 3 * 11, 0);
+    p->h_have_upd.assign(2 * N, 0);
+    p->h_upd.assign(2 * N * 4 * 8 * 3 * 11, 0);
     p->bitstreams.resize(N);
     ZwFrameParams t;
     memset(&t, 0, sizeof t);
@@ -587,28 +617,26 @@ static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_
     return ZW_OK;
 }
 
-// Copy a packed chunk to the lane's pinned buffer on the copy stream once
-// `ready` (recorded after chunk_pack) has fired.  h_finfo[2*i] = offset of frame fa+i.
-static int chunk_fetch(zw_pipe* p, PipeLane& L, int fa, int na, int slot, hipEvent_t ready)
+// Copy a packed chunk into B once `ready` (recorded after chunk_pack) has
+// fired.  B.finfo[2*i] = offset of frame fa+i in B.pack.
+static int chunk_fetch(zw_pipe* p, PipeLane& L, FetchBuf& B, int fa, int na, int slot, hipEvent_t ready)
 {
     const size_t F = (size_t)fa;
     HIPOK(hipEventSynchronize(ready));
-    int r = ctx_d2h(p->ctx, L.h_total.data() + slot, L.d_ctr + slot, sizeof(unsigned long long));
+    int r = ctx_d2h(p->ctx, B.total.data(), L.d_ctr + slot, sizeof(unsigned long long));
     const bool p2 = slot & 1;
     if (!r)
-        r = ctx_d2h(p->ctx, L.h_finfo.data(), (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
+        r = ctx_d2h(p->ctx, B.finfo.data(), (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
                     2 * (size_t)na * sizeof(unsigned long long));
     if (r) return r;
-    const unsigned long long total = L.h_total[slot];
-    if (total > L.h_pack_cap) {
-        if (L.h_pack) (void)hipHostFree(L.h_pack);
-        L.h_pack = nullptr;
-        L.h_pack_cap = 0;
+    const unsigned long long total = B.total[0];
+    if (total > B.cap) {
+        B.release();
         const size_t cap = (size_t)(total * 1.25) + 4096;
-        if (hipHostMalloc((void**)&L.h_pack, cap, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
-        L.h_pack_cap = cap;
+        if (hipHostMalloc((void**)&B.pack, cap, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
+        B.cap = cap;
     }
-    return ctx_d2h(p->ctx, L.h_pack, (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, total);
+    return ctx_d2h(p->ctx, B.pack, (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, total);
 }
 
 // Fetch the chunk's k_stats output (device pre-aggregated ProbaStats) once
@@ -619,35 +647,39 @@ static int chunk_fetch_stats(zw_pipe* p, PipeLane& L, int fa, int na, hipEvent_t
     return ctx_d2h(p->ctx, L.h_stats.data() + (fa - L.f0), p->d_stats + fa, (size_t)na * sizeof(ZwStatsOut));
 }
 
-static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na)
+// Header state of frame f in the batch-parity copy `par`.
+static inline size_t hidx(const zw_pipe* p, int par, size_t f) { return (size_t)par * p->n + f; }
+
+static int chunk_stats(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa, n = (size_t)na;
+    ZwFrameParams* hp = p->h_params.data() + hidx(p, par, F);
     // segment params of the chunk (written by k_segments before pass 1)
     {
-        const int r = ctx_d2h(p->ctx, p->h_params.data() + F, p->d_params + F, n * sizeof(ZwFrameParams));
+        const int r = ctx_d2h(p->ctx, hp, p->d_params + F, n * sizeof(ZwFrameParams));
         if (r) return r;
     }
     parallel_for(na, [&](int i) {
-        const size_t f = F + i;
+        const size_t f = F + i, hf = hidx(p, par, f);
         zwh::Stats st;
         int sp;
         if (p->host_stats) {
-            sp = zwh::replay_stats(st, L.h_pack + L.h_finfo[2 * i], p->mbw, p->mbh);
+            sp = zwh::replay_stats(st, L.fb[0].pack + L.fb[0].finfo[2 * i], p->mbw, p->mbh);
         } else {
             const ZwStatsOut& so = L.h_stats[f - L.f0];
             memcpy(st.s, so.s, sizeof st.s);
             sp = zwh::skip_prob(so.total_mbs, so.nonzero_mbs);
         }
-        uint8_t* upd = p->h_upd.data() + f * 4 * 8 * 3 * 11;
+        uint8_t* upd = p->h_upd.data() + hf * 4 * 8 * 3 * 11;
         bool have = zwh::updated_probs(st, (uint8_t(*)[8][3][11])upd);
-        p->h_have_upd[f] = have;
-        ZwFrameParams& P = p->h_params[f];
+        p->h_have_upd[hf] = have;
+        ZwFrameParams& P = p->h_params[hf];
         P.skip_prob = sp;
         memcpy(P.probs, upd, sizeof P.probs);
         zwh::level_costs(p->h_lcost[f], (const uint8_t(*)[8][3][11])upd);
     });
-    HIPOK(hipMemcpyAsync(p->d_params + F, p->h_params.data() + F, n * sizeof(ZwFrameParams), hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(p->d_params + F, hp, n * sizeof(ZwFrameParams), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(p->d_lcost + F, p->h_lcost.data() + F, n * sizeof(ZwLevelCosts), hipMemcpyHostToDevice, s));
     return ZW_OK;
 }
@@ -666,16 +698,17 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
     return ZW_OK;
 }
 
-static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na)
+static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
+    const FetchBuf& B = L.fb[1];
     parallel_for(na, [&](int i) {
-        const size_t f = F + i;
+        const size_t f = F + i, hf = hidx(p, par, f);
         std::vector<uint8_t>& out = p->bitstreams[f];
         if (!p->container) {
-            zwh::emit_frame(out, p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h, p->h_have_upd[f] != 0,
-                            (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
+            zwh::emit_frame(out, p->h_params[hf], B.pack + B.finfo[2 * i], p->w, p->h, p->h_have_upd[hf] != 0,
+                            (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11));
             return;
         }
         // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the
@@ -683,8 +716,8 @@ static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na)
         thread_local std::vector<uint8_t> vp8, alph;
         vp8.clear();
         alph.clear();
-        zwh::emit_frame(vp8, p->h_params[f], L.h_pack + L.h_finfo[2 * i], p->w, p->h, p->h_have_upd[f] != 0,
-                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + f * 4 * 8 * 3 * 11));
+        zwh::emit_frame(vp8, p->h_params[hf], B.pack + B.finfo[2 * i], p->w, p->h, p->h_have_upd[hf] != 0,
+                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11));
         // the image was validated by zw_pipe_set_container (size, dimensions)
         if (has_alpha) (void)zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph);
         const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
@@ -702,17 +735,20 @@ static void lane_times(PipeLane& L)
     (void)hipEventElapsedTime(&L.kms[3], L.ev[4], L.ev[5]);  // pass 2
 }
 
-// Software-pipelined encode of one lane: all pass-1 launches are queued first;
-// the host works on chunk c (stats, then tokens) while the GPU runs later chunks.
-//   GPU (stream):  P1(0) P1(1) .. P1(C-1) P2(0) P2(1) .. P2(C-1)
-//   host:                 S(0)   S(1) ..          E(0)   E(1) .. E(C-1)
+// Software-pipelined encode of one lane.  Per batch: pass 1 of every chunk is
+// queued up front; then per chunk the lane thread fetches the pass-1
+// statistics, builds the probabilities / level costs and queues pass 2.  The
+// pass-2 records of the batch are fetched and emitted by an emission thread
+// while the lane thread already works on the next batch (nb > 1):
+//   GPU (stream):  P1(b,0) P1(b,1) P2(b,0) P2(b,1) P1(b+1,0) P1(b+1,1) P2(b+1,0) ..
+//   lane thread:           S(b,0)  S(b,1)                   S(b+1,0)  S(b+1,1) ..
+//   emitter:                               E(b,0)  E(b,1) ......
+// so pass 2 of batch b+1 waits only for its own statistics, not for the
+// emission of batch b.  The per-frame header state has one copy per batch
+// parity, and pass 2 of (b+1, c) is queued only once the emitter has copied
+// out the records of (b, c), whose device buffers it reuses.
 static double g_trace_t0 = 0;
 static bool g_trace = false;
-// Encode the lane's frames `nb` times back to back (nb = 1: one batch).  Per
-// batch: pass 1 of every chunk is queued up front; then per chunk fetch the
-// pass-1 records, replay statistics, queue pass 2; then per chunk fetch the
-// pass-2 records and emit.  With nb > 1 the next batch's pass 1 is queued
-// before this batch's emit loop, so the GPU runs it while the host emits.
 static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
 {
     const int nch = (L.n + L.chunk - 1) / L.chunk;
@@ -736,44 +772,85 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         }
         return ZW_OK;
     };
+    const long long FAILED = std::numeric_limits<long long>::max();
     double fetch = 0, stats = 0, fetch2 = 0, tok = 0;
+    int emit_rc = ZW_OK;
+    {
+        std::lock_guard<std::mutex> lk(L.sync->mu);
+        L.sync->fetched = 0;
+    }
+    // emission of batch b (runs on `em`)
+    auto emitter = [&](int b) {
+        for (int c = 0; c < nch; c++) {
+            const double t0 = now_ms();
+            const int r = chunk_fetch(p, L, L.fb[1], ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
+            {
+                std::lock_guard<std::mutex> lk(L.sync->mu);
+                L.sync->fetched = r ? FAILED : L.sync->fetched + 1;
+            }
+            L.sync->cv.notify_all();
+            if (r) {
+                emit_rc = r;
+                return;
+            }
+            const double t1 = now_ms();
+            chunk_emit(p, L, ca(c), cn(c), b & 1);
+            tok += now_ms() - t1;
+            fetch2 += t1 - t0;
+            if (g_trace)
+                fprintf(stderr, "  lane %d batch %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, b, c,
+                        t1 - g_trace_t0, now_ms() - g_trace_t0);
+        }
+    };
+    std::thread em;
+    auto join_emitter = [&]() {
+        if (em.joinable()) em.join();
+        return emit_rc;
+    };
+    auto fail = [&](int r) {
+        join_emitter();
+        return r;
+    };
     int r = queue_pass1();
     if (r) return r;
     for (int b = 0; b < nb; b++) {
         for (int c = 0; c < nch; c++) {
-            double t0 = now_ms();
-            r = p->host_stats ? chunk_fetch(p, L, ca(c), cn(c), 2 * c, L.cev[2 * c])
+            const double t0 = now_ms();
+            r = p->host_stats ? chunk_fetch(p, L, L.fb[0], ca(c), cn(c), 2 * c, L.cev[2 * c])
                               : chunk_fetch_stats(p, L, ca(c), cn(c), L.cev[2 * c]);
-            if (r) return r;
-            double t1 = now_ms();
-            r = chunk_stats(p, L, ca(c), cn(c));
-            if (r) return r;
+            if (r) return fail(r);
+            const double t1 = now_ms();
+            if ((r = chunk_stats(p, L, ca(c), cn(c), b & 1))) return fail(r);
             stats += now_ms() - t1;
             fetch += t1 - t0;
             if (g_trace)
                 fprintf(stderr, "  lane %d batch %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, b, c,
                         t1 - g_trace_t0, now_ms() - g_trace_t0);
+            if (emit && b > 0) {  // the emitter has copied out chunk c of batch b-1
+                std::unique_lock<std::mutex> lk(L.sync->mu);
+                const long long need = (long long)(b - 1) * nch + c + 1;
+                L.sync->cv.wait(lk, [&] { return L.sync->fetched >= need; });
+                if (L.sync->fetched == FAILED) {
+                    lk.unlock();
+                    return fail(ZW_EDEVICE);
+                }
+            }
             r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
             if (!r && emit) r = chunk_pack(p, L, ca(c), cn(c), p->d_out2, 2 * c + 1);
-            if (r) return r;
-            HIPOK(hipEventRecord(L.cev[2 * c + 1], L.stream));
+            if (!r && hipEventRecord(L.cev[2 * c + 1], L.stream) != hipSuccess) r = ZW_EDEVICE;
+            if (r) return fail(r);
         }
-        if (b + 1 < nb && (r = queue_pass1())) return r;
+        if (b + 1 < nb && (r = queue_pass1())) return fail(r);
         if (emit) {
-            for (int c = 0; c < nch; c++) {
-                double t0 = now_ms();
-                r = chunk_fetch(p, L, ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
-                if (r) return r;
-                double t1 = now_ms();
-                chunk_emit(p, L, ca(c), cn(c));
-                tok += now_ms() - t1;
-                fetch2 += t1 - t0;
-                if (g_trace)
-                    fprintf(stderr, "  lane %d batch %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, b, c,
-                            t1 - g_trace_t0, now_ms() - g_trace_t0);
-            }
+            if ((r = join_emitter())) return r;
+            em = std::thread([&, b]() {
+                (void)hipSetDevice(p->ctx->device);
+                emitter(b);
+            });
         }
     }
+    if ((r = join_emitter())) return r;
+    p->out_par = (nb - 1) & 1;
     HIPOK(hipStreamSynchronize(L.stream));
     if ((r = rows_check(p, L))) return r;
     L.hms[0] = fetch / nb;
@@ -922,8 +999,9 @@ extern "C" int zw_pipe_read_mbinfo(zw_pipe* p, int frame, int pass, uint8_t* mod
 extern "C" int zw_pipe_read_probs(zw_pipe* p, int frame, uint8_t* probs, int* skip_prob)
 {
     if (!p || frame < 0 || frame >= p->n) return ZW_EINVAL;
-    if (probs) memcpy(probs, p->h_params[frame].probs, sizeof p->h_params[frame].probs);
-    if (skip_prob) *skip_prob = p->h_params[frame].skip_prob;
+    const ZwFrameParams& P = p->h_params[hidx(p, p->out_par, (size_t)frame)];
+    if (probs) memcpy(probs, P.probs, sizeof P.probs);
+    if (skip_prob) *skip_prob = P.skip_prob;
     return ZW_OK;
 }
 
