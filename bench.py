@@ -266,15 +266,26 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
            "kernel_frames_per_s": frames / ((rk + lf) * 1e-3),
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                         "alg_bytes_per_mb": 1208}}
-    # decode to packed RGBA (decode_rgba: fancy upsampling on the device, k_yuv2rgb);
+    # decode to packed RGBA (fancy upsampling on the device, k_yuv2rgb) into the
+    # caller's reused buffers (decode_rgba_into, api.rs:1004), and into fresh
+    # per-frame buffers (decode_rgba's Vec per call: page faults on 8 MB each);
     # k_yuv2rgb algorithmic bytes per pixel: Y 1 + U,V 0.5 read, RGBA 4 written
+    import numpy as np
+    bufs = [np.empty(w * h * 4, np.uint8) for _ in range(frames)]
+    zwebp.decode_rgb_batch_into(batch, bufs, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    t0 = time.perf_counter()
+    zwebp.decode_rgb_batch_into(batch, bufs, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    el_rgb = time.perf_counter() - t0
+    yk = zwebp.decode_rgb_kernel_ms(ctx=ctx)
+    del bufs
     zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
     t0 = time.perf_counter()
     zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
-    el_rgb = time.perf_counter() - t0
-    yk = zwebp.decode_rgb_kernel_ms(ctx=ctx)
+    el_alloc = time.perf_counter() - t0
     yb = 5.5 * w * h * frames
-    out["rgba"] = {"batch_decodes_per_s": frames / el_rgb, "k_yuv2rgb_ms": yk,
+    out["rgba"] = {"batch_decodes_per_s": frames / el_rgb, "batch_decodes_per_s_alloc": frames / el_alloc,
+                   "note": "into reused caller buffers (decode_rgba_into); _alloc: a new buffer per frame",
+                   "k_yuv2rgb_ms": yk,
                    "roofline": {"bound": "hbm", "achieved": yb / (yk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": yb / (yk * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                 "alg_bytes_per_px": 5.5}}

@@ -804,13 +804,19 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
 // Frame::fill_rgb / fill_rgba (decoder/vp8.rs:200-258) after decode_frame, on
 // the device: decode -> k_yuv2rgb -> packed RGB(A) down.  Every frame of the
 // batch must have the same dimensions (their packed images are contiguous).
-extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int bpp,
-                                       int upsampling, zw_bytes* outs, uint32_t* widths, uint32_t* heights)
+// The images land either in new buffers (outs) or in the caller's buffers
+// (dst[i], dst_lens[i] bytes, rows `stride` bytes apart: decode_rgba_into /
+// decode_rgb_into, api.rs:1004-1128), where a repeated decode touches no fresh
+// pages.
+static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int bpp, int upsampling,
+                         zw_bytes* outs, uint8_t* const* dst, const size_t* dst_lens, size_t stride, uint32_t* widths,
+                         uint32_t* heights)
 {
-    if (!ctx || n <= 0 || !data || !lens || !outs || (bpp != 3 && bpp != 4) ||
+    if (!ctx || n <= 0 || !data || !lens || (!outs && !dst) || (bpp != 3 && bpp != 4) ||
         (upsampling != ZW_UPSAMPLE_BILINEAR && upsampling != ZW_UPSAMPLE_SIMPLE))
         return ZW_EINVAL;
-    for (int i = 0; i < n; i++) outs[i].data = nullptr, outs[i].len = 0;
+    if (outs)
+        for (int i = 0; i < n; i++) outs[i].data = nullptr, outs[i].len = 0;
     // dimensions first (they size the device output)
     size_t w = 0, h = 0;
     {
@@ -820,7 +826,12 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
         w = f0.width;
         h = f0.height;
     }
-    const size_t fbytes = w * h * (size_t)bpp;
+    const size_t row = w * (size_t)bpp, fbytes = row * h;
+    if (dst) {  // decode_rgba_into: stride >= width * bpp, buffer >= stride * height
+        if (!dst_lens || stride < row) return ZW_EINVAL;
+        for (int i = 0; i < n; i++)
+            if (!dst[i] || dst_lens[i] < stride * h) return ZW_EINVAL;
+    }
     hipStream_t s = ctx_stream(ctx);
     auto enqueue = [&](DecBatch& B, int, int cn) -> int {
         for (int i = 0; i < cn; i++)
@@ -838,12 +849,22 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
         if (int r = ctx_d2h(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
         std::vector<int> oom(cn, 0);
         parallel_for(cn, [&](int i) {
+            const uint8_t* src = hout + (size_t)i * fbytes;
+            if (dst) {
+                uint8_t* o = dst[f0 + i];
+                if (stride == row) {
+                    memcpy(o, src, fbytes);
+                } else {
+                    for (size_t y = 0; y < h; y++) memcpy(o + y * stride, src + y * row, row);
+                }
+                return;
+            }
             uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
             if (!buf) {
                 oom[i] = 1;
                 return;
             }
-            memcpy(buf, hout + (size_t)i * fbytes, fbytes);
+            memcpy(buf, src, fbytes);
             outs[f0 + i].data = buf;
             outs[f0 + i].len = fbytes;
         });
@@ -855,7 +876,8 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
     };
     const int r = dec_pipeline(ctx, n, data, lens, fbytes, enqueue, finish);
     if (r) {
-        for (int k = 0; k < n; k++) zw_bytes_free(&outs[k]);
+        if (outs)
+            for (int k = 0; k < n; k++) zw_bytes_free(&outs[k]);
         return r;
     }
     for (int i = 0; i < n; i++) {
@@ -863,6 +885,21 @@ extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const*
         if (heights) heights[i] = (uint32_t)h;
     }
     return ZW_OK;
+}
+
+extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int bpp,
+                                       int upsampling, zw_bytes* outs, uint32_t* widths, uint32_t* heights)
+{
+    if (!outs) return ZW_EINVAL;
+    return dec_rgb_batch(ctx, n, data, lens, bpp, upsampling, outs, nullptr, nullptr, 0, widths, heights);
+}
+
+extern "C" int zw_vp8_decode_rgb_batch_into(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
+                                            int bpp, int upsampling, uint8_t* const* outs, const size_t* out_lens,
+                                            uint32_t stride_bytes, uint32_t* widths, uint32_t* heights)
+{
+    if (!outs) return ZW_EINVAL;
+    return dec_rgb_batch(ctx, n, data, lens, bpp, upsampling, nullptr, outs, out_lens, stride_bytes, widths, heights);
 }
 
 extern "C" int zw_vp8_decode_rgb(zw_ctx* ctx, const uint8_t* vp8, size_t len, int bpp, int upsampling, zw_bytes* out,
@@ -1038,6 +1075,28 @@ extern "C" int zw_webp_parse(const uint8_t* data, size_t len, zw_webp_info* info
         return ZW_ECHUNK_HEADER;
     }
     if (info->vp8_offset + info->vp8_len > len) return ZW_EBITSTREAM;
+    return ZW_OK;
+}
+
+// decode_rgba_into / decode_rgb_into (decoder/api.rs:1004-1128): a lossy WebP
+// file into the caller's buffer with a row stride.
+extern "C" int zw_webp_decode_into(zw_ctx* ctx, const uint8_t* data, size_t len, int bpp, int upsampling, uint8_t* out,
+                                   size_t out_len, uint32_t stride_bytes, uint32_t* width, uint32_t* height)
+{
+    if (!ctx || !out) return ZW_EINVAL;
+    zw_webp_info info;
+    if (int r = zw_webp_parse(data, len, &info)) return r;
+    if ((size_t)stride_bytes < (size_t)info.width * bpp || out_len < (size_t)stride_bytes * info.height)
+        return ZW_EINVAL;  // InvalidParameter: stride / output buffer too small
+    const uint8_t* d[1] = {data + info.vp8_offset};
+    const size_t l[1] = {(size_t)info.vp8_len};
+    uint8_t* o[1] = {out};
+    const size_t ol[1] = {out_len};
+    uint32_t w = 0, h = 0;
+    if (int r = dec_rgb_batch(ctx, 1, d, l, bpp, upsampling, nullptr, o, ol, stride_bytes, &w, &h)) return r;
+    if (w != info.width || h != info.height) return ZW_EINCONSISTENT_SIZES;
+    if (width) *width = w;
+    if (height) *height = h;
     return ZW_OK;
 }
 

@@ -200,6 +200,9 @@ struct AnalysisTile {
     uint8_t corner[4];     // Y, U, V
 };
 
+#ifndef ZW_AN_MPW
+#define ZW_AN_MPW 8
+#endif
 extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
                                                              const uint8_t* __restrict__ V, int mbw, int mbh,
                                                              size_t ysz, size_t csz, uint8_t* __restrict__ alpha,
@@ -207,49 +210,75 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
 {
     __shared__ uint32_t hist[4][4][32];  // [wave][histogram][bin]
     __shared__ AnalysisTile tile[4];
+    __shared__ uint32_t ahist[256];      // the workgroup's share of the frame's alpha histogram
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    const int mb = blockIdx.x * 4 + wv;
     const int nmb = mbw * mbh;
-    for (int i = lane; i < 128; i += 64) (&hist[wv][0][0])[i] = 0;
+    ahist[threadIdx.x] = 0;
+    __syncthreads();
+    const int ys = mbw * 16, cs = mbw * 8;
+    const uint8_t* Yf = Y + (size_t)f * ysz;
+    const uint8_t* Uf = U + (size_t)f * csz;
+    const uint8_t* Vf = V + (size_t)f * csz;
+    // This lane's share of an MB and its edges (coalesced u32 loads): y = one
+    // luma word; x = a chroma word (lanes < 32), the top row (32..39) or a left
+    // pixel (40..63); x2 = the V left pixel (56..63); corner (lanes < 3).
+    struct AnFetch {
+        uint32_t y, x;
+        uint8_t x2, corner;
+    };
+    auto fetch = [&](int mb) {
+        AnFetch r = {0u, 0u, 0, 0};
+        if (mb >= nmb) return r;
+        const int mbx = mb % mbw, mby = mb / mbw;
+        const bool ht = mby > 0, hl = mbx > 0;
+        r.y = ((const uint32_t*)(Yf + (size_t)(mby * 16 + (lane >> 2)) * ys + mbx * 16))[lane & 3];
+        if (lane < 32) {
+            const int pl = lane >> 4, rr = (lane >> 1) & 7, w = lane & 1;
+            r.x = ((const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + rr) * cs + mbx * 8))[w];
+        } else if (lane < 36) {
+            r.x = ht ? ((const uint32_t*)(Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16))[lane - 32] : 0u;
+        } else if (lane < 40) {
+            const int pl = (lane - 36) >> 1, w = lane & 1;
+            r.x = ht ? ((const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 1) * cs + mbx * 8))[w] : 0u;
+        } else if (lane < 56) {
+            r.x = hl ? Yf[(size_t)(mby * 16 + lane - 40) * ys + mbx * 16 - 1] : 0u;
+        } else {
+            const int rr = lane - 56;  // 0..7: U and V left columns
+            r.x = hl ? Uf[(size_t)(mby * 8 + rr) * cs + mbx * 8 - 1] : 0u;
+            r.x2 = hl ? Vf[(size_t)(mby * 8 + rr) * cs + mbx * 8 - 1] : (uint8_t)0;
+        }
+        if (lane < 3) {
+            const uint8_t* P = lane == 0 ? Yf : (lane == 1 ? Uf : Vf);
+            const int st = lane == 0 ? ys : cs, sz = lane == 0 ? 16 : 8;
+            r.corner = (ht && hl) ? P[(size_t)(mby * sz - 1) * st + mbx * sz - 1] : (uint8_t)0;
+        }
+        return r;
+    };
+    // ZW_AN_MPW MBs per wave, the workgroup's 4 waves on adjacent MBs; each
+    // MB's loads are issued one MB ahead
+    AnFetch nx = fetch(blockIdx.x * ZW_AN_MPW * 4 + wv);
+    for (int k = 0; k < ZW_AN_MPW; k++) {
+    const int mb = (blockIdx.x * ZW_AN_MPW + k) * 4 + wv;
+    const AnFetch cur = nx;
+    if (k + 1 < ZW_AN_MPW) nx = fetch(mb + 4);
     wsync();
     if (mb < nmb) {
         const int mbx = mb % mbw, mby = mb / mbw;
-        const int ys = mbw * 16, cs = mbw * 8;
-        const uint8_t* Yf = Y + (size_t)f * ysz;
-        const uint8_t* Uf = U + (size_t)f * csz;
-        const uint8_t* Vf = V + (size_t)f * csz;
-        // ---- stage the MB and its edges in LDS (coalesced u32 loads) ----
+        // ---- stage the MB and its edges in LDS ----
         // tiles: [plane][row][col] with interior rows 0..15 / 0..7, top row, left column, corner
         AnalysisTile* A = &tile[wv];
         const bool ht = mby > 0, hl = mbx > 0;
-        {
-            const uint32_t* y32 = (const uint32_t*)(Yf + (size_t)(mby * 16 + (lane >> 2)) * ys + mbx * 16);
-            A->y[lane >> 2][lane & 3] = y32[lane & 3];
-            if (lane < 32) {
-                const int pl = lane >> 4, r = (lane >> 1) & 7, w = lane & 1;
-                const uint8_t* P = pl ? Vf : Uf;
-                A->c[pl][r][w] = ((const uint32_t*)(P + (size_t)(mby * 8 + r) * cs + mbx * 8))[w];
-            } else if (lane < 36) {
-                A->ytop[lane - 32] = ht ? ((const uint32_t*)(Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16))[lane - 32] : 0u;
-            } else if (lane < 40) {
-                const int pl = (lane - 36) >> 1, w = lane & 1;
-                const uint8_t* P = pl ? Vf : Uf;
-                A->ctop[pl][w] = ht ? ((const uint32_t*)(P + (size_t)(mby * 8 - 1) * cs + mbx * 8))[w] : 0u;
-            } else if (lane < 56) {
-                const int r = lane - 40;
-                A->yleft[r] = hl ? Yf[(size_t)(mby * 16 + r) * ys + mbx * 16 - 1] : (uint8_t)0;
-            } else {
-                const int r = lane - 56;  // 0..7: U and V left columns
-                A->cleft[0][r] = hl ? Uf[(size_t)(mby * 8 + r) * cs + mbx * 8 - 1] : (uint8_t)0;
-                A->cleft[1][r] = hl ? Vf[(size_t)(mby * 8 + r) * cs + mbx * 8 - 1] : (uint8_t)0;
-            }
-            if (lane < 3) {
-                const uint8_t* P = lane == 0 ? Yf : (lane == 1 ? Uf : Vf);
-                const int st = lane == 0 ? ys : cs, sz = lane == 0 ? 16 : 8;
-                A->corner[lane] = (ht && hl) ? P[(size_t)(mby * sz - 1) * st + mbx * sz - 1] : (uint8_t)0;
-            }
+        A->y[lane >> 2][lane & 3] = cur.y;
+        if (lane < 32) A->c[lane >> 4][(lane >> 1) & 7][lane & 1] = cur.x;
+        else if (lane < 36) A->ytop[lane - 32] = cur.x;
+        else if (lane < 40) A->ctop[(lane - 36) >> 1][lane & 1] = cur.x;
+        else if (lane < 56) A->yleft[lane - 40] = (uint8_t)cur.x;
+        else {
+            A->cleft[0][lane - 56] = (uint8_t)cur.x;
+            A->cleft[1][lane - 56] = cur.x2;
         }
+        if (lane < 3) A->corner[lane] = cur.corner;
         wsync();
         uint8_t bins[16];
         uint32_t z = 0;
@@ -334,6 +363,8 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
         if (slow) {
             // bin 0 holds most coefficients: count it in the lane, add the rest
             // with (far less contended) LDS atomics
+            for (int i = lane; i < 128; i += 64) (&hist[wv][0][0])[i] = 0;
+            wsync();
             if (lane < 48) {
 #pragma unroll
                 for (int k = 0; k < 16; k++)
@@ -373,9 +404,13 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
             al = 255 - al;
             al = al < 0 ? 0 : (al > 255 ? 255 : al);
             alpha[(size_t)f * nmb + mb] = (uint8_t)al;
-            atomicAdd(&histo[(size_t)f * 256 + al], 1u);
+            atomicAdd(&ahist[al], 1u);
         }
     }
+    }
+    __syncthreads();
+    const uint32_t c = ahist[threadIdx.x];
+    if (c) atomicAdd(&histo[(size_t)f * 256 + threadIdx.x], c);
 }
 
 // ---------------------------------------------------------------------------
@@ -2937,7 +2972,8 @@ extern "C" hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_
                                    int mbh, size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes)
 {
     const int nmb = mbw * mbh;
-    hipLaunchKernelGGL(k_analysis, dim3((nmb + 3) / 4, nframes), dim3(256), 0, s, Y, U, V, mbw, mbh, ysz, csz, alpha,
+    hipLaunchKernelGGL(k_analysis, dim3((nmb + 4 * ZW_AN_MPW - 1) / (4 * ZW_AN_MPW), nframes), dim3(256), 0, s, Y, U, V,
+                       mbw, mbh, ysz, csz, alpha,
                        histo);
     return hipGetLastError();
 }

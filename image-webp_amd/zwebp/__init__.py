@@ -34,6 +34,7 @@ __all__ = [
     "Frame", "Pipeline", "encode_frame_lossy", "encode_batch", "vp8_decode_frame", "decode_batch",
     "rgb_to_yuv420", "loop_filter_frame", "quant_blocks", "transform_quant_blocks", "library_path", "load_library",
     "UpsamplingMethod", "WebPDecoder", "decode_rgb", "decode_rgba", "vp8_decode_rgb", "decode_rgb_batch",
+    "decode_rgb_batch_into", "decode_rgba_into", "decode_rgb_into",
     "yuv_to_rgb", "webp_parse", "encode_frame_lossless", "encode_alpha",
 ]
 
@@ -133,7 +134,11 @@ SIGNATURES = [
                                ctypes.POINTER(_U32)]),
     ("zw_vp8_decode_rgb_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _I,
                                      ctypes.POINTER(_Bytes), _VP, _VP]),
+    ("zw_vp8_decode_rgb_batch_into", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _I,
+                                          ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _U32, _VP, _VP]),
     ("zw_webp_parse", _I, [_VP, _SZ, ctypes.POINTER(_WebpInfo)]),
+    ("zw_webp_decode_into", _I, [_VP, _VP, _SZ, _I, _I, _VP, _SZ, _U32, ctypes.POINTER(_U32),
+                                 ctypes.POINTER(_U32)]),
     ("zw_webp_decode", _I, [_VP, _VP, _SZ, _I, _I, ctypes.POINTER(_Bytes), ctypes.POINTER(_U32),
                             ctypes.POINTER(_U32)]),
     ("zw_decode_rgb_kernel_ms", _I, [_VP, ctypes.POINTER(ctypes.c_float)]),
@@ -480,6 +485,66 @@ def decode_rgb_batch(frames, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=No
     _check(L.zw_vp8_decode_rgb_batch(c.handle, n, ptrs, lens, bpp, upsampling, outs, ws, hs), "decode_rgb_batch",
            DecodingError)
     return [_take_image(L, outs[i], ws[i], hs[i], bpp) for i in range(n)]
+
+
+def _writable_u8(buf):
+    a = np.asarray(buf)
+    if a.dtype != np.uint8 or not a.flags.c_contiguous or not a.flags.writeable:
+        raise ValueError("output must be a writable C-contiguous uint8 buffer")
+    return a
+
+
+def decode_rgb_batch_into(frames, outs, bpp=3, upsampling=UpsamplingMethod.Bilinear, stride_bytes=None, ctx=None):
+    """decode_rgb_batch into the caller's buffers (decode_rgba_into / decode_rgb_into,
+    decoder/api.rs:1004-1128): outs[i] is a writable uint8 array of at least
+    stride * height bytes, rows stride_bytes (default width * bpp) apart.
+    Returns [(width, height)] per frame."""
+    c = _ctx(ctx)
+    L = c._lib
+    arrs = [_as_u8(d) for d in frames]
+    dst = [_writable_u8(o) for o in outs]
+    n = len(arrs)
+    if len(dst) != n or n == 0:
+        raise ValueError("one output buffer per frame")
+    if stride_bytes is None:
+        w0 = webp_frame_width(arrs[0])
+        stride_bytes = w0 * bpp
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    lens = (ctypes.c_size_t * n)(*[a.size for a in arrs])
+    optr = (ctypes.c_void_p * n)(*[o.ctypes.data for o in dst])
+    olen = (ctypes.c_size_t * n)(*[o.nbytes for o in dst])
+    ws, hs = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+    _check(L.zw_vp8_decode_rgb_batch_into(c.handle, n, ptrs, lens, bpp, upsampling, optr, olen, int(stride_bytes),
+                                          ws, hs), "decode_rgb_batch_into", DecodingError)
+    return [(ws[i], hs[i]) for i in range(n)]
+
+
+def webp_frame_width(vp8):
+    """Width field of a VP8 key-frame header (frame tag + start code + 14-bit width);
+    0 for a frame too short to hold one (the decode then reports the error)."""
+    a = _as_u8(vp8)
+    return int(a[6]) | ((int(a[7]) & 0x3F) << 8) if a.size >= 10 else 0
+
+
+def _decode_into(data, output, stride_bytes, bpp, ctx):
+    c = _ctx(ctx)
+    a = _as_u8(data)
+    o = _writable_u8(output)
+    w, h = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(c._lib.zw_webp_decode_into(c.handle, _ptr(a) if a.size else None, a.size, bpp, UpsamplingMethod.Bilinear,
+                                      o.ctypes.data, o.nbytes, int(stride_bytes), ctypes.byref(w), ctypes.byref(h)),
+           "decode_into", DecodingError)
+    return w.value, h.value
+
+
+def decode_rgba_into(data, output, stride_bytes, ctx=None):
+    """decode_rgba_into (decoder/api.rs:1004): decode into `output` with row stride; (width, height)."""
+    return _decode_into(data, output, stride_bytes, 4, ctx)
+
+
+def decode_rgb_into(data, output, stride_bytes, ctx=None):
+    """decode_rgb_into (decoder/api.rs:1067): decode into `output` with row stride; (width, height)."""
+    return _decode_into(data, output, stride_bytes, 3, ctx)
 
 
 def decode_rgb_kernel_ms(ctx=None):

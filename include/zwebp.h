@@ -16,6 +16,7 @@
  *   zw_vp8_decode_rgb       decode_frame + Frame::fill_rgb/fill_rgba  src/decoder/vp8.rs:200-258
  *   zw_webp_parse           WebPDecoder::new (read_data)  src/decoder/api.rs:334-510
  *   zw_webp_decode          decode_rgb / decode_rgba   src/decoder/api.rs:938-993
+ *   zw_webp_decode_into     decode_rgb_into / decode_rgba_into  src/decoder/api.rs:1004-1128
  *   zw_yuv_to_rgb           fill_rgb_buffer_fancy/_simple  src/decoder/yuv.rs:82 / :402
  *   zw_rgb_to_yuv420        convert_image_yuv/_y      src/decoder/yuv.rs:656 / :806
  *   zw_loop_filter_frame    filter_row_in_cache       src/decoder/vp8.rs:1172-1345
@@ -168,6 +169,13 @@ int zw_vp8_decode_rgb(zw_ctx *ctx, const uint8_t *vp8, size_t len, int bpp, int 
 /* n frames of identical dimensions (new: batch); widths/heights may be NULL. */
 int zw_vp8_decode_rgb_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, int bpp,
                             int upsampling, zw_bytes *outs, uint32_t *widths, uint32_t *heights);
+/* The same into the caller's buffers (decode_rgba_into / decode_rgb_into,
+ * decoder/api.rs:1004-1128, batched): outs[i] holds out_lens[i] >= stride_bytes
+ * * height bytes, rows stride_bytes >= width * bpp apart; ZW_EINVAL otherwise
+ * (the reference's InvalidParameter). */
+int zw_vp8_decode_rgb_batch_into(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, int bpp,
+                                 int upsampling, uint8_t *const *outs, const size_t *out_lens, uint32_t stride_bytes,
+                                 uint32_t *widths, uint32_t *heights);
 /* WebPDecoder::new (container parse, no decoding; lossy subset: ALPH, VP8L and
  * animation return ZW_EUNSUPPORTED with info filled as far as parsed). */
 int zw_webp_parse(const uint8_t *data, size_t len, zw_webp_info *info);
@@ -175,6 +183,10 @@ int zw_webp_parse(const uint8_t *data, size_t len, zw_webp_info *info);
  * WebP file; WebPDecoder::set_lossy_upsampling via `upsampling`. */
 int zw_webp_decode(zw_ctx *ctx, const uint8_t *data, size_t len, int bpp, int upsampling, zw_bytes *out,
                    uint32_t *width, uint32_t *height);
+/* decode_rgba_into (bpp 4) / decode_rgb_into (bpp 3) (decoder/api.rs:1004-1128)
+ * of a lossy WebP file into out (out_len >= stride_bytes * height bytes). */
+int zw_webp_decode_into(zw_ctx *ctx, const uint8_t *data, size_t len, int bpp, int upsampling, uint8_t *out,
+                        size_t out_len, uint32_t stride_bytes, uint32_t *width, uint32_t *height);
 /* Device time (HIP events on the context stream) of the last decode batch:
  * ms[0] = k_dec_recon (dequant + iWHT/iDCT + prediction), ms[1] = k_loopfilter. */
 int zw_decode_kernel_times(zw_ctx *ctx, float *ms);

@@ -129,6 +129,52 @@ def test_decode_rgb_batch(ctx, monkeypatch, chunk):
         assert np.array_equal(img.reshape(-1), _oracle_rgb(r["y"], r["u"], r["v"], w, h, 4, BIL))
 
 
+@pytest.mark.parametrize("bpp,pad", [(3, 0), (4, 0), (3, 13), (4, 64)])
+@pytest.mark.parametrize("chunk", [None, "2"])
+def test_decode_rgb_batch_into(ctx, monkeypatch, bpp, pad, chunk):
+    """decode_rgba_into / decode_rgb_into semantics (api.rs:1004-1128), batched:
+    the caller's buffers with a row stride; the padding bytes stay untouched."""
+    if chunk:
+        monkeypatch.setenv("ZW_DEC_CHUNK", chunk)
+    w, h = 161, 97
+    streams = [O.encode(synth_rgba(w, h, 0x5EED0200 + i), w, h, 3, 30 + 10 * i, 4)[1] for i in range(5)]
+    stride = w * bpp + pad
+    outs = [np.full(stride * h + 7, 0xA5, np.uint8) for _ in streams]
+    dims = zwebp.decode_rgb_batch_into(streams, outs, bpp, BIL, stride_bytes=stride, ctx=ctx)
+    assert dims == [(w, h)] * len(streams)
+    for s, o in zip(streams, outs):
+        rc, r = O.decode(s)
+        rows = o[:stride * h].reshape(h, stride)
+        exp = _oracle_rgb(r["y"], r["u"], r["v"], w, h, bpp, BIL).reshape(h, w * bpp)
+        assert np.array_equal(rows[:, :w * bpp], exp)
+        assert np.all(rows[:, w * bpp:] == 0xA5) and np.all(o[stride * h:] == 0xA5)
+
+
+def test_decode_rgb_into_errors(ctx):
+    vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
+    out = np.zeros(64 * 48 * 4, np.uint8)
+    with pytest.raises(zwebp.DecodingError) as e:  # stride below width * bpp
+        zwebp.decode_rgb_batch_into([vp8], [out], 4, BIL, stride_bytes=64 * 4 - 1, ctx=ctx)
+    assert e.value.code == 3
+    with pytest.raises(zwebp.DecodingError) as e:  # buffer below stride * height
+        zwebp.decode_rgb_batch_into([vp8], [out[:-1]], 4, BIL, ctx=ctx)
+    assert e.value.code == 3
+    with pytest.raises(zwebp.DecodingError):
+        zwebp.decode_rgba_into(_riff(vp8), out, 64 * 4 + 1, ctx=ctx)  # needs stride * height > buffer
+
+
+def test_decode_rgba_into_container(ctx):
+    """decode_rgba_into / decode_rgb_into of a lossy RIFF file == decode_rgba / decode_rgb."""
+    vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
+    riff = _riff(vp8)
+    for fn_into, fn, bpp in ((zwebp.decode_rgba_into, zwebp.decode_rgba, 4), (zwebp.decode_rgb_into, zwebp.decode_rgb, 3)):
+        stride = 64 * bpp + 8
+        out = np.zeros(stride * 48, np.uint8)
+        assert fn_into(riff, out, stride, ctx=ctx) == (64, 48)
+        flat, w, h = fn(riff, ctx=ctx)
+        assert np.array_equal(out.reshape(48, stride)[:, :64 * bpp].reshape(-1), flat)
+
+
 def test_encode_decode_rgb_roundtrip(ctx):
     """Our encoder -> RIFF -> our RGB decoder == oracle decode + oracle upsampling."""
     w, h = 333, 211

@@ -16,7 +16,10 @@ ctx = zwebp.Context(0)
 imgs = [synth_rgba(w, h, 0x5EED0000 + i) for i in range(4)]
 streams = zwebp.encode_batch(imgs, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
 vp8 = [streams[i % 4] for i in range(F)]
-for name, fn in (("yuv", lambda: zwebp.decode_batch(vp8, ctx=ctx)),
+import numpy as np  # noqa: E402
+bufs = [np.empty(w * h * 4, np.uint8) for _ in range(F)]
+for name, fn in (("rgba_into", lambda: zwebp.decode_rgb_batch_into(vp8, bufs, 4, ctx=ctx)),
+                 ("yuv", lambda: zwebp.decode_batch(vp8, ctx=ctx)),
                  ("rgba", lambda: zwebp.decode_rgb_batch(vp8, bpp=4, ctx=ctx)),
                  ("rgb", lambda: zwebp.decode_rgb_batch(vp8, bpp=3, ctx=ctx))):
     fn()
