@@ -1312,6 +1312,247 @@ DI void i4_lane_init(const Ctx& C, I4Lane& L)
     L.tm = mv == 1;
 }
 
+// The quad's row-transform inputs broadcast to every lane: lane q forms
+// column q of the row stage (dct4x4 transform.rs:176) for rows 0..3, then the
+// column stage: c[r] = coefficient (r, q), natural index 4 r + q.
+DI void uvq_fdct(uint32_t A, uint32_t D, int q, int c[4])
+{
+    const bool odd = q & 1;
+    const zs2 k0 = {8, 8}, k2 = {8, -8}, k1 = {10704, 4434}, k3 = {4434, -10704};
+    const uint32_t k = q == 0 ? as_zu(k0) : (q == 1 ? as_zu(k1) : (q == 2 ? as_zu(k2) : as_zu(k3)));
+    const int rnd = q == 1 ? 3625 : (q == 3 ? 1875 : 0);
+    const int sh = odd ? 10 : 0;
+    // (csel, not ?: -- a select of two DPP results may be folded into one DPP
+    // of a select, which would take the source lane's choice)
+    int t[4];
+    t[0] = dot2v((uint32_t)csel(odd, qb0((int)D), qb0((int)A)), k, rnd) >> sh;
+    t[1] = dot2v((uint32_t)csel(odd, qb1((int)D), qb1((int)A)), k, rnd) >> sh;
+    t[2] = dot2v((uint32_t)csel(odd, qb2((int)D), qb2((int)A)), k, rnd) >> sh;
+    t[3] = dot2v((uint32_t)csel(odd, qb3((int)D), qb3((int)A)), k, rnd) >> sh;
+    const uint32_t X01 = pack_lo(t[0], t[1]), X32 = pack_lo(t[3], t[2]);
+    const zs2 XA = as_zs2(X01) + as_zs2(X32), XD = as_zs2(X01) - as_zs2(X32);
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+    c[0] = dot2(XA, k1p, 7) >> 4;
+    c[2] = dot2(XA, k1m, 7) >> 4;
+    c[1] = (dot2(XD, k2a, 12000) >> 16) + ((as_zu(XD) & 0xffffu) != 0u ? 1 : 0);
+    c[3] = dot2(XD, k2b, 51000) >> 16;
+}
+
+// idct4x4 (transform.rs:19) of the quad's dequantised columns (lane q holds
+// column q, rows 0..3), then the reconstruction clamp(pred + residual) of row q
+// as i16 pairs (x0, x1), (x3, x2).
+DI void uvq_idct_recon(const int dq[4], uint32_t p01, uint32_t p32, int q, uint32_t& r01, uint32_t& r32)
+{
+    uint32_t lo, hi;
+    {
+        const int x0 = dq[0], x1 = dq[1], x2 = dq[2], x3 = dq[3];
+        const int a1 = x0 + x2, b1 = x0 - x2;
+        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
+        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
+        lo = pack_lo(a1 + d1, b1 + c1);
+        hi = pack_lo(b1 - c1, a1 - d1);
+    }
+    // row q of every column: the lane of column j holds it in lo (rows 0, 1) or hi (rows 2, 3)
+    const bool upper = q >= 2;
+    const uint32_t off = 16u * (uint32_t)(q & 1);
+    const int y0 = __builtin_amdgcn_sbfe(csel(upper, qb0((int)hi), qb0((int)lo)), off, 16);
+    const int y1 = __builtin_amdgcn_sbfe(csel(upper, qb1((int)hi), qb1((int)lo)), off, 16);
+    const int y2 = __builtin_amdgcn_sbfe(csel(upper, qb2((int)hi), qb2((int)lo)), off, 16);
+    const int y3 = __builtin_amdgcn_sbfe(csel(upper, qb3((int)hi), qb3((int)lo)), off, 16);
+    const int a1 = y0 + y2, b1 = y0 - y2;
+    const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
+    const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
+    const int o0 = (a1 + d1 + 4) >> 3, o1 = (b1 + c1 + 4) >> 3, o2 = (b1 - c1 + 4) >> 3, o3 = (a1 - d1 + 4) >> 3;
+    r01 = clamp_pk(add_pk(pack_lo(o0, o1), p01));
+    r32 = clamp_pk(add_pk(pack_lo(o3, o2), p32));
+}
+
+DI int quad_or(int v)
+{
+    v |= DPP(v, 0xB1);
+    return v | DPP(v, 0x4E);
+}
+DI int quad_sum(int v)
+{
+    v += DPP(v, 0xB1);
+    return v + DPP(v, 0x4E);
+}
+
+// get_residual_cost (cost.rs:1670, quirk A1) of a quad's block, first position
+// 0: lane q holds column q, av[r] = |level| at natural index n = 4 r + q.
+// Uniform in the quad.  LC = false: pass 1 (zero LevelCosts, quirk A2).
+template <bool LC>
+DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* T, int& last_o)
+{
+    unsigned nz = 0, big = 0, sc = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int n = 4 * r + q;
+        nz |= (unsigned)min(av[r], 1) << n;
+        big |= (unsigned)(av[r] >= 2) << n;
+        sc |= (unsigned)min(av[r], 2) << (2 * r);
+    }
+    nz = (unsigned)quad_or((int)nz);
+    big = (unsigned)quad_or((int)big);
+    const int last = 31 - __clz((int)nz);
+    last_o = last;
+    int part = 0;
+    if (LC) {
+        // the context of position n is min(|level[n - 1]|, 2): lane q - 1 of the
+        // same row, for q = 0 lane 3 of the row above (ctx0 at n = 0)
+        const unsigned pv = (unsigned)DPP((int)sc, 0x93);  // quad_perm [3, 0, 1, 2]
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int n = 4 * r + q;
+            const int c_same = (int)((pv >> (2 * r)) & 3u);
+            const int c_q0 = r == 0 ? ctx0 : (int)((pv >> (2 * r - 2)) & 3u);
+            const int ctx = csel(q == 0, c_q0, c_same);
+            const int a = av[r];
+            const int tl = T->lfc[min(a, 2047)] + T->lc[ctype][band_of(n)][ctx][min(a, 67)];
+            part += tl & -(int)(n <= last);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) part += T->lfc[min(av[r], 2047)];
+    }
+    const int sum = quad_sum(part);
+    const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
+    const int tail = (int)T->beob[ctype][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
+    const int head = (int)T->binit[ctype][0][ctx0] & -(int)(ctx0 == 0);
+    return last < 0 ? (int)T->beob[ctype][0][ctx0] : head + sum + tail;
+}
+
+// Candidate evaluation of an I4 step in quad form (K <= 4: methods 0-4).  The
+// step's candidate set -- the K modes of smallest prediction SSE per block,
+// `rank` from the pair layout -- is evaluated with four lanes per (block,
+// candidate): lane = 16 slot + 4 k + q, q = pixel row / coefficient column,
+// k = the candidate's rank.  A lane does a quarter of a block's arithmetic
+// (the quad transforms of the chroma chain), and only the K candidates are
+// transformed instead of all ten modes.  The winner is the smallest (score,
+// rank) of each slot's row: the reference's first strict minimum over its
+// candidates in SSE order.
+template <int PASS, int NB>
+DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0, const int* y0, const int* tctx,
+                     const int* lctx, const int* nzc, int K, int rank, uint32_t vp, uint32_t ap01, uint32_t ap32,
+                     I4State& st, bool keep)
+{
+    PH_START();
+    WaveLds* W = C.W;
+    const ZwSegment& S = *C.S;
+    const LdsTables* T = C.T;
+    const int l = C.lane, m = l & 15, hf = l >> 5;
+    // candidate modes: k-th of each slot from the pair layout's ranks (lane
+    // 16 slot + mode of the lower half), four bits each, slot 1 at bit 16
+    uint32_t modes = 0;
+    for (int k = 0; k < K; k++) {
+        const unsigned long long b = __ballot(hf == 0 && m < 10 && rank == k);
+        const uint32_t lo = (uint32_t)b & 0xffffu, hi = ((uint32_t)b >> 16) & 0xffffu;
+        modes |= (uint32_t)__builtin_ctz(lo | 0x10000u) << (4 * k);
+        if (NB == 2) modes |= (uint32_t)__builtin_ctz(hi | 0x10000u) << (16 + 4 * k);
+    }
+    const int slot = NB == 2 ? (l >> 4) & 1 : 0, k = (l >> 2) & 3, q = l & 3;
+    const int mq = (int)((modes >> (16 * slot + 4 * k)) & 15u);
+    const int mv = k < K ? mq : 0;  // (k >= K: a valid mode, never eligible)
+    const int sl = NB == 2 ? 1 : 0;
+    const int bx = csel(slot, sbx[sl], sbx[0]), by = csel(slot, sby[sl], sby[0]);
+    const int ctx0 = csel(slot, nzc[sl], nzc[0]);
+    const int mcost = T->fci4[csel(slot, tctx[sl], tctx[0])][csel(slot, lctx[sl], lctx[0])][mv];
+    // prediction of row q: V indices of its four pixels (254: TrueMotion,
+    // V[3 - q] + the top offsets; 255: the DC entry V[38])
+    uint32_t p01, p32;
+    {
+        const uint32_t iw = *(const uint32_t*)&T->i4idx[mv][4 * q];
+        const uint32_t psel = (l & 16) ? 0x0c060c02u : 0x0c040c00u;
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = (int)((iw >> (8 * j)) & 255u);
+            const int sidx = csel(idx == 254, 3 - q, csel(idx == 255, 38, idx));
+            v[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(sidx << 2, (int)vp);
+        }
+        const uint32_t q01 = __builtin_amdgcn_perm(v[1], v[0], psel), q32 = __builtin_amdgcn_perm(v[2], v[3], psel);
+        const bool tm = mv == 1;
+        p01 = tm ? clamp_pk(add_pk(q01, ap01)) : q01;
+        p32 = tm ? clamp_pk(add_pk(q32, ap32)) : q32;
+    }
+    uint32_t s01, s32;
+    {
+        const uint32_t sw = *(const uint32_t*)(C.sY + (by * 4 + q) * 16 + bx * 4);
+        s01 = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
+        s32 = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
+    }
+    const uint32_t R01 = sub_pk(s01, p01), R32 = sub_pk(s32, p32);
+    int cf[4];
+    uvq_fdct(add_pk(R01, R32), sub_pk(R01, R32), q, cf);
+    int av[4], dq[4], lv[4];
+    {
+        const uint32_t iq0 = q ? S.y1.iq[1] : S.y1.iq[0], bs0 = q ? S.y1.bias[1] : S.y1.bias[0];
+        const int q0 = q ? (int)S.y1.q[1] : (int)S.y1.q[0];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool dcs = r == 0;  // (0, q): the DC for q = 0
+            const int v = cf[r];
+            const int a = (int)((__umul24((uint32_t)iabs(v), dcs ? iq0 : S.y1.iq[1]) + (dcs ? bs0 : S.y1.bias[1])) >> 17);
+            av[r] = a;
+            lv[r] = v < 0 ? -a : a;
+            dq[r] = m24(lv[r], dcs ? q0 : (int)S.y1.q[1]);
+        }
+    }
+    int last;
+    const int cost = rcost_quad<PASS == 2>(av, q, ctx0, 3, T, last);  // get_cost_luma4 (ctype 3, first 0)
+    uint32_t r01, r32;
+    uvq_idct_recon(dq, p01, p32, q, r01, r32);
+    int sse = 0;
+    {
+        const uint32_t d01 = sub_pk(s01, r01), d32 = sub_pk(s32, r32);
+        sse = dot2v(d01, d01, sse);
+        sse = dot2v(d32, d32, sse);
+    }
+    sse = quad_sum(sse);
+    const uint32_t rate = (uint32_t)(mcost + cost);
+    // rd_score (cost.rs): sse * 256 + u16(rate) * lambda_i4 < 2^29
+    const uint32_t score = (uint32_t)sse * 256u + (rate & 0xffffu) * S.l_i4;
+    const uint32_t key2 = k < K ? (score << 2) | (uint32_t)k : 0xffffffffu;
+    const uint32_t kmin = min16u(key2);
+    const unsigned long long win = __ballot(key2 == kmin);
+    PH_MARK_L(12, l, 0);
+    int bk[NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        bk[h] = __builtin_ctz((uint32_t)(win >> (16 * h)) & 0xffffu) >> 2;
+        const int bmode = (int)((modes >> (16 * h + 4 * bk[h])) & 15u);
+        const int wl = 16 * h + 4 * bk[h];
+        const uint32_t bsse = (uint32_t)__builtin_amdgcn_readlane(sse, wl);
+        const uint32_t brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, wl);
+        const int bnz = __builtin_amdgcn_readlane((int)(last >= 0), wl);
+        const int i = sby[h] * 4 + sbx[h];
+        st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
+        st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
+        st.nzm |= (uint32_t)bnz << i;
+        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode];
+        st.running += rdscore(bsse, brate, S.l_mode);
+        st.mpack |= (unsigned long long)bmode << (4 * i);
+        if (l == h) W->modes[i] = (uint8_t)bmode;
+    }
+    // the winners' quads write their rows of the reconstruction (and, when the
+    // final pass reuses them, their columns of levels in zigzag order)
+    const int bks = csel(slot, bk[sl], bk[0]);
+    if (k == bks && l < 16 * NB) {
+        const int xo = csel(slot, x0[sl], x0[0]), yo = csel(slot, y0[sl], y0[0]);
+        const uint32_t wd = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
+        uint8_t* p = W->ws + (yo + q) * ZW_BPS + xo;
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[j] = (uint8_t)(wd >> (8 * j));
+        if (keep) {
+            int16_t* lvp = W->lev[by * 4 + bx];
+#pragma unroll
+            for (int r = 0; r < 4; r++) lvp[izz_of(4 * r + q)] = (int16_t)lv[r];
+        }
+    }
+    wsync();
+    PH_MARK_L(13, l, 0);
+}
+
 template <int PASS, int NB>
 __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, const I4Lane& LC,
                                         I4State& st, bool keep)
@@ -1392,6 +1633,13 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
     ZW_RANK_STEP(11) ZW_RANK_STEP(12) ZW_RANK_STEP(13) ZW_RANK_STEP(14) ZW_RANK_STEP(15)
 #undef ZW_RANK_STEP
     PH_MARK_L(11, l, 0);
+#ifndef ZW_I4_QUAD
+#define ZW_I4_QUAD 1
+#endif
+    if (ZW_I4_QUAD && K <= 4) {
+        i4_cand_quad<PASS, NB>(C, sbx, sby, x0, y0, tctx, lctx, nzc, K, rank, vp, ap01, ap32, st, keep);
+        return;
+    }
     // transform, quantiser, rate, reconstruction and distortion of every
     // (block, mode): natural coefficient index n = 4 row + 2 hf + col, the DC
     // (n = 0) in the lower half's column 0
@@ -1926,72 +2174,6 @@ DI void uvq_border(const Ctx& C, const UvQ& U)
         else U.w[(l - 8) * ZW_BPS] = C.mbx == 0 ? 129 : U.left[l - 8];
     }
     wsync();
-}
-
-// The quad's row-transform inputs broadcast to every lane: lane q forms
-// column q of the row stage (dct4x4 transform.rs:176) for rows 0..3, then the
-// column stage: c[r] = coefficient (r, q), natural index 4 r + q.
-DI void uvq_fdct(uint32_t A, uint32_t D, int q, int c[4])
-{
-    const bool odd = q & 1;
-    const zs2 k0 = {8, 8}, k2 = {8, -8}, k1 = {10704, 4434}, k3 = {4434, -10704};
-    const uint32_t k = q == 0 ? as_zu(k0) : (q == 1 ? as_zu(k1) : (q == 2 ? as_zu(k2) : as_zu(k3)));
-    const int rnd = q == 1 ? 3625 : (q == 3 ? 1875 : 0);
-    const int sh = odd ? 10 : 0;
-    // (csel, not ?: -- a select of two DPP results may be folded into one DPP
-    // of a select, which would take the source lane's choice)
-    int t[4];
-    t[0] = dot2v((uint32_t)csel(odd, qb0((int)D), qb0((int)A)), k, rnd) >> sh;
-    t[1] = dot2v((uint32_t)csel(odd, qb1((int)D), qb1((int)A)), k, rnd) >> sh;
-    t[2] = dot2v((uint32_t)csel(odd, qb2((int)D), qb2((int)A)), k, rnd) >> sh;
-    t[3] = dot2v((uint32_t)csel(odd, qb3((int)D), qb3((int)A)), k, rnd) >> sh;
-    const uint32_t X01 = pack_lo(t[0], t[1]), X32 = pack_lo(t[3], t[2]);
-    const zs2 XA = as_zs2(X01) + as_zs2(X32), XD = as_zs2(X01) - as_zs2(X32);
-    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
-    c[0] = dot2(XA, k1p, 7) >> 4;
-    c[2] = dot2(XA, k1m, 7) >> 4;
-    c[1] = (dot2(XD, k2a, 12000) >> 16) + ((as_zu(XD) & 0xffffu) != 0u ? 1 : 0);
-    c[3] = dot2(XD, k2b, 51000) >> 16;
-}
-
-// idct4x4 (transform.rs:19) of the quad's dequantised columns (lane q holds
-// column q, rows 0..3), then the reconstruction clamp(pred + residual) of row q
-// as i16 pairs (x0, x1), (x3, x2).
-DI void uvq_idct_recon(const int dq[4], uint32_t p01, uint32_t p32, int q, uint32_t& r01, uint32_t& r32)
-{
-    uint32_t lo, hi;
-    {
-        const int x0 = dq[0], x1 = dq[1], x2 = dq[2], x3 = dq[3];
-        const int a1 = x0 + x2, b1 = x0 - x2;
-        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
-        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
-        lo = pack_lo(a1 + d1, b1 + c1);
-        hi = pack_lo(b1 - c1, a1 - d1);
-    }
-    // row q of every column: the lane of column j holds it in lo (rows 0, 1) or hi (rows 2, 3)
-    const bool upper = q >= 2;
-    const uint32_t off = 16u * (uint32_t)(q & 1);
-    const int y0 = __builtin_amdgcn_sbfe(csel(upper, qb0((int)hi), qb0((int)lo)), off, 16);
-    const int y1 = __builtin_amdgcn_sbfe(csel(upper, qb1((int)hi), qb1((int)lo)), off, 16);
-    const int y2 = __builtin_amdgcn_sbfe(csel(upper, qb2((int)hi), qb2((int)lo)), off, 16);
-    const int y3 = __builtin_amdgcn_sbfe(csel(upper, qb3((int)hi), qb3((int)lo)), off, 16);
-    const int a1 = y0 + y2, b1 = y0 - y2;
-    const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
-    const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
-    const int o0 = (a1 + d1 + 4) >> 3, o1 = (b1 + c1 + 4) >> 3, o2 = (b1 - c1 + 4) >> 3, o3 = (a1 - d1 + 4) >> 3;
-    r01 = clamp_pk(add_pk(pack_lo(o0, o1), p01));
-    r32 = clamp_pk(add_pk(pack_lo(o3, o2), p32));
-}
-
-DI int quad_or(int v)
-{
-    v |= DPP(v, 0xB1);
-    return v | DPP(v, 0x4E);
-}
-DI int quad_sum(int v)
-{
-    v += DPP(v, 0xB1);
-    return v + DPP(v, 0x4E);
 }
 
 // get_residual_cost (cost.rs:1670; ctype 2, first 0, ctx0 0; pass 1: the
@@ -2618,7 +2800,46 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             if (luma_rank(v) == k) w = v;
         return w;
     };
-    const int rw = ROWS ? 0 : luma_rank(wv);
+    // ZW_P1_SLOWSKIP (pass 1, batch shape): the luma waves on SIMD 0 (beside
+    // the chain) take fewer rows.  Rows go out in rounds: the nfast rows of the
+    // other SIMDs' waves, then the round's share of SIMD-0 rows (the SIMD-0
+    // waves in turn), ZW_P1_SLOW_NUM SIMD-0 rows per ZW_P1_SLOW_DEN rounds.  So
+    // SIMD 0 carries the chain plus fewer luma rows, and its rows keep pace
+    // with the rest instead of throttling every row behind them.
+#ifndef ZW_P1_SLOWSKIP
+#define ZW_P1_SLOWSKIP 1
+#endif
+#ifndef ZW_P1_SLOW_NUM
+#define ZW_P1_SLOW_NUM 4
+#endif
+#ifndef ZW_P1_SLOW_DEN
+#define ZW_P1_SLOW_DEN 3
+#endif
+    constexpr bool skip_mode = ZW_P1_SLOWSKIP && PASS == 1 && !ROWS && NCH == 1 && NW > 4;
+    constexpr int nslow = (NW - 1) / 4 > 0 ? (NW - 1) / 4 : 1;  // luma waves on SIMD 0: 4, 8, ..
+    constexpr int nfast = NW - NCH - (NW - 1) / 4;             // luma waves on SIMDs 1..3
+    auto fast_wave = [](int i) { return i + 1 + i / 3; };
+    auto wave_of_row = [&](int y) {
+        if (!skip_mode) return luma_wave(y % (nrw > 0 ? nrw : 1));
+        constexpr int L = ZW_P1_SLOW_DEN * nfast + ZW_P1_SLOW_NUM;
+        int r = y % L, before = (y / L) * ZW_P1_SLOW_NUM;
+        for (int k = 0; k < ZW_P1_SLOW_DEN; k++) {
+            const int sk = ((k + 1) * ZW_P1_SLOW_NUM) / ZW_P1_SLOW_DEN - (k * ZW_P1_SLOW_NUM) / ZW_P1_SLOW_DEN;
+            if (r < nfast) return fast_wave(r);
+            r -= nfast;
+            if (r < sk) return 4 * (1 + (before + r) % nslow);
+            r -= sk;
+            before += sk;
+        }
+        return 0;  // unreachable
+    };
+    // skip mode: the wave's next row after `y`
+    auto next_row = [&](int y) {
+        for (y++; y < mbh; y++)
+            if (wave_of_row(y) == wv) break;
+        return y;
+    };
+    const int rw = ROWS ? 0 : (skip_mode ? next_row(-1) : luma_rank(wv));
     if (ROWS) {
         // the wave's window stands in for the frame-wide top arrays (offsets 0)
         C.top_y = W->win_y;
@@ -2632,8 +2853,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     uint8_t* const gtv = ROWS ? rb + RL.tv : nullptr;
     uint8_t* const gtc = ROWS ? rb + RL.tc : nullptr;
     uint8_t* const gtd = ROWS ? rb + RL.td : nullptr;
-    for (int it = 0;; it++) {
-        const int mby = ROWS ? row_ticket(&rsync[0]) : rw + it * nrw;
+    for (int it = 0, yk = rw;; it++) {
+        const int mby = ROWS ? row_ticket(&rsync[0]) : (skip_mode ? yk : rw + it * nrw);
+        if (skip_mode) yk = next_row(yk);
         if (mby >= mbh) break;
         if (lane < 20) W->left_y[lane] = 129;
         if (lane < 12) {
@@ -2643,7 +2865,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         }
         if (lane < 4) W->left_derr[lane] = 0;
         wsync();
-        const int prevw = (!ROWS && mby > 0) ? luma_wave((mby - 1) % nrw) : 0;
+        const int prevw = (!ROWS && mby > 0) ? wave_of_row(mby - 1) : 0;
         int seen = -1;  // ROWS: last progress value read of the row above
         int* const prog_above = ROWS ? rsync + 4 + (mby > 0 ? mby - 1 : 0) : nullptr;
         // the row above has finished `need` MBs
