@@ -81,7 +81,7 @@ def xform_traffic(blocks):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=int(os.environ.get("ZW_BENCH_FRAMES", "1024")),
                     help="frames per rank per step (weak scaling)")
