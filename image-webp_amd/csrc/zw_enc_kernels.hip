@@ -1887,11 +1887,18 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
                 nzbits |= (unsigned)z << bb;
             }
             const int srcl = (int)((code >> (2 * b)) & 3u) * 16 + b;
+            // gather the chosen context's levels as i16 pairs (|level| <= 2047)
+            // and dequantise them again (the trellis leaves level * q at the AC
+            // positions; the DC position is replaced by the Y2 output below)
+            lv[0] = 0;
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                lv[k] = __shfl(lv[k], srcl);
-                dq[k] = __shfl(dq[k], srcl);
+            for (int i = 0; i < 8; i++) {
+                const uint32_t w = (uint32_t)__shfl((int)pack_lo(lv[2 * i], lv[2 * i + 1]), srcl);
+                lv[2 * i] = lo16(w);
+                lv[2 * i + 1] = hi16(w);
             }
+#pragma unroll
+            for (int n = 1; n < 16; n++) dq[kZZ(n)] = m24(lv[n], (int)S.y1.q[1]);
             nzb = (nzbits >> b) & 1u;
             PH_MARK_L(18, l, 0);
         } else if (l < 16) {
