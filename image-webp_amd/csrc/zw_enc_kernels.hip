@@ -1625,12 +1625,18 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
     }
     pse = hx_sum(pse);
     const int key = m < 10 ? (pse << 4) | m : 0x7fffffff;
-    int rank = 0;
-#define ZW_RANK_STEP(R)                                                                      \
-    rank += (int)((uint32_t)(__builtin_amdgcn_update_dpp(0, key, 0x120 + (R), 0xf, 0xf, false) - key) >> 31);
-    ZW_RANK_STEP(1) ZW_RANK_STEP(2) ZW_RANK_STEP(3) ZW_RANK_STEP(4) ZW_RANK_STEP(5)
-    ZW_RANK_STEP(6) ZW_RANK_STEP(7) ZW_RANK_STEP(8) ZW_RANK_STEP(9) ZW_RANK_STEP(10)
-    ZW_RANK_STEP(11) ZW_RANK_STEP(12) ZW_RANK_STEP(13) ZW_RANK_STEP(14) ZW_RANK_STEP(15)
+    // rank = #{lanes of the 16-lane row with a smaller key}: per rotation the
+    // borrow of a DPP subtraction (keys are in [0, 2^31), so the borrow is
+    // rot(key) < key) into VCC, then an add-with-carry
+    int rank = 0, scratch_;
+#define ZW_RANK_STEP(R) "v_sub_co_u32_dpp %1, vcc, %2, %2 row_ror:" #R " row_mask:0xf bank_mask:0xf\n" \
+                        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+    asm volatile("s_nop 1\n" ZW_RANK_STEP(1) ZW_RANK_STEP(2) ZW_RANK_STEP(3) ZW_RANK_STEP(4) ZW_RANK_STEP(5)
+                     ZW_RANK_STEP(6) ZW_RANK_STEP(7) ZW_RANK_STEP(8) ZW_RANK_STEP(9) ZW_RANK_STEP(10)
+                         ZW_RANK_STEP(11) ZW_RANK_STEP(12) ZW_RANK_STEP(13) ZW_RANK_STEP(14) ZW_RANK_STEP(15)
+                 : "+v"(rank), "=&v"(scratch_)
+                 : "v"(key)
+                 : "vcc");
 #undef ZW_RANK_STEP
     PH_MARK_L(11, l, 0);
 #ifndef ZW_I4_QUAD
@@ -1926,7 +1932,8 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
                 wsp[(y + 1) * ZW_BPS + 1 + x] = (uint8_t)clamp255(pr[k] + dq[k]);
             }
         }
-        for (int k = 0; k < 16; k++) y_nz_out[k] = __shfl(nzb, k);
+        const unsigned nzmask = (unsigned)__ballot(l < 16 && nzb);  // block b's flag at bit b
+        for (int k = 0; k < 16; k++) y_nz_out[k] = (int)((nzmask >> k) & 1u);
         wsync();
         PH_MARK_L(14, l, 0);
     } else {
