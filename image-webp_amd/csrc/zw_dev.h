@@ -267,6 +267,7 @@ struct LdsTables {
     uint16_t ent[256];        // VP8_ENTROPY_COST
     uint16_t fci4[10][10][10];  // VP8_FIXED_COSTS_I4
     uint8_t i4idx[10][16];    // d_I4_IDX
+    uint8_t i4qa[10][16];     // 4 x the V index of pixel p under mode m (254 -> 3 - row, 255 -> 38)
     uint8_t zz[16];           // ZIGZAG
     uint8_t bands[17];        // VP8_ENC_BANDS
     uint8_t izz[16];          // inverse zigzag: natural index -> position
@@ -286,7 +287,11 @@ DI void load_static_tables(LdsTables* T, int tid, int nt, const uint8_t* probs /
     for (int i = tid; i < 2048; i += nt) T->lfc[i] = d_VP8_LEVEL_FIXED_COSTS[i];
     for (int i = tid; i < 256; i += nt) T->ent[i] = d_VP8_ENTROPY_COST[i];
     for (int i = tid; i < 1000; i += nt) (&T->fci4[0][0][0])[i] = (&d_VP8_FIXED_COSTS_I4[0][0][0])[i];
-    for (int i = tid; i < 160; i += nt) (&T->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
+    for (int i = tid; i < 160; i += nt) {
+        const int idx = (&d_I4_IDX[0][0])[i], p = i & 15;
+        (&T->i4idx[0][0])[i] = (uint8_t)idx;
+        (&T->i4qa[0][0])[i] = (uint8_t)(4 * (idx == 254 ? 3 - (p >> 2) : (idx == 255 ? 38 : idx)));
+    }
     for (int i = tid; i < 16; i += nt) T->zz[i] = d_ZIGZAG[i];
     for (int i = tid; i < 17; i += nt) T->bands[i] = d_VP8_ENC_BANDS[i];
     for (int i = tid; i < 16; i += nt) T->izz[d_ZIGZAG[i]] = (uint8_t)i;

@@ -1138,7 +1138,7 @@ DI int rcost_pair(const int av[2][4], int h, int ctx0, int ctype, const LdsTable
     const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
     const int tail = (int)T->beob[ctype][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
     const int head = (int)T->binit[ctype][0][ctx0] & -(int)(ctx0 == 0);
-    return last < 0 ? (int)T->beob[ctype][0][ctx0] : head + sum + tail;
+    return csel(last < 0, (int)T->beob[ctype][0][ctx0], head + sum + tail);  // (no divergent branch)
 }
 
 // Chroma DC predictors of both planes (uniform values): lanes 0..15 sum U,
@@ -1319,9 +1319,10 @@ DI void uvq_fdct(uint32_t A, uint32_t D, int q, int c[4])
 {
     const bool odd = q & 1;
     const zs2 k0 = {8, 8}, k2 = {8, -8}, k1 = {10704, 4434}, k3 = {4434, -10704};
-    const uint32_t k = q == 0 ? as_zu(k0) : (q == 1 ? as_zu(k1) : (q == 2 ? as_zu(k2) : as_zu(k3)));
-    const int rnd = q == 1 ? 3625 : (q == 3 ? 1875 : 0);
-    const int sh = odd ? 10 : 0;
+    // (arithmetic selects: lane-dependent ?: chains became divergent branches)
+    const uint32_t k = (uint32_t)sel4(q, (int)as_zu(k0), (int)as_zu(k1), (int)as_zu(k2), (int)as_zu(k3));
+    const int rnd = sel4(q, 0, 3625, 0, 1875);
+    const int sh = csel(odd, 10, 0);
     // (csel, not ?: -- a select of two DPP results may be folded into one DPP
     // of a select, which would take the source lane's choice)
     int t[4];
@@ -1419,7 +1420,7 @@ DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* 
     const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
     const int tail = (int)T->beob[ctype][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
     const int head = (int)T->binit[ctype][0][ctx0] & -(int)(ctx0 == 0);
-    return last < 0 ? (int)T->beob[ctype][0][ctx0] : head + sum + tail;
+    return csel(last < 0, (int)T->beob[ctype][0][ctx0], head + sum + tail);  // (no divergent branch)
 }
 
 // Candidate evaluation of an I4 step in quad form (K <= 4: methods 0-4).  The
@@ -1461,15 +1462,13 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
     // V[3 - q] + the top offsets; 255: the DC entry V[38])
     uint32_t p01, p32;
     {
-        const uint32_t iw = *(const uint32_t*)&T->i4idx[mv][4 * q];
+        // bpermute byte addresses of the row's four pixels (T->i4qa: 4 x V index)
+        const uint32_t iw = *(const uint32_t*)&T->i4qa[mv][4 * q];
         const uint32_t psel = (l & 16) ? 0x0c060c02u : 0x0c040c00u;
         uint32_t v[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int idx = (int)((iw >> (8 * j)) & 255u);
-            const int sidx = csel(idx == 254, 3 - q, csel(idx == 255, 38, idx));
-            v[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(sidx << 2, (int)vp);
-        }
+        for (int j = 0; j < 4; j++)
+            v[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((iw >> (8 * j)) & 255u), (int)vp);
         const uint32_t q01 = __builtin_amdgcn_perm(v[1], v[0], psel), q32 = __builtin_amdgcn_perm(v[2], v[3], psel);
         const bool tm = mv == 1;
         p01 = tm ? clamp_pk(add_pk(q01, ap01)) : q01;
@@ -2211,7 +2210,7 @@ DI int uvq_rcost(const int av[4], int q, const LdsTables* T)
     const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
     const int tail = (int)T->beob[2][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
     const int head = (int)T->binit[2][0][0];
-    return last < 0 ? (int)T->beob[2][0][0] : head + sum + tail;
+    return csel(last < 0, (int)T->beob[2][0][0], head + sum + tail);  // (no divergent branch)
 }
 
 // pick_best_uv (vp8.rs:2050-2200) with the partner plane's wave: returns the
