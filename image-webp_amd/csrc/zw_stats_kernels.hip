@@ -13,9 +13,9 @@
 //                  flags of its 25 blocks (eob > first), which alone fix every
 //                  block's token context;
 //   k_stats_hist   one workgroup per stripe of ZS_STRIPE MBs: every block's
-//                  decisions in parallel into 32 lane-private LDS copies of the
-//                  counters (lane & 31: at most two lanes of a wave share an
-//                  address), reduced to per-stripe (decisions, ones);
+//                  decisions in parallel into ZS_COPIES lane-private LDS copies
+//                  of the counters (lane % ZS_COPIES), reduced to per-stripe
+//                  (decisions, ones);
 //   k_stats_final  one workgroup per frame: counters with <= 65 534 decisions are
 //                  final, s = (n << 16) | ones; every other ("heavy") counter is
 //                  replayed exactly, one wave per counter, in raster order:
@@ -29,7 +29,13 @@
 
 #define ZS_WG 1024
 #define ZS_STRIPE 512
-#define ZS_COPIES 32
+#ifndef ZS_COPIES
+#define ZS_COPIES 16
+#endif
+static_assert((ZS_STRIPE * 25 + ZS_COPIES - 1) / ZS_COPIES * 9 < 65536, "a packed 16:16 copy must not carry");
+#ifndef ZS_HWG
+#define ZS_HWG 512  // k_stats_hist workgroup size (16 copies x 512 threads: two workgroups per CU)
+#endif
 #define ZS_NCTR (4 * 8 * 3 * 11)
 
 typedef ZwStatsOut StatsOut;
@@ -191,10 +197,10 @@ extern "C" __global__ __launch_bounds__(256) void k_stats_flags(const ZwMbOut* _
 }
 
 // Per-stripe (decisions, ones) of every counter.  Copy j of the counters takes
-// the items it = j (mod 32) of the stripe: <= ceil(512 * 25 / 32) blocks, each
-// adding <= 9 decisions to one counter (band 6 spans 9 positions), so the
-// packed 16:16 copy cannot carry.
-extern "C" __global__ __launch_bounds__(ZS_WG) void k_stats_hist(const ZwMbOut* __restrict__ mbs,
+// the items it = j (mod ZS_COPIES) of the stripe: <= ceil(512 * 25 / 16) blocks,
+// each adding <= 9 decisions to one counter (band 6 spans 9 positions), so the
+// packed 16:16 copy cannot carry (14 400 < 65 536 even at 8 copies).
+extern "C" __global__ __launch_bounds__(ZS_HWG) void k_stats_hist(const ZwMbOut* __restrict__ mbs,
                                                                 const uint32_t* __restrict__ flags, int mbw, int mbh,
                                                                 uint2* __restrict__ part)
 {
@@ -204,11 +210,11 @@ extern "C" __global__ __launch_bounds__(ZS_WG) void k_stats_hist(const ZwMbOut* 
     const int nmb = mbw * mbh;
     const ZwMbOut* F = mbs + (size_t)f * nmb;
     const uint32_t* fl = flags + (size_t)f * nmb;
-    for (int i = tid; i < ZS_COPIES * ZS_NCTR; i += ZS_WG) cp[i] = 0;
+    for (int i = tid; i < ZS_COPIES * ZS_NCTR; i += ZS_HWG) cp[i] = 0;
     __syncthreads();
     uint32_t* my = cp + (tid & (ZS_COPIES - 1)) * ZS_NCTR;
     const int mb0 = st * ZS_STRIPE, mb1 = min(nmb, mb0 + ZS_STRIPE);
-    for (int it = tid; it < (mb1 - mb0) * 25; it += ZS_WG) {
+    for (int it = tid; it < (mb1 - mb0) * 25; it += ZS_HWG) {
         const int mb = mb0 + it / 25, b = it % 25;
         const uint32_t fm = fl[mb];
         if (fm & ZS_SKIP) continue;
@@ -221,7 +227,7 @@ extern "C" __global__ __launch_bounds__(ZS_WG) void k_stats_hist(const ZwMbOut* 
         zs_walk(lv, zs_eob(lv), t, first, ctx, [&](int c, int bit) { atomicAdd(&my[c], 0x10000u + (bit ? 1u : 0u)); });
     }
     __syncthreads();
-    for (int c = tid; c < ZS_NCTR; c += ZS_WG) {
+    for (int c = tid; c < ZS_NCTR; c += ZS_HWG) {
         uint32_t n = 0, o = 0;
 #pragma unroll 8
         for (int j = 0; j < ZS_COPIES; j++) {
@@ -352,7 +358,7 @@ extern "C" hipError_t zwk_stats(hipStream_t s, const ZwMbOut* mbs, int mbw, int 
     uint32_t* fl = (uint32_t*)scratch;
     uint2* part = (uint2*)((uint8_t*)scratch + (size_t)nframes * zs_flag_bytes(nmb));
     hipLaunchKernelGGL(k_stats_flags, dim3((nmb + 255) / 256, nframes), dim3(256), 0, s, mbs, nmb, fl);
-    hipLaunchKernelGGL(k_stats_hist, dim3(nst, nframes), dim3(ZS_WG), (size_t)ZS_COPIES * ZS_NCTR * 4, s, mbs, fl,
+    hipLaunchKernelGGL(k_stats_hist, dim3(nst, nframes), dim3(ZS_HWG), (size_t)ZS_COPIES * ZS_NCTR * 4, s, mbs, fl,
                        mbw, mbh, part);
     const size_t lds0 = ZS_NCTR * 4 + 8;
     const int fl_lds = lds0 + (size_t)nmb * 4 <= 160 * 1024;
