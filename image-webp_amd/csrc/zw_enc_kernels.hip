@@ -2823,10 +2823,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_P1_SLOWSKIP 1
 #endif
 #ifndef ZW_P1_SLOW_NUM
-#define ZW_P1_SLOW_NUM 4
+#define ZW_P1_SLOW_NUM 3
 #endif
 #ifndef ZW_P1_SLOW_DEN
-#define ZW_P1_SLOW_DEN 3
+#define ZW_P1_SLOW_DEN 2
 #endif
     constexpr bool skip_mode = ZW_P1_SLOWSKIP && PASS == 1 && !ROWS && NCH == 1 && NW > 4;
     constexpr int nslow = (NW - 1) / 4 > 0 ? (NW - 1) / 4 : 1;  // luma waves on SIMD 0: 4, 8, ..
