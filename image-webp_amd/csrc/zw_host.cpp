@@ -333,6 +333,7 @@ struct zw_pipe {
     // chunk of an LA8 / RGBA8 frame encoded from its host copy
     bool container = false;
     std::vector<const uint8_t*> host_frames;
+    int nparts = 1;  // token partitions per frame (zw_pipe_set_token_partitions)
     std::vector<PipeLane> lanes;
     float kms[8];
 };
@@ -548,6 +549,13 @@ extern "C" int zw_pipe_set_container(zw_pipe* p, int enable, const uint8_t* cons
     return ZW_OK;
 }
 
+extern "C" int zw_pipe_set_token_partitions(zw_pipe* p, int nparts)
+{
+    if (!p || (nparts != 1 && nparts != 2 && nparts != 4 && nparts != 8)) return ZW_EINVAL;
+    p->nparts = nparts;
+    return ZW_OK;
+}
+
 extern "C" int zw_pipe_upload(zw_pipe* p, int frame, const uint8_t* data, size_t len)
 {
     if (!p || frame < 0 || frame >= p->n || !data) return ZW_EINVAL;
@@ -698,6 +706,25 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
     return ZW_OK;
 }
 
+// One frame's VP8 bitstream from its pass-2 records.  With token partitions
+// and a chunk of one frame (a single-frame call) the partitions are coded on
+// their own threads; otherwise the frame's thread codes them in turn.
+static void emit_vp8(zw_pipe* p, std::vector<uint8_t>& out, const uint8_t* rec, size_t hf, int na)
+{
+    const uint8_t(*upd)[8][3][11] = (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11);
+    const ZwFrameParams& P = p->h_params[hf];
+    if (p->nparts == 1) {
+        zwh::emit_frame(out, P, rec, p->w, p->h, p->h_have_upd[hf] != 0, upd);
+    } else if (na == 1) {
+        zwh::emit_frame_parts(out, P, rec, p->w, p->h, p->h_have_upd[hf] != 0, upd, p->nparts,
+                              [](int n, auto fn) { parallel_for(n, fn); });
+    } else {
+        zwh::emit_frame_parts(out, P, rec, p->w, p->h, p->h_have_upd[hf] != 0, upd, p->nparts, [](int n, auto fn) {
+            for (int i = 0; i < n; i++) fn(i);
+        });
+    }
+}
+
 static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
@@ -707,8 +734,7 @@ static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
         const size_t f = F + i, hf = hidx(p, par, f);
         std::vector<uint8_t>& out = p->bitstreams[f];
         if (!p->container) {
-            zwh::emit_frame(out, p->h_params[hf], B.pack + B.finfo[2 * i], p->w, p->h, p->h_have_upd[hf] != 0,
-                            (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11));
+            emit_vp8(p, out, B.pack + B.finfo[2 * i], hf, na);
             return;
         }
         // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the
@@ -716,8 +742,7 @@ static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
         thread_local std::vector<uint8_t> vp8, alph;
         vp8.clear();
         alph.clear();
-        zwh::emit_frame(vp8, p->h_params[hf], B.pack + B.finfo[2 * i], p->w, p->h, p->h_have_upd[hf] != 0,
-                        (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11));
+        emit_vp8(p, vp8, B.pack + B.finfo[2 * i], hf, na);
         // the image was validated by zw_pipe_set_container (size, dimensions)
         if (has_alpha) (void)zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph);
         const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
@@ -1051,7 +1076,15 @@ static int check_encode_args(const uint8_t* data, size_t len, uint32_t width, ui
 extern "C" int zw_encode_batch(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t quality, uint8_t method,
                                zw_bytes* outs)
 {
+    return zw_encode_batch_ex(ctx, n, imgs, quality, method, 1, outs);
+}
+
+extern "C" int zw_encode_batch_ex(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t quality, uint8_t method,
+                                  int token_partitions, zw_bytes* outs)
+{
     if (!ctx || n <= 0 || !imgs || !outs) return ZW_EINVAL;
+    if (token_partitions != 1 && token_partitions != 2 && token_partitions != 4 && token_partitions != 8)
+        return ZW_EINVAL;
     for (int i = 0; i < n; i++) {
         outs[i].data = nullptr;
         outs[i].len = 0;
@@ -1075,7 +1108,7 @@ extern "C" int zw_encode_batch(zw_ctx* ctx, int n, const zw_image* imgs, uint8_t
             memcpy(ctx->pipe1_key, key, sizeof key);
         }
     }
-    r = ZW_OK;
+    r = zw_pipe_set_token_partitions(p, token_partitions);
     for (int i = 0; i < n && !r; i++) r = zw_pipe_upload(p, i, imgs[i].data, imgs[i].len);
     if (!r) r = zw_pipe_encode(p);
     for (int i = 0; i < n && !r; i++) r = zw_pipe_output(p, i, &outs[i]);
@@ -1114,13 +1147,20 @@ extern "C" int zw_encode_webp_batch(zw_ctx* ctx, int n, const zw_image* imgs, ui
 extern "C" int zw_encode_frame_lossy(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
                                      int color, uint8_t quality, uint8_t method, zw_bytes* out)
 {
+    return zw_encode_frame_lossy_ex(ctx, data, len, width, height, color, quality, method, 1, out);
+}
+
+extern "C" int zw_encode_frame_lossy_ex(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width,
+                                        uint32_t height, int color, uint8_t quality, uint8_t method,
+                                        int token_partitions, zw_bytes* out)
+{
     if (!ctx || !out) return ZW_EINVAL;
     out->data = nullptr;
     out->len = 0;
     int r = check_encode_args(data, len, width, height, color, quality);
     if (r) return r;
     zw_image im = {data, len, width, height, color};
-    return zw_encode_batch(ctx, 1, &im, quality, method, out);
+    return zw_encode_batch_ex(ctx, 1, &im, quality, method, token_partitions, out);
 }
 
 extern "C" int zw_encode_webp(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,

@@ -502,17 +502,12 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* 
     return eobi > 0;
 }
 
-// Frame assembly: compressed header (vp8.rs:332), MB headers (:498), residual
-// partition (:650), frame tag (:315).
-inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const uint8_t* packed, int width,
-                       int height, bool have_updated, const uint8_t upd[4][8][3][11])
+// Compressed frame header (encode_compressed_frame_header vp8.rs:332-372) with
+// log2(nparts) token partitions; `probs` leaves with the probabilities in force.
+inline void emit_frame_header(BoolEncoder& H, const ZwFrameParams& P, bool have_updated,
+                              const uint8_t upd[4][8][3][11], int nparts, uint8_t probs[4][8][3][11])
 {
-    PackedMb m;
-    const int mbw = P.mbw, mbh = P.mbh;
-    BoolEncoder H, T;
-    T.buf.reserve((size_t)mbw * mbh * 16 + 4096);
-    uint8_t probs[4][8][3][11];
-    memcpy(probs, COEFF_PROBS, sizeof probs);
+    memcpy(probs, COEFF_PROBS, sizeof(COEFF_PROBS));
     H.literal(1, 0);
     H.literal(1, 0);
     H.flag(P.seg_enabled);
@@ -539,7 +534,7 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
     H.literal(6, P.filter_level);
     H.literal(3, 0);
     H.flag(0);
-    H.literal(2, 0);
+    H.literal(2, nparts == 8 ? 3 : nparts >> 1);  // vp8.rs:352-354
     H.literal(7, P.base_qi);
     for (int i = 0; i < 5; i++) H.flag(0);
     H.literal(1, 0);
@@ -558,80 +553,89 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
                 }
     H.literal(1, 1);
     H.literal(8, P.skip_prob);
+}
 
+// write_macroblock_header (vp8.rs:498-560) of MB x of the current row.
+inline void emit_mb_header(BoolEncoder& H, const ZwFrameParams& P, const PackedMb& m, uint8_t* top_bp, uint8_t left_bp[4],
+                           int x)
+{
     static const TreePaths seg_t(SEGMENT_ID_TREE, 6, 4), ymode_t(YMODE_TREE, 8, 5), bmode_t(BMODE_TREE, 18, 10),
         uvmode_t(UVMODE_TREE, 6, 4);
-    std::vector<Cplx> top(mbw);
-    memset(top.data(), 0, sizeof(Cplx) * mbw);
-    std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
-    for (int y = 0; y < mbh; y++) {
-        Cplx left;
-        memset(&left, 0, sizeof left);
-        uint8_t left_bp[4] = {0, 0, 0, 0};
-        for (int x = 0; x < mbw; x++) {
-            packed = view_mb(packed, m);
-            if (P.seg_enabled && P.seg_update_map) seg_t.put(H, P.seg_probs, m.segment);
-            H.put(m.skip, P.skip_prob);
-            ymode_t.put(H, KEYFRAME_YMODE_PROBS, m.luma);
-            if (m.luma == 4) {
-                for (int by = 0; by < 4; by++) {
-                    int l = left_bp[by];
-                    for (int bx = 0; bx < 4; bx++) {
-                        int t = top_bp[x * 4 + bx], md = m.bpred[by * 4 + bx];
-                        bmode_t.put(H, KEYFRAME_BPRED_MODE_PROBS[t][l], md);
-                        l = md;
-                        top_bp[x * 4 + bx] = (uint8_t)md;
-                    }
-                    left_bp[by] = (uint8_t)l;
-                }
-            } else {
-                static const int intra_of[4] = {0, 2, 3, 1};
-                for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma];
+    if (P.seg_enabled && P.seg_update_map) seg_t.put(H, P.seg_probs, m.segment);
+    H.put(m.skip, P.skip_prob);
+    ymode_t.put(H, KEYFRAME_YMODE_PROBS, m.luma);
+    if (m.luma == 4) {
+        for (int by = 0; by < 4; by++) {
+            int l = left_bp[by];
+            for (int bx = 0; bx < 4; bx++) {
+                int t = top_bp[x * 4 + bx], md = m.bpred[by * 4 + bx];
+                bmode_t.put(H, KEYFRAME_BPRED_MODE_PROBS[t][l], md);
+                l = md;
+                top_bp[x * 4 + bx] = (uint8_t)md;
             }
-            uvmode_t.put(H, KEYFRAME_UV_MODE_PROBS, m.chroma);
-            const bool i4 = m.luma == 4;
-            if (m.skip) {
-                left.clear(!i4);
-                top[x].clear(!i4);
-                continue;
+            left_bp[by] = (uint8_t)l;
+        }
+    } else {
+        static const int intra_of[4] = {0, 2, 3, 1};
+        for (int i = 0; i < 4; i++) left_bp[i] = top_bp[x * 4 + i] = (uint8_t)intra_of[m.luma];
+    }
+    uvmode_t.put(H, KEYFRAME_UV_MODE_PROBS, m.chroma);
+}
+
+// encode_residual_data (vp8.rs:650-800) of one MB with its left / top
+// complexity (non-zero) contexts.  Without an encoder (E == nullptr) only the
+// contexts advance: a block's context bit is eob > 0, as emit_block returns.
+inline void emit_mb_tokens(BoolEncoder* E, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
+{
+    const bool i4 = m.luma == 4;
+    if (m.skip) {
+        left.clear(!i4);
+        top.clear(!i4);
+        return;
+    }
+    const int plane = i4 ? 3 : 0;
+    if (!i4) {
+        int hc = E ? emit_block(*E, probs[1], m.lv[16], m.eob[16], 0, left.y2 + top.y2) : m.eob[16] > 0;
+        left.y2 = top.y2 = (uint8_t)hc;
+    }
+    const int first = i4 ? 0 : 1;
+    for (int by = 0; by < 4; by++) {
+        int l = left.y[by];
+        for (int bx = 0; bx < 4; bx++) {
+            const int b = by * 4 + bx;
+            int hc = E ? emit_block(*E, probs[plane], m.lv[b], m.eob[b], first, l + top.y[bx]) : m.eob[b] > 0;
+            l = hc;
+            top.y[bx] = (uint8_t)hc;
+        }
+        left.y[by] = (uint8_t)l;
+    }
+    for (int pl = 0; pl < 2; pl++) {
+        uint8_t* lc = pl ? left.v : left.u;
+        uint8_t* tc = pl ? top.v : top.u;
+        for (int by = 0; by < 2; by++) {
+            int l = lc[by];
+            for (int bx = 0; bx < 2; bx++) {
+                const int b = 17 + 4 * pl + by * 2 + bx;
+                int hc = E ? emit_block(*E, probs[2], m.lv[b], m.eob[b], 0, l + tc[bx]) : m.eob[b] > 0;
+                l = hc;
+                tc[bx] = (uint8_t)hc;
             }
-            int plane = i4 ? 3 : 0;
-            if (!i4) {
-                int hc = emit_block(T, probs[1], m.lv[16], m.eob[16], 0, left.y2 + top[x].y2);
-                left.y2 = top[x].y2 = (uint8_t)hc;
-            }
-            const int first = i4 ? 0 : 1;
-            for (int by = 0; by < 4; by++) {
-                int l = left.y[by];
-                for (int bx = 0; bx < 4; bx++) {
-                    const int b = by * 4 + bx;
-                    int hc = emit_block(T, probs[plane], m.lv[b], m.eob[b], first, l + top[x].y[bx]);
-                    l = hc;
-                    top[x].y[bx] = (uint8_t)hc;
-                }
-                left.y[by] = (uint8_t)l;
-            }
-            for (int pl = 0; pl < 2; pl++) {
-                uint8_t* lc = pl ? left.v : left.u;
-                uint8_t* tc = pl ? top[x].v : top[x].u;
-                for (int by = 0; by < 2; by++) {
-                    int l = lc[by];
-                    for (int bx = 0; bx < 2; bx++) {
-                        const int b = 17 + 4 * pl + by * 2 + bx;
-                        int hc = emit_block(T, probs[2], m.lv[b], m.eob[b], 0, l + tc[bx]);
-                        l = hc;
-                        tc[bx] = (uint8_t)hc;
-                    }
-                    lc[by] = (uint8_t)l;
-                }
-            }
+            lc[by] = (uint8_t)l;
         }
     }
-    H.flush();
-    T.flush();
-    out.resize(10 + H.buf.size() + T.buf.size());
+}
+
+// Frame tag (write_uncompressed_frame_header vp8.rs:315-330), the first
+// partition, then for nparts > 1 the nparts - 1 3-byte partition sizes and the
+// token partitions (RFC 6386 9.5; read back by decoder/vp8.rs:421-450).
+inline void assemble_frame(std::vector<uint8_t>& out, const std::vector<uint8_t>& H, const BoolEncoder* T, int nparts,
+                           int width, int height)
+{
+    size_t tot = 10 + H.size() + 3 * (size_t)(nparts - 1);
+    for (int p = 0; p < nparts; p++) tot += T[p].buf.size();
+    out.resize(tot);
     uint8_t* o = out.data();
-    uint32_t tag = ((uint32_t)H.buf.size() << 5) | (1u << 4);
+    uint32_t tag = ((uint32_t)H.size() << 5) | (1u << 4);
     o[0] = (uint8_t)tag;
     o[1] = (uint8_t)(tag >> 8);
     o[2] = (uint8_t)(tag >> 16);
@@ -642,8 +646,102 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
     o[7] = (uint8_t)((width >> 8) & 0x3f);
     o[8] = (uint8_t)(height & 0xff);
     o[9] = (uint8_t)((height >> 8) & 0x3f);
-    memcpy(o + 10, H.buf.data(), H.buf.size());
-    memcpy(o + 10 + H.buf.size(), T.buf.data(), T.buf.size());
+    memcpy(o + 10, H.data(), H.size());
+    size_t w = 10 + H.size();
+    for (int p = 0; p + 1 < nparts; p++, w += 3) {
+        const size_t n = T[p].buf.size();
+        o[w] = (uint8_t)n;
+        o[w + 1] = (uint8_t)(n >> 8);
+        o[w + 2] = (uint8_t)(n >> 16);
+    }
+    for (int p = 0; p < nparts; p++) {
+        memcpy(o + w, T[p].buf.data(), T[p].buf.size());
+        w += T[p].buf.size();
+    }
+}
+
+// Frame assembly: compressed header (vp8.rs:332), MB headers (:498), residual
+// partition (:650), frame tag (:315).  One token partition: headers and tokens
+// in one raster walk.
+inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const uint8_t* packed, int width,
+                       int height, bool have_updated, const uint8_t upd[4][8][3][11])
+{
+    PackedMb m;
+    const int mbw = P.mbw, mbh = P.mbh;
+    BoolEncoder H, T;
+    T.buf.reserve((size_t)mbw * mbh * 16 + 4096);
+    uint8_t probs[4][8][3][11];
+    emit_frame_header(H, P, have_updated, upd, 1, probs);
+    std::vector<Cplx> top(mbw);
+    memset(top.data(), 0, sizeof(Cplx) * mbw);
+    std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
+    for (int y = 0; y < mbh; y++) {
+        Cplx left;
+        memset(&left, 0, sizeof left);
+        uint8_t left_bp[4] = {0, 0, 0, 0};
+        for (int x = 0; x < mbw; x++) {
+            packed = view_mb(packed, m);
+            emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
+            emit_mb_tokens(&T, probs, m, left, top[x]);
+        }
+    }
+    H.flush();
+    T.flush();
+    assemble_frame(out, H.buf, &T, 1, width, height);
+}
+
+// The same with nparts (2, 4, 8) token partitions: MB row y's tokens go to
+// partition y % nparts (vp8.rs:1419-1421).  A serial walk writes the MB headers
+// and records where each row's records start and the top contexts it begins
+// with; the partitions are then coded independently -- concurrently through
+// `run(n, fn)` (fn(i) for i < n, e.g. parallel_for), or in turn without one.
+template <class Run>
+inline void emit_frame_parts(std::vector<uint8_t>& out, const ZwFrameParams& P, const uint8_t* packed, int width,
+                             int height, bool have_updated, const uint8_t upd[4][8][3][11], int nparts, Run run)
+{
+    if (nparts <= 1) {
+        emit_frame(out, P, packed, width, height, have_updated, upd);
+        return;
+    }
+    PackedMb m;
+    const int mbw = P.mbw, mbh = P.mbh;
+    BoolEncoder H, T[8];
+    uint8_t probs[4][8][3][11];
+    emit_frame_header(H, P, have_updated, upd, nparts, probs);
+    std::vector<const uint8_t*> row_at((size_t)mbh);
+    std::vector<Cplx> top_at((size_t)mbh * mbw), top(mbw);
+    memset(top.data(), 0, sizeof(Cplx) * mbw);
+    std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
+    for (int y = 0; y < mbh; y++) {
+        row_at[y] = packed;
+        memcpy(&top_at[(size_t)y * mbw], top.data(), sizeof(Cplx) * mbw);
+        Cplx left;
+        memset(&left, 0, sizeof left);
+        uint8_t left_bp[4] = {0, 0, 0, 0};
+        for (int x = 0; x < mbw; x++) {
+            packed = view_mb(packed, m);
+            emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
+            emit_mb_tokens(nullptr, probs, m, left, top[x]);
+        }
+    }
+    H.flush();
+    run(nparts, [&](int p) {
+        PackedMb pm;
+        BoolEncoder& E = T[p];
+        E.buf.reserve((size_t)mbw * mbh * 16 / nparts + 4096);
+        for (int y = p; y < mbh; y += nparts) {
+            const uint8_t* q = row_at[y];
+            Cplx* tr = &top_at[(size_t)y * mbw];
+            Cplx left;
+            memset(&left, 0, sizeof left);
+            for (int x = 0; x < mbw; x++) {
+                q = view_mb(q, pm);
+                emit_mb_tokens(&E, probs, pm, left, tr[x]);
+            }
+        }
+        E.flush();
+    });
+    assemble_frame(out, H.buf, T, nparts, width, height);
 }
 
 // quality_to_quant_index (vp8.rs:37-55) with fast_math::cbrt/round (fast_math.rs:15-42).

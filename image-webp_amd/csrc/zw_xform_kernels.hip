@@ -129,6 +129,54 @@ __global__ __launch_bounds__(256) void k_fdct_quant_t(const v4u* __restrict__ sr
     }
 }
 
+// The same with the level stores coalesced: each wave stages its 64 blocks'
+// 32-byte level rows in LDS and writes them back as two fully contiguous 1 KB
+// store instructions (the direct form's stores are 16 B per lane at a 32 B
+// lane stride, two half-filled instructions per 2 KB).
+template <int V>
+__global__ __launch_bounds__(256) void k_fdct_quant_lds(const v4u* __restrict__ src, const v4u* __restrict__ pred,
+                                                        size_t n, XformArgs a, v4u* __restrict__ levels,
+                                                        v4u* __restrict__ recon)
+{
+    __shared__ v4u stage[256 * 2];
+    const int t = threadIdx.x, l = t & 63;
+    v4u* ws = stage + (t >> 6) * 128;
+    const size_t stride = (size_t)gridDim.x * 256 * V;
+    // (every lane of a wave stays in the loop while any of its blocks is in range:
+    // the exchange reads other lanes' rows)
+    for (size_t b0 = (size_t)blockIdx.x * 256 * V + threadIdx.x; b0 - l < n; b0 += stride) {
+        v4u s4[V], p4[V];
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const size_t b = b0 + (size_t)u * 256;
+            if (b < n) {
+                s4[u] = __builtin_nontemporal_load(&src[b]);
+                p4[u] = __builtin_nontemporal_load(&pred[b]);
+            } else {
+                s4[u] = p4[u] = v4u{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const size_t b = b0 + (size_t)u * 256, w0 = b - l;  // the wave's first block
+            if (w0 >= n) break;
+            v4u l0, l1, r0;
+            xform_block(s4[u], p4[u], a, l0, l1, r0);
+            ws[2 * l] = l0;
+            ws[2 * l + 1] = l1;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const v4u o0 = ws[l], o1 = ws[64 + l];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const size_t e = 2 * w0 + l;  // level row halves e and e + 64
+            if (e < 2 * n) __builtin_nontemporal_store(o0, &levels[e]);
+            if (e + 64 < 2 * n) __builtin_nontemporal_store(o1, &levels[e + 64]);
+            if (b < n) __builtin_nontemporal_store(r0, &recon[b]);
+        }
+    }
+}
+
 // Same traffic shape with no arithmetic (calibration of the read:write mix).
 __global__ __launch_bounds__(256) void k_fdct_quant_copy(const v4u* __restrict__ src, const v4u* __restrict__ pred,
                                                          size_t n, XformArgs a, v4u* __restrict__ levels,
@@ -172,6 +220,7 @@ extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void*
     // Tuning knobs (defaults are the measured best on MI355X: 4 blocks per
     // thread, non-temporal stores, one pass over the data -- no grid-stride cap).
     //   ZW_XFORM_VARIANT  0: V1 nt  1: V2 nt  2: V1  3: V2  4: V4  5: V4 nt (default)
+    //                     6/7/8: V4/V2/V1 nt, level stores coalesced through LDS
     //                     99: same traffic, no arithmetic (bandwidth calibration only)
     //   ZW_XFORM_GRID     cap on workgroups, as a multiple of the CU count
     // (read per launch: bench.py times the variant-99 copy ceiling beside the real pass in one process)
@@ -179,7 +228,7 @@ extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void*
     const char* eg = getenv("ZW_XFORM_GRID");
     const int variant = ev ? atoi(ev) : 5;
     const int gmul = eg ? atoi(eg) : 1 << 20;
-    const int V = variant >= 98 ? 1 : (variant >= 4 ? 4 : ((variant & 1) ? 2 : 1));
+    const int V = variant >= 98 ? 1 : variant == 7 ? 2 : variant == 8 ? 1 : (variant >= 4 ? 4 : ((variant & 1) ? 2 : 1));
     size_t grid = (n + 256 * V - 1) / (256 * V);
     const size_t cap = (size_t)(cus > 0 ? cus : 256) * gmul;
     if (grid > cap) grid = cap;
@@ -193,6 +242,9 @@ extern "C" hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void*
     case 2: hipLaunchKernelGGL((k_fdct_quant_t<1, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 3: hipLaunchKernelGGL((k_fdct_quant_t<2, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 4: hipLaunchKernelGGL((k_fdct_quant_t<4, false>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 6: hipLaunchKernelGGL((k_fdct_quant_lds<4>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 7: hipLaunchKernelGGL((k_fdct_quant_lds<2>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
+    case 8: hipLaunchKernelGGL((k_fdct_quant_lds<1>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 99: hipLaunchKernelGGL(k_fdct_quant_copy, g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     case 98: hipLaunchKernelGGL(k_fdct_quant_copy_planar, g, blk, 0, s, sp, pp, n, a, lp, rp); break;
     default: hipLaunchKernelGGL((k_fdct_quant_t<4, true>), g, blk, 0, s, sp, pp, n, a, lp, rp); break;

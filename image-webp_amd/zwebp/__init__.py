@@ -121,12 +121,14 @@ SIGNATURES = [
     ("zw_bytes_free", None, [ctypes.POINTER(_Bytes)]),
     ("zw_frame_free", None, [ctypes.POINTER(_Frame)]),
     ("zw_encode_frame_lossy", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_frame_lossy_ex", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_webp", _I, [_VP, _VP, _SZ, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_encode_webp_ex", _I, [_VP, _VP, _SZ, _U32, _U32, _I, ctypes.POINTER(_EncParams), ctypes.POINTER(_Metadata),
                                ctypes.POINTER(_Bytes)]),
     ("zw_encode_frame_lossless", _I, [_VP, _SZ, _U32, _U32, _I, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_alpha", _I, [_VP, _SZ, _U32, _U32, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
+    ("zw_encode_batch_ex", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, _I, ctypes.POINTER(_Bytes)]),
     ("zw_encode_webp_batch", _I, [_VP, _I, ctypes.POINTER(_Image), _U8, _U8, ctypes.POINTER(_Bytes)]),
     ("zw_vp8_decode_frame", _I, [_VP, _VP, _SZ, ctypes.POINTER(_Frame)]),
     ("zw_vp8_decode_batch", _I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_SZ), ctypes.POINTER(_Frame)]),
@@ -153,6 +155,7 @@ SIGNATURES = [
     ("zw_pipe_input_device_ptr", _VP, [_VP]),
     ("zw_pipe_upload", _I, [_VP, _I, _VP, _SZ]),
     ("zw_pipe_set_container", _I, [_VP, _I, ctypes.POINTER(_VP)]),
+    ("zw_pipe_set_token_partitions", _I, [_VP, _I]),
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
@@ -262,18 +265,21 @@ def _as_u8(data):
     return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
 
 
-def encode_frame_lossy(data, width, height, color, quality=75, method=4, ctx=None):
-    """encode_frame_lossy (encoder/vp8.rs:3132): raw VP8 frame bytes."""
+def encode_frame_lossy(data, width, height, color, quality=75, method=4, ctx=None, token_partitions=1):
+    """encode_frame_lossy (encoder/vp8.rs:3132): raw VP8 frame bytes.
+    token_partitions (1, 2, 4, 8): MB row y's tokens in partition y % n
+    (vp8.rs:352-354, :1419-1421; the reference fixes 1), coded on parallel
+    host threads; 1 gives the reference's bytes."""
     c = _ctx(ctx)
     L = c._lib
     a = _as_u8(data)
     out = _Bytes()
-    _check(L.zw_encode_frame_lossy(c.handle, _ptr(a), a.size, width, height, color, quality, method,
-                                   ctypes.byref(out)), "encode_frame_lossy", EncodingError)
+    _check(L.zw_encode_frame_lossy_ex(c.handle, _ptr(a), a.size, width, height, color, quality, method,
+                                      token_partitions, ctypes.byref(out)), "encode_frame_lossy", EncodingError)
     return _take_bytes(L, out)
 
 
-def encode_batch(images, width, height, color, quality=75, method=4, ctx=None):
+def encode_batch(images, width, height, color, quality=75, method=4, ctx=None, token_partitions=1):
     """Encode many same-sized frames in one device pass; returns list of VP8 frames."""
     c = _ctx(ctx)
     L = c._lib
@@ -283,7 +289,8 @@ def encode_batch(images, width, height, color, quality=75, method=4, ctx=None):
     for i, a in enumerate(arrs):
         imgs[i] = _Image(a.ctypes.data, a.size, width, height, color)
     outs = (_Bytes * n)()
-    _check(L.zw_encode_batch(c.handle, n, imgs, quality, method, outs), "encode_batch", EncodingError)
+    _check(L.zw_encode_batch_ex(c.handle, n, imgs, quality, method, token_partitions, outs), "encode_batch",
+           EncodingError)
     return [_take_bytes(L, outs[i]) for i in range(n)]
 
 
@@ -742,6 +749,10 @@ class Pipeline:
             ptrs = (ctypes.c_void_p * len(self._host_frames))(*[f.ctypes.data for f in self._host_frames])
         _check(self._lib.zw_pipe_set_container(self._h, 1 if enable else 0, ptrs), "zw_pipe_set_container",
                EncodingError)
+
+    def set_token_partitions(self, n):
+        """Token partitions (1, 2, 4, 8) of every frame (zw_pipe_set_token_partitions)."""
+        _check(self._lib.zw_pipe_set_token_partitions(self._h, n), "zw_pipe_set_token_partitions", EncodingError)
 
     def encode(self):
         _check(self._lib.zw_pipe_encode(self._h), "zw_pipe_encode", EncodingError)

@@ -133,6 +133,16 @@ typedef struct {
 int zw_encode_frame_lossy(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
                           int color, uint8_t quality, uint8_t method, zw_bytes *out);
 
+/* The same with token_partitions (1, 2, 4 or 8) residual partitions: MB row y's
+ * tokens go to partition y % n (the reference encoder's partition machinery,
+ * vp8.rs:352-354 / :1419-1421, fixed there at one partition, vp8.rs:273); the
+ * partition sizes follow the first partition as RFC 6386 9.5 and the reference
+ * decoder (decoder/vp8.rs:421-450) read them.  1 gives encode_frame_lossy's
+ * bytes.  A single frame's partitions are entropy-coded on parallel host
+ * threads.  ZW_EINVAL for any other count. */
+int zw_encode_frame_lossy_ex(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
+                             int color, uint8_t quality, uint8_t method, int token_partitions, zw_bytes *out);
+
 /* WebPEncoder::encode with EncoderParams::lossy(quality, method): RIFF container
  * ("VP8 " simple form; VP8X + ALPH + "VP8 " for LA8 / RGBA8 inputs). */
 int zw_encode_webp(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color,
@@ -150,6 +160,9 @@ int zw_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t he
 
 /* n independent frames of identical size/color; outs[i] receives frame i. */
 int zw_encode_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method, zw_bytes *outs);
+/* ... with token_partitions (1, 2, 4, 8) per frame, as zw_encode_frame_lossy_ex. */
+int zw_encode_batch_ex(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quality, uint8_t method,
+                       int token_partitions, zw_bytes *outs);
 /* n independent WebPEncoder::encode calls with EncoderParams::lossy(quality,
  * method) (api.rs:1291-1398; new: batch): outs[i] is frame i's RIFF container,
  * with VP8X + ALPH for LA8 / RGBA8.  The ALPH chunks are encoded on the host
@@ -246,6 +259,9 @@ int zw_pipe_upload(zw_pipe *p, int frame, const uint8_t *data, size_t len);
  * valid while the pipe encodes); host_frames may be NULL for L8 / RGB8.
  * enable = 0 switches back to bare frames. */
 int zw_pipe_set_container(zw_pipe *p, int enable, const uint8_t *const *host_frames);
+/* Token partitions (1, 2, 4, 8) of every frame the pipe emits (default 1);
+ * see zw_encode_frame_lossy_ex.  ZW_EINVAL for any other count. */
+int zw_pipe_set_token_partitions(zw_pipe *p, int nparts);
 /* Runs the full encode of all frames; bitstreams retrievable afterwards. */
 int zw_pipe_encode(zw_pipe *p);
 /* Encodes the uploaded batch n times back to back, streaming-style: batch k+1's

@@ -792,7 +792,8 @@ typedef struct {
     uint8_t *top_y, *top_u, *top_v;
     int8_t (*top_derr)[2][2];
     int8_t left_derr[2][2];
-    benc_t hdr, part;
+    benc_t hdr, parts[8], *part; /* token partitions; part = the current row's (mby % nparts) */
+    int nparts;
     or_enc_debug *dbg;
     int pass;
 } enc_t;
@@ -1489,32 +1490,32 @@ static int encode_coeffs(enc_t *e, const int32_t *blk, int plane, int ctx, const
         int a = or_abs(coeff);
         int token;
         if (a == 0) {
-            be_tree(&e->part, TOKEN_TREE, 22, pr, 0, start);
+            be_tree(e->part, TOKEN_TREE, 22, pr, 0, start);
             skip_eob = 1;
             token = 0;
         } else if (a <= 4) {
-            be_tree(&e->part, TOKEN_TREE, 22, pr, a, start);
+            be_tree(e->part, TOKEN_TREE, 22, pr, a, start);
             skip_eob = 0;
             token = a;
         } else {
             int cat = a <= 6 ? 5 : a <= 10 ? 6 : a <= 18 ? 7 : a <= 34 ? 8 : a <= 66 ? 9 : 10;
-            be_tree(&e->part, TOKEN_TREE, 22, pr, cat, start);
+            be_tree(e->part, TOKEN_TREE, 22, pr, cat, start);
             const uint8_t *cp = PROB_DCT_CAT[cat - 5];
             int extra = a - DCT_CAT_BASE[cat - 5];
             int mask = cat == 10 ? 1 << 10 : 1 << (cat - 5);
             for (int k = 0; k < 12 && cp[k]; k++) {
-                be_bool(&e->part, (extra & mask) > 0, cp[k]);
+                be_bool(e->part, (extra & mask) > 0, cp[k]);
                 mask >>= 1;
             }
             skip_eob = 0;
             token = cat;
         }
-        if (token != 0) be_flag(&e->part, !(coeff > 0));
+        if (token != 0) be_flag(e->part, !(coeff > 0));
         ctx = token == 0 ? 0 : (token == 1 ? 1 : 2);
     }
     if (eobi < 16) {
         int bi = first > eobi ? first : eobi;
-        be_tree(&e->part, TOKEN_TREE, 22, P[COEFF_BANDS[bi]][ctx], 11, 0);
+        be_tree(e->part, TOKEN_TREE, 22, P[COEFF_BANDS[bi]][ctx], 11, 0);
     }
     return eobi > 0;
 }
@@ -1637,6 +1638,20 @@ static void reset_row(enc_t *e)
 int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, int quality,
               int method, uint8_t **out, size_t *out_len, or_enc_debug *dbg)
 {
+    return or_encode_parts(data, len, width, height, color, quality, method, 1, out, out_len, dbg);
+}
+
+/* The same with `nparts` (1, 2, 4 or 8) token partitions: MB row y's residual
+ * tokens go to partition y % nparts (vp8.rs:1419-1421); the frame header codes
+ * log2(nparts) (vp8.rs:352-354).  Layout after the first partition follows RFC
+ * 6386 9.5 and the reference decoder (decoder/vp8.rs:421-450): the nparts - 1
+ * 3-byte little-endian sizes, then the partitions.  (The reference encoder's own
+ * write_partitions, vp8.rs:374-390, would interleave each size with its data;
+ * it is never reached, since the encoder always has one partition, vp8.rs:273,
+ * :1275.) */
+int or_encode_parts(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, int quality,
+                    int method, int nparts, uint8_t **out, size_t *out_len, or_enc_debug *dbg)
+{
     *out = NULL;
     *out_len = 0;
     /* error order follows the reference: u16 dims (vp8.rs:3143), data length
@@ -1647,9 +1662,11 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
     int bpp = bpp_of[color];
     if ((uint64_t)width * height * bpp != len) return OR_EINVALID_BUFFER_SIZE;
     if (quality > 100 || quality < 0) return OR_EINVAL;
+    if (nparts != 1 && nparts != 2 && nparts != 4 && nparts != 8) return OR_EINVAL;
 
     enc_t E, *e = &E;
     memset(e, 0, sizeof E);
+    e->nparts = nparts;
     e->dbg = dbg;
     e->width = (int)width;
     e->height = (int)height;
@@ -1801,7 +1818,7 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
     memset(e->top_y, 127, (size_t)e->mbw * 16 + 64);
     memset(e->top_u, 127, (size_t)e->mbw * 8 + 64);
     memset(e->top_v, 127, (size_t)e->mbw * 8 + 64);
-    be_init(&e->part);
+    for (int p = 0; p < e->nparts; p++) be_init(&e->parts[p]);
     be_init(&e->hdr);
 
     /* encode_compressed_frame_header vp8.rs:332-372 */
@@ -1831,7 +1848,7 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
     be_lit(&e->hdr, 6, e->filter_level);
     be_lit(&e->hdr, 3, e->sharpness);
     be_flag(&e->hdr, 0);                 /* loop_filter_adjustments */
-    be_lit(&e->hdr, 2, 0);               /* 1 partition */
+    be_lit(&e->hdr, 2, e->nparts == 8 ? 3 : e->nparts >> 1); /* log2(token partitions) */
     be_lit(&e->hdr, 7, e->qi);           /* yac_abs */
     for (int i = 0; i < 5; i++) be_flag(&e->hdr, 0); /* no deltas */
     be_lit(&e->hdr, 1, 0);               /* refresh entropy probs */
@@ -1859,6 +1876,7 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
     for (int mby = 0; mby < e->mbh; mby++) {
         reset_row(e);
         memset(e->left_derr, 0, sizeof e->left_derr);
+        e->part = &e->parts[mby % e->nparts];
         for (int mbx = 0; mbx < e->mbw; mbx++) {
             mbinfo_t mi;
             choose_mb(e, mbx, mby, &mi);
@@ -1885,10 +1903,14 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
         }
     }
     be_flush(&e->hdr);
-    be_flush(&e->part);
+    size_t plen = 0;
+    for (int p = 0; p < e->nparts; p++) {
+        be_flush(&e->parts[p]);
+        plen += e->parts[p].len;
+    }
 
     /* write_uncompressed_frame_header vp8.rs:315-330 + partitions */
-    size_t total = 10 + e->hdr.len + e->part.len;
+    size_t total = 10 + e->hdr.len + 3 * (size_t)(e->nparts - 1) + plen;
     uint8_t *o = (uint8_t *)malloc(total);
     uint32_t tag = ((uint32_t)e->hdr.len << 5) | (1u << 4);
     o[0] = (uint8_t)tag; o[1] = (uint8_t)(tag >> 8); o[2] = (uint8_t)(tag >> 16);
@@ -1896,11 +1918,19 @@ int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, 
     o[6] = (uint8_t)(width & 0xff); o[7] = (uint8_t)((width >> 8) & 0x3f);
     o[8] = (uint8_t)(height & 0xff); o[9] = (uint8_t)((height >> 8) & 0x3f);
     memcpy(o + 10, e->hdr.buf, e->hdr.len);
-    memcpy(o + 10 + e->hdr.len, e->part.buf, e->part.len);
+    size_t w = 10 + e->hdr.len;
+    for (int p = 0; p + 1 < e->nparts; p++, w += 3) {
+        o[w] = (uint8_t)e->parts[p].len; o[w + 1] = (uint8_t)(e->parts[p].len >> 8); o[w + 2] = (uint8_t)(e->parts[p].len >> 16);
+    }
+    for (int p = 0; p < e->nparts; p++) {
+        memcpy(o + w, e->parts[p].buf, e->parts[p].len);
+        w += e->parts[p].len;
+    }
     *out = o;
     *out_len = total;
 
-    free(e->hdr.buf); free(e->part.buf);
+    free(e->hdr.buf);
+    for (int p = 0; p < e->nparts; p++) free(e->parts[p].buf);
     free(e->Y); free(e->U); free(e->V);
     free(e->top_c); free(e->top_bpred); free(e->seg_map);
     free(e->top_y); free(e->top_u); free(e->top_v); free(e->top_derr);

@@ -65,6 +65,9 @@ typedef struct {
 /* encode_frame_lossy (encoder/vp8.rs:3132): raw VP8 frame bytes (malloc'd). */
 int or_encode(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, int quality,
               int method, uint8_t **out, size_t *out_len, or_enc_debug *dbg);
+/* ... with nparts (1, 2, 4, 8) token partitions (vp8.rs:352-354, :1419-1421). */
+int or_encode_parts(const uint8_t *data, size_t len, uint32_t width, uint32_t height, int color, int quality,
+                    int method, int nparts, uint8_t **out, size_t *out_len, or_enc_debug *dbg);
 void or_free(void *p);
 
 /* Vp8Decoder::decode_frame (decoder/vp8.rs:1526).  Planes are MB-aligned:

@@ -53,6 +53,8 @@ def lib():
         L.or_encode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+        L.or_encode_parts.restype = ctypes.c_int
+        L.or_encode_parts.argtypes = L.or_encode.argtypes[:7] + [ctypes.c_int] + L.or_encode.argtypes[7:]
         L.or_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_void_p] * 8
         L.or_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.or_free.argtypes = [ctypes.c_void_p]
@@ -108,8 +110,8 @@ def rgb_to_yuv420(img, w, h, bpp):
     return y, u, v
 
 
-def encode(img, w, h, color, quality=75, method=4, debug=False):
-    """Returns (rc, vp8_bytes, debug_dict_or_None)."""
+def encode(img, w, h, color, quality=75, method=4, debug=False, nparts=1):
+    """Returns (rc, vp8_bytes, debug_dict_or_None).  nparts: token partitions (1, 2, 4, 8)."""
     L = lib()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     out = ctypes.c_void_p()
@@ -134,8 +136,8 @@ def encode(img, w, h, color, quality=75, method=4, debug=False):
         dbg.p2_info = ctypes.addressof(p2)
         keep["p1_info"] = p1
         keep["p2_info"] = p2
-    rc = L.or_encode(_p(img), img.size, w, h, color, quality, method, ctypes.byref(out), ctypes.byref(n),
-                     ctypes.byref(dbg) if dbg is not None else None)
+    rc = L.or_encode_parts(_p(img), img.size, w, h, color, quality, method, nparts, ctypes.byref(out),
+                           ctypes.byref(n), ctypes.byref(dbg) if dbg is not None else None)
     data = b""
     if rc == 0:
         data = ctypes.string_at(out.value, n.value)

@@ -488,6 +488,20 @@ def test_transform_quant_blocks(ctx, q_dc, q_ac, mtype, first):
     assert np.array_equal(rc.astype(np.int32), orc)
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1025, 256 * 4 * 3 + 7])
+def test_transform_quant_blocks_ragged(ctx, n):
+    """Block counts off the wave / workgroup / unroll multiples (the tails)."""
+    rng = np.random.default_rng(n)
+    src = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    pred = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    lv, rc = zwebp.transform_quant_blocks(src, pred, 24, 30, 0, 0, ctx=ctx)
+    co = O.blocks("or_fdct_c", src.astype(np.int32) - pred.astype(np.int32))
+    olv, odq = O.quant_blocks(co, 0, 3, 0, False, 0, 24, 30, 0)
+    orc = np.clip(pred.astype(np.int32) + O.blocks("or_idct_c", odq).reshape(n, 16), 0, 255)
+    assert np.array_equal(lv.astype(np.int32), olv)
+    assert np.array_equal(rc.astype(np.int32), orc)
+
+
 def test_transform_quant_blocks_empty(ctx):
     lv, rc = zwebp.transform_quant_blocks(np.zeros((0, 16), np.uint8), np.zeros((0, 16), np.uint8), 24, 30, ctx=ctx)
     assert lv.shape == (0, 16)
