@@ -312,6 +312,12 @@ def single_frame(ctx, img, w, h, q, m, reps=3):
     for _ in range(reps):
         zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
     seam_ms = (time.perf_counter() - t0) / reps * 1e3
+    # the same seam with 8 token partitions, coded on parallel host threads
+    zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx, token_partitions=8)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx, token_partitions=8)
+    parts8_ms = (time.perf_counter() - t0) / reps * 1e3
     p = zwebp.Pipeline(1, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
     p.upload(0, img)
     p.encode()
@@ -322,7 +328,8 @@ def single_frame(ctx, img, w, h, q, m, reps=3):
     pipe_ms = (time.perf_counter() - t0) / reps * 1e3
     k = p.kernel_times()
     p.close()
-    return {"encode_frame_lossy_ms": seam_ms, "pipeline_1_frame_ms": pipe_ms,
+    return {"encode_frame_lossy_ms": seam_ms, "encode_frame_lossy_8_partitions_ms": parts8_ms,
+            "pipeline_1_frame_ms": pipe_ms,
             "kernel_ms": {"rgb2yuv": k[0], "analysis_segments": k[1], "encode_pass1": k[2], "encode_pass2": k[3]},
             "note": "one frame: the row-parallel encode kernels (one wave per MB row, rows handed over through "
                     "global memory); pass 1 is bounded by the chroma raster chain (quirk A5) on one wave"}
