@@ -223,36 +223,61 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
     // This lane's share of an MB and its edges (coalesced u32 loads): y = one
     // luma word; x = a chroma word (lanes < 32), the top row (32..39) or a left
     // pixel (40..63); x2 = the V left pixel (56..63); corner (lanes < 3).
+    // Branch-free: every lane issues the same three dword loads at lane-computed
+    // addresses (a byte is taken from its aligned dword when the MB is staged; a
+    // lane with nothing to fetch reads the frame's first word and discards it),
+    // so the next MB's loads stay in flight while this MB is analysed (a
+    // lane-divergent if-chain of loads made the compiler wait for each in turn).
+    //   y: one luma word;  x: lanes 0..31 chroma words (plane lane >> 4, row
+    //   (lane >> 1) & 7), 32..35 the luma top row, 36..39 the chroma top rows,
+    //   40..55 the luma left column (bytes), 56..63 the U left column (bytes);
+    //   z: lanes 0..2 the Y / U / V corner, 56..63 the V left column (bytes).
     struct AnFetch {
-        uint32_t y, x;
-        uint8_t x2, corner;
+        uint32_t y, xw, zw;
+        uint32_t m;  // bits 0..4: x byte shift, 5: x ok, 6: x is a byte; 8..12: z shift, 13: z ok
     };
     auto fetch = [&](int mb) {
-        AnFetch r = {0u, 0u, 0, 0};
+        AnFetch r = {0u, 0u, 0u, 0u};
         if (mb >= nmb) return r;
         const int mbx = mb % mbw, mby = mb / mbw;
         const bool ht = mby > 0, hl = mbx > 0;
-        r.y = ((const uint32_t*)(Yf + (size_t)(mby * 16 + (lane >> 2)) * ys + mbx * 16))[lane & 3];
+        r.y = *(const uint32_t*)(Yf + (size_t)(mby * 16 + (lane >> 2)) * ys + mbx * 16 + 4 * (lane & 3));
+        const int rr = (lane >> 1) & 7, w = lane & 1, cr = lane - 56;
+        const uint8_t* xp;
+        size_t xo;
+        bool xok = true, xbyte = false;
         if (lane < 32) {
-            const int pl = lane >> 4, rr = (lane >> 1) & 7, w = lane & 1;
-            r.x = ((const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + rr) * cs + mbx * 8))[w];
+            xp = lane >> 4 ? Vf : Uf;
+            xo = (size_t)(mby * 8 + rr) * cs + mbx * 8 + 4 * w;
         } else if (lane < 36) {
-            r.x = ht ? ((const uint32_t*)(Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16))[lane - 32] : 0u;
+            xp = Yf;
+            xo = (size_t)(mby * 16 - 1) * ys + mbx * 16 + 4 * (lane - 32);
+            xok = ht;
         } else if (lane < 40) {
-            const int pl = (lane - 36) >> 1, w = lane & 1;
-            r.x = ht ? ((const uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 - 1) * cs + mbx * 8))[w] : 0u;
+            xp = ((lane - 36) >> 1) ? Vf : Uf;
+            xo = (size_t)(mby * 8 - 1) * cs + mbx * 8 + 4 * w;
+            xok = ht;
         } else if (lane < 56) {
-            r.x = hl ? Yf[(size_t)(mby * 16 + lane - 40) * ys + mbx * 16 - 1] : 0u;
+            xp = Yf;
+            xo = (size_t)(mby * 16 + lane - 40) * ys + mbx * 16 - 1;
+            xok = hl;
+            xbyte = true;
         } else {
-            const int rr = lane - 56;  // 0..7: U and V left columns
-            r.x = hl ? Uf[(size_t)(mby * 8 + rr) * cs + mbx * 8 - 1] : 0u;
-            r.x2 = hl ? Vf[(size_t)(mby * 8 + rr) * cs + mbx * 8 - 1] : (uint8_t)0;
+            xp = Uf;
+            xo = (size_t)(mby * 8 + cr) * cs + mbx * 8 - 1;
+            xok = hl;
+            xbyte = true;
         }
-        if (lane < 3) {
-            const uint8_t* P = lane == 0 ? Yf : (lane == 1 ? Uf : Vf);
-            const int st = lane == 0 ? ys : cs, sz = lane == 0 ? 16 : 8;
-            r.corner = (ht && hl) ? P[(size_t)(mby * sz - 1) * st + mbx * sz - 1] : (uint8_t)0;
-        }
+        const int zsz = lane == 0 ? 16 : 8, zst = lane == 0 ? ys : cs;
+        const uint8_t* zp = lane < 3 ? (lane == 0 ? Yf : (lane == 1 ? Uf : Vf)) : Vf;
+        const size_t zo = lane < 3 ? (size_t)(mby * zsz - 1) * zst + mbx * zsz - 1 : (size_t)(mby * 8 + cr) * cs + mbx * 8 - 1;
+        const bool zok = lane < 3 ? (ht && hl) : (lane >= 56 && hl);
+        xo = xok ? xo : 0;
+        const size_t zo2 = zok ? zo : 0;
+        r.xw = *(const uint32_t*)((xok ? xp : Yf) + (xo & ~(size_t)3));
+        r.zw = *(const uint32_t*)((zok ? zp : Yf) + (zo2 & ~(size_t)3));
+        r.m = (uint32_t)(8 * (xo & 3)) | (xok ? 32u : 0u) | (xbyte ? 64u : 0u) | ((uint32_t)(8 * (zo2 & 3)) << 8) |
+              (zok ? 0x2000u : 0u);
         return r;
     };
     // ZW_AN_MPW MBs per wave, the workgroup's 4 waves on adjacent MBs; each
@@ -269,16 +294,18 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
         // tiles: [plane][row][col] with interior rows 0..15 / 0..7, top row, left column, corner
         AnalysisTile* A = &tile[wv];
         const bool ht = mby > 0, hl = mbx > 0;
+        const uint32_t xm = (cur.m & 32u) ? ((cur.m & 64u) ? (cur.xw >> (cur.m & 31u)) & 255u : cur.xw) : 0u;
+        const uint8_t zb = (cur.m & 0x2000u) ? (uint8_t)(cur.zw >> ((cur.m >> 8) & 31u)) : (uint8_t)0;
         A->y[lane >> 2][lane & 3] = cur.y;
-        if (lane < 32) A->c[lane >> 4][(lane >> 1) & 7][lane & 1] = cur.x;
-        else if (lane < 36) A->ytop[lane - 32] = cur.x;
-        else if (lane < 40) A->ctop[(lane - 36) >> 1][lane & 1] = cur.x;
-        else if (lane < 56) A->yleft[lane - 40] = (uint8_t)cur.x;
+        if (lane < 32) A->c[lane >> 4][(lane >> 1) & 7][lane & 1] = xm;
+        else if (lane < 36) A->ytop[lane - 32] = xm;
+        else if (lane < 40) A->ctop[(lane - 36) >> 1][lane & 1] = xm;
+        else if (lane < 56) A->yleft[lane - 40] = (uint8_t)xm;
         else {
-            A->cleft[0][lane - 56] = (uint8_t)cur.x;
-            A->cleft[1][lane - 56] = cur.x2;
+            A->cleft[0][lane - 56] = (uint8_t)xm;
+            A->cleft[1][lane - 56] = zb;
         }
-        if (lane < 3) A->corner[lane] = cur.corner;
+        if (lane < 3) A->corner[lane] = zb;
         wsync();
         uint8_t bins[16];
         uint32_t z = 0;

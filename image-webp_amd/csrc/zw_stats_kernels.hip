@@ -124,9 +124,10 @@ __device__ __forceinline__ void zs_walk(const int16_t* lv, int eob, int t, int f
 // Token context of block b of MB mb (raster), from the neighbours' flags
 // (record_residual_stats' left/top contexts; skipped MBs read as zero, and
 // the Y2 context skips over I4 MBs, which neither set nor clear it).
-__device__ __forceinline__ int zs_ctx(const uint32_t* fl, int mb, int mbx, int mby, int mbw, int b)
+template <class FL>
+__device__ __forceinline__ int zs_ctx_f(FL&& flag, int mb, int mbx, int mby, int mbw, int b)
 {
-    auto nz = [&](int m, int bb) -> int { return (int)((fl[m] >> bb) & 1u); };
+    auto nz = [&](int m, int bb) -> int { return (int)((flag(m) >> bb) & 1u); };
     int l = 0, t = 0;
     if (b < 16) {
         const int bx = b & 3, by = b >> 2;
@@ -134,12 +135,12 @@ __device__ __forceinline__ int zs_ctx(const uint32_t* fl, int mb, int mbx, int m
         t = by > 0 ? nz(mb, b - 4) : (mby > 0 ? nz(mb - mbw, b + 12) : 0);
     } else if (b == 16) {
         for (int x = mbx - 1; x >= 0; x--)
-            if (!(fl[mb - (mbx - x)] & ZS_I4)) {
+            if (!(flag(mb - (mbx - x)) & ZS_I4)) {
                 l = nz(mb - (mbx - x), 16);
                 break;
             }
         for (int y = mby - 1; y >= 0; y--)
-            if (!(fl[mb - (mby - y) * mbw] & ZS_I4)) {
+            if (!(flag(mb - (mby - y) * mbw) & ZS_I4)) {
                 t = nz(mb - (mby - y) * mbw, 16);
                 break;
             }
@@ -149,6 +150,10 @@ __device__ __forceinline__ int zs_ctx(const uint32_t* fl, int mb, int mbx, int m
         t = by > 0 ? nz(mb, b - 2) : (mby > 0 ? nz(mb - mbw, b + 2) : 0);
     }
     return min(l + t, 2);
+}
+__device__ __forceinline__ int zs_ctx(const uint32_t* fl, int mb, int mbx, int mby, int mbw, int b)
+{
+    return zs_ctx_f([&](int m) { return fl[m]; }, mb, mbx, mby, mbw, b);
 }
 
 // Walk the decisions of MB mb's blocks of token type t (a counter's type), in
@@ -175,55 +180,86 @@ __device__ __forceinline__ void zs_rec(uint32_t& s, int bit)
     s += 0x00010000u + (bit ? 1u : 0u);
 }
 
-// Per-MB flags (bits 0..24 non-zero blocks, ZS_I4, ZS_SKIP): one thread per MB.
+// Per-MB flags (bits 0..24 non-zero blocks, ZS_I4, ZS_SKIP): 32 lanes per MB,
+// lane b < 25 reads block b's 16 levels (the MB's record is read as one
+// contiguous run across the lanes) and the half-wave ballot forms the mask.
 extern "C" __global__ __launch_bounds__(256) void k_stats_flags(const ZwMbOut* __restrict__ mbs, int nmb,
                                                               uint32_t* __restrict__ fl)
 {
-    const int mb = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
-    if (mb >= nmb) return;
-    const ZwMbOut& M = mbs[(size_t)f * nmb + mb];
+    const int b = threadIdx.x & 31, f = blockIdx.y;
+    const int mb = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const bool in = mb < nmb;
+    const ZwMbOut& M = mbs[(size_t)f * nmb + (in ? mb : 0)];
     const bool i4 = M.luma_mode == 4;
-    const int first = i4 ? 0 : 1;
-    uint32_t m = 0;
-#pragma unroll
-    for (int b = 0; b < 25; b++) {
+    int nzb = 0;
+    if (in && b < 25) {
         const int e = zs_eob(M.levels[b]);
-        const int nzb = b < 16 ? e > first : e > 0;
-        if (b != 16 || !i4) m |= (uint32_t)nzb << b;
+        nzb = b < 16 ? e > (i4 ? 0 : 1) : (b == 16 ? (!i4 && e > 0) : e > 0);
     }
+    const unsigned long long bal = __ballot(nzb);
+    uint32_t m = (uint32_t)(bal >> (threadIdx.x & 32));
     // check_all_coeffs_zero on the pass-1 levels (mb_all_zero_p1)
     if (m == 0) m = ZS_SKIP;
-    fl[(size_t)f * nmb + mb] = m | (i4 ? ZS_I4 : 0u);
+    if (in && b == 0) fl[(size_t)f * nmb + mb] = m | (i4 ? ZS_I4 : 0u);
 }
 
 // Per-stripe (decisions, ones) of every counter.  Copy j of the counters takes
 // the items it = j (mod ZS_COPIES) of the stripe: <= ceil(512 * 25 / 16) blocks,
 // each adding <= 9 decisions to one counter (band 6 spans 9 positions), so the
 // packed 16:16 copy cannot carry (14 400 < 65 536 even at 8 copies).
+// The stripe's flags and the MB row above it are staged in LDS first, so a
+// block's context costs no dependent global load, and each block's levels are
+// loaded one item ahead of its walk.
+#define ZS_FL_MAX (ZS_STRIPE + 1024)  // staged flags: the stripe + up to 1024 MBs of the row above
 extern "C" __global__ __launch_bounds__(ZS_HWG) void k_stats_hist(const ZwMbOut* __restrict__ mbs,
                                                                 const uint32_t* __restrict__ flags, int mbw, int mbh,
                                                                 uint2* __restrict__ part)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cp = (uint32_t*)smem;  // [ZS_COPIES][ZS_NCTR] (decisions << 16) | ones
+    uint32_t* sfl = cp + ZS_COPIES * ZS_NCTR;  // [ZS_FL_MAX] flags of MBs lo .. mb1 - 1
     const int st = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, nst = gridDim.x;
     const int nmb = mbw * mbh;
     const ZwMbOut* F = mbs + (size_t)f * nmb;
     const uint32_t* fl = flags + (size_t)f * nmb;
-    for (int i = tid; i < ZS_COPIES * ZS_NCTR; i += ZS_HWG) cp[i] = 0;
-    __syncthreads();
-    uint32_t* my = cp + (tid & (ZS_COPIES - 1)) * ZS_NCTR;
     const int mb0 = st * ZS_STRIPE, mb1 = min(nmb, mb0 + ZS_STRIPE);
-    for (int it = tid; it < (mb1 - mb0) * 25; it += ZS_HWG) {
+    const int lo = max(0, mb0 - min(mbw, 1024));
+    for (int i = tid; i < ZS_COPIES * ZS_NCTR; i += ZS_HWG) cp[i] = 0;
+    for (int m = lo + tid; m < mb1; m += ZS_HWG) sfl[m - lo] = fl[m];
+    __syncthreads();
+    auto flag = [&](int m) -> uint32_t { return m >= lo ? sfl[m - lo] : fl[m]; };
+    uint32_t* my = cp + (tid & (ZS_COPIES - 1)) * ZS_NCTR;
+    const int nit = (mb1 - mb0) * 25;
+    // (ZwMbOut records are 4-byte aligned: the levels are read as words)
+    struct Lv {
+        uint32_t w[8];
+    };
+    auto lv_of = [&](int it) {
+        Lv r;
+        const uint32_t* p = (const uint32_t*)F[mb0 + it / 25].levels[it % 25];
+#pragma unroll
+        for (int k = 0; k < 8; k++) r.w[k] = p[k];
+        return r;
+    };
+    Lv nx;
+    if (tid < nit) nx = lv_of(tid);
+    for (int it = tid; it < nit; it += ZS_HWG) {
+        const Lv cur = nx;
+        if (it + ZS_HWG < nit) nx = lv_of(it + ZS_HWG);
         const int mb = mb0 + it / 25, b = it % 25;
-        const uint32_t fm = fl[mb];
+        const uint32_t fm = sfl[mb - lo];
         if (fm & ZS_SKIP) continue;
         const bool i4 = (fm & ZS_I4) != 0;
         if (b == 16 && i4) continue;
         const int t = b < 16 ? (i4 ? 3 : 0) : (b == 16 ? 1 : 2);
         const int first = b < 16 && !i4 ? 1 : 0;
-        const int ctx = zs_ctx(fl, mb, mb % mbw, mb / mbw, mbw, b);
-        const int16_t* lv = F[mb].levels[b];
+        const int ctx = zs_ctx_f(flag, mb, mb % mbw, mb / mbw, mbw, b);
+        int16_t lv[16];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            lv[2 * k] = (int16_t)(cur.w[k] & 0xffffu);
+            lv[2 * k + 1] = (int16_t)(cur.w[k] >> 16);
+        }
         zs_walk(lv, zs_eob(lv), t, first, ctx, [&](int c, int bit) { atomicAdd(&my[c], 0x10000u + (bit ? 1u : 0u)); });
     }
     __syncthreads();
@@ -357,9 +393,9 @@ extern "C" hipError_t zwk_stats(hipStream_t s, const ZwMbOut* mbs, int mbw, int 
     if (nmb <= 0 || nframes <= 0) return hipErrorInvalidValue;
     uint32_t* fl = (uint32_t*)scratch;
     uint2* part = (uint2*)((uint8_t*)scratch + (size_t)nframes * zs_flag_bytes(nmb));
-    hipLaunchKernelGGL(k_stats_flags, dim3((nmb + 255) / 256, nframes), dim3(256), 0, s, mbs, nmb, fl);
-    hipLaunchKernelGGL(k_stats_hist, dim3(nst, nframes), dim3(ZS_HWG), (size_t)ZS_COPIES * ZS_NCTR * 4, s, mbs, fl,
-                       mbw, mbh, part);
+    hipLaunchKernelGGL(k_stats_flags, dim3((nmb + 7) / 8, nframes), dim3(256), 0, s, mbs, nmb, fl);
+    hipLaunchKernelGGL(k_stats_hist, dim3(nst, nframes), dim3(ZS_HWG), (size_t)(ZS_COPIES * ZS_NCTR + ZS_FL_MAX) * 4, s,
+                       mbs, fl, mbw, mbh, part);
     const size_t lds0 = ZS_NCTR * 4 + 8;
     const int fl_lds = lds0 + (size_t)nmb * 4 <= 160 * 1024;
     hipLaunchKernelGGL(k_stats_final, dim3(nframes), dim3(ZS_WG), lds0 + (fl_lds ? (size_t)nmb * 4 : 0), s, mbs, fl,

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Parity tests of the default library (TESTS, -k KSEL), then an alternating
+# A/B of short verified benches: tools/gpu_ab2.sh libA.so libB.so [reps]
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+fatal() { case $1 in 124|137|134|139|135|132) return 0;; *) return 1;; esac; }
+tools/gpu_step.sh ab_tests 400 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py tests/test_gpu_batch.py} -q -x --timeout 300 --timeout-method thread ${KSEL:+-k "$KSEL"} || exit $?
+for r in $(seq 1 ${3:-2}); do
+  for lib in "$1" "$2"; do
+    n=$(basename $lib .so)
+    ZWEBP_LIB=$PWD/image-webp_amd/zwebp/$lib timeout -k 10 200 python bench.py --steps ${STEPS:-10} --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/ab_${n}_$r.log 2>&1; rc=$?
+    echo "== $n rep $r rc=$rc"; grep '^{' gpurun_out/ab_${n}_$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value'],1), d['verified'], {k: round(v,2) for k,v in d['kernel_ms_per_launch'].items()})"
+    fatal $rc && exit $rc
+  done
+done
+exit 0
