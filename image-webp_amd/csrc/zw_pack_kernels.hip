@@ -101,7 +101,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restr
 }
 
 // MB sizes are even (header 26 or 34 bytes + 2 per level) and so are the
-// frame slices, so every level lands on a 2-byte aligned address.
+// frame slices, so every level lands on a 2-byte aligned address.  The eobs
+// are recomputed from the level words (as k_pack_size does) rather than read
+// back, so every load of a wave is issued in one round: the MB's words, its
+// header and its offset.
 extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
     const ZwMbOut* __restrict__ mbs, int nmb, int nframes, const uint8_t* __restrict__ eobs,
     const uint32_t* __restrict__ offs, const unsigned long long* __restrict__ frame_info, uint8_t* __restrict__ out)
@@ -111,12 +114,30 @@ extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
     if (mb >= (size_t)nmb * nframes) return;
     const int f = (int)(mb / nmb);
     const ZwMbOut& M = mbs[mb];
+    const uint32_t* W = (const uint32_t*)&M.levels[0][0];
+    uint32_t w[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) w[r] = lane + 64 * r < 200 ? W[lane + 64 * r] : 0u;
+    const uint32_t hw = *(const uint32_t*)&M;  // luma, chroma, skip, segment
+    const uint32_t bp = lane < 8 ? *(const uint16_t*)&M.bpred[2 * lane] : 0u;
     uint8_t* o = out + frame_info[2 * f] + offs[mb];
-    const int luma = M.luma_mode;
+    const int luma = (int)(hw & 255u), chroma = (int)((hw >> 8) & 255u), skip = (int)((hw >> 16) & 255u),
+              seg = (int)(hw >> 24);
     const int hdr = 1 + (luma == 4 ? 8 : 0);
-    if (lane == 0) o[0] = (uint8_t)(luma | (M.skip << 3) | (M.segment << 4) | (M.chroma_mode << 6));
-    if (luma == 4 && lane < 8) o[1 + lane] = (uint8_t)(M.bpred[2 * lane] | (M.bpred[2 * lane + 1] << 4));
-    const int eob = lane < 25 ? eobs[mb * 25 + lane] : 0;
+    // eob of block j >> 3 in every lane of its 8-lane group, per round
+    int eb4[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) eb4[r] = skip ? 0 : max8(pk_word_eob(w[r], lane + 64 * r));
+    // block b's eob into lane b (lanes 0..24): group b lives in round b >> 3, lanes 8 (b & 7)..
+    int eob = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int v = __shfl(eb4[r], 8 * (lane & 7));
+        eob = (lane >> 3) == r ? v : eob;
+    }
+    eob = lane < 25 ? eob : 0;
+    if (lane == 0) o[0] = (uint8_t)(luma | (skip << 3) | (seg << 4) | (chroma << 6));
+    if (luma == 4 && lane < 8) o[1 + lane] = (uint8_t)((bp & 15u) | (((bp >> 8) & 15u) << 4));
     if (lane < 25) o[hdr + lane] = (uint8_t)eob;
     // exclusive prefix of eobs over lanes 0..24
     int pre = eob;
@@ -127,14 +148,13 @@ extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
     }
     pre -= eob;
     int16_t* lv = (int16_t*)(o + hdr + 25);
-    const uint32_t* W = (const uint32_t*)&M.levels[0][0];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int j = lane + 64 * r;
         const int b = min(j >> 3, 24), n0 = 2 * (j & 7);
-        const int eb = __shfl(eob, b), st = __shfl(pre, b);
+        const int eb = eb4[r], st = __shfl(pre, b);
         if (j < 200 && n0 < eb) {
-            const uint32_t v = W[j];
+            const uint32_t v = w[r];
             lv[st + n0] = (int16_t)(v & 0xffffu);
             if (n0 + 1 < eb) lv[st + n0 + 1] = (int16_t)(v >> 16);
         }
