@@ -633,6 +633,7 @@ struct EncArgs {
     int mbw, mbh, pass;
     int* dbg;                   // optional pass-2 I4 dump (16*34 ints per MB), may be null
     uint8_t* rows;              // row-parallel kernels: zero-filled ZW_ROWS_HDR + nframes * RowsLayout::frame
+    uint32_t* sizes;            // pass 2, may be null: per MB its packed record size (zw_pack_kernels.hip)
 };
 
 // per-wave LDS scratch
@@ -3051,6 +3052,22 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 }
                 store_chroma_borders(C);
                 write_levels(C, 0, 25, skip);
+                if (a.sizes) {
+                    // the packed record size k_pack_size would compute from these
+                    // levels: header, eob bytes and every block's levels up to its eob
+                    int e = 0;
+                    if (lane < 25 && !skip) {
+                        const uint32_t* lw = (const uint32_t*)W->lev[lane];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const uint32_t v = lw[q];
+                            e = (v >> 16) ? 2 * q + 2 : ((v & 0xffffu) ? 2 * q + 1 : e);
+                        }
+                    }
+                    const int es = wave_sum(e);
+                    if (lane == 0)
+                        a.sizes[(size_t)f * nmb + (size_t)mby * mbw + mbx] = (uint32_t)(1 + (lm == 4 ? 8 : 0) + 25 + 2 * es);
+                }
             } else {
                 write_levels(C, 0, 17, false);
                 if (lane == 0) o->skip = 0;  // pass-1 skip is decided on the host from the levels
@@ -3258,10 +3275,11 @@ extern "C" size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes)
 extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                                  const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost,
                                  int8_t* derr, ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz,
-                                 size_t csz, int mbw, int mbh, int nframes, int* dbg, uint8_t* rows)
+                                 size_t csz, int mbw, int mbh, int nframes, int* dbg, uint8_t* rows, uint32_t* sizes)
 {
     EncArgs a;
     a.dbg = dbg;
+    a.sizes = pass == 2 ? sizes : nullptr;
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
     a.rows = rows;

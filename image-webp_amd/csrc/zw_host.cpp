@@ -37,7 +37,7 @@ hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParam
 hipError_t zwk_stats(hipStream_t s, const ZwMbOut* mbs, int mbw, int mbh, void* scratch, void* out, int nframes);
 size_t zw_stats_scratch_bytes(int nmb, int nframes);
 hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
-                     unsigned long long* counter, unsigned long long* frame_info, uint8_t* out);
+                     unsigned long long* counter, unsigned long long* frame_info, uint8_t* out, int sizes_ready);
 hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m, int first,
                           void* levels, void* recon, int cus);
 hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
@@ -45,7 +45,7 @@ hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                       const uint8_t* alpha, const ZwFrameParams* params, const ZwLevelCosts* lcost, int8_t* derr,
                       ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
-                      int nframes, int* dbg, uint8_t* rows);
+                      int nframes, int* dbg, uint8_t* rows, uint32_t* sizes = nullptr);
 size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
 }
 
@@ -611,6 +611,17 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
     return ZW_OK;
 }
 
+// Pass 2 writes each MB's packed record size (EncArgs::sizes), so packing
+// its records skips k_pack_size.  ZW_PASS2_SIZES=0 restores the separate kernel.
+static bool pass2_sizes(const zw_pipe* p)
+{
+    static const bool on = []() {
+        const char* e = getenv("ZW_PASS2_SIZES");
+        return !(e && atoi(e) == 0);
+    }();
+    return on && p->d_sizes != nullptr;
+}
+
 // Pack the chunk's MB records on the kernel stream (right after the pass that
 // produced them: the encode kernels occupy every CU, so a pack kernel queued
 // elsewhere would wait for the next chunk's pass).  slot: 2*chunk + pass-1.
@@ -621,7 +632,7 @@ static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_
                                // the pass-1 buffers while the host is still fetching pass-2 data)
     HIPOK(zwk_pack(L.stream, d_out + F * p->nmb, p->nmb, na, p->d_eobs + F * p->nmb * 25, p->d_sizes + F * p->nmb,
                    L.d_ctr + slot, (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
-                   (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride));
+                   (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, p2 && pass2_sizes(p)));
     return ZW_OK;
 }
 
@@ -701,7 +712,8 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
     HIPOK(zwk_encode(s, 2, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
                      p->d_params + F, p->d_lcost + F, p->d_derr + F * p->mbw * 4, p->d_out2 + F * p->nmb,
                      p->d_ry + F * p->ysz, p->d_ru + F * p->csz, p->d_rv + F * p->csz, p->ysz, p->csz, p->mbw, p->mbh,
-                     na, p->d_dbg ? p->d_dbg + F * p->nmb * 16 * 34 : nullptr, L.d_rows));
+                     na, p->d_dbg ? p->d_dbg + F * p->nmb * 16 * 34 : nullptr, L.d_rows,
+                     pass2_sizes(p) ? p->d_sizes + F * p->nmb : nullptr));
     if (timed) HIPOK(hipEventRecord(L.ev[5], s));
     return ZW_OK;
 }

@@ -161,14 +161,18 @@ extern "C" __global__ __launch_bounds__(64 * PK_WAVES) void k_pack_write(
     }
 }
 
+// sizes_ready: the producing pass already wrote the MB sizes (pass 2 does; see
+// EncArgs::sizes), so k_pack_size is skipped.
 extern "C" hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uint8_t* eobs, uint32_t* sizes,
-                               unsigned long long* counter, unsigned long long* frame_info, uint8_t* out)
+                               unsigned long long* counter, unsigned long long* frame_info, uint8_t* out,
+                               int sizes_ready)
 {
     const size_t total = (size_t)nmb * nframes;
     const unsigned grid = (unsigned)((total + PK_WAVES - 1) / PK_WAVES);
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);  // this chunk's own counter
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pack_size, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes);
+    if (!sizes_ready)
+        hipLaunchKernelGGL(k_pack_size, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes);
     hipLaunchKernelGGL(k_pack_scan, dim3(nframes), dim3(1024), 0, s, sizes, nmb, counter, frame_info);
     hipLaunchKernelGGL(k_pack_write, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes, frame_info,
                        out);
