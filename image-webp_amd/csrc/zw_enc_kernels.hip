@@ -2175,9 +2175,10 @@ __device__ void store_chroma_borders(const Ctx& C)
 __device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
 {
     ZwMbOut* o = C.a->out + (size_t)C.f * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx;
-    int16_t* dst = &o->levels[0][0];
-    const int16_t* srcl = &C.W->lev[0][0];
-    for (int k = C.lane; k < nblk * 16; k += 64) dst[first_blk * 16 + k] = zero ? (int16_t)0 : srcl[first_blk * 16 + k];
+    // as words (ZwMbOut records and the LDS levels are 4-byte aligned)
+    uint32_t* dst = (uint32_t*)&o->levels[first_blk][0];
+    const uint32_t* srcl = (const uint32_t*)&C.W->lev[first_blk][0];
+    for (int k = C.lane; k < nblk * 8; k += 64) dst[k] = zero ? 0u : srcl[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -3064,7 +3065,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                             e = (v >> 16) ? 2 * q + 2 : ((v & 0xffffu) ? 2 * q + 1 : e);
                         }
                     }
-                    const int es = wave_sum(e);
+                    // lanes 0..24 hold the eobs: DPP sums per 16-lane row, rows 0 and 1 added
+                    const int r16 = red16(e);
+                    const int es = __builtin_amdgcn_readlane(r16, 0) + __builtin_amdgcn_readlane(r16, 16);
                     if (lane == 0)
                         a.sizes[(size_t)f * nmb + (size_t)mby * mbw + mbx] = (uint32_t)(1 + (lm == 4 ? 8 : 0) + 25 + 2 * es);
                 }
