@@ -370,16 +370,19 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
         // coefficients (256 luma, 128 chroma), no other bin can exceed it, so
         // max_value = that count and last_non_zero = the largest bin index.
         // Sums over the 8-lane groups, then the luma 16-lane groups.
+        // (DPP: quad xor 1, quad xor 2, row half mirror give each 8-lane group's
+        // total in all its lanes; the row mirror then pairs the row's two groups)
         uint32_t zs = z;
         int vm = vmax;
-#pragma unroll
-        for (int o2 = 1; o2 <= 4; o2 <<= 1) {
-            zs += (uint32_t)__shfl_xor((int)zs, o2);
-            vm = max(vm, __shfl_xor(vm, o2));
-        }
+        zs += (uint32_t)DPP((int)zs, 0xB1);
+        vm = max(vm, DPP(vm, 0xB1));
+        zs += (uint32_t)DPP((int)zs, 0x4E);
+        vm = max(vm, DPP(vm, 0x4E));
+        zs += (uint32_t)DPP((int)zs, 0x141);
+        vm = max(vm, DPP(vm, 0x141));
         {
-            const uint32_t zo = (uint32_t)__shfl_xor((int)zs, 8);
-            const int vo = __shfl_xor(vm, 8);
+            const uint32_t zo = (uint32_t)DPP((int)zs, 0x140);
+            const int vo = DPP(vm, 0x140);
             if (lane < 32) {
                 zs += zo;
                 vm = max(vm, vo);
@@ -414,8 +417,11 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
             for (int ps = 0; ps < 2; ps++) {
                 const uint32_t c = hist[wv][2 * ps + (lane >> 5)][lane & 31];
                 uint32_t mx = c;
-#pragma unroll
-                for (int o2 = 16; o2 >= 1; o2 >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o2));
+                mx = max(mx, (uint32_t)DPP((int)mx, 0xB1));
+                mx = max(mx, (uint32_t)DPP((int)mx, 0x4E));
+                mx = max(mx, (uint32_t)DPP((int)mx, 0x141));
+                mx = max(mx, (uint32_t)DPP((int)mx, 0x140));
+                mx = max(mx, (uint32_t)__shfl_xor((int)mx, 16));
                 const uint32_t half = (uint32_t)(__ballot(c > 0) >> (lane & 32));
                 const int lnz = half ? 31 - __clz((int)half) : 1;
                 const int ah = mx > 1 ? (int)(510u * (uint32_t)lnz / mx) : 0;
