@@ -28,13 +28,20 @@
 #include "zw_dev.h"
 
 #define ZS_WG 1024
-#define ZS_STRIPE 512
+// Stripe of MBs per k_stats_hist workgroup and lane-private LDS copies of the
+// counters: measured per 256 1080p frames (hist + final), 512 / 16 copies:
+// 1.37 + 0.78 ms; 128 / 4: 1.06 + 0.29 ms (small stripes bound the MB walk of
+// a heavy counter's exact replay to 128 MBs; few copies leave LDS for four
+// workgroups per CU).
+#ifndef ZS_STRIPE
+#define ZS_STRIPE 128
+#endif
 #ifndef ZS_COPIES
-#define ZS_COPIES 16
+#define ZS_COPIES 4
 #endif
 static_assert((ZS_STRIPE * 25 + ZS_COPIES - 1) / ZS_COPIES * 9 < 65536, "a packed 16:16 copy must not carry");
 #ifndef ZS_HWG
-#define ZS_HWG 512  // k_stats_hist workgroup size (16 copies x 512 threads: two workgroups per CU)
+#define ZS_HWG 512  // k_stats_hist workgroup size
 #endif
 #define ZS_NCTR (4 * 8 * 3 * 11)
 
@@ -204,7 +211,7 @@ extern "C" __global__ __launch_bounds__(256) void k_stats_flags(const ZwMbOut* _
 }
 
 // Per-stripe (decisions, ones) of every counter.  Copy j of the counters takes
-// the items it = j (mod ZS_COPIES) of the stripe: <= ceil(512 * 25 / 16) blocks,
+// the items it = j (mod ZS_COPIES) of the stripe: <= ceil(ZS_STRIPE * 25 / ZS_COPIES) blocks,
 // each adding <= 9 decisions to one counter (band 6 spans 9 positions), so the
 // packed 16:16 copy cannot carry (14 400 < 65 536 even at 8 copies).
 // The stripe's flags and the MB row above it are staged in LDS first, so a
