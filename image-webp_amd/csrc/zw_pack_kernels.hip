@@ -16,7 +16,9 @@
 // k_pack_write: one wave per MB.
 #include "zw_dev.h"
 
-#define PK_WAVES 4
+#ifndef PK_WAVES
+#define PK_WAVES 4  // MBs (one wave each) per workgroup
+#endif
 
 __device__ __forceinline__ int pk_mb_size(int luma, int eobsum) { return 1 + (luma == 4 ? 8 : 0) + 25 + 2 * eobsum; }
 
