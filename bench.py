@@ -570,6 +570,9 @@ def main():
                        **({"total_frames": a.total_frames} if a.total_frames else {})},
             "kernel_ms_per_step": {"rgb2yuv": float(k[0]), "analysis_segments": float(k[1]),
                                    "encode_pass1": float(k[2]), "encode_pass2": p2_ms, "launch_frames": per_launch},
+            "kernel_ms_per_step_note": "HIP-event spans per launch on each lane's stream in the pipelined two-lane "
+                                       "run: a span includes waiting for the other lane's kernels, so the phases "
+                                       "do not add up to the step; kernel_ms_per_launch has one-lane kernel times",
             "host_ms_per_step": {"fetch_pass1": float(k[4]), "stats_probs": float(k[5]),
                                  "fetch_pass2": float(k[6]), "emit": float(k[7]), "threads": threads},
             "host_emit_frames_per_s_per_core": B / (emit_s * threads) if emit_s > 0 else None,
