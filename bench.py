@@ -59,12 +59,25 @@ sys.path.insert(0, os.path.join(ROOT, "image-webp_amd"))
 ALG_BYTES_PER_MB = 1568           # src YUV 384 + levels 800 + recon 384
 ALG_BYTES_PER_BLOCK = 64          # the same per 4x4 block: src 16 + levels 32 + recon 16
 PRED_BYTES_PER_BLOCK = 16         # materialised prediction: moved, not counted (8(d))
+XMB_RECORD_BYTES = 96             # k_xform_mb's per-MB record (modes, borders, diffusion terms): moved, not counted
 HBM_PEAK_GBS = 8000.0
 VALU_PEAK_PER_CU_CYCLE = 2.0      # wave64 VALU instructions: 4 SIMD32 x 1 per 2 cycles
 CLOCK_GHZ = 2.4
 XFORM_PMC = os.path.join(ROOT, "profiles", "r01_xform_pmc_traffic.json")
 ENCODE_PMC = os.path.join(ROOT, "profiles", "r02_encode_pmc.json")
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+XMB_PMC = os.path.join(ROOT, "profiles", "r03_xmb_pmc.json")
+
+
+def pmc_traffic(path, units):
+    """PMC-measured HBM bytes per launch (profiles/<file>: traffic_bytes over
+    `units` of the profiled launch, scaled to `units`), or None when absent."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["traffic_bytes"] / d["units"] * units
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
 
 
 def xform_traffic(blocks):
@@ -120,9 +133,38 @@ def cpu_info():
             "cpu_share": share}
 
 
-def cpu_baseline(imgs, w, h, q, m, budget_s):
+def cpu_config1(O, q, m, digests, budget_s=4.0):
+    """BASELINE config 1: the CPU reference path on a 768x512 frame (the Kodak
+    size; Kodak is absent here, so synth_rgba frames stand in) -- the oracle's
+    per-frame time on one core beside the reference's published 65 ms
+    (README.md:87-93, CLAUDE.md:10-17), and its bitstreams against the digests."""
+    from zwebp.shard import frame_seed
+    from zwebp.synth import synth_rgba
+    w, h = 768, 512
+    seeds = [frame_seed(i) for i in range(4)]
+    imgs = [synth_rgba(w, h, sd) for sd in seeds]
+    ok = 0
+    for img, sd in zip(imgs, seeds):
+        rc, bs, _ = O.encode(img, w, h, 3, q, m)
+        ok += rc == 0 and hashlib.sha256(bs).hexdigest() == digests.get(f"{w}x{h}/q{q}m{m}/{sd:#010x}")
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.encode(imgs[n % 4], w, h, 3, q, m)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    return {"workload": f"{w}x{h} synth_rgba RGBA Q{q} m{m}, oracle/ C restatement (-O3), 1 thread",
+            "ms_per_frame": el / n * 1e3, "frames_timed": n, "published_reference_ms": 65.0,
+            "published_source": "reference README.md:87-93 (768x512 Kodak, Q75 m4, SIMD Rust, unspecified x86)",
+            "verified": ok == 4, "verification": {"frames_checked": 4, "matched": int(ok)}}
+
+
+def cpu_baseline(imgs, w, h, q, m, budget_s, digests=None):
     """Oracle (C restatement of the reference CPU encoder, -O3), bounded sample:
-    (i) one frame on one thread, (ii) one frame per thread over the job's CPU share."""
+    (i) one frame on one thread, (ii) one frame per thread over the job's CPU share,
+    (iii) BASELINE config 1 (768x512) on one thread beside the published figure."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     info = cpu_info()
@@ -162,6 +204,7 @@ def cpu_baseline(imgs, w, h, q, m, budget_s):
         out["batch_all_cores"] = {"value": sum(counts) / el, "unit": "encodes/s", "cores": nt,
                                   "sample": f"{sum(counts)} frames, one frame per thread, {nt} threads "
                                             f"(job CPU share of {info['affinity_cpus']} visible), {el:.1f} s"}
+    out["config1"] = cpu_config1(O, q, m, digests or {})
     return out
 
 
@@ -227,14 +270,99 @@ def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
                              "pass_over_copy": ms_copy / ms}}
 
 
-def decode_path(ctx, streams, frames, w, h, with_cpu):
+def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, digests=None):
+    """SURVEY 8(d)'s HBM-roofline pass: the streaming DCT+quant pass over per-MB
+    records (k_xform_mb, zw_transform_quant_mbs_device) on `frames` 1080p frames
+    resident in HBM.  The records carry the modes, segments and reconstructed
+    borders the timed encode chose for its first `nd` distinct frames
+    (Pipeline.mbinfo / planes) and deterministic error-diffusion inputs
+    (zwebp.xmb.synthetic_derr); frame i is distinct frame i % nd.  Algorithmic
+    bytes 1568 per MB (source 384 + levels 800 + recon 384); the 96-byte record
+    is traffic the pass moves but 8(d) does not count.  HIP events on the launch
+    stream; the copy ceiling (ZW_XMB_VARIANT=99) moves the same bytes with no
+    arithmetic.  Outside the timed region every frame's levels and
+    reconstruction are hashed against the oracle's digests (make_bench_digests.py)."""
+    import numpy as np
+    import zwebp
+    from zwebp.xmb import build_records, synthetic_derr
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    nmb = mbw * mbh
+    recs, srcs, sq = [], [], []
+    for i in range(nd):
+        md = pipe.mbinfo(i, 2)[0]
+        ry, ru, rv = pipe.planes(i, 1)
+        recs.append(build_records(mbw, mbh, md, ry, ru, rv, synthetic_derr(nmb, seeds[i])))
+        srcs.append(pipe.planes(i, 0))
+        sq.append(pipe.segments(i))
+    pick = [i % nd for i in range(frames)]
+    tY = torch.from_numpy(np.concatenate([srcs[i][0] for i in pick])).to(dev)
+    tU = torch.from_numpy(np.concatenate([srcs[i][1] for i in pick])).to(dev)
+    tV = torch.from_numpy(np.concatenate([srcs[i][2] for i in pick])).to(dev)
+    tR = torch.from_numpy(np.concatenate([recs[i].reshape(-1) for i in pick])).to(dev)
+    tS = torch.from_numpy(zwebp.xmb_seg_table(np.stack([sq[i] for i in pick]))).to(dev)
+    lv = torch.empty(frames * nmb * 400, dtype=torch.int16, device=dev)
+    oY, oU, oV = torch.empty_like(tY), torch.empty_like(tU), torch.empty_like(tV)
+    stream = torch.cuda.Stream(dev)
+    sh = stream.cuda_stream
+
+    def run():
+        zwebp.transform_quant_mbs_device(frames, mbw, mbh, tY.data_ptr(), tU.data_ptr(), tV.data_ptr(), tR.data_ptr(),
+                                         tS.data_ptr(), lv.data_ptr(), oY.data_ptr(), oU.data_ptr(), oV.data_ptr(),
+                                         stream=sh, ctx=ctx)
+
+    ms = timed_launches(torch, dev, stream, run, reps)
+    # output check (outside the timed region): every frame against its distinct frame's digest
+    ok = bad = miss = 0
+    if digests is not None:
+        L = lv.view(frames, nmb * 400).cpu().numpy()
+        Y, U, V = (t.view(frames, -1).cpu().numpy() for t in (oY, oU, oV))
+        for f in range(frames):
+            want = digests.get(f"xmb/{w}x{h}/q{q}m{m}/{seeds[pick[f]]:#010x}")
+            if want is None:
+                miss += 1
+                continue
+            hsh = hashlib.sha256()
+            for a in (L[f], Y[f], U[f], V[f]):
+                hsh.update(a.tobytes())
+            ok, bad = (ok + 1, bad) if hsh.hexdigest() == want else (ok, bad + 1)
+    prev = os.environ.get("ZW_XMB_VARIANT")
+    os.environ["ZW_XMB_VARIANT"] = "99"
+    try:
+        ms_copy = timed_launches(torch, dev, stream, run, reps)
+    finally:
+        if prev is None:
+            os.environ.pop("ZW_XMB_VARIANT", None)
+        else:
+            os.environ["ZW_XMB_VARIANT"] = prev
+    del tY, tU, tV, tR, tS, lv, oY, oU, oV
+    torch.cuda.empty_cache()
+    mbs = frames * nmb
+    alg = mbs * ALG_BYTES_PER_MB
+    moved = mbs * (ALG_BYTES_PER_MB + XMB_RECORD_BYTES)
+    ach = alg / (ms * 1e-3) / 1e9
+    copy_gbs = moved / (ms_copy * 1e-3) / 1e9
+    return {"kernel": "k_xform_mb", "workload": f"{frames} frames x {nmb} MBs ({w}x{h}), the timed encode's modes",
+            "mbs_per_launch": mbs, "alg_bytes_per_mb": ALG_BYTES_PER_MB, "alg_bytes_per_launch": alg,
+            "record_bytes_per_mb": XMB_RECORD_BYTES, "ms_per_launch": ms, "achieved": ach,
+            "frac": ach / HBM_PEAK_GBS, "achieved_incl_records": moved / (ms * 1e-3) / 1e9,
+            "verified": bad == 0 and miss == 0 and ok == frames,
+            "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss},
+            "copy_ceiling": {"kernel": "k_xform_mb<copy> (ZW_XMB_VARIANT=99: same loads and stores, no arithmetic)",
+                             "ms_per_launch": ms_copy, "achieved": copy_gbs, "frac": copy_gbs / HBM_PEAK_GBS,
+                             "pass_over_copy": ms_copy / ms}}
+
+
+def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     """SURVEY config 3: the decode path on this GPU.  Host bool decoding + MB
     records up, k_dec_recon (dequant, iWHT/iDCT, prediction) + k_loopfilter,
     planes down.  Single frame end to end, plus a batch for the kernels'
-    throughput; algorithmic bytes 1208 B/MB (levels 800 + side info 24 + YUV 384)."""
+    throughput; algorithmic bytes 1208 B/MB (levels 800 + side info 24 + YUV 384).
+    Outside the timed calls, every decoded frame's Y/U/V planes and RGBA image
+    (stream i = the bench's distinct frame tags[i]) are hashed against the
+    oracle's decode digests."""
     import zwebp
     one = [streams[0]]
-    zwebp.decode_batch(one, ctx=ctx)
+    dec1 = zwebp.decode_batch(one, ctx=ctx)
     reps = 5
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -244,8 +372,26 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
     batch = [streams[i % len(streams)] for i in range(frames)]
     zwebp.decode_batch(batch, ctx=ctx)  # warm-up: grows the pinned staging buffers
     t0 = time.perf_counter()
-    zwebp.decode_batch(batch, ctx=ctx)  # pipelined chunks (parse / device / download overlap)
+    decb = zwebp.decode_batch(batch, ctx=ctx)  # pipelined chunks (parse / device / download overlap)
     el = time.perf_counter() - t0
+    vy = [0, 0, 0]  # matched, mismatched, no digest
+
+    def tally(v, i, *arrs):
+        want = digests.get(f"{i}") if digests is not None else None
+        if want is None:
+            v[2] += 1
+            return
+        hsh = hashlib.sha256()
+        for a in arrs:
+            hsh.update(np.ascontiguousarray(a).tobytes())
+        v[0 if hsh.hexdigest() == want else 1] += 1
+
+    import numpy as np
+    if tags is not None:
+        for i, fr in enumerate(dec1 + decb):
+            j = 0 if i == 0 else (i - 1) % len(streams)
+            tally(vy, "dec_yuv/" + tags[j], fr.ybuf, fr.ubuf, fr.vbuf)
+    del decb, dec1
     # kernel throughput: the whole batch as one launch of the per-frame kernels
     env0 = {k: os.environ.get(k) for k in ("ZW_DEC_CHUNK", "ZW_DEC_ROWS")}
     os.environ["ZW_DEC_CHUNK"], os.environ["ZW_DEC_ROWS"] = str(frames), "0"
@@ -260,7 +406,11 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
                 os.environ[k] = v
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * frames
     ach = 1208 * nmb / ((rk + lf) * 1e-3) / 1e9
-    out = {"single_frame_ms": single_ms, "single_frame_kernel_ms": {"k_dec_recon": rk1, "k_loopfilter": lf1},
+    out = {"verified": tags is not None and vy[1] + vy[2] + vr[1] + vr[2] == 0 and vy[0] > 0 and vr[0] > 0,
+           "verification": {"yuv": {"matched": vy[0], "mismatched": vy[1], "no_digest": vy[2]},
+                            "rgba": {"matched": vr[0], "mismatched": vr[1], "no_digest": vr[2]},
+                            "against": "dec_yuv/ and dec_rgba/ oracle digests (decode_frame, fill_rgba fancy)"},
+           "single_frame_ms": single_ms, "single_frame_kernel_ms": {"k_dec_recon": rk1, "k_loopfilter": lf1},
            "batch_frames": frames, "batch_decodes_per_s": frames / el,
            "batch_kernel_ms": {"k_dec_recon": rk, "k_loopfilter": lf, "launch": "whole batch, one workgroup per frame"},
            "kernel_frames_per_s": frames / ((rk + lf) * 1e-3),
@@ -270,13 +420,16 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
     # caller's reused buffers (decode_rgba_into, api.rs:1004), and into fresh
     # per-frame buffers (decode_rgba's Vec per call: page faults on 8 MB each);
     # k_yuv2rgb algorithmic bytes per pixel: Y 1 + U,V 0.5 read, RGBA 4 written
-    import numpy as np
     bufs = [np.empty(w * h * 4, np.uint8) for _ in range(frames)]
     zwebp.decode_rgb_batch_into(batch, bufs, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
     t0 = time.perf_counter()
     zwebp.decode_rgb_batch_into(batch, bufs, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
     el_rgb = time.perf_counter() - t0
     yk = zwebp.decode_rgb_kernel_ms(ctx=ctx)
+    vr = [0, 0, 0]
+    if tags is not None:
+        for i, b in enumerate(bufs):
+            tally(vr, "dec_rgba/" + tags[i % len(streams)], b)
     del bufs
     zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
     t0 = time.perf_counter()
@@ -302,18 +455,21 @@ def decode_path(ctx, streams, frames, w, h, with_cpu):
     return out
 
 
-def single_frame(ctx, img, w, h, q, m, reps=3):
-    """Latency of one frame through the drop-in seam (zw_encode_frame_lossy:
-    buffers allocated per call, as encode_frame_lossy would) and through a
-    persistent one-frame pipeline (encode + output, buffers reused)."""
+def single_frame(ctx, img, w, h, q, m, seed, digests, reps=3):
+    """Latency of one frame through the drop-in seam (zw_encode_frame_lossy,
+    encode_frame_lossy vp8.rs:3132: the row-parallel kernels) and through a
+    persistent one-frame pipeline (encode + output, buffers reused).  The
+    seam's outputs (1 and 8 token partitions) are hashed against the oracle's
+    digests outside the timed loops."""
     import zwebp
-    zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    tag = f"{w}x{h}/q{q}m{m}/{seed:#010x}"
+    out1 = zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
     t0 = time.perf_counter()
     for _ in range(reps):
         zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
     seam_ms = (time.perf_counter() - t0) / reps * 1e3
     # the same seam with 8 token partitions, coded on parallel host threads
-    zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx, token_partitions=8)
+    out8 = zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx, token_partitions=8)
     t0 = time.perf_counter()
     for _ in range(reps):
         zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx, token_partitions=8)
@@ -328,9 +484,13 @@ def single_frame(ctx, img, w, h, q, m, reps=3):
     pipe_ms = (time.perf_counter() - t0) / reps * 1e3
     k = p.kernel_times()
     p.close()
+    v1 = hashlib.sha256(out1).hexdigest() == digests.get(tag)
+    v8 = hashlib.sha256(out8).hexdigest() == digests.get("p8/" + tag)
     return {"encode_frame_lossy_ms": seam_ms, "encode_frame_lossy_8_partitions_ms": parts8_ms,
             "pipeline_1_frame_ms": pipe_ms,
             "kernel_ms": {"rgb2yuv": k[0], "analysis_segments": k[1], "encode_pass1": k[2], "encode_pass2": k[3]},
+            "verified": v1 and v8, "verification": {"seam_1_partition": v1, "seam_8_partitions": v8,
+                                                    "against": "oracle digests " + tag + " / p8/" + tag},
             "note": "one frame: the row-parallel encode kernels (one wave per MB row, rows handed over through "
                     "global memory); pass 1 is bounded by the chroma raster chain (quirk A5) on one wave"}
 
@@ -340,8 +500,8 @@ def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
     RGBA input, api.rs:1291-1398): the pipe's container mode adds, per frame on
     the emission threads, the ALPH chunk (encode_alpha_lossless of the host copy
     of the frame's alpha plane) and the VP8X container.  Same device-resident
-    inputs as the headline line; the VP8 chunk of every output is checked
-    against the oracle digests."""
+    inputs as the headline line; every whole RIFF file (VP8X + ALPH + VP8) is
+    hashed against the oracle's digest outside the timed region."""
     import struct
     n = pipe.n
     pipe.set_container([host_imgs[i % len(host_imgs)] for i in range(n)])
@@ -350,20 +510,21 @@ def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
         t0 = time.perf_counter()
         pipe.encode_repeat(steps)
         el = time.perf_counter() - t0
-        ok = bad = 0
+        ok = bad = miss = 0
         alph_bytes = 0
         for i in range(n):
             c = pipe.output(i)
-            off, vp8 = 12, None
-            while off + 8 <= len(c):
-                tag, ln = c[off:off + 4], struct.unpack("<I", c[off + 4:off + 8])[0]
-                if tag == b"VP8 ":
-                    vp8 = c[off + 8:off + 8 + ln]
-                elif tag == b"ALPH" and i == 0:
-                    alph_bytes = ln
-                off += 8 + ln + (ln & 1)
-            key = f"{w}x{h}/q{q}m{m}/{seeds[i % len(seeds)]:#010x}"
-            if vp8 is not None and hashlib.sha256(vp8).hexdigest() == digests.get(key):
+            if i == 0:
+                off = 12
+                while off + 8 <= len(c):
+                    tag, ln = c[off:off + 4], struct.unpack("<I", c[off + 4:off + 8])[0]
+                    if tag == b"ALPH":
+                        alph_bytes = ln
+                    off += 8 + ln + (ln & 1)
+            want = digests.get(f"riff/{w}x{h}/q{q}m{m}/{seeds[i % len(seeds)]:#010x}")
+            if want is None:
+                miss += 1
+            elif hashlib.sha256(c).hexdigest() == want:
                 ok += 1
             else:
                 bad += 1
@@ -372,8 +533,45 @@ def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
         pipe.set_container(None, enable=False)
     return {"container_rgba_encodes_per_s": n * steps / el, "frames": n * steps, "ms_per_batch": el / steps * 1e3,
             "host_emit_ms_per_batch": float(k[7]), "alph_bytes_frame0": alph_bytes,
-            "verified_vp8_chunks": ok, "mismatched": bad,
+            "verified": bad == 0 and miss == 0 and ok == n,
+            "verification": {"files_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss,
+                             "against": "riff/... oracle digests (RIFF + VP8X + ALPH + VP8)"},
             "note": "RIFF + VP8X + ALPH + VP8 per frame; inputs resident in HBM, alpha planes read from host memory"}
+
+
+def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0):
+    """A device-resident batch of `frames` w x h frames (distinct synthetic
+    frames seeds[i % len(seeds)]), `steps` pipelined batches timed after one
+    warm-up, every bitstream hashed against the oracle's digests afterwards.
+    BASELINE config 5 at N=1 (3840x2160) and the GPU side of config 1 (768x512)."""
+    import zwebp
+    from zwebp.synth import synth_rgba
+    imgs = [synth_rgba(w, h, sd) for sd in seeds]
+    p = zwebp.Pipeline(frames, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    try:
+        for i in range(frames):
+            p.upload(i, imgs[i % len(imgs)])
+        p.encode_repeat(1)
+        t0 = time.perf_counter()
+        p.encode_repeat(steps)
+        el = time.perf_counter() - t0
+        k = p.kernel_times()
+        ok, bad, miss = verify(p, frames, seeds, w, h, q, m, digests)
+        nbytes = sum(len(p.output(i)) for i in range(min(frames, len(seeds))))
+        threads = zwebp.host_threads()
+        emit_s = float(k[7]) * 1e-3
+        return {"workload": f"{w}x{h} RGBA Q{q} m{m}, {frames} frames per device batch, {steps} pipelined batches",
+                "encodes_per_s": frames * steps / el, "ms_per_batch": el / steps * 1e3,
+                "frames_per_step": frames, "launch_frames": p.launch_frames,
+                "kernel_ms_per_launch_span": {"encode_pass1": float(k[2]), "encode_pass2": float(k[3])},
+                "host_emit_ms_per_batch": float(k[7]), "host_threads": threads,
+                "host_emit_frames_per_s_per_core": frames / (emit_s * threads) if emit_s > 0 else None,
+                "avg_frame_bytes": nbytes / max(1, min(frames, len(seeds))),
+                "verified": bad == 0 and miss == 0 and ok == frames,
+                "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad,
+                                 "no_digest": miss, "against": "tests/golden/bench_digests.json (oracle SHA-256)"}}
+    finally:
+        p.close()
 
 
 def encode_roofline(p2_ms, launch_frames, nmb):
@@ -579,26 +777,74 @@ def main():
             "avg_frame_bytes": bytes_out / max(1, min(B, D)),
         }
         if not a.no_extras:
-            dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
-            line["roofline"] = {"bound": "hbm", "achieved": dq["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": dq["frac"], "traffic": xform_traffic(dq["blocks"]),
-                                "kernel": "k_fdct_quant", "workload": dq["workload"],
-                                "blocks_per_launch": dq["blocks"], "alg_bytes_per_block": ALG_BYTES_PER_BLOCK,
-                                "alg_bytes_per_launch": dq["alg_bytes_per_launch"],
-                                "ms_per_launch": dq["ms_per_launch"],
-                                "achieved_incl_pred": dq["achieved_incl_pred"], "frac_incl_pred": dq["frac_incl_pred"],
-                                "copy_ceiling": dq["copy_ceiling"],
-                                "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"}
-            lk = launch_kernel_times(ctx, imgs, w, h, a.quality, a.method, min(B, 256))
+            q, m = a.quality, a.method
+            tags = [f"{w}x{h}/q{q}m{m}/{sd:#010x}" for sd in seeds]
+            lk = launch_kernel_times(ctx, imgs, w, h, q, m, min(B, 256))
             line["kernel_ms_per_launch"] = lk
-            line["encode_roofline"] = encode_roofline(lk["encode_pass2"], lk["launch_frames"], nmb)
-            line["single_frame"] = single_frame(ctx, imgs[0], w, h, a.quality, a.method)
+            er = encode_roofline(lk["encode_pass2"], lk["launch_frames"], nmb)
+            line["encode_roofline"] = er
+            xm = xmb_pass(ctx, torch, dev, pipes[0][0], min(B, D), seeds, w, h, q, m, 256, 10, digests)
+            line["roofline"] = {"bound": "hbm", "achieved": xm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": xm["frac"], "traffic": pmc_traffic(XMB_PMC, xm["mbs_per_launch"]),
+                                "kernel": "k_xform_mb", "workload": xm["workload"],
+                                "mbs_per_launch": xm["mbs_per_launch"], "alg_bytes_per_mb": ALG_BYTES_PER_MB,
+                                "alg_bytes_per_launch": xm["alg_bytes_per_launch"],
+                                "ms_per_launch": xm["ms_per_launch"],
+                                "record_bytes_per_mb": XMB_RECORD_BYTES,
+                                "achieved_incl_records": xm["achieved_incl_records"],
+                                "copy_ceiling": xm["copy_ceiling"], "verified": xm["verified"],
+                                "verification": xm["verification"],
+                                "traffic_source": "profiles/r03_xmb_pmc.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)",
+                                "fused_path": {"kernel": "k_encode_pass2 (RD search fused with the final "
+                                                         "DCT+quant+recon, the timed step's dominant kernel)",
+                                               "hbm_frac": er["hbm_frac"] if er else None,
+                                               "valu_frac": er["frac"] if er else None}}
+            dq = dct_quant_pass(ctx, torch, dev, 256, nmb)
+            line["roofline_blocks"] = {"kernel": "k_fdct_quant (4x4 blocks, prediction materialised in HBM)",
+                                       "achieved": dq["achieved"], "frac": dq["frac"],
+                                       "traffic": xform_traffic(dq["blocks"]), "blocks_per_launch": dq["blocks"],
+                                       "alg_bytes_per_block": ALG_BYTES_PER_BLOCK, "ms_per_launch": dq["ms_per_launch"],
+                                       "achieved_incl_pred": dq["achieved_incl_pred"],
+                                       "copy_ceiling": dq["copy_ceiling"],
+                                       "traffic_source": "profiles/r01_xform_pmc_traffic.json (rocprofv3 --pmc)"}
+            line["single_frame"] = single_frame(ctx, imgs[0], w, h, q, m, seeds[0], digests)
             streams = [bytes(pipes[0][0].output(i)) for i in range(min(B, D))]  # VP8 frames, before container mode
-            line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, a.quality, a.method, seeds, digests)
-            line["decode_path"] = decode_path(ctx, streams, 256, w, h, not a.no_cpu_baseline)
+            line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, q, m, seeds, digests)
+            line["decode_path"] = decode_path(ctx, streams, 256, w, h, not a.no_cpu_baseline, tags, digests)
+            del streams
+            for pipe, _ in pipes:  # free the headline batch before the 4K leg
+                pipe.close()
+            pipes = []
+            s4 = [frame_seed(i) for i in range(4)]
+            line["config5_4k_n1"] = batch_leg(ctx, 3840, 2160, q, m, 256, 2, s4, digests)
+            line["config1_768x512_gpu"] = batch_leg(ctx, 768, 512, q, m, 256, 4, s4, digests)
+            c5 = line["config5_4k_n1"]
+            fpc = c5.get("host_emit_frames_per_s_per_core")
+            line["host_budget"] = {
+                "threads_per_rank": threads,
+                "emit_frames_per_s_per_core_1080p": line["host_emit_frames_per_s_per_core"],
+                "emit_frames_per_s_per_core_4k": fpc,
+                "cores_for_8x_this_gpu_1080p": 8 * line["value"] / line["host_emit_frames_per_s_per_core"]
+                if line["host_emit_frames_per_s_per_core"] else None,
+                "cores_for_8x_this_gpu_4k": 8 * c5["encodes_per_s"] / fpc if fpc else None,
+                "note": "host cores the bool coder needs to keep 8 GPUs at this GPU's measured rate; "
+                        "threads per rank = affinity CPUs / LOCAL_WORLD_SIZE, capped by OMP_NUM_THREADS"}
         line["cpu_baseline"] = None
         if not a.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds, digests)
+        if not a.no_extras:
+            cb = line["cpu_baseline"] or {}
+            line["configs"] = {
+                "1_768x512_cpu_reference_path": {"verified": bool(cb.get("config1", {}).get("verified")) and
+                                                 line["config1_768x512_gpu"]["verified"],
+                                                 "see": "cpu_baseline.config1, config1_768x512_gpu"},
+                "2_1080p_dct_quant_idct_kernels": {"verified": line["roofline"]["verified"], "see": "roofline"},
+                "3_1080p_decode_path": {"verified": line["decode_path"]["verified"], "see": "decode_path"},
+                "4_1080p_batch_encode": {"verified": line["verified"] and line["single_frame"]["verified"] and
+                                         line["container_rgba"]["verified"],
+                                         "see": "value, single_frame, container_rgba"},
+                "5_4k_batch_n1": {"verified": line["config5_4k_n1"]["verified"], "see": "config5_4k_n1 (N=1 anchor "
+                                  "of the 4096-frame split; the driver's SCALE run measures N=2/4/8)"}}
         print(json.dumps(line), flush=True)
     for pipe, _ in pipes:
         pipe.close()

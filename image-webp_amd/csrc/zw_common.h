@@ -81,6 +81,10 @@ struct ZwMbOut {
 //            nonzero); blocks 0..23, then 24 = Y2   [68..79] pad
 //   [80..] int16 levels, zigzag order; pad to 16.
 // The device expands it into a ZwDecMb in LDS.
+// k_pack_scan's per-chunk counter words: [0] running offset, [1] frames done,
+// [2] the chunk's total bytes (read by the host), [3] pad.  The last frame's
+// workgroup publishes the total and clears [0] and [1] for the next launch.
+#define ZW_PACK_CTR_WORDS 4
 #define ZW_DREC_HDR 80
 #define ZW_DREC_MAX (ZW_DREC_HDR + 25 * 16 * 2)  // 880 B = 55 lines
 

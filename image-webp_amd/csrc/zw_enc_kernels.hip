@@ -540,7 +540,9 @@ __device__ void segment_init(ZwSegment& s, int qi, int delta)
     s.quantizer_level = delta;
 }
 
-extern "C" __global__ void k_segments(const uint32_t* __restrict__ histo, const ZwFrameParams* __restrict__ tmpl,
+// Consumes the frame's alpha histogram and clears it for the next launch of
+// k_analysis (zeroed once at pipeline creation; no per-launch memset blit).
+extern "C" __global__ void k_segments(uint32_t* __restrict__ histo, const ZwFrameParams* __restrict__ tmpl,
                                       ZwFrameParams* __restrict__ params, int nframes)
 {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -622,6 +624,8 @@ extern "C" __global__ void k_segments(const uint32_t* __restrict__ histo, const 
         P.seg_enabled = 1;
     }
     params[f] = P;
+    uint4* Hz = (uint4*)(histo + (size_t)f * 256);
+    for (int i = 0; i < 64; i++) Hz[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -2584,11 +2588,15 @@ DI void row_wait(const int* prog, int need, int* err, int& seen)
             break;
         }
     }
+    // pairs with row_publish's release: the row state loads below may not be
+    // hoisted above the poll (C++ memory model, not only GFX9's in-order returns)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 DI void row_publish(int* prog, int val)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are out
-    if ((threadIdx.x & 63) == 0) st_sc1(prog, (uint32_t)val);
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store((uint32_t*)prog, (uint32_t)val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -3286,7 +3294,7 @@ extern "C" hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_
     return hipGetLastError();
 }
 
-extern "C" hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl,
+extern "C" hipError_t zwk_segments(hipStream_t s, uint32_t* histo, const ZwFrameParams* tmpl,
                                    ZwFrameParams* params, int nframes)
 {
     hipLaunchKernelGGL(k_segments, dim3((nframes + 63) / 64), dim3(64), 0, s, histo, tmpl, params, nframes);

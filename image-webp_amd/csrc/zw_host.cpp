@@ -32,7 +32,7 @@ hipError_t zwk_rgb2yuv(hipStream_t s, const uint8_t* img, int w, int h, int bpp,
                        uint8_t* U, uint8_t* V, size_t img_stride, size_t ysz, size_t csz, int nframes);
 hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int mbw, int mbh,
                         size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes);
-hipError_t zwk_segments(hipStream_t s, const uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
+hipError_t zwk_segments(hipStream_t s, uint32_t* histo, const ZwFrameParams* tmpl, ZwFrameParams* params,
                         int nframes);
 hipError_t zwk_stats(hipStream_t s, const ZwMbOut* mbs, int mbw, int mbh, void* scratch, void* out, int nframes);
 size_t zw_stats_scratch_bytes(int nmb, int nframes);
@@ -40,6 +40,11 @@ hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uin
                      unsigned long long* counter, unsigned long long* frame_info, uint8_t* out, int sizes_ready);
 hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m, int first,
                           void* levels, void* recon, int cus);
+hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, const uint8_t* recs,
+                        const void* segs, int mbw, int mbh, int nframes, int16_t* levels, uint8_t* RY, uint8_t* RU,
+                        uint8_t* RV, int variant);
+size_t zwk_xform_mb_seg_bytes(void);
+void zwk_xform_mb_pack_segs(const ZwMatrix* m, int n, void* out);
 hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
                             const uint8_t* probs, const void* args, int* levels, int* dq);
 hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
@@ -151,6 +156,7 @@ static bool sdma_probe(zw_ctx* c)
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return ZW_OK;
+    if (c->poisoned.load(std::memory_order_acquire)) return ZW_EDEVICE;
     if (sdma_probe(c)) {
         hsa_signal_t sig;
         if (hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS) {
@@ -163,9 +169,15 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
                 v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 100000000ull, HSA_WAIT_STATE_BLOCKED);
                 if (v == 0 || std::chrono::steady_clock::now() > deadline) break;
             }
+            if (st == HSA_STATUS_SUCCESS && v != 0) {
+                // timed out with the copy still queued or running: the engine may yet
+                // write `dst` and decrement `sig`, so the signal is leaked, not destroyed,
+                // and the context refuses every later copy
+                c->poisoned.store(true, std::memory_order_release);
+                return ZW_EDEVICE;
+            }
             (void)hsa_signal_destroy(sig);
-            if (st == HSA_STATUS_SUCCESS && v == 0) return ZW_OK;
-            if (st == HSA_STATUS_SUCCESS) return ZW_EDEVICE;  // the copy itself failed
+            if (st == HSA_STATUS_SUCCESS) return ZW_OK;
         }
         c->sdma.store(0, std::memory_order_release);  // HSA path unusable: fall back for good
     }
@@ -178,8 +190,11 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream_) (void)hipStreamSynchronize(c->stream_);  // nothing queued may still use them
-    zw_pipe_destroy(c->pipe1);
-    c->pipe1 = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c->pipe1_mu);
+        zw_pipe_destroy(c->pipe1);
+        c->pipe1 = nullptr;
+    }
     for (auto& v : c->dec_recs) std::vector<zw_ctx::RecBuf>().swap(v);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
@@ -463,6 +478,8 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
               hipMalloc(&p->d_pack2, N * p->pack_stride) == hipSuccess;
     // Pass-1 statistics are pre-aggregated on the device (zwk_stats) unless
     // ZW_HOST_STATS asks for the host replay of the packed records.
+    // k_segments clears each frame's histogram after use; k_pack_scan resets its counters
+    ok = ok && hipMemset(p->d_histo, 0, N * 256 * sizeof(uint32_t)) == hipSuccess;
     p->host_stats = getenv("ZW_HOST_STATS") != nullptr;
     ok = ok && (p->host_stats || (hipMalloc(&p->d_stats, N * sizeof(ZwStatsOut)) == hipSuccess &&
                                   hipMalloc(&p->d_stats_tmp, zw_stats_scratch_bytes(p->nmb, n)) == hipSuccess));
@@ -479,7 +496,8 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
         L.cev.assign(2 * (size_t)nch, nullptr);
         ok = ok && hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) == hipSuccess &&
              hipStreamCreateWithFlags(&L.stream2, hipStreamNonBlocking) == hipSuccess &&
-             hipMalloc(&L.d_ctr, 2 * (size_t)nch * sizeof(unsigned long long)) == hipSuccess;
+             hipMalloc(&L.d_ctr, 2 * (size_t)nch * ZW_PACK_CTR_WORDS * sizeof(unsigned long long)) == hipSuccess &&
+             hipMemset(L.d_ctr, 0, 2 * (size_t)nch * ZW_PACK_CTR_WORDS * sizeof(unsigned long long)) == hipSuccess;
         if (ok && pipe_rows_for(L.chunk, p->mbh, ctx->device)) {
             const size_t rb = zwk_encode_rows_bytes(p->mbw, p->mbh, L.chunk);
             ok = hipMalloc(&L.d_rows, rb) == hipSuccess && hipMemset(L.d_rows, 0, rb) == hipSuccess;
@@ -596,7 +614,6 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
     HIPOK(zwk_rgb2yuv(s, p->d_img + F * p->img_stride, p->w, p->h, p->bpp, p->mbw, p->mbh, p->d_Y + F * p->ysz,
                       p->d_U + F * p->csz, p->d_V + F * p->csz, p->img_stride, p->ysz, p->csz, n));
     if (timed) HIPOK(hipEventRecord(L.ev[1], s));
-    HIPOK(hipMemsetAsync(p->d_histo + F * 256, 0, (size_t)n * 256 * sizeof(uint32_t), s));
     HIPOK(zwk_analysis(s, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->mbw, p->mbh, p->ysz,
                        p->csz, p->d_alpha + F * p->nmb, p->d_histo + F * 256, n));
     HIPOK(zwk_segments(s, p->d_histo + F * 256, p->d_tmpl, p->d_params + F, n));
@@ -631,7 +648,7 @@ static int chunk_pack(zw_pipe* p, PipeLane& L, int fa, int na, const ZwMbOut* d_
     const bool p2 = slot & 1;  // pass-2 streams have their own buffers (a later batch's pass 1 may overwrite
                                // the pass-1 buffers while the host is still fetching pass-2 data)
     HIPOK(zwk_pack(L.stream, d_out + F * p->nmb, p->nmb, na, p->d_eobs + F * p->nmb * 25, p->d_sizes + F * p->nmb,
-                   L.d_ctr + slot, (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
+                   L.d_ctr + ZW_PACK_CTR_WORDS * slot, (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
                    (p2 ? p->d_pack2 : p->d_pack) + F * p->pack_stride, p2 && pass2_sizes(p)));
     return ZW_OK;
 }
@@ -642,7 +659,7 @@ static int chunk_fetch(zw_pipe* p, PipeLane& L, FetchBuf& B, int fa, int na, int
 {
     const size_t F = (size_t)fa;
     HIPOK(hipEventSynchronize(ready));
-    int r = ctx_d2h(p->ctx, B.total.data(), L.d_ctr + slot, sizeof(unsigned long long));
+    int r = ctx_d2h(p->ctx, B.total.data(), L.d_ctr + ZW_PACK_CTR_WORDS * slot + 2, sizeof(unsigned long long));
     const bool p2 = slot & 1;
     if (!r)
         r = ctx_d2h(p->ctx, B.finfo.data(), (p2 ? p->d_finfo2 : p->d_finfo) + 2 * F,
@@ -1042,6 +1059,14 @@ extern "C" int zw_pipe_read_probs(zw_pipe* p, int frame, uint8_t* probs, int* sk
     return ZW_OK;
 }
 
+extern "C" int zw_pipe_read_segments(zw_pipe* p, int frame, int32_t* seg_qi)
+{
+    if (!p || frame < 0 || frame >= p->n || !seg_qi) return ZW_EINVAL;
+    const ZwFrameParams& P = p->h_params[hidx(p, p->out_par, (size_t)frame)];
+    for (int i = 0; i < 4; i++) seg_qi[i] = P.seg[i].quant_index;
+    return ZW_OK;
+}
+
 extern "C" int zw_pipe_enable_debug(zw_pipe* p)
 {
     if (!p) return ZW_EINVAL;
@@ -1109,23 +1134,31 @@ extern "C" int zw_encode_batch_ex(zw_ctx* ctx, int n, const zw_image* imgs, uint
     int r;
     const int key[5] = {(int)imgs[0].width, (int)imgs[0].height, imgs[0].color, quality, method};
     const bool one = n == 1;
-    if (one && ctx->pipe1 && !memcmp(key, ctx->pipe1_key, sizeof key)) {
-        p = ctx->pipe1;  // a one-frame pipeline of this shape from an earlier call
-    } else {
+    if (one) {  // a one-frame pipeline of this shape from an earlier call, taken out for this call
+        std::lock_guard<std::mutex> lk(ctx->pipe1_mu);
+        if (ctx->pipe1 && !memcmp(key, ctx->pipe1_key, sizeof key)) {
+            p = ctx->pipe1;
+            ctx->pipe1 = nullptr;
+        }
+    }
+    if (!p) {
         r = zw_pipe_create(ctx, n, imgs[0].width, imgs[0].height, imgs[0].color, quality, method, &p);
         if (r) return r;
-        if (one) {
-            zw_pipe_destroy(ctx->pipe1);
-            ctx->pipe1 = p;
-            memcpy(ctx->pipe1_key, key, sizeof key);
-        }
     }
     r = zw_pipe_set_token_partitions(p, token_partitions);
     for (int i = 0; i < n && !r; i++) r = zw_pipe_upload(p, i, imgs[i].data, imgs[i].len);
     if (!r) r = zw_pipe_encode(p);
     for (int i = 0; i < n && !r; i++) r = zw_pipe_output(p, i, &outs[i]);
-    if (!one || r) {
-        if (p == ctx->pipe1) ctx->pipe1 = nullptr;  // not reused after a failure
+    if (one && !r) {  // kept for the next call of this shape (not after a failure)
+        zw_pipe* old;
+        {
+            std::lock_guard<std::mutex> lk(ctx->pipe1_mu);
+            old = ctx->pipe1;
+            ctx->pipe1 = p;
+            memcpy(ctx->pipe1_key, key, sizeof key);
+        }
+        zw_pipe_destroy(old);
+    } else {
         zw_pipe_destroy(p);
     }
     return r;
@@ -1326,6 +1359,93 @@ extern "C" int zw_transform_quant_blocks(zw_ctx* ctx, size_t n, const uint8_t* s
     if (r) return r;
     HIPOK(hipMemcpyAsync(levels, d + o_l, n * 32, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(recon, d + o_r, n * 16, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming DCT+quant pass over per-MB records (zw_xmb_kernels.hip)
+// ---------------------------------------------------------------------------
+extern "C" size_t zw_xmb_seg_table_bytes(int nframes) { return nframes > 0 ? (size_t)nframes * zwk_xform_mb_seg_bytes() : 0; }
+
+// Segment::init_matrices (types.rs:806) from each segment's quantizer index,
+// as the encoder's seg_from_index: y2dc = 2*dc, y2ac = 155/100*ac (>= 8), uv
+// uncapped (quirk A17).
+extern "C" int zw_xmb_seg_table(int nframes, const int32_t* seg_qi, void* out)
+{
+    if (nframes <= 0 || !seg_qi || !out) return ZW_EINVAL;
+    std::vector<ZwMatrix> m((size_t)nframes * 12);
+    for (int i = 0; i < nframes * 4; i++) {
+        const int qi = seg_qi[i];
+        if (qi < 0 || qi > 127) return ZW_EINVAL;
+        const int dc = zwh::DC_QUANT[qi], ac = zwh::AC_QUANT[qi];
+        int y2ac = ac * 155 / 100;
+        if (y2ac < 8) y2ac = 8;
+        if (make_matrix(m[i * 3 + 0], dc, ac, 0) || make_matrix(m[i * 3 + 1], 2 * dc, y2ac, 1) ||
+            make_matrix(m[i * 3 + 2], dc, ac, 2))
+            return ZW_EINVAL;
+    }
+    zwk_xform_mb_pack_segs(m.data(), nframes, out);
+    return ZW_OK;
+}
+
+static int xmb_variant()
+{
+    const char* e = getenv("ZW_XMB_VARIANT");  // 99: same loads and stores, no arithmetic (copy ceiling)
+    return e ? atoi(e) : 0;
+}
+
+extern "C" int zw_transform_quant_mbs_device(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint32_t mbh,
+                                             const void* d_y, const void* d_u, const void* d_v, const void* d_recs,
+                                             const void* d_segs, void* d_levels, void* d_ry, void* d_ru, void* d_rv)
+{
+    if (!ctx || nframes < 0 || mbw == 0 || mbh == 0 || mbw > 1024 || mbh > 1024) return ZW_EINVAL;
+    if (nframes == 0) return ZW_OK;
+    if (!d_y || !d_u || !d_v || !d_recs || !d_segs || !d_levels || !d_ry || !d_ru || !d_rv) return ZW_EINVAL;
+    // 16-byte loads and stores: records, planes and levels must be 16-byte aligned (chroma rows 8)
+    const uintptr_t a16 = (uintptr_t)d_y | (uintptr_t)d_recs | (uintptr_t)d_levels | (uintptr_t)d_ry;
+    const uintptr_t a8 = (uintptr_t)d_u | (uintptr_t)d_v | (uintptr_t)d_ru | (uintptr_t)d_rv;
+    if ((a16 & 15) || (a8 & 7)) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    HIPOK(zwk_xform_mb(stream ? (hipStream_t)stream : ctx_stream(ctx), (const uint8_t*)d_y, (const uint8_t*)d_u,
+                       (const uint8_t*)d_v, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes,
+                       (int16_t*)d_levels, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, xmb_variant()));
+    return ZW_OK;
+}
+
+extern "C" int zw_transform_quant_mbs(zw_ctx* ctx, int nframes, uint32_t mbw, uint32_t mbh, const uint8_t* y,
+                                      const uint8_t* u, const uint8_t* v, const uint8_t* recs, const int32_t* seg_qi,
+                                      int16_t* levels, uint8_t* ry, uint8_t* ru, uint8_t* rv)
+{
+    if (!ctx || nframes < 0 || mbw == 0 || mbh == 0 || mbw > 1024 || mbh > 1024) return ZW_EINVAL;
+    if (nframes == 0) return ZW_OK;
+    if (!y || !u || !v || !recs || !seg_qi || !levels || !ry || !ru || !rv) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    const size_t F = (size_t)nframes, nmb = (size_t)mbw * mbh;
+    const size_t ysz = nmb * 256 * F, csz = nmb * 64 * F, rb = nmb * ZW_XMB_RECORD_BYTES * F, lb = nmb * 800 * F;
+    const size_t sb = zw_xmb_seg_table_bytes(nframes);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_y = 0, o_u = al(ysz), o_v = o_u + al(csz), o_r = o_v + al(csz), o_s = o_r + al(rb),
+                 o_l = o_s + al(sb), o_ry = o_l + al(lb), o_ru = o_ry + al(ysz), o_rv = o_ru + al(csz),
+                 total = o_rv + al(csz);
+    std::vector<uint8_t> segs(sb);
+    int r = zw_xmb_seg_table(nframes, seg_qi, segs.data());
+    if (r) return r;
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx_stream(ctx);
+    HIPOK(hipMemcpyAsync(d + o_y, y, ysz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_u, u, csz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_v, v, csz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_r, recs, rb, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_s, segs.data(), sb, hipMemcpyHostToDevice, s));
+    r = zw_transform_quant_mbs_device(ctx, s, nframes, mbw, mbh, d + o_y, d + o_u, d + o_v, d + o_r, d + o_s, d + o_l,
+                                      d + o_ry, d + o_ru, d + o_rv);
+    if (r) return r;
+    HIPOK(hipMemcpyAsync(levels, d + o_l, lb, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(ry, d + o_ry, ysz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(ru, d + o_ru, csz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(rv, d + o_rv, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
     return ZW_OK;
 }

@@ -27,6 +27,9 @@ struct zw_ctx {
     // Probed once under sdma_mu (pipe lanes call ctx_d2h from several threads).
     std::atomic<int> sdma{-1};  // -1 unprobed, 0 unavailable, 1 ready
     std::mutex sdma_mu;
+    // set when a DMA copy did not complete in time: the engine may still write
+    // into its destination, so every later copy of this context fails
+    std::atomic<bool> poisoned{false};
     hsa_agent_t gpu_agent{}, cpu_agent{};
     // grow-only pinned host staging (decode batch: MB records up, planes down)
     // [0] / [2]: the two upload buffers of the pipelined decode, [1] downloads,
@@ -41,8 +44,11 @@ struct zw_ctx {
     // one-frame encode pipeline kept between encode_frame_lossy calls of the
     // same shape (dimensions, colour type, quality, method): its device buffers
     // and streams are reused instead of allocated per call
+    // A call takes the cached pipe out under pipe1_mu and puts it back when it
+    // succeeds, so two threads sharing a context never run on one pipe.
     struct zw_pipe* pipe1 = nullptr;
     int pipe1_key[5] = {0, 0, 0, 0, 0};
+    std::mutex pipe1_mu;
     // decode: per-frame worst-case record buffers of the two pipelined buffer
     // sets, kept between chunks and calls (a parse touches only the pages it
     // writes; reallocating them per chunk cost page faults and unmaps)

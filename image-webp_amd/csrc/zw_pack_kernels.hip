@@ -99,6 +99,16 @@ extern "C" __global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restr
         base = atomicAdd(counter, tot);
         frame_info[2 * f] = base;
         frame_info[2 * f + 1] = tot;
+        // the last frame to reserve its slice publishes the chunk total and
+        // clears the counters for the next launch (no memset blit per chunk)
+        __threadfence();
+        if (atomicAdd(counter + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
+            __threadfence();
+            const unsigned long long all = atomicAdd(counter, 0ull);
+            counter[2] = all;
+            atomicExch(counter, 0ull);
+            atomicExch(counter + 1, 0ull);
+        }
     }
 }
 
@@ -171,8 +181,7 @@ extern "C" hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int n
 {
     const size_t total = (size_t)nmb * nframes;
     const unsigned grid = (unsigned)((total + PK_WAVES - 1) / PK_WAVES);
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);  // this chunk's own counter
-    if (e != hipSuccess) return e;
+    // counter: this chunk's ZW_PACK_CTR_WORDS words (zeroed at creation, reset by k_pack_scan)
     if (!sizes_ready)
         hipLaunchKernelGGL(k_pack_size, dim3(grid), dim3(64 * PK_WAVES), 0, s, mbs, nmb, nframes, eobs, sizes);
     hipLaunchKernelGGL(k_pack_scan, dim3(nframes), dim3(1024), 0, s, sizes, nmb, counter, frame_info);

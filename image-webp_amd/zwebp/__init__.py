@@ -25,6 +25,7 @@ built, or no HIP device is visible, the first call raises.
 """
 import ctypes
 import os
+import threading
 import weakref
 
 import numpy as np
@@ -148,6 +149,10 @@ SIGNATURES = [
     ("zw_rgb_to_yuv420", _I, [_VP, _VP, _U32, _U32, _I, _VP, _VP, _VP]),
     ("zw_transform_quant_blocks", _I, [_VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
     ("zw_transform_quant_blocks_device", _I, [_VP, _VP, _SZ, _VP, _VP, _I, _I, _I, _I, _VP, _VP]),
+    ("zw_transform_quant_mbs", _I, [_VP, _I, _U32, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("zw_xmb_seg_table_bytes", _SZ, [_I]),
+    ("zw_xmb_seg_table", _I, [_I, _VP, _VP]),
+    ("zw_transform_quant_mbs_device", _I, [_VP, _VP, _I, _U32, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("zw_quant_blocks", _I, [_VP, _I, _VP, _VP, _I, _I, _I, _U32, _I, _I, _I, _VP, _VP, _VP]),
     ("zw_loop_filter_frame", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I]),
     ("zw_pipe_create", _I, [_VP, _I, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_VP)]),
@@ -167,6 +172,7 @@ SIGNATURES = [
     ("zw_pipe_read_alpha", _I, [_VP, _I, _VP]),
     ("zw_pipe_enable_debug", _I, [_VP]),
     ("zw_pipe_read_debug", _I, [_VP, _I, _VP]),
+    ("zw_pipe_read_segments", _I, [_VP, _I, _VP]),
     ("zw_pipe_read_probs", _I, [_VP, _I, _VP, ctypes.POINTER(_I)]),
     ("zw_pipe_kernel_times", _I, [_VP, ctypes.POINTER(ctypes.c_float), _I]),
     ("zw_pipe_lanes", _I, [_VP]),
@@ -243,14 +249,16 @@ _DEFAULT = {}
 
 
 def _ctx(ctx):
+    """The caller's context, else this thread's default one (a zw_ctx is not
+    thread-safe, and ctypes releases the GIL during every call)."""
     if ctx is not None:
         return ctx
-    pid = os.getpid()
-    if pid not in _DEFAULT:
+    key = (os.getpid(), threading.get_ident())
+    if key not in _DEFAULT:
         dev = int(os.environ.get("LOCAL_RANK", "0")) if os.environ.get("ZWEBP_DEVICE") is None else int(
             os.environ["ZWEBP_DEVICE"])
-        _DEFAULT[pid] = Context(dev)
-    return _DEFAULT[pid]
+        _DEFAULT[key] = Context(dev)
+    return _DEFAULT[key]
 
 
 def _take_bytes(L, b):
@@ -700,6 +708,47 @@ def transform_quant_blocks_device(n, d_src, d_pred, q_dc, q_ac, matrix_type, fir
                                                    d_levels, d_recon), "transform_quant_blocks_device")
 
 
+def transform_quant_mbs(y, u, v, recs, seg_qi, nframes, mbw, mbh, ctx=None):
+    """Streaming DCT+quant pass over per-MB records (zw_transform_quant_mbs):
+    the encoder's final transform with the trellis off, every MB independent.
+
+    y/u/v: MB-padded source planes of nframes frames; recs: (nframes*mbw*mbh, 96)
+    uint8 records (zwebp.xmb.build_records); seg_qi: (nframes, 4) quantizer
+    indices.  Returns (levels (nframes*nmb, 25, 16) int16 zigzag, ry, ru, rv)."""
+    c = _ctx(ctx)
+    nmb = mbw * mbh
+    y, u, v = (np.ascontiguousarray(a, dtype=np.uint8).reshape(-1) for a in (y, u, v))
+    r = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1)
+    q = np.ascontiguousarray(seg_qi, dtype=np.int32).reshape(-1)
+    if y.size != nframes * nmb * 256 or u.size != nframes * nmb * 64 or v.size != u.size:
+        raise ValueError("planes must be MB-padded, nframes frames")
+    if r.size != nframes * nmb * 96 or q.size != nframes * 4:
+        raise ValueError("one 96-byte record per MB and 4 quantizer indices per frame")
+    lv = np.zeros((nframes * nmb, 25, 16), np.int16)
+    ry, ru, rv = np.zeros_like(y), np.zeros_like(u), np.zeros_like(v)
+    _check(c._lib.zw_transform_quant_mbs(c.handle, nframes, mbw, mbh, _ptr(y), _ptr(u), _ptr(v), _ptr(r), _ptr(q),
+                                         _ptr(lv), _ptr(ry), _ptr(ru), _ptr(rv)), "transform_quant_mbs")
+    return lv, ry, ru, rv
+
+
+def xmb_seg_table(seg_qi):
+    """Host quantiser table of zw_transform_quant_mbs_device for (nframes, 4) indices (uint8 bytes)."""
+    L = load_library()
+    q = np.ascontiguousarray(seg_qi, dtype=np.int32).reshape(-1, 4)
+    n = q.shape[0]
+    out = np.zeros(L.zw_xmb_seg_table_bytes(n), np.uint8)
+    _check(L.zw_xmb_seg_table(n, _ptr(q), _ptr(out)), "xmb_seg_table")
+    return out
+
+
+def transform_quant_mbs_device(nframes, mbw, mbh, d_y, d_u, d_v, d_recs, d_segs, d_levels, d_ry, d_ru, d_rv,
+                               stream=None, ctx=None):
+    """Device-pointer form of transform_quant_mbs; asynchronous on `stream` (int handle or None)."""
+    c = _ctx(ctx)
+    _check(c._lib.zw_transform_quant_mbs_device(c.handle, stream, nframes, mbw, mbh, d_y, d_u, d_v, d_recs, d_segs,
+                                                d_levels, d_ry, d_ru, d_rv), "transform_quant_mbs_device")
+
+
 def loop_filter_frame(y, u, v, mbw, mbh, mb_flags, filter_type, filter_level, sharpness, segments_enabled=0,
                       seg_delta_values=0, seg_lf_level=(0, 0, 0, 0), lf_adj_enabled=0, ref_delta0=0, mode_delta0=0,
                       ctx=None):
@@ -798,6 +847,12 @@ class Pipeline:
         d = np.zeros(self.mbw * self.mbh * 16 * 34, np.int32)
         _check(self._lib.zw_pipe_read_debug(self._h, i, _ptr(d)), "zw_pipe_read_debug")
         return d.reshape(self.mbw * self.mbh, 16, 34)
+
+    def segments(self, i):
+        """(4,) int32 quantizer index of each segment of frame i (last encode)."""
+        q = np.zeros(4, np.int32)
+        _check(self._lib.zw_pipe_read_segments(self._h, i, _ptr(q)), "read_segments")
+        return q
 
     def probs(self, i):
         pr = np.zeros(4 * 8 * 3 * 11, np.uint8)

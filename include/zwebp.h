@@ -236,6 +236,44 @@ int zw_transform_quant_blocks(zw_ctx *ctx, size_t n, const uint8_t *src, const u
  * context's stream), asynchronous. */
 int zw_transform_quant_blocks_device(zw_ctx *ctx, void *stream, size_t n, const void *d_src, const void *d_pred,
                                      int q_dc, int q_ac, int matrix_type, int first, void *d_levels, void *d_recon);
+/* Streaming DCT+quant pass over per-MB records (SURVEY 8(d)'s HBM-roofline
+ * pass): the encoder's final transform with the trellis off, per MB,
+ *   luma I16  transform_luma_block      (encoder/vp8.rs:2647-2780): prediction,
+ *             dct4x4 x16, wht4x4 -> Y2 quantize/dequantize -> iwht4x4, Y1 AC
+ *             quantize_coeff/dequantize, idct4x4, add_residue;
+ *   luma I4   transform_luma_blocks_4x4 (:2785-2916), sub-blocks in order;
+ *   chroma    transform_chroma_blocks   (:3039-3121) with
+ *             apply_chroma_error_diffusion (:572-647).
+ * Each MB is independent: the borders create_border_luma/chroma would build
+ * (common/prediction.rs:15-130) and the incoming error-diffusion terms come
+ * from its 96-byte record, raster order per frame:
+ *   [0] luma mode (0 DC, 1 V, 2 H, 3 TM, 4 B)   [1] chroma mode (0..3)
+ *   [2] segment (0..3)   [3] bit 0: MB row > 0, bit 1: MB column > 0 (the
+ *       DC predictors' edge availability, prediction.rs:182-211)
+ *   [4..11] I4 sub-modes, 4 bits each (sub-block i: byte 4 + i/2, low nibble for even i)
+ *   [12..15] U error diffusion in: top[0], top[1], left[0], left[1] (int8)
+ *   [16..19] the same for V
+ *   [20] luma corner  [21] U corner  [22] V corner  [23] 0
+ *   [24..43] luma top 16 + top-right 4   [44..59] luma left 16   [60..63] 0
+ *   [64..71] U top 8   [72..79] U left 8   [80..87] V top 8   [88..95] V left 8
+ * Planes y/u/v and ry/ru/rv are MB-padded (stride mbw*16 / mbw*8), frame-major.
+ * levels: [nframes*mbw*mbh][25][16] int16, zigzag, blocks 0..15 Y, 16 Y2 (zero
+ * for I4 MBs), 17..20 U, 21..24 V (the ZwMbOut order).  seg_qi: [nframes][4]
+ * quantizer index (0..127) of each segment (Segment::init_matrices,
+ * types.rs:806). */
+#define ZW_XMB_RECORD_BYTES 96
+int zw_transform_quant_mbs(zw_ctx *ctx, int nframes, uint32_t mbw, uint32_t mbh, const uint8_t *y, const uint8_t *u,
+                           const uint8_t *v, const uint8_t *recs, const int32_t *seg_qi, int16_t *levels, uint8_t *ry,
+                           uint8_t *ru, uint8_t *rv);
+/* Device form: the quantiser table of nframes frames (zw_xmb_seg_table, host
+ * memory of zw_xmb_seg_table_bytes(nframes) bytes, copied by the caller to the
+ * device as d_segs), device pointers, enqueued on `stream` (NULL = the
+ * context's stream), asynchronous. */
+size_t zw_xmb_seg_table_bytes(int nframes);
+int zw_xmb_seg_table(int nframes, const int32_t *seg_qi, void *out);
+int zw_transform_quant_mbs_device(zw_ctx *ctx, void *stream, int nframes, uint32_t mbw, uint32_t mbh, const void *d_y,
+                                  const void *d_u, const void *d_v, const void *d_recs, const void *d_segs,
+                                  void *d_levels, void *d_ry, void *d_ru, void *d_rv);
 /* In-place loop filter of MB-aligned planes; per-MB flags (luma_mode 0..4,
  * segment, skip, non_zero_dct) as 4 bytes per MB, raster order. */
 int zw_loop_filter_frame(zw_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, uint32_t mbw, uint32_t mbh,
@@ -284,6 +322,9 @@ int zw_pipe_read_alpha(zw_pipe *p, int frame, uint8_t *alpha);
  * (fDCT coefficients[16], prediction[16], ctx0, sub-mode).  Enable before encoding. */
 int zw_pipe_enable_debug(zw_pipe *p);
 int zw_pipe_read_debug(zw_pipe *p, int frame, int32_t *out);
+/* Quantizer index of each of the frame's 4 segments in the last encode
+ * (Segment::quant_index, types.rs:761). */
+int zw_pipe_read_segments(zw_pipe *p, int frame, int32_t *seg_qi);
 /* Token probabilities (4*8*3*11) and skip probability used by pass 2. */
 int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
 /* The pipe splits its frames into lanes (env ZW_PIPE_LANES; default 2 from two launches of frames up, else 1), each with

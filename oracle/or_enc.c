@@ -1278,6 +1278,15 @@ static void transform_chroma(enc_t *e, int mbx, int mby, int mode, int32_t ub[64
     pred_chroma(mode, mbx, mby, e->top_v, e->left_v, pv);
     chroma_blocks(e, pu, e->U, mbx, mby, ub);
     chroma_blocks(e, pv, e->V, mbx, mby, vb);
+    if (e->dbg && e->dbg->derr_in && e->pass == 2) {
+        int8_t *d = e->dbg->derr_in + (size_t)(mby * e->mbw + mbx) * 8;
+        for (int ch = 0; ch < 2; ch++) {
+            d[4 * ch + 0] = e->top_derr[mbx][ch][0];
+            d[4 * ch + 1] = e->top_derr[mbx][ch][1];
+            d[4 * ch + 2] = e->left_derr[ch][0];
+            d[4 * ch + 3] = e->left_derr[ch][1];
+        }
+    }
     error_diffusion(e, ub, vb, mbx, &s->uv);
     for (int b = 0; b < 4; b++) {
         int32_t du[16], dv[16];
@@ -2039,3 +2048,141 @@ void or_seg_lambdas(uint32_t q, uint32_t out[8])
 }
 /* add_residue (prediction.rs:138) on a 4x4 block of stride 4 */
 void or_add_residue_kat(uint8_t pblock[16], const int32_t r[16]) { or_add_residue(pblock, r, 0, 0, 4); }
+
+/* ======================================================================== */
+/* Streaming final transform over explicit per-MB records (the arithmetic of  */
+/* transform_luma_block vp8.rs:2647-2780 with do_trellis off, of              */
+/* transform_luma_blocks_4x4 :2785-2916 and of transform_chroma_blocks        */
+/* :3039-3121 with apply_chroma_error_diffusion :572-647).  Every input the   */
+/* encoder would take from its running state (the borders create_border_luma */
+/* / create_border_chroma build, prediction.rs:15-130, and the incoming       */
+/* top/left error-diffusion terms) comes from the MB's 96-byte record instead */
+/* (layout in include/zwebp.h, zw_transform_quant_mbs), so MBs are            */
+/* independent.  Checker for the device kernel k_xform_mb.                    */
+/* ======================================================================== */
+static void xmb_luma_ws(const uint8_t *r, uint8_t ws[OR_LUMA_WS])
+{
+    memset(ws, 0, OR_LUMA_WS);
+    ws[0] = r[20];
+    for (int i = 0; i < 20; i++) ws[1 + i] = r[24 + i];
+    for (int i = 17; i < 21; i++) ws[4 * OR_BPS + i] = ws[8 * OR_BPS + i] = ws[12 * OR_BPS + i] = ws[i];
+    for (int i = 0; i < 16; i++) ws[(i + 1) * OR_BPS] = r[44 + i];
+}
+static void xmb_chroma_ws(const uint8_t *r, int plane, uint8_t ws[OR_CHROMA_WS])
+{
+    memset(ws, 0, OR_CHROMA_WS);
+    ws[0] = r[21 + plane];
+    for (int i = 0; i < 8; i++) ws[1 + i] = r[64 + 16 * plane + i];
+    for (int i = 0; i < 8; i++) ws[(i + 1) * OR_BPS] = r[72 + 16 * plane + i];
+}
+static void xmb_put_levels(int16_t *out, const int32_t *lvl)
+{
+    for (int n = 0; n < 16; n++) out[n] = (int16_t)lvl[ZIGZAG[n]];
+}
+
+void or_xform_mbs(int nframes, int mbw, int mbh, const uint8_t *Y, const uint8_t *U, const uint8_t *V,
+                  const uint8_t *recs, const int32_t *seg_qi, int16_t *levels, uint8_t *RY, uint8_t *RU, uint8_t *RV)
+{
+    const int ys = mbw * 16, cs = mbw * 8, nmb = mbw * mbh;
+    const size_t ysz = (size_t)ys * mbh * 16, csz = (size_t)cs * mbh * 8;
+    for (int f = 0; f < nframes; f++) {
+        seg_t seg[4];
+        for (int i = 0; i < 4; i++) seg_from_index(&seg[i], seg_qi[f * 4 + i], 0);
+        const uint8_t *Yf = Y + f * ysz, *Uf = U + f * csz, *Vf = V + f * csz;
+        uint8_t *RYf = RY + f * ysz, *RUf = RU + f * csz, *RVf = RV + f * csz;
+        for (int mb = 0; mb < nmb; mb++) {
+            const int mbx = mb % mbw, mby = mb / mbw;
+            const uint8_t *r = recs + ((size_t)f * nmb + mb) * 96;
+            int16_t *out = levels + ((size_t)f * nmb + mb) * 25 * 16;
+            const seg_t *s = &seg[r[2] & 3];
+            const int has_top = r[3] & 1, has_left = (r[3] >> 1) & 1;
+            uint8_t ws[OR_LUMA_WS];
+            int32_t lvl[16];
+            xmb_luma_ws(r, ws);
+            const uint8_t *src = Yf + (size_t)mby * 16 * ys + mbx * 16;
+            if (r[0] != 4) {
+                switch (r[0]) {
+                case 1: or_pred_v(ws, 16, 1, 1, OR_BPS); break;
+                case 2: or_pred_h(ws, 16, 1, 1, OR_BPS); break;
+                case 3: or_pred_tm(ws, 16, 1, 1, OR_BPS); break;
+                default: or_pred_dc(ws, 16, OR_BPS, has_top, has_left); break;
+                }
+                int32_t lb[256], c0[16], y2d[16];
+                for (int by = 0; by < 4; by++)
+                    for (int bx = 0; bx < 4; bx++)
+                        fdct_res(src + by * 4 * ys + bx * 4, ys, ws + (by * 4 + 1) * OR_BPS + bx * 4 + 1, OR_BPS,
+                                 lb + (by * 4 + bx) * 16);
+                for (int i = 0; i < 16; i++) c0[i] = lb[i * 16];
+                or_wht(c0);
+                for (int i = 0; i < 16; i++) {
+                    c0[i] = quant(&s->y2, c0[i], i);
+                    y2d[i] = dequant(&s->y2, c0[i], i);
+                }
+                xmb_put_levels(out + 16 * 16, c0);
+                or_iwht(y2d);
+                for (int i = 0; i < 16; i++) {
+                    int32_t *blk = lb + i * 16;
+                    lvl[0] = 0;
+                    for (int k = 1; k < 16; k++) {
+                        lvl[k] = quant(&s->y1, blk[k], k);
+                        blk[k] = dequant(&s->y1, lvl[k], k);
+                    }
+                    xmb_put_levels(out + i * 16, lvl);
+                    blk[0] = y2d[i];
+                    or_idct(blk);
+                    or_add_residue(ws, blk, 1 + (i / 4) * 4, 1 + (i % 4) * 4, OR_BPS);
+                }
+            } else {
+                for (int i = 0; i < 16; i++) out[16 * 16 + i] = 0;
+                for (int i = 0; i < 16; i++) {
+                    const int sby = i / 4, sbx = i % 4, y0 = sby * 4 + 1, x0 = sbx * 4 + 1;
+                    const int mode = (r[4 + i / 2] >> (4 * (i & 1))) & 15;
+                    or_pred_b(ws, mode, x0, y0, OR_BPS);
+                    int32_t cur[16];
+                    fdct_res(src + sby * 4 * ys + sbx * 4, ys, ws + y0 * OR_BPS + x0, OR_BPS, cur);
+                    for (int k = 0; k < 16; k++) {
+                        lvl[k] = quant(&s->y1, cur[k], k);
+                        cur[k] = dequant(&s->y1, lvl[k], k);
+                    }
+                    xmb_put_levels(out + i * 16, lvl);
+                    or_idct(cur);
+                    or_add_residue(ws, cur, y0, x0, OR_BPS);
+                }
+            }
+            store_recon(NULL, ws, 16, OR_BPS, RYf, ys, mbx * 16, mby * 16);
+            for (int plane = 0; plane < 2; plane++) {
+                uint8_t cw[OR_CHROMA_WS];
+                xmb_chroma_ws(r, plane, cw);
+                switch (r[1]) {
+                case 1: or_pred_v(cw, 8, 1, 1, OR_BPS); break;
+                case 2: or_pred_h(cw, 8, 1, 1, OR_BPS); break;
+                case 3: or_pred_tm(cw, 8, 1, 1, OR_BPS); break;
+                default: or_pred_dc(cw, 8, OR_BPS, has_top, has_left); break;
+                }
+                const uint8_t *P = plane ? Vf : Uf;
+                int32_t cb[64];
+                for (int by = 0; by < 2; by++)
+                    for (int bx = 0; bx < 2; bx++)
+                        fdct_res(P + (size_t)(mby * 8 + by * 4) * cs + mbx * 8 + bx * 4, cs,
+                                 cw + (by * 4 + 1) * OR_BPS + bx * 4 + 1, OR_BPS, cb + (by * 2 + bx) * 16);
+                /* apply_chroma_error_diffusion: incoming top/left terms from the record */
+                const int8_t *d = (const int8_t *)r + 12 + 4 * plane;
+                int8_t e0 = diffuse(&cb[0], d[0], d[2], &s->uv);
+                int8_t e1 = diffuse(&cb[16], d[1], e0, &s->uv);
+                int8_t e2 = diffuse(&cb[32], e0, d[3], &s->uv);
+                (void)diffuse(&cb[48], e1, e2, &s->uv);
+                for (int b = 0; b < 4; b++) {
+                    int32_t *blk = cb + b * 16;
+                    for (int k = 0; k < 16; k++) {
+                        lvl[k] = quant(&s->uv, blk[k], k);
+                        blk[k] = dequant(&s->uv, lvl[k], k);
+                    }
+                    xmb_put_levels(out + (17 + 4 * plane + b) * 16, lvl);
+                    or_idct(blk);
+                    or_add_residue(cw, blk, 1 + (b / 2) * 4, 1 + (b % 2) * 4, OR_BPS);
+                }
+                store_recon(NULL, cw, 8, OR_BPS, plane ? RVf : RUf, cs, mbx * 8, mby * 8);
+            }
+        }
+    }
+}

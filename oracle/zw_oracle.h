@@ -60,6 +60,8 @@ typedef struct {
     int seg_quant_index[4];
     int segments_enabled, filter_level, base_quant_index, skip_prob;
     int8_t p1_top_derr_last[1];
+    int8_t *derr_in;                      /* pass 2: mbw*mbh*8 incoming error-diffusion terms (U top0, top1,
+                                           * left0, left1, then V), the zw_transform_quant_mbs record order */
 } or_enc_debug;
 
 /* encode_frame_lossy (encoder/vp8.rs:3132): raw VP8 frame bytes (malloc'd). */
@@ -107,6 +109,10 @@ int or_encode_alpha(const uint8_t *data, size_t len, uint32_t width, uint32_t he
  * length-limit reassignment order of build_huffman_tree, api.rs:259-260);
  * sorts the (idx[i], key[i]) pairs in place. */
 void or_rust_sort_unstable_by_key(uint32_t *idx, uint32_t *key, size_t n);
+/* Streaming final transform over per-MB records (zw_transform_quant_mbs's
+ * checker): levels [nframes*mbw*mbh][25][16] zigzag, recon MB-padded planes. */
+void or_xform_mbs(int nframes, int mbw, int mbh, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                  const uint8_t *recs, const int32_t *seg_qi, int16_t *levels, uint8_t *ry, uint8_t *ru, uint8_t *rv);
 void or_yuv_to_rgb_simple_c(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, int bpp, uint8_t *out);
 void or_analyze(const uint8_t *Y, const uint8_t *U, const uint8_t *V, int width, int height,
                 uint8_t *mb_alphas, uint32_t histo[256]);

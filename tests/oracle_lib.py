@@ -29,7 +29,8 @@ class EncDebug(ctypes.Structure):
                 ("seg_quant_index", ctypes.c_int * 4),
                 ("segments_enabled", ctypes.c_int), ("filter_level", ctypes.c_int),
                 ("base_quant_index", ctypes.c_int), ("skip_prob", ctypes.c_int),
-                ("p1_top_derr_last", ctypes.c_int8 * 1)]
+                ("p1_top_derr_last", ctypes.c_int8 * 1),
+                ("derr_in", ctypes.c_void_p)]
 
 
 class FrameHdr(ctypes.Structure):
@@ -126,7 +127,8 @@ def encode(img, w, h, color, quality=75, method=4, debug=False, nparts=1):
                     recon1_y=np.zeros(ys, np.uint8),
                     mb_alpha=np.zeros(mbw * mbh, np.uint8), seg_map=np.zeros(mbw * mbh, np.uint8),
                     levels=np.zeros(mbw * mbh * 25 * 16, np.int32),
-                    i4_dump=np.zeros(mbw * mbh * 16 * 34, np.int32))
+                    i4_dump=np.zeros(mbw * mbh * 16 * 34, np.int32),
+                    derr_in=np.zeros(mbw * mbh * 8, np.int8))
         p1 = (MbInfo * (mbw * mbh))()
         p2 = (MbInfo * (mbw * mbh))()
         dbg = EncDebug()
@@ -262,3 +264,17 @@ def riff_vp8_chunk(data):
             return data[off + 8:off + 8 + size]
         off += 8 + size + (size & 1)
     raise ValueError("no VP8 chunk")
+
+
+def xform_mbs(y, u, v, recs, seg_qi, nframes, mbw, mbh):
+    """Streaming final transform over per-MB records (checker of zw_transform_quant_mbs).
+    Returns (levels (nframes*nmb, 25, 16) int16 zigzag, ry, ru, rv)."""
+    nmb = mbw * mbh
+    y, u, v = (np.ascontiguousarray(a, dtype=np.uint8).reshape(-1) for a in (y, u, v))
+    r = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1)
+    q = np.ascontiguousarray(seg_qi, dtype=np.int32).reshape(-1)
+    assert r.size == nframes * nmb * 96 and q.size == nframes * 4
+    lv = np.zeros((nframes * nmb, 25, 16), np.int16)
+    ry, ru, rv = np.zeros_like(y), np.zeros_like(u), np.zeros_like(v)
+    lib().or_xform_mbs(nframes, mbw, mbh, _p(y), _p(u), _p(v), _p(r), _p(q), _p(lv), _p(ry), _p(ru), _p(rv))
+    return lv, ry, ru, rv
