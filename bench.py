@@ -406,10 +406,7 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
                 os.environ[k] = v
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * frames
     ach = 1208 * nmb / ((rk + lf) * 1e-3) / 1e9
-    out = {"verified": tags is not None and vy[1] + vy[2] + vr[1] + vr[2] == 0 and vy[0] > 0 and vr[0] > 0,
-           "verification": {"yuv": {"matched": vy[0], "mismatched": vy[1], "no_digest": vy[2]},
-                            "rgba": {"matched": vr[0], "mismatched": vr[1], "no_digest": vr[2]},
-                            "against": "dec_yuv/ and dec_rgba/ oracle digests (decode_frame, fill_rgba fancy)"},
+    out = {"verified": False, "verification": None,
            "single_frame_ms": single_ms, "single_frame_kernel_ms": {"k_dec_recon": rk1, "k_loopfilter": lf1},
            "batch_frames": frames, "batch_decodes_per_s": frames / el,
            "batch_kernel_ms": {"k_dec_recon": rk, "k_loopfilter": lf, "launch": "whole batch, one workgroup per frame"},
@@ -431,6 +428,10 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
         for i, b in enumerate(bufs):
             tally(vr, "dec_rgba/" + tags[i % len(streams)], b)
     del bufs
+    out["verified"] = tags is not None and vy[1] + vy[2] + vr[1] + vr[2] == 0 and vy[0] > 0 and vr[0] > 0
+    out["verification"] = {"yuv": {"matched": vy[0], "mismatched": vy[1], "no_digest": vy[2]},
+                           "rgba": {"matched": vr[0], "mismatched": vr[1], "no_digest": vr[2]},
+                           "against": "dec_yuv/ and dec_rgba/ oracle digests (decode_frame, fill_rgba fancy)"}
     zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
     t0 = time.perf_counter()
     zwebp.decode_rgb_batch(batch, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
@@ -776,7 +777,9 @@ def main():
             "host_emit_frames_per_s_per_core": B / (emit_s * threads) if emit_s > 0 else None,
             "avg_frame_bytes": bytes_out / max(1, min(B, D)),
         }
-        if not a.no_extras:
+        # the extra legs are single-GPU measurements: only the N=1 run carries them
+        extras = not a.no_extras and world == 1
+        if extras:
             q, m = a.quality, a.method
             tags = [f"{w}x{h}/q{q}m{m}/{sd:#010x}" for sd in seeds]
             lk = launch_kernel_times(ctx, imgs, w, h, q, m, min(B, 256))
@@ -832,7 +835,7 @@ def main():
         line["cpu_baseline"] = None
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(imgs, w, h, a.quality, a.method, a.cpu_seconds, digests)
-        if not a.no_extras:
+        if extras:
             cb = line["cpu_baseline"] or {}
             line["configs"] = {
                 "1_768x512_cpu_reference_path": {"verified": bool(cb.get("config1", {}).get("verified")) and

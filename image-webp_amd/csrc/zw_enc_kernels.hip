@@ -3301,6 +3301,24 @@ extern "C" hipError_t zwk_segments(hipStream_t s, uint32_t* histo, const ZwFrame
     return hipGetLastError();
 }
 
+// The widest frame (in MBs) whose per-frame LDS arrays (top rows, contexts)
+// fit the 160 KiB of a CU in every encode kernel shape.  encode_frame_lossy
+// takes any u16 width (vp8.rs:3143-3148); wider frames than this return
+// ZW_EINVALID_DIMENSIONS (boundary).
+extern "C" int zwk_encode_max_mbw(void)
+{
+    const int nws[4] = {PassShape<1>::NW, PassShape<2>::NW, RowsShape<1>::NW, 1};
+    int lo = 1, hi = 65536 / 16;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        bool ok = true;
+        for (int i = 0; i < 4; i++) ok = ok && encode_lds_bytes(mid, nws[i]) <= 160 * 1024;
+        if (ok) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 // Bytes of zero-filled scratch the row-parallel kernels need for nframes frames.
 extern "C" size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes)
 {

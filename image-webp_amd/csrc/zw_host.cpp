@@ -52,6 +52,7 @@ hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* 
                       ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
                       int nframes, int* dbg, uint8_t* rows, uint32_t* sizes = nullptr);
 size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
+int zwk_encode_max_mbw(void);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -429,12 +430,24 @@ static bool pipe_rows_for(int chunk, int mbh, int device)
     return (long long)chunk * (mbh + 1) <= 12LL * cus;  // measured: rows win up to ~48 1080p frames
 }
 
+// encode_frame_lossy's dimension rule (vp8.rs:3143-3148): any u16, the header
+// keeping the low 14 bits (vp8.rs:326-327; zwh::emit_frame does the same).
+// Zero is refused (the reference has no meaningful zero-MB frame), and so is a
+// width whose per-frame LDS rows exceed a CU (zwk_encode_max_mbw MBs, about
+// 27 000 pixels): the one divergence, documented in INTEGRATION.md.
+static bool encode_dims_ok(uint32_t width, uint32_t height)
+{
+    if (width == 0 || height == 0 || width > 65535 || height > 65535) return false;
+    static const int max_mbw = zwk_encode_max_mbw();
+    return (int)((width + 15) / 16) <= max_mbw;
+}
+
 extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t height, int color, uint8_t quality,
                               uint8_t method, zw_pipe** out)
 {
     if (!ctx || !out || n <= 0) return ZW_EINVAL;
     *out = nullptr;
-    if (width == 0 || height == 0 || width > 16383 || height > 16383) return ZW_EINVALID_DIMENSIONS;
+    if (!encode_dims_ok(width, height)) return ZW_EINVALID_DIMENSIONS;
     if (color < 0 || color > 3) return ZW_EINVAL;
     if (quality > 100) return ZW_EINVAL;
     HIPOK(hipSetDevice(ctx->device));
@@ -1101,8 +1114,7 @@ extern "C" int zw_pipe_read_alpha(zw_pipe* p, int frame, uint8_t* alpha)
 static int check_encode_args(const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
                              uint8_t quality)
 {
-    if (width > 65535 || height > 65535 || width == 0 || height == 0) return ZW_EINVALID_DIMENSIONS;
-    if (width > 16383 || height > 16383) return ZW_EINVALID_DIMENSIONS; /* 14-bit VP8 header fields */
+    if (!encode_dims_ok(width, height)) return ZW_EINVALID_DIMENSIONS;
     if (color < 0 || color > 3) return ZW_EINVAL;
     static const int bpp_of[4] = {1, 2, 3, 4};
     if ((uint64_t)width * height * bpp_of[color] != len || !data) return ZW_EINVALID_BUFFER_SIZE;

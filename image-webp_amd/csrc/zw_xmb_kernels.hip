@@ -54,6 +54,7 @@ struct XmbLds {
     uint32_t ct[2][8][16];       // U, V tiles: 8 rows x 8 MBs x 8 B
     uint8_t ws[4][17 * ZW_BPS + 4];  // I4 work buffers (origin at byte 3: row pixels dword aligned)
     uint8_t vv[64][40];          // per-lane I4 value vectors (dec_i4_values layout)
+    XmbSeg seg[4];               // the frame's four segment matrices (per-lane segment reads hit LDS, not HBM)
 };
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
@@ -141,7 +142,10 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
                                                            uint8_t* __restrict__ RU, uint8_t* __restrict__ RV)
 {
     __shared__ XmbLds lds[XMB_WAVES];
+    __shared__ uint8_t i4idx[10][16];  // d_I4_IDX
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (!COPY && threadIdx.x < 40) ((uint32_t*)i4idx)[threadIdx.x] = ((const uint32_t*)d_I4_IDX)[threadIdx.x];
+    __syncthreads();
     XmbLds& L = lds[wv];
     const int ngx = (mbw + XMB_MBS - 1) / XMB_MBS;
     const long long id = (long long)blockIdx.x * XMB_WAVES + wv;
@@ -176,14 +180,18 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
             c0 = __builtin_nontemporal_load((const v2u*)(Uf + cr * cs + cm * 8));
             c1 = __builtin_nontemporal_load((const v2u*)(Vf + cr * cs + cm * 8));
         }
+        // the frame's segment table: 4 x 96 B = 24 lines of 16 B
+        v4u s4 = {0u, 0u, 0u, 0u};
+        if (!COPY && lane >= 40) s4 = *((const v4u*)(segs + (size_t)f * 4) + (lane - 40));
         if (lane < 48) *(v4u*)&L.rec[rm][4 * rq] = r4;
+        if (!COPY && lane >= 40) *((v4u*)L.seg + (lane - 40)) = s4;
         *(v4u*)&L.yt[yr][4 * yc] = y0;
         *(v4u*)&L.yt[yr + 8][4 * yc] = y1;
         *(v2u*)&L.ct[0][cr][2 * cm] = c0;
         *(v2u*)&L.ct[1][cr][2 * cm] = c1;
         wsync();
     }
-    const XmbSeg* S = segs + (size_t)f * 4;
+    const XmbSeg* S = L.seg;
 
     if (COPY) {
         // calibration: the same loads and stores, no arithmetic
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
                             uint32_t w = 0;
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
-                                const int idx = d_I4_IDX[sm][4 * r + j];
+                                const int idx = i4idx[sm][4 * r + j];
                                 int v;
                                 if (idx == 254) v = clamp255(E[3 - r] + E[5 + j] - E[4]);
                                 else v = vv[idx == 255 ? 38 : idx];

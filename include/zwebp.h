@@ -134,12 +134,18 @@ int zw_encode_frame_lossy(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t
                           int color, uint8_t quality, uint8_t method, zw_bytes *out);
 
 /* The same with token_partitions (1, 2, 4 or 8) residual partitions: MB row y's
- * tokens go to partition y % n (the reference encoder's partition machinery,
- * vp8.rs:352-354 / :1419-1421, fixed there at one partition, vp8.rs:273); the
- * partition sizes follow the first partition as RFC 6386 9.5 and the reference
- * decoder (decoder/vp8.rs:421-450) read them.  1 gives encode_frame_lossy's
- * bytes.  A single frame's partitions are entropy-coded on parallel host
- * threads.  ZW_EINVAL for any other count. */
+ * tokens go to partition y % n (the row-to-partition map of the reference
+ * encoder, vp8.rs:352-354 / :1419-1421, which fixes one partition, vp8.rs:273).
+ * The partition-size LAYOUT deliberately follows RFC 6386 9.5 and the reference
+ * DECODER (decoder/vp8.rs:421-450): all n-1 sizes right after the first
+ * partition, then the partitions.  It does NOT follow the reference encoder's
+ * write_partitions (vp8.rs:381-386), which would put each size directly before
+ * its partition; that writer is unreachable there (one partition) and its
+ * layout is not one decoders read.  Byte parity for n > 1 is therefore not
+ * pinned by any reference fixture; the checks are the oracle's identical
+ * bytes plus libwebp / device decodes to the same pixels.  1 gives
+ * encode_frame_lossy's bytes.  A single frame's partitions are entropy-coded
+ * on parallel host threads.  ZW_EINVAL for any other count. */
 int zw_encode_frame_lossy_ex(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
                              int color, uint8_t quality, uint8_t method, int token_partitions, zw_bytes *out);
 

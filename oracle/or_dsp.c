@@ -272,6 +272,21 @@ void or_add_residue(uint8_t *ws, const int32_t r[16], int y0, int x0, int stride
 
 static inline uint8_t avg3(int l, int t, int r) { return (uint8_t)((l + 2 * t + r + 2) >> 2); }
 static inline uint8_t avg2(int t, int r) { return (uint8_t)((t + r + 1) >> 1); }
+/* KAT entry points: avg3 / avg2 (prediction.rs:154-161) and the edge gathers
+ * top_pixels (:349) / edge_pixels (:373) as or_i4_preds below reads them. */
+int or_avg3(int l, int t, int r) { return avg3(l, t, r); }
+int or_avg2(int t, int r) { return avg2(t, r); }
+void or_top_pixels(const uint8_t *a, int x0, int y0, int stride, uint8_t out[8])
+{
+    memcpy(out, a + (y0 - 1) * stride + x0, 8);
+}
+void or_edge_pixels(const uint8_t *a, int x0, int y0, int stride, uint8_t out[9])
+{
+    /* e0..e3: left column bottom-up, e4: corner, e5..e8: top row */
+    for (int k = 0; k < 4; k++) out[k] = a[(y0 + 3 - k) * stride + x0 - 1];
+    out[4] = a[(y0 - 1) * stride + x0 - 1];
+    for (int k = 0; k < 4; k++) out[5 + k] = a[(y0 - 1) * stride + x0 + k];
+}
 
 /* predict_vpred, prediction.rs:164 */
 void or_pred_v(uint8_t *a, int size, int x0, int y0, int stride)
@@ -316,12 +331,12 @@ void or_pred_tm(uint8_t *a, int size, int x0, int y0, int stride)
 /* I4Predictions::compute, prediction.rs:568-855 (all ten 4x4 predictors). */
 void or_i4_preds(const uint8_t *src, int x0, int y0, int stride, uint8_t d[10][16])
 {
-    int p = src[(y0 - 1) * stride + x0 - 1];
-    const uint8_t *T = src + (y0 - 1) * stride + x0;
+    uint8_t T[8], E[9];
+    or_top_pixels(src, x0, y0, stride, T);
+    or_edge_pixels(src, x0, y0, stride, E);
     int a0 = T[0], a1 = T[1], a2 = T[2], a3 = T[3], a4 = T[4], a5 = T[5], a6 = T[6], a7 = T[7];
-    int l0 = src[y0 * stride + x0 - 1], l1 = src[(y0 + 1) * stride + x0 - 1];
-    int l2 = src[(y0 + 2) * stride + x0 - 1], l3 = src[(y0 + 3) * stride + x0 - 1];
-    int e0 = l3, e1 = l2, e2 = l1, e3 = l0, e4 = p, e5 = a0, e6 = a1, e7 = a2, e8 = a3;
+    int e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3], e4 = E[4], e5 = E[5], e6 = E[6], e7 = E[7], e8 = E[8];
+    int p = e4, l0 = e3, l1 = e2, l2 = e1, l3 = e0;
     /* DC */
     {
         uint32_t v = 4 + a0 + a1 + a2 + a3 + l0 + l1 + l2 + l3;

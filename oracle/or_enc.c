@@ -2046,6 +2046,22 @@ void or_seg_lambdas(uint32_t q, uint32_t out[8])
     const uint32_t v[8] = {s.l_i4, s.l_i16, s.l_uv, s.l_mode, s.lt_i4, s.lt_i16, s.lt_uv, s.tlambda};
     memcpy(out, v, sizeof v);
 }
+/* calc_i4_penalty (cost.rs:341-343): max(1000 q^2, 1).  Not on the encode
+ * path (the reference never calls it outside its test, cost.rs:2110-2119);
+ * restated only so the KAT pins the formula. */
+uint64_t or_i4_penalty(uint32_t q)
+{
+    const uint64_t p = 1000ull * q * q;
+    return p > 1 ? p : 1;
+}
+/* rd_score_with_coeffs (cost.rs:1108-1112): sse * 256 + (mode + coeff) * lambda.
+ * Also off the path (used only by its test, cost.rs:2210-2223). */
+uint64_t or_rd_score_with_coeffs(uint32_t sse, uint32_t mode_cost, uint32_t coeff_cost, uint32_t lambda)
+{
+    return (uint64_t)sse * 256u + ((uint64_t)(uint16_t)mode_cost + coeff_cost) * lambda;
+}
+/* VP8_ENC_BANDS (tables.rs), the band of zigzag position n (n = 16: the eob sentinel) */
+int or_enc_band(int n) { return VP8_ENC_BANDS[n]; }
 /* add_residue (prediction.rs:138) on a 4x4 block of stride 4 */
 void or_add_residue_kat(uint8_t pblock[16], const int32_t r[16]) { or_add_residue(pblock, r, 0, 0, 4); }
 

@@ -255,6 +255,33 @@ def test_encode_api_errors(ctx):
     assert e.value.code in (1, 2)
 
 
+@pytest.mark.parametrize("w,h", [(16400, 16), (16, 20000), (25088, 8)])
+def test_encode_beyond_14bit_dims(ctx, w, h):
+    """encode_frame_lossy accepts any u16 dimension (vp8.rs:3143-3148) and the
+    header keeps the low 14 bits (vp8.rs:326-327): the product's bytes equal the
+    oracle's up to the widest frame whose LDS rows fit a CU (1568 MBs)."""
+    img = np.ascontiguousarray(synth_rgba(w, h, 0x5EED2000 + w)[..., :3])
+    rc, ref, _ = O.encode(img, w, h, 2, 75, 4)
+    assert rc == 0
+    out = zwebp.encode_frame_lossy(img, w, h, 2, 75, 4, ctx=ctx)
+    assert out == ref
+    assert int.from_bytes(out[6:8], "little") == w & 0x3FFF and int.from_bytes(out[8:10], "little") == h & 0x3FFF
+
+
+def test_encode_width_beyond_lds_is_refused(ctx):
+    """The documented divergence: wider than 1568 MBs the
+    product returns InvalidDimensions where the reference would encode."""
+    w, h = 25089, 1
+    img = np.zeros(w * h * 3, np.uint8)
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossy(img, w, h, 2, 75, 4, ctx=ctx)
+    assert e.value.code == 1
+    assert O.encode(img, w, h, 2, 75, 4)[0] == 0
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_frame_lossy(np.zeros(65536 * 3, np.uint8), 65536, 1, 2, 75, 4, ctx=ctx)
+    assert e.value.code == 1
+
+
 def test_webp_container(ctx):
     w, h = 48, 32
     img = np.ascontiguousarray(synth_rgba(w, h)[..., :3])

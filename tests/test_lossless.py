@@ -141,6 +141,54 @@ def test_rust_sort_unstable_is_not_stable():
     assert not np.array_equal(idx, _stable_order(keys))
 
 
+# Drift guards.  Where these came from: the oracle's restatement of
+# Rust 1.92 core::slice::sort::unstable (ipnsort) at commit c7fefce, reviewed
+# against that algorithm (insertion sort <= 20, run detection, limit
+# 2*ilog2(len|1), small-sort cutoff 32 for (usize, u32), median3_rec, ancestor
+# pivot, cyclic Lomuto partition, heapsort fallback).  No Rust toolchain exists
+# here, so they pin the restatement against later edits, NOT against Rust itself:
+# parity with the reference's VP8L bytes stays unpinned (no VP8L byte fixtures
+# ship with the reference).
+PINNED_SORT = [
+    (np.array([(i * 7 + 3) % 5 for i in range(48)], np.uint32),
+     [1, 6, 11, 16, 21, 26, 31, 36, 41, 46, 4, 9, 14, 19, 24, 29, 34, 39, 44, 42, 2, 22, 27, 12, 32, 37, 7, 17, 47,
+      20, 10, 25, 5, 30, 35, 15, 40, 0, 45, 23, 28, 13, 33, 3, 38, 43, 18, 8]),
+    (np.array([(i * i * 13 + 7) % 9 for i in range(100)], np.uint32),
+     [1, 8, 10, 17, 19, 26, 28, 35, 37, 44, 46, 53, 55, 62, 64, 71, 73, 80, 82, 89, 91, 98, 52, 97, 25, 7, 29, 34, 2,
+      38, 43, 11, 47, 56, 61, 65, 70, 16, 74, 79, 83, 88, 20, 92, 63, 99, 33, 48, 51, 0, 12, 54, 6, 57, 60, 27, 15, 36,
+      66, 24, 9, 30, 72, 39, 75, 78, 18, 81, 84, 87, 42, 90, 21, 3, 93, 96, 45, 69, 32, 40, 67, 68, 5, 41, 13, 85, 86,
+      49, 14, 31, 23, 4, 50, 58, 94, 95, 76, 77, 22, 59]),
+]
+# SHA-256 of the tie-split image's VP8L (predictor on / off) and ALPH payloads,
+# same provenance: the oracle at c7fefce.
+PINNED_TIED = {"vp8l_pred": "6cbb062244e0a3d8ecf6570b386da2e0e7f8f8b77f9fa90a9ccfee458f528e5a",
+               "vp8l_nopred": "34ac80c9cc73112b21fc81bd6b6848cac38b0e8e43c566bbd952420bbfa95a0e",
+               "alph": "ac975ba636b085ad030b9db4dec047dfd098e31abdcefb0b730ba50043dc83b0"}
+
+
+@pytest.mark.parametrize("case", range(len(PINNED_SORT)))
+def test_rust_sort_unstable_pinned(case):
+    keys, want = PINNED_SORT[case]
+    idx, _ = O.rust_sort_unstable_by_key(keys)
+    assert idx.tolist() == want
+
+
+def test_tie_split_bytes_pinned():
+    """The oracle AND the product's host coder give the pinned bytes on the image
+    whose length-limited trees split tie groups (so both sort restatements are
+    held to the same permutation, not just to each other)."""
+    import hashlib
+    name, w, h, img = next(i for i in IMAGES if i[0] == "tied640x256")
+    img = np.ascontiguousarray(img)
+    for pred, key in ((True, "vp8l_pred"), (False, "vp8l_nopred")):
+        rc, ref = O.encode_lossless(img, w, h, 3, pred)
+        assert rc == 0 and hashlib.sha256(bytes(ref)).hexdigest() == PINNED_TIED[key]
+        assert hashlib.sha256(bytes(zwebp.encode_frame_lossless(img, w, h, 3, pred))).hexdigest() == PINNED_TIED[key]
+    rc, a = O.encode_alpha(img, w, h, 3)
+    assert rc == 0 and hashlib.sha256(bytes(a)).hexdigest() == PINNED_TIED["alph"]
+    assert hashlib.sha256(bytes(zwebp.encode_alpha(img, w, h, 3))).hexdigest() == PINNED_TIED["alph"]
+
+
 def test_oracle_lossless_errors():
     img = np.zeros((4, 4, 4), np.uint8)
     assert O.encode_lossless(img, 4, 4, 3)[0] == 0

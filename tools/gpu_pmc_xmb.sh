@@ -13,4 +13,4 @@ run sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM
 run sq2 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE; rc=$?; fatal $rc && exit $rc
 run fetch --pmc FETCH_SIZE; rc=$?; fatal $rc && exit $rc
 run write --pmc WRITE_SIZE; rc=$?; fatal $rc && exit $rc
-timeout -k 10 120 python3 tools/xmb_bench.py --no-i4 > gpurun_out/pmc/noi4.log 2>&1; echo "[noi4] rc=$?"; tail -1 gpurun_out/pmc/noi4.log
+
