@@ -270,18 +270,25 @@ def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
                              "pass_over_copy": ms_copy / ms}}
 
 
-def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, digests=None):
+def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, digests=None, imgs=None):
     """SURVEY 8(d)'s HBM-roofline pass: the streaming DCT+quant pass over per-MB
-    records (k_xform_mb, zw_transform_quant_mbs_device) on `frames` 1080p frames
-    resident in HBM.  The records carry the modes, segments and reconstructed
-    borders the timed encode chose for its first `nd` distinct frames
-    (Pipeline.mbinfo / planes) and deterministic error-diffusion inputs
-    (zwebp.xmb.synthetic_derr); frame i is distinct frame i % nd.  Algorithmic
-    bytes 1568 per MB (source 384 + levels 800 + recon 384); the 96-byte record
-    is traffic the pass moves but 8(d) does not count.  HIP events on the launch
-    stream; the copy ceiling (ZW_XMB_VARIANT=99) moves the same bytes with no
-    arithmetic.  Outside the timed region every frame's levels and
-    reconstruction are hashed against the oracle's digests (make_bench_digests.py)."""
+    records (k_xform_mb + k_xform_mb_i4) on `frames` frames resident in HBM, in
+    both source forms:
+      "rgba": BASELINE config 2 -- the synthetic RGBA frames in, convert_image_yuv
+              fused into the pass (zw_transform_quant_mbs_rgb_device); algorithmic
+              bytes per frame = the RGBA read w*h*4 + levels 800 + recon 384 per MB
+              (8(d)'s fused form, with the true RGBA size instead of 1 024 B/MB);
+      "yuv":  the MB-padded Y/U/V planes in (zw_transform_quant_mbs_device);
+              1 568 B/MB (source 384 + levels 800 + recon 384).
+    The records carry the modes, segments and reconstructed borders the timed
+    encode chose for its first `nd` distinct frames (Pipeline.mbinfo / planes)
+    and deterministic error-diffusion inputs (zwebp.xmb.synthetic_derr); frame
+    i is distinct frame i % nd.  The 96-byte record is traffic the pass moves
+    but 8(d) does not count.  HIP events on the launch stream; the copy ceiling
+    (ZW_XMB_VARIANT=99) moves the same bytes without the transform arithmetic.
+    Outside the timed region every frame's levels and reconstruction are hashed
+    against the oracle's digests (make_bench_digests.py) -- the same digests for
+    both forms, since the fused conversion must give the pipe's planes."""
     import numpy as np
     import zwebp
     from zwebp.xmb import build_records, synthetic_derr
@@ -295,25 +302,20 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
         srcs.append(pipe.planes(i, 0))
         sq.append(pipe.segments(i))
     pick = [i % nd for i in range(frames)]
-    tY = torch.from_numpy(np.concatenate([srcs[i][0] for i in pick])).to(dev)
-    tU = torch.from_numpy(np.concatenate([srcs[i][1] for i in pick])).to(dev)
-    tV = torch.from_numpy(np.concatenate([srcs[i][2] for i in pick])).to(dev)
     tR = torch.from_numpy(np.concatenate([recs[i].reshape(-1) for i in pick])).to(dev)
     tS = torch.from_numpy(zwebp.xmb_seg_table(np.stack([sq[i] for i in pick]))).to(dev)
     lv = torch.empty(frames * nmb * 400, dtype=torch.int16, device=dev)
-    oY, oU, oV = torch.empty_like(tY), torch.empty_like(tU), torch.empty_like(tV)
+    oY = torch.empty(frames * nmb * 256, dtype=torch.uint8, device=dev)
+    oU = torch.empty(frames * nmb * 64, dtype=torch.uint8, device=dev)
+    oV = torch.empty_like(oU)
     stream = torch.cuda.Stream(dev)
     sh = stream.cuda_stream
+    mbs = frames * nmb
 
-    def run():
-        zwebp.transform_quant_mbs_device(frames, mbw, mbh, tY.data_ptr(), tU.data_ptr(), tV.data_ptr(), tR.data_ptr(),
-                                         tS.data_ptr(), lv.data_ptr(), oY.data_ptr(), oU.data_ptr(), oV.data_ptr(),
-                                         stream=sh, ctx=ctx)
-
-    ms = timed_launches(torch, dev, stream, run, reps)
-    # output check (outside the timed region): every frame against its distinct frame's digest
-    ok = bad = miss = 0
-    if digests is not None:
+    def check():
+        ok = bad = miss = 0
+        if digests is None:
+            return ok, bad, miss
         L = lv.view(frames, nmb * 400).cpu().numpy()
         Y, U, V = (t.view(frames, -1).cpu().numpy() for t in (oY, oU, oV))
         for f in range(frames):
@@ -325,31 +327,59 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
             for a in (L[f], Y[f], U[f], V[f]):
                 hsh.update(a.tobytes())
             ok, bad = (ok + 1, bad) if hsh.hexdigest() == want else (ok, bad + 1)
-    prev = os.environ.get("ZW_XMB_VARIANT")
-    os.environ["ZW_XMB_VARIANT"] = "99"
-    try:
-        ms_copy = timed_launches(torch, dev, stream, run, reps)
-    finally:
-        if prev is None:
-            os.environ.pop("ZW_XMB_VARIANT", None)
-        else:
-            os.environ["ZW_XMB_VARIANT"] = prev
+        return ok, bad, miss
+
+    def leg(run, alg, src_moved, name):
+        lv.zero_()
+        ms = timed_launches(torch, dev, stream, run, reps)
+        ok, bad, miss = check()
+        prev = os.environ.get("ZW_XMB_VARIANT")
+        os.environ["ZW_XMB_VARIANT"] = "99"
+        try:
+            ms_copy = timed_launches(torch, dev, stream, run, reps)
+        finally:
+            if prev is None:
+                os.environ.pop("ZW_XMB_VARIANT", None)
+            else:
+                os.environ["ZW_XMB_VARIANT"] = prev
+        moved = src_moved + mbs * (1184 + XMB_RECORD_BYTES)
+        ach = alg / (ms * 1e-3) / 1e9
+        copy_gbs = moved / (ms_copy * 1e-3) / 1e9
+        return {"kernel": "k_xform_mb + k_xform_mb_i4", "source": name,
+                "workload": f"{frames} frames x {nmb} MBs ({w}x{h}), the timed encode's modes",
+                "mbs_per_launch": mbs, "alg_bytes_per_launch": alg, "alg_bytes_per_mb": alg / mbs,
+                "record_bytes_per_mb": XMB_RECORD_BYTES, "ms_per_launch": ms, "achieved": ach,
+                "frac": ach / HBM_PEAK_GBS, "achieved_incl_records": moved / (ms * 1e-3) / 1e9,
+                "verified": bad == 0 and miss == 0 and ok == frames,
+                "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad,
+                                 "no_digest": miss},
+                "copy_ceiling": {"kernel": "k_xform_mb<copy> (ZW_XMB_VARIANT=99: the same loads and stores, no "
+                                           "transform arithmetic)", "ms_per_launch": ms_copy, "achieved": copy_gbs,
+                                 "frac": copy_gbs / HBM_PEAK_GBS, "pass_over_copy": ms_copy / ms}}
+
+    out = {}
+    if imgs is not None:
+        fb = w * h * 4
+        tI = torch.from_numpy(np.concatenate([np.ascontiguousarray(imgs[i]).reshape(-1) for i in pick])).to(dev)
+
+        def run_rgba():
+            zwebp.transform_quant_mbs_rgb_device(frames, w, h, 4, tI.data_ptr(), fb, tR.data_ptr(), tS.data_ptr(),
+                                                 lv.data_ptr(), oY.data_ptr(), oU.data_ptr(), oV.data_ptr(),
+                                                 stream=sh, ctx=ctx)
+        out["rgba"] = leg(run_rgba, frames * (fb + 1184 * nmb), frames * fb, "RGBA frames (fused convert_image_yuv)")
+        del tI
+    tY = torch.from_numpy(np.concatenate([srcs[i][0] for i in pick])).to(dev)
+    tU = torch.from_numpy(np.concatenate([srcs[i][1] for i in pick])).to(dev)
+    tV = torch.from_numpy(np.concatenate([srcs[i][2] for i in pick])).to(dev)
+
+    def run_yuv():
+        zwebp.transform_quant_mbs_device(frames, mbw, mbh, tY.data_ptr(), tU.data_ptr(), tV.data_ptr(), tR.data_ptr(),
+                                         tS.data_ptr(), lv.data_ptr(), oY.data_ptr(), oU.data_ptr(), oV.data_ptr(),
+                                         stream=sh, ctx=ctx)
+    out["yuv"] = leg(run_yuv, mbs * ALG_BYTES_PER_MB, mbs * 384, "MB-padded Y/U/V planes")
     del tY, tU, tV, tR, tS, lv, oY, oU, oV
     torch.cuda.empty_cache()
-    mbs = frames * nmb
-    alg = mbs * ALG_BYTES_PER_MB
-    moved = mbs * (ALG_BYTES_PER_MB + XMB_RECORD_BYTES)
-    ach = alg / (ms * 1e-3) / 1e9
-    copy_gbs = moved / (ms_copy * 1e-3) / 1e9
-    return {"kernel": "k_xform_mb", "workload": f"{frames} frames x {nmb} MBs ({w}x{h}), the timed encode's modes",
-            "mbs_per_launch": mbs, "alg_bytes_per_mb": ALG_BYTES_PER_MB, "alg_bytes_per_launch": alg,
-            "record_bytes_per_mb": XMB_RECORD_BYTES, "ms_per_launch": ms, "achieved": ach,
-            "frac": ach / HBM_PEAK_GBS, "achieved_incl_records": moved / (ms * 1e-3) / 1e9,
-            "verified": bad == 0 and miss == 0 and ok == frames,
-            "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss},
-            "copy_ceiling": {"kernel": "k_xform_mb<copy> (ZW_XMB_VARIANT=99: same loads and stores, no arithmetic)",
-                             "ms_per_launch": ms_copy, "achieved": copy_gbs, "frac": copy_gbs / HBM_PEAK_GBS,
-                             "pass_over_copy": ms_copy / ms}}
+    return out
 
 
 def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
@@ -786,11 +816,16 @@ def main():
             line["kernel_ms_per_launch"] = lk
             er = encode_roofline(lk["encode_pass2"], lk["launch_frames"], nmb)
             line["encode_roofline"] = er
-            xm = xmb_pass(ctx, torch, dev, pipes[0][0], min(B, D), seeds, w, h, q, m, 256, 10, digests)
+            xa = xmb_pass(ctx, torch, dev, pipes[0][0], min(B, D), seeds, w, h, q, m, 256, 10, digests, imgs)
+            xm = xa["rgba"]
             line["roofline"] = {"bound": "hbm", "achieved": xm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": xm["frac"], "traffic": pmc_traffic(XMB_PMC, xm["mbs_per_launch"]),
-                                "kernel": "k_xform_mb", "workload": xm["workload"],
-                                "mbs_per_launch": xm["mbs_per_launch"], "alg_bytes_per_mb": ALG_BYTES_PER_MB,
+                                "kernel": "k_xform_mb<RGBA> + k_xform_mb_i4 (BASELINE config 2: RGBA in, "
+                                          "DCT/quant/IDCT, levels + reconstructed YUV out)",
+                                "workload": xm["workload"], "mbs_per_launch": xm["mbs_per_launch"],
+                                "alg_bytes_per_mb": xm["alg_bytes_per_mb"],
+                                "alg_bytes_note": "RGBA read (w*h*4 per frame) + levels 800 + recon 384 per MB: "
+                                                  "SURVEY 8(d)'s fused-RGB->YUV form",
                                 "alg_bytes_per_launch": xm["alg_bytes_per_launch"],
                                 "ms_per_launch": xm["ms_per_launch"],
                                 "record_bytes_per_mb": XMB_RECORD_BYTES,
@@ -798,6 +833,7 @@ def main():
                                 "copy_ceiling": xm["copy_ceiling"], "verified": xm["verified"],
                                 "verification": xm["verification"],
                                 "traffic_source": "profiles/r03_xmb_pmc.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)",
+                                "yuv_planes_form": xa["yuv"],
                                 "fused_path": {"kernel": "k_encode_pass2 (RD search fused with the final "
                                                          "DCT+quant+recon, the timed step's dominant kernel)",
                                                "hbm_frac": er["hbm_frac"] if er else None,
@@ -841,7 +877,8 @@ def main():
                 "1_768x512_cpu_reference_path": {"verified": bool(cb.get("config1", {}).get("verified")) and
                                                  line["config1_768x512_gpu"]["verified"],
                                                  "see": "cpu_baseline.config1, config1_768x512_gpu"},
-                "2_1080p_dct_quant_idct_kernels": {"verified": line["roofline"]["verified"], "see": "roofline"},
+                "2_1080p_dct_quant_idct_kernels": {"verified": line["roofline"]["verified"] and
+                                                   line["roofline"]["yuv_planes_form"]["verified"], "see": "roofline"},
                 "3_1080p_decode_path": {"verified": line["decode_path"]["verified"], "see": "decode_path"},
                 "4_1080p_batch_encode": {"verified": line["verified"] and line["single_frame"]["verified"] and
                                          line["container_rgba"]["verified"],

@@ -61,6 +61,22 @@ DI int izz_of(int k) { return (int)((0xfea9db83c7426510ull >> (4 * k)) & 15); } 
 DI int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 DI int iabs(int v) { return v < 0 ? -v : v; }
 
+// rgb_to_y / the raw U and V sums of yuv.rs:859-896 on a pixel word 0x..BBGGRR
+// (U/V: the 2x2 sum of these + (512 << 16), then (s + 2^17) >> 18)
+__device__ __forceinline__ int pk_y(uint32_t p)
+{
+    return (16839 * (int)(p & 255u) + 33059 * (int)((p >> 8) & 255u) + 6420 * (int)((p >> 16) & 255u) + (1 << 15) +
+            (16 << 16)) >> 16;
+}
+__device__ __forceinline__ int pk_u(uint32_t p)
+{
+    return -9719 * (int)(p & 255u) - 19081 * (int)((p >> 8) & 255u) + 28800 * (int)((p >> 16) & 255u);
+}
+__device__ __forceinline__ int pk_v(uint32_t p)
+{
+    return 28800 * (int)(p & 255u) - 24116 * (int)((p >> 8) & 255u) - 4684 * (int)((p >> 16) & 255u);
+}
+
 // Intra-wave LDS hand-off: lanes of one wave exchange data through LDS.  A
 // wave's DS instructions execute in issue order, so a wavefront-scope fence
 // (compiler ordering only, no s_waitcnt on outstanding global stores) is all

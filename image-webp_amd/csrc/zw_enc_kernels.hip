@@ -127,19 +127,6 @@ __device__ __forceinline__ void rgb_run8(const uint8_t* __restrict__ row, uint32
         }
     }
 }
-__device__ __forceinline__ int pk_y(uint32_t p)
-{
-    return (16839 * (int)(p & 255u) + 33059 * (int)((p >> 8) & 255u) + 6420 * (int)((p >> 16) & 255u) + (1 << 15) +
-            (16 << 16)) >> 16;
-}
-__device__ __forceinline__ int pk_u(uint32_t p)
-{
-    return -9719 * (int)(p & 255u) - 19081 * (int)((p >> 8) & 255u) + 28800 * (int)((p >> 16) & 255u);
-}
-__device__ __forceinline__ int pk_v(uint32_t p)
-{
-    return 28800 * (int)(p & 255u) - 24116 * (int)((p >> 8) & 255u) - 4684 * (int)((p >> 16) & 255u);
-}
 
 template <int BPP>
 __global__ __launch_bounds__(256) void k_rgb2yuv_rows(const uint8_t* __restrict__ img, int w, int h, int mbw, int mbh,

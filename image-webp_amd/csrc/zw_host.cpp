@@ -40,10 +40,11 @@ hipError_t zwk_pack(hipStream_t s, const ZwMbOut* mbs, int nmb, int nframes, uin
                      unsigned long long* counter, unsigned long long* frame_info, uint8_t* out, int sizes_ready);
 hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size_t n, const ZwMatrix* m, int first,
                           void* levels, void* recon, int cus);
-hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, const uint8_t* recs,
-                        const void* segs, int mbw, int mbh, int nframes, int16_t* levels, uint8_t* RY, uint8_t* RU,
-                        uint8_t* RV, int variant);
+hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp, int w,
+                        int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw, int mbh, int nframes,
+                        int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, uint32_t* queue, int variant);
 size_t zwk_xform_mb_seg_bytes(void);
+size_t zwk_xform_mb_queue_bytes(int mbw, int mbh, int nframes);
 void zwk_xform_mb_pack_segs(const ZwMatrix* m, int n, void* out);
 hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const uint8_t* ctx0s, const ZwLevelCosts* lcost,
                             const uint8_t* probs, const void* args, int* levels, int* dq);
@@ -200,6 +201,9 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     c->dscratch = c->dscratch1 = nullptr;
+    if (c->xmb_mask) (void)hipFree(c->xmb_mask);
+    c->xmb_mask = nullptr;
+    c->xmb_mask_cap = 0;
     c->dscratch_cap = c->dscratch1_cap = 0;
     for (int i = 0; i < 4; i++) {
         if (c->hpin[i]) (void)hipHostFree(c->hpin[i]);
@@ -215,6 +219,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     zw_pipe_destroy(c->pipe1);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
+    if (c->xmb_mask) (void)hipFree(c->xmb_mask);
     for (hipEvent_t e : c->dev_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->dev_ev1)
@@ -1407,22 +1412,57 @@ static int xmb_variant()
     return e ? atoi(e) : 0;
 }
 
+// Both source forms: src_bpp 0 = Y/U/V planes (d_y, d_u, d_v), 3 / 4 = RGB / RGBA
+// pixels at d_y (frame stride img_stride, image w x h).
+static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint32_t mbh, int src_bpp, uint32_t w,
+                      uint32_t h, size_t img_stride, const void* d_y, const void* d_u, const void* d_v,
+                      const void* d_recs, const void* d_segs, void* d_levels, void* d_ry, void* d_ru, void* d_rv)
+{
+    if (!ctx || nframes < 0 || mbw == 0 || mbh == 0 || mbw > 1024 || mbh > 1024) return ZW_EINVAL;
+    if (nframes == 0) return ZW_OK;
+    if (!d_y || (src_bpp == 0 && (!d_u || !d_v)) || !d_recs || !d_segs || !d_levels || !d_ry || !d_ru || !d_rv)
+        return ZW_EINVAL;
+    // 16-byte loads and stores: records, planes and levels must be 16-byte aligned (chroma rows 8)
+    const uintptr_t a16 = (uintptr_t)d_recs | (uintptr_t)d_levels | (uintptr_t)d_ry | (src_bpp ? 0 : (uintptr_t)d_y);
+    const uintptr_t a8 = (uintptr_t)d_ru | (uintptr_t)d_rv | (src_bpp ? 0 : ((uintptr_t)d_u | (uintptr_t)d_v));
+    if ((a16 & 15) || (a8 & 7)) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    // the I4 queue k_xform_mb fills and k_xform_mb_i4 drains (grow-only; its
+    // counters are zeroed once here and every launch leaves them zero; a regrow
+    // frees the old buffer, which hipFree orders after queued work)
+    const size_t qb = zwk_xform_mb_queue_bytes((int)mbw, (int)mbh, nframes);
+    if (ctx->xmb_mask_cap < qb) {
+        if (ctx->xmb_mask) (void)hipFree(ctx->xmb_mask);
+        ctx->xmb_mask = nullptr;
+        ctx->xmb_mask_cap = 0;
+        if (hipMalloc(&ctx->xmb_mask, qb) != hipSuccess) return ZW_ENOMEM;
+        if (hipMemset(ctx->xmb_mask, 0, 256) != hipSuccess) return ZW_EDEVICE;
+        ctx->xmb_mask_cap = qb;
+    }
+    HIPOK(zwk_xform_mb(stream ? (hipStream_t)stream : ctx_stream(ctx), (const uint8_t*)d_y, (const uint8_t*)d_u,
+                       (const uint8_t*)d_v, src_bpp, (int)w, (int)h, img_stride, (const uint8_t*)d_recs, d_segs,
+                       (int)mbw, (int)mbh, nframes, (int16_t*)d_levels, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv,
+                       (uint32_t*)ctx->xmb_mask, xmb_variant()));
+    return ZW_OK;
+}
+
 extern "C" int zw_transform_quant_mbs_device(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint32_t mbh,
                                              const void* d_y, const void* d_u, const void* d_v, const void* d_recs,
                                              const void* d_segs, void* d_levels, void* d_ry, void* d_ru, void* d_rv)
 {
-    if (!ctx || nframes < 0 || mbw == 0 || mbh == 0 || mbw > 1024 || mbh > 1024) return ZW_EINVAL;
-    if (nframes == 0) return ZW_OK;
-    if (!d_y || !d_u || !d_v || !d_recs || !d_segs || !d_levels || !d_ry || !d_ru || !d_rv) return ZW_EINVAL;
-    // 16-byte loads and stores: records, planes and levels must be 16-byte aligned (chroma rows 8)
-    const uintptr_t a16 = (uintptr_t)d_y | (uintptr_t)d_recs | (uintptr_t)d_levels | (uintptr_t)d_ry;
-    const uintptr_t a8 = (uintptr_t)d_u | (uintptr_t)d_v | (uintptr_t)d_ru | (uintptr_t)d_rv;
-    if ((a16 & 15) || (a8 & 7)) return ZW_EINVAL;
-    HIPOK(hipSetDevice(ctx->device));
-    HIPOK(zwk_xform_mb(stream ? (hipStream_t)stream : ctx_stream(ctx), (const uint8_t*)d_y, (const uint8_t*)d_u,
-                       (const uint8_t*)d_v, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes,
-                       (int16_t*)d_levels, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, xmb_variant()));
-    return ZW_OK;
+    return xmb_launch(ctx, stream, nframes, mbw, mbh, 0, 0, 0, 0, d_y, d_u, d_v, d_recs, d_segs, d_levels, d_ry, d_ru,
+                      d_rv);
+}
+
+extern "C" int zw_transform_quant_mbs_rgb_device(zw_ctx* ctx, void* stream, int nframes, uint32_t width,
+                                                 uint32_t height, int bpp, const void* d_img, size_t img_stride,
+                                                 const void* d_recs, const void* d_segs, void* d_levels, void* d_ry,
+                                                 void* d_ru, void* d_rv)
+{
+    if (bpp != 3 && bpp != 4) return ZW_EINVAL;
+    if (width == 0 || height == 0 || img_stride < (size_t)width * height * bpp) return ZW_EINVAL;
+    return xmb_launch(ctx, stream, nframes, (width + 15) / 16, (height + 15) / 16, bpp, width, height, img_stride,
+                      d_img, nullptr, nullptr, d_recs, d_segs, d_levels, d_ry, d_ru, d_rv);
 }
 
 extern "C" int zw_transform_quant_mbs(zw_ctx* ctx, int nframes, uint32_t mbw, uint32_t mbh, const uint8_t* y,
@@ -1453,6 +1493,42 @@ extern "C" int zw_transform_quant_mbs(zw_ctx* ctx, int nframes, uint32_t mbw, ui
     HIPOK(hipMemcpyAsync(d + o_s, segs.data(), sb, hipMemcpyHostToDevice, s));
     r = zw_transform_quant_mbs_device(ctx, s, nframes, mbw, mbh, d + o_y, d + o_u, d + o_v, d + o_r, d + o_s, d + o_l,
                                       d + o_ry, d + o_ru, d + o_rv);
+    if (r) return r;
+    HIPOK(hipMemcpyAsync(levels, d + o_l, lb, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(ry, d + o_ry, ysz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(ru, d + o_ru, csz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(rv, d + o_rv, csz, hipMemcpyDeviceToHost, s));
+    HIPOK(hipStreamSynchronize(s));
+    return ZW_OK;
+}
+
+extern "C" int zw_transform_quant_mbs_rgb(zw_ctx* ctx, int nframes, uint32_t width, uint32_t height, int bpp,
+                                          const uint8_t* img, const uint8_t* recs, const int32_t* seg_qi,
+                                          int16_t* levels, uint8_t* ry, uint8_t* ru, uint8_t* rv)
+{
+    if (!ctx || nframes < 0 || width == 0 || height == 0 || (bpp != 3 && bpp != 4)) return ZW_EINVAL;
+    const uint32_t mbw = (width + 15) / 16, mbh = (height + 15) / 16;
+    if (mbw > 1024 || mbh > 1024) return ZW_EINVAL;
+    if (nframes == 0) return ZW_OK;
+    if (!img || !recs || !seg_qi || !levels || !ry || !ru || !rv) return ZW_EINVAL;
+    HIPOK(hipSetDevice(ctx->device));
+    const size_t F = (size_t)nframes, nmb = (size_t)mbw * mbh, fsz = (size_t)width * height * bpp;
+    const size_t isz = fsz * F, ysz = nmb * 256 * F, csz = nmb * 64 * F, rb = nmb * ZW_XMB_RECORD_BYTES * F;
+    const size_t lb = nmb * 800 * F, sb = zw_xmb_seg_table_bytes(nframes);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_i = 0, o_r = al(isz), o_s = o_r + al(rb), o_l = o_s + al(sb), o_ry = o_l + al(lb),
+                 o_ru = o_ry + al(ysz), o_rv = o_ru + al(csz), total = o_rv + al(csz);
+    std::vector<uint8_t> segs(sb);
+    int r = zw_xmb_seg_table(nframes, seg_qi, segs.data());
+    if (r) return r;
+    uint8_t* d = (uint8_t*)ctx_scratch(ctx, total);
+    if (!d) return ZW_ENOMEM;
+    hipStream_t s = ctx_stream(ctx);
+    HIPOK(hipMemcpyAsync(d + o_i, img, isz, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_r, recs, rb, hipMemcpyHostToDevice, s));
+    HIPOK(hipMemcpyAsync(d + o_s, segs.data(), sb, hipMemcpyHostToDevice, s));
+    r = zw_transform_quant_mbs_rgb_device(ctx, s, nframes, width, height, bpp, d + o_i, fsz, d + o_r, d + o_s,
+                                          d + o_l, d + o_ry, d + o_ru, d + o_rv);
     if (r) return r;
     HIPOK(hipMemcpyAsync(levels, d + o_l, lb, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(ry, d + o_ry, ysz, hipMemcpyDeviceToHost, s));

@@ -20,6 +20,8 @@ struct zw_ctx {
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
     void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
+    void* xmb_mask = nullptr;   // zw_transform_quant_mbs_device: the I4 queue of k_xform_mb / k_xform_mb_i4
+    size_t xmb_mask_cap = 0;
     size_t dscratch1_cap = 0;
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
     // D2H runs as a blit kernel, which cannot be dispatched while an encode

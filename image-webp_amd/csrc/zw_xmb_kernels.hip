@@ -46,15 +46,32 @@ struct XmbSeg {
 };
 
 #define XMB_MBS 8  // MBs per wave
-#define XMB_WAVES 4
+#ifndef XMB_WAVES
+#define XMB_WAVES 2  // waves per workgroup (LDS: 10.6 KB per wave)
+#endif
 
+#define XMB_LEVW 200  // words of levels per MB (25 x 16 i16)
 struct XmbLds {
-    uint32_t rec[XMB_MBS][24];   // the 8 records
-    uint32_t yt[16][32];         // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction)
-    uint32_t ct[2][8][16];       // U, V tiles: 8 rows x 8 MBs x 8 B
-    uint8_t ws[4][17 * ZW_BPS + 4];  // I4 work buffers (origin at byte 3: row pixels dword aligned)
-    uint8_t vv[64][40];          // per-lane I4 value vectors (dec_i4_values layout)
-    XmbSeg seg[4];               // the frame's four segment matrices (per-lane segment reads hit LDS, not HBM)
+    uint32_t rec[XMB_MBS][24];      // the 8 records
+    uint32_t yt[16][32];            // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction)
+    uint32_t ct[2][8][16];          // U, V tiles: 8 rows x 8 MBs x 8 B
+    uint32_t lev[XMB_MBS][XMB_LEVW];  // the group's levels, laid out as in HBM (one contiguous store run)
+    XmbSeg seg[4];                  // the frame's four segment matrices (per-lane segment reads hit LDS, not HBM)
+};
+
+// k_xform_mb_i4: four I4 MBs per wave (lane = 16 slot + block).  Queue
+// layout (u32 words): [0] count (k_xform_mb appends), [1] workgroups done,
+// [64..] global MB indexes.  Zero counters on entry; k_xform_mb_i4's last
+// workgroup zeroes them for the next launch.
+#define XI4_COUNT 0
+#define XI4_DONE 1
+#define XI4_LIST 64
+struct XmbI4Lds {
+    uint32_t rec[4][24];              // the slots' records
+    uint32_t yt[4][16][4];            // per slot: source rows, then reconstruction rows
+    XmbMat y1[4];                     // per slot: its frame's / segment's Y1 matrix
+    uint8_t ws[4][17 * ZW_BPS + 4];   // work buffers (origin at byte 3: row pixels dword aligned)
+    uint8_t vv[64][40];               // per-lane value vectors (dec_i4_values layout)
 };
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
@@ -81,6 +98,15 @@ DI void recon_words(int* c, const uint32_t* pw, uint32_t* rw)
         for (int j = 0; j < 4; j++) w |= (uint32_t)clamp255(c[4 * i + j] + (int)byte_of(pw[i], j)) << (8 * j);
         rw[i] = w;
     }
+}
+// a block's 16 levels in zigzag order as 8 words of i16 pairs, into LDS
+DI void stage_levels(uint32_t* o, const int* lv)
+{
+    uint32_t lw[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) lw[q] = pack_lo(lv[kZZ(2 * q)], lv[kZZ(2 * q + 1)]);
+    *(v4u*)o = v4u{lw[0], lw[1], lw[2], lw[3]};
+    *(v4u*)(o + 4) = v4u{lw[4], lw[5], lw[6], lw[7]};
 }
 DI void store_levels(int16_t* out, const int* lv)
 {
@@ -134,18 +160,108 @@ DI int diffuse_err(int dc, const XmbMat& m)
 }
 DI int adj_dc(int dc, int te, int le) { return dc + ((7 * te + 8 * le) >> 3); }
 
-template <bool COPY>
-__global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
-                                                           const uint8_t* __restrict__ V, const uint8_t* __restrict__ recs,
-                                                           const XmbSeg* __restrict__ segs, int mbw, int mbh, int nframes,
-                                                           int16_t* __restrict__ levels, uint8_t* __restrict__ RY,
-                                                           uint8_t* __restrict__ RU, uint8_t* __restrict__ RV)
+#ifndef XMB_OCC
+#define XMB_OCC 0  // >0: waves per SIMD the main pass is compiled for (amdgpu_waves_per_eu)
+#endif
+#if XMB_OCC > 0
+#define XMB_ATTR __attribute__((amdgpu_waves_per_eu(XMB_OCC)))
+#else
+#define XMB_ATTR
+#endif
+
+// RGB(A) source (SRC = 3 / 4): convert_image_yuv (yuv.rs:656-804) of the
+// group's 16 x 128 luma pixels / 2 x 8 x 64 chroma samples straight into the
+// tiles, with the MB padding of the encoder's planes (edge replication: luma
+// pixel (x, y) is pixel (min(x, w-1), min(y, h-1)); chroma sample (cx, cy) is
+// the 2x2 average at (min(cx, cw-1), min(cy, ch-1)), its pixel pairs clamped
+// likewise).  Item = 8 pixels x 2 rows (4 chroma samples per plane).
+template <int BPP>
+DI uint32_t px_at(const uint8_t* img, int w, int x, int y)
+{
+    const uint8_t* p = img + ((size_t)y * w + x) * BPP;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+}
+template <int BPP>
+DI void rgb_item(const uint8_t* __restrict__ img, int w, int h, bool runs, int px0, int cy, uint32_t ya[2],
+                 uint32_t yb[2], uint32_t& uw, uint32_t& vw)
+{
+    uint32_t a[8], b[8], ca[8], cb[8];  // luma rows 2cy, 2cy+1; chroma rows
+    const int ch = (h + 1) / 2, cw = (w + 1) / 2;
+    if (runs && px0 + 8 <= w && 2 * cy + 1 < h) {
+        // interior: the two rows' 8-pixel runs, 16-byte (RGBA) / 8-byte (RGB) loads
+        const uint8_t* ra = img + ((size_t)(2 * cy) * w + px0) * BPP;
+        const uint8_t* rb = ra + (size_t)w * BPP;
+        if (BPP == 4) {
+            const v4u a0 = __builtin_nontemporal_load((const v4u*)ra), a1 = __builtin_nontemporal_load((const v4u*)ra + 1);
+            const v4u b0 = __builtin_nontemporal_load((const v4u*)rb), b1 = __builtin_nontemporal_load((const v4u*)rb + 1);
+            a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+            b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const uint8_t* row = r ? rb : ra;
+                const v2u x0 = __builtin_nontemporal_load((const v2u*)row), x1 = __builtin_nontemporal_load((const v2u*)(row + 8));
+                const v2u x2 = __builtin_nontemporal_load((const v2u*)(row + 16));
+                const uint32_t wd[6] = {x0.x, x0.y, x1.x, x1.y, x2.x, x2.y};
+                uint32_t* o = r ? b : a;
+#pragma unroll
+                for (int q = 0; q < 2; q++) {  // 4 pixels in 3 words
+                    const uint32_t w0 = wd[3 * q], w1 = wd[3 * q + 1], w2 = wd[3 * q + 2];
+                    o[4 * q] = w0;
+                    o[4 * q + 1] = __builtin_amdgcn_alignbyte(w1, w0, 3);
+                    o[4 * q + 2] = __builtin_amdgcn_alignbyte(w2, w1, 2);
+                    o[4 * q + 3] = w2 >> 8;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            ca[i] = a[i];
+            cb[i] = b[i];
+        }
+    } else {
+        // edges and padding: every pixel at its clamped coordinates
+        const int y0 = min(2 * cy, h - 1), y1 = min(2 * cy + 1, h - 1);
+        const int ccy = min(cy, ch - 1), cy0 = 2 * ccy, cy1 = min(2 * ccy + 1, h - 1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = min(px0 + i, w - 1);
+            a[i] = px_at<BPP>(img, w, x, y0);
+            b[i] = px_at<BPP>(img, w, x, y1);
+            const int ccx = min((px0 >> 1) + (i >> 1), cw - 1);
+            const int cxx = (i & 1) ? min(2 * ccx + 1, w - 1) : 2 * ccx;
+            ca[i] = px_at<BPP>(img, w, cxx, cy0);
+            cb[i] = px_at<BPP>(img, w, cxx, cy1);
+        }
+    }
+    ya[0] = ya[1] = yb[0] = yb[1] = uw = vw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        ya[i >> 2] |= (uint32_t)pk_y(a[i]) << (8 * (i & 3));
+        yb[i >> 2] |= (uint32_t)pk_y(b[i]) << (8 * (i & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int su = pk_u(ca[2 * j]) + pk_u(ca[2 * j + 1]) + pk_u(cb[2 * j]) + pk_u(cb[2 * j + 1]) + (512 << 16);
+        const int sv = pk_v(ca[2 * j]) + pk_v(ca[2 * j + 1]) + pk_v(cb[2 * j]) + pk_v(cb[2 * j + 1]) + (512 << 16);
+        uw |= (uint32_t)((su + (1 << 17)) >> 18) << (8 * j);
+        vw |= (uint32_t)((sv + (1 << 17)) >> 18) << (8 * j);
+    }
+}
+
+// SRC: 0 = Y/U/V planes (MB-padded), 3 / 4 = RGB / RGBA pixels at Y (frame f at
+// Y + f * img_stride; w, h the image size; runs: every 8-pixel run is aligned
+// for its 16-byte (RGBA) / 8-byte (RGB) loads, else all pixels go the per-pixel
+// way).  COPY: the calibration variant -- the same loads and stores, no arithmetic.
+template <int SRC, bool COPY>
+__global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
+    const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U, const uint8_t* __restrict__ V, int w, int h,
+    size_t img_stride, bool runs, const uint8_t* __restrict__ recs, const XmbSeg* __restrict__ segs, int mbw, int mbh, int nframes,
+    int16_t* __restrict__ levels, uint8_t* __restrict__ RY, uint8_t* __restrict__ RU, uint8_t* __restrict__ RV,
+    uint32_t* __restrict__ i4q)
 {
     __shared__ XmbLds lds[XMB_WAVES];
-    __shared__ uint8_t i4idx[10][16];  // d_I4_IDX
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (!COPY && threadIdx.x < 40) ((uint32_t*)i4idx)[threadIdx.x] = ((const uint32_t*)d_I4_IDX)[threadIdx.x];
-    __syncthreads();
     XmbLds& L = lds[wv];
     const int ngx = (mbw + XMB_MBS - 1) / XMB_MBS;
     const long long id = (long long)blockIdx.x * XMB_WAVES + wv;
@@ -158,79 +274,91 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
     const size_t ys = (size_t)mbw * 16, cs = (size_t)mbw * 8;
     const size_t ysz = ys * mbh * 16, csz = cs * mbh * 8;
     const size_t mb0 = (size_t)f * nmb + (size_t)mby * mbw + x0;  // first MB of the group
-    const uint8_t* Yf = Y + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
-    const uint8_t* Uf = U + f * csz + (size_t)mby * 8 * cs + x0 * 8;
-    const uint8_t* Vf = V + f * csz + (size_t)mby * 8 * cs + x0 * 8;
+    // chroma 16-byte pieces: plane cp, row cr, piece cq (MBs 2cq, 2cq+1)
+    const int cp = lane >> 5, cr = (lane >> 2) & 7, cq = lane & 3;
+    const int cn = min(max(nact - 2 * cq, 0), 2);  // MBs of the piece inside the group
 
-    // ---- stage: records (48 lanes x 16 B), luma rows (2 x 16 B), chroma rows (2 x 8 B)
+    // ---- stage: records (48 lanes x 16 B), the source tiles, the segment table
     {
         const int rm = lane / 6, rq = lane % 6;
         v4u r4 = {0u, 0u, 0u, 0u};
         if (lane < 48 && rm < nact) r4 = __builtin_nontemporal_load((const v4u*)(recs + (mb0 + rm) * 96) + rq);
-        const int yc = lane & 7, yr = lane >> 3;
-        v4u y0 = {0u, 0u, 0u, 0u}, y1 = y0;
-        if (yc < nact) {
-            y0 = __builtin_nontemporal_load((const v4u*)(Yf + yr * ys + yc * 16));
-            y1 = __builtin_nontemporal_load((const v4u*)(Yf + (yr + 8) * ys + yc * 16));
-        }
-        // chroma: 128 8-byte pieces (plane, row, MB), two per lane
-        v2u c0 = {0u, 0u}, c1 = c0;
-        const int cm = lane & 7, cr = (lane >> 3) & 7;
-        if (cm < nact) {
-            c0 = __builtin_nontemporal_load((const v2u*)(Uf + cr * cs + cm * 8));
-            c1 = __builtin_nontemporal_load((const v2u*)(Vf + cr * cs + cm * 8));
-        }
-        // the frame's segment table: 4 x 96 B = 24 lines of 16 B
         v4u s4 = {0u, 0u, 0u, 0u};
         if (!COPY && lane >= 40) s4 = *((const v4u*)(segs + (size_t)f * 4) + (lane - 40));
+        if (SRC == 0) {
+            const uint8_t* Yf = Y + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
+            const int yc = lane & 7, yr = lane >> 3;
+            v4u y0 = {0u, 0u, 0u, 0u}, y1 = y0;
+            if (yc < nact) {
+                y0 = __builtin_nontemporal_load((const v4u*)(Yf + yr * ys + yc * 16));
+                y1 = __builtin_nontemporal_load((const v4u*)(Yf + (yr + 8) * ys + yc * 16));
+            }
+            const uint8_t* Cf = (cp ? V : U) + f * csz + (size_t)(mby * 8 + cr) * cs + (x0 + 2 * cq) * 8;
+            v4u c4 = {0u, 0u, 0u, 0u};
+            if (cn == 2) c4 = __builtin_nontemporal_load((const v4u*)Cf);
+            else if (cn == 1) {
+                const v2u c2 = __builtin_nontemporal_load((const v2u*)Cf);
+                c4.x = c2.x;
+                c4.y = c2.y;
+            }
+            *(v4u*)&L.yt[yr][4 * yc] = y0;
+            *(v4u*)&L.yt[yr + 8][4 * yc] = y1;
+            *(v4u*)&L.ct[cp][cr][4 * cq] = c4;
+        } else {
+            const uint8_t* img = Y + (size_t)f * img_stride;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int item = lane + 64 * k, pr = item >> 4, xr = item & 15;
+                if ((xr >> 1) < nact) {
+                    uint32_t ya[2], yb[2], uw, vw;
+                    rgb_item<SRC>(img, w, h, runs, (x0 + (xr >> 1)) * 16 + 8 * (xr & 1), mby * 8 + pr, ya, yb, uw, vw);
+                    *(v2u*)&L.yt[2 * pr][2 * xr] = v2u{ya[0], ya[1]};
+                    *(v2u*)&L.yt[2 * pr + 1][2 * xr] = v2u{yb[0], yb[1]};
+                    L.ct[0][pr][xr] = uw;
+                    L.ct[1][pr][xr] = vw;
+                }
+            }
+        }
         if (lane < 48) *(v4u*)&L.rec[rm][4 * rq] = r4;
         if (!COPY && lane >= 40) *((v4u*)L.seg + (lane - 40)) = s4;
-        *(v4u*)&L.yt[yr][4 * yc] = y0;
-        *(v4u*)&L.yt[yr + 8][4 * yc] = y1;
-        *(v2u*)&L.ct[0][cr][2 * cm] = c0;
-        *(v2u*)&L.ct[1][cr][2 * cm] = c1;
         wsync();
     }
     const XmbSeg* S = L.seg;
 
     if (COPY) {
-        // calibration: the same loads and stores, no arithmetic
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int m = 4 * h + (lane >> 4), blk = lane & 15;
-            if (m < nact) {
-                int lv[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) lv[k] = (int)L.rec[m][k] + blk;
-                store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
-                if (blk < 8) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + 2 * blk) = L.rec[m][blk];
-            }
-        }
-        {
-            const int m = lane >> 3, b = lane & 7;
-            if (m < nact) {
-                int lv[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) lv[k] = (int)L.rec[m][k + 8] + b;
-                store_levels(levels + ((mb0 + m) * 25 + 17 + b) * 16, lv);
-            }
-        }
+        // calibration: levels staged from the records, no arithmetic
+        for (int i = lane; i < XMB_MBS * XMB_LEVW; i += 64) (&L.lev[0][0])[i] = (&L.rec[0][0])[i % (XMB_MBS * 24)];
+        wsync();
     } else {
-        // ---- luma: MBs 0-3, then 4-7; lane = 16*mb + block
+        // the group's I4 MBs go on k_xform_mb_i4's queue (their luma is left to it)
+        {
+            const bool i4 = lane < nact && (L.rec[lane & 7][0] & 255u) == 4u;
+            const unsigned long long b = __ballot(i4);
+            if (b) {
+                uint32_t base = 0;
+                if (lane == 0)
+                    base = __hip_atomic_fetch_add(&i4q[XI4_COUNT], (uint32_t)__popcll(b), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                base = (uint32_t)__shfl((int)base, 0);
+                const int rank = __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u);
+                if (i4) i4q[XI4_LIST + base + rank] = (uint32_t)(mb0 + lane);
+            }
+        }
+        // ---- luma of the I16 MBs: MBs 0-3, then 4-7; lane = 16*mb + block
         const int blk = lane & 15, bx = blk & 3, by = blk >> 2;
 #pragma unroll 1
-        for (int h = 0; h < 2; h++) {
-            const int m = 4 * h + (lane >> 4);
+        for (int hh = 0; hh < 2; hh++) {
+            const int m = 4 * hh + (lane >> 4);
             const uint32_t* R = L.rec[m];
             const int mode = (int)(R[0] & 255u);
             const int seg = (int)((R[0] >> 16) & 3u);
             const int has_top = (int)((R[0] >> 24) & 1u), has_left = (int)((R[0] >> 25) & 1u);
             const XmbMat& my1 = S[seg].y1;
-            uint32_t sw[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) sw[r] = L.yt[by * 4 + r][m * 4 + bx];
             int y2l = 0;
             if (mode != 4) {
+                uint32_t sw[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) sw[r] = L.yt[by * 4 + r][m * 4 + bx];
                 // I16 (transform_luma_block): prediction of this lane's 4x4 from the record's edges
                 const uint8_t* Rb = (const uint8_t*)R;
                 const uint32_t T = R[6 + bx];
@@ -254,102 +382,17 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
                     c[k] = lv[k] * my1.q[1];
                 }
                 c[0] = dcv;
-                if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
+                stage_levels(&L.lev[m][8 * blk], lv);
                 uint32_t rw[4];
                 recon_words(c, pw, rw);
 #pragma unroll
                 for (int r = 0; r < 4; r++) L.yt[by * 4 + r][m * 4 + bx] = rw[r];
             }
-            // I4 MBs of this half (transform_luma_blocks_4x4): x+2y anti-diagonals
-            const bool any_i4 = __builtin_amdgcn_ballot_w64(mode == 4) != 0;
-            if (any_i4) {
-                uint8_t* ws = L.ws[m & 3] + 3;
-                if (mode == 4) {
-                    // create_border_luma from the record: corner, top 16 + top-right 4, left 16,
-                    // the top-right 4 copied to rows 4, 8, 12
-                    if (blk < 5) *(uint32_t*)(ws + 1 + 4 * blk) = R[6 + blk];
-                    if (blk == 5) ws[0] = (uint8_t)(R[5] & 255u);
-                    if (blk >= 6 && blk < 9) *(uint32_t*)(ws + 4 * (blk - 5) * ZW_BPS + 17) = R[10];
-                    ws[(blk + 1) * ZW_BPS] = ((const uint8_t*)R)[44 + blk];
-                }
-                wsync();
-                const int sm = (int)((R[1 + (blk >> 3)] >> (4 * (blk & 7))) & 15u);  // bpred[blk]
-                const int xo = bx * 4 + 1, yo = by * 4 + 1;
-                uint8_t* vv = L.vv[lane];
-#pragma unroll 1
-                for (int t = 0; t < 10; t++) {
-                    if (mode == 4 && bx + 2 * by == t) {
-                        // the 39-value vector of this sub-block's edges (k_dec_recon's dec_i4_values)
-                        int E[13];
-#pragma unroll
-                        for (int k = 0; k < 4; k++) E[k] = ws[(yo + 3 - k) * ZW_BPS + xo - 1];
-                        E[4] = ws[(yo - 1) * ZW_BPS + xo - 1];
-#pragma unroll
-                        for (int k = 5; k < 13; k++) E[k] = ws[(yo - 1) * ZW_BPS + xo + (k - 5)];
-                        uint32_t vw[10];
-#pragma unroll
-                        for (int q = 0; q < 10; q++) {
-                            uint32_t w = 0;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const int i = 4 * q + j;
-                                int v;
-                                if (i < 13) v = E[i];
-                                else if (i < 24) v = (E[i - 13] + 2 * E[i - 12] + E[i - 11] + 2) >> 2;
-                                else if (i < 36) v = (E[i - 24] + E[i - 23] + 1) >> 1;
-                                else if (i == 36) v = (E[11] + 3 * E[12] + 2) >> 2;
-                                else if (i == 37) v = (E[1] + 3 * E[0] + 2) >> 2;
-                                else if (i == 38) v = (4 + E[0] + E[1] + E[2] + E[3] + E[5] + E[6] + E[7] + E[8]) >> 3;
-                                else v = 0;
-                                w |= (uint32_t)v << (8 * j);
-                            }
-                            vw[q] = w;
-                        }
-#pragma unroll
-                        for (int q = 0; q < 10; q++) *(uint32_t*)(vv + 4 * q) = vw[q];
-                        uint32_t pw[4];
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            uint32_t w = 0;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const int idx = i4idx[sm][4 * r + j];
-                                int v;
-                                if (idx == 254) v = clamp255(E[3 - r] + E[5 + j] - E[4]);
-                                else v = vv[idx == 255 ? 38 : idx];
-                                w |= (uint32_t)v << (8 * j);
-                            }
-                            pw[r] = w;
-                        }
-                        uint32_t s4[4];
-#pragma unroll
-                        for (int r = 0; r < 4; r++) s4[r] = sw[r];
-                        int c[16], lv[16];
-                        fdct_words(s4, pw, c);
-#pragma unroll
-                        for (int k = 0; k < 16; k++) {
-                            const int tk = k > 0;
-                            lv[k] = qz(c[k], my1, tk);
-                            c[k] = lv[k] * my1.q[tk];
-                        }
-                        if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
-                        uint32_t rw[4];
-                        recon_words(c, pw, rw);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            *(uint32_t*)(ws + (yo + r) * ZW_BPS + xo) = rw[r];
-                            L.yt[by * 4 + r][m * 4 + bx] = rw[r];
-                        }
-                    }
-                    wsync();
-                }
-            }
-            // Y2 levels in zigzag order (zeros for I4 MBs): eight 4-byte stores per MB
+            // Y2 levels in zigzag order (zeros for I4 MBs)
             const int zsrc = (lane & ~15) | kZZ(blk);
             const int zv = __shfl(y2l, zsrc);
             const int zn = __shfl_down(zv, 1);
-            if ((blk & 1) == 0 && m < nact)
-                *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
+            if ((blk & 1) == 0) L.lev[m][128 + (blk >> 1)] = pack_lo(zv, zn);
         }
 
         // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB)
@@ -389,7 +432,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
                 lv[k] = qz(c[k], muv, tk);
                 c[k] = lv[k] * muv.q[tk];
             }
-            if (m < nact) store_levels(levels + ((mb0 + m) * 25 + 17 + 4 * plane + sub) * 16, lv);
+            stage_levels(&L.lev[m][136 + 8 * (4 * plane + sub)], lv);
             uint32_t rw[4];
             recon_words(c, pw, rw);
 #pragma unroll
@@ -398,25 +441,181 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb(const uint8_t* __re
         wsync();
     }
 
-    // ---- reconstruction tiles back to the planes
+    // ---- out: the group's levels as one contiguous run (nact x 800 B, 16 B a
+    // lane), the reconstruction tiles row-coalesced (an I4 MB's luma tile still
+    // holds its source: k_xform_mb_i4, next on the stream, reads it there and
+    // overwrites it with the reconstruction)
     {
+        const int nch = nact * (XMB_LEVW / 4);
+        v4u* lo = (v4u*)(levels + mb0 * 400);
+#pragma unroll
+        for (int k = 0; k < (XMB_MBS * XMB_LEVW / 4 + 63) / 64; k++) {
+            const int c = 64 * k + lane;
+            if (c < nch) __builtin_nontemporal_store(*((const v4u*)&L.lev[0][0] + c), lo + c);
+        }
         uint8_t* RYf = RY + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
-        uint8_t* RUf = RU + f * csz + (size_t)mby * 8 * cs + x0 * 8;
-        uint8_t* RVf = RV + f * csz + (size_t)mby * 8 * cs + x0 * 8;
         const int yc = lane & 7, yr = lane >> 3;
-        const int cm = lane & 7, cr = (lane >> 3) & 7;
         if (yc < nact) {
             __builtin_nontemporal_store(*(const v4u*)&L.yt[yr][4 * yc], (v4u*)(RYf + yr * ys + yc * 16));
             __builtin_nontemporal_store(*(const v4u*)&L.yt[yr + 8][4 * yc], (v4u*)(RYf + (yr + 8) * ys + yc * 16));
         }
-        if (cm < nact) {
-            __builtin_nontemporal_store(*(const v2u*)&L.ct[0][cr][2 * cm], (v2u*)(RUf + cr * cs + cm * 8));
-            __builtin_nontemporal_store(*(const v2u*)&L.ct[1][cr][2 * cm], (v2u*)(RVf + cr * cs + cm * 8));
+        uint8_t* Cf = (cp ? RV : RU) + f * csz + (size_t)(mby * 8 + cr) * cs + (x0 + 2 * cq) * 8;
+        const v4u c4 = *(const v4u*)&L.ct[cp][cr][4 * cq];
+        if (cn == 2) __builtin_nontemporal_store(c4, (v4u*)Cf);
+        else if (cn == 1) __builtin_nontemporal_store(v2u{c4.x, c4.y}, (v2u*)Cf);
+    }
+}
+
+// The I4 MBs' luma (transform_luma_blocks_4x4, vp8.rs:2785-2916), after
+// k_xform_mb: the queue it filled runs four MBs per wave at a time, lane = 16
+// slot + block, the 16 sub-blocks along the x+2y anti-diagonals (10 steps) in
+// an LDS work buffer with the reference's 32-byte stride.  I4 MBs are rare
+// (2-20 % at Q75 m4) and cluster in textured regions, so a queue balances them
+// over the whole grid and the main pass never waits on their serial chains.
+__global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* __restrict__ recs,
+                                                              const XmbSeg* __restrict__ segs, int mbw, int mbh,
+                                                              int nframes, int16_t* __restrict__ levels,
+                                                              uint8_t* __restrict__ RY, uint32_t* __restrict__ i4q)
+{
+    __shared__ XmbI4Lds lds[XMB_WAVES];
+    __shared__ uint8_t i4idx[10][16];  // d_I4_IDX
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < 40) ((uint32_t*)i4idx)[threadIdx.x] = ((const uint32_t*)d_I4_IDX)[threadIdx.x];
+    __syncthreads();
+    XmbI4Lds& L = lds[wv];
+    const int nmb = mbw * mbh;
+    const uint32_t cap = (uint32_t)((long long)nframes * nmb);
+    const uint32_t n = min(__hip_atomic_load(&i4q[XI4_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), cap);
+    const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
+    const int slot = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
+    const uint32_t nbatch = (n + 3) / 4, nwaves = gridDim.x * XMB_WAVES;
+#pragma unroll 1
+    for (uint32_t bt = blockIdx.x * XMB_WAVES + wv; bt < nbatch; bt += nwaves) {
+        const uint32_t k = 4 * bt;
+        {
+            const bool valid = k + slot < n;
+            const size_t gm = i4q[XI4_LIST + (valid ? k + slot : k)];
+            const int f = (int)(gm / nmb), r = (int)(gm % nmb), mby = r / mbw, x = r % mbw;
+            // k_xform_mb left the MB's source luma in its reconstruction tile
+            uint8_t* yrow = RY + f * ysz + (size_t)(mby * 16 + blk) * ys + (size_t)x * 16;
+            // stage: record (lanes 0-5 of the slot), source row `blk` of the slot's MB, Y1 matrix
+            {
+                v4u r4 = {0u, 0u, 0u, 0u};
+                if (blk < 6) r4 = *((const v4u*)(recs + gm * 96) + blk);
+                const v4u y4 = *(const v4u*)yrow;
+                if (blk < 6) *(v4u*)&L.rec[slot][4 * blk] = r4;
+                *(v4u*)&L.yt[slot][blk][0] = y4;
+                wsync();
+                const int seg = (int)((L.rec[slot][0] >> 16) & 3u);
+                if (blk < 2) {
+                    const v4u m4 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1 + blk);
+                    *((v4u*)&L.y1[slot] + blk) = m4;
+                }
+            }
+            const uint32_t* R = L.rec[slot];
+            uint8_t* ws = L.ws[slot] + 3;
+            // create_border_luma from the record: corner, top 16 + top-right 4, left 16,
+            // the top-right 4 copied to rows 4, 8, 12
+            if (blk < 5) *(uint32_t*)(ws + 1 + 4 * blk) = R[6 + blk];
+            if (blk == 5) ws[0] = (uint8_t)(R[5] & 255u);
+            if (blk >= 6 && blk < 9) *(uint32_t*)(ws + 4 * (blk - 5) * ZW_BPS + 17) = R[10];
+            ws[(blk + 1) * ZW_BPS] = ((const uint8_t*)R)[44 + blk];
+            wsync();
+            const XmbMat& my1 = L.y1[slot];
+            const int sm = (int)((R[1 + (blk >> 3)] >> (4 * (blk & 7))) & 15u);  // bpred[blk]
+            const int xo = bx * 4 + 1, yo = by * 4 + 1;
+            uint8_t* vv = L.vv[lane];
+            int16_t* lvl = levels + (gm * 25 + blk) * 16;
+#pragma unroll 1
+            for (int t = 0; t < 10; t++) {
+                if (valid && bx + 2 * by == t) {
+                    // the 39-value vector of this sub-block's edges (k_dec_recon's dec_i4_values)
+                    int E[13];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) E[j] = ws[(yo + 3 - j) * ZW_BPS + xo - 1];
+                    E[4] = ws[(yo - 1) * ZW_BPS + xo - 1];
+#pragma unroll
+                    for (int j = 5; j < 13; j++) E[j] = ws[(yo - 1) * ZW_BPS + xo + (j - 5)];
+                    uint32_t vw[10];
+#pragma unroll
+                    for (int q = 0; q < 10; q++) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int i = 4 * q + j;
+                            int v;
+                            if (i < 13) v = E[i];
+                            else if (i < 24) v = (E[i - 13] + 2 * E[i - 12] + E[i - 11] + 2) >> 2;
+                            else if (i < 36) v = (E[i - 24] + E[i - 23] + 1) >> 1;
+                            else if (i == 36) v = (E[11] + 3 * E[12] + 2) >> 2;
+                            else if (i == 37) v = (E[1] + 3 * E[0] + 2) >> 2;
+                            else if (i == 38) v = (4 + E[0] + E[1] + E[2] + E[3] + E[5] + E[6] + E[7] + E[8]) >> 3;
+                            else v = 0;
+                            w |= (uint32_t)v << (8 * j);
+                        }
+                        vw[q] = w;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 10; q++) *(uint32_t*)(vv + 4 * q) = vw[q];
+                    uint32_t pw[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int idx = i4idx[sm][4 * r + j];
+                            int v;
+                            if (idx == 254) v = clamp255(E[3 - r] + E[5 + j] - E[4]);
+                            else v = vv[idx == 255 ? 38 : idx];
+                            w |= (uint32_t)v << (8 * j);
+                        }
+                        pw[r] = w;
+                    }
+                    uint32_t s4[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) s4[r] = L.yt[slot][by * 4 + r][bx];
+                    int cf[16], lv[16];
+                    fdct_words(s4, pw, cf);
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const int tk = j > 0;
+                        lv[j] = qz(cf[j], my1, tk);
+                        cf[j] = lv[j] * my1.q[tk];
+                    }
+                    store_levels(lvl, lv);
+                    uint32_t rw[4];
+                    recon_words(cf, pw, rw);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        *(uint32_t*)(ws + (yo + r) * ZW_BPS + xo) = rw[r];
+                        L.yt[slot][by * 4 + r][bx] = rw[r];
+                    }
+                }
+                wsync();
+            }
+            // the reconstruction rows back to the plane (row blk of the slot's MB)
+            if (valid) __builtin_nontemporal_store(*(const v4u*)&L.yt[slot][blk][0], (v4u*)yrow);
+            wsync();
+        }
+    }
+    // the last workgroup out zeroes the queue counters for the next launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t d = __hip_atomic_fetch_add(&i4q[XI4_DONE], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == gridDim.x - 1) {
+            __hip_atomic_store(&i4q[XI4_COUNT], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&i4q[XI4_DONE], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
 
 extern "C" size_t zwk_xform_mb_seg_bytes(void) { return sizeof(XmbSeg) * 4; }
+// Bytes of the I4 queue (k_xform_mb appends, k_xform_mb_i4 drains); its
+// first 8 bytes must be zero before the first launch.
+extern "C" size_t zwk_xform_mb_queue_bytes(int mbw, int mbh, int nframes)
+{
+    return 4 * (XI4_LIST + (size_t)nframes * mbw * mbh);
+}
 
 // segs: per frame 4 x (y1, y2, uv) as {q_dc, q_ac, iq_dc, iq_ac, bias_dc, bias_ac} host-built ZwMatrix
 // triples, converted here into the branch-free quantiser form.  variant 99: copy calibration.
@@ -437,19 +636,41 @@ extern "C" void zwk_xform_mb_pack_segs(const ZwMatrix* m /* [n][4][3] */, int n,
     }
 }
 
-extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V,
-                                   const uint8_t* recs, const void* segs, int mbw, int mbh, int nframes,
-                                   int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, int variant)
+// queue: zwk_xform_mb_queue_bytes of device memory whose two counters are zero
+// (as every launch leaves them).  src_bpp: 0 = Y/U/V planes; 3 / 4 = RGB / RGBA
+// pixels at Y (frame stride img_stride, image w x h).
+extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp,
+                                   int w, int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw,
+                                   int mbh, int nframes, int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV,
+                                   uint32_t* queue, int variant)
 {
     const long long waves = (long long)nframes * mbh * ((mbw + XMB_MBS - 1) / XMB_MBS);
     const unsigned grid = (unsigned)((waves + XMB_WAVES - 1) / XMB_WAVES);
     if (grid == 0) return hipSuccess;
+    if (src_bpp != 0 && src_bpp != 3 && src_bpp != 4) return hipErrorInvalidValue;
     const XmbSeg* sg = (const XmbSeg*)segs;
-    if (variant == 99)
-        hipLaunchKernelGGL((k_xform_mb<true>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, recs, sg, mbw, mbh,
-                           nframes, levels, RY, RU, RV);
-    else
-        hipLaunchKernelGGL((k_xform_mb<false>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, recs, sg, mbw, mbh,
-                           nframes, levels, RY, RU, RV);
+    const bool copy = variant == 99;
+    const int ra = src_bpp == 4 ? 16 : 8;
+    const bool runs = src_bpp != 0 && (uintptr_t)Y % ra == 0 && img_stride % ra == 0 && ((size_t)w * src_bpp) % ra == 0;
+#define XMB_LAUNCH(SRC, CP)                                                                                         \
+    hipLaunchKernelGGL((k_xform_mb<SRC, CP>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, w, h, img_stride, runs,  \
+                       recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue)
+    if (src_bpp == 0) {
+        if (copy) XMB_LAUNCH(0, true);
+        else XMB_LAUNCH(0, false);
+    } else if (src_bpp == 3) {
+        if (copy) XMB_LAUNCH(3, true);
+        else XMB_LAUNCH(3, false);
+    } else {
+        if (copy) XMB_LAUNCH(4, true);
+        else XMB_LAUNCH(4, false);
+    }
+#undef XMB_LAUNCH
+    if (copy) return hipGetLastError();
+    // the I4 queue: one workgroup per 256 MBs of the launch, at most 1024
+    const long long nmbs = (long long)nframes * mbw * mbh;
+    const unsigned g4 = (unsigned)min((nmbs + 255) / 256, 1024LL);
+    hipLaunchKernelGGL(k_xform_mb_i4, dim3(g4), dim3(64 * XMB_WAVES), 0, s, recs, sg, mbw, mbh, nframes, levels, RY,
+                       queue);
     return hipGetLastError();
 }

@@ -153,6 +153,8 @@ SIGNATURES = [
     ("zw_xmb_seg_table_bytes", _SZ, [_I]),
     ("zw_xmb_seg_table", _I, [_I, _VP, _VP]),
     ("zw_transform_quant_mbs_device", _I, [_VP, _VP, _I, _U32, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("zw_transform_quant_mbs_rgb", _I, [_VP, _I, _U32, _U32, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("zw_transform_quant_mbs_rgb_device", _I, [_VP, _VP, _I, _U32, _U32, _I, _VP, _SZ, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("zw_quant_blocks", _I, [_VP, _I, _VP, _VP, _I, _I, _I, _U32, _I, _I, _I, _VP, _VP, _VP]),
     ("zw_loop_filter_frame", _I, [_VP, _VP, _VP, _VP, _U32, _U32, _VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I]),
     ("zw_pipe_create", _I, [_VP, _I, _U32, _U32, _I, _U8, _U8, ctypes.POINTER(_VP)]),
@@ -747,6 +749,38 @@ def transform_quant_mbs_device(nframes, mbw, mbh, d_y, d_u, d_v, d_recs, d_segs,
     c = _ctx(ctx)
     _check(c._lib.zw_transform_quant_mbs_device(c.handle, stream, nframes, mbw, mbh, d_y, d_u, d_v, d_recs, d_segs,
                                                 d_levels, d_ry, d_ru, d_rv), "transform_quant_mbs_device")
+
+
+def transform_quant_mbs_rgb(img, width, height, bpp, recs, seg_qi, nframes, ctx=None):
+    """The streaming pass fused with convert_image_yuv (zw_transform_quant_mbs_rgb):
+    nframes RGB (bpp 3) / RGBA (bpp 4) frames of width x height pixels in, the
+    same (levels, ry, ru, rv) as transform_quant_mbs on the encoder's MB-padded
+    planes of those frames."""
+    c = _ctx(ctx)
+    mbw, mbh = (width + 15) // 16, (height + 15) // 16
+    nmb = mbw * mbh
+    im = np.ascontiguousarray(img, dtype=np.uint8).reshape(-1)
+    r = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1)
+    q = np.ascontiguousarray(seg_qi, dtype=np.int32).reshape(-1)
+    if im.size != nframes * width * height * bpp:
+        raise ValueError("nframes frames of width x height x bpp bytes")
+    if r.size != nframes * nmb * 96 or q.size != nframes * 4:
+        raise ValueError("one 96-byte record per MB and 4 quantizer indices per frame")
+    lv = np.zeros((nframes * nmb, 25, 16), np.int16)
+    ry = np.zeros(nframes * nmb * 256, np.uint8)
+    ru, rv = np.zeros(nframes * nmb * 64, np.uint8), np.zeros(nframes * nmb * 64, np.uint8)
+    _check(c._lib.zw_transform_quant_mbs_rgb(c.handle, nframes, width, height, bpp, _ptr(im), _ptr(r), _ptr(q),
+                                             _ptr(lv), _ptr(ry), _ptr(ru), _ptr(rv)), "transform_quant_mbs_rgb")
+    return lv, ry, ru, rv
+
+
+def transform_quant_mbs_rgb_device(nframes, width, height, bpp, d_img, img_stride, d_recs, d_segs, d_levels, d_ry,
+                                   d_ru, d_rv, stream=None, ctx=None):
+    """Device-pointer form of transform_quant_mbs_rgb; asynchronous on `stream`."""
+    c = _ctx(ctx)
+    _check(c._lib.zw_transform_quant_mbs_rgb_device(c.handle, stream, nframes, width, height, bpp, d_img, img_stride,
+                                                    d_recs, d_segs, d_levels, d_ry, d_ru, d_rv),
+           "transform_quant_mbs_rgb_device")
 
 
 def loop_filter_frame(y, u, v, mbw, mbh, mb_flags, filter_type, filter_level, sharpness, segments_enabled=0,

@@ -280,6 +280,19 @@ int zw_xmb_seg_table(int nframes, const int32_t *seg_qi, void *out);
 int zw_transform_quant_mbs_device(zw_ctx *ctx, void *stream, int nframes, uint32_t mbw, uint32_t mbh, const void *d_y,
                                   const void *d_u, const void *d_v, const void *d_recs, const void *d_segs,
                                   void *d_levels, void *d_ry, void *d_ru, void *d_rv);
+/* The same pass fused with the colour conversion it follows in the encoder
+ * (convert_image_yuv::<3/4>, encoder/yuv.rs:656-804, with the MB padding of
+ * :765-803): nframes frames of RGB (bpp 3) or RGBA (bpp 4) pixels, width x
+ * height, frame after frame (the device form: frame f at d_img + f *
+ * img_stride).  Outputs equal zw_transform_quant_mbs on the planes
+ * zw_rgb_to_yuv420 makes of the same frames; the planes themselves are never
+ * written (BASELINE config 2: RGBA in, DCT/quant/IDCT, reconstructed YUV out). */
+int zw_transform_quant_mbs_rgb(zw_ctx *ctx, int nframes, uint32_t width, uint32_t height, int bpp, const uint8_t *img,
+                               const uint8_t *recs, const int32_t *seg_qi, int16_t *levels, uint8_t *ry, uint8_t *ru,
+                               uint8_t *rv);
+int zw_transform_quant_mbs_rgb_device(zw_ctx *ctx, void *stream, int nframes, uint32_t width, uint32_t height, int bpp,
+                                      const void *d_img, size_t img_stride, const void *d_recs, const void *d_segs,
+                                      void *d_levels, void *d_ry, void *d_ru, void *d_rv);
 /* In-place loop filter of MB-aligned planes; per-MB flags (luma_mode 0..4,
  * segment, skip, non_zero_dct) as 4 bytes per MB, raster order. */
 int zw_loop_filter_frame(zw_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, uint32_t mbw, uint32_t mbh,

@@ -189,3 +189,25 @@ def test_gpu_xform_mbs_errors(ctx):
         zwebp.transform_quant_mbs(y, u, v, recs, np.full((nf, 4), 200, np.int32), nf, mbw, mbh, ctx=ctx)
     with pytest.raises(ValueError):
         zwebp.transform_quant_mbs(y, u, v, recs[:-1], sq, nf, mbw, mbh, ctx=ctx)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,bpp,nframes", [(1920, 1080, 4, 2), (97, 33, 4, 2), (200, 136, 3, 1), (15, 7, 4, 1),
+                                             (64, 48, 3, 2), (130, 17, 3, 1), (257, 255, 4, 1)])
+def test_gpu_xform_mbs_rgb(ctx, w, h, bpp, nframes):
+    """The pass fused with convert_image_yuv (zw_transform_quant_mbs_rgb, BASELINE
+    config 2 from RGB(A)): equals the oracle's rgb_to_yuv420 followed by the
+    streaming restatement, at aligned widths (16-/8-byte pixel runs) and at
+    ragged ones, odd heights and the MB padding rows (per-pixel edge path)."""
+    import zwebp
+    rng = np.random.default_rng(w * 7 + h + bpp)
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    _, _, _, recs, sq = _random_case(rng, nframes, mbw, mbh, 0.2)
+    imgs = [synth_rgba(w, h, 0x5EED3000 + f, "natural" if f % 2 else "noise")[..., :bpp] for f in range(nframes)]
+    planes = [O.rgb_to_yuv420(np.ascontiguousarray(im), w, h, bpp) for im in imgs]
+    y, u, v = (np.concatenate([p[k] for p in planes]) for k in range(3))
+    want = O.xform_mbs(y, u, v, recs, sq, nframes, mbw, mbh)
+    got = zwebp.transform_quant_mbs_rgb(np.stack(imgs), w, h, bpp, recs, sq, nframes, ctx=ctx)
+    for name, a, b in zip(("levels", "ry", "ru", "rv"), got, want):
+        bad = np.argwhere(a != b)
+        assert bad.size == 0, f"{name}: {len(bad)} differences, first {bad[:4].tolist()}"

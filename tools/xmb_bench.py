@@ -2,7 +2,8 @@
 """Standalone run of bench.py's k_xform_mb leg (the 8(d) roofline pass) for
 rocprofv3 --kernel-trace / --pmc passes: encodes 4 synthetic 1080p frames
 (Q75 m4) to get real modes and borders, then times the record-based streaming
-DCT+quant pass over 256 frames.  Prints one JSON line."""
+DCT+quant pass over 256 frames, RGBA-fused and from Y/U/V planes.  Prints one
+JSON line."""
 import argparse
 import json
 import os
@@ -19,6 +20,7 @@ def main():
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-i4", action="store_true", help="rewrite I4 MBs as I16 DC (cost of the I4 chains)")
+    ap.add_argument("--yuv-only", action="store_true", help="only the Y/U/V-plane form (no RGBA-fused leg)")
     a = ap.parse_args()
     if a.no_i4:
         import zwebp.xmb as X
@@ -38,10 +40,12 @@ def main():
     dev = torch.device("cuda", 0)
     seeds = [frame_seed(i) for i in range(nd)]
     p = zwebp.Pipeline(nd, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    imgs = [synth_rgba(w, h, sd) for sd in seeds]
     for i in range(nd):
-        p.upload(i, synth_rgba(w, h, seeds[i]))
+        p.upload(i, imgs[i])
     p.encode()
-    r = bench.xmb_pass(ctx, torch, dev, p, nd, seeds, w, h, q, m, a.frames, a.reps, bench.load_digests())
+    r = bench.xmb_pass(ctx, torch, dev, p, nd, seeds, w, h, q, m, a.frames, a.reps, bench.load_digests(),
+                       None if a.yuv_only else imgs)
     p.close()
     print(json.dumps(r), flush=True)
 
