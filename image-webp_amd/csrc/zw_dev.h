@@ -621,6 +621,13 @@ DI zs2 as_zs2(uint32_t v) { return __builtin_bit_cast(zs2, v); }
 DI uint32_t as_zu(zs2 v) { return __builtin_bit_cast(uint32_t, v); }
 // (lo16(a), lo16(b)) packed
 DI uint32_t pack_lo(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+DI uint32_t clamp_pk(uint32_t v)  // per i16 half: clamp to [0, 255]
+{
+    const zs2 z = {0, 0}, m = {255, 255};
+    return as_zu(__builtin_elementwise_min(__builtin_elementwise_max(as_zs2(v), z), m));
+}
+DI uint32_t add_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) + as_zs2(b)); }
+DI uint32_t sub_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) - as_zs2(b)); }
 // VOP3P v_dot2_i32_i16, accumulator from an SGPR (the builtin selects the VOP2
 // dot2c form, which costs a v_mov of the accumulator every time)
 DI int dot2(zs2 a, zs2 b, int c)

@@ -995,13 +995,6 @@ __device__ __forceinline__ int hx_sum(int v)  // v(l) + v(l ^ 32), in both lanes
     const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     return (int)r[0] + (int)r[1];
 }
-DI uint32_t clamp_pk(uint32_t v)  // per i16 half: clamp to [0, 255]
-{
-    const zs2 z = {0, 0}, m = {255, 255};
-    return as_zu(__builtin_elementwise_min(__builtin_elementwise_max(as_zs2(v), z), m));
-}
-DI uint32_t add_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) + as_zs2(b)); }
-DI uint32_t sub_pk(uint32_t a, uint32_t b) { return as_zu(as_zs2(a) - as_zs2(b)); }
 DI int dot2v(uint32_t a, uint32_t b, int acc)  // v_dot2_i32_i16, both operands in VGPRs
 {
     int d;

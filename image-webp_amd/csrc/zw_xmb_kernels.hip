@@ -51,52 +51,72 @@ struct XmbSeg {
 #endif
 
 #define XMB_LEVW 200  // words of levels per MB (25 x 16 i16)
+#ifndef XMB_STAGE_LEV
+#define XMB_STAGE_LEV 1  // 1: levels staged in LDS, stored as one contiguous run; 0: stored from the lanes
+#endif
 struct XmbLds {
     uint32_t rec[XMB_MBS][24];      // the 8 records
-    uint32_t yt[16][32];            // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction)
-    uint32_t ct[2][8][16];          // U, V tiles: 8 rows x 8 MBs x 8 B
+    uint32_t yt[16][36];            // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction), rows padded
+                                    // to 144 B: the lanes of a block row (4 MBs x 4 block rows x 4 columns) hit 64 banks
+    uint32_t ct[2][8][20];          // U, V tiles: 8 rows x 8 MBs x 8 B, rows padded to 80 B (64 banks, as yt)
+#if XMB_STAGE_LEV
     uint32_t lev[XMB_MBS][XMB_LEVW];  // the group's levels, laid out as in HBM (one contiguous store run)
+#endif
     XmbSeg seg[4];                  // the frame's four segment matrices (per-lane segment reads hit LDS, not HBM)
 };
 
-// k_xform_mb_i4: four I4 MBs per wave (lane = 16 slot + block).  Queue
+// k_xform_mb_i4: one I4 MB per lane.  Queue
 // layout (u32 words): [0] count (k_xform_mb appends), [1] workgroups done,
 // [64..] global MB indexes.  Zero counters on entry; k_xform_mb_i4's last
 // workgroup zeroes them for the next launch.
 #define XI4_COUNT 0
 #define XI4_DONE 1
 #define XI4_LIST 64
-struct XmbI4Lds {
-    uint32_t rec[4][24];              // the slots' records
-    uint32_t yt[4][16][4];            // per slot: source rows, then reconstruction rows
-    XmbMat y1[4];                     // per slot: its frame's / segment's Y1 matrix
-    uint8_t ws[4][17 * ZW_BPS + 4];   // work buffers (origin at byte 3: row pixels dword aligned)
-    uint8_t vv[64][40];               // per-lane value vectors (dec_i4_values layout)
-};
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
 DI uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
 
-// residual rows (src - pred, 4 bytes a row) -> dct4x4 (transform.rs:176), packed-i16 form
+// byte pairs (b0, b1) and (b3, b2) of a row word as i16 pairs
+DI uint32_t pr01(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c010c00u); }
+DI uint32_t pr32(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c020c03u); }
+// residual rows (src - pred, 4 bytes a row) -> dct4x4 (transform.rs:176): the
+// residual pairs are formed packed (v_perm + v_pk_sub_i16) and fed straight to
+// the packed-i16 row stage of fdct16_pk
 DI void fdct_words(const uint32_t* sw, const uint32_t* pw, int* c)
 {
-    int r[16];
+    const zs2 k8p = {8, 8}, k8m = {8, -8}, k1a = {10704, 4434}, k1b = {4434, -10704};
+    int o[16];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < 4; i++) {
+        const zs2 R01 = as_zs2(sub_pk(pr01(sw[i]), pr01(pw[i]))), R32 = as_zs2(sub_pk(pr32(sw[i]), pr32(pw[i])));
+        const zs2 A = R01 + R32, D = R01 - R32;
+        o[4 * i] = dot2(A, k8p, 0);
+        o[4 * i + 2] = dot2(A, k8m, 0);
+        o[4 * i + 1] = dot2(D, k1a, 3625) >> 10;
+        o[4 * i + 3] = dot2(D, k1b, 1875) >> 10;
+    }
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
 #pragma unroll
-        for (int j = 0; j < 4; j++) r[4 * i + j] = (int)byte_of(sw[i], j) - (int)byte_of(pw[i], j);
-    fdct16_pk(r, c);
+    for (int i = 0; i < 4; i++) {
+        const zs2 X01 = as_zs2(pack_lo(o[i], o[4 + i])), X32 = as_zs2(pack_lo(o[12 + i], o[8 + i]));
+        const zs2 A = X01 + X32, D = X01 - X32;
+        c[i] = dot2(A, k1p, 7) >> 4;
+        c[8 + i] = dot2(A, k1m, 7) >> 4;
+        c[4 + i] = (dot2(D, k2a, 12000) >> 16) + ((as_zu(D) & 0xffffu) != 0u ? 1 : 0);
+        c[12 + i] = dot2(D, k2b, 51000) >> 16;
+    }
 }
-// iDCT (transform.rs:19) + add_residue (prediction.rs:138): reconstruction rows
+// iDCT (transform.rs:19) + add_residue (prediction.rs:138): reconstruction rows,
+// the add and the [0, 255] clamp on i16 pairs (residuals of encoder-made levels
+// stay far inside i16)
 DI void recon_words(int* c, const uint32_t* pw, uint32_t* rw)
 {
     idct16(c);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) w |= (uint32_t)clamp255(c[4 * i + j] + (int)byte_of(pw[i], j)) << (8 * j);
-        rw[i] = w;
+        const uint32_t r01 = clamp_pk(add_pk(pack_lo(c[4 * i], c[4 * i + 1]), pr01(pw[i])));
+        const uint32_t r32 = clamp_pk(add_pk(pack_lo(c[4 * i + 3], c[4 * i + 2]), pr32(pw[i])));
+        rw[i] = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
     }
 }
 // a block's 16 levels in zigzag order as 8 words of i16 pairs, into LDS
@@ -153,7 +173,7 @@ DI void pred_rows(int mode, uint32_t T, const uint8_t* left /* 4 bytes of this b
 DI int diffuse_err(int dc, const XmbMat& m)
 {
     const int level = iabs(qz(dc, m, 0));
-    const int err = iabs(dc) - level * m.q[0];
+    const int err = iabs(dc) - m24(level, m.q[0]);
     const int se = dc < 0 ? -err : err;
     const int e = se >> 1;
     return e < -127 ? -127 : (e > 127 ? 127 : e);
@@ -327,7 +347,17 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 
     if (COPY) {
         // calibration: levels staged from the records, no arithmetic
+#if XMB_STAGE_LEV
         for (int i = lane; i < XMB_MBS * XMB_LEVW; i += 64) (&L.lev[0][0])[i] = (&L.rec[0][0])[i % (XMB_MBS * 24)];
+#else
+        for (int k = 0; k < 3; k++) {
+            const int m = (lane >> 3), b = (lane & 7) + 8 * k;  // 24 blocks of every MB, 8 lanes per MB
+            int lv[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) lv[j] = (int)L.rec[m][j] + b;
+            if (m < nact) store_levels(levels + ((mb0 + m) * 25 + b + (b >= 16)) * 16, lv);
+        }
+#endif
         wsync();
     } else {
         // the group's I4 MBs go on k_xform_mb_i4's queue (their luma is left to it)
@@ -373,16 +403,20 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                 const int t2 = blk > 0;
                 const int y2c = wht_g(c[0], blk);
                 y2l = qz(y2c, my2, t2);
-                const int dcv = iwht_g(y2l * my2.q[t2], blk);
+                const int dcv = iwht_g(m24(y2l, my2.q[t2]), blk);
                 int lv[16];
                 lv[0] = 0;
 #pragma unroll
                 for (int k = 1; k < 16; k++) {
                     lv[k] = qz(c[k], my1, 1);
-                    c[k] = lv[k] * my1.q[1];
+                    c[k] = m24(lv[k], my1.q[1]);
                 }
                 c[0] = dcv;
+#if XMB_STAGE_LEV
                 stage_levels(&L.lev[m][8 * blk], lv);
+#else
+                if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
+#endif
                 uint32_t rw[4];
                 recon_words(c, pw, rw);
 #pragma unroll
@@ -392,7 +426,11 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const int zsrc = (lane & ~15) | kZZ(blk);
             const int zv = __shfl(y2l, zsrc);
             const int zn = __shfl_down(zv, 1);
+#if XMB_STAGE_LEV
             if ((blk & 1) == 0) L.lev[m][128 + (blk >> 1)] = pack_lo(zv, zn);
+#else
+            if ((blk & 1) == 0 && m < nact) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
+#endif
         }
 
         // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB)
@@ -430,9 +468,13 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             for (int k = 0; k < 16; k++) {
                 const int tk = k > 0;
                 lv[k] = qz(c[k], muv, tk);
-                c[k] = lv[k] * muv.q[tk];
+                c[k] = m24(lv[k], muv.q[tk]);
             }
+#if XMB_STAGE_LEV
             stage_levels(&L.lev[m][136 + 8 * (4 * plane + sub)], lv);
+#else
+            if (m < nact) store_levels(levels + ((mb0 + m) * 25 + 17 + 4 * plane + sub) * 16, lv);
+#endif
             uint32_t rw[4];
             recon_words(c, pw, rw);
 #pragma unroll
@@ -446,6 +488,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     // holds its source: k_xform_mb_i4, next on the stream, reads it there and
     // overwrites it with the reconstruction)
     {
+#if XMB_STAGE_LEV
         const int nch = nact * (XMB_LEVW / 4);
         v4u* lo = (v4u*)(levels + mb0 * 400);
 #pragma unroll
@@ -453,6 +496,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const int c = 64 * k + lane;
             if (c < nch) __builtin_nontemporal_store(*((const v4u*)&L.lev[0][0] + c), lo + c);
         }
+#endif
         uint8_t* RYf = RY + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
         const int yc = lane & 7, yr = lane >> 3;
         if (yc < nact) {
@@ -467,135 +511,143 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 }
 
 // The I4 MBs' luma (transform_luma_blocks_4x4, vp8.rs:2785-2916), after
-// k_xform_mb: the queue it filled runs four MBs per wave at a time, lane = 16
-// slot + block, the 16 sub-blocks along the x+2y anti-diagonals (10 steps) in
-// an LDS work buffer with the reference's 32-byte stride.  I4 MBs are rare
-// (2-20 % at Q75 m4) and cluster in textured regions, so a queue balances them
-// over the whole grid and the main pass never waits on their serial chains.
+// k_xform_mb: the queue it filled runs ONE MB PER LANE, 64 per wave, each lane
+// walking its MB's 16 sub-blocks in raster order with the running edges in
+// registers (top row of each block column, the left column, the corner):
+// every wave-instruction does 64 MBs' work, where a lane-per-block layout
+// would leave all but the 1-2 blocks of the current anti-diagonal idle.  I4
+// MBs are rare (2-20 % at Q75 m4) and cluster in textured regions, so the
+// queue balances them over the whole grid and the main pass never waits on
+// their serial chains.
 __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* __restrict__ recs,
                                                               const XmbSeg* __restrict__ segs, int mbw, int mbh,
                                                               int nframes, int16_t* __restrict__ levels,
                                                               uint8_t* __restrict__ RY, uint32_t* __restrict__ i4q)
 {
-    __shared__ XmbI4Lds lds[XMB_WAVES];
-    __shared__ uint8_t i4idx[10][16];  // d_I4_IDX
+    __shared__ uint32_t vvs[XMB_WAVES][10][64];  // per lane: the 39-value vector (word q of lane l at [q][l])
+    __shared__ uint8_t i4idx[10][16];            // d_I4_IDX
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x < 40) ((uint32_t*)i4idx)[threadIdx.x] = ((const uint32_t*)d_I4_IDX)[threadIdx.x];
     __syncthreads();
-    XmbI4Lds& L = lds[wv];
+    const uint8_t* vvb = (const uint8_t*)&vvs[wv][0][0];
     const int nmb = mbw * mbh;
     const uint32_t cap = (uint32_t)((long long)nframes * nmb);
     const uint32_t n = min(__hip_atomic_load(&i4q[XI4_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), cap);
     const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
-    const int slot = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
-    const uint32_t nbatch = (n + 3) / 4, nwaves = gridDim.x * XMB_WAVES;
+    const uint32_t nwaves = gridDim.x * XMB_WAVES;
 #pragma unroll 1
-    for (uint32_t bt = blockIdx.x * XMB_WAVES + wv; bt < nbatch; bt += nwaves) {
-        const uint32_t k = 4 * bt;
+    for (uint32_t k = 64 * (blockIdx.x * XMB_WAVES + wv); k < n; k += 64 * nwaves) {
+        if (k + lane >= n) continue;  // (no cross-lane operations below)
+        const size_t gm = i4q[XI4_LIST + k + lane];
+        const int f = (int)(gm / nmb), rr = (int)(gm % nmb), mby = rr / mbw, x = rr % mbw;
+        // record words 0..15: modes/segment, bpred, corner, top 16 + top-right 4, left 16
+        uint32_t R[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const v4u r4 = *((const v4u*)(recs + gm * 96) + q);
+            R[4 * q] = r4.x; R[4 * q + 1] = r4.y; R[4 * q + 2] = r4.z; R[4 * q + 3] = r4.w;
+        }
+        const int seg = (int)((R[0] >> 16) & 3u);
+        XmbMat my1;
         {
-            const bool valid = k + slot < n;
-            const size_t gm = i4q[XI4_LIST + (valid ? k + slot : k)];
-            const int f = (int)(gm / nmb), r = (int)(gm % nmb), mby = r / mbw, x = r % mbw;
-            // k_xform_mb left the MB's source luma in its reconstruction tile
-            uint8_t* yrow = RY + f * ysz + (size_t)(mby * 16 + blk) * ys + (size_t)x * 16;
-            // stage: record (lanes 0-5 of the slot), source row `blk` of the slot's MB, Y1 matrix
-            {
-                v4u r4 = {0u, 0u, 0u, 0u};
-                if (blk < 6) r4 = *((const v4u*)(recs + gm * 96) + blk);
-                const v4u y4 = *(const v4u*)yrow;
-                if (blk < 6) *(v4u*)&L.rec[slot][4 * blk] = r4;
-                *(v4u*)&L.yt[slot][blk][0] = y4;
-                wsync();
-                const int seg = (int)((L.rec[slot][0] >> 16) & 3u);
-                if (blk < 2) {
-                    const v4u m4 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1 + blk);
-                    *((v4u*)&L.y1[slot] + blk) = m4;
-                }
-            }
-            const uint32_t* R = L.rec[slot];
-            uint8_t* ws = L.ws[slot] + 3;
-            // create_border_luma from the record: corner, top 16 + top-right 4, left 16,
-            // the top-right 4 copied to rows 4, 8, 12
-            if (blk < 5) *(uint32_t*)(ws + 1 + 4 * blk) = R[6 + blk];
-            if (blk == 5) ws[0] = (uint8_t)(R[5] & 255u);
-            if (blk >= 6 && blk < 9) *(uint32_t*)(ws + 4 * (blk - 5) * ZW_BPS + 17) = R[10];
-            ws[(blk + 1) * ZW_BPS] = ((const uint8_t*)R)[44 + blk];
-            wsync();
-            const XmbMat& my1 = L.y1[slot];
-            const int sm = (int)((R[1 + (blk >> 3)] >> (4 * (blk & 7))) & 15u);  // bpred[blk]
-            const int xo = bx * 4 + 1, yo = by * 4 + 1;
-            uint8_t* vv = L.vv[lane];
-            int16_t* lvl = levels + (gm * 25 + blk) * 16;
+            const v4u m0 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1), m1 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1 + 1);
+            my1.iq[0] = (int)m0.x; my1.iq[1] = (int)m0.y; my1.bp[0] = (int)m0.z; my1.bp[1] = (int)m0.w;
+            my1.bn[0] = (int)m1.x; my1.bn[1] = (int)m1.y; my1.q[0] = (int)m1.z; my1.q[1] = (int)m1.w;
+        }
+        // k_xform_mb left the MB's source luma in its reconstruction tile
+        uint8_t* ymb = RY + f * ysz + (size_t)mby * 16 * ys + (size_t)x * 16;
+        uint32_t top[4] = {R[6], R[7], R[8], R[9]};  // bottom row above each block column
+        uint32_t lc[4] = {R[11], R[12], R[13], R[14]};  // the MB's left column, 4 rows a word
+        uint32_t pc0 = R[5] & 255u;                      // corner of block (0, by)
 #pragma unroll 1
-            for (int t = 0; t < 10; t++) {
-                if (valid && bx + 2 * by == t) {
-                    // the 39-value vector of this sub-block's edges (k_dec_recon's dec_i4_values)
-                    int E[13];
+        for (int by = 0; by < 4; by++) {
+            uint32_t src[4][4], rec[4][4];  // [row][block column]
 #pragma unroll
-                    for (int j = 0; j < 4; j++) E[j] = ws[(yo + 3 - j) * ZW_BPS + xo - 1];
-                    E[4] = ws[(yo - 1) * ZW_BPS + xo - 1];
-#pragma unroll
-                    for (int j = 5; j < 13; j++) E[j] = ws[(yo - 1) * ZW_BPS + xo + (j - 5)];
-                    uint32_t vw[10];
-#pragma unroll
-                    for (int q = 0; q < 10; q++) {
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const int i = 4 * q + j;
-                            int v;
-                            if (i < 13) v = E[i];
-                            else if (i < 24) v = (E[i - 13] + 2 * E[i - 12] + E[i - 11] + 2) >> 2;
-                            else if (i < 36) v = (E[i - 24] + E[i - 23] + 1) >> 1;
-                            else if (i == 36) v = (E[11] + 3 * E[12] + 2) >> 2;
-                            else if (i == 37) v = (E[1] + 3 * E[0] + 2) >> 2;
-                            else if (i == 38) v = (4 + E[0] + E[1] + E[2] + E[3] + E[5] + E[6] + E[7] + E[8]) >> 3;
-                            else v = 0;
-                            w |= (uint32_t)v << (8 * j);
-                        }
-                        vw[q] = w;
-                    }
-#pragma unroll
-                    for (int q = 0; q < 10; q++) *(uint32_t*)(vv + 4 * q) = vw[q];
-                    uint32_t pw[4];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const int idx = i4idx[sm][4 * r + j];
-                            int v;
-                            if (idx == 254) v = clamp255(E[3 - r] + E[5 + j] - E[4]);
-                            else v = vv[idx == 255 ? 38 : idx];
-                            w |= (uint32_t)v << (8 * j);
-                        }
-                        pw[r] = w;
-                    }
-                    uint32_t s4[4];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) s4[r] = L.yt[slot][by * 4 + r][bx];
-                    int cf[16], lv[16];
-                    fdct_words(s4, pw, cf);
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const int tk = j > 0;
-                        lv[j] = qz(cf[j], my1, tk);
-                        cf[j] = lv[j] * my1.q[tk];
-                    }
-                    store_levels(lvl, lv);
-                    uint32_t rw[4];
-                    recon_words(cf, pw, rw);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        *(uint32_t*)(ws + (yo + r) * ZW_BPS + xo) = rw[r];
-                        L.yt[slot][by * 4 + r][bx] = rw[r];
-                    }
-                }
-                wsync();
+            for (int r = 0; r < 4; r++) {
+                const v4u v = *(const v4u*)(ymb + (size_t)(4 * by + r) * ys);
+                src[r][0] = v.x; src[r][1] = v.y; src[r][2] = v.z; src[r][3] = v.w;
             }
-            // the reconstruction rows back to the plane (row blk of the slot's MB)
-            if (valid) __builtin_nontemporal_store(*(const v4u*)&L.yt[slot][blk][0], (v4u*)yrow);
-            wsync();
+            const uint32_t bpw = (by < 2 ? R[1] : R[2]) >> (16 * (by & 1));
+            uint32_t L = lc[0], P = pc0;
+#pragma unroll
+            for (int bx = 0; bx < 4; bx++) {
+                const uint32_t T = top[bx], TR = bx < 3 ? top[bx + 1] : R[10];
+                const int sm = (int)((bpw >> (4 * bx)) & 15u);
+                // the 13 edges: left column bottom-up, corner, top 4 + top-right 4
+                int E[13];
+#pragma unroll
+                for (int j = 0; j < 4; j++) E[j] = (int)byte_of(L, 3 - j);
+                E[4] = (int)P;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    E[5 + j] = (int)byte_of(T, j);
+                    E[9 + j] = (int)byte_of(TR, j);
+                }
+                // the 39-value vector (k_dec_recon's dec_i4_values), then this mode's pixels
+#pragma unroll
+                for (int q = 0; q < 10; q++) {
+                    uint32_t wd = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int i = 4 * q + j;
+                        int v;
+                        if (i < 13) v = E[i];
+                        else if (i < 24) v = (E[i - 13] + 2 * E[i - 12] + E[i - 11] + 2) >> 2;
+                        else if (i < 36) v = (E[i - 24] + E[i - 23] + 1) >> 1;
+                        else if (i == 36) v = (E[11] + 3 * E[12] + 2) >> 2;
+                        else if (i == 37) v = (E[1] + 3 * E[0] + 2) >> 2;
+                        else if (i == 38) v = (4 + E[0] + E[1] + E[2] + E[3] + E[5] + E[6] + E[7] + E[8]) >> 3;
+                        else v = 0;
+                        wd |= (uint32_t)v << (8 * j);
+                    }
+                    vvs[wv][q][lane] = wd;
+                }
+                uint32_t pw[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    uint32_t wd = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int idx = i4idx[sm][4 * r + j];
+                        int v;
+                        if (idx == 254) v = clamp255(E[3 - r] + E[5 + j] - E[4]);
+                        else {
+                            const int ii = idx == 255 ? 38 : idx;
+                            v = vvb[((ii >> 2) * 64 + lane) * 4 + (ii & 3)];
+                        }
+                        wd |= (uint32_t)v << (8 * j);
+                    }
+                    pw[r] = wd;
+                }
+                uint32_t s4[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) s4[r] = src[r][bx];
+                int cf[16], lv[16];
+                fdct_words(s4, pw, cf);
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const int tk = j > 0;
+                    lv[j] = qz(cf[j], my1, tk);
+                    cf[j] = m24(lv[j], my1.q[tk]);
+                }
+                store_levels(levels + (gm * 25 + 4 * by + bx) * 16, lv);
+                uint32_t rw[4];
+                recon_words(cf, pw, rw);
+#pragma unroll
+                for (int r = 0; r < 4; r++) rec[r][bx] = rw[r];
+                // the next block's edges: this block's right column, the corner above it
+                P = T >> 24;
+                L = (rw[0] >> 24) | ((rw[1] >> 24) << 8) | ((rw[2] >> 24) << 16) | (rw[3] & 0xff000000u);
+                top[bx] = rw[3];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                __builtin_nontemporal_store(v4u{rec[r][0], rec[r][1], rec[r][2], rec[r][3]},
+                                            (v4u*)(ymb + (size_t)(4 * by + r) * ys));
+            pc0 = lc[0] >> 24;
+            lc[0] = lc[1];
+            lc[1] = lc[2];
+            lc[2] = lc[3];
         }
     }
     // the last workgroup out zeroes the queue counters for the next launch
@@ -667,9 +719,10 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     }
 #undef XMB_LAUNCH
     if (copy) return hipGetLastError();
-    // the I4 queue: one workgroup per 256 MBs of the launch, at most 1024
+    // the I4 queue: waves of 64 MBs; one per 64 x 16 MBs of the launch (an I4
+    // share up to 1/16 runs in one pass over the grid), at most 1024 workgroups
     const long long nmbs = (long long)nframes * mbw * mbh;
-    const unsigned g4 = (unsigned)min((nmbs + 255) / 256, 1024LL);
+    const unsigned g4 = (unsigned)min((nmbs + 64 * 16 * XMB_WAVES - 1) / (64 * 16 * XMB_WAVES), 1024LL);
     hipLaunchKernelGGL(k_xform_mb_i4, dim3(g4), dim3(64 * XMB_WAVES), 0, s, recs, sg, mbw, mbh, nframes, levels, RY,
                        queue);
     return hipGetLastError();
