@@ -946,12 +946,15 @@ __global__ __launch_bounds__(256) void k_yuv2rgb(const uint8_t* __restrict__ Y, 
     V += (size_t)f * csz;
     uint8_t* o = out + ((size_t)f * h + r) * (size_t)w * BPP + (size_t)x * BPP;
     const int cw1 = ((w + 1) >> 1) - 1, ch1 = ((h + 1) >> 1) - 1;
-    const bool fast = x >= 8 && x + 8 <= w && (x >> 1) + 5 <= cw1 + 1 && (x >> 1) + 8 <= cs && (ys & 7) == 0 &&
-                      (cs & 3) == 0 && ((uintptr_t)o & (BPP == 4 ? 15 : 3)) == 0;
+    // (every full 8-pixel run takes the vector path; at the image's left / right
+    // edge the fancy filter's outer chroma column is the edge column itself, so
+    // the neighbour word is not loaded and the edge byte stands in for it)
+    const bool fast = x + 8 <= w && (ys & 7) == 0 && (cs & 3) == 0 && ((uintptr_t)o & (BPP == 4 ? 15 : 3)) == 0;
     uint32_t px[8];
     if (fast) {
         const uint2 yy = *(const uint2*)(Y + (size_t)r * ys + x);
-        const int cb = (x >> 1) - 4;
+        const bool lok = x > 0, rok = (x >> 1) + 4 <= cw1;
+        const int c1 = x >> 1, c0 = lok ? c1 - 4 : c1, c2 = rok ? c1 + 4 : c1;
         int mr, sr;
         if (FANCY) {
             const int k = (r + 1) >> 1;
@@ -960,27 +963,38 @@ __global__ __launch_bounds__(256) void k_yuv2rgb(const uint8_t* __restrict__ Y, 
         } else {
             mr = sr = r >> 1;
         }
-        const uint32_t* um = (const uint32_t*)(U + (size_t)mr * cs + cb);
-        const uint32_t* vm = (const uint32_t*)(V + (size_t)mr * cs + cb);
-        const uint32_t um0 = um[0], um1 = um[1], um2 = um[2], vm0 = vm[0], vm1 = vm[1], vm2 = vm[2];
-        uint32_t us0 = um0, us1 = um1, us2 = um2, vs0 = vm0, vs1 = vm1, vs2 = vm2;
+        auto row3 = [&](const uint8_t* P, int rr, int& b0, int& b5, uint32_t& mid) {
+            const uint8_t* q = P + (size_t)rr * cs;
+            const uint32_t a = *(const uint32_t*)(q + c0), m = *(const uint32_t*)(q + c1), z = *(const uint32_t*)(q + c2);
+            b0 = (int)(lok ? a >> 24 : m & 255u);
+            b5 = (int)(rok ? z & 255u : m >> 24);
+            mid = m;
+        };
+        int um_l, um_r, vm_l, vm_r, us_l, us_r, vs_l, vs_r;
+        uint32_t umw, vmw, usw, vsw;
+        row3(U, mr, um_l, um_r, umw);
+        row3(V, mr, vm_l, vm_r, vmw);
         if (FANCY) {
-            const uint32_t* us = (const uint32_t*)(U + (size_t)sr * cs + cb);
-            const uint32_t* vs = (const uint32_t*)(V + (size_t)sr * cs + cb);
-            us0 = us[0], us1 = us[1], us2 = us[2], vs0 = vs[0], vs1 = vs[1], vs2 = vs[2];
+            row3(U, sr, us_l, us_r, usw);
+            row3(V, sr, vs_l, vs_r, vsw);
+        } else {
+            us_l = um_l, us_r = um_r, usw = umw, vs_l = vm_l, vs_r = vm_r, vsw = vmw;
         }
         // fancy: 9 m + 3 s1 + 3 s2 + t = 3 (3 um + us)[mc] + (3 um + us)[sc], so
-        // blend the two chroma rows once per column (local columns 3..8)
+        // blend the two chroma rows once per column (local columns x/2-1 .. x/2+4)
         int tu[6], tv[6];
 #pragma unroll
         for (int j = 0; j < 6; j++) {
-            const int c = 3 + j;
+            const int um = j == 0 ? um_l : (j == 5 ? um_r : (int)((umw >> (8 * (j - 1))) & 255u));
+            const int us = j == 0 ? us_l : (j == 5 ? us_r : (int)((usw >> (8 * (j - 1))) & 255u));
+            const int vm = j == 0 ? vm_l : (j == 5 ? vm_r : (int)((vmw >> (8 * (j - 1))) & 255u));
+            const int vs = j == 0 ? vs_l : (j == 5 ? vs_r : (int)((vsw >> (8 * (j - 1))) & 255u));
             if (FANCY) {
-                tu[j] = 3 * byte_of(um0, um1, um2, c) + byte_of(us0, us1, us2, c);
-                tv[j] = 3 * byte_of(vm0, vm1, vm2, c) + byte_of(vs0, vs1, vs2, c);
+                tu[j] = 3 * um + us;
+                tv[j] = 3 * vm + vs;
             } else {
-                tu[j] = byte_of(um0, um1, um2, c);
-                tv[j] = byte_of(vm0, vm1, vm2, c);
+                tu[j] = um;
+                tv[j] = vm;
             }
         }
 #pragma unroll

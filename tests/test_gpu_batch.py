@@ -128,6 +128,42 @@ def test_webp_container_alpha(ctx, color, w, h):
         assert np.array_equal(dec[..., 3], img[..., -1])
 
 
+def _tied_alpha_img(w=640, h=256):
+    """Alpha whose length-limited Huffman trees split tie groups (the order of
+    the reference's sort_unstable_by_key decides which equal-frequency symbols
+    get the longer codes, api.rs:259-260; the same distribution as
+    test_lossless's tied640x256)."""
+    rng = np.random.default_rng(7)
+    parts = [np.full(int(1.6 ** k), 100 + k, np.uint8) for k in range(22)]
+    parts += [np.full(c, s, np.uint8) for s, c in zip(range(0, 90), [1, 2, 3] * 30)]
+    g = np.resize(np.concatenate(parts), w * h)
+    rng.shuffle(g)
+    img = synth_rgba(w, h, 0x5EED0077)
+    img[..., 3] = g.reshape(h, w)
+    return np.ascontiguousarray(img)
+
+
+# SHA-256 of the oracle's ALPH payload for _tied_alpha_img() (drift guard; the
+# oracle at c7fefce, parity with the reference's VP8L bytes unpinned: no fixture)
+TIED_ALPH_SHA256 = "08401df9d5aa9a5b05e160fd3a4b0b8ff95c994185148dda6f22914325e6e24d"
+
+
+def test_webp_container_tied_alpha(ctx):
+    """WebPEncoder::encode (lossy, RGBA) on the tie-split alpha: the whole RIFF
+    (VP8X + ALPH + VP8) equals the oracle's, and the ALPH payload its pinned digest."""
+    import hashlib
+    w, h = 640, 256
+    img = _tied_alpha_img(w, h)
+    rc, vp8, _ = O.encode(img, w, h, 3, 75, 4)
+    assert rc == 0
+    rc, alph = O.encode_alpha(img, w, h, 3)
+    assert rc == 0 and hashlib.sha256(bytes(alph)).hexdigest() == TIED_ALPH_SHA256
+    enc = zwebp.WebPEncoder(ctx=ctx)
+    enc.set_params(zwebp.EncoderParams.lossy(75, 4))
+    got = bytes(enc.encode(img, w, h, zwebp.ColorType.Rgba8))
+    assert got == _riff(_vp8x(w, h, 0x10), _chunk(b"ALPH", alph), _chunk(b"VP8 ", vp8))
+
+
 def test_encode_webp_rgba_entry(ctx):
     """zw_encode_webp (EncoderParams::lossy) for RGBA8 equals the _ex form."""
     w, h = 200, 120

@@ -532,3 +532,4 @@ def test_transform_quant_blocks_ragged(ctx, n):
 def test_transform_quant_blocks_empty(ctx):
     lv, rc = zwebp.transform_quant_blocks(np.zeros((0, 16), np.uint8), np.zeros((0, 16), np.uint8), 24, 30, ctx=ctx)
     assert lv.shape == (0, 16)
+
