@@ -25,15 +25,20 @@ timed region and the max time is taken with an all-reduce.
                    GPUs): a step encodes T frames in total, rank r the block
                    shard_range(T, r, N), in device batches of `--batch` frames.
 
-`roofline`: SURVEY.md 8(d)'s designated HBM-bound kernel, the streaming
-DCT+quant pass k_fdct_quant, over 256 frames' worth of 4x4 blocks (24 per MB)
-resident in HBM: ALGORITHMIC bytes 64 per block (16 src + 32 levels + 16
-recon; 1568 B/MB) / the average launch time from HIP events on the launch
-stream.  The materialised prediction (16 B per block) is traffic the kernel
-moves but 8(d) does not count; it is reported separately
-(achieved_incl_pred).  `copy_ceiling` times a kernel with the same read:write
-mix and no arithmetic on the same buffers (ZW_XFORM_VARIANT=99).  `traffic`
-is the PMC-measured HBM bytes per launch from profiles/ scaled to this launch.
+`roofline`: SURVEY.md 8(d)'s designated HBM-bound pass, the streaming
+DCT+quant pass over per-MB records (k_xform_mb + k_xform_mb_i4) on 256 frames
+resident in HBM, BASELINE config 2's form: the synthetic RGBA frames in
+(convert_image_yuv fused), levels + reconstructed YUV out.  ALGORITHMIC bytes =
+the RGBA read (w*h*4 per frame) + levels 800 + recon 384 per MB (8(d)'s
+fused-RGB->YUV form) / the average launch time from HIP events on the launch
+stream.  The 96-byte record is traffic the pass moves but 8(d) does not count
+(achieved_incl_records).  `yuv_planes_form` is the same pass from Y/U/V planes
+at 1568 B/MB.  `copy_ceiling` runs the same loads and stores with no transform
+arithmetic (ZW_XMB_VARIANT=99).  `traffic` is the PMC-measured HBM bytes per
+launch from profiles/r03_xmb_pmc.json scaled to this launch.  Every frame's
+levels and reconstruction are hashed against the oracle's digests.
+`roofline_blocks`: k_fdct_quant, the same arithmetic on 4x4 blocks with the
+prediction materialised (64 B per block counted, 16 B of prediction moved).
 `encode_roofline`: the step's dominant kernel, k_encode_pass2 (RD mode search
 fused with the final DCT+quant+recon), against the VALU issue peak: its VALU
 instructions per launch (rocprofv3 SQ_INSTS_VALU, profiles/) over the live

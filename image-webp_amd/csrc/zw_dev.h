@@ -76,6 +76,40 @@ __device__ __forceinline__ int pk_v(uint32_t p)
 {
     return 28800 * (int)(p & 255u) - 24116 * (int)((p >> 8) & 255u) - 4684 * (int)((p >> 16) & 255u);
 }
+// The same sums by 16-bit dot products (identical integers): Y from the (R, G)
+// pair of the pixel word by one v_dot2_u32_u16 plus 6420 B; the 2x2 U / V sums
+// from the four pixels' (R, B) pairs and G added first (packed u16 adds, at
+// most 1 020 each), then one v_dot2_i32_i16 and one multiply-add per plane.
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t d;
+    asm("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ int sdot2(uint32_t a, uint32_t b, int c)
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t pk_y2(uint32_t p)
+{
+    const uint32_t rg = __builtin_amdgcn_perm(0u, p, 0x0c010c00u);  // (R, G)
+    return udot2(rg, 0x812341c7u /* (16839, 33059) */, ((p >> 16) & 255u) * 6420u + (1u << 15) + (16u << 16)) >> 16;
+}
+// (U, V) bytes of the 2x2 of pixels a, b (row 0) and c, d (row 1): (s + 2^17) >> 18
+// of s = sum of pk_u / pk_v + (512 << 16)
+__device__ __forceinline__ void pk_uv4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t& u, uint32_t& v)
+{
+    const uint32_t sel = 0x0c020c00u;  // (R, B)
+    const uint32_t rb = __builtin_amdgcn_perm(0u, a, sel) + __builtin_amdgcn_perm(0u, b, sel) +
+                        __builtin_amdgcn_perm(0u, c, sel) + __builtin_amdgcn_perm(0u, d, sel);
+    const int g = (int)(((a >> 8) & 255u) + ((b >> 8) & 255u) + ((c >> 8) & 255u) + ((d >> 8) & 255u));
+    const int su = sdot2(rb, 0x7080da09u /* (-9719, 28800) */, g * -19081 + (512 << 16));
+    const int sv = sdot2(rb, 0xedb47080u /* (28800, -4684) */, g * -24116 + (512 << 16));
+    u = (uint32_t)((su + (1 << 17)) >> 18);
+    v = (uint32_t)((sv + (1 << 17)) >> 18);
+}
 
 // Intra-wave LDS hand-off: lanes of one wave exchange data through LDS.  A
 // wave's DS instructions execute in issue order, so a wavefront-scope fence

@@ -147,6 +147,9 @@ DI uint32_t dc_word(uint32_t sum_top, uint32_t sum_left, int has_top, int has_le
 }
 DI uint32_t bsum(uint32_t w) { return __builtin_amdgcn_sad_u8(w, 0u, 0u); }
 // V / H / TM / DC prediction rows of the 4x4 block at (bx, by) of a 16x16 or 8x8 block
+// (predict_vpred / hpred / tmpred / dcpred, prediction.rs:164-324).  Branches:
+// the MBs of a wave mostly share a mode (measured: a branch-free select of all
+// four was 4 % slower from Y/U/V planes).  TM on i16 pairs: clamp(L + T[j] - P).
 DI void pred_rows(int mode, uint32_t T, const uint8_t* left /* 4 bytes of this block's rows */, int P, uint32_t dcw,
                   uint32_t* pw)
 {
@@ -159,9 +162,10 @@ DI void pred_rows(int mode, uint32_t T, const uint8_t* left /* 4 bytes of this b
         } else if (mode == 2) {
             w = (uint32_t)L * 0x01010101u;
         } else if (mode == 3) {
-            w = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) w |= (uint32_t)clamp255(L + (int)byte_of(T, j) - P) << (8 * j);
+            const uint32_t d = (uint32_t)(L - P) & 0xffffu, dd = d | (d << 16);
+            const uint32_t r01 = clamp_pk(add_pk(__builtin_amdgcn_perm(0u, T, 0x0c010c00u), dd));
+            const uint32_t r32 = clamp_pk(add_pk(__builtin_amdgcn_perm(0u, T, 0x0c020c03u), dd));
+            w = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
         } else {
             w = dcw;
         }
@@ -257,15 +261,15 @@ DI void rgb_item(const uint8_t* __restrict__ img, int w, int h, bool runs, int p
     ya[0] = ya[1] = yb[0] = yb[1] = uw = vw = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        ya[i >> 2] |= (uint32_t)pk_y(a[i]) << (8 * (i & 3));
-        yb[i >> 2] |= (uint32_t)pk_y(b[i]) << (8 * (i & 3));
+        ya[i >> 2] |= pk_y2(a[i]) << (8 * (i & 3));
+        yb[i >> 2] |= pk_y2(b[i]) << (8 * (i & 3));
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int su = pk_u(ca[2 * j]) + pk_u(ca[2 * j + 1]) + pk_u(cb[2 * j]) + pk_u(cb[2 * j + 1]) + (512 << 16);
-        const int sv = pk_v(ca[2 * j]) + pk_v(ca[2 * j + 1]) + pk_v(cb[2 * j]) + pk_v(cb[2 * j + 1]) + (512 << 16);
-        uw |= (uint32_t)((su + (1 << 17)) >> 18) << (8 * j);
-        vw |= (uint32_t)((sv + (1 << 17)) >> 18) << (8 * j);
+        uint32_t u, v;
+        pk_uv4(ca[2 * j], ca[2 * j + 1], cb[2 * j], cb[2 * j + 1], u, v);
+        uw |= u << (8 * j);
+        vw |= v << (8 * j);
     }
 }
 
