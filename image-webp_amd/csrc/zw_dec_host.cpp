@@ -24,8 +24,7 @@ extern "C" {
 hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
                           ZwDecMb* mbs, int nmb, int nframes);
 hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
-                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes,
-                         const ZwFilterParams* fused_fp);
+                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
                        int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
 hipError_t zwk_dec_rows(hipStream_t s, int phase, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
@@ -35,7 +34,7 @@ hipError_t zwk_dec_rows_init(hipStream_t s, int* rowsync, int mbh, int nframes);
 size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
-                          const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes);
+                          const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw);
 }
 
 namespace {
@@ -648,9 +647,8 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     HIPOK(hipEventRecord(ev[0], s));
     HIPOK(zwk_dec_expand(s, d + o_mbs, (const uint32_t*)(d + o_mbs + o_moff), (const uint64_t*)(d + o_mbs + o_base),
                          (ZwDecMb*)(d + o_full), (int)nmb, n));
-    // two wavefront kernels (ZW_DEC_FUSE=1: one fused wavefront; measured slower on
-    // a 1080p frame, 8.2 vs 4.6 + 3.0 ms: the per-MB latencies add up in one chain)
-    static const bool split = getenv("ZW_DEC_FUSE") == nullptr;
+    // two wavefront kernels (a fused recon + filter wavefront measured slower: the
+    // per-MB latencies add up in one chain, and its registers spilled)
     if (rows) {
         int* rs = (int*)(d + o_rs);
         HIPOK(zwk_dec_rows_init(s, rs, mbh, n));
@@ -662,11 +660,9 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
     } else {
         HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh,
-                            ysz, csz, n, split ? nullptr : (const ZwFilterParams*)(d + o_fp)));
+                            ysz, csz, n));
         HIPOK(hipEventRecord(ev[1], s));
-        if (split)
-            HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz,
-                                 n));
+        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n, mbw));
     }
     HIPOK(hipEventRecord(ev[2], s));
     if (dec_timing()) {
@@ -993,7 +989,8 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
         HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp),
                            (int)mbw, (int)mbh, ysz, csz, 1, (int*)(d + o_rs), nullptr, (int)mbh));
     } else {
-        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1));
+        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1,
+                             (int)mbw));
     }
     HIPOK(hipMemcpyAsync(y, d + o_y, ysz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));

@@ -7,11 +7,15 @@
 //
 // Both kernels run one workgroup per frame; macroblock rows go round-robin to
 // NWD waves and advance as an x+2y wavefront (MB x of row y starts once row
-// y-1 has finished MB x+1).  Reconstruction keeps the prediction borders in LDS
-// (they are the unfiltered pixels, vp8.rs:791-797).  The loop filter stages
-// each MB's 20x20 luma / 12x12 chroma neighbourhood in LDS, filters it in the
-// reference's edge order and writes it back; the wavefront order makes every
-// overlapping access happen in raster order, as in the reference.
+// y-1 has finished MB x+1).  Reconstruction works in quad form (lane = 4 block
+// + pixel row: the iDCT's column pass in the lane, the transpose by DPP, the
+// row as one word of the plane) from the unfiltered borders kept in LDS
+// (vp8.rs:791-797); only I4 MBs chain through an LDS work area.  The loop
+// filter stages each MB's 20x20 luma / 12x12 chroma neighbourhood in LDS,
+// filters one row per lane across the vertical edges and then one column per
+// lane across the horizontal ones (the reference's edge order, each line in
+// registers), and writes it back; the wavefront order makes every overlapping
+// access happen in raster order, as in the reference.
 #include "zw_dev.h"
 
 #ifndef ZW_NWD
@@ -27,27 +31,29 @@ struct ZwDecQuant {
 struct DecLds {
     uint4 rec[52];  // the current MB's ZwDecMb record (832 B), prefetched one MB ahead
     uint8_t i4idx[10][16];
-    uint8_t ws[17 * ZW_BPS];
-    uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
+    uint8_t ws[17 * ZW_BPS];  // I4 MBs: the luma work area (border row / column + 16x16)
     uint8_t left_y[20], left_u[12], left_v[12];
     int V[40];
-    int dc[16];
-    int res[16];
-    int misc[4];
     uint32_t twy[8], twu[2], twv[2];  // row-parallel kernel: the row above's bottom pixels around this MB
     ZwDecQuant q[4];                  // row-parallel kernel: the frame's segment quantisers
 };
 
+// Row hand-off inside a workgroup.  Everything a row passes to the row below
+// (border pixels, progress) lives in LDS, so publishing waits only for this
+// wave's LDS writes (lgkmcnt), never for its global stores: those are written
+// by one wave each and read by no other wave of the kernel.  LDS accesses are
+// coherent across the CU's waves, so once the consumer has read the progress
+// word its later LDS reads see every write made before it.
 __device__ __forceinline__ void dec_wait(const int* progress, int w, int need)
 {
-    while (__hip_atomic_load(&progress[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+    while (__hip_atomic_load(&progress[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
         __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void dec_publish(int* progress, int w, int val)
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(&progress[w], val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(&progress[w], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -99,64 +105,74 @@ __device__ __forceinline__ int c8(int v) { return v < -128 ? -128 : (v > 127 ? 1
 __device__ __forceinline__ int u2s(int v) { return v - 128; }
 __device__ __forceinline__ uint8_t s2u(int v) { return (uint8_t)(c8(v) + 128); }
 
-// p points at q0; s = step across the edge.
-__device__ __forceinline__ int lf_common(int outer, uint8_t* p, int s)
+// One edge of one line, branch-free (loop_filter.rs): the eight pixels across
+// the edge, p3 p2 p1 p0 | q0 q1 q2 q3, as unsigned values.  KIND 0: simple
+// filter (simple_segment), 1: inner edge (subblock_filter), 2: macroblock edge
+// (macroblock_filter).  en: the edge is filtered on this line at all.
+template <int KIND>
+__device__ __forceinline__ void lf_edge(bool en, int ht, int il, int el, int& p3, int& p2, int& p1, int& p0, int& q0,
+                                        int& q1, int& q2, int& q3)
 {
-    const int p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]), q0 = u2s(p[0]), q1 = u2s(p[s]);
-    const int o = outer ? c8(p1 - q1) : 0;
-    int a = c8(o + 3 * (q0 - p0));
-    const int b = c8(a + 3) >> 3;
+    const int P1 = u2s(p1), P0 = u2s(p0), Q0 = u2s(q0), Q1 = u2s(q1);
+    const bool th = iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= el;
+    bool on = en && th;
+    bool hev = false;
+    if (KIND != 0) {
+        on = on && iabs(p3 - p2) <= il && iabs(p2 - p1) <= il && iabs(p1 - p0) <= il && iabs(q3 - q2) <= il &&
+             iabs(q2 - q1) <= il && iabs(q1 - q0) <= il;
+        hev = iabs(p1 - p0) > ht || iabs(q1 - q0) > ht;
+    }
+    // common_adjust (use_outer_taps = simple || hev || the mb edge's hev branch)
+    const bool outer = KIND == 0 || hev;
+    int a = c8(csel(outer, c8(P1 - Q1), 0) + 3 * (Q0 - P0));
+    const int b3 = c8(a + 3) >> 3;
     a = c8(a + 4) >> 3;
-    p[0] = s2u(q0 - a);
-    p[-s] = s2u(p0 + b);
-    return a;
-}
-__device__ __forceinline__ bool lf_simple_th(int lim, const uint8_t* p, int s)
-{
-    return iabs(p[-s] - p[0]) * 2 + iabs(p[-2 * s] - p[s]) / 2 <= lim;
-}
-__device__ __forceinline__ bool lf_should(int il, int el, const uint8_t* p, int s)
-{
-    return lf_simple_th(el, p, s) && iabs(p[-4 * s] - p[-3 * s]) <= il && iabs(p[-3 * s] - p[-2 * s]) <= il &&
-           iabs(p[-2 * s] - p[-s]) <= il && iabs(p[3 * s] - p[2 * s]) <= il && iabs(p[2 * s] - p[s]) <= il &&
-           iabs(p[s] - p[0]) <= il;
-}
-__device__ __forceinline__ bool lf_hev(int t, const uint8_t* p, int s) { return iabs(p[-2 * s] - p[-s]) > t || iabs(p[s] - p[0]) > t; }
-
-__device__ void lf_simple(int el, uint8_t* p, int s)
-{
-    if (lf_simple_th(el, p, s)) lf_common(1, p, s);
-}
-__device__ void lf_inner(int ht, int il, int el, uint8_t* p, int s)
-{
-    if (lf_should(il, el, p, s)) {
-        const bool hv = lf_hev(ht, p, s);
-        const int a = (lf_common(hv, p, s) + 1) >> 1;
-        if (!hv) {
-            p[s] = s2u(u2s(p[s]) - a);
-            p[-2 * s] = s2u(u2s(p[-2 * s]) + a);
-        }
+    int n_p0 = s2u(P0 + b3), n_q0 = s2u(Q0 - a), n_p1 = p1, n_q1 = q1, n_p2 = p2, n_q2 = q2;
+    if (KIND == 1) {
+        const int a2 = (a + 1) >> 1;
+        n_p1 = csel(hev, p1, s2u(P1 + a2));
+        n_q1 = csel(hev, q1, s2u(Q1 - a2));
+    } else if (KIND == 2) {
+        const int w = c8(c8(P1 - Q1) + 3 * (Q0 - P0));
+        const int a27 = c8((27 * w + 63) >> 7), a18 = c8((18 * w + 63) >> 7), a9 = c8((9 * w + 63) >> 7);
+        n_p0 = csel(hev, n_p0, s2u(P0 + a27));
+        n_q0 = csel(hev, n_q0, s2u(Q0 - a27));
+        n_p1 = csel(hev, p1, s2u(P1 + a18));
+        n_q1 = csel(hev, q1, s2u(Q1 - a18));
+        n_p2 = csel(hev, p2, s2u(u2s(p2) + a9));
+        n_q2 = csel(hev, q2, s2u(u2s(q2) - a9));
+    }
+    p0 = csel(on, n_p0, p0);
+    q0 = csel(on, n_q0, q0);
+    if (KIND != 0) {
+        p1 = csel(on, n_p1, p1);
+        q1 = csel(on, n_q1, q1);
+    }
+    if (KIND == 2) {
+        p2 = csel(on, n_p2, p2);
+        q2 = csel(on, n_q2, q2);
     }
 }
-__device__ void lf_mb(int ht, int il, int el, uint8_t* p, int s)
+
+// The edges of one line in the reference's order: v[i] is the pixel at offset
+// i - 4 from the MB origin along the line (the 4 before it belong to the
+// left / upper neighbour).  The MB edge sits at 4, the inner edges at 8, 12, 16
+// (chroma: 8 only, en12 false).
+template <bool SIMPLE>
+__device__ __forceinline__ void lf_line(int* v, bool en_mb, bool en_in, bool en12, int ht, int il, int mbe, int sube)
 {
-    if (lf_should(il, el, p, s)) {
-        if (!lf_hev(ht, p, s)) {
-            const int p2 = u2s(p[-3 * s]), p1 = u2s(p[-2 * s]), p0 = u2s(p[-s]);
-            const int q0 = u2s(p[0]), q1 = u2s(p[s]), q2 = u2s(p[2 * s]);
-            const int w = c8(c8(p1 - q1) + 3 * (q0 - p0));
-            int a = c8((27 * w + 63) >> 7);
-            p[0] = s2u(q0 - a);
-            p[-s] = s2u(p0 + a);
-            a = c8((18 * w + 63) >> 7);
-            p[s] = s2u(q1 - a);
-            p[-2 * s] = s2u(p1 + a);
-            a = c8((9 * w + 63) >> 7);
-            p[2 * s] = s2u(q2 - a);
-            p[-3 * s] = s2u(p2 + a);
-        } else {
-            lf_common(1, p, s);
-        }
+    if (SIMPLE) {
+        lf_edge<0>(en_mb, ht, il, mbe, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+#pragma unroll
+        for (int e = 8; e <= 16; e += 4)
+            lf_edge<0>(en_in && (e == 8 || en12), ht, il, sube, v[e - 4], v[e - 3], v[e - 2], v[e - 1], v[e], v[e + 1],
+                       v[e + 2], v[e + 3]);
+    } else {
+        lf_edge<2>(en_mb, ht, il, mbe, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+#pragma unroll
+        for (int e = 8; e <= 16; e += 4)
+            lf_edge<1>(en_in && (e == 8 || en12), ht, il, sube, v[e - 4], v[e - 3], v[e - 2], v[e - 1], v[e], v[e + 1],
+                       v[e + 2], v[e + 3]);
     }
 }
 
@@ -166,7 +182,63 @@ __device__ void lf_mb(int ht, int il, int el, uint8_t* p, int s)
 struct LfLds {
     uint8_t y[LFY * LFY];
     uint8_t u[LFC * LFC], v[LFC * LFC];
+    uint8_t pad[8];  // the last chroma row's 5-word read stays inside the tile
 };
+
+// The filtering of one staged tile by 32 lanes (hl = lane in the group):
+// lines 0..15 luma, 16..23 U, 24..31 V.  Phase A: the vertical edges (left MB
+// edge, then x = 4, 8, 12), one row per lane; phase B: the horizontal edges
+// (top MB edge, then y = 4, 8, 12), one column per lane.  en: this group filters
+// (lanes with en false run the same code on a valid line and store nothing).
+__device__ __forceinline__ void lf_filter_tile(LfLds* L, int hl, bool en, bool simple, bool chroma, bool left_edge,
+                                               bool top_edge, bool inner, int ht, int il, int mbe, int sube)
+{
+    const bool isy = hl < 16, isu = hl >= 16 && hl < 24;
+    const bool act = en && (isy || chroma);
+    const int li = isy ? hl : (hl - 16) & 7;
+    uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
+    const int W_ = isy ? LFY : LFC;
+    {
+        uint32_t* row = (uint32_t*)(buf + (li + 4) * W_);
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = row[k];  // (chroma: words 3-4 are the next row's, never filtered)
+        int v[20];
+#pragma unroll
+        for (int k = 0; k < 20; k++) v[k] = (int)((w[k >> 2] >> (8 * (k & 3))) & 255u);
+        if (simple) lf_line<true>(v, act && left_edge, act && inner, isy, ht, il, mbe, sube);
+        else lf_line<false>(v, act && left_edge, act && inner, isy, ht, il, mbe, sube);
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            w[k] = (uint32_t)v[4 * k] | ((uint32_t)v[4 * k + 1] << 8) | ((uint32_t)v[4 * k + 2] << 16) |
+                   ((uint32_t)v[4 * k + 3] << 24);
+        if (act) {
+            row[0] = w[0];
+            row[1] = w[1];
+            row[2] = w[2];
+            if (isy) {
+                row[3] = w[3];
+                row[4] = w[4];
+            }
+        }
+    }
+    wsync();
+    {
+        uint8_t* col = buf + 4 + li;
+        const int kmax = isy ? 19 : 11;
+        int v[20];
+#pragma unroll
+        for (int k = 0; k < 20; k++) v[k] = col[min(k, kmax) * W_];
+        if (simple) lf_line<true>(v, act && top_edge, act && inner, isy, ht, il, mbe, sube);
+        else lf_line<false>(v, act && top_edge, act && inner, isy, ht, il, mbe, sube);
+        if (act) {
+#pragma unroll
+            for (int k = 1; k <= 17; k++)
+                if (k <= 9 || isy) col[k * W_] = (uint8_t)v[k];
+        }
+    }
+    wsync();
+}
 
 // Filter one MB (filter_row_in_cache's per-MB edge order, decoder/vp8.rs:1172-1345)
 // on its LDS tile and write the tile back.  The lane holds the MB's interior
@@ -189,10 +261,15 @@ __device__ __forceinline__ void st_sc1(uint8_t* p, uint32_t v)
 }
 // pub() runs once the rows the MB row below reads (luma 12..15, chroma 4..7 of
 // this tile) are stored; the rest of the write-back follows it.
+// !XCU: those rows go to the workgroup's LDS hand-off rows hy / hu / hv (4 rows
+// each, plane-wide) instead of global memory, and the row below writes them
+// out as its rows -4..-1 (always, filtered or not); only the frame's last MB row
+// (last) stores its own rows 12..15.  So no two waves store the same bytes.
 template <bool XCU, class PUB>
 __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
                                         uint8_t* Vf, int ys, int cs, int mbx, int mby, int i4, int seg, int skip,
-                                        int nzd, uint32_t cy, uint32_t cc, bool write_interior_always, PUB&& pub)
+                                        int nzd, uint32_t cy, uint32_t cc, uint8_t* hy, uint8_t* hu, uint8_t* hv,
+                                        bool last, PUB&& pub)
 {
     auto ld = [](const uint8_t* p) -> uint32_t { return XCU ? ld_sc1(p) : *(const uint32_t*)p; };
     auto st = [](uint8_t* p, uint32_t v) {
@@ -221,83 +298,131 @@ __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams
     if (mby > 0) {  // the 4 rows above: luma lanes 0..15 (row lane>>2), chroma lanes 32..47
         if (lane < 16) {
             const int r = lane >> 2, w = lane & 3;
-            ((uint32_t*)(L->y + r * LFY + 4))[w] = ld(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w);
+            ((uint32_t*)(L->y + r * LFY + 4))[w] =
+                XCU ? ld(Yf + (size_t)(y0 - 4 + r) * ys + x0 + 4 * w) : *(const uint32_t*)(hy + r * ys + x0 + 4 * w);
         } else if (chroma && lane >= 32 && lane < 48) {
             const int t = lane - 32, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
             ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] =
-                ld((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w);
+                XCU ? ld((pl ? Vf : Uf) + (size_t)(mby * 8 - 4 + r) * cs + mbx * 8 + 4 * w)
+                    : *(const uint32_t*)((pl ? hv : hu) + r * cs + mbx * 8 + 4 * w);
         }
     }
     wsync();
-    if (lvl != 0) {
-        const int mbe = (lvl + 2) * 2 + il, sube = lvl * 2 + il;
-        const int inner = i4 || (!skip && nzd);
-        // lane roles: 0..15 luma line, 16..23 U line, 24..31 V line
-        const bool isy = lane < 16, isu = lane >= 16 && lane < 24, isv = lane >= 24 && lane < 32;
-        const int li = isy ? lane : (lane - 16) & 7;
-        uint8_t* buf = isy ? L->y : (isu ? L->u : L->v);
-        const int W_ = isy ? LFY : LFC;
-        const bool act = isy || (chroma && (isu || isv));
-        // left MB edge (vertical edge, filter along rows)
-        if (mbx > 0 && act) {
-            uint8_t* p = buf + (li + 4) * W_ + 4;
-            if (F.filter_type) lf_simple(mbe, p, 1);
-            else lf_mb(ht, il, mbe, p, 1);
-        }
-        wsync();
-        if (inner) {
-            for (int x = 4; x < 16; x += 4) {
-                if (isy) {
-                    uint8_t* p = buf + (li + 4) * W_ + 4 + x;
-                    if (F.filter_type) lf_simple(sube, p, 1);
-                    else lf_inner(ht, il, sube, p, 1);
-                } else if (act && x == 4) {
-                    lf_inner(ht, il, sube, buf + (li + 4) * W_ + 4 + 4, 1);
+    if (lvl != 0)
+        lf_filter_tile(L, lane & 31, lane < 32, F.filter_type != 0, chroma, mbx > 0, mby > 0, i4 || (!skip && nzd), ht, il,
+                       (lvl + 2) * 2 + il, lvl * 2 + il);
+    const bool wb = lvl != 0;
+    auto tile_y = [&](int r, int w) { return ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]; };
+    auto tile_c = [&](int pl, int r, int w) { return ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]; };
+    if (XCU) {
+        // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame);
+        // part 0: the rows the MB row below reads, part 1: the others
+        for (int part = 0; part < 2; part++) {
+            if (wb) {
+                for (int t = lane; t < LFY * 5; t += 64) {
+                    const int r = t / 5 - 4, w = t % 5 - 1;
+                    if ((r >= 12) == (part == 0) && y0 + r >= 0 && x0 + 4 * w >= 0)
+                        st(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w, tile_y(r, w));
                 }
-                wsync();
-            }
-        }
-        if (mby > 0 && act) {
-            uint8_t* p = buf + 4 * W_ + 4 + li;
-            if (F.filter_type) lf_simple(mbe, p, W_);
-            else lf_mb(ht, il, mbe, p, W_);
-        }
-        wsync();
-        if (inner) {
-            for (int y = 4; y < 16; y += 4) {
-                if (isy) {
-                    uint8_t* p = buf + (4 + y) * W_ + 4 + li;
-                    if (F.filter_type) lf_simple(sube, p, W_);
-                    else lf_inner(ht, il, sube, p, W_);
-                } else if (act && y == 4) {
-                    lf_inner(ht, il, sube, buf + (4 + 4) * W_ + 4 + li, W_);
-                }
-                wsync();
-            }
-        }
-    }
-    const bool wb = lvl != 0 || write_interior_always;
-    // write back: luma 20 rows x 5 words, chroma 2 x 12 rows x 3 words (inside the frame);
-    // part 0: the rows the MB row below reads, part 1: the others
-    for (int part = 0; part < 2; part++) {
-        if (wb) {
-            for (int t = lane; t < LFY * 5; t += 64) {
-                const int r = t / 5 - 4, w = t % 5 - 1;
-                if ((r >= 12) == (part == 0) && y0 + r >= 0 && x0 + 4 * w >= 0)
-                    st(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w, ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]);
-            }
-            if (chroma) {  // (the simple filter leaves chroma alone: the caller stores it)
-                for (int t = lane; t < 2 * LFC * 3; t += 64) {
-                    const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
-                    if ((r >= 4) == (part == 0) && mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
-                        st((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w,
-                           ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]);
+                if (chroma) {  // (the simple filter leaves chroma alone)
+                    for (int t = lane; t < 2 * LFC * 3; t += 64) {
+                        const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+                        if ((r >= 4) == (part == 0) && mby * 8 + r >= 0 && mbx * 8 + 4 * w >= 0)
+                            st((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w, tile_c(pl, r, w));
+                    }
                 }
             }
+            if (part == 0) pub();
         }
-        if (part == 0) pub();
+    } else {
+        // hand-off rows (luma rows 12..15, chroma 4..7 with the carried columns), then publish
+        if (lane < 20) {
+            const int r = 12 + lane / 5, w = lane % 5 - 1;
+            if (x0 + 4 * w >= 0) *(uint32_t*)(hy + (r - 12) * ys + x0 + 4 * w) = tile_y(r, w);
+        } else if (chroma && lane >= 32 && lane < 56) {
+            const int t = lane - 32, pl = t / 12, rr = t % 12, r = 4 + rr / 3, w = rr % 3 - 1;
+            if (mbx * 8 + 4 * w >= 0) *(uint32_t*)((pl ? hv : hu) + (r - 4) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
+        }
+        pub();
+        // global: rows -4..-1 always (the row above left them to this row), rows 0..11 when
+        // filtered, rows 12..15 when filtered in the last MB row
+        for (int t = lane; t < LFY * 5; t += 64) {
+            const int r = t / 5 - 4, w = t % 5 - 1;
+            const bool need = r < 0 ? mby > 0 : (wb && (r < 12 || last));
+            if (need && x0 + 4 * w >= 0) st(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w, tile_y(r, w));
+        }
+        if (chroma) {
+            for (int t = lane; t < 2 * LFC * 3; t += 64) {
+                const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+                const bool need = r < 0 ? mby > 0 : (wb && (r < 4 || last));
+                if (need && mbx * 8 + 4 * w >= 0)
+                    st((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w, tile_c(pl, r, w));
+            }
+        }
     }
     wsync();
+}
+
+// idct16_exact (zw_dev.h; transform_simd_intrinsics.rs:478, exact i16
+// semantics) in quad form: lane q of the quad holds column q of the block
+// (x_r = element (r, q)) and gets row q of the result.  The column pass runs in
+// the lane; the transpose is the quad's i16 pairs broadcast by DPP.
+DI void idct_quad_exact(int x0, int x1, int x2, int x3, int q, int o[4])
+{
+    x0 = sat16(x0);
+    x1 = sat16(x1);
+    x2 = sat16(x2);
+    x3 = sat16(x3);
+    const int a = w16(x0 + x2), bb = w16(x0 - x2);
+    const int c = w16(w16(x1 - x3) + w16(mulhi16(x1, -30068) - mulhi16(x3, 20091)));
+    const int d = w16(w16(x1 + x3) + w16(mulhi16(x1, 20091) + mulhi16(x3, -30068)));
+    // rows 0, 1 of column q in lo, rows 2, 3 in hi (pack_lo keeps the low 16 bits: the i16 wrap)
+    const uint32_t lo = pack_lo(a + d, bb + c), hi = pack_lo(bb - c, a - d);
+    const bool upper = q >= 2;
+    const uint32_t off = 16u * (uint32_t)(q & 1);
+    // (csel, not ?: -- a select of two DPP results may be folded into one DPP of a select)
+    const int y0 = __builtin_amdgcn_sbfe(csel(upper, qb0((int)hi), qb0((int)lo)), off, 16);
+    const int y1 = __builtin_amdgcn_sbfe(csel(upper, qb1((int)hi), qb1((int)lo)), off, 16);
+    const int y2 = __builtin_amdgcn_sbfe(csel(upper, qb2((int)hi), qb2((int)lo)), off, 16);
+    const int y3 = __builtin_amdgcn_sbfe(csel(upper, qb3((int)hi), qb3((int)lo)), off, 16);
+    const int dc = w16(y0 + 4);
+    const int A = w16(dc + y2), B = w16(dc - y2);
+    const int C = w16(w16(y1 - y3) + w16(mulhi16(y1, -30068) - mulhi16(y3, 20091)));
+    const int D = w16(w16(y1 + y3) + w16(mulhi16(y1, 20091) + mulhi16(y3, -30068)));
+    o[0] = w16(A + D) >> 3;
+    o[1] = w16(B + C) >> 3;
+    o[2] = w16(B - C) >> 3;
+    o[3] = w16(A - D) >> 3;
+}
+
+// Row q of a 4x4 block: residual (full iDCT when the block's token run was
+// non-empty, else the DC-only (c0 + 4) >> 3, vp8.rs:1110-1117) plus the
+// prediction of mode m (0 DC, 1 V, 2 H, 3 TM; predict_* prediction.rs:164-324)
+// from the top word T (the 4 pixels above the block's columns), the left pixel
+// L of this row, the corner P and the DC value; returns the 4 pixels as a word.
+DI uint32_t recon_row_quad(const int x[4], int q, bool nz, int c0, int m, uint32_t T, int L, int P, int dcv)
+{
+    int o[4];
+    idct_quad_exact(x[0], x[1], x[2], x[3], q, o);
+    const int d = (c0 + 4) >> 3;
+    const uint32_t R01 = nz ? pack_lo(o[0], o[1]) : pack_lo(d, d);
+    const uint32_t R32 = nz ? pack_lo(o[3], o[2]) : pack_lo(d, d);
+    const uint32_t t01 = __builtin_amdgcn_perm(0u, T, 0x0c010c00u), t32 = __builtin_amdgcn_perm(0u, T, 0x0c020c03u);
+    uint32_t p01, p32;
+    if (m == 0) {
+        p01 = p32 = (uint32_t)dcv * 0x10001u;
+    } else if (m == 1) {
+        p01 = t01;
+        p32 = t32;
+    } else if (m == 2) {
+        p01 = p32 = (uint32_t)L * 0x10001u;
+    } else {
+        const uint32_t dd = ((uint32_t)(L - P) & 0xffffu) * 0x10001u;
+        p01 = clamp_pk(add_pk(t01, dd));
+        p32 = clamp_pk(add_pk(t32, dd));
+    }
+    const uint32_t r01 = clamp_pk(add_pk(R01, p01)), r32 = clamp_pk(add_pk(R32, p32));
+    return __builtin_amdgcn_perm(r32, r01, 0x04060200u);
 }
 
 // One MB row of the reconstruction (shared by the one-workgroup-per-frame
@@ -306,16 +431,25 @@ __device__ __forceinline__ void lf_tile(LfLds* L, int lane, const ZwFilterParams
 // run on another CU / XCD, so its bottom pixels are exchanged through the
 // global border rows gty/gtu/gtv with sc1 stores and loads; otherwise
 // gty/gtu/gtv are the workgroup's LDS border rows.
-template <bool FUSE, bool XCU, class WAIT, class PUB>
+//
+// Lane layout (I16 luma, chroma): lane = 4 b + q, block b, pixel row q of the
+// block; the lane's row is one word of the plane.  The borders come straight
+// from the top row (words) and the left column; only I4 MBs, whose
+// sub-blocks chain through their own reconstruction, build the LDS work area
+// ws and run the 16 sub-blocks in turn.
+template <bool XCU, class WAIT, class PUB>
 __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuant* __restrict__ quant, uint8_t* Y,
-                                              uint8_t* U, uint8_t* V, uint8_t* flags,
-                                              const ZwFilterParams* __restrict__ fp, int f, int mbw, int mbh,
-                                              size_t ysz, size_t csz, int mby, DecLds* W, LfLds* LF, uint8_t* gty,
-                                              uint8_t* gtu, uint8_t* gtv, WAIT&& wait, PUB&& pub)
+                                              uint8_t* U, uint8_t* V, uint8_t* flags, int f, int mbw, int mbh,
+                                              size_t ysz, size_t csz, int mby, DecLds* W, uint8_t* gty, uint8_t* gtu,
+                                              uint8_t* gtv, WAIT&& wait, PUB&& pub)
 {
     const int lane = threadIdx.x & 63;
     const int ys = mbw * 16, cs = mbw * 8;
     const size_t nmb = (size_t)mbw * mbh;
+    const int b = lane >> 2, q = lane & 3, bx = b & 3, by = b >> 2;
+    // chroma: lanes 0..31 (lanes 32..63 mirror them and store nothing)
+    const int pl = (lane >> 4) & 1, cb = (lane >> 2) & 3, cbx = cb & 1, cby = cb >> 1;
+    const bool above = mby != 0;
     if (lane < 20) W->left_y[lane] = 129;
     if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
     wsync();
@@ -330,205 +464,141 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
             else if (lane < 10) W->twu[lane - 8] = ld_sc1(gtu + mbx * 8 + 4 * (lane - 8));
             else if (lane < 12) W->twv[lane - 10] = ld_sc1(gtv + mbx * 8 + 4 * (lane - 10));
         }
-        const uint8_t* top_y = XCU ? (const uint8_t*)W->twy - mbx * 16 : gty;
-        const uint8_t* top_u = XCU ? (const uint8_t*)W->twu - mbx * 8 : gtu;
-        const uint8_t* top_v = XCU ? (const uint8_t*)W->twv - mbx * 8 : gtv;
+        const uint8_t* top_y = XCU ? (const uint8_t*)W->twy : gty + mbx * 16;
+        const uint8_t* top_u = XCU ? (const uint8_t*)W->twu : gtu + mbx * 8;
+        const uint8_t* top_v = XCU ? (const uint8_t*)W->twv : gtv + mbx * 8;
         if (lane < 52) W->rec[lane] = cur;
         wsync();
         const ZwDecMb& M = *(const ZwDecMb*)W->rec;
-        const ZwDecQuant& Q = quant[(XCU ? 0 : (size_t)f * 4) + M.segment];  // XCU: quant is the frame's LDS copy
-        const int lm = M.luma_mode;
-        // --- luma border (create_border_luma) ---
-        uint8_t* ws = W->ws;
-        if (lane < 32) {
-            int v;
-            if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
-            else if (mby == 0) v = 127;
-            else if (lane <= 16) v = top_y[mbx * 16 + lane - 1];
-            else if (mbx == mbw - 1) v = top_y[mbx * 16 + 15];
-            else v = top_y[mbx * 16 + lane - 1];
-            ws[lane] = (uint8_t)v;
-            if (lane >= 17 && lane < 21) ws[4 * ZW_BPS + lane] = ws[8 * ZW_BPS + lane] = ws[12 * ZW_BPS + lane] = (uint8_t)v;
-        } else if (lane < 48) {
-            ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
-        }
-        wsync();
-        int nzdct = 0;
+        const int seg = __builtin_amdgcn_readfirstlane(M.segment);
+        const ZwDecQuant& Q = quant[(XCU ? 0 : (size_t)f * 4) + seg];  // XCU: quant is the frame's LDS copy
+        const int lm = __builtin_amdgcn_readfirstlane(M.luma_mode);
+        const uint32_t nzm = (uint32_t)__builtin_amdgcn_readfirstlane((int)M.nz_mask);
+        const bool left = mbx != 0;
+        // ---- luma ----
+        const uint32_t TW = above ? ((const uint32_t*)top_y)[bx] : 0x7f7f7f7fu;
+        const int corner_y = (int)((uint32_t)__builtin_amdgcn_readlane((int)TW, 12) >> 24);  // top pixel 15: the next MB's corner
+        uint32_t RW;
+        int nzdct;
         if (lm != 4) {
-            // Y2 in group form: lane b holds block b's DC after the iWHT (zero when skipped)
-            const int b = lane & 15, bx = b & 3, by = b >> 2;
-            const int y2v = M.skip ? 0 : (int)M.y2[b] * (b ? Q.y2ac : Q.y2dc);
-            const int dcb = iwht_g(y2v, b);
-            // DC predictor sum: lanes 0..15 top row, 16..31 left column
-            const int above = mby != 0, left = mbx != 0;
-            int dcv;
-            {
-                const int top = lane < 16;
-                const int v = (int)ws[csel(top, 1 + b, (b + 1) * ZW_BPS)] & -(int)(lane < 32 && (top ? above : left));
-                const int sum = red16(v);
-                const int su = __builtin_amdgcn_readlane(sum, 0) + __builtin_amdgcn_readlane(sum, 16);
-                const int shf = 3 + above + left;
-                dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
-            }
-            int blocknz = 0;
-            if (lane < 16) {
-                int c[16];
-                c[0] = dcb;
+            // Y2 in group form (lane k = block k's DC after the iWHT), moved to the quads
+            const int k = lane & 15;
+            const int y2v = M.skip ? 0 : (int)M.y2[k] * (k ? Q.y2ac : Q.y2dc);
+            const int dcb = iwht_g(y2v, k);
+            const int dc = __builtin_amdgcn_ds_bpermute(4 * b, dcb);
+            const int16_t* cf = M.coeffs[b];
+            int x[4];
 #pragma unroll
-                for (int k = 1; k < 16; k++) c[k] = (int)M.coeffs[b][k] * Q.yac;
-                const int nz = (M.nz_mask >> b) & 1;
-                blocknz = (c[0] != 0) || nz;
-                dec_block_residual(c, nz);
-                const int P0 = ws[0];
-                int px[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
-                    const int L = ws[(y + 1) * ZW_BPS], T = ws[1 + x];
-                    const int p = lm == 0 ? dcv : (lm == 1 ? T : (lm == 2 ? L : clamp255(L + T - P0)));
-                    px[k] = clamp255(p + c[k]);
-                }
-                wsync();
-#pragma unroll
-                for (int k = 0; k < 16; k++) ws[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
-            } else {
-                wsync();
-            }
-            nzdct |= __any(blocknz) ? 1 : 0;
-            wsync();
+            for (int r = 0; r < 4; r++) x[r] = (int)cf[4 * r + q] * Q.yac;
+            x[0] = csel(q == 0, dc, x[0]);
+            const int L = left ? (int)W->left_y[1 + 4 * by + q] : 129;
+            const int P = above ? (left ? (int)W->left_y[0] : 129) : 127;
+            // DC predictor: the top row (lanes of blocks 0..3, q = 0) and the left column (bx = 0)
+            int sv = (above && b < 4 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TW, 0u, 0u) : 0) + (left && bx == 0 ? L : 0);
+            sv = red16(sv);
+            const int su = __builtin_amdgcn_readlane(sv, 0) + __builtin_amdgcn_readlane(sv, 16) +
+                           __builtin_amdgcn_readlane(sv, 32) + __builtin_amdgcn_readlane(sv, 48);
+            const int shf = 3 + above + left;
+            const int dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
+            const bool nz = (nzm >> b) & 1u;
+            RW = recon_row_quad(x, q, nz, dc, lm, TW, L, P, dcv);
+            nzdct = __any(dc != 0 || nz) ? 1 : 0;
         } else {
+            // --- luma border (create_border_luma) in ws, then the 16 sub-blocks ---
+            uint8_t* ws = W->ws;
+            const uint8_t* ty = top_y - mbx * 16;
+            if (lane < 32) {
+                int v;
+                if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
+                else if (mby == 0) v = 127;
+                else if (lane <= 16) v = ty[mbx * 16 + lane - 1];
+                else if (mbx == mbw - 1) v = ty[mbx * 16 + 15];
+                else v = ty[mbx * 16 + lane - 1];
+                ws[lane] = (uint8_t)v;
+                if (lane >= 17 && lane < 21) ws[4 * ZW_BPS + lane] = ws[8 * ZW_BPS + lane] = ws[12 * ZW_BPS + lane] = (uint8_t)v;
+            } else if (lane < 48) {
+                ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
+            }
+            wsync();
             // group form: lane k = coefficient k of the sub-block (all four groups alike)
             const int k = lane & 15;
+            int nzd = 0;
             for (int i = 0; i < 16; i++) {
                 const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
                 dec_i4_values(W, lane, x0, y0);
                 const int c = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
-                const int nz = (M.nz_mask >> i) & 1;
+                const int nz = (nzm >> i) & 1;
                 const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
                 const int full = idct_g_exact(c, k);
                 const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
-                nzdct |= nz || c0 != 0;
+                nzd |= nz || c0 != 0;
                 const int v = clamp255(dec_i4_px(W, M.bpred[i], k) + r);
                 if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
                 wsync();
             }
+            nzdct = nzd;
+            const uint8_t* pr = ws + (4 * by + q + 1) * ZW_BPS + 1 + 4 * bx;
+            RW = (uint32_t)pr[0] | ((uint32_t)pr[1] << 8) | ((uint32_t)pr[2] << 16) | ((uint32_t)pr[3] << 24);
         }
-        // --- chroma ---
-        if (lane < 34) {  // per plane: corner, 8 top, 8 left
-            const int pl = lane >= 17;
-            const int i = pl ? lane - 17 : lane;
-            uint8_t* w = pl ? W->cv : W->cu;
-            const uint8_t* top = pl ? top_v : top_u;
-            const uint8_t* lft = pl ? W->left_v : W->left_u;
-            if (i == 0) w[0] = mby == 0 ? 127 : (mbx == 0 ? 129 : lft[0]);
-            else if (i <= 8) w[i] = mby == 0 ? 127 : top[mbx * 8 + i - 1];
-            else w[(i - 8) * ZW_BPS] = mbx == 0 ? 129 : lft[i - 8];
+        // ---- chroma ----
+        uint32_t RC;
+        {
+            const uint8_t* tc = pl ? top_v : top_u;
+            const uint8_t* lc = pl ? W->left_v : W->left_u;
+            const uint32_t TC = above ? ((const uint32_t*)tc)[cbx] : 0x7f7f7f7fu;
+            const int L = left ? (int)lc[1 + 4 * cby + q] : 129;
+            const int P = above ? (left ? (int)lc[0] : 129) : 127;
+            int sv = (above && cby == 0 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TC, 0u, 0u) : 0) + (left && cbx == 0 ? L : 0);
+            sv = red16(sv);  // the plane's 16-lane group
+            const int shf = 2 + above + left;
+            const int dcv = (above || left) ? ((sv + (1 << (shf - 1))) >> shf) : 128;
+            const int cbk = 16 + 4 * pl + cb;
+            const int16_t* cf = M.coeffs[cbk];
+            int x[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) x[r] = (int)cf[4 * r + q] * (r == 0 && q == 0 ? Q.uvdc : Q.uvac);
+            const int c0 = qb0(x[0]);
+            const bool nz = (nzm >> cbk) & 1u;
+            const int cm = __builtin_amdgcn_readfirstlane(M.chroma_mode);
+            RC = recon_row_quad(x, q, nz, c0, cm, TC, L, P, dcv);
+            nzdct |= __any(lane < 32 && (c0 != 0 || nz)) ? 1 : 0;
+        }
+        const int corner_u = (int)((uint32_t)__builtin_amdgcn_readlane(above ? (int)((const uint32_t*)top_u)[1] : 0x7f7f7f7f, 0) >> 24);
+        const int corner_v = (int)((uint32_t)__builtin_amdgcn_readlane(above ? (int)((const uint32_t*)top_v)[1] : 0x7f7f7f7f, 0) >> 24);
+        wsync();
+        // ---- borders for the next MB and the row below, output ----
+        if (bx == 3) W->left_y[1 + 4 * by + q] = (uint8_t)(RW >> 24);
+        if (lane == 0) {
+            W->left_y[0] = (uint8_t)corner_y;
+            W->left_u[0] = (uint8_t)corner_u;
+            W->left_v[0] = (uint8_t)corner_v;
+        }
+        if (lane < 32 && cbx == 1) (pl ? W->left_v : W->left_u)[1 + 4 * cby + q] = (uint8_t)(RC >> 24);
+        uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
+        uint8_t* co = (pl ? V : U) + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
+        if (XCU) {  // bottom rows for the row below (sc1), then publish, then the planes
+            if (by == 3 && q == 3) st_sc1(gty + mbx * 16 + 4 * bx, RW);
+            if (lane < 32 && cby == 1 && q == 3) st_sc1((pl ? gtv : gtu) + mbx * 8 + 4 * cbx, RC);
+            pub(mbx + 1);  // the row below needs only the border: publish before the plane stores
+        } else {  // LDS border rows; the publish waits for LDS only, not for the plane stores
+            if (by == 3 && q == 3) *(uint32_t*)(gty + mbx * 16 + 4 * bx) = RW;
+            if (lane < 32 && cby == 1 && q == 3) *(uint32_t*)((pl ? gtv : gtu) + mbx * 8 + 4 * cbx) = RC;
+            pub(mbx + 1);
+        }
+        *(uint32_t*)(yo + (size_t)(4 * by + q) * ys + 4 * bx) = RW;
+        if (lane < 32) *(uint32_t*)(co + (size_t)(4 * cby + q) * cs + 4 * cbx) = RC;
+        if (lane < 4) {
+            const int v = lane == 0 ? lm : (lane == 1 ? seg : (lane == 2 ? (int)M.skip : nzdct));
+            flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
         }
         wsync();
-        {
-            int blocknz = 0;
-            int px[16];
-            const int b = lane & 7, pl = b >= 4, bb = b & 3, bx = bb & 1, by = bb >> 1;
-            uint8_t* w = pl ? W->cv : W->cu;
-            if (lane < 8) {
-                const int cm = M.chroma_mode;
-                const int above = mby != 0, left = mbx != 0;
-                int dcv = 128;
-                {
-                    uint32_t s = 0;
-                    int shf = 2;
-                    if (left) {
-                        for (int y = 0; y < 8; y++) s += w[(y + 1) * ZW_BPS];
-                        shf++;
-                    }
-                    if (above) {
-                        for (int x = 1; x <= 8; x++) s += w[x];
-                        shf++;
-                    }
-                    if (above || left) dcv = (int)((s + (1u << (shf - 1))) >> shf);
-                }
-                int c[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) c[k] = (int)M.coeffs[16 + b][k] * (k ? Q.uvac : Q.uvdc);
-                const int nz = (M.nz_mask >> (16 + b)) & 1;
-                blocknz = (c[0] != 0) || nz;
-                dec_block_residual(c, nz);
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
-                    const int L = w[(y + 1) * ZW_BPS], T = w[1 + x];
-                    const int p = cm == 0 ? dcv : (cm == 1 ? T : (cm == 2 ? L : clamp255(L + T - w[0])));
-                    px[k] = clamp255(p + c[k]);
-                }
-            }
-            wsync();
-            if (lane < 8) {
-#pragma unroll
-                for (int k = 0; k < 16; k++) w[(by * 4 + (k >> 2) + 1) * ZW_BPS + 1 + bx * 4 + (k & 3)] = (uint8_t)px[k];
-            }
-            nzdct |= __any(blocknz) ? 1 : 0;
-            wsync();
-        }
-        // --- borders, output ---
-        if (lane < 17) W->left_y[lane] = ws[lane * ZW_BPS + 16];
-        else if (!XCU && lane < 33) gty[mbx * 16 + lane - 17] = ws[16 * ZW_BPS + lane - 17 + 1];
-        if (lane < 9) {
-            W->left_u[lane] = W->cu[lane * ZW_BPS + 8];
-            W->left_v[lane] = W->cv[lane * ZW_BPS + 8];
-        } else if (!XCU && lane >= 40 && lane < 48) {
-            gtu[mbx * 8 + lane - 40] = W->cu[8 * ZW_BPS + lane - 40 + 1];
-            gtv[mbx * 8 + lane - 40] = W->cv[8 * ZW_BPS + lane - 40 + 1];
-        }
-        if (XCU && lane >= 48 && lane < 56) {  // bottom row for the row below: 4 + 2 + 2 words, sc1
-            const int t = lane - 48;
-            const uint8_t* src =
-                t < 4 ? ws + 16 * ZW_BPS + 1 + 4 * t : (t < 6 ? W->cu : W->cv) + 8 * ZW_BPS + 1 + 4 * (t & 1);
-            const uint32_t w =
-                (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
-            st_sc1(t < 4 ? gty + mbx * 16 + 4 * t : (t < 6 ? gtu : gtv) + mbx * 8 + 4 * (t & 1), w);
-        }
-        if (XCU) pub(mbx + 1);  // the row below needs only the border: publish before the plane stores
-        uint8_t* uo = U + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
-        uint8_t* vo = V + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
-        if (FUSE) {
-            const ZwFilterParams& F = fp[f];
-            // interior words: luma row lane>>2 word lane&3; chroma plane lane>>4, row (lane>>1)&7, word lane&1
-            const int iy_r = lane >> 2, iy_w = lane & 3;
-            const uint8_t* py = ws + (iy_r + 1) * ZW_BPS + 1 + 4 * iy_w;
-            const uint32_t cy = (uint32_t)py[0] | ((uint32_t)py[1] << 8) | ((uint32_t)py[2] << 16) | ((uint32_t)py[3] << 24);
-            const uint8_t* pc = ((lane >> 4) & 1 ? W->cv : W->cu) + (((lane >> 1) & 7) + 1) * ZW_BPS + 1 + 4 * (lane & 1);
-            const uint32_t cc = (uint32_t)pc[0] | ((uint32_t)pc[1] << 8) | ((uint32_t)pc[2] << 16) | ((uint32_t)pc[3] << 24);
-            if (F.filter_type) {  // simple filter: chroma is final as reconstructed
-                uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-                vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-            }
-            lf_tile<false>(LF, lane, F, Y + (size_t)f * ysz, U + (size_t)f * csz, V + (size_t)f * csz, ys, cs, mbx, mby,
-                    lm == 4, M.segment, M.skip, nzdct, cy, cc, true, [] {});
-        } else {
-            uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
-            for (int k = lane; k < 256; k += 64) yo[(size_t)(k >> 4) * ys + (k & 15)] = ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
-            uo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cu[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-            vo[(size_t)(lane >> 3) * cs + (lane & 7)] = W->cv[((lane >> 3) + 1) * ZW_BPS + 1 + (lane & 7)];
-            if (lane < 4) {
-                const int v = lane == 0 ? lm : (lane == 1 ? M.segment : (lane == 2 ? M.skip : nzdct));
-                flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
-            }
-            wsync();
-        }
-            if (!XCU) pub(mbx + 1);
-        }
+    }
 }
 
-// FUSE: the loop filter runs in the same wavefront right after each MB's
-// reconstruction (the prediction of later MBs reads the unfiltered borders kept
-// in LDS, vp8.rs:791-797; the filter reads and writes the planes in the same
-// raster-consistent order as k_loopfilter), so a frame pays one wavefront
-// instead of two.
-template <bool FUSE>
 __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
-                                                              size_t csz, const ZwFilterParams* __restrict__ fp)
+                                                              size_t csz)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -542,8 +612,6 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     uint8_t* top_u = smem + off;
     off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
     uint8_t* top_v = smem + off;
-    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
-    LfLds* LF = (LfLds*)(smem + off) + wv;  // FUSE only
     DecLds* W = (DecLds*)((uint8_t*)Wall + ((sizeof(DecLds) + 15) & ~(size_t)15) * wv);
     for (int i = lane; i < 160; i += 64) (&W->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WGD) top_y[i] = 127;
@@ -552,8 +620,8 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     __syncthreads();
     const uint4* recs = (const uint4*)mbs;  // 52 lines per record
     for (int mby = wv; mby < mbh; mby += NWD) {
-        dec_recon_row<FUSE, false>(
-            recs, quant, Y, U, V, flags, fp, f, mbw, mbh, ysz, csz, mby, W, LF, top_y, top_u, top_v,
+        dec_recon_row<false>(
+            recs, quant, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
             [&](int need) { dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + need); },
             [&](int done) { dec_publish(progress, wv, mby * 65536 + done); });
     }
@@ -623,55 +691,142 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const ZwDecMb* __restrict
         const int mby = row_ticket(&rs[0]);
         if (mby >= mbh) break;
         int seen = -1;
-        dec_recon_row<false, true>(
-            (const uint4*)mbs, W->q, Y, U, V, flags, nullptr, f, mbw, mbh, ysz, csz, mby, W, nullptr, gty, gtu, gtv,
+        dec_recon_row<true>(
+            (const uint4*)mbs, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, gty, gtu, gtv,
             [&](int need) { row_wait(&prog[mby - 1], need, &rs[2], seen); },
             [&](int done) { row_publish(&prog[mby], done); });
     }
 }
 
-// Per wave, row by row: the MB's 16x16 / 8x8 interiors only change when the
-// MB itself is filtered, so they are prefetched into registers one MB ahead.
+// One MB of the batch loop filter on one half-wave (hl = lane in the half,
+// 0..31; on: the half has an MB this step).  The tile is assembled from the
+// prefetched interior (luma words hl and hl + 32: row w >> 2, word w & 3;
+// chroma word hl: plane hl >> 4, row (hl >> 1) & 7, word hl & 1), the carried
+// left columns and the LDS hand-off rows above; filtered; its rows 12..15
+// (chroma 4..7) go to the hand-off rows, the rest to the planes (rows -4..-1
+// always: the row above left them to this row; the last MB row also stores its
+// own rows 12..15).  No two waves store the same bytes.
+__device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
+                                        uint8_t* Vf, int ys, int cs, int mbx, int mby, uint32_t fl, uint32_t cy0,
+                                        uint32_t cy1, uint32_t cc, uint8_t* hy, uint8_t* hu, uint8_t* hv, bool last)
+{
+    const bool chroma = !F.filter_type;
+    const int i4 = (fl & 255u) == 4u, seg = (int)((fl >> 8) & 3u), skip = (int)((fl >> 16) & 255u), nzd = (int)(fl >> 24);
+    const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
+    const int x0 = mbx * 16, y0 = mby * 16;
+    // ---- assemble the tile ----
+    if (on && mbx > 0) {  // left 4 columns (rows -4..15) from the previous tile's columns 12..15
+        if (hl < LFY) {
+            uint32_t* row = (uint32_t*)(L->y + hl * LFY);
+            row[0] = row[4];
+        }
+        if (chroma && hl < 2 * LFC) {
+            uint32_t* row = (uint32_t*)((hl >= LFC ? L->v : L->u) + (hl % LFC) * LFC);
+            row[0] = row[2];
+        }
+    }
+    if (on) {
+        ((uint32_t*)(L->y + (4 + (hl >> 2)) * LFY + 4))[hl & 3] = cy0;
+        ((uint32_t*)(L->y + (12 + (hl >> 2)) * LFY + 4))[hl & 3] = cy1;
+        if (chroma) ((uint32_t*)((((hl >> 4) & 1) ? L->v : L->u) + (4 + ((hl >> 1) & 7)) * LFC + 4))[hl & 1] = cc;
+        if (mby > 0) {  // the 4 rows above from the hand-off rows: luma hl < 16, chroma hl >= 16
+            if (hl < 16) {
+                const int r = hl >> 2, w = hl & 3;
+                ((uint32_t*)(L->y + r * LFY + 4))[w] = *(const uint32_t*)(hy + r * ys + x0 + 4 * w);
+            } else if (chroma) {
+                const int t = hl - 16, pl = t >> 3, r = (t >> 1) & 3, w = t & 1;
+                ((uint32_t*)((pl ? L->v : L->u) + r * LFC + 4))[w] = *(const uint32_t*)((pl ? hv : hu) + r * cs + mbx * 8 + 4 * w);
+            }
+        }
+    }
+    wsync();
+    lf_filter_tile(L, hl, on && lvl != 0, F.filter_type != 0, chroma, mbx > 0, mby > 0, i4 || (!skip && nzd), ht, il,
+                   (lvl + 2) * 2 + il, lvl * 2 + il);
+    if (!on) return;
+    auto tile_y = [&](int r, int w) { return ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]; };
+    auto tile_c = [&](int pl, int r, int w) { return ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]; };
+    // hand-off rows: luma rows 12..15 (20 words with the carried columns), chroma 4..7 (24)
+    if (hl < 20) {
+        const int r = 12 + hl / 5, w = hl % 5 - 1;
+        if (x0 + 4 * w >= 0) *(uint32_t*)(hy + (r - 12) * ys + x0 + 4 * w) = tile_y(r, w);
+    }
+    if (chroma && hl < 24) {
+        const int pl = hl / 12, rr = hl % 12, r = 4 + rr / 3, w = rr % 3 - 1;
+        if (mbx * 8 + 4 * w >= 0) *(uint32_t*)((pl ? hv : hu) + (r - 4) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
+    }
+    const bool wb = lvl != 0;
+    for (int t = hl; t < LFY * 5; t += 32) {
+        const int r = t / 5 - 4, w = t % 5 - 1;
+        const bool need = r < 0 ? mby > 0 : (wb && (r < 12 || last));
+        if (need && x0 + 4 * w >= 0) *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = tile_y(r, w);
+    }
+    if (chroma) {
+        for (int t = hl; t < 2 * LFC * 3; t += 32) {
+            const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
+            const bool need = r < 0 ? mby > 0 : (wb && (r < 4 || last));
+            if (need && mbx * 8 + 4 * w >= 0)
+                *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
+        }
+    }
+}
+
+// Batch loop filter: one workgroup per frame, NWD waves; wave wv takes MB-row
+// pairs wv, wv + NWD, ...  A pair runs as one stream of steps: at step s the
+// upper row (lanes 0..31) filters MB s and the lower row (lanes 32..63) MB
+// s - 2 -- the x+2y wavefront inside the wave; the two tiles never overlap.
+// Every lane does useful work, so a frame costs half the instructions and half
+// the serial steps of one row per wave.  The next pair's upper row waits on the
+// lower row's progress.  The rows hand over through LDS (hy/hu/hv: the last
+// filtered MB row's bottom 4 rows, plane-wide).
 extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8_t* U, uint8_t* V,
                                                                const uint8_t* __restrict__ flags,
                                                                const ZwFilterParams* __restrict__ fp, size_t ysz,
                                                                size_t csz)
 {
-    __shared__ __attribute__((aligned(16))) LfLds lds[NWD];
+    __shared__ __attribute__((aligned(16))) LfLds lds[NWD][2];
     __shared__ int progress[NWD];
+    __shared__ ZwFilterParams Fs;
+    extern __shared__ __attribute__((aligned(16))) uint8_t hand[];  // hand-off rows: 4 luma + 2 x 4 chroma
     const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const ZwFilterParams& F = fp[f];
-    const int mbw = F.mbw, mbh = F.mbh, ys = mbw * 16, cs = mbw * 8;
-    const size_t nmb = (size_t)mbw * mbh;
+    const int h = lane >> 5, hl = lane & 31;
+    if (threadIdx.x < sizeof(ZwFilterParams) / 4) ((uint32_t*)&Fs)[threadIdx.x] = ((const uint32_t*)(fp + f))[threadIdx.x];
     if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
     __syncthreads();
-    LfLds* L = &lds[wv];
+    const ZwFilterParams& F = Fs;
+    const int mbw = F.mbw, mbh = F.mbh, ys = mbw * 16, cs = mbw * 8;
+    const size_t nmb = (size_t)mbw * mbh;
+    uint8_t* hy = hand;
+    uint8_t* hu = hand + 4 * ys;
+    uint8_t* hv = hu + 4 * cs;
+    LfLds* L = &lds[wv][h];
     uint8_t* Yf = Y + (size_t)f * ysz;
     uint8_t* Uf = U + (size_t)f * csz;
     uint8_t* Vf = V + (size_t)f * csz;
     const bool chroma = !F.filter_type;
-    const int iy_r = lane >> 2, iy_w = lane & 3;
-    const int ic_p = (lane >> 4) & 1, ic_r = (lane >> 1) & 7, ic_w = lane & 1;
-    auto load_interior = [&](int mby, int mbx, uint32_t& py, uint32_t& pc) {
-        py = *(const uint32_t*)(Yf + (size_t)(mby * 16 + iy_r) * ys + mbx * 16 + 4 * iy_w);
-        pc = 0;
-        if (chroma && lane < 32)
-            pc = *(const uint32_t*)((ic_p ? Vf : Uf) + (size_t)(mby * 8 + ic_r) * cs + mbx * 8 + 4 * ic_w);
+    const uint8_t* fflags = flags + (size_t)f * nmb * 4;
+    auto load = [&](int my, int mx, uint32_t& y0w, uint32_t& y1w, uint32_t& cw, uint32_t& flw) {
+        const uint8_t* yb = Yf + (size_t)(my * 16) * ys + mx * 16 + 4 * (hl & 3);
+        y0w = *(const uint32_t*)(yb + (size_t)(hl >> 2) * ys);
+        y1w = *(const uint32_t*)(yb + (size_t)(8 + (hl >> 2)) * ys);
+        cw = chroma ? *(const uint32_t*)((((hl >> 4) & 1) ? Vf : Uf) + (size_t)(my * 8 + ((hl >> 1) & 7)) * cs + mx * 8 +
+                                         4 * (hl & 1))
+                    : 0u;
+        flw = *(const uint32_t*)(fflags + ((size_t)my * mbw + mx) * 4);
     };
-    for (int mby = wv; mby < mbh; mby += NWD) {
-        uint32_t ny, nc;
-        load_interior(mby, 0, ny, nc);
-        uint32_t nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw) * 4);
-        for (int mbx = 0; mbx < mbw; mbx++) {
-            const uint32_t cy = ny, cc = nc, fl = nfl;
-            if (mbx + 1 < mbw) {
-                load_interior(mby, mbx + 1, ny, nc);
-                nfl = *(const uint32_t*)(flags + ((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 4);
-            }
-            if (mby > 0) dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + min(mbx + 2, mbw));
-            lf_tile<false>(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255,
-                           (fl >> 16) & 255, fl >> 24, cy, cc, false, [] {});
-            dec_publish(progress, wv, mby * 65536 + mbx + 1);
+    for (int pr = wv; 2 * pr < mbh; pr += NWD) {
+        const int my = 2 * pr + h;  // this half's MB row
+        const bool rowok = my < mbh;
+        uint32_t ny0 = 0, ny1 = 0, nc = 0, nfl = 0;
+        if (rowok && h == 0) load(my, 0, ny0, ny1, nc, nfl);  // step 0: the lower half starts at step 2
+        for (int st = 0; st < mbw + 2; st++) {
+            const int mx = st - 2 * h;
+            const bool on = rowok && mx >= 0 && mx < mbw;
+            const uint32_t cy0 = ny0, cy1 = ny1, cc = nc, fl = nfl;
+            if (rowok && mx + 1 >= 0 && mx + 1 < mbw) load(my, mx + 1, ny0, ny1, nc, nfl);
+            if (pr > 0 && st < mbw) dec_wait(progress, (pr - 1) % NWD, (pr - 1) * 65536 + min(st + 2, mbw));
+            lf_half(L, hl, on, F, Yf, Uf, Vf, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1);
+            wsync();
+            if (st >= 2) dec_publish(progress, wv, pr * 65536 + st - 1);  // the lower row has finished st - 1 MBs
         }
     }
 }
@@ -718,7 +873,8 @@ __global__ __launch_bounds__(64) void k_loopfilter_rows(uint8_t* Y, uint8_t* U, 
             }
             if (mby > 0) row_wait(&prog[mby - 1], min(mbx + 2, mbw), &rs[2], seen);
             lf_tile<true>(L, lane, F, Yf, Uf, Vf, ys, cs, mbx, mby, (fl & 255) == 4, (fl >> 8) & 255,
-                          (fl >> 16) & 255, fl >> 24, cy, cc, false, [&] { row_publish(&prog[mby], mbx + 1); });
+                          (fl >> 16) & 255, fl >> 24, cy, cc, nullptr, nullptr, nullptr, false,
+                          [&] { row_publish(&prog[mby], mbx + 1); });
         }
     }
 }
@@ -765,7 +921,6 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
     size_t off = ((sizeof(DecLds) + 15) & ~(size_t)15) * NWD + 64;
     off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
     off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
-    off += sizeof(LfLds) * NWD;
     return off;
 }
 
@@ -827,30 +982,30 @@ extern "C" hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const u
     return hipGetLastError();
 }
 
-// fp == nullptr: reconstruction only (k_loopfilter follows); else the fused kernel.
 extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
-                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes,
-                                    const ZwFilterParams* fp)
+                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
 {
     static const bool attr = []() {
-        (void)hipFuncSetAttribute((const void*)k_dec_recon<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_dec_recon<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
-    if (fp)
-        hipLaunchKernelGGL(k_dec_recon<true>, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs,
-                           (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, fp);
-    else
-        hipLaunchKernelGGL(k_dec_recon<false>, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs,
-                           (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, fp);
+    hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs, (const ZwDecQuant*)quant,
+                       Y, U, V, flags, mbw, mbh, ysz, csz);
     return hipGetLastError();
 }
 
+// mbw: the frames' width in MBs (every frame of a launch has the same size)
 extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
-                                     const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes)
+                                     const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw)
 {
-    hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), 0, s, Y, U, V, flags, fp, ysz, csz);
+    static const bool attr = []() {
+        (void)hipFuncSetAttribute((const void*)k_loopfilter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024 - (int)(sizeof(LfLds) * 2 * NWD + 4 * NWD + sizeof(ZwFilterParams)));
+        return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), (size_t)mbw * 128, s, Y, U, V, flags, fp, ysz, csz);
     return hipGetLastError();
 }
 

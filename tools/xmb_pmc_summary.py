@@ -3,7 +3,8 @@
 dispatch of every counter (summed over XCDs), kernel-trace average duration,
 and the HBM traffic per MB (FETCH_SIZE doubled for the wide streaming reads,
 MI355X_MICROARCH.md HBM section; WRITE_SIZE as is; both KiB).
-usage: xmb_pmc_summary.py DIR  ->  JSON on stdout"""
+usage: xmb_pmc_summary.py DIR [KERNEL_SUBSTRING [UNITS]]  ->  JSON on stdout
+(defaults: xform_mb, 256 x 8160 MBs; tools/gpu_pmc_dec.sh passes dec_recon|loopfilter)"""
 import collections
 import csv
 import glob
@@ -12,7 +13,8 @@ import statistics
 import sys
 
 root = sys.argv[1]
-MBS = 256 * 8160  # the xmb_bench launch: 256 1080p frames
+MBS = int(sys.argv[3]) if len(sys.argv) > 3 else 256 * 8160  # the xmb_bench launch: 256 1080p frames
+PATS = (sys.argv[2] if len(sys.argv) > 2 else "xform_mb").split("|")
 
 
 def short(name):
@@ -33,7 +35,7 @@ for f in glob.glob(f"{root}/trace/*kernel_stats.csv"):
         dur[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
 out = {}
 for k, cs in per.items():
-    if "xform_mb" not in k:
+    if not any(p in k for p in PATS):
         continue
     d = {c: statistics.median(v) for c, v in cs.items()}
     e = {"counters_median_per_dispatch": d, "trace": dur.get(k)}
@@ -43,5 +45,6 @@ for k, cs in per.items():
                   "traffic_bytes_per_mb": (rd + wr) / MBS})
     if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
         e["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        e["valu_insts_per_unit"] = d["SQ_INSTS_VALU"] / MBS
     out[k] = e
 json.dump(out, sys.stdout, indent=1)
