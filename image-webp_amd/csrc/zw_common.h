@@ -80,22 +80,14 @@ struct ZwMbOut {
 //            start[b+1]-1 of the level array (its zigzag prefix up to the last
 //            nonzero); blocks 0..23, then 24 = Y2   [68..79] pad
 //   [80..] int16 levels, zigzag order; pad to 16.
-// The device expands it into a ZwDecMb in LDS.
+// k_dec_recon / k_dec_recon_rows read it straight from the upload (one MB
+// ahead, staged in LDS); a level is start[b] + zigzag position < start[b+1].
 // k_pack_scan's per-chunk counter words: [0] running offset, [1] frames done,
 // [2] the chunk's total bytes (read by the host), [3] pad.  The last frame's
 // workgroup publishes the total and clears [0] and [1] for the next launch.
 #define ZW_PACK_CTR_WORDS 4
 #define ZW_DREC_HDR 80
 #define ZW_DREC_MAX (ZW_DREC_HDR + 25 * 16 * 2)  // 880 B = 55 lines
-
-struct ZwDecMb {
-    uint8_t luma_mode, chroma_mode, segment, skip;
-    uint8_t bpred[16];
-    uint32_t nz_mask;          // bit b: block b's token run was non-empty (0..15 Y, 16..19 U, 20..23 V)
-    int16_t y2[16];            // Y2 levels, natural order (luma_mode != 4 && !skip)
-    int16_t coeffs[24][16];    // levels, natural order; dequantised on the device
-    uint32_t pad[2];           // 832 B: whole 16-byte lines (one coalesced load per lane)
-};
 
 // Loop-filter parameters per segment x {i16, i4} (calculate_filter_parameters,
 // decoder/vp8.rs:1470): level, interior limit, hev threshold.

@@ -3,7 +3,7 @@
 //
 //   host  : frame header (decoder/vp8.rs:553-670), partitions (:421-450),
 //           quantiser indices (:452-504), MB modes (:681-734) and residual
-//           tokens (:872-1058) -> one ZwDecMb record per macroblock.  The
+//           tokens (:872-1058) -> one packed record per macroblock.  The
 //           boolean decoder follows decoder/bit_reader.rs (libwebp-style
 //           56-bit refill, one zero byte past the end then eof).
 //   device: k_dec_recon (dequant, iWHT, iDCT, prediction) and k_loopfilter.
@@ -21,15 +21,14 @@
 #include "zw_host_internal.h"
 
 extern "C" {
-hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
-                          ZwDecMb* mbs, int nmb, int nframes);
-hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
-                         uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes);
+hipError_t zwk_dec_recon(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
+                         const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V, uint8_t* flags, int mbw, int mbh,
+                         size_t ysz, size_t csz, int nframes);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
                        int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
-hipError_t zwk_dec_rows(hipStream_t s, int phase, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
-                        uint8_t* V, uint8_t* flags, const ZwFilterParams* fp, int mbw, int mbh, size_t ysz, size_t csz,
-                        int nframes, int* rowsync, uint8_t* borders, int rows);
+hipError_t zwk_dec_rows(hipStream_t s, int phase, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
+                        const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V, uint8_t* flags, const ZwFilterParams* fp,
+                        int mbw, int mbh, size_t ysz, size_t csz, int nframes, int* rowsync, uint8_t* borders, int rows);
 hipError_t zwk_dec_rows_init(hipStream_t s, int* rowsync, int mbh, int nframes);
 size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
@@ -476,7 +475,7 @@ extern "C" void zw_frame_free(zw_frame* f)
 // Decoded planes of a batch, resident in the context's device scratch.
 struct DecBatch {
     std::vector<DecFrame> F;
-    hipEvent_t* ev = nullptr;  // [0] expand done / recon start, [1] recon done, [2] filter done, [3] caller's
+    hipEvent_t* ev = nullptr;  // [0] recon start, [1] recon done, [2] filter done, [3] caller's
     uint8_t* d = nullptr;  // device scratch base
     size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
     int mbw = 0, mbh = 0;
@@ -607,7 +606,7 @@ static int dec_parse(zw_ctx* ctx, int n, const uint8_t* const* data, const size_
     return ZW_OK;
 }
 
-// Device half: upload set bi's records, expand, reconstruct, filter (leaving
+// Device half: upload set bi's records, reconstruct, filter (leaving
 // `extra_bytes` of scratch at B.o_extra for the caller).
 static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
 {
@@ -621,8 +620,7 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     HIPOK(hipSetDevice(ctx->device));
     const size_t o_mbs = 0, o_q = al256(o_mbs + up_bytes);
     const size_t o_fp = al256(o_q + quant.size() * sizeof(DecQuant));
-    const size_t o_full = al256(o_fp + fps.size() * sizeof(ZwFilterParams));  // expanded ZwDecMb records
-    const size_t o_fl = al256(o_full + (size_t)n * nmb * sizeof(ZwDecMb));
+    const size_t o_fl = al256(o_fp + fps.size() * sizeof(ZwFilterParams));
     const size_t o_y = al256(o_fl + (size_t)n * nmb * 4);
     const size_t o_u = al256(o_y + (size_t)n * ysz), o_v = al256(o_u + (size_t)n * csz);
     // Small batches run the row-parallel kernels (one wave per MB row, the x+2y
@@ -645,22 +643,23 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     for (int e = 0; e < 4; e++)
         if (!ev[e]) HIPOK(hipEventCreate(&ev[e]));
     HIPOK(hipEventRecord(ev[0], s));
-    HIPOK(zwk_dec_expand(s, d + o_mbs, (const uint32_t*)(d + o_mbs + o_moff), (const uint64_t*)(d + o_mbs + o_base),
-                         (ZwDecMb*)(d + o_full), (int)nmb, n));
+    // the kernels read the packed records straight from the upload
+    const uint8_t* recs = d + o_mbs;
+    const uint32_t* moff = (const uint32_t*)(d + o_mbs + o_moff);
+    const uint64_t* fbase = (const uint64_t*)(d + o_mbs + o_base);
     // two wavefront kernels (a fused recon + filter wavefront measured slower: the
     // per-MB latencies add up in one chain, and its registers spilled)
     if (rows) {
         int* rs = (int*)(d + o_rs);
         HIPOK(zwk_dec_rows_init(s, rs, mbh, n));
         if (dec_force_error()) HIPOK(hipMemsetAsync(rs + 2, 1, sizeof(int), s));
-        HIPOK(zwk_dec_rows(s, 1, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
+        HIPOK(zwk_dec_rows(s, 1, recs, moff, fbase, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
         HIPOK(hipEventRecord(ev[1], s));
-        HIPOK(zwk_dec_rows(s, 2, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
+        HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, nullptr, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
     } else {
-        HIPOK(zwk_dec_recon(s, (const ZwDecMb*)(d + o_full), d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh,
-                            ysz, csz, n));
+        HIPOK(zwk_dec_recon(s, recs, moff, fbase, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz, csz, n));
         HIPOK(hipEventRecord(ev[1], s));
         HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n, mbw));
     }
@@ -986,7 +985,7 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     if (rows_env != 0) {
         HIPOK(zwk_dec_rows_init(s, (int*)(d + o_rs), (int)mbh, 1));
         if (dec_force_error()) HIPOK(hipMemsetAsync(d + o_rs + 2 * sizeof(int), 1, sizeof(int), s));
-        HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp),
+        HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, nullptr, nullptr, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp),
                            (int)mbw, (int)mbh, ysz, csz, 1, (int*)(d + o_rs), nullptr, (int)mbh));
     } else {
         HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1,

@@ -29,7 +29,7 @@ struct ZwDecQuant {
 };
 
 struct DecLds {
-    uint4 rec[52];  // the current MB's ZwDecMb record (832 B), prefetched one MB ahead
+    uint4 rec[55];  // the current MB's packed record (zw_common.h ZW_DREC_*, <= 880 B), prefetched one MB ahead
     uint8_t i4idx[10][16];
     uint8_t ws[17 * ZW_BPS];  // I4 MBs: the luma work area (border row / column + 16x16)
     uint8_t left_y[20], left_u[12], left_v[12];
@@ -97,6 +97,21 @@ __device__ __forceinline__ void dec_block_residual(int* c, int nz)
         for (int k = 0; k < 16; k++) c[k] = d;
     }
 }
+
+// Packed MB record (zw_common.h ZW_DREC_*, written by zw_dec_host.cpp
+// PackedMb): byte 0 luma mode (bits 0-2), chroma mode (3-4), skip (5); byte 1
+// segment; bytes 4-7 the non-zero mask; 8-15 the I4 sub-modes as nibbles;
+// halfwords 8.. the level start of each block (0-23, 24 = Y2) and the end;
+// from byte ZW_DREC_HDR each block's levels in zigzag order up to its last
+// non-zero one.  drec_lv: the level at natural index n of the block whose
+// levels are [s0, s1).
+DI int drec_lv(const uint8_t* rb, int s0, int s1, int n)
+{
+    const int idx = s0 + izz_of(n);
+    const int v = ((const int16_t*)(rb + ZW_DREC_HDR))[idx];  // (past the record: LDS garbage, masked)
+    return idx < s1 ? v : 0;
+}
+DI int drec_start(const uint8_t* rb, int b) { return ((const uint16_t*)(rb + 16))[b]; }
 
 // ---------------------------------------------------------------------------
 // Loop filter (decoder/loop_filter.rs) on LDS-staged neighbourhoods.
@@ -438,7 +453,8 @@ DI uint32_t recon_row_quad(const int x[4], int q, bool nz, int c0, int m, uint32
 // sub-blocks chain through their own reconstruction, build the LDS work area
 // ws and run the 16 sub-blocks in turn.
 template <bool XCU, class WAIT, class PUB>
-__device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuant* __restrict__ quant, uint8_t* Y,
+__device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, const uint32_t* __restrict__ moff,
+                                              const uint64_t* __restrict__ fbase, const ZwDecQuant* __restrict__ quant, uint8_t* Y,
                                               uint8_t* U, uint8_t* V, uint8_t* flags, int f, int mbw, int mbh,
                                               size_t ysz, size_t csz, int mby, DecLds* W, uint8_t* gty, uint8_t* gtu,
                                               uint8_t* gtv, WAIT&& wait, PUB&& pub)
@@ -453,11 +469,22 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
     if (lane < 20) W->left_y[lane] = 129;
     if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
     wsync();
-    uint4 nxt = {0u, 0u, 0u, 0u};
-    if (lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw) * 52 + lane];
+    // packed records of this row: MB x spans [fmo[x], fmo[x + 1]) bytes of the frame's records
+    const uint8_t* frec = recs + fbase[f];
+    const uint32_t* fmo = moff + (size_t)f * (nmb + 1) + (size_t)mby * mbw;
+    auto load_rec = [&](uint32_t a, uint32_t e) -> uint4 {
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (lane < 55 && a + 16u * (uint32_t)lane < e) v = *(const uint4*)(frec + a + 16u * (uint32_t)lane);
+        return v;
+    };
+    uint32_t a1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[1]);
+    uint32_t a2 = mbw >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[2]) : 0u;
+    uint4 nxt = load_rec((uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[0]), a1);
     for (int mbx = 0; mbx < mbw; mbx++) {
         const uint4 cur = nxt;
-        if (mbx + 1 < mbw && lane < 52) nxt = recs[((size_t)f * nmb + (size_t)mby * mbw + mbx + 1) * 52 + lane];
+        if (mbx + 1 < mbw) nxt = load_rec(a1, a2);  // MB x+1
+        a1 = a2;
+        if (mbx + 3 <= mbw) a2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[mbx + 3]);
         if (mby > 0) wait(min(mbx + 2, mbw));
         if (XCU && mby > 0) {  // the row above's bottom pixels (written by another workgroup)
             if (lane < 8) W->twy[lane] = ld_sc1(gty + mbx * 16 + 4 * lane);
@@ -467,13 +494,14 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
         const uint8_t* top_y = XCU ? (const uint8_t*)W->twy : gty + mbx * 16;
         const uint8_t* top_u = XCU ? (const uint8_t*)W->twu : gtu + mbx * 8;
         const uint8_t* top_v = XCU ? (const uint8_t*)W->twv : gtv + mbx * 8;
-        if (lane < 52) W->rec[lane] = cur;
+        if (lane < 55) W->rec[lane] = cur;
         wsync();
-        const ZwDecMb& M = *(const ZwDecMb*)W->rec;
-        const int seg = __builtin_amdgcn_readfirstlane(M.segment);
+        const uint8_t* rb = (const uint8_t*)W->rec;
+        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[0]);
+        const int seg = (int)((h0 >> 8) & 3u), skip = (int)((h0 >> 5) & 1u);
         const ZwDecQuant& Q = quant[(XCU ? 0 : (size_t)f * 4) + seg];  // XCU: quant is the frame's LDS copy
-        const int lm = __builtin_amdgcn_readfirstlane(M.luma_mode);
-        const uint32_t nzm = (uint32_t)__builtin_amdgcn_readfirstlane((int)M.nz_mask);
+        const int lm = (int)(h0 & 7u);
+        const uint32_t nzm = (uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[1]);
         const bool left = mbx != 0;
         // ---- luma ----
         const uint32_t TW = above ? ((const uint32_t*)top_y)[bx] : 0x7f7f7f7fu;
@@ -483,13 +511,13 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
         if (lm != 4) {
             // Y2 in group form (lane k = block k's DC after the iWHT), moved to the quads
             const int k = lane & 15;
-            const int y2v = M.skip ? 0 : (int)M.y2[k] * (k ? Q.y2ac : Q.y2dc);
+            const int y2v = skip ? 0 : drec_lv(rb, drec_start(rb, 24), drec_start(rb, 25), k) * (k ? Q.y2ac : Q.y2dc);
             const int dcb = iwht_g(y2v, k);
             const int dc = __builtin_amdgcn_ds_bpermute(4 * b, dcb);
-            const int16_t* cf = M.coeffs[b];
+            const int s0 = drec_start(rb, b), s1 = drec_start(rb, b + 1);
             int x[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) x[r] = (int)cf[4 * r + q] * Q.yac;
+            for (int r = 0; r < 4; r++) x[r] = drec_lv(rb, s0, s1, 4 * r + q) * Q.yac;
             x[0] = csel(q == 0, dc, x[0]);
             const int L = left ? (int)W->left_y[1 + 4 * by + q] : 129;
             const int P = above ? (left ? (int)W->left_y[0] : 129) : 127;
@@ -526,13 +554,13 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
             for (int i = 0; i < 16; i++) {
                 const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
                 dec_i4_values(W, lane, x0, y0);
-                const int c = (int)M.coeffs[i][k] * (k ? Q.yac : Q.ydc);
+                const int c = drec_lv(rb, drec_start(rb, i), drec_start(rb, i + 1), k) * (k ? Q.yac : Q.ydc);
                 const int nz = (nzm >> i) & 1;
                 const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
                 const int full = idct_g_exact(c, k);
                 const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
                 nzd |= nz || c0 != 0;
-                const int v = clamp255(dec_i4_px(W, M.bpred[i], k) + r);
+                const int v = clamp255(dec_i4_px(W, (rb[8 + (i >> 1)] >> (4 * (i & 1))) & 15, k) + r);
                 if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
                 wsync();
             }
@@ -553,13 +581,13 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
             const int shf = 2 + above + left;
             const int dcv = (above || left) ? ((sv + (1 << (shf - 1))) >> shf) : 128;
             const int cbk = 16 + 4 * pl + cb;
-            const int16_t* cf = M.coeffs[cbk];
+            const int s0 = drec_start(rb, cbk), s1 = drec_start(rb, cbk + 1);
             int x[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) x[r] = (int)cf[4 * r + q] * (r == 0 && q == 0 ? Q.uvdc : Q.uvac);
+            for (int r = 0; r < 4; r++) x[r] = drec_lv(rb, s0, s1, 4 * r + q) * (r == 0 && q == 0 ? Q.uvdc : Q.uvac);
             const int c0 = qb0(x[0]);
             const bool nz = (nzm >> cbk) & 1u;
-            const int cm = __builtin_amdgcn_readfirstlane(M.chroma_mode);
+            const int cm = (int)((h0 >> 3) & 3u);
             RC = recon_row_quad(x, q, nz, c0, cm, TC, L, P, dcv);
             nzdct |= __any(lane < 32 && (c0 != 0 || nz)) ? 1 : 0;
         }
@@ -588,14 +616,16 @@ __device__ __forceinline__ void dec_recon_row(const uint4* recs, const ZwDecQuan
         *(uint32_t*)(yo + (size_t)(4 * by + q) * ys + 4 * bx) = RW;
         if (lane < 32) *(uint32_t*)(co + (size_t)(4 * cby + q) * cs + 4 * cbx) = RC;
         if (lane < 4) {
-            const int v = lane == 0 ? lm : (lane == 1 ? seg : (lane == 2 ? (int)M.skip : nzdct));
+            const int v = lane == 0 ? lm : (lane == 1 ? seg : (lane == 2 ? skip : nzdct));
             flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
         }
         wsync();
     }
 }
 
-__global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const ZwDecMb* __restrict__ mbs,
+__global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NWD / 4))) void k_dec_recon(const uint8_t* __restrict__ recs,
+                                                              const uint32_t* __restrict__ moff,
+                                                              const uint64_t* __restrict__ fbase,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
                                                               size_t csz)
@@ -618,10 +648,9 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WGD) top_u[i] = top_v[i] = 127;
     if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
     __syncthreads();
-    const uint4* recs = (const uint4*)mbs;  // 52 lines per record
     for (int mby = wv; mby < mbh; mby += NWD) {
         dec_recon_row<false>(
-            recs, quant, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
+            recs, moff, fbase, quant, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
             [&](int need) { dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + need); },
             [&](int done) { dec_publish(progress, wv, mby * 65536 + done); });
     }
@@ -670,7 +699,9 @@ __device__ __forceinline__ void row_publish(int* prog, int val)
 // then progress[2][mbh] (recon, filter), initialised to -1.
 __device__ __forceinline__ int* rs_frame(int* rowsync, int f, int mbh) { return rowsync + (size_t)f * (4 + 2 * mbh); }
 
-__global__ __launch_bounds__(64) void k_dec_recon_rows(const ZwDecMb* __restrict__ mbs,
+__global__ __launch_bounds__(64) void k_dec_recon_rows(const uint8_t* __restrict__ recs,
+                                                       const uint32_t* __restrict__ moff,
+                                                       const uint64_t* __restrict__ fbase,
                                                        const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                        uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
                                                        size_t csz, int* rowsync, uint8_t* borders)
@@ -692,7 +723,7 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const ZwDecMb* __restrict
         if (mby >= mbh) break;
         int seen = -1;
         dec_recon_row<true>(
-            (const uint4*)mbs, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, gty, gtu, gtv,
+            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, gty, gtu, gtv,
             [&](int need) { row_wait(&prog[mby - 1], need, &rs[2], seen); },
             [&](int done) { row_publish(&prog[mby], done); });
     }
@@ -889,14 +920,17 @@ extern "C" size_t zw_dec_rows_border_bytes(int mbw, int nframes)
 // rowsync must hold zeros in [0..3] and -1 in the progress words of every
 // frame (zw_dec_rows_sync_init); rows = workgroups (waves) per frame.
 // phase 1: reconstruction, 2: loop filter.
-extern "C" hipError_t zwk_dec_rows(hipStream_t s, int phase, const ZwDecMb* mbs, const void* quant, uint8_t* Y,
-                                   uint8_t* U, uint8_t* V, uint8_t* flags, const ZwFilterParams* fp, int mbw, int mbh,
-                                   size_t ysz, size_t csz, int nframes, int* rowsync, uint8_t* borders, int rows)
+// recs / moff / fbase: the packed MB records (zw_common.h ZW_DREC_*), each
+// frame's MB byte offsets (nmb + 1 per frame) and each frame's base offset.
+extern "C" hipError_t zwk_dec_rows(hipStream_t s, int phase, const uint8_t* recs, const uint32_t* moff,
+                                   const uint64_t* fbase, const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V,
+                                   uint8_t* flags, const ZwFilterParams* fp, int mbw, int mbh, size_t ysz, size_t csz,
+                                   int nframes, int* rowsync, uint8_t* borders, int rows)
 {
     const int R = rows < 1 ? 1 : (rows > mbh ? mbh : rows);
     if (phase == 1)
-        hipLaunchKernelGGL(k_dec_recon_rows, dim3(R, nframes), dim3(64), 0, s, mbs, (const ZwDecQuant*)quant, Y, U,
-                           V, flags, mbw, mbh, ysz, csz, rowsync, borders);
+        hipLaunchKernelGGL(k_dec_recon_rows, dim3(R, nframes), dim3(64), 0, s, recs, moff, fbase,
+                           (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, rowsync, borders);
     else
         hipLaunchKernelGGL(k_loopfilter_rows, dim3(R, nframes), dim3(64), 0, s, Y, U, V, flags, fp, ysz, csz,
                            rowsync);
@@ -924,74 +958,17 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
     return off;
 }
 
-// k_dec_expand: packed MB records (what crossed PCIe, zw_common.h ZW_DREC_*)
-// -> full ZwDecMb records for k_dec_recon.  One wave per MB, fully parallel
-// over the batch: the wavefront kernel keeps its one-MB-ahead prefetch of
-// fixed-size records.  Slot sl = block (sl >> 4, 24 = Y2) x zigzag position.
-extern "C" __global__ __launch_bounds__(256) void k_dec_expand(const uint8_t* __restrict__ recs,
-                                                                 const uint32_t* __restrict__ moff,
-                                                                 const uint64_t* __restrict__ fbase, ZwDecMb* mbs,
-                                                                 int nmb)
-{
-    __shared__ uint4 raw[4][55];
-    const int f = blockIdx.y, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + wv;
-    if (i >= nmb) return;
-    const uint32_t* fo = moff + (size_t)f * (nmb + 1);
-    const uint32_t a = fo[i], e = fo[i + 1];
-    if (a + 16u * (uint32_t)lane < e && lane < 55) raw[wv][lane] = *(const uint4*)(recs + fbase[f] + a + 16u * lane);
-    wsync();
-    const uint8_t* rb = (const uint8_t*)raw[wv];
-    const uint16_t* st = (const uint16_t*)(rb + 16);
-    const int16_t* lv = (const int16_t*)(rb + ZW_DREC_HDR);
-    // the 832-byte record as 52 16-byte lines: lane l < 52 assembles line l
-    // from 8 halfwords (line 0: header bytes and bpred, line 1..: y2/coeffs)
-    uint4* out = (uint4*)(mbs + (size_t)f * nmb + i);
-    if (lane < 52) {
-        uint16_t h[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int byte = lane * 16 + q * 2;  // offset in ZwDecMb
-            int v = 0;
-            if (byte >= 24 && byte < 824) {  // y2[16] at 24, coeffs[24][16] at 56
-                const int c = (byte - 24) >> 1, b = c < 16 ? 24 : (c - 16) >> 4, nat = c & 15;
-                const int k = izz_of(nat), s0 = st[b], s1 = st[b + 1];
-                v = s0 + k < s1 ? (int)(uint16_t)lv[s0 + k] : 0;
-            } else if (byte < 24) {
-                auto hb = [&](int o) -> int {
-                    if (o == 0) return rb[0] & 7;
-                    if (o == 1) return (rb[0] >> 3) & 3;
-                    if (o == 2) return rb[1];
-                    if (o == 3) return (rb[0] >> 5) & 1;
-                    if (o < 20) return (rb[8 + ((o - 4) >> 1)] >> (4 * ((o - 4) & 1))) & 15;
-                    return rb[4 + (o - 20)];  // nz_mask
-                };
-                v = hb(byte) | (hb(byte + 1) << 8);
-            }
-            h[q] = (uint16_t)v;
-        }
-        out[lane] = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16), h[4] | ((uint32_t)h[5] << 16),
-                               h[6] | ((uint32_t)h[7] << 16));
-    }
-}
-
-extern "C" hipError_t zwk_dec_expand(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
-                                     ZwDecMb* mbs, int nmb, int nframes)
-{
-    hipLaunchKernelGGL(k_dec_expand, dim3((nmb + 3) / 4, nframes), dim3(256), 0, s, recs, moff, fbase, mbs, nmb);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t zwk_dec_recon(hipStream_t s, const ZwDecMb* mbs, const void* quant, uint8_t* Y, uint8_t* U,
-                                    uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz, size_t csz, int nframes)
+extern "C" hipError_t zwk_dec_recon(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
+                                    const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V, uint8_t* flags, int mbw,
+                                    int mbh, size_t ysz, size_t csz, int nframes)
 {
     static const bool attr = []() {
         (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, mbs, (const ZwDecQuant*)quant,
-                       Y, U, V, flags, mbw, mbh, ysz, csz);
+    hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, recs, moff, fbase,
+                       (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz);
     return hipGetLastError();
 }
 
