@@ -415,10 +415,11 @@ DI void idct_quad_exact(int x0, int x1, int x2, int x3, int q, int o[4])
 // prediction of mode m (0 DC, 1 V, 2 H, 3 TM; predict_* prediction.rs:164-324)
 // from the top word T (the 4 pixels above the block's columns), the left pixel
 // L of this row, the corner P and the DC value; returns the 4 pixels as a word.
-DI uint32_t recon_row_quad(const int x[4], int q, bool nz, int c0, int m, uint32_t T, int L, int P, int dcv)
+// any_nz: some block of the wave has a non-empty run (else the iDCT is skipped).
+DI uint32_t recon_row_quad(const int x[4], int q, bool nz, bool any_nz, int c0, int m, uint32_t T, int L, int P, int dcv)
 {
-    int o[4];
-    idct_quad_exact(x[0], x[1], x[2], x[3], q, o);
+    int o[4] = {0, 0, 0, 0};
+    if (any_nz) idct_quad_exact(x[0], x[1], x[2], x[3], q, o);
     const int d = (c0 + 4) >> 3;
     const uint32_t R01 = nz ? pack_lo(o[0], o[1]) : pack_lo(d, d);
     const uint32_t R32 = nz ? pack_lo(o[3], o[2]) : pack_lo(d, d);
@@ -459,32 +460,37 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
                                               size_t ysz, size_t csz, int mby, DecLds* W, uint8_t* gty, uint8_t* gtu,
                                               uint8_t* gtv, WAIT&& wait, PUB&& pub)
 {
-    const int lane = threadIdx.x & 63;
+    const int lane0 = threadIdx.x & 63;
     const int ys = mbw * 16, cs = mbw * 8;
     const size_t nmb = (size_t)mbw * mbh;
-    const int b = lane >> 2, q = lane & 3, bx = b & 3, by = b >> 2;
-    // chroma: lanes 0..31 (lanes 32..63 mirror them and store nothing)
-    const int pl = (lane >> 4) & 1, cb = (lane >> 2) & 3, cbx = cb & 1, cby = cb >> 1;
     const bool above = mby != 0;
+    const int lane = lane0;  // (outside the MB loop)
     if (lane < 20) W->left_y[lane] = 129;
     if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
     wsync();
     // packed records of this row: MB x spans [fmo[x], fmo[x + 1]) bytes of the frame's records
     const uint8_t* frec = recs + fbase[f];
     const uint32_t* fmo = moff + (size_t)f * (nmb + 1) + (size_t)mby * mbw;
-    auto load_rec = [&](uint32_t a, uint32_t e) -> uint4 {
+    auto load_rec = [&](int ln, uint32_t a, uint32_t e) -> uint4 {
         uint4 v = {0u, 0u, 0u, 0u};
-        if (lane < 55 && a + 16u * (uint32_t)lane < e) v = *(const uint4*)(frec + a + 16u * (uint32_t)lane);
+        if (ln < 55 && a + 16u * (uint32_t)ln < e) v = *(const uint4*)(frec + a + 16u * (uint32_t)ln);
         return v;
     };
     uint32_t a1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[1]);
     uint32_t a2 = mbw >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[2]) : 0u;
-    uint4 nxt = load_rec((uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[0]), a1);
+    uint4 nxt = load_rec(lane, (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[0]), a1);
     for (int mbx = 0; mbx < mbw; mbx++) {
+        // the lane's roles, recomputed per MB from an opaque copy of the lane id:
+        // hoisted out of the loop, their exec masks were spilled to VGPR lanes
+        // and reloaded with v_readlane every MB
+        const int lane = pin(lane0);
         const uint4 cur = nxt;
-        if (mbx + 1 < mbw) nxt = load_rec(a1, a2);  // MB x+1
+        if (mbx + 1 < mbw) nxt = load_rec(lane, (uint32_t)__builtin_amdgcn_readfirstlane((int)a1),
+                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)a2));  // MB x+1
         a1 = a2;
-        if (mbx + 3 <= mbw) a2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[mbx + 3]);
+        // (a vector load: a scalar one would be waited for with lgkmcnt(0) by the
+        // next LDS access, a full memory round trip per MB)
+        if (mbx + 3 <= mbw) a2 = fmo[mbx + 3 + (lane >> 6)];
         if (mby > 0) wait(min(mbx + 2, mbw));
         if (XCU && mby > 0) {  // the row above's bottom pixels (written by another workgroup)
             if (lane < 8) W->twy[lane] = ld_sc1(gty + mbx * 16 + 4 * lane);
@@ -496,10 +502,14 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
         const uint8_t* top_v = XCU ? (const uint8_t*)W->twv : gtv + mbx * 8;
         if (lane < 55) W->rec[lane] = cur;
         wsync();
+        const int ln = lane;
+        const int b = ln >> 2, q = ln & 3, bx = b & 3, by = b >> 2;
+        // chroma: lanes 0..31 (lanes 32..63 mirror them and store nothing)
+        const int pl = (ln >> 4) & 1, cb = (ln >> 2) & 3, cbx = cb & 1, cby = cb >> 1;
         const uint8_t* rb = (const uint8_t*)W->rec;
         const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[0]);
         const int seg = (int)((h0 >> 8) & 3u), skip = (int)((h0 >> 5) & 1u);
-        const ZwDecQuant& Q = quant[(XCU ? 0 : (size_t)f * 4) + seg];  // XCU: quant is the frame's LDS copy
+        const ZwDecQuant& Q = quant[seg];  // the frame's LDS copy
         const int lm = (int)(h0 & 7u);
         const uint32_t nzm = (uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[1]);
         const bool left = mbx != 0;
@@ -511,9 +521,12 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
         if (lm != 4) {
             // Y2 in group form (lane k = block k's DC after the iWHT), moved to the quads
             const int k = lane & 15;
-            const int y2v = skip ? 0 : drec_lv(rb, drec_start(rb, 24), drec_start(rb, 25), k) * (k ? Q.y2ac : Q.y2dc);
-            const int dcb = iwht_g(y2v, k);
-            const int dc = __builtin_amdgcn_ds_bpermute(4 * b, dcb);
+            const int y2s = __builtin_amdgcn_readfirstlane(drec_start(rb, 24)), y2e = __builtin_amdgcn_readfirstlane(drec_start(rb, 25));
+            int dc = 0;
+            if (!skip && y2e > y2s) {
+                const int y2v = drec_lv(rb, y2s, y2e, k) * (k ? Q.y2ac : Q.y2dc);
+                dc = __builtin_amdgcn_ds_bpermute(4 * b, iwht_g(y2v, k));
+            }
             const int s0 = drec_start(rb, b), s1 = drec_start(rb, b + 1);
             int x[4];
 #pragma unroll
@@ -521,15 +534,17 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             x[0] = csel(q == 0, dc, x[0]);
             const int L = left ? (int)W->left_y[1 + 4 * by + q] : 129;
             const int P = above ? (left ? (int)W->left_y[0] : 129) : 127;
-            // DC predictor: the top row (lanes of blocks 0..3, q = 0) and the left column (bx = 0)
-            int sv = (above && b < 4 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TW, 0u, 0u) : 0) + (left && bx == 0 ? L : 0);
-            sv = red16(sv);
-            const int su = __builtin_amdgcn_readlane(sv, 0) + __builtin_amdgcn_readlane(sv, 16) +
-                           __builtin_amdgcn_readlane(sv, 32) + __builtin_amdgcn_readlane(sv, 48);
-            const int shf = 3 + above + left;
-            const int dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
+            int dcv = 128;
+            if (lm == 0) {  // DC predictor: the top row (lanes of blocks 0..3, q = 0) and the left column (bx = 0)
+                int sv = (above && b < 4 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TW, 0u, 0u) : 0) + (left && bx == 0 ? L : 0);
+                sv = red16(sv);
+                const int su = __builtin_amdgcn_readlane(sv, 0) + __builtin_amdgcn_readlane(sv, 16) +
+                               __builtin_amdgcn_readlane(sv, 32) + __builtin_amdgcn_readlane(sv, 48);
+                const int shf = 3 + above + left;
+                if (above || left) dcv = (su + (1 << (shf - 1))) >> shf;
+            }
             const bool nz = (nzm >> b) & 1u;
-            RW = recon_row_quad(x, q, nz, dc, lm, TW, L, P, dcv);
+            RW = recon_row_quad(x, q, nz, (nzm & 0xffffu) != 0u, dc, lm, TW, L, P, dcv);
             nzdct = __any(dc != 0 || nz) ? 1 : 0;
         } else {
             // --- luma border (create_border_luma) in ws, then the 16 sub-blocks ---
@@ -576,10 +591,14 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             const uint32_t TC = above ? ((const uint32_t*)tc)[cbx] : 0x7f7f7f7fu;
             const int L = left ? (int)lc[1 + 4 * cby + q] : 129;
             const int P = above ? (left ? (int)lc[0] : 129) : 127;
-            int sv = (above && cby == 0 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TC, 0u, 0u) : 0) + (left && cbx == 0 ? L : 0);
-            sv = red16(sv);  // the plane's 16-lane group
-            const int shf = 2 + above + left;
-            const int dcv = (above || left) ? ((sv + (1 << (shf - 1))) >> shf) : 128;
+            const int cm = (int)((h0 >> 3) & 3u);
+            int dcv = 128;
+            if (cm == 0) {
+                int sv = (above && cby == 0 && q == 0 ? (int)__builtin_amdgcn_sad_u8(TC, 0u, 0u) : 0) + (left && cbx == 0 ? L : 0);
+                sv = red16(sv);  // the plane's 16-lane group
+                const int shf = 2 + above + left;
+                if (above || left) dcv = (sv + (1 << (shf - 1))) >> shf;
+            }
             const int cbk = 16 + 4 * pl + cb;
             const int s0 = drec_start(rb, cbk), s1 = drec_start(rb, cbk + 1);
             int x[4];
@@ -587,8 +606,7 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             for (int r = 0; r < 4; r++) x[r] = drec_lv(rb, s0, s1, 4 * r + q) * (r == 0 && q == 0 ? Q.uvdc : Q.uvac);
             const int c0 = qb0(x[0]);
             const bool nz = (nzm >> cbk) & 1u;
-            const int cm = (int)((h0 >> 3) & 3u);
-            RC = recon_row_quad(x, q, nz, c0, cm, TC, L, P, dcv);
+            RC = recon_row_quad(x, q, nz, (nzm >> 16) != 0u, c0, cm, TC, L, P, dcv);
             nzdct |= __any(lane < 32 && (c0 != 0 || nz)) ? 1 : 0;
         }
         const int corner_u = (int)((uint32_t)__builtin_amdgcn_readlane(above ? (int)((const uint32_t*)top_u)[1] : 0x7f7f7f7f, 0) >> 24);
@@ -644,13 +662,14 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     uint8_t* top_v = smem + off;
     DecLds* W = (DecLds*)((uint8_t*)Wall + ((sizeof(DecLds) + 15) & ~(size_t)15) * wv);
     for (int i = lane; i < 160; i += 64) (&W->i4idx[0][0])[i] = (&d_I4_IDX[0][0])[i];
+    if (lane < 24) ((int32_t*)W->q)[lane] = ((const int32_t*)(quant + (size_t)f * 4))[lane];
     for (int i = threadIdx.x; i < mbw * 16 + 48; i += WGD) top_y[i] = 127;
     for (int i = threadIdx.x; i < mbw * 8 + 48; i += WGD) top_u[i] = top_v[i] = 127;
     if (threadIdx.x < NWD) progress[threadIdx.x] = -1;
     __syncthreads();
     for (int mby = wv; mby < mbh; mby += NWD) {
         dec_recon_row<false>(
-            recs, moff, fbase, quant, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
+            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
             [&](int need) { dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + need); },
             [&](int done) { dec_publish(progress, wv, mby * 65536 + done); });
     }

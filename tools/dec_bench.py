@@ -34,6 +34,9 @@ def main():
     el, rk, lf = best
     nmb = ((w + 15) // 16) * ((h + 15) // 16) * F
     gbs = DEC_BYTES_PER_MB * nmb / ((rk + lf) * 1e-3) / 1e9
+    if os.environ.get("DEC_BATCH_ONLY"):  # (profiling runs: the batch launches only)
+        print(f"{F} frames: kernels recon {rk:.2f} ms + loopfilter {lf:.2f} ms")
+        return
     # single frame (SURVEY config 3): end to end, and the oracle's CPU decode of the same stream
     one = [vp8[0]]
     zwebp.decode_batch(one, ctx=ctx)

@@ -3,7 +3,7 @@
 # frame): kernel trace + SQ counter passes over tools/dec_bench.py.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmcdec
-export ZW_DEC_CHUNK=256 ZW_DEC_ROWS=0
+export ZW_DEC_CHUNK=256 ZW_DEC_ROWS=0 DEC_BATCH_ONLY=1
 run() {  # name, rocprofv3 args...
   local n=$1; shift
   timeout -k 10 150 rocprofv3 "$@" --output-format csv -d gpurun_out/pmcdec/$n -o $n -- python3 tools/dec_bench.py 256 2 > gpurun_out/pmcdec/$n.log 2>&1
