@@ -1546,7 +1546,8 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
         st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
         st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
         st.nzm |= (uint32_t)bnz << i;
-        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode];
+        // the winner's mode cost is its lane's mcost (= fci4[tctx][lctx][bmode]): no LDS round trip on the step chain
+        st.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);
         st.running += rdscore(bsse, brate, S.l_mode);
         st.mpack |= (unsigned long long)bmode << (4 * i);
         if (l == h) W->modes[i] = (uint8_t)bmode;
@@ -1729,7 +1730,7 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
         st.tnz = (st.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
         st.lnz = (st.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
         st.nzm |= (uint32_t)bnz << i;
-        st.total_mc += T->fci4[tctx[h]][lctx[h]][bmode[h]];
+        st.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);  // (lane wl's mode is bmode[h])
         st.running += rdscore(bsse, brate, S.l_mode);
         st.mpack |= (unsigned long long)bmode[h] << (4 * i);
         if (l == h) W->modes[i] = (uint8_t)bmode[h];
