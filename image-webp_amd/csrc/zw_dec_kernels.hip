@@ -33,7 +33,7 @@ struct DecLds {
     uint8_t i4idx[10][16];
     uint8_t ws[17 * ZW_BPS];  // I4 MBs: the luma work area (border row / column + 16x16)
     uint8_t left_y[20], left_u[12], left_v[12];
-    int V[40];
+    int16_t res4[16 * 16];  // I4 MBs: the 16 sub-blocks' residuals (block, row, column), computed up front
     uint32_t twy[8], twu[2], twv[2];  // row-parallel kernel: the row above's bottom pixels around this MB
     ZwDecQuant q[4];                  // row-parallel kernel: the frame's segment quantisers
 };
@@ -57,46 +57,11 @@ __device__ __forceinline__ void dec_publish(int* progress, int w, int val)
     __builtin_amdgcn_wave_barrier();
 }
 
-// I4 value vector for sub-block (x0,y0) of ws (see zw_dev.h d_I4_IDX).
-__device__ void dec_i4_values(DecLds* W, int lane, int x0, int y0)
-{
-    const uint8_t* ws = W->ws;
-    auto E = [&](int k) -> int {
-        if (k < 4) return ws[(y0 + 3 - k) * ZW_BPS + x0 - 1];
-        if (k == 4) return ws[(y0 - 1) * ZW_BPS + x0 - 1];
-        return ws[(y0 - 1) * ZW_BPS + x0 + (k - 5)];
-    };
-    if (lane < 13) W->V[lane] = E(lane);
-    else if (lane < 24) { int k = lane - 13; W->V[lane] = (E(k) + 2 * E(k + 1) + E(k + 2) + 2) >> 2; }
-    else if (lane < 36) { int k = lane - 24; W->V[lane] = (E(k) + E(k + 1) + 1) >> 1; }
-    else if (lane == 36) W->V[36] = (E(11) + 3 * E(12) + 2) >> 2;
-    else if (lane == 37) W->V[37] = (E(1) + 3 * E(0) + 2) >> 2;
-    else if (lane == 38) {
-        int v = 4;
-        for (int k = 0; k < 4; k++) v += E(k) + E(5 + k);
-        W->V[38] = v >> 3;
-    }
-    wsync();
-}
-__device__ __forceinline__ int dec_i4_px(const DecLds* W, int mode, int p)
-{
-    const int idx = W->i4idx[mode][p];
-    if (idx == 255) return W->V[38];
-    if (idx == 254) return clamp255(W->V[3 - (p >> 2)] + W->V[5 + (p & 3)] - W->V[4]);
-    return W->V[idx];
-}
+// I4 edge offsets: E(j) of the sub-block whose top-left pixel is ws[base]
+// (j < 4: the left column bottom-up, 4: the corner, 5..12: the row above and
+// the above-right four; the d_I4_IDX value-vector order, zw_dev.h).
+DI int i4_eoff(int j) { return j < 4 ? (3 - j) * ZW_BPS - 1 : (j == 4 ? -ZW_BPS - 1 : -ZW_BPS + (j - 5)); }
 
-// Residual of one 4x4 block: full iDCT when the block's token run was
-// non-empty, DC-only iDCT when only the DC is set (vp8.rs:1110-1117).
-__device__ __forceinline__ void dec_block_residual(int* c, int nz)
-{
-    if (nz) idct16_exact(c);
-    else if (c[0] != 0) {
-        const int d = (c[0] + 4) >> 3;
-#pragma unroll
-        for (int k = 0; k < 16; k++) c[k] = d;
-    }
-}
 
 // Packed MB record (zw_common.h ZW_DREC_*, written by zw_dec_host.cpp
 // PackedMb): byte 0 luma mode (bits 0-2), chroma mode (3-4), skip (5); byte 1
@@ -491,7 +456,9 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
         // (a vector load: a scalar one would be waited for with lgkmcnt(0) by the
         // next LDS access, a full memory round trip per MB)
         if (mbx + 3 <= mbw) a2 = fmo[mbx + 3 + (lane >> 6)];
+#ifndef ZW_EXP_NO_WAIT
         if (mby > 0) wait(min(mbx + 2, mbw));
+#endif
         if (XCU && mby > 0) {  // the row above's bottom pixels (written by another workgroup)
             if (lane < 8) W->twy[lane] = ld_sc1(gty + mbx * 16 + 4 * lane);
             else if (lane < 10) W->twu[lane - 8] = ld_sc1(gtu + mbx * 8 + 4 * (lane - 8));
@@ -518,7 +485,11 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
         const int corner_y = (int)((uint32_t)__builtin_amdgcn_readlane((int)TW, 12) >> 24);  // top pixel 15: the next MB's corner
         uint32_t RW;
         int nzdct;
+#ifdef ZW_EXP_NO_I4
+        if (true) {
+#else
         if (lm != 4) {
+#endif
             // Y2 in group form (lane k = block k's DC after the iWHT), moved to the quads
             const int k = lane & 15;
             const int y2s = __builtin_amdgcn_readfirstlane(drec_start(rb, 24)), y2e = __builtin_amdgcn_readfirstlane(drec_start(rb, 25));
@@ -547,10 +518,26 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             RW = recon_row_quad(x, q, nz, (nzm & 0xffffu) != 0u, dc, lm, TW, L, P, dcv);
             nzdct = __any(dc != 0 || nz) ? 1 : 0;
         } else {
-            // --- luma border (create_border_luma) in ws, then the 16 sub-blocks ---
+            // --- the 16 residuals in quad form first (they do not depend on the
+            // prediction), then the sub-blocks' predictions in raster order ---
+            {
+                const int s0 = drec_start(rb, b), s1 = drec_start(rb, b + 1);
+                int x[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) x[r] = drec_lv(rb, s0, s1, 4 * r + q) * (r == 0 && q == 0 ? Q.ydc : Q.yac);
+                const int c0 = qb0(x[0]);
+                const bool nz = (nzm >> b) & 1u;
+                int o[4] = {0, 0, 0, 0};
+                if ((nzm & 0xffffu) != 0u) idct_quad_exact(x[0], x[1], x[2], x[3], q, o);
+                const int d = (c0 + 4) >> 3;  // DC-only: (c0 + 4) >> 3 (0 for c0 = 0)
+                uint32_t* rp = (uint32_t*)&W->res4[b * 16 + q * 4];
+                rp[0] = nz ? pack_lo(o[0], o[1]) : pack_lo(d, d);
+                rp[1] = nz ? pack_lo(o[2], o[3]) : pack_lo(d, d);
+                nzdct = __any(nz || c0 != 0) ? 1 : 0;
+            }
             uint8_t* ws = W->ws;
             const uint8_t* ty = top_y - mbx * 16;
-            if (lane < 32) {
+            if (lane < 32) {  // luma border (create_border_luma)
                 int v;
                 if (lane == 0) v = mby == 0 ? 127 : (mbx == 0 ? 129 : W->left_y[0]);
                 else if (mby == 0) v = 127;
@@ -563,23 +550,35 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
                 ws[(lane - 31) * ZW_BPS] = mbx == 0 ? 129 : W->left_y[lane - 31];
             }
             wsync();
-            // group form: lane k = coefficient k of the sub-block (all four groups alike)
+            // value vector V (lane l < 39 holds V[l]): E(a) + wb E(b) + wc E(c) rounded, or the DC sum
+            int ja = lane, jb = 0, jc = 0, wb = 0, wc = 0, rnd = 0, sh = 0;
+            if (lane >= 13 && lane < 24) { ja = lane - 13; jb = ja + 1; jc = ja + 2; wb = 2; wc = 1; rnd = 2; sh = 2; }
+            else if (lane >= 24 && lane < 36) { ja = lane - 24; jb = ja + 1; wb = 1; rnd = 1; sh = 1; }
+            else if (lane == 36) { ja = 11; jb = 12; wb = 3; rnd = 2; sh = 2; }
+            else if (lane == 37) { ja = 1; jb = 0; wb = 3; rnd = 2; sh = 2; }
+            else if (lane >= 38) ja = 0;
+            const int oa = i4_eoff(ja), ob = i4_eoff(jb), oc = i4_eoff(jc);
+            const bool dcl = lane < 4 || (lane >= 5 && lane < 9);
             const int k = lane & 15;
-            int nzd = 0;
+            const uint64_t bp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[2]) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t*)rb)[3]) << 32);
             for (int i = 0; i < 16; i++) {
-                const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
-                dec_i4_values(W, lane, x0, y0);
-                const int c = drec_lv(rb, drec_start(rb, i), drec_start(rb, i + 1), k) * (k ? Q.yac : Q.ydc);
-                const int nz = (nzm >> i) & 1;
-                const int c0 = __builtin_amdgcn_readfirstlane(c);  // lane 0 holds the DC
-                const int full = idct_g_exact(c, k);
-                const int r = nz ? full : (c0 != 0 ? (c0 + 4) >> 3 : 0);
-                nzd |= nz || c0 != 0;
-                const int v = clamp255(dec_i4_px(W, (rb[8 + (i >> 1)] >> (4 * (i & 1))) & 15, k) + r);
-                if (lane < 16) ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)v;
+                const int x0 = (i & 3) * 4 + 1, y0 = (i >> 2) * 4 + 1, base = y0 * ZW_BPS + x0;
+                const int mode = (int)((bp >> (4 * i)) & 15u);
+                const int idx = W->i4idx[mode][k];
+                const int res = W->res4[i * 16 + k];
+                const int ea = ws[base + oa], eb = ws[base + ob], ec = ws[base + oc];
+                const int V = (ea + wb * eb + wc * ec + rnd) >> sh;
+                const int dsum = red16(dcl ? ea : 0);
+                const int dcv = (__builtin_amdgcn_readlane(dsum, 0) + 4) >> 3;
+                const int vi = __builtin_amdgcn_ds_bpermute(4 * (idx >= 254 ? 0 : idx), V);
+                const int tl = __builtin_amdgcn_ds_bpermute(4 * (3 - (k >> 2)), V);
+                const int tt = __builtin_amdgcn_ds_bpermute(4 * (5 + (k & 3)), V);
+                const int P = __builtin_amdgcn_readlane(V, 4);
+                const int pred = idx == 254 ? clamp255(tl + tt - P) : (idx == 255 ? dcv : vi);
+                if (lane < 16) ws[base + (k >> 2) * ZW_BPS + (k & 3)] = (uint8_t)clamp255(pred + res);
                 wsync();
             }
-            nzdct = nzd;
             const uint8_t* pr = ws + (4 * by + q + 1) * ZW_BPS + 1 + 4 * bx;
             RW = (uint32_t)pr[0] | ((uint32_t)pr[1] << 8) | ((uint32_t)pr[2] << 16) | ((uint32_t)pr[3] << 24);
         }
@@ -756,9 +755,11 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const uint8_t* __restrict
 // (chroma 4..7) go to the hand-off rows, the rest to the planes (rows -4..-1
 // always: the row above left them to this row; the last MB row also stores its
 // own rows 12..15).  No two waves store the same bytes.
+template <class PF>
 __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
                                         uint8_t* Vf, int ys, int cs, int mbx, int mby, uint32_t fl, uint32_t cy0,
-                                        uint32_t cy1, uint32_t cc, uint8_t* hy, uint8_t* hu, uint8_t* hv, bool last)
+                                        uint32_t cy1, uint32_t cc, uint8_t* hy, uint8_t* hu, uint8_t* hv, bool last,
+                                        PF&& prefetch)
 {
     const bool chroma = !F.filter_type;
     const int i4 = (fl & 255u) == 4u, seg = (int)((fl >> 8) & 3u), skip = (int)((fl >> 16) & 255u), nzd = (int)(fl >> 24);
@@ -789,9 +790,12 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
             }
         }
     }
+    prefetch();  // the next step's interior: issued once this one's is in LDS (fewer live registers)
     wsync();
+#ifndef ZW_EXP_NO_LF
     lf_filter_tile(L, hl, on && lvl != 0, F.filter_type != 0, chroma, mbx > 0, mby > 0, i4 || (!skip && nzd), ht, il,
                    (lvl + 2) * 2 + il, lvl * 2 + il);
+#endif
     if (!on) return;
     auto tile_y = [&](int r, int w) { return ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]; };
     auto tile_c = [&](int pl, int r, int w) { return ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]; };
@@ -804,18 +808,31 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
         const int pl = hl / 12, rr = hl % 12, r = 4 + rr / 3, w = rr % 3 - 1;
         if (mbx * 8 + 4 * w >= 0) *(uint32_t*)((pl ? hv : hu) + (r - 4) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
     }
+    // the planes: every LDS read first, then the stores (unrolled: 4 luma + 3 chroma words a lane)
     const bool wb = lvl != 0;
-    for (int t = hl; t < LFY * 5; t += 32) {
-        const int r = t / 5 - 4, w = t % 5 - 1;
-        const bool need = r < 0 ? mby > 0 : (wb && (r < 12 || last));
-        if (need && x0 + 4 * w >= 0) *(uint32_t*)(Yf + (size_t)(y0 + r) * ys + x0 + 4 * w) = tile_y(r, w);
+    // the planes, one tile row per lane (luma: a word for the carried columns + 16 bytes;
+    // chroma: a word + 8 bytes): rows -4..-1 always (the row above left them to this
+    // row), rows 0..11 (chroma 0..3) when filtered, 12..15 (4..7) also in the last MB row
+    if (hl < LFY) {
+        const int r = hl - 4;
+        if (r < 0 ? mby > 0 : (wb && (r < 12 || last))) {
+            const uint32_t* row = (const uint32_t*)(L->y + hl * LFY);
+            const uint32_t w0 = row[0];
+            const uint4 wv = make_uint4(row[1], row[2], row[3], row[4]);
+            uint8_t* dst = Yf + (y0 + r) * ys + x0;
+            if (mbx > 0) *(uint32_t*)(dst - 4) = w0;
+            *(uint4*)dst = wv;
+        }
     }
-    if (chroma) {
-        for (int t = hl; t < 2 * LFC * 3; t += 32) {
-            const int pl = t / (LFC * 3), rr = t % (LFC * 3), r = rr / 3 - 4, w = rr % 3 - 1;
-            const bool need = r < 0 ? mby > 0 : (wb && (r < 4 || last));
-            if (need && mbx * 8 + 4 * w >= 0)
-                *(uint32_t*)((pl ? Vf : Uf) + (size_t)(mby * 8 + r) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
+    if (chroma && hl < 2 * LFC) {
+        const int pl = hl >= LFC, rr = hl - LFC * pl, r = rr - 4;
+        if (r < 0 ? mby > 0 : (wb && (r < 4 || last))) {
+            const uint32_t* row = (const uint32_t*)((pl ? L->v : L->u) + rr * LFC);
+            const uint32_t w0 = row[0];
+            const uint2 wv = make_uint2(row[1], row[2]);
+            uint8_t* dst = (pl ? Vf : Uf) + (mby * 8 + r) * cs + mbx * 8;
+            if (mbx > 0) *(uint32_t*)(dst - 4) = w0;
+            *(uint2*)dst = wv;
         }
     }
 }
@@ -872,9 +889,11 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
             const int mx = st - 2 * h;
             const bool on = rowok && mx >= 0 && mx < mbw;
             const uint32_t cy0 = ny0, cy1 = ny1, cc = nc, fl = nfl;
-            if (rowok && mx + 1 >= 0 && mx + 1 < mbw) load(my, mx + 1, ny0, ny1, nc, nfl);
+#ifndef ZW_EXP_NO_WAIT
             if (pr > 0 && st < mbw) dec_wait(progress, (pr - 1) % NWD, (pr - 1) * 65536 + min(st + 2, mbw));
-            lf_half(L, hl, on, F, Yf, Uf, Vf, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1);
+#endif
+            if (rowok && mx + 1 >= 0 && mx + 1 < mbw) load(my, mx + 1, ny0, ny1, nc, nfl);
+            lf_half(L, hl, on, F, Yf, Uf, Vf, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1, [] {});
             wsync();
             if (st >= 2) dec_publish(progress, wv, pr * 65536 + st - 1);  // the lower row has finished st - 1 MBs
         }
