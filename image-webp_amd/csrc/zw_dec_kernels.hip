@@ -239,6 +239,26 @@ __device__ __forceinline__ void st_sc1(uint8_t* p, uint32_t v)
 {
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Raw buffer loads / stores with a per-lane offset; ZW_OOB (past num_records)
+// makes a lane's load return 0 and its store vanish.  The batch kernels issue
+// every global access of an MB step this way, unconditionally, so the number
+// of memory operations between a prefetch and its use is the same on every
+// path: the compiler then waits for the prefetch alone (vmcnt(N)) instead of
+// vmcnt(0), which would also wait for the step's own stores.
+#define ZW_OOB 0x80000000u
+typedef uint32_t zu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t zu4 __attribute__((ext_vector_type(4)));
+DI __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+DI uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0); }
+DI zu4 bld128(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0); }
+DI void bst8(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)off, 0, 0); }
+DI void bst32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0); }
+DI void bst64(zu2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
+DI void bst128(zu4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
+
 // pub() runs once the rows the MB row below reads (luma 12..15, chroma 4..7 of
 // this tile) are stored; the rest of the write-back follows it.
 // !XCU: those rows go to the workgroup's LDS hand-off rows hy / hu / hv (4 rows
@@ -433,29 +453,39 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
     if (lane < 20) W->left_y[lane] = 129;
     if (lane < 12) W->left_u[lane] = W->left_v[lane] = 129;
     wsync();
-    // packed records of this row: MB x spans [fmo[x], fmo[x + 1]) bytes of the frame's records
-    const uint8_t* frec = recs + fbase[f];
-    const uint32_t* fmo = moff + (size_t)f * (nmb + 1) + (size_t)mby * mbw;
+    // packed records of this row: MB x spans [fmo[x], fmo[x + 1]) bytes of the frame's
+    // records.  Every global access of an MB step is an unconditional buffer op (ZW_OOB
+    // for the lanes that have nothing to move), so the step's stores never join the
+    // wait for the next MB's prefetch.
+    const uint32_t* fmo_f = moff + (size_t)f * (nmb + 1);
+    const uint32_t fbytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo_f[nmb]);
+    const __amdgpu_buffer_rsrc_t rrec = brsrc(recs + fbase[f], fbytes);
+    const __amdgpu_buffer_rsrc_t rmo = brsrc(fmo_f, (uint32_t)(nmb + 1) * 4u);
+    const __amdgpu_buffer_rsrc_t ryp = brsrc(Y + (size_t)f * ysz, (uint32_t)ysz);
+    const __amdgpu_buffer_rsrc_t rup = brsrc(U + (size_t)f * csz, (uint32_t)csz);
+    const __amdgpu_buffer_rsrc_t rvp = brsrc(V + (size_t)f * csz, (uint32_t)csz);
+    const __amdgpu_buffer_rsrc_t rfl = brsrc(flags + (size_t)f * nmb * 4, (uint32_t)nmb * 4u);
+    const uint32_t row0 = (uint32_t)(mby * mbw);
     auto load_rec = [&](int ln, uint32_t a, uint32_t e) -> uint4 {
-        uint4 v = {0u, 0u, 0u, 0u};
-        if (ln < 55 && a + 16u * (uint32_t)ln < e) v = *(const uint4*)(frec + a + 16u * (uint32_t)ln);
-        return v;
+        const uint32_t o = a + 16u * (uint32_t)ln;
+        const zu4 v = bld128(rrec, ln < 55 && o < e ? o : ZW_OOB);
+        return make_uint4(v.x, v.y, v.z, v.w);
     };
-    uint32_t a1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[1]);
-    uint32_t a2 = mbw >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[2]) : 0u;
-    uint4 nxt = load_rec(lane, (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo[0]), a1);
+    uint32_t a1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo_f[row0 + 1]);
+    uint32_t a2 = mbw >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo_f[row0 + 2]) : 0u;
+    uint4 nxt = load_rec(lane, (uint32_t)__builtin_amdgcn_readfirstlane((int)fmo_f[row0]), a1);
     for (int mbx = 0; mbx < mbw; mbx++) {
         // the lane's roles, recomputed per MB from an opaque copy of the lane id:
         // hoisted out of the loop, their exec masks were spilled to VGPR lanes
         // and reloaded with v_readlane every MB
         const int lane = pin(lane0);
         const uint4 cur = nxt;
-        if (mbx + 1 < mbw) nxt = load_rec(lane, (uint32_t)__builtin_amdgcn_readfirstlane((int)a1),
-                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)a2));  // MB x+1
+        nxt = load_rec(mbx + 1 < mbw ? lane : 64, (uint32_t)__builtin_amdgcn_readfirstlane((int)a1),
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)a2));  // MB x+1
         a1 = a2;
         // (a vector load: a scalar one would be waited for with lgkmcnt(0) by the
         // next LDS access, a full memory round trip per MB)
-        if (mbx + 3 <= mbw) a2 = fmo[mbx + 3 + (lane >> 6)];
+        a2 = bld32(rmo, mbx + 3 <= mbw ? (row0 + (uint32_t)mbx + 3u) * 4u : ZW_OOB);
 #ifndef ZW_EXP_NO_WAIT
         if (mby > 0) wait(min(mbx + 2, mbw));
 #endif
@@ -619,8 +649,6 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             W->left_v[0] = (uint8_t)corner_v;
         }
         if (lane < 32 && cbx == 1) (pl ? W->left_v : W->left_u)[1 + 4 * cby + q] = (uint8_t)(RC >> 24);
-        uint8_t* yo = Y + (size_t)f * ysz + (size_t)mby * 16 * ys + mbx * 16;
-        uint8_t* co = (pl ? V : U) + (size_t)f * csz + (size_t)mby * 8 * cs + mbx * 8;
         if (XCU) {  // bottom rows for the row below (sc1), then publish, then the planes
             if (by == 3 && q == 3) st_sc1(gty + mbx * 16 + 4 * bx, RW);
             if (lane < 32 && cby == 1 && q == 3) st_sc1((pl ? gtv : gtu) + mbx * 8 + 4 * cbx, RC);
@@ -630,11 +658,14 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             if (lane < 32 && cby == 1 && q == 3) *(uint32_t*)((pl ? gtv : gtu) + mbx * 8 + 4 * cbx) = RC;
             pub(mbx + 1);
         }
-        *(uint32_t*)(yo + (size_t)(4 * by + q) * ys + 4 * bx) = RW;
-        if (lane < 32) *(uint32_t*)(co + (size_t)(4 * cby + q) * cs + 4 * cbx) = RC;
-        if (lane < 4) {
+        {
+            const uint32_t oy = (uint32_t)((mby * 16 + 4 * by + q) * ys + mbx * 16 + 4 * bx);
+            const uint32_t oc = (uint32_t)((mby * 8 + 4 * cby + q) * cs + mbx * 8 + 4 * cbx);
+            bst32(RW, ryp, oy);
+            bst32(RC, rup, lane < 32 && !pl ? oc : ZW_OOB);
+            bst32(RC, rvp, lane < 32 && pl ? oc : ZW_OOB);
             const int v = lane == 0 ? lm : (lane == 1 ? seg : (lane == 2 ? skip : nzdct));
-            flags[((size_t)f * nmb + (size_t)mby * mbw + mbx) * 4 + lane] = (uint8_t)v;
+            bst8((uint32_t)v, rfl, lane < 4 ? (row0 + (uint32_t)mbx) * 4u + (uint32_t)lane : ZW_OOB);
         }
         wsync();
     }
@@ -756,10 +787,10 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const uint8_t* __restrict
 // always: the row above left them to this row; the last MB row also stores its
 // own rows 12..15).  No two waves store the same bytes.
 template <class PF>
-__device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilterParams& F, uint8_t* Yf, uint8_t* Uf,
-                                        uint8_t* Vf, int ys, int cs, int mbx, int mby, uint32_t fl, uint32_t cy0,
-                                        uint32_t cy1, uint32_t cc, uint8_t* hy, uint8_t* hu, uint8_t* hv, bool last,
-                                        PF&& prefetch)
+__device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilterParams& F, __amdgpu_buffer_rsrc_t ry,
+                                        __amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, int ys, int cs, int mbx,
+                                        int mby, uint32_t fl, uint32_t cy0, uint32_t cy1, uint32_t cc, uint8_t* hy,
+                                        uint8_t* hu, uint8_t* hv, bool last, PF&& prefetch)
 {
     const bool chroma = !F.filter_type;
     const int i4 = (fl & 255u) == 4u, seg = (int)((fl >> 8) & 3u), skip = (int)((fl >> 16) & 255u), nzd = (int)(fl >> 24);
@@ -796,44 +827,44 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
     lf_filter_tile(L, hl, on && lvl != 0, F.filter_type != 0, chroma, mbx > 0, mby > 0, i4 || (!skip && nzd), ht, il,
                    (lvl + 2) * 2 + il, lvl * 2 + il);
 #endif
-    if (!on) return;
     auto tile_y = [&](int r, int w) { return ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]; };
     auto tile_c = [&](int pl, int r, int w) { return ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]; };
     // hand-off rows: luma rows 12..15 (20 words with the carried columns), chroma 4..7 (24)
-    if (hl < 20) {
+    if (on && hl < 20) {
         const int r = 12 + hl / 5, w = hl % 5 - 1;
         if (x0 + 4 * w >= 0) *(uint32_t*)(hy + (r - 12) * ys + x0 + 4 * w) = tile_y(r, w);
     }
-    if (chroma && hl < 24) {
+    if (on && chroma && hl < 24) {
         const int pl = hl / 12, rr = hl % 12, r = 4 + rr / 3, w = rr % 3 - 1;
         if (mbx * 8 + 4 * w >= 0) *(uint32_t*)((pl ? hv : hu) + (r - 4) * cs + mbx * 8 + 4 * w) = tile_c(pl, r, w);
     }
-    // the planes: every LDS read first, then the stores (unrolled: 4 luma + 3 chroma words a lane)
     const bool wb = lvl != 0;
+#ifdef ZW_EXP_NO_WB
+    return;
+#endif
     // the planes, one tile row per lane (luma: a word for the carried columns + 16 bytes;
     // chroma: a word + 8 bytes): rows -4..-1 always (the row above left them to this
-    // row), rows 0..11 (chroma 0..3) when filtered, 12..15 (4..7) also in the last MB row
-    if (hl < LFY) {
-        const int r = hl - 4;
-        if (r < 0 ? mby > 0 : (wb && (r < 12 || last))) {
-            const uint32_t* row = (const uint32_t*)(L->y + hl * LFY);
-            const uint32_t w0 = row[0];
-            const uint4 wv = make_uint4(row[1], row[2], row[3], row[4]);
-            uint8_t* dst = Yf + (y0 + r) * ys + x0;
-            if (mbx > 0) *(uint32_t*)(dst - 4) = w0;
-            *(uint4*)dst = wv;
-        }
+    // row), rows 0..11 (chroma 0..3) when filtered, 12..15 (4..7) also in the last MB row.
+    // Every lane issues every store; the ones not wanted go to ZW_OOB.
+    {
+        const int lr = min(hl, LFY - 1), r = lr - 4;
+        const bool need = on && hl < LFY && (r < 0 ? mby > 0 : (wb && (r < 12 || last)));
+        const uint32_t* row = (const uint32_t*)(L->y + lr * LFY);
+        const zu4 wv = {row[1], row[2], row[3], row[4]};
+        const uint32_t off = (uint32_t)((y0 + r) * ys + x0);
+        bst32(row[0], ry, need && mbx > 0 ? off - 4 : ZW_OOB);
+        bst128(wv, ry, need ? off : ZW_OOB);
     }
-    if (chroma && hl < 2 * LFC) {
-        const int pl = hl >= LFC, rr = hl - LFC * pl, r = rr - 4;
-        if (r < 0 ? mby > 0 : (wb && (r < 4 || last))) {
-            const uint32_t* row = (const uint32_t*)((pl ? L->v : L->u) + rr * LFC);
-            const uint32_t w0 = row[0];
-            const uint2 wv = make_uint2(row[1], row[2]);
-            uint8_t* dst = (pl ? Vf : Uf) + (mby * 8 + r) * cs + mbx * 8;
-            if (mbx > 0) *(uint32_t*)(dst - 4) = w0;
-            *(uint2*)dst = wv;
-        }
+    {
+        const int lr = min(hl, 2 * LFC - 1), pl = lr >= LFC, rr = lr - LFC * pl, r = rr - 4;
+        const bool need = on && chroma && hl < 2 * LFC && (r < 0 ? mby > 0 : (wb && (r < 4 || last)));
+        const uint32_t* row = (const uint32_t*)((pl ? L->v : L->u) + rr * LFC);
+        const zu2 wv = {row[1], row[2]};
+        const uint32_t off = (uint32_t)((mby * 8 + r) * cs + mbx * 8);
+        bst32(row[0], ru, need && !pl && mbx > 0 ? off - 4 : ZW_OOB);
+        bst64(wv, ru, need && !pl ? off : ZW_OOB);
+        bst32(row[0], rv, need && pl && mbx > 0 ? off - 4 : ZW_OOB);
+        bst64(wv, rv, need && pl ? off : ZW_OOB);
     }
 }
 
@@ -870,21 +901,27 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
     uint8_t* Uf = U + (size_t)f * csz;
     uint8_t* Vf = V + (size_t)f * csz;
     const bool chroma = !F.filter_type;
-    const uint8_t* fflags = flags + (size_t)f * nmb * 4;
-    auto load = [&](int my, int mx, uint32_t& y0w, uint32_t& y1w, uint32_t& cw, uint32_t& flw) {
-        const uint8_t* yb = Yf + (size_t)(my * 16) * ys + mx * 16 + 4 * (hl & 3);
-        y0w = *(const uint32_t*)(yb + (size_t)(hl >> 2) * ys);
-        y1w = *(const uint32_t*)(yb + (size_t)(8 + (hl >> 2)) * ys);
-        cw = chroma ? *(const uint32_t*)((((hl >> 4) & 1) ? Vf : Uf) + (size_t)(my * 8 + ((hl >> 1) & 7)) * cs + mx * 8 +
-                                         4 * (hl & 1))
-                    : 0u;
-        flw = *(const uint32_t*)(fflags + ((size_t)my * mbw + mx) * 4);
+    const __amdgpu_buffer_rsrc_t ry = brsrc(Yf, (uint32_t)ysz), ru = brsrc(Uf, (uint32_t)csz), rv = brsrc(Vf, (uint32_t)csz);
+    const __amdgpu_buffer_rsrc_t rf = brsrc(flags + (size_t)f * nmb * 4, (uint32_t)(nmb * 4));
+    // the interior words and the flags of MB (mx, my) (every lane loads; invalid -> ZW_OOB -> 0)
+    auto load = [&](bool valid, int my, int mx, uint32_t& y0w, uint32_t& y1w, uint32_t& cw, uint32_t& flw) {
+#ifdef ZW_EXP_NO_LOAD
+        y0w = y1w = cw = (uint32_t)(mx * 77 + hl); flw = 0x01000000u | (uint32_t)(mx & 1);
+        return;
+#endif
+        const uint32_t oy = (uint32_t)((my * 16 + (hl >> 2)) * ys + mx * 16 + 4 * (hl & 3));
+        y0w = bld32(ry, valid ? oy : ZW_OOB);
+        y1w = bld32(ry, valid ? oy + 8u * (uint32_t)ys : ZW_OOB);
+        const uint32_t oc = (uint32_t)((my * 8 + ((hl >> 1) & 7)) * cs + mx * 8 + 4 * (hl & 1));
+        const bool cv = valid && chroma;
+        cw = bld32(ru, cv && !((hl >> 4) & 1) ? oc : ZW_OOB) | bld32(rv, cv && ((hl >> 4) & 1) ? oc : ZW_OOB);
+        flw = bld32(rf, valid ? (uint32_t)((my * mbw + mx) * 4) : ZW_OOB);
     };
     for (int pr = wv; 2 * pr < mbh; pr += NWD) {
         const int my = 2 * pr + h;  // this half's MB row
         const bool rowok = my < mbh;
         uint32_t ny0 = 0, ny1 = 0, nc = 0, nfl = 0;
-        if (rowok && h == 0) load(my, 0, ny0, ny1, nc, nfl);  // step 0: the lower half starts at step 2
+        load(rowok && h == 0, my, 0, ny0, ny1, nc, nfl);  // step 0: the lower half starts at step 2
         for (int st = 0; st < mbw + 2; st++) {
             const int mx = st - 2 * h;
             const bool on = rowok && mx >= 0 && mx < mbw;
@@ -892,8 +929,8 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
 #ifndef ZW_EXP_NO_WAIT
             if (pr > 0 && st < mbw) dec_wait(progress, (pr - 1) % NWD, (pr - 1) * 65536 + min(st + 2, mbw));
 #endif
-            if (rowok && mx + 1 >= 0 && mx + 1 < mbw) load(my, mx + 1, ny0, ny1, nc, nfl);
-            lf_half(L, hl, on, F, Yf, Uf, Vf, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1, [] {});
+            load(rowok && mx + 1 >= 0 && mx + 1 < mbw, my, mx + 1, ny0, ny1, nc, nfl);
+            lf_half(L, hl, on, F, ry, ru, rv, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1, [] {});
             wsync();
             if (st >= 2) dec_publish(progress, wv, pr * 65536 + st - 1);  // the lower row has finished st - 1 MBs
         }
