@@ -1127,116 +1127,117 @@ __device__ __forceinline__ uint32_t yuv2rgb_px(const uint8_t* Y, const uint8_t* 
     return yuv_px(yv, u, v);
 }
 
-__device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int i)  // i constant after unrolling
-{
-    const uint32_t w = i < 4 ? w0 : (i < 8 ? w1 : w2);
-    return (int)((w >> (8 * (i & 3))) & 255u);
-}
-
-// One thread per 8 horizontally adjacent pixels of one output row (x = 8 *
-// thread): Y as one 8-byte load, each chroma row as three aligned words
-// covering columns x/2-4 .. x/2+7, so the interior does two vector loads per
-// plane row and no per-sample addressing; the 8 pixels leave as two 16-byte
-// (RGBA) or six 4-byte (RGB) stores.  Threads at the image edges, or whose
-// row start is not 4-byte aligned in the packed RGB output, take the
-// per-pixel form.
+// One thread per 8 horizontally adjacent pixels of an output ROW PAIR: rows
+// 2j-1 and 2j blend the same two chroma rows (j-1 and j, clamped), with their
+// main / secondary roles swapped (fancy) or one each (simple), so the pair
+// shares one set of chroma loads.  Y is one 8-byte load per row, each chroma
+// row three aligned words covering columns x/2-4 .. x/2+7; the 8 pixels of a
+// row leave as two 16-byte nontemporal stores (RGBA; the output is written
+// once and not read back here) or six 4-byte stores (RGB).  Threads at the
+// image edges, or whose rows do not start 4-byte aligned in the packed output,
+// take the per-pixel form.
 template <int BPP, bool FANCY>
 __global__ __launch_bounds__(256) void k_yuv2rgb(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
                                                  const uint8_t* __restrict__ V, size_t ysz, size_t csz, int w, int h,
                                                  int ys, int cs, uint8_t* __restrict__ out)
 {
-    const int f = blockIdx.z, r = blockIdx.y;
+    const int f = blockIdx.z, j = blockIdx.y;
     const int x = (int)(blockIdx.x * 256u + threadIdx.x) * 8;
     if (x >= w) return;
     Y += (size_t)f * ysz;
     U += (size_t)f * csz;
     V += (size_t)f * csz;
-    uint8_t* o = out + ((size_t)f * h + r) * (size_t)w * BPP + (size_t)x * BPP;
     const int cw1 = ((w + 1) >> 1) - 1, ch1 = ((h + 1) >> 1) - 1;
+    const int rA = 2 * j - 1, rB = 2 * j;  // rA = -1 / rB = h: not in the image
+    const bool hasA = rA >= 0, hasB = rB < h;
+    const int cA = max(j - 1, 0), cB = min(j, ch1);  // chroma rows: row rA (main cA), row rB (main cB)
+    uint8_t* oA = out + ((size_t)f * h + (size_t)max(rA, 0)) * (size_t)w * BPP + (size_t)x * BPP;
+    uint8_t* oB = out + ((size_t)f * h + (size_t)min(rB, h - 1)) * (size_t)w * BPP + (size_t)x * BPP;
+    const uintptr_t am = BPP == 4 ? 15 : 3;
     // (every full 8-pixel run takes the vector path; at the image's left / right
     // edge the fancy filter's outer chroma column is the edge column itself, so
     // the neighbour word is not loaded and the edge byte stands in for it)
-    const bool fast = x + 8 <= w && (ys & 7) == 0 && (cs & 3) == 0 && ((uintptr_t)o & (BPP == 4 ? 15 : 3)) == 0;
-    uint32_t px[8];
+    const bool fast = x + 8 <= w && (ys & 7) == 0 && (cs & 3) == 0 && (((uintptr_t)oA | (uintptr_t)oB) & am) == 0;
     if (fast) {
-        const uint2 yy = *(const uint2*)(Y + (size_t)r * ys + x);
         const bool lok = x > 0, rok = (x >> 1) + 4 <= cw1;
         const int c1 = x >> 1, c0 = lok ? c1 - 4 : c1, c2 = rok ? c1 + 4 : c1;
-        int mr, sr;
-        if (FANCY) {
-            const int k = (r + 1) >> 1;
-            mr = (r & 1) ? k - 1 : k;
-            sr = max(min((r & 1) ? k : k - 1, ch1), 0);
-        } else {
-            mr = sr = r >> 1;
-        }
-        auto row3 = [&](const uint8_t* P, int rr, int& b0, int& b5, uint32_t& mid) {
+        // the six local chroma columns x/2-1 .. x/2+4 of one plane row
+        auto cols = [&](const uint8_t* P, int rr, int* c6) {
             const uint8_t* q = P + (size_t)rr * cs;
             const uint32_t a = *(const uint32_t*)(q + c0), m = *(const uint32_t*)(q + c1), z = *(const uint32_t*)(q + c2);
-            b0 = (int)(lok ? a >> 24 : m & 255u);
-            b5 = (int)(rok ? z & 255u : m >> 24);
-            mid = m;
+            c6[0] = (int)(lok ? a >> 24 : m & 255u);
+            c6[5] = (int)(rok ? z & 255u : m >> 24);
+#pragma unroll
+            for (int k = 1; k < 5; k++) c6[k] = (int)((m >> (8 * (k - 1))) & 255u);
         };
-        int um_l, um_r, vm_l, vm_r, us_l, us_r, vs_l, vs_r;
-        uint32_t umw, vmw, usw, vsw;
-        row3(U, mr, um_l, um_r, umw);
-        row3(V, mr, vm_l, vm_r, vmw);
-        if (FANCY) {
-            row3(U, sr, us_l, us_r, usw);
-            row3(V, sr, vs_l, vs_r, vsw);
-        } else {
-            us_l = um_l, us_r = um_r, usw = umw, vs_l = vm_l, vs_r = vm_r, vsw = vmw;
-        }
-        // fancy: 9 m + 3 s1 + 3 s2 + t = 3 (3 um + us)[mc] + (3 um + us)[sc], so
-        // blend the two chroma rows once per column (local columns x/2-1 .. x/2+4)
-        int tu[6], tv[6];
+        int uA[6], uB[6], vA[6], vB[6];
+        cols(U, cA, uA);
+        cols(V, cA, vA);
+        cols(U, cB, uB);
+        cols(V, cB, vB);
+        auto row8 = [&](uint2 yy, bool rowA, uint32_t* px) {
+            // fancy: 9 m + 3 s1 + 3 s2 + t = 3 (3 m + s)[mc] + (3 m + s)[sc] per column pair
+            int tu[6], tv[6];
 #pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const int um = j == 0 ? um_l : (j == 5 ? um_r : (int)((umw >> (8 * (j - 1))) & 255u));
-            const int us = j == 0 ? us_l : (j == 5 ? us_r : (int)((usw >> (8 * (j - 1))) & 255u));
-            const int vm = j == 0 ? vm_l : (j == 5 ? vm_r : (int)((vmw >> (8 * (j - 1))) & 255u));
-            const int vs = j == 0 ? vs_l : (j == 5 ? vs_r : (int)((vsw >> (8 * (j - 1))) & 255u));
-            if (FANCY) {
-                tu[j] = 3 * um + us;
-                tv[j] = 3 * vm + vs;
+            for (int k = 0; k < 6; k++) {
+                if (FANCY) {
+                    tu[k] = rowA ? 3 * uA[k] + uB[k] : 3 * uB[k] + uA[k];
+                    tv[k] = rowA ? 3 * vA[k] + vB[k] : 3 * vB[k] + vA[k];
+                } else {
+                    tu[k] = rowA ? uA[k] : uB[k];
+                    tv[k] = rowA ? vA[k] : vB[k];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int yv = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 255u);
+                const int jm = 1 + (i >> 1);  // local chroma column of pixel x + i
+                int u, v;
+                if (FANCY) {
+                    const int js = (i & 1) ? jm + 1 : jm - 1;
+                    u = (3 * tu[jm] + tu[js] + 8) >> 4;
+                    v = (3 * tv[jm] + tv[js] + 8) >> 4;
+                } else {
+                    u = tu[jm];
+                    v = tv[jm];
+                }
+                px[i] = yuv_px(yv, u, v);
+            }
+        };
+        auto store8 = [&](uint8_t* o, const uint32_t* px) {
+            if (BPP == 4) {
+                __builtin_nontemporal_store(zu4{px[0], px[1], px[2], px[3]}, (zu4*)o);
+                __builtin_nontemporal_store(zu4{px[4], px[5], px[6], px[7]}, (zu4*)o + 1);
             } else {
-                tu[j] = um;
-                tv[j] = vm;
-            }
-        }
+                uint32_t* d = (uint32_t*)o;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int yv = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 255u);
-            const int jm = 1 + (i >> 1);  // local chroma column (x + i) / 2 - 3
-            int u, v;
-            if (FANCY) {
-                const int js = (i & 1) ? jm + 1 : jm - 1;
-                u = (3 * tu[jm] + tu[js] + 8) >> 4;
-                v = (3 * tv[jm] + tv[js] + 8) >> 4;
-            } else {
-                u = tu[jm];
-                v = tv[jm];
+                for (int g = 0; g < 2; g++) {
+                    const uint32_t p0 = px[4 * g], p1 = px[4 * g + 1], p2 = px[4 * g + 2], p3 = px[4 * g + 3];
+                    d[3 * g + 0] = (p0 & 0xffffffu) | (p1 << 24);
+                    d[3 * g + 1] = ((p1 >> 8) & 0xffffu) | (p2 << 16);
+                    d[3 * g + 2] = ((p2 >> 16) & 0xffu) | ((p3 & 0xffffffu) << 8);
+                }
             }
-            px[i] = yuv_px(yv, u, v);
+        };
+        uint32_t px[8];
+        if (hasA) {
+            row8(*(const uint2*)(Y + (size_t)rA * ys + x), true, px);
+            store8(oA, px);
         }
-        if (BPP == 4) {
-            ((uint4*)o)[0] = make_uint4(px[0], px[1], px[2], px[3]);
-            ((uint4*)o)[1] = make_uint4(px[4], px[5], px[6], px[7]);
-        } else {
-            uint32_t* d = (uint32_t*)o;
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                const uint32_t p0 = px[4 * g], p1 = px[4 * g + 1], p2 = px[4 * g + 2], p3 = px[4 * g + 3];
-                d[3 * g + 0] = (p0 & 0xffffffu) | (p1 << 24);
-                d[3 * g + 1] = ((p1 >> 8) & 0xffffu) | (p2 << 16);
-                d[3 * g + 2] = ((p2 >> 16) & 0xffu) | ((p3 & 0xffffffu) << 8);
-            }
+        if (hasB) {
+            row8(*(const uint2*)(Y + (size_t)rB * ys + x), false, px);
+            store8(oB, px);
         }
     } else {
         const int n = min(8, w - x);
-        for (int i = 0; i < n; i++) {
-            const uint32_t p = yuv2rgb_px<FANCY>(Y, U, V, ys, cs, cw1, ch1, r, x + i);
-            for (int c = 0; c < BPP; c++) o[(size_t)i * BPP + c] = (uint8_t)(p >> (8 * c));
+        for (int t = 0; t < 2; t++) {
+            const int r = t ? rB : rA;
+            if (r < 0 || r >= h) continue;
+            uint8_t* o = t ? oB : oA;
+            for (int i = 0; i < n; i++) {
+                const uint32_t p = yuv2rgb_px<FANCY>(Y, U, V, ys, cs, cw1, ch1, r, x + i);
+                for (int c = 0; c < BPP; c++) o[(size_t)i * BPP + c] = (uint8_t)(p >> (8 * c));
+            }
         }
     }
 }
@@ -1245,7 +1246,7 @@ extern "C" hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t
                                   size_t csz, int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out,
                                   int nframes)
 {
-    const dim3 grid(((unsigned)w + 2047) / 2048, (unsigned)h, (unsigned)nframes);
+    const dim3 grid(((unsigned)w + 2047) / 2048, (unsigned)h / 2 + 1, (unsigned)nframes);  // row pairs (2j-1, 2j)
     if (bpp == 4) {
         if (fancy) hipLaunchKernelGGL((k_yuv2rgb<4, true>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
         else hipLaunchKernelGGL((k_yuv2rgb<4, false>), grid, dim3(256), 0, s, Y, U, V, ysz, csz, w, h, ys, cs, out);
