@@ -23,7 +23,7 @@
 extern "C" {
 hipError_t zwk_dec_recon(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
                          const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V, uint8_t* flags, int mbw, int mbh,
-                         size_t ysz, size_t csz, int nframes);
+                         size_t ysz, size_t csz, int nframes, uint8_t* tiles);
 hipError_t zwk_yuv2rgb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, size_t ysz, size_t csz,
                        int w, int h, int ys, int cs, int bpp, int fancy, uint8_t* out, int nframes);
 hipError_t zwk_dec_rows(hipStream_t s, int phase, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
@@ -33,7 +33,7 @@ hipError_t zwk_dec_rows_init(hipStream_t s, int* rowsync, int mbh, int nframes);
 size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
-                          const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw);
+                          const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw, const uint8_t* tiles);
 }
 
 namespace {
@@ -630,7 +630,8 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     const bool rows = rows_env >= 0 ? rows_env != 0 : n < 128;  // measured: rows faster up to 64, slower at 256
     const size_t o_rs = al256(o_v + (size_t)n * csz);
     const size_t o_bd = al256(o_rs + (rows ? zw_dec_rows_sync_bytes(mbh, n) : 0));
-    const size_t o_extra = al256(o_bd + (rows ? zw_dec_rows_border_bytes(mbw, n) : 0));
+    const size_t o_t = al256(o_bd + (rows ? zw_dec_rows_border_bytes(mbw, n) : 0));  // batch: recon -> filter MB tiles
+    const size_t o_extra = al256(o_t + (rows ? 0 : (size_t)n * nmb * 384));
     const size_t total = al256(o_extra + extra_bytes);
     uint8_t* d = (uint8_t*)ctx_scratch(ctx, total, bi);
     if (!d) return ZW_ENOMEM;
@@ -659,9 +660,11 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
         HIPOK(zwk_dec_rows(s, 2, nullptr, nullptr, nullptr, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl,
                            (const ZwFilterParams*)(d + o_fp), mbw, mbh, ysz, csz, n, rs, d + o_bd, mbh));
     } else {
-        HIPOK(zwk_dec_recon(s, recs, moff, fbase, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz, csz, n));
+        HIPOK(zwk_dec_recon(s, recs, moff, fbase, d + o_q, d + o_y, d + o_u, d + o_v, d + o_fl, mbw, mbh, ysz, csz, n,
+                            d + o_t));
         HIPOK(hipEventRecord(ev[1], s));
-        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n, mbw));
+        HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, n, mbw,
+                             d + o_t));
     }
     HIPOK(hipEventRecord(ev[2], s));
     if (dec_timing()) {
@@ -989,7 +992,7 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
                            (int)mbw, (int)mbh, ysz, csz, 1, (int*)(d + o_rs), nullptr, (int)mbh));
     } else {
         HIPOK(zwk_loopfilter(s, d + o_y, d + o_u, d + o_v, d + o_fl, (const ZwFilterParams*)(d + o_fp), ysz, csz, 1,
-                             (int)mbw));
+                             (int)mbw, nullptr));
     }
     HIPOK(hipMemcpyAsync(y, d + o_y, ysz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(u, d + o_u, csz, hipMemcpyDeviceToHost, s));

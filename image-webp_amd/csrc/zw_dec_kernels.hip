@@ -23,6 +23,7 @@
 #endif
 #define NWD ZW_NWD
 #define WGD (NWD * 64)
+#define ZW_DEC_TILE 384  // batch recon -> filter hand-over: one MB, luma 16 x 16 then U, V 8 x 8
 
 struct ZwDecQuant {
     int32_t ydc, yac, y2dc, y2ac, uvdc, uvac;
@@ -443,7 +444,7 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
                                               const uint64_t* __restrict__ fbase, const ZwDecQuant* __restrict__ quant, uint8_t* Y,
                                               uint8_t* U, uint8_t* V, uint8_t* flags, int f, int mbw, int mbh,
                                               size_t ysz, size_t csz, int mby, DecLds* W, uint8_t* gty, uint8_t* gtu,
-                                              uint8_t* gtv, WAIT&& wait, PUB&& pub)
+                                              uint8_t* gtv, uint8_t* tiles, WAIT&& wait, PUB&& pub)
 {
     const int lane0 = threadIdx.x & 63;
     const int ys = mbw * 16, cs = mbw * 8;
@@ -465,6 +466,10 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
     const __amdgpu_buffer_rsrc_t rup = brsrc(U + (size_t)f * csz, (uint32_t)csz);
     const __amdgpu_buffer_rsrc_t rvp = brsrc(V + (size_t)f * csz, (uint32_t)csz);
     const __amdgpu_buffer_rsrc_t rfl = brsrc(flags + (size_t)f * nmb * 4, (uint32_t)nmb * 4u);
+    // !XCU: the MBs go to the frame's tiles (ZW_DEC_TILE bytes each: luma 16 x 16, U, V 8 x 8,
+    // row-major), whole cache lines; k_loopfilter reads them and writes the planes
+    const __amdgpu_buffer_rsrc_t rty = brsrc(XCU ? (const uint8_t*)Y : tiles + (size_t)f * nmb * ZW_DEC_TILE,
+                                             XCU ? 0u : (uint32_t)(nmb * ZW_DEC_TILE));
     const uint32_t row0 = (uint32_t)(mby * mbw);
     auto load_rec = [&](int ln, uint32_t a, uint32_t e) -> uint4 {
         const uint32_t o = a + 16u * (uint32_t)ln;
@@ -658,12 +663,18 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
             if (lane < 32 && cby == 1 && q == 3) *(uint32_t*)((pl ? gtv : gtu) + mbx * 8 + 4 * cbx) = RC;
             pub(mbx + 1);
         }
-        {
+        if (XCU) {
             const uint32_t oy = (uint32_t)((mby * 16 + 4 * by + q) * ys + mbx * 16 + 4 * bx);
             const uint32_t oc = (uint32_t)((mby * 8 + 4 * cby + q) * cs + mbx * 8 + 4 * cbx);
             bst32(RW, ryp, oy);
             bst32(RC, rup, lane < 32 && !pl ? oc : ZW_OOB);
             bst32(RC, rvp, lane < 32 && pl ? oc : ZW_OOB);
+        } else {
+            const uint32_t tb = (row0 + (uint32_t)mbx) * ZW_DEC_TILE;
+            bst32(RW, rty, tb + (uint32_t)((4 * by + q) * 16 + 4 * bx));
+            bst32(RC, rty, lane < 32 ? tb + 256u + (uint32_t)(pl * 64 + (4 * cby + q) * 8 + 4 * cbx) : ZW_OOB);
+        }
+        {
             const int v = lane == 0 ? lm : (lane == 1 ? seg : (lane == 2 ? skip : nzdct));
             bst8((uint32_t)v, rfl, lane < 4 ? (row0 + (uint32_t)mbx) * 4u + (uint32_t)lane : ZW_OOB);
         }
@@ -676,7 +687,7 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
                                                               const uint64_t* __restrict__ fbase,
                                                               const ZwDecQuant* __restrict__ quant, uint8_t* Y, uint8_t* U,
                                                               uint8_t* V, uint8_t* flags, int mbw, int mbh, size_t ysz,
-                                                              size_t csz)
+                                                              size_t csz, uint8_t* tiles)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(WGD) __attribute__((amdgpu_waves_per_eu(NWD / 4, NW
     __syncthreads();
     for (int mby = wv; mby < mbh; mby += NWD) {
         dec_recon_row<false>(
-            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v,
+            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, top_y, top_u, top_v, tiles,
             [&](int need) { dec_wait(progress, (mby - 1) % NWD, (mby - 1) * 65536 + need); },
             [&](int done) { dec_publish(progress, wv, mby * 65536 + done); });
     }
@@ -772,7 +783,7 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const uint8_t* __restrict
         if (mby >= mbh) break;
         int seen = -1;
         dec_recon_row<true>(
-            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, gty, gtu, gtv,
+            recs, moff, fbase, W->q, Y, U, V, flags, f, mbw, mbh, ysz, csz, mby, W, gty, gtu, gtv, nullptr,
             [&](int need) { row_wait(&prog[mby - 1], need, &rs[2], seen); },
             [&](int done) { row_publish(&prog[mby], done); });
     }
@@ -787,12 +798,13 @@ __global__ __launch_bounds__(64) void k_dec_recon_rows(const uint8_t* __restrict
 // always: the row above left them to this row; the last MB row also stores its
 // own rows 12..15).  No two waves store the same bytes.
 template <class PF>
+// cmove: chroma is moved (tile -> planes) even when the simple filter leaves it alone.
 __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilterParams& F, __amdgpu_buffer_rsrc_t ry,
                                         __amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, int ys, int cs, int mbx,
                                         int mby, uint32_t fl, uint32_t cy0, uint32_t cy1, uint32_t cc, uint8_t* hy,
-                                        uint8_t* hu, uint8_t* hv, bool last, PF&& prefetch)
+                                        uint8_t* hu, uint8_t* hv, bool last, bool cmove, PF&& prefetch)
 {
-    const bool chroma = !F.filter_type;
+    const bool chroma = cmove;  // (staging, hand-off and stores; the filter itself takes !F.filter_type)
     const int i4 = (fl & 255u) == 4u, seg = (int)((fl >> 8) & 3u), skip = (int)((fl >> 16) & 255u), nzd = (int)(fl >> 24);
     const int lvl = F.level[seg][i4], il = F.ilimit[seg][i4], ht = F.hev[seg][i4];
     const int x0 = mbx * 16, y0 = mby * 16;
@@ -824,8 +836,8 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
     prefetch();  // the next step's interior: issued once this one's is in LDS (fewer live registers)
     wsync();
 #ifndef ZW_EXP_NO_LF
-    lf_filter_tile(L, hl, on && lvl != 0, F.filter_type != 0, chroma, mbx > 0, mby > 0, i4 || (!skip && nzd), ht, il,
-                   (lvl + 2) * 2 + il, lvl * 2 + il);
+    lf_filter_tile(L, hl, on && lvl != 0, F.filter_type != 0, !F.filter_type, mbx > 0, mby > 0, i4 || (!skip && nzd),
+                   ht, il, (lvl + 2) * 2 + il, lvl * 2 + il);
 #endif
     auto tile_y = [&](int r, int w) { return ((const uint32_t*)(L->y + (r + 4) * LFY))[w + 1]; };
     auto tile_c = [&](int pl, int r, int w) { return ((const uint32_t*)((pl ? L->v : L->u) + (r + 4) * LFC))[w + 1]; };
@@ -844,11 +856,13 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
 #endif
     // the planes, one tile row per lane (luma: a word for the carried columns + 16 bytes;
     // chroma: a word + 8 bytes): rows -4..-1 always (the row above left them to this
-    // row), rows 0..11 (chroma 0..3) when filtered, 12..15 (4..7) also in the last MB row.
-    // Every lane issues every store; the ones not wanted go to ZW_OOB.
+    // row), rows 0..11 (chroma 0..3) always (the planes get every byte from here), 12..15
+    // (4..7) in the last MB row.  Every lane issues every store; the ones not wanted go to
+    // ZW_OOB.
+    (void)wb;
     {
         const int lr = min(hl, LFY - 1), r = lr - 4;
-        const bool need = on && hl < LFY && (r < 0 ? mby > 0 : (wb && (r < 12 || last)));
+        const bool need = on && hl < LFY && (r < 0 ? mby > 0 : (r < 12 || last));
         const uint32_t* row = (const uint32_t*)(L->y + lr * LFY);
         const zu4 wv = {row[1], row[2], row[3], row[4]};
         const uint32_t off = (uint32_t)((y0 + r) * ys + x0);
@@ -857,7 +871,7 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
     }
     {
         const int lr = min(hl, 2 * LFC - 1), pl = lr >= LFC, rr = lr - LFC * pl, r = rr - 4;
-        const bool need = on && chroma && hl < 2 * LFC && (r < 0 ? mby > 0 : (wb && (r < 4 || last)));
+        const bool need = on && chroma && hl < 2 * LFC && (r < 0 ? mby > 0 : (r < 4 || last));
         const uint32_t* row = (const uint32_t*)((pl ? L->v : L->u) + rr * LFC);
         const zu2 wv = {row[1], row[2]};
         const uint32_t off = (uint32_t)((mby * 8 + r) * cs + mbx * 8);
@@ -876,10 +890,12 @@ __device__ __forceinline__ void lf_half(LfLds* L, int hl, bool on, const ZwFilte
 // the serial steps of one row per wave.  The next pair's upper row waits on the
 // lower row's progress.  The rows hand over through LDS (hy/hu/hv: the last
 // filtered MB row's bottom 4 rows, plane-wide).
+// tiles: the batch reconstruction's MB tiles (ZW_DEC_TILE bytes per MB), or nullptr:
+// the planes hold the unfiltered frame (the loop-filter-only entry point).
 extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8_t* U, uint8_t* V,
                                                                const uint8_t* __restrict__ flags,
                                                                const ZwFilterParams* __restrict__ fp, size_t ysz,
-                                                               size_t csz)
+                                                               size_t csz, const uint8_t* __restrict__ tiles)
 {
     __shared__ __attribute__((aligned(16))) LfLds lds[NWD][2];
     __shared__ int progress[NWD];
@@ -900,8 +916,10 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
     uint8_t* Yf = Y + (size_t)f * ysz;
     uint8_t* Uf = U + (size_t)f * csz;
     uint8_t* Vf = V + (size_t)f * csz;
-    const bool chroma = !F.filter_type;
+    const bool chroma = !F.filter_type || tiles != nullptr;  // chroma staged and stored (see lf_half)
     const __amdgpu_buffer_rsrc_t ry = brsrc(Yf, (uint32_t)ysz), ru = brsrc(Uf, (uint32_t)csz), rv = brsrc(Vf, (uint32_t)csz);
+    const __amdgpu_buffer_rsrc_t rt = brsrc(tiles ? tiles + (size_t)f * nmb * ZW_DEC_TILE : (const uint8_t*)Yf,
+                                            tiles ? (uint32_t)(nmb * ZW_DEC_TILE) : 0u);
     const __amdgpu_buffer_rsrc_t rf = brsrc(flags + (size_t)f * nmb * 4, (uint32_t)(nmb * 4));
     // the interior words and the flags of MB (mx, my) (every lane loads; invalid -> ZW_OOB -> 0)
     auto load = [&](bool valid, int my, int mx, uint32_t& y0w, uint32_t& y1w, uint32_t& cw, uint32_t& flw) {
@@ -909,12 +927,17 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
         y0w = y1w = cw = (uint32_t)(mx * 77 + hl); flw = 0x01000000u | (uint32_t)(mx & 1);
         return;
 #endif
+        // tiles: whole lines (luma words hl, hl + 32: rows hl >> 2 and 8 + (hl >> 2); chroma
+        // word hl); else the planes.  The same four loads either way (a uniform choice of
+        // resource and offsets, no branch: the waits stay counted)
+        const bool t = tiles != nullptr, pv = (hl >> 4) & 1, cv = valid && chroma;
+        const uint32_t tb = (uint32_t)(my * mbw + mx) * ZW_DEC_TILE + 4u * (uint32_t)hl;
         const uint32_t oy = (uint32_t)((my * 16 + (hl >> 2)) * ys + mx * 16 + 4 * (hl & 3));
-        y0w = bld32(ry, valid ? oy : ZW_OOB);
-        y1w = bld32(ry, valid ? oy + 8u * (uint32_t)ys : ZW_OOB);
         const uint32_t oc = (uint32_t)((my * 8 + ((hl >> 1) & 7)) * cs + mx * 8 + 4 * (hl & 1));
-        const bool cv = valid && chroma;
-        cw = bld32(ru, cv && !((hl >> 4) & 1) ? oc : ZW_OOB) | bld32(rv, cv && ((hl >> 4) & 1) ? oc : ZW_OOB);
+        y0w = bld32(t ? rt : ry, !valid ? ZW_OOB : (t ? tb : oy));
+        y1w = bld32(t ? rt : ry, !valid ? ZW_OOB : (t ? tb + 128u : oy + 8u * (uint32_t)ys));
+        cw = bld32(t ? rt : ru, !cv ? ZW_OOB : (t ? tb + 256u : (!pv ? oc : ZW_OOB))) |
+             bld32(rv, cv && !t && pv ? oc : ZW_OOB);
         flw = bld32(rf, valid ? (uint32_t)((my * mbw + mx) * 4) : ZW_OOB);
     };
     for (int pr = wv; 2 * pr < mbh; pr += NWD) {
@@ -930,7 +953,7 @@ extern "C" __global__ __launch_bounds__(WGD) void k_loopfilter(uint8_t* Y, uint8
             if (pr > 0 && st < mbw) dec_wait(progress, (pr - 1) % NWD, (pr - 1) * 65536 + min(st + 2, mbw));
 #endif
             load(rowok && mx + 1 >= 0 && mx + 1 < mbw, my, mx + 1, ny0, ny1, nc, nfl);
-            lf_half(L, hl, on, F, ry, ru, rv, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1, [] {});
+            lf_half(L, hl, on, F, ry, ru, rv, ys, cs, mx, my, fl, cy0, cy1, cc, hy, hu, hv, my == mbh - 1, chroma, [] {});
             wsync();
             if (st >= 2) dec_publish(progress, wv, pr * 65536 + st - 1);  // the lower row has finished st - 1 MBs
         }
@@ -1033,9 +1056,11 @@ extern "C" size_t zw_dec_lds_bytes(int mbw)
     return off;
 }
 
+// tiles: nframes * mbw * mbh * ZW_DEC_TILE bytes (k_loopfilter's input; the planes
+// are written by the filter)
 extern "C" hipError_t zwk_dec_recon(hipStream_t s, const uint8_t* recs, const uint32_t* moff, const uint64_t* fbase,
                                     const void* quant, uint8_t* Y, uint8_t* U, uint8_t* V, uint8_t* flags, int mbw,
-                                    int mbh, size_t ysz, size_t csz, int nframes)
+                                    int mbh, size_t ysz, size_t csz, int nframes, uint8_t* tiles)
 {
     static const bool attr = []() {
         (void)hipFuncSetAttribute((const void*)k_dec_recon, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1043,13 +1068,14 @@ extern "C" hipError_t zwk_dec_recon(hipStream_t s, const uint8_t* recs, const ui
     }();
     (void)attr;
     hipLaunchKernelGGL(k_dec_recon, dim3(nframes), dim3(WGD), zw_dec_lds_bytes(mbw), s, recs, moff, fbase,
-                       (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz);
+                       (const ZwDecQuant*)quant, Y, U, V, flags, mbw, mbh, ysz, csz, tiles);
     return hipGetLastError();
 }
 
 // mbw: the frames' width in MBs (every frame of a launch has the same size)
 extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
-                                     const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw)
+                                     const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw,
+                                     const uint8_t* tiles)
 {
     static const bool attr = []() {
         (void)hipFuncSetAttribute((const void*)k_loopfilter, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1057,7 +1083,7 @@ extern "C" hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), (size_t)mbw * 128, s, Y, U, V, flags, fp, ysz, csz);
+    hipLaunchKernelGGL(k_loopfilter, dim3(nframes), dim3(WGD), (size_t)mbw * 128, s, Y, U, V, flags, fp, ysz, csz, tiles);
     return hipGetLastError();
 }
 
