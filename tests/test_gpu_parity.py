@@ -299,8 +299,16 @@ def _manifest():
         return json.load(f)["streams"]
 
 
+@pytest.mark.parametrize("rows", ["default", "0"])
 @pytest.mark.parametrize("entry", _manifest(), ids=lambda e: e["name"])
-def test_decode_goldens(ctx, entry):
+def test_decode_goldens(ctx, monkeypatch, entry, rows):
+    """The committed streams' planes (SHA-256 from the reference's own decode
+    fixtures / libwebp).  rows=0 forces the batch kernels (one workgroup per
+    frame, reconstruction -> MB tiles -> loop filter), which otherwise only run
+    for batches of 128+ frames: odd sizes and the gallery1 simple-filter
+    streams (chroma moved through the tiles unfiltered) go through them too."""
+    if rows != "default":
+        monkeypatch.setenv("ZW_DEC_ROWS", rows)
     vp8 = open(os.path.join(GOLD, entry["name"] + ".vp8"), "rb").read()
     fr = zwebp.vp8_decode_frame(vp8, ctx=ctx)
     w, h = entry["width"], entry["height"]
