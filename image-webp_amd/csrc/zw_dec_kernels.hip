@@ -240,25 +240,7 @@ __device__ __forceinline__ void st_sc1(uint8_t* p, uint32_t v)
 {
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Raw buffer loads / stores with a per-lane offset; ZW_OOB (past num_records)
-// makes a lane's load return 0 and its store vanish.  The batch kernels issue
-// every global access of an MB step this way, unconditionally, so the number
-// of memory operations between a prefetch and its use is the same on every
-// path: the compiler then waits for the prefetch alone (vmcnt(N)) instead of
-// vmcnt(0), which would also wait for the step's own stores.
-#define ZW_OOB 0x80000000u
-typedef uint32_t zu2 __attribute__((ext_vector_type(2)));
-typedef uint32_t zu4 __attribute__((ext_vector_type(4)));
-DI __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
-}
-DI uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0); }
-DI zu4 bld128(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0); }
-DI void bst8(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)off, 0, 0); }
-DI void bst32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0); }
-DI void bst64(zu2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
-DI void bst128(zu4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
+// (buffer-op helpers brsrc / bld* / bst* and ZW_OOB: zw_dev.h)
 
 // pub() runs once the rows the MB row below reads (luma 12..15, chroma 4..7 of
 // this tile) are stored; the rest of the write-back follows it.

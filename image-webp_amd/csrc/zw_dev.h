@@ -122,6 +122,31 @@ DI void wsync()
     __builtin_amdgcn_wave_barrier();
 }
 
+// Raw buffer loads / stores with a per-lane offset; ZW_OOB (past num_records)
+// makes a lane's load return 0 and its store vanish.  The streaming kernels
+// issue every global access of a step this way, unconditionally, so the number
+// of memory operations between a prefetch and its use is the same on every
+// path: the compiler then waits for the prefetch alone (vmcnt(N)) instead of
+// vmcnt(0), which would also wait for the step's own stores.  The *nt forms
+// set the nontemporal cache policy (CPol NT, bit 1).
+#define ZW_OOB 0x80000000u
+typedef uint32_t zu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t zu4 __attribute__((ext_vector_type(4)));
+DI __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+DI uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0); }
+DI zu2 bld64nt(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 2); }
+DI zu4 bld128(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0); }
+DI zu4 bld128nt(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2); }
+DI void bst8(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)off, 0, 0); }
+DI void bst32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0); }
+DI void bst64(zu2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
+DI void bst64nt(zu2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 2); }
+DI void bst128(zu4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
+DI void bst128nt(zu4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 2); }
+
 DI int wave_sum(int v)
 {
 #pragma unroll
