@@ -40,10 +40,12 @@ levels and reconstruction are hashed against the oracle's digests.
 `roofline_blocks`: k_fdct_quant, the same arithmetic on 4x4 blocks with the
 prediction materialised (64 B per block counted, 16 B of prediction moved).
 `encode_roofline`: the step's dominant kernel, k_encode_pass2 (RD mode search
-fused with the final DCT+quant+recon), against the VALU issue peak: its VALU
-instructions per launch (rocprofv3 SQ_INSTS_VALU, profiles/) over the live
-launch time, against 2 wave-instructions per CU-cycle (4 SIMD32, a wave64 VALU
-op every 2 cycles per SIMD).
+fused with the final DCT+quant+recon), against the VALU issue peak of 2
+wave-instructions per CU-cycle (4 SIMD32, a wave64 VALU op every 2 cycles per
+SIMD): `frac` from one rocprofv3 --pmc dispatch (SQ_INSTS_VALU over that
+dispatch's GRBM_GUI_ACTIVE cycles, clock_ghz from its timestamps;
+profiles/r03_encode_pmc.json), `frac_live` the same instruction count over this
+run's launch time at that clock.
 cpu_baseline times the C restatement of the reference encoder (oracle/, -O3)
 on a bounded sample of the same frames.
 """
@@ -69,7 +71,7 @@ HBM_PEAK_GBS = 8000.0
 VALU_PEAK_PER_CU_CYCLE = 2.0      # wave64 VALU instructions: 4 SIMD32 x 1 per 2 cycles
 CLOCK_GHZ = 2.4
 XFORM_PMC = os.path.join(ROOT, "profiles", "r01_xform_pmc_traffic.json")
-ENCODE_PMC = os.path.join(ROOT, "profiles", "r02_encode_pmc.json")
+ENCODE_PMC = os.path.join(ROOT, "profiles", "r03_encode_pmc.json")
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
 XMB_PMC = os.path.join(ROOT, "profiles", "r03_xmb_pmc.json")
 
@@ -611,8 +613,11 @@ def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0
 
 
 def encode_roofline(p2_ms, launch_frames, nmb):
-    """k_encode_pass2 against the VALU issue peak: SQ_INSTS_VALU per MB from the
-    committed rocprofv3 --pmc summary x MBs per launch / the live launch time."""
+    """k_encode_pass2 against the VALU issue peak.  `frac` comes from ONE
+    rocprofv3 --pmc dispatch (committed summary): SQ_INSTS_VALU over that
+    dispatch's own GRBM_GUI_ACTIVE cycles x 256 CUs x 2 per cycle, with the clock
+    the dispatch ran at (its cycles over its timestamps).  `frac_live` prices the
+    same instruction count over this run's launch time at that clock."""
     try:
         with open(ENCODE_PMC) as f:
             d = json.load(f)["k_encode_pass2"]
@@ -621,14 +626,21 @@ def encode_roofline(p2_ms, launch_frames, nmb):
     mbs = launch_frames * nmb
     insts = d["valu_insts_per_mb"] * mbs
     cus = 256
-    achieved = insts / (p2_ms * 1e-3) / 1e9  # G wave-instructions / s
-    peak = VALU_PEAK_PER_CU_CYCLE * cus * CLOCK_GHZ
-    return {"kernel": "k_encode_pass2", "bound": "valu", "achieved": achieved, "peak": peak,
-            "unit": "G wave64-VALU-instructions/s", "frac": achieved / peak,
-            "valu_insts_per_mb": d["valu_insts_per_mb"], "ms_per_launch": p2_ms, "mbs_per_launch": mbs,
-            "pmc_frac": d.get("valu_issue_frac"), "hbm_achieved": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9,
+    clock = d.get("clock_ghz", CLOCK_GHZ)
+    peak = VALU_PEAK_PER_CU_CYCLE * cus * clock  # G wave-instructions / s at the dispatch's clock
+    achieved_pmc = d["valu_insts_per_mb"] * mbs / (d["dispatch_ms"] * 1e-3) / 1e9 if d.get("dispatch_ms") else None
+    achieved = insts / (p2_ms * 1e-3) / 1e9
+    return {"kernel": "k_encode_pass2", "bound": "valu",
+            "achieved": achieved_pmc if achieved_pmc is not None else achieved, "peak": peak,
+            "unit": "G wave64-VALU-instructions/s",
+            "frac": d.get("valu_issue_frac", achieved / peak),
+            "clock_ghz": clock, "pmc_dispatch_ms": d.get("dispatch_ms"),
+            "frac_live": achieved / peak, "ms_per_launch": p2_ms,
+            "valu_insts_per_mb": d["valu_insts_per_mb"], "mbs_per_launch": mbs,
+            "hbm_achieved": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9,
             "hbm_frac": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "source": "profiles/r02_encode_pmc.json (rocprofv3 --pmc SQ_INSTS_VALU, GRBM_GUI_ACTIVE)"}
+            "source": "profiles/r03_encode_pmc.json (rocprofv3 --pmc SQ_INSTS_VALU + GRBM_GUI_ACTIVE in one "
+                      "pass, one dispatch; clock from its timestamps; tools/gpu_pmc_encode.sh)"}
 
 
 def launch_kernel_times(ctx, imgs, w, h, q, m, frames):
