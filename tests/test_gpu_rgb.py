@@ -59,6 +59,27 @@ def test_yuv_to_rgb_kernel(ctx, w, h, bpp, up):
     assert np.array_equal(got.reshape(-1), exp)
 
 
+@pytest.mark.parametrize("bpp", [3, 4])
+def test_yuv_to_rgb_exhaustive(ctx, bpp):
+    """Every (y, u, v) triple exactly once (yuv_to_r/g/b, yuv.rs:63-78, through the
+    kernel's u16-pair arithmetic): simple upsampling of a 4096 x 4096 frame whose
+    chroma sample (cx, cy) is (u, v) = (cx % 256, cy % 256) -- each pair 64 times,
+    occurrence o = cx // 256 + 8 (cy // 256) -- and whose four pixels under it
+    carry y = 4 o + 0..3."""
+    w = h = 4096
+    cy, cx = np.meshgrid(np.arange(h // 2), np.arange(w // 2), indexing="ij")
+    u = (cx % 256).astype(np.uint8)
+    v = (cy % 256).astype(np.uint8)
+    o = (cx // 256 + 8 * (cy // 256)).astype(np.int32)
+    py, px = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    y = (4 * o[py // 2, px // 2] + (px & 1) + 2 * (py & 1)).astype(np.uint8)
+    triples = (y.astype(np.int64) << 16) | (u[py // 2, px // 2].astype(np.int64) << 8) | v[py // 2, px // 2]
+    assert np.unique(triples).size == 1 << 24  # (the construction covers the cube)
+    y, u, v = y.reshape(-1), u.reshape(-1), v.reshape(-1)
+    got = zwebp.yuv_to_rgb(y, u, v, w, h, w, w // 2, bpp, SIMPLE, ctx=ctx)
+    assert np.array_equal(got.reshape(-1), _oracle_rgb(y, u, v, w, h, bpp, SIMPLE))
+
+
 def test_yuv_to_rgb_extremes(ctx):
     # clip both ends: every (y, u, v) corner of the cube
     w, h = 16, 16
