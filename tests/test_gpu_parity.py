@@ -52,6 +52,27 @@ def test_rgb_to_yuv420(ctx, w, h, bpp):
     assert np.array_equal(gv, ov)
 
 
+@pytest.mark.parametrize("bpp", [3, 4])
+def test_rgb_to_yuv420_exhaustive_luma(ctx, bpp):
+    """rgb_to_y (yuv.rs:859-873) for every (r, g, b) exactly once: a 4096 x 4096 image
+    whose pixel i is (i & 255, (i >> 8) & 255, i >> 16), through the row-coalesced
+    kernel's 16-bit dot-product form; the chroma planes (2x2 sums of neighbouring
+    triples) are checked as well."""
+    w = h = 4096
+    i = np.arange(w * h, dtype=np.uint32)
+    img = np.empty((h, w, bpp), np.uint8)
+    img[..., 0] = (i & 255).reshape(h, w)
+    img[..., 1] = ((i >> 8) & 255).reshape(h, w)
+    img[..., 2] = (i >> 16).reshape(h, w)
+    if bpp == 4:
+        img[..., 3] = 255
+    gy, gu, gv = zwebp.rgb_to_yuv420(img, w, h, bpp, ctx=ctx)
+    oy, ou, ov = O.rgb_to_yuv420(img, w, h, bpp)
+    assert np.array_equal(gy, oy)
+    assert np.array_equal(gu, ou)
+    assert np.array_equal(gv, ov)
+
+
 # --------------------------------------------------------------------------
 # a2..a18: the full encoder, stage by stage
 # --------------------------------------------------------------------------
