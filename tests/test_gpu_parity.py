@@ -420,6 +420,37 @@ def test_decode_errors(ctx):
         zwebp.vp8_decode_frame(vp8[:40], ctx=ctx)
 
 
+@pytest.mark.parametrize("name", ["libwebp_natural_64x48_q75.vp8", "gallery1_1.vp8"])
+def test_decode_damaged_streams(ctx, name):
+    """Truncated and byte-flipped streams (the header's 10 bytes kept, so the
+    dimensions stay sane): wherever the oracle decodes (decode_frame,
+    decoder/vp8.rs:1526, reading zeros past the end as bit_reader.rs does), the
+    device path gives the same planes; wherever it fails, the product raises
+    DecodingError.  Never a crash or a silent difference."""
+    path = os.path.join(GOLD, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not in tests/golden")
+    vp8 = open(path, "rb").read()
+    rng = np.random.default_rng(len(vp8))
+    cases = [vp8[:n] for n in range(10, len(vp8), max(1, len(vp8) // 24))]
+    for _ in range(24):
+        b = bytearray(vp8)
+        for k in rng.integers(10, len(vp8), int(rng.integers(1, 4))):
+            b[k] ^= int(rng.integers(1, 256))
+        cases.append(bytes(b))
+    agree = 0
+    for s in cases:
+        rc, r = O.decode(s)
+        if rc != 0:
+            with pytest.raises(zwebp.DecodingError):
+                zwebp.vp8_decode_frame(s, ctx=ctx)
+        else:
+            fr = zwebp.vp8_decode_frame(s, ctx=ctx)
+            assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+        agree += 1
+    assert agree == len(cases)
+
+
 @pytest.mark.parametrize("ftype,level,sharp,seg", [(0, 6, 0, 0), (0, 40, 3, 1), (1, 20, 0, 0), (0, 63, 7, 1),
                                                    (1, 63, 5, 1), (0, 15, 1, 0)])
 @pytest.mark.parametrize("rows", ["1", "0"])
