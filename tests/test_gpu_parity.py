@@ -420,6 +420,20 @@ def test_decode_errors(ctx):
         zwebp.vp8_decode_frame(vp8[:40], ctx=ctx)
 
 
+@pytest.mark.parametrize("m", [0, 1, 3, 6])
+def test_encode_quality_method_sweep(ctx, m):
+    """encode_frame_lossy (vp8.rs:3132) over the quality range at methods the
+    stage-by-stage cases visit only at Q75: the device bitstream equals the oracle's
+    byte for byte (RGB and RGBA sources, a 96 x 64 natural image)."""
+    for q in (1, 5, 33, 50, 66, 88, 99):
+        for color in (zwebp.ColorType.Rgb8, zwebp.ColorType.Rgba8):
+            img = _img(96, 64, "natural", 1000 + q, color)
+            rc, ref, _ = O.encode(img, 96, 64, color, q, m)
+            assert rc == 0
+            got = zwebp.encode_frame_lossy(img, 96, 64, color, q, m, ctx=ctx)
+            assert bytes(got) == bytes(ref), f"q={q} m={m} color={color}"
+
+
 @pytest.mark.parametrize("name", ["libwebp_natural_64x48_q75.vp8", "gallery1_1.vp8"])
 def test_decode_damaged_streams(ctx, name):
     """Truncated and byte-flipped streams (the header's 10 bytes kept, so the
