@@ -360,8 +360,8 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
                 "verified": bad == 0 and miss == 0 and ok == frames,
                 "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad,
                                  "no_digest": miss},
-                "copy_ceiling": {"kernel": "k_xform_mb<copy> (ZW_XMB_VARIANT=99: the same loads and stores, no "
-                                           "transform arithmetic)", "ms_per_launch": ms_copy, "achieved": copy_gbs,
+                "copy_ceiling": {"kernel": "k_xform_mb<copy> (ZW_XMB_VARIANT=99: the same bytes in and out, "
+                                           "levels as one contiguous run, no transform arithmetic)", "ms_per_launch": ms_copy, "achieved": copy_gbs,
                                  "frac": copy_gbs / HBM_PEAK_GBS, "pass_over_copy": ms_copy / ms}}
 
     out = {}

@@ -52,16 +52,25 @@ struct XmbSeg {
 
 #define XMB_LEVW 200  // words of levels per MB (25 x 16 i16)
 #ifndef XMB_STAGE_LEV
-#define XMB_STAGE_LEV 1  // 1: levels staged in LDS, stored as one contiguous run; 0: stored from the lanes
+// 1: levels staged in LDS, stored as one contiguous run; 0: stored from the lanes;
+// -1 (default): staged for RGB(A) sources, from the lanes for Y/U/V planes (measured:
+// staging 1.38-1.40 vs 1.43-1.44 ms per 256 RGBA frames; from the lanes 1.10 vs
+// 1.15-1.16 ms from planes, whose occupancy the 6.4 KB of staging then no longer caps)
+#define XMB_STAGE_LEV -1
 #endif
-struct XmbLds {
+template <bool STG>
+struct XmbLev {
+    uint32_t lev[XMB_MBS][XMB_LEVW];  // the group's levels, laid out as in HBM (one contiguous store run)
+};
+template <>
+struct XmbLev<false> {
+};
+template <bool STG>
+struct XmbLds : XmbLev<STG> {
     uint32_t rec[XMB_MBS][24];      // the 8 records
     uint32_t yt[16][36];            // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction), rows padded
                                     // to 144 B: the lanes of a block row (4 MBs x 4 block rows x 4 columns) hit 64 banks
     uint32_t ct[2][8][20];          // U, V tiles: 8 rows x 8 MBs x 8 B, rows padded to 80 B (64 banks, as yt)
-#if XMB_STAGE_LEV
-    uint32_t lev[XMB_MBS][XMB_LEVW];  // the group's levels, laid out as in HBM (one contiguous store run)
-#endif
     XmbSeg seg[4];                  // the frame's four segment matrices (per-lane segment reads hit LDS, not HBM)
 };
 
@@ -284,9 +293,12 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     int16_t* __restrict__ levels, uint8_t* __restrict__ RY, uint8_t* __restrict__ RU, uint8_t* __restrict__ RV,
     uint32_t* __restrict__ i4q)
 {
-    __shared__ XmbLds lds[XMB_WAVES];
+    // (the copy calibration always stages: the same bytes in and out, levels as one
+    // contiguous run -- the ceiling for moving them)
+    constexpr bool STG = COPY || (XMB_STAGE_LEV < 0 ? SRC != 0 : XMB_STAGE_LEV != 0);
+    __shared__ XmbLds<STG> lds[XMB_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    XmbLds& L = lds[wv];
+    XmbLds<STG>& L = lds[wv];
     const int ngx = (mbw + XMB_MBS - 1) / XMB_MBS;
     const long long id = (long long)blockIdx.x * XMB_WAVES + wv;
     if (id >= (long long)nframes * mbh * ngx) return;
@@ -351,17 +363,17 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 
     if (COPY) {
         // calibration: levels staged from the records, no arithmetic
-#if XMB_STAGE_LEV
-        for (int i = lane; i < XMB_MBS * XMB_LEVW; i += 64) (&L.lev[0][0])[i] = (&L.rec[0][0])[i % (XMB_MBS * 24)];
-#else
-        for (int k = 0; k < 3; k++) {
-            const int m = (lane >> 3), b = (lane & 7) + 8 * k;  // 24 blocks of every MB, 8 lanes per MB
-            int lv[16];
+        if constexpr (STG) {
+            for (int i = lane; i < XMB_MBS * XMB_LEVW; i += 64) (&L.lev[0][0])[i] = (&L.rec[0][0])[i % (XMB_MBS * 24)];
+        } else {
+            for (int k = 0; k < 3; k++) {
+                const int m = (lane >> 3), b = (lane & 7) + 8 * k;  // 24 blocks of every MB, 8 lanes per MB
+                int lv[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) lv[j] = (int)L.rec[m][j] + b;
-            if (m < nact) store_levels(levels + ((mb0 + m) * 25 + b + (b >= 16)) * 16, lv);
+                for (int j = 0; j < 16; j++) lv[j] = (int)L.rec[m][j] + b;
+                if (m < nact) store_levels(levels + ((mb0 + m) * 25 + b + (b >= 16)) * 16, lv);
+            }
         }
-#endif
         wsync();
     } else {
         // the group's I4 MBs go on k_xform_mb_i4's queue (their luma is left to it)
@@ -416,11 +428,8 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                     c[k] = m24(lv[k], my1.q[1]);
                 }
                 c[0] = dcv;
-#if XMB_STAGE_LEV
-                stage_levels(&L.lev[m][8 * blk], lv);
-#else
-                if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
-#endif
+                if constexpr (STG) stage_levels(&L.lev[m][8 * blk], lv);
+                else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
                 uint32_t rw[4];
                 recon_words(c, pw, rw);
 #pragma unroll
@@ -430,11 +439,11 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const int zsrc = (lane & ~15) | kZZ(blk);
             const int zv = __shfl(y2l, zsrc);
             const int zn = __shfl_down(zv, 1);
-#if XMB_STAGE_LEV
-            if ((blk & 1) == 0) L.lev[m][128 + (blk >> 1)] = pack_lo(zv, zn);
-#else
-            if ((blk & 1) == 0 && m < nact) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
-#endif
+            if constexpr (STG) {
+                if ((blk & 1) == 0) L.lev[m][128 + (blk >> 1)] = pack_lo(zv, zn);
+            } else {
+                if ((blk & 1) == 0 && m < nact) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
+            }
         }
 
         // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB)
@@ -474,11 +483,8 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                 lv[k] = qz(c[k], muv, tk);
                 c[k] = m24(lv[k], muv.q[tk]);
             }
-#if XMB_STAGE_LEV
-            stage_levels(&L.lev[m][136 + 8 * (4 * plane + sub)], lv);
-#else
-            if (m < nact) store_levels(levels + ((mb0 + m) * 25 + 17 + 4 * plane + sub) * 16, lv);
-#endif
+            if constexpr (STG) stage_levels(&L.lev[m][136 + 8 * (4 * plane + sub)], lv);
+            else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + 17 + 4 * plane + sub) * 16, lv);
             uint32_t rw[4];
             recon_words(c, pw, rw);
 #pragma unroll
@@ -492,15 +498,15 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     // holds its source: k_xform_mb_i4, next on the stream, reads it there and
     // overwrites it with the reconstruction)
     {
-#if XMB_STAGE_LEV
-        const int nch = nact * (XMB_LEVW / 4);
-        v4u* lo = (v4u*)(levels + mb0 * 400);
+        if constexpr (STG) {
+            const int nch = nact * (XMB_LEVW / 4);
+            v4u* lo = (v4u*)(levels + mb0 * 400);
 #pragma unroll
-        for (int k = 0; k < (XMB_MBS * XMB_LEVW / 4 + 63) / 64; k++) {
-            const int c = 64 * k + lane;
-            if (c < nch) __builtin_nontemporal_store(*((const v4u*)&L.lev[0][0] + c), lo + c);
+            for (int k = 0; k < (XMB_MBS * XMB_LEVW / 4 + 63) / 64; k++) {
+                const int c = 64 * k + lane;
+                if (c < nch) __builtin_nontemporal_store(*((const v4u*)&L.lev[0][0] + c), lo + c);
+            }
         }
-#endif
         uint8_t* RYf = RY + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
         const int yc = lane & 7, yr = lane >> 3;
         if (yc < nact) {
