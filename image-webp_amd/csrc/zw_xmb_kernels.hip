@@ -58,15 +58,21 @@ struct XmbSeg {
 // 1.15-1.16 ms from planes, whose occupancy the 6.4 KB of staging then no longer caps)
 #define XMB_STAGE_LEV -1
 #endif
-template <bool STG>
+#ifndef XMB_HALF_STAGE
+// 1: the staged forms hold half the group's levels at a time (MBs 0-3, then 4-7: the
+// chroma pass runs first and keeps its packed levels in registers until its half
+// leaves), so the staging buffer is 3.2 instead of 6.4 KB a wave
+#define XMB_HALF_STAGE 1
+#endif
+template <int NL>
 struct XmbLev {
-    uint32_t lev[XMB_MBS][XMB_LEVW];  // the group's levels, laid out as in HBM (one contiguous store run)
+    uint32_t lev[NL][XMB_LEVW];  // NL MBs' levels, laid out as in HBM (one contiguous store run)
 };
 template <>
-struct XmbLev<false> {
+struct XmbLev<0> {
 };
-template <bool STG>
-struct XmbLds : XmbLev<STG> {
+template <int NL>
+struct XmbLds : XmbLev<NL> {
     uint32_t rec[XMB_MBS][24];      // the 8 records
     uint32_t yt[16][36];            // luma tile: 16 rows x 8 MBs x 16 B (source, then reconstruction), rows padded
                                     // to 144 B: the lanes of a block row (4 MBs x 4 block rows x 4 columns) hit 64 banks
@@ -296,9 +302,11 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     // (the copy calibration always stages: the same bytes in and out, levels as one
     // contiguous run -- the ceiling for moving them)
     constexpr bool STG = COPY || (XMB_STAGE_LEV < 0 ? SRC != 0 : XMB_STAGE_LEV != 0);
-    __shared__ XmbLds<STG> lds[XMB_WAVES];
+    constexpr bool HALF = STG && !COPY && XMB_HALF_STAGE;
+    constexpr int NL = !STG ? 0 : (HALF ? XMB_MBS / 2 : XMB_MBS);
+    __shared__ XmbLds<NL> lds[XMB_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    XmbLds<STG>& L = lds[wv];
+    XmbLds<NL>& L = lds[wv];
     const int ngx = (mbw + XMB_MBS - 1) / XMB_MBS;
     const long long id = (long long)blockIdx.x * XMB_WAVES + wv;
     if (id >= (long long)nframes * mbh * ngx) return;
@@ -390,65 +398,12 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                 if (i4) i4q[XI4_LIST + base + rank] = (uint32_t)(mb0 + lane);
             }
         }
-        // ---- luma of the I16 MBs: MBs 0-3, then 4-7; lane = 16*mb + block
-        const int blk = lane & 15, bx = blk & 3, by = blk >> 2;
-#pragma unroll 1
-        for (int hh = 0; hh < 2; hh++) {
-            const int m = 4 * hh + (lane >> 4);
-            const uint32_t* R = L.rec[m];
-            const int mode = (int)(R[0] & 255u);
-            const int seg = (int)((R[0] >> 16) & 3u);
-            const int has_top = (int)((R[0] >> 24) & 1u), has_left = (int)((R[0] >> 25) & 1u);
-            const XmbMat& my1 = S[seg].y1;
-            int y2l = 0;
-            if (mode != 4) {
-                uint32_t sw[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++) sw[r] = L.yt[by * 4 + r][m * 4 + bx];
-                // I16 (transform_luma_block): prediction of this lane's 4x4 from the record's edges
-                const uint8_t* Rb = (const uint8_t*)R;
-                const uint32_t T = R[6 + bx];
-                const uint32_t st = bsum(R[6]) + bsum(R[7]) + bsum(R[8]) + bsum(R[9]);
-                const uint32_t sl = bsum(R[11]) + bsum(R[12]) + bsum(R[13]) + bsum(R[14]);
-                uint32_t pw[4];
-                pred_rows(mode, T, Rb + 44 + by * 4, Rb[20], dc_word(st, sl, has_top, has_left, 3), pw);
-                int c[16];
-                fdct_words(sw, pw, c);
-                // Y2: WHT of the 16 DCs (lane blk = block blk = Y2 position blk), quant, dequant, iWHT
-                const XmbMat& my2 = S[seg].y2;
-                const int t2 = blk > 0;
-                const int y2c = wht_g(c[0], blk);
-                y2l = qz(y2c, my2, t2);
-                const int dcv = iwht_g(m24(y2l, my2.q[t2]), blk);
-                int lv[16];
-                lv[0] = 0;
-#pragma unroll
-                for (int k = 1; k < 16; k++) {
-                    lv[k] = qz(c[k], my1, 1);
-                    c[k] = m24(lv[k], my1.q[1]);
-                }
-                c[0] = dcv;
-                if constexpr (STG) stage_levels(&L.lev[m][8 * blk], lv);
-                else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
-                uint32_t rw[4];
-                recon_words(c, pw, rw);
-#pragma unroll
-                for (int r = 0; r < 4; r++) L.yt[by * 4 + r][m * 4 + bx] = rw[r];
-            }
-            // Y2 levels in zigzag order (zeros for I4 MBs)
-            const int zsrc = (lane & ~15) | kZZ(blk);
-            const int zv = __shfl(y2l, zsrc);
-            const int zn = __shfl_down(zv, 1);
-            if constexpr (STG) {
-                if ((blk & 1) == 0) L.lev[m][128 + (blk >> 1)] = pack_lo(zv, zn);
-            } else {
-                if ((blk & 1) == 0 && m < nact) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
-            }
-        }
-
-        // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB)
-        {
-            const int m = lane >> 3, plane = (lane >> 2) & 1, sub = lane & 3, bx = sub & 1, by = sub >> 1;
+        // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB);
+        // the block's 16 levels leave as 8 packed words in clw
+        const int cm = lane >> 3, cplane = (lane >> 2) & 1, csub = lane & 3;
+        uint32_t clw[8];
+        auto chroma = [&]() {
+            const int m = cm, plane = cplane, sub = csub, bx = sub & 1, by = sub >> 1;
             const uint32_t* R = L.rec[m];
             const uint8_t* Rb = (const uint8_t*)R;
             const int mode = (int)((R[0] >> 8) & 255u);
@@ -483,22 +438,131 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                 lv[k] = qz(c[k], muv, tk);
                 c[k] = m24(lv[k], muv.q[tk]);
             }
-            if constexpr (STG) stage_levels(&L.lev[m][136 + 8 * (4 * plane + sub)], lv);
-            else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + 17 + 4 * plane + sub) * 16, lv);
+#pragma unroll
+            for (int q = 0; q < 8; q++) clw[q] = pack_lo(lv[kZZ(2 * q)], lv[kZZ(2 * q + 1)]);
             uint32_t rw[4];
             recon_words(c, pw, rw);
 #pragma unroll
             for (int r = 0; r < 4; r++) L.ct[plane][by * 4 + r][m * 2 + bx] = rw[r];
+        };
+        if constexpr (HALF) {
+            // MBs 0-3's chroma levels join their luma in the staging buffer; MBs 4-7's
+            // leave from the lanes (256 B a MB), so no level is held across the luma
+            chroma();
+            if (cm < XMB_MBS / 2) {
+                uint32_t* o = &L.lev[cm][136 + 8 * (4 * cplane + csub)];
+                *(v4u*)o = v4u{clw[0], clw[1], clw[2], clw[3]};
+                *(v4u*)(o + 4) = v4u{clw[4], clw[5], clw[6], clw[7]};
+            } else if (cm < nact) {
+                v4u* o = (v4u*)(levels + ((mb0 + cm) * 25 + 17 + 4 * cplane + csub) * 16);
+                __builtin_nontemporal_store(v4u{clw[0], clw[1], clw[2], clw[3]}, o);
+                __builtin_nontemporal_store(v4u{clw[4], clw[5], clw[6], clw[7]}, o + 1);
+            }
+        }
+
+        // ---- luma of the I16 MBs: MBs 0-3, then 4-7; lane = 16*mb + block
+        const int blk = lane & 15, bx = blk & 3, by = blk >> 2;
+#pragma unroll 1
+        for (int hh = 0; hh < 2; hh++) {
+            const int m = 4 * hh + (lane >> 4);
+            const int ml = HALF ? (m & 3) : m;  // the MB's staging slot
+            const uint32_t* R = L.rec[m];
+            const int mode = (int)(R[0] & 255u);
+            const int seg = (int)((R[0] >> 16) & 3u);
+            const int has_top = (int)((R[0] >> 24) & 1u), has_left = (int)((R[0] >> 25) & 1u);
+            const XmbMat& my1 = S[seg].y1;
+            int y2l = 0;
+            if (mode != 4) {
+                uint32_t sw[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) sw[r] = L.yt[by * 4 + r][m * 4 + bx];
+                // I16 (transform_luma_block): prediction of this lane's 4x4 from the record's edges
+                const uint8_t* Rb = (const uint8_t*)R;
+                const uint32_t T = R[6 + bx];
+                const uint32_t st = bsum(R[6]) + bsum(R[7]) + bsum(R[8]) + bsum(R[9]);
+                const uint32_t sl = bsum(R[11]) + bsum(R[12]) + bsum(R[13]) + bsum(R[14]);
+                uint32_t pw[4];
+                pred_rows(mode, T, Rb + 44 + by * 4, Rb[20], dc_word(st, sl, has_top, has_left, 3), pw);
+                int c[16];
+                fdct_words(sw, pw, c);
+                // Y2: WHT of the 16 DCs (lane blk = block blk = Y2 position blk), quant, dequant, iWHT
+                const XmbMat& my2 = S[seg].y2;
+                const int t2 = blk > 0;
+                const int y2c = wht_g(c[0], blk);
+                y2l = qz(y2c, my2, t2);
+                const int dcv = iwht_g(m24(y2l, my2.q[t2]), blk);
+                int lv[16];
+                lv[0] = 0;
+#pragma unroll
+                for (int k = 1; k < 16; k++) {
+                    lv[k] = qz(c[k], my1, 1);
+                    c[k] = m24(lv[k], my1.q[1]);
+                }
+                c[0] = dcv;
+                if constexpr (STG) stage_levels(&L.lev[ml][8 * blk], lv);
+                else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
+                uint32_t rw[4];
+                recon_words(c, pw, rw);
+#pragma unroll
+                for (int r = 0; r < 4; r++) L.yt[by * 4 + r][m * 4 + bx] = rw[r];
+            }
+            // Y2 levels in zigzag order (zeros for I4 MBs)
+            const int zsrc = (lane & ~15) | kZZ(blk);
+            const int zv = __shfl(y2l, zsrc);
+            const int zn = __shfl_down(zv, 1);
+            if constexpr (STG) {
+                if ((blk & 1) == 0) L.lev[ml][128 + (blk >> 1)] = pack_lo(zv, zn);
+            } else {
+                if ((blk & 1) == 0 && m < nact) *(uint32_t*)(levels + ((mb0 + m) * 25 + 16) * 16 + blk) = pack_lo(zv, zn);
+            }
+            if constexpr (HALF) {
+                wsync();
+                if (hh == 0) {
+                    // MBs 0-3 whole (their chroma was staged first): one contiguous run of 4 x 800 B
+                    const int nch = min(nact, XMB_MBS / 2) * (XMB_LEVW / 4);
+                    v4u* lo = (v4u*)(levels + mb0 * 400);
+#pragma unroll
+                    for (int k = 0; k < (XMB_MBS / 2 * XMB_LEVW / 4 + 63) / 64; k++) {
+                        const int c = 64 * k + lane;
+                        if (c < nch) __builtin_nontemporal_store(*((const v4u*)&L.lev[0][0] + c), lo + c);
+                    }
+                } else {
+                    // MBs 4-7: Y1 + Y2 (544 B a MB; their chroma left from the lanes)
+                    const int nch = max(nact - XMB_MBS / 2, 0) * 34;
+#pragma unroll
+                    for (int k = 0; k < (XMB_MBS / 2 * 34 + 63) / 64; k++) {
+                        const int c = 64 * k + lane, mm = c / 34, q = c - 34 * mm;
+                        if (c < nch)
+                            __builtin_nontemporal_store(*(const v4u*)&L.lev[mm][4 * q],
+                                                        (v4u*)(levels + (mb0 + XMB_MBS / 2 + mm) * 400) + q);
+                    }
+                }
+                wsync();
+            }
+        }
+
+        if constexpr (!HALF) {
+            chroma();
+            const int m = cm;
+            if constexpr (STG) {
+                uint32_t* o = &L.lev[m][136 + 8 * (4 * cplane + csub)];
+                *(v4u*)o = v4u{clw[0], clw[1], clw[2], clw[3]};
+                *(v4u*)(o + 4) = v4u{clw[4], clw[5], clw[6], clw[7]};
+            } else if (m < nact) {
+                v4u* o = (v4u*)(levels + ((mb0 + m) * 25 + 17 + 4 * cplane + csub) * 16);
+                __builtin_nontemporal_store(v4u{clw[0], clw[1], clw[2], clw[3]}, o);
+                __builtin_nontemporal_store(v4u{clw[4], clw[5], clw[6], clw[7]}, o + 1);
+            }
         }
         wsync();
     }
 
     // ---- out: the group's levels as one contiguous run (nact x 800 B, 16 B a
-    // lane), the reconstruction tiles row-coalesced (an I4 MB's luma tile still
-    // holds its source: k_xform_mb_i4, next on the stream, reads it there and
-    // overwrites it with the reconstruction)
+    // lane; the half-staged form has sent them already), the reconstruction tiles
+    // row-coalesced (an I4 MB's luma tile still holds its source: k_xform_mb_i4,
+    // next on the stream, reads it there and overwrites it with the reconstruction)
     {
-        if constexpr (STG) {
+        if constexpr (STG && !HALF) {
             const int nch = nact * (XMB_LEVW / 4);
             v4u* lo = (v4u*)(levels + mb0 * 400);
 #pragma unroll
