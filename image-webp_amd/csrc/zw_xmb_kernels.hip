@@ -64,6 +64,9 @@ struct XmbSeg {
 // leaves), so the staging buffer is 3.2 instead of 6.4 KB a wave
 #define XMB_HALF_STAGE 1
 #endif
+#ifndef XMB_PLANES_HALF
+#define XMB_PLANES_HALF 0  // 1: the Y/U/V-planes form half-stages its levels too (else from the lanes)
+#endif
 template <int NL>
 struct XmbLev {
     uint32_t lev[NL][XMB_LEVW];  // NL MBs' levels, laid out as in HBM (one contiguous store run)
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 {
     // (the copy calibration always stages: the same bytes in and out, levels as one
     // contiguous run -- the ceiling for moving them)
-    constexpr bool STG = COPY || (XMB_STAGE_LEV < 0 ? SRC != 0 : XMB_STAGE_LEV != 0);
+    constexpr bool STG = COPY || (XMB_STAGE_LEV < 0 ? (SRC != 0 || XMB_PLANES_HALF) : XMB_STAGE_LEV != 0);
     constexpr bool HALF = STG && !COPY && XMB_HALF_STAGE;
     constexpr int NL = !STG ? 0 : (HALF ? XMB_MBS / 2 : XMB_MBS);
     __shared__ XmbLds<NL> lds[XMB_WAVES];
