@@ -155,6 +155,8 @@ static bool sdma_probe(zw_ctx* c)
     return st == 1;
 }
 
+std::atomic<bool> g_dma_poisoned{false};
+
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return ZW_OK;
@@ -176,6 +178,7 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
                 // write `dst` and decrement `sig`, so the signal is leaked, not destroyed,
                 // and the context refuses every later copy
                 c->poisoned.store(true, std::memory_order_release);
+                g_dma_poisoned.store(true, std::memory_order_release);
                 return ZW_EDEVICE;
             }
             (void)hsa_signal_destroy(sig);
@@ -201,12 +204,13 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     c->dscratch = c->dscratch1 = nullptr;
-    if (c->xmb_mask) (void)hipFree(c->xmb_mask);
-    c->xmb_mask = nullptr;
-    c->xmb_mask_cap = 0;
+    (void)hipDeviceSynchronize();  // queues may serve streams other than the context's
+    for (auto& q : c->xmb_q)
+        if (q.buf) (void)hipFree(q.buf);
+    c->xmb_q.clear();
     c->dscratch_cap = c->dscratch1_cap = 0;
     for (int i = 0; i < 4; i++) {
-        if (c->hpin[i]) (void)hipHostFree(c->hpin[i]);
+        pinned_free(c->hpin[i]);
         c->hpin[i] = nullptr;
         c->hpin_cap[i] = 0;
     }
@@ -219,13 +223,13 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     zw_pipe_destroy(c->pipe1);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
-    if (c->xmb_mask) (void)hipFree(c->xmb_mask);
+    for (auto& q : c->xmb_q)
+        if (q.buf) (void)hipFree(q.buf);
     for (hipEvent_t e : c->dev_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->dev_ev1)
         if (e) (void)hipEventDestroy(e);
-    for (void* h : c->hpin)
-        if (h) (void)hipHostFree(h);
+    for (void* h : c->hpin) pinned_free(h);
     if (c->stream_) (void)hipStreamDestroy(c->stream_);
     delete c;
 }
@@ -270,7 +274,7 @@ struct Pinned {
     }
     void free()
     {
-        if (p) (void)hipHostFree(p);
+        pinned_free(p);
         p = nullptr;
         n = 0;
     }
@@ -289,7 +293,7 @@ struct FetchBuf {
     Pinned<unsigned long long> total;  // [1] bytes of the chunk
     void release()
     {
-        if (pack) (void)hipHostFree(pack);
+        pinned_free(pack);
         pack = nullptr;
         cap = 0;
     }
@@ -357,6 +361,10 @@ struct zw_pipe {
     int nparts = 1;  // token partitions per frame (zw_pipe_set_token_partitions)
     std::vector<PipeLane> lanes;
     float kms[8];
+    // Set when a run stops partway: k_segments' histograms and k_pack_scan's
+    // counters, which the kernels clear themselves, may then be left nonzero,
+    // so every later run of this pipe fails instead of reading them.
+    bool broken = false;
 };
 
 static void pipe_free(zw_pipe* p)
@@ -576,6 +584,9 @@ extern "C" int zw_pipe_set_container(zw_pipe* p, int enable, const uint8_t* cons
     }
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
     if (has_alpha) {
+        // encode_alpha_lossless refuses > 16384 (api.rs:1187): InvalidDimensions
+        // up front, not a VP8X file with an empty ALPH chunk
+        if (p->w > 16384 || p->h > 16384) return ZW_EINVALID_DIMENSIONS;
         if (!host_frames) return ZW_EINVAL;
         for (int i = 0; i < p->n; i++)
             if (!host_frames[i]) return ZW_EINVAL;
@@ -772,11 +783,12 @@ static void emit_vp8(zw_pipe* p, std::vector<uint8_t>& out, const uint8_t* rec, 
     }
 }
 
-static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
+static int chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
     const FetchBuf& B = L.fb[1];
+    std::atomic<int> err{ZW_OK};
     parallel_for(na, [&](int i) {
         const size_t f = F + i, hf = hidx(p, par, f);
         std::vector<uint8_t>& out = p->bitstreams[f];
@@ -790,12 +802,18 @@ static void chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
         vp8.clear();
         alph.clear();
         emit_vp8(p, vp8, B.pack + B.finfo[2 * i], hf, na);
-        // the image was validated by zw_pipe_set_container (size, dimensions)
-        if (has_alpha) (void)zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph);
-        const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
         out.clear();
+        if (has_alpha) {
+            if (const int r = zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph)) {
+                int ok = ZW_OK;
+                err.compare_exchange_strong(ok, r);
+                return;
+            }
+        }
+        const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
         zw_webp_wrap(out, vp8.data(), vp8.size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w, p->h, md);
     });
+    return err.load();
 }
 
 static void lane_times(PipeLane& L)
@@ -866,7 +884,15 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                 return;
             }
             const double t1 = now_ms();
-            chunk_emit(p, L, ca(c), cn(c), b & 1);
+            if (const int re = chunk_emit(p, L, ca(c), cn(c), b & 1)) {
+                {  // the lane thread may wait for later chunks: release it
+                    std::lock_guard<std::mutex> lk(L.sync->mu);
+                    L.sync->fetched = FAILED;
+                }
+                L.sync->cv.notify_all();
+                emit_rc = re;
+                return;
+            }
             tok += now_ms() - t1;
             fetch2 += t1 - t0;
             if (g_trace)
@@ -904,7 +930,8 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                 L.sync->cv.wait(lk, [&] { return L.sync->fetched >= need; });
                 if (L.sync->fetched == FAILED) {
                     lk.unlock();
-                    return fail(ZW_EDEVICE);
+                    const int re = join_emitter();
+                    return re ? re : ZW_EDEVICE;
                 }
             }
             r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
@@ -965,8 +992,9 @@ static void pipe_collect_times(zw_pipe* p)
 extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
 {
     if (!p) return ZW_EINVAL;
+    if (p->broken) return ZW_EDEVICE;
     HIPOK(hipSetDevice(p->ctx->device));
-    return run_lanes(p, [&](PipeLane& L) -> int {
+    const int r = run_lanes(p, [&](PipeLane& L) -> int {
         for (int fa = L.f0; fa < L.f0 + L.n; fa += L.chunk) {
             int r = chunk_pass1(p, L, fa, std::min(L.chunk, L.f0 + L.n - fa), false, write_recon != 0);
             if (r) return r;
@@ -974,20 +1002,25 @@ extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
         HIPOK(hipStreamSynchronize(L.stream));
         return rows_check(p, L);
     });
+    if (r) p->broken = true;
+    return r;
 }
 
 extern "C" int zw_pipe_run_device(zw_pipe* p)
 {
     if (!p) return ZW_EINVAL;
+    if (p->broken) return ZW_EDEVICE;
     HIPOK(hipSetDevice(p->ctx->device));
     int r = run_lanes(p, [&](PipeLane& L) -> int { return lane_encode(p, L, false); });
     pipe_collect_times(p);
+    if (r) p->broken = true;
     return r;
 }
 
 static int pipe_encode(zw_pipe* p, int nb)
 {
     if (!p || nb < 1) return ZW_EINVAL;
+    if (p->broken) return ZW_EDEVICE;
     HIPOK(hipSetDevice(p->ctx->device));
     static const bool trace = getenv("ZW_PIPE_TRACE") != nullptr;
     const double T0 = now_ms();
@@ -1003,6 +1036,7 @@ static int pipe_encode(zw_pipe* p, int nb)
         return q;
     });
     pipe_collect_times(p);
+    if (r) p->broken = true;
     return r;
 }
 
@@ -1427,22 +1461,45 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
     const uintptr_t a8 = (uintptr_t)d_ru | (uintptr_t)d_rv | (src_bpp ? 0 : ((uintptr_t)d_u | (uintptr_t)d_v));
     if ((a16 & 15) || (a8 & 7)) return ZW_EINVAL;
     HIPOK(hipSetDevice(ctx->device));
-    // the I4 queue k_xform_mb fills and k_xform_mb_i4 drains (grow-only; its
-    // counters are zeroed once here and every launch leaves them zero; a regrow
-    // frees the old buffer, which hipFree orders after queued work)
+    // The I4 queue k_xform_mb fills and k_xform_mb_i4 drains: one per launch
+    // stream, grow-only (a regrow frees the old buffer, which hipFree orders
+    // after queued work).  A completed launch pair leaves its counters zero; a
+    // new buffer, or one whose last launch pair failed to queue, is reset on the
+    // launch stream first.  So neither an overlapping launch on another stream
+    // nor a launch that stopped partway can leave a stale count.
+    const hipStream_t ls = stream ? (hipStream_t)stream : ctx_stream(ctx);
     const size_t qb = zwk_xform_mb_queue_bytes((int)mbw, (int)mbh, nframes);
-    if (ctx->xmb_mask_cap < qb) {
-        if (ctx->xmb_mask) (void)hipFree(ctx->xmb_mask);
-        ctx->xmb_mask = nullptr;
-        ctx->xmb_mask_cap = 0;
-        if (hipMalloc(&ctx->xmb_mask, qb) != hipSuccess) return ZW_ENOMEM;
-        if (hipMemset(ctx->xmb_mask, 0, 256) != hipSuccess) return ZW_EDEVICE;
-        ctx->xmb_mask_cap = qb;
+    void* q = nullptr;
+    zw_ctx::XmbQueue* qe = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(ctx->xmb_mu);
+        zw_ctx::XmbQueue* e = nullptr;
+        for (auto& x : ctx->xmb_q)
+            if (x.stream == ls) e = &x;
+        if (!e) {
+            ctx->xmb_q.push_back({ls, nullptr, 0});
+            e = &ctx->xmb_q.back();
+        }
+        if (e->cap < qb) {
+            if (e->buf) (void)hipFree(e->buf);
+            e->buf = nullptr;
+            e->cap = 0;
+            if (hipMalloc(&e->buf, qb) != hipSuccess) return ZW_ENOMEM;
+            e->cap = qb;
+            e->dirty = true;
+        }
+        q = e->buf;
+        qe = e;
+        if (qe->dirty) HIPOK(hipMemsetAsync(q, 0, 16, ls));
+        qe->dirty = true;
     }
-    HIPOK(zwk_xform_mb(stream ? (hipStream_t)stream : ctx_stream(ctx), (const uint8_t*)d_y, (const uint8_t*)d_u,
-                       (const uint8_t*)d_v, src_bpp, (int)w, (int)h, img_stride, (const uint8_t*)d_recs, d_segs,
-                       (int)mbw, (int)mbh, nframes, (int16_t*)d_levels, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv,
-                       (uint32_t*)ctx->xmb_mask, xmb_variant()));
+    HIPOK(zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp, (int)w, (int)h,
+                       img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes, (int16_t*)d_levels,
+                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, xmb_variant()));
+    {
+        std::lock_guard<std::mutex> lk(ctx->xmb_mu);
+        qe->dirty = false;  // both kernels queued: the pair leaves the counters zero
+    }
     return ZW_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <sched.h>
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -20,8 +21,17 @@ struct zw_ctx {
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
     void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
-    void* xmb_mask = nullptr;   // zw_transform_quant_mbs_device: the I4 queue of k_xform_mb / k_xform_mb_i4
-    size_t xmb_mask_cap = 0;
+    // zw_transform_quant_mbs*_device: the I4 queue of k_xform_mb / k_xform_mb_i4,
+    // one per launch stream (launches on different streams may overlap; launches
+    // on one stream are ordered), its counters reset on that stream per launch
+    struct XmbQueue {
+        hipStream_t stream = nullptr;
+        void* buf = nullptr;
+        size_t cap = 0;
+        bool dirty = true;  // counters not known to be zero: reset on the stream first
+    };
+    std::deque<XmbQueue> xmb_q;  // (a deque: entries stay put while others are added)
+    std::mutex xmb_mu;
     size_t dscratch1_cap = 0;
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
     // D2H runs as a blit kernel, which cannot be dispatched while an encode
@@ -150,11 +160,21 @@ static inline hipStream_t ctx_stream(zw_ctx* c)
 // (hipHostMalloc): the DMA engine cannot reach pageable memory.
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
 
+// Set (process-wide) once an SDMA copy timed out with the engine possibly
+// still writing its destination: from then on pinned host buffers, which are
+// the destinations of those copies, are leaked instead of freed, so a late
+// DMA write cannot land in memory the allocator has handed out again.
+extern std::atomic<bool> g_dma_poisoned;
+static inline void pinned_free(void* h)
+{
+    if (h && !g_dma_poisoned.load(std::memory_order_acquire)) (void)hipHostFree(h);
+}
+
 // Pinned host staging buffer `which` of at least `bytes` owned by the context.
 static inline void* ctx_pinned(zw_ctx* c, int which, size_t bytes)
 {
     if (c->hpin_cap[which] < bytes) {
-        if (c->hpin[which]) (void)hipHostFree(c->hpin[which]);
+        pinned_free(c->hpin[which]);
         c->hpin[which] = nullptr;
         c->hpin_cap[which] = 0;
         if (hipHostMalloc(&c->hpin[which], bytes, hipHostMallocDefault) != hipSuccess) return nullptr;

@@ -398,7 +398,10 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                                                   __HIP_MEMORY_SCOPE_AGENT);
                 base = (uint32_t)__shfl((int)base, 0);
                 const int rank = __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u);
-                if (i4) i4q[XI4_LIST + base + rank] = (uint32_t)(mb0 + lane);
+                // bounded: the queue holds one launch's MBs (a count past that
+                // would mean a shared or stale queue, which the host rules out)
+                if (i4 && base + rank < (uint32_t)nframes * (uint32_t)(mbw * mbh))
+                    i4q[XI4_LIST + base + rank] = (uint32_t)(mb0 + lane);
             }
         }
         // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB);

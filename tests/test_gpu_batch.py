@@ -210,6 +210,23 @@ def test_encode_webp_batch(ctx, color):
         assert outs[i] == want, f"frame {i}"
 
 
+@pytest.mark.parametrize("color", [zwebp.ColorType.Rgba8, zwebp.ColorType.La8])
+def test_encode_webp_batch_alpha_too_large(ctx, color):
+    """An alpha input taller than 16384 rows: encode_alpha_lossless returns
+    InvalidDimensions (encoder/api.rs:1187), so the batch container path
+    fails with ZW_EINVALID_DIMENSIONS instead of writing an empty ALPH chunk;
+    the same frame without alpha (RGB8) encodes."""
+    w, h = 64, 16400
+    bpp = 4 if color == zwebp.ColorType.Rgba8 else 2
+    img = np.full(w * h * bpp, 200, np.uint8)
+    with pytest.raises(zwebp.EncodingError) as e:
+        zwebp.encode_webp_batch([img], w, h, color, 75, 0, ctx=ctx)
+    assert e.value.code == 1  # ZW_EINVALID_DIMENSIONS
+    rgb = np.full(w * h * 3, 200, np.uint8)
+    out = zwebp.encode_webp_batch([rgb], w, h, zwebp.ColorType.Rgb8, 75, 0, ctx=ctx)
+    assert out[0][:4] == b"RIFF" and out[0][12:16] == b"VP8 "
+
+
 def test_rows_encode_error_reported(ctx, monkeypatch):
     """Row-parallel encode: a set launch error word (a wave that gave up
     waiting) fails the encode with ZW_EDEVICE instead of returning streams."""

@@ -407,17 +407,34 @@ def test_decode_rows_and_frame_kernels(ctx, monkeypatch, rows):
         assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
 
 
+def _header_damage_cases(vp8):
+    """Streams that fail in the frame tag / key-frame header / first partition
+    (decoder/vp8.rs:553-680): every DecodingError variant the header can raise."""
+    out = []
+    b = bytearray(vp8); b[3] = 0; out.append(bytes(b))            # start code -> Vp8MagicInvalid
+    b = bytearray(vp8); b[0] |= 1; out.append(bytes(b))           # inter frame -> UnsupportedFeature
+    b = bytearray(vp8); b[0] &= 0x1F; b[1] = b[2] = 0; out.append(bytes(b))  # first partition size 0
+    out += [vp8[:n] for n in range(0, 12)]                        # truncated tag / start code / dims
+    b = bytearray(vp8); b[10] |= 0x80; out.append(bytes(b))       # color space bit
+    out.append(vp8[:40])
+    return out
+
+
 def test_decode_errors(ctx):
+    """Each failing header gives the oracle's DecodingError variant (codes 10-17 =
+    decoder/api.rs:79-110 in declaration order)."""
     vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
-    bad = bytearray(vp8)
-    bad[3] = 0
-    with pytest.raises(zwebp.DecodingError) as e:
-        zwebp.vp8_decode_frame(bytes(bad), ctx=ctx)
-    assert e.value.code == 10
-    with pytest.raises(zwebp.DecodingError):
-        zwebp.vp8_decode_frame(vp8[:2], ctx=ctx)
-    with pytest.raises(zwebp.DecodingError):
-        zwebp.vp8_decode_frame(vp8[:40], ctx=ctx)
+    seen = set()
+    for s in _header_damage_cases(vp8):
+        rc, _ = O.decode(s)
+        if rc == 0:
+            fr = zwebp.vp8_decode_frame(s, ctx=ctx)
+            continue
+        with pytest.raises(zwebp.DecodingError) as e:
+            zwebp.vp8_decode_frame(s, ctx=ctx)
+        assert e.value.code == rc, (len(s), e.value.code, rc)
+        seen.add(rc)
+    assert {10, 11, 15, 16, 17}.issubset(seen), seen
 
 
 @pytest.mark.parametrize("m", [0, 1, 3, 6])
@@ -456,8 +473,10 @@ def test_decode_damaged_streams(ctx, name):
     for s in cases:
         rc, r = O.decode(s)
         if rc != 0:
-            with pytest.raises(zwebp.DecodingError):
+            # the DecodingError variant itself (decoder/api.rs:79-110), not just "raises"
+            with pytest.raises(zwebp.DecodingError) as e:
                 zwebp.vp8_decode_frame(s, ctx=ctx)
+            assert e.value.code == rc, f"variant {e.value.code} != oracle {rc}"
         else:
             fr = zwebp.vp8_decode_frame(s, ctx=ctx)
             assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])

@@ -155,6 +155,26 @@ zwebp.transform_quant_mbs_device(nf, mbw, mbh, *args, ctx=ctx)
 torch.cuda.synchronize()
 assert np.array_equal(lv.cpu().numpy().reshape(-1, 25, 16), want[0])
 assert np.array_equal(ry.cpu().numpy(), want[1]) and np.array_equal(rv.cpu().numpy(), want[3])
+# two launches in flight on two streams at once (each stream has its own I4
+# queue): both equal the oracle
+cases = []
+for seed, (nf2, w2, h2) in ((11, (3, 40, 20)), (12, (2, 33, 25))):
+    c = _random_case(np.random.default_rng(seed), nf2, w2, h2, 0.5)
+    tt = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (c[0], c[1], c[2], c[3].reshape(-1))]
+    tt.append(torch.from_numpy(zwebp.xmb_seg_table(c[4])).to(dev))
+    outs = (torch.empty(nf2 * w2 * h2 * 400, dtype=torch.int16, device=dev), torch.empty_like(tt[0]),
+            torch.empty_like(tt[1]), torch.empty_like(tt[2]))
+    cases.append((nf2, w2, h2, c, tt, outs, torch.cuda.Stream(dev)))
+torch.cuda.synchronize()
+for rep in range(3):
+    for nf2, w2, h2, c, tt, outs, st in cases:
+        zwebp.transform_quant_mbs_device(nf2, w2, h2, *[x.data_ptr() for x in tt], *[o.data_ptr() for o in outs],
+                                         stream=st.cuda_stream, ctx=ctx)
+    torch.cuda.synchronize()
+    for nf2, w2, h2, c, tt, outs, st in cases:
+        want2 = O.xform_mbs(c[0], c[1], c[2], c[3], c[4], nf2, w2, h2)
+        assert np.array_equal(outs[0].cpu().numpy().reshape(-1, 25, 16), want2[0]), "levels, two streams"
+        assert np.array_equal(outs[1].cpu().numpy(), want2[1]), "ry, two streams"
 bad = list(args)
 bad[3] += 4  # misaligned records
 try:

@@ -12,6 +12,13 @@ Inputs and expected outputs only -- no reference source is copied:
         (UpsamplingMethod::Simple), gallery1;
       - yuv_sha256: SHA-256 of the cropped Y, U, V planes decoded by the system
         libwebp (WebPDecodeYUV), the independent decoder the survey pins on.
+  * regression/dark.webp (a bare 1x1 'VP8 ' frame) and the four full-canvas
+    VP8 keyframes of animated/random_lossy.webp (ANMF at 0,0, no ALPH, so the
+    reference's composite_frame copies each frame's RGB unchanged,
+    decoder/extended.rs:31-134) with their golden PNGs
+    (tests/reference/regression/dark.png, animated/random_lossy-1..4.png;
+    tests/decode.rs:116-149, :193-202).  Fancy upsampling only (the reference
+    holds no nofancy golden for them).
   * libwebp-encoded synthetic streams (WebPEncodeRGB at several qualities) with
     their libwebp YUV digests -- different quantisers / filter levels /
     segment maps than the gallery.
@@ -53,6 +60,25 @@ _W.WebPEncodeRGB.restype = ctypes.c_size_t
 _W.WebPEncodeRGB.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                              ctypes.POINTER(ctypes.c_void_p)]
 _W.WebPFree.argtypes = [ctypes.c_void_p]
+
+
+def anmf_vp8(data):
+    """VP8 payloads of the ANMF frames of an animated RIFF, with their offsets
+    and sizes (ANMF layout: 3-byte x/2, y/2, w-1, h-1, duration, flags)."""
+    assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"
+    out, off = [], 12
+    while off + 8 <= len(data):
+        tag = data[off:off + 4]
+        size = int.from_bytes(data[off + 4:off + 8], "little")
+        if tag == b"ANMF":
+            p = data[off + 8:off + 8 + size]
+            x, y = 2 * int.from_bytes(p[0:3], "little"), 2 * int.from_bytes(p[3:6], "little")
+            w, h = int.from_bytes(p[6:9], "little") + 1, int.from_bytes(p[9:12], "little") + 1
+            assert p[16:20] == b"VP8 ", "frame is not a bare VP8 chunk"
+            n = int.from_bytes(p[20:24], "little")
+            out.append((x, y, w, h, p[24:24 + n]))
+        off += 8 + size + (size & 1)
+    return out
 
 
 def libwebp_yuv_digests(riff):
@@ -106,6 +132,29 @@ def main():
         W, H, d = libwebp_yuv_digests(wrap_riff(vp8))
         manifest["streams"].append(dict(name=name, source=f"tests/images/gallery2/{i}_webp_a.webp", width=W,
                                         height=H, yuv_sha256=d))
+    # regression/dark (tests/decode.rs:197): 1x1 frame
+    riff = open(f"{REF}/images/regression/dark.webp", "rb").read()
+    vp8 = riff_vp8(riff)
+    open(os.path.join(OUT, "regression_dark.vp8"), "wb").write(vp8)
+    W, H, d = libwebp_yuv_digests(riff)
+    png = np.asarray(Image.open(f"{REF}/reference/regression/dark.png").convert("RGB"))
+    assert png.shape == (H, W, 3)
+    manifest["streams"].append(dict(name="regression_dark", source="tests/images/regression/dark.webp", width=W,
+                                    height=H, yuv_sha256=d, rgb_sha256=hashlib.sha256(png.tobytes()).hexdigest()))
+    # animated/random_lossy (tests/decode.rs:193, every frame :116-149)
+    riff = open(f"{REF}/images/animated/random_lossy.webp", "rb").read()
+    for i, (x, y, w, h, vp8) in enumerate(anmf_vp8(riff), 1):
+        cw = int.from_bytes(riff[24:27], "little") + 1
+        ch = int.from_bytes(riff[27:30], "little") + 1
+        assert (x, y, w, h) == (0, 0, cw, ch), "not a full-canvas frame"
+        name = f"random_lossy_{i}"
+        open(os.path.join(OUT, name + ".vp8"), "wb").write(vp8)
+        W, H, d = libwebp_yuv_digests(wrap_riff(vp8))
+        png = np.asarray(Image.open(f"{REF}/reference/animated/random_lossy-{i}.png").convert("RGB"))
+        assert png.shape == (H, W, 3)
+        manifest["streams"].append(dict(name=name, source=f"tests/images/animated/random_lossy.webp frame {i}",
+                                        width=W, height=H, yuv_sha256=d,
+                                        rgb_sha256=hashlib.sha256(png.tobytes()).hexdigest()))
     for (w, h, kind, q) in [(64, 48, "natural", 75), (333, 211, "natural", 30), (256, 256, "noise", 90),
                             (200, 120, "natural", 5), (160, 96, "natural", 100)]:
         rgb = np.ascontiguousarray(synth_rgba(w, h, 0x5EED0000 + w, kind)[..., :3])
