@@ -533,6 +533,80 @@ def single_frame(ctx, img, w, h, q, m, seed, digests, reps=3):
                     "global memory); pass 1 is bounded by the chroma raster chain (quirk A5) on one wave"}
 
 
+def host_resident(pipe, host_imgs, nb, w, h, q, m, seeds, digests):
+    """PCIe-inclusive rate (zw_pipe_encode_host): the same batch encoded from
+    host memory, as WebPEncoder::encode(&[u8]) callers hand frames over
+    (encoder/api.rs:1291).  Each of the batch's frames is its own pageable host
+    buffer (frame i holds the synthetic frame seeds[i % D]); per batch every
+    frame crosses PCIe again.  Each lane's uploader thread copies batch b+1 into
+    the second device input buffer while batch b's passes run.  The last batch's
+    bitstreams are hashed against the oracle's digests."""
+    import numpy as np
+    n = pipe.n
+    frames = [np.array(host_imgs[i % len(host_imgs)], copy=True) for i in range(n)]
+    pipe.encode_host([frames])  # warm-up: allocates the second input buffer, streams, events
+    t0 = time.perf_counter()
+    pipe.encode_host([frames] * nb)
+    el = time.perf_counter() - t0
+    ok, bad, miss = verify(pipe, n, seeds, w, h, q, m, digests)
+    fb = frames[0].size
+    del frames
+    return {"encodes_per_s": n * nb / el, "frames": n * nb, "batches": nb, "ms_per_batch": el / nb * 1e3,
+            "h2d_bytes_per_frame": fb, "h2d_gbs": n * nb * fb / el / 1e9,
+            "verified": bad == 0 and miss == 0 and ok == n,
+            "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss,
+                             "against": "tests/golden/bench_digests.json (last batch)"},
+            "note": "zw_pipe_encode_host from pageable host RGBA (one buffer per frame); uploads of batch b+1 "
+                    "overlap batch b's kernels on a separate stream per lane"}
+
+
+def seam_threads(img, w, h, q, m, seed, digests, threads=(1, 4, 16), seconds=3.0):
+    """encode_frame_lossy (vp8.rs:3132) as callers use it: T host threads, one
+    context each (a context is not thread-safe), every call one frame from host
+    memory, all on this one GPU.  Each thread warms its context's one-frame
+    pipeline first, then calls the seam in a loop for ~`seconds`.  Every output
+    is hashed against the oracle's digest."""
+    import threading
+    import zwebp
+    tag = f"{w}x{h}/q{q}m{m}/{seed:#010x}"
+    want = digests.get(tag)
+    out = {}
+    for T in threads:
+        ctxs = [zwebp.Context(0) for _ in range(T)]
+        for c in ctxs:
+            zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=c)
+        counts, good = [0] * T, [True] * T
+        start = threading.Barrier(T + 1)
+        stop = [False]
+
+        def work(t):
+            start.wait()
+            while not stop[0]:
+                b = zwebp.encode_frame_lossy(img, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctxs[t])
+                good[t] = good[t] and hashlib.sha256(b).hexdigest() == want
+                counts[t] += 1
+
+        th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        start.wait()
+        t0 = time.perf_counter()
+        time.sleep(seconds)
+        stop[0] = True
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        out[str(T)] = {"encodes_per_s": sum(counts) / el, "calls": sum(counts),
+                       "ms_per_call": T * el / max(1, sum(counts)) * 1e3,
+                       "verified": want is not None and all(good)}
+        for c in ctxs:
+            c.close()
+        del ctxs
+    return {"threads": out, "verified": all(v["verified"] for v in out.values()),
+            "note": "T threads x T contexts, zw_encode_frame_lossy per call (host RGBA in, VP8 bytes out): "
+                    "the row-parallel kernels of concurrent calls share the GPU"}
+
+
 def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
     """Full-container rate (WebPEncoder::encode with EncoderParams::lossy on
     RGBA input, api.rs:1291-1398): the pipe's container mode adds, per frame on
@@ -866,6 +940,8 @@ def main():
             line["single_frame"] = single_frame(ctx, imgs[0], w, h, q, m, seeds[0], digests)
             streams = [bytes(pipes[0][0].output(i)) for i in range(min(B, D))]  # VP8 frames, before container mode
             line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, q, m, seeds, digests)
+            line["host_resident"] = host_resident(pipes[0][0], imgs, 3, w, h, q, m, seeds, digests)
+            line["seam_threads"] = seam_threads(imgs[0], w, h, q, m, seeds[0], digests)
             line["decode_path"] = decode_path(ctx, streams, 256, w, h, not a.no_cpu_baseline, tags, digests)
             del streams
             for pipe, _ in pipes:  # free the headline batch before the 4K leg
@@ -898,8 +974,9 @@ def main():
                                                    line["roofline"]["yuv_planes_form"]["verified"], "see": "roofline"},
                 "3_1080p_decode_path": {"verified": line["decode_path"]["verified"], "see": "decode_path"},
                 "4_1080p_batch_encode": {"verified": line["verified"] and line["single_frame"]["verified"] and
-                                         line["container_rgba"]["verified"],
-                                         "see": "value, single_frame, container_rgba"},
+                                         line["container_rgba"]["verified"] and line["host_resident"]["verified"]
+                                         and line["seam_threads"]["verified"],
+                                         "see": "value, single_frame, container_rgba, host_resident, seam_threads"},
                 "5_4k_batch_n1": {"verified": line["config5_4k_n1"]["verified"], "see": "config5_4k_n1 (N=1 anchor "
                                   "of the 4096-frame split; the driver's SCALE run measures N=2/4/8)"}}
         print(json.dumps(line), flush=True)

@@ -737,9 +737,9 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         const double td = dec_now_ms();
         {
-            int r = ctx_d2h(ctx, hout, d + B.o_y, (size_t)cn * ysz);
-            if (!r) r = ctx_d2h(ctx, hout + (size_t)cn * ysz, d + B.o_u, (size_t)cn * csz);
-            if (!r) r = ctx_d2h(ctx, hout + (size_t)cn * (ysz + csz), d + B.o_v, (size_t)cn * csz);
+            int r = ctx_d2h_stream(ctx, hout, d + B.o_y, (size_t)cn * ysz);
+            if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * ysz, d + B.o_u, (size_t)cn * csz);
+            if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * (ysz + csz), d + B.o_v, (size_t)cn * csz);
             if (r) return r;
         }
         std::vector<int> oom(cn, 0);
@@ -828,7 +828,7 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[3]));
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
-        if (int r = ctx_d2h(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
+        if (int r = ctx_d2h_stream(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
         std::vector<int> oom(cn, 0);
         parallel_for(cn, [&](int i) {
             const uint8_t* src = hout + (size_t)i * fbytes;

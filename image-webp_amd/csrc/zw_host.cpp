@@ -190,6 +190,15 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
     return ZW_OK;
 }
 
+int ctx_d2h_stream(zw_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (bytes == 0) return ZW_OK;
+    if (!c->copy_) HIPOK(hipStreamCreateWithFlags(&c->copy_, hipStreamNonBlocking));
+    HIPOK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->copy_));
+    HIPOK(hipStreamSynchronize(c->copy_));
+    return ZW_OK;
+}
+
 extern "C" void zw_ctx_release_buffers(zw_ctx* c)
 {
     if (!c) return;
@@ -231,6 +240,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
         if (e) (void)hipEventDestroy(e);
     for (void* h : c->hpin) pinned_free(h);
     if (c->stream_) (void)hipStreamDestroy(c->stream_);
+    if (c->copy_) (void)hipStreamDestroy(c->copy_);
     delete c;
 }
 
@@ -313,6 +323,13 @@ struct PipeLane {
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
     int rc = 0;
+    // Host-source streaming (zw_pipe_encode_host): the lane's uploader thread
+    // copies batch b's frames into input buffer b & 1 on `ustream`, one event
+    // per chunk (uev); the kernel stream waits for it before rgb2yuv and records
+    // rev once rgb2yuv has read the buffer, which the upload of batch b + 2 waits for.
+    hipStream_t ustream = nullptr;
+    std::vector<hipEvent_t> uev[2], rev[2];
+    long long uploaded = 0, p1_queued = 0;  // chunks issued (over all batches), under sync->mu
     // Emission runs on its own thread, one batch behind the lane thread.
     // `fetched` counts the chunks whose pass-2 records it has copied out
     // (over all batches): pass 2 of the next batch may then reuse the chunk's
@@ -365,12 +382,17 @@ struct zw_pipe {
     // counters, which the kernels clear themselves, may then be left nonzero,
     // so every later run of this pipe fails instead of reading them.
     bool broken = false;
+    // zw_pipe_encode_host: second input buffer and the host frames of the call
+    // (batch b, frame i at host_src[b * n + i]); null outside such a call
+    uint8_t* d_img2 = nullptr;
+    const uint8_t* const* host_src = nullptr;
+    uint8_t* img_buf(int parity) const { return parity ? d_img2 : d_img; }
 };
 
 static void pipe_free(zw_pipe* p)
 {
     if (!p) return;
-    void* ptrs[] = {p->d_img, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
+    void* ptrs[] = {p->d_img, p->d_img2, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
                     p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg,
                     p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack, p->d_finfo2, p->d_pack2, p->d_stats, p->d_stats_tmp};
     for (void* q : ptrs)
@@ -386,6 +408,13 @@ static void pipe_free(zw_pipe* p)
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
         if (L.stream2) (void)hipStreamDestroy(L.stream2);
+        if (L.ustream) (void)hipStreamDestroy(L.ustream);
+        for (int k = 0; k < 2; k++) {
+            for (hipEvent_t e : L.uev[k])
+                if (e) (void)hipEventDestroy(e);
+            for (hipEvent_t e : L.rev[k])
+                if (e) (void)hipEventDestroy(e);
+        }
     }
     delete p;
 }
@@ -634,14 +663,18 @@ static int rows_check(zw_pipe* p, PipeLane& L)
 }
 
 // ---- per-chunk stages (frames [fa, fa + na) of a lane) ----
-static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false)
+static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false,
+                       int parity = 0, hipEvent_t uploaded = nullptr, hipEvent_t read = nullptr)
 {
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa;
     const int n = na;
+    if (uploaded) HIPOK(hipStreamWaitEvent(s, uploaded, 0));
     if (timed) HIPOK(hipEventRecord(L.ev[0], s));
-    HIPOK(zwk_rgb2yuv(s, p->d_img + F * p->img_stride, p->w, p->h, p->bpp, p->mbw, p->mbh, p->d_Y + F * p->ysz,
-                      p->d_U + F * p->csz, p->d_V + F * p->csz, p->img_stride, p->ysz, p->csz, n));
+    HIPOK(zwk_rgb2yuv(s, p->img_buf(parity) + F * p->img_stride, p->w, p->h, p->bpp, p->mbw, p->mbh,
+                      p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->img_stride, p->ysz, p->csz,
+                      n));
+    if (read) HIPOK(hipEventRecord(read, s));
     if (timed) HIPOK(hipEventRecord(L.ev[1], s));
     HIPOK(zwk_analysis(s, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->mbw, p->mbh, p->ysz,
                        p->csz, p->d_alpha + F * p->nmb, p->d_histo + F * 256, n));
@@ -844,9 +877,29 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     const int nch = (L.n + L.chunk - 1) / L.chunk;
     auto ca = [&](int c) { return L.f0 + c * L.chunk; };
     auto cn = [&](int c) { return std::min(L.chunk, L.n - c * L.chunk); };
+    const bool host = p->host_src != nullptr;
+    const long long FAILED = std::numeric_limits<long long>::max();
+    int qb = 0;  // batch whose pass 1 queue_pass1 queues next
     auto queue_pass1 = [&]() -> int {
+        const int b = qb++;
         for (int c = 0; c < nch; c++) {
-            int r = chunk_pass1(p, L, ca(c), cn(c), c == 0);
+            hipEvent_t ue = nullptr, re = nullptr;
+            if (host) {  // wait until the uploader has issued this chunk's copy
+                std::unique_lock<std::mutex> lk(L.sync->mu);
+                const long long need = (long long)b * nch + c + 1;
+                L.sync->cv.wait(lk, [&] { return L.uploaded >= need; });
+                if (L.uploaded == FAILED) return ZW_EDEVICE;
+                ue = L.uev[b & 1][c];
+                re = L.rev[b & 1][c];
+            }
+            int r = chunk_pass1(p, L, ca(c), cn(c), c == 0, false, host ? (b & 1) : 0, ue, re);
+            if (host) {
+                {
+                    std::lock_guard<std::mutex> lk(L.sync->mu);
+                    L.p1_queued = r ? FAILED : L.p1_queued + 1;
+                }
+                L.sync->cv.notify_all();
+            }
             if (!r) {
                 if (p->host_stats) {
                     r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
@@ -862,13 +915,63 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         }
         return ZW_OK;
     };
-    const long long FAILED = std::numeric_limits<long long>::max();
     double fetch = 0, stats = 0, fetch2 = 0, tok = 0;
     int emit_rc = ZW_OK;
     {
         std::lock_guard<std::mutex> lk(L.sync->mu);
         L.sync->fetched = 0;
+        L.uploaded = L.p1_queued = 0;
     }
+    // host-source uploads: batch b's chunks into input buffer b & 1, each once
+    // rgb2yuv of batch b - 2 has read that buffer's chunk (the copies of batch
+    // b + 1 run while batch b's passes hold the GPU)
+    int up_rc = ZW_OK;
+    std::thread up;
+    if (host) {
+        up = std::thread([&]() {
+            (void)hipSetDevice(p->ctx->device);
+            for (int b = 0; b < nb && !up_rc; b++)
+                for (int c = 0; c < nch && !up_rc; c++) {
+                    if (b >= 2) {
+                        std::unique_lock<std::mutex> lk(L.sync->mu);
+                        const long long need = (long long)(b - 2) * nch + c + 1;
+                        L.sync->cv.wait(lk, [&] { return L.p1_queued >= need; });
+                        if (L.p1_queued == FAILED) {
+                            up_rc = ZW_EDEVICE;
+                            break;
+                        }
+                    }
+                    int r = ZW_OK;
+                    if (b >= 2 && hipStreamWaitEvent(L.ustream, L.rev[b & 1][c], 0) != hipSuccess) r = ZW_EDEVICE;
+                    uint8_t* dst = p->img_buf(b & 1) + (size_t)ca(c) * p->img_stride;
+                    for (int i = 0; i < cn(c) && !r; i++)
+                        if (hipMemcpyAsync(dst + (size_t)i * p->img_stride, p->host_src[(size_t)b * p->n + ca(c) + i],
+                                           p->img_stride, hipMemcpyHostToDevice, L.ustream) != hipSuccess)
+                            r = ZW_EDEVICE;
+                    if (!r && hipEventRecord(L.uev[b & 1][c], L.ustream) != hipSuccess) r = ZW_EDEVICE;
+                    {
+                        std::lock_guard<std::mutex> lk(L.sync->mu);
+                        L.uploaded = r ? FAILED : L.uploaded + 1;
+                    }
+                    L.sync->cv.notify_all();
+                    up_rc = r;
+                }
+        });
+    }
+    auto join_up = [&]() {
+        if (up.joinable()) {
+            if (up_rc == ZW_OK) {  // a lane failure: release the uploader's waits
+                std::lock_guard<std::mutex> lk(L.sync->mu);
+                if (L.p1_queued != FAILED && L.p1_queued < (long long)nb * nch) L.p1_queued = FAILED;
+            }
+            L.sync->cv.notify_all();
+            up.join();
+        }
+    };
+    struct UpGuard {  // every return path joins the uploader
+        decltype(join_up)& f;
+        ~UpGuard() { f(); }
+    } up_guard{join_up};
     // emission of batch b (runs on `em`)
     auto emitter = [&](int b) {
         for (int c = 0; c < nch; c++) {
@@ -910,7 +1013,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         return r;
     };
     int r = queue_pass1();
-    if (r) return r;
+    if (r) return fail(r);
     for (int b = 0; b < nb; b++) {
         for (int c = 0; c < nch; c++) {
             const double t0 = now_ms();
@@ -949,6 +1052,8 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         }
     }
     if ((r = join_emitter())) return r;
+    join_up();
+    if (up_rc) return up_rc;
     p->out_par = (nb - 1) & 1;
     HIPOK(hipStreamSynchronize(L.stream));
     if ((r = rows_check(p, L))) return r;
@@ -1041,6 +1146,41 @@ static int pipe_encode(zw_pipe* p, int nb)
 }
 
 extern "C" int zw_pipe_encode(zw_pipe* p) { return pipe_encode(p, 1); }
+
+// nb batches whose frames are in host memory (frames[b * n + i], img_stride
+// bytes each, any host memory): each lane's uploader thread copies batch b + 1
+// into the second input buffer while batch b's passes run (the PCIe-inclusive
+// form of zw_pipe_encode_repeat).  Outputs are those of the last batch.
+extern "C" int zw_pipe_encode_host(zw_pipe* p, int nb, const uint8_t* const* frames)
+{
+    if (!p || nb < 1 || !frames) return ZW_EINVAL;
+    if (p->broken) return ZW_EDEVICE;
+    if (p->container) return ZW_EINVAL;  // (the ALPH coder reads the frames set by zw_pipe_set_container)
+    for (size_t i = 0; i < (size_t)nb * p->n; i++)
+        if (!frames[i]) return ZW_EINVAL;
+    HIPOK(hipSetDevice(p->ctx->device));
+    if (nb > 1 && !p->d_img2 && hipMalloc(&p->d_img2, (size_t)p->n * p->img_stride + 64) != hipSuccess)
+        return ZW_ENOMEM;
+    for (PipeLane& L : p->lanes) {
+        const int nch = (L.n + L.chunk - 1) / L.chunk;
+        if (!L.ustream) HIPOK(hipStreamCreateWithFlags(&L.ustream, hipStreamNonBlocking));
+        for (int k = 0; k < 2; k++)
+            while ((int)L.uev[k].size() < nch) {
+                hipEvent_t a = nullptr, b = nullptr;
+                HIPOK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+                if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+                    (void)hipEventDestroy(a);
+                    return ZW_EDEVICE;
+                }
+                L.uev[k].push_back(a);
+                L.rev[k].push_back(b);
+            }
+    }
+    p->host_src = frames;
+    const int r = pipe_encode(p, nb);
+    p->host_src = nullptr;
+    return r;
+}
 
 extern "C" int zw_pipe_encode_repeat(zw_pipe* p, int n) { return pipe_encode(p, n); }
 

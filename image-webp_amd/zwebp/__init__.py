@@ -166,6 +166,7 @@ SIGNATURES = [
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
+    ("zw_pipe_encode_host", _I, [_VP, _I, _VP]),
     ("zw_pipe_run_pass1", _I, [_VP, _I]),
     ("zw_pipe_run_device", _I, [_VP]),
     ("zw_pipe_output", _I, [_VP, _I, ctypes.POINTER(_Bytes)]),
@@ -844,6 +845,20 @@ class Pipeline:
         """Encode the batch n times back to back with batch k+1's GPU passes
         overlapping batch k's host token emission (streaming throughput)."""
         _check(self._lib.zw_pipe_encode_repeat(self._h, int(n)), "zw_pipe_encode_repeat", EncodingError)
+
+    def encode_host(self, batches):
+        """PCIe-inclusive streaming encode (zw_pipe_encode_host): batches is a list
+        of nb lists of n host frames; batch b+1 is uploaded while batch b encodes.
+        Outputs (output(i)) are the last batch's."""
+        nb = len(batches)
+        arrs = [_as_u8(im) for bt in batches for im in bt]
+        if nb == 0 or len(arrs) != nb * self.n:
+            raise ValueError("nb batches of n frames")
+        want = self.width * self.height * (1, 2, 3, 4)[self.color]
+        if any(a.size != want for a in arrs):
+            raise ValueError("every frame must be width*height*bpp bytes")
+        ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        _check(self._lib.zw_pipe_encode_host(self._h, nb, ptrs), "zw_pipe_encode_host", EncodingError)
 
     def run_pass1(self, write_recon=True):
         _check(self._lib.zw_pipe_run_pass1(self._h, 1 if write_recon else 0), "zw_pipe_run_pass1", EncodingError)

@@ -326,6 +326,14 @@ int zw_pipe_encode(zw_pipe *p);
  * and the host entropy stage overlap across batches.  Outputs afterwards are
  * those of the last batch (identical to zw_pipe_encode's). */
 int zw_pipe_encode_repeat(zw_pipe *p, int n);
+/* PCIe-inclusive streaming encode of nb batches from host memory: frames[b*n + i]
+ * (img bytes each, any host memory) is frame i of batch b.  Each lane's uploader
+ * thread copies batch b+1 into a second device input buffer while batch b's
+ * passes run, so the host->device copies overlap the kernels.  The outputs
+ * (zw_pipe_output) are the last batch's.  Not with container output (ZW_EINVAL).
+ * Replaces the caller-side loop WebPEncoder::encode(&[u8]) per frame
+ * (encoder/api.rs:1291) for a stream of host frames. */
+int zw_pipe_encode_host(zw_pipe *p, int nb, const uint8_t *const *frames);
 /* Device-only passes (rgb2yuv, analysis, segments, pass 1, stats, pass 2) without
  * token emission, for kernel timing.  Returns 0 or an error. */
 int zw_pipe_run_device(zw_pipe *p);

@@ -210,6 +210,34 @@ def test_encode_webp_batch(ctx, color):
         assert outs[i] == want, f"frame {i}"
 
 
+@pytest.mark.parametrize("nb,lanes,chunk", [(1, "1", "4"), (3, "2", "2"), (4, "1", "3"), (5, "2", "4")])
+def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk):
+    """zw_pipe_encode_host: nb batches streamed from host memory (batch b+1
+    uploaded into the other input buffer while batch b encodes; lanes and chunks
+    forced small so the uploads wait on rgb2yuv of batch b-2 per chunk).  Every
+    batch holds different frames; the last batch's bitstreams equal the oracle's."""
+    monkeypatch.setenv("ZW_PIPE_LANES", lanes)
+    monkeypatch.setenv("ZW_PIPE_CHUNK", chunk)
+    monkeypatch.setenv("ZW_ENC_ROWS", "0")
+    w, h, n = 96, 64, 16  # (two lanes need >= 8 frames each)
+    batches = [[synth_rgba(w, h, 0x5EED6000 + 16 * b + i, ("natural", "noise")[(b + i) % 2]) for i in range(n)]
+               for b in range(nb)]
+    p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    try:
+        p.encode_host(batches)
+        for i in range(n):
+            rc, ref, _ = O.encode(batches[-1][i], w, h, 3, 75, 4)
+            assert rc == 0 and p.output(i) == ref, f"frame {i} of the last batch"
+        # the same pipe afterwards from device-resident input (the first buffer)
+        for i in range(n):
+            p.upload(i, batches[0][i])
+        p.encode()
+        rc, ref, _ = O.encode(batches[0][3], w, h, 3, 75, 4)
+        assert p.output(3) == ref
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("color", [zwebp.ColorType.Rgba8, zwebp.ColorType.La8])
 def test_encode_webp_batch_alpha_too_large(ctx, color):
     """An alpha input taller than 16384 rows: encode_alpha_lossless returns
