@@ -687,6 +687,7 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     const int C = dec_chunk_frames(), nch = (n + C - 1) / C;
     DecBatch B[2];
     ctx->dec_ms[0] = ctx->dec_ms[1] = ctx->dec_ms[2] = 0.f;
+    ctx->dec_host_ms[0] = ctx->dec_host_ms[1] = ctx->dec_host_ms[2] = 0;
     auto first = [&](int c) { return c * C; };
     auto count = [&](int c) { return std::min(C, n - c * C); };
     int err = ZW_OK;
@@ -703,7 +704,10 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
                 if (hipEventElapsedTime(&ms, b.ev[1], b.ev[2]) == hipSuccess) ctx->dec_ms[1] += ms;
             });
         }
-        if (c < nch) err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+        if (c < nch) {
+            err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+            ctx->dec_host_ms[0] += B[c & 1].parse_ms;
+        }
         if (fin.joinable()) fin.join();
         err = err_f ? err_f : err_p;
         if (c < nch && !err) {
@@ -742,6 +746,8 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
             if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * (ysz + csz), d + B.o_v, (size_t)cn * csz);
             if (r) return r;
         }
+        const double tf = dec_now_ms();
+        ctx->dec_host_ms[1] += tf - td;
         std::vector<int> oom(cn, 0);
         parallel_for(cn, [&](int i) {
             uint8_t* buf = (uint8_t*)malloc(fsz);
@@ -754,6 +760,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
             memcpy(buf + ysz + csz, hout + (size_t)cn * (ysz + csz) + (size_t)i * csz, csz);
             outs[f0 + i].y = buf;
         });
+        ctx->dec_host_ms[2] += dec_now_ms() - tf;
         if (dec_timing()) fprintf(stderr, "[dec] download+fanout %.2f ms\n", dec_now_ms() - td);
         int r = ZW_OK;
         for (int i = 0; i < cn; i++) {
@@ -828,7 +835,10 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[3]));
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
+        const double td = dec_now_ms();
         if (int r = ctx_d2h_stream(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
+        const double tf = dec_now_ms();
+        ctx->dec_host_ms[1] += tf - td;
         std::vector<int> oom(cn, 0);
         parallel_for(cn, [&](int i) {
             const uint8_t* src = hout + (size_t)i * fbytes;
@@ -850,6 +860,7 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
             outs[f0 + i].data = buf;
             outs[f0 + i].len = fbytes;
         });
+        ctx->dec_host_ms[2] += dec_now_ms() - tf;
         for (int i = 0; i < cn; i++)
             if (oom[i]) return ZW_ENOMEM;
         float ms = 0.f;
@@ -927,6 +938,13 @@ extern "C" int zw_decode_kernel_times(zw_ctx* ctx, float* ms)
     if (!ctx || !ms) return ZW_EINVAL;
     ms[0] = ctx->dec_ms[0];
     ms[1] = ctx->dec_ms[1];
+    return ZW_OK;
+}
+
+extern "C" int zw_decode_stage_times(zw_ctx* ctx, float* ms)
+{
+    if (!ctx || !ms) return ZW_EINVAL;
+    for (int i = 0; i < 3; i++) ms[i] = (float)ctx->dec_host_ms[i];
     return ZW_OK;
 }
 

@@ -54,6 +54,9 @@ struct zw_ctx {
     hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t dev_ev1[4] = {nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
+    // host stages of the last decode batch, wall ms summed over its chunks:
+    // [0] parse (bool decoder + records), [1] download, [2] fan-out / copy-out
+    double dec_host_ms[3] = {0, 0, 0};
     // one-frame encode pipeline kept between encode_frame_lossy calls of the
     // same shape (dimensions, colour type, quality, method): its device buffers
     // and streams are reused instead of allocated per call

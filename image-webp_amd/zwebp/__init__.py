@@ -164,6 +164,7 @@ SIGNATURES = [
     ("zw_pipe_set_container", _I, [_VP, _I, ctypes.POINTER(_VP)]),
     ("zw_pipe_set_token_partitions", _I, [_VP, _I]),
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
+    ("zw_decode_stage_times", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_encode_host", _I, [_VP, _I, _VP]),
@@ -460,6 +461,15 @@ def decode_kernel_times(ctx=None):
     ms = (ctypes.c_float * 2)()
     _check(c._lib.zw_decode_kernel_times(c.handle, ms), "decode_kernel_times")
     return float(ms[0]), float(ms[1])
+
+
+def decode_stage_times(ctx=None):
+    """Host stages of the last decode batch on `ctx`, wall ms summed over its
+    chunks: (parse, download, fan-out)."""
+    c = _ctx(ctx)
+    ms = (ctypes.c_float * 3)()
+    _check(c._lib.zw_decode_stage_times(c.handle, ms), "decode_stage_times")
+    return float(ms[0]), float(ms[1]), float(ms[2])
 
 
 class UpsamplingMethod:

@@ -209,6 +209,11 @@ int zw_webp_decode_into(zw_ctx *ctx, const uint8_t *data, size_t len, int bpp, i
 /* Device time (HIP events on the context stream) of the last decode batch:
  * ms[0] = k_dec_recon (dequant + iWHT/iDCT + prediction), ms[1] = k_loopfilter. */
 int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
+/* Host stages of the last decode batch on ctx, wall ms summed over its chunks
+ * (chunks overlap: parse of chunk c runs beside the download of chunk c-1):
+ * ms[0] header/mode/token parse (bool decoder, all host threads), ms[1] planes
+ * or images device->host, ms[2] fan-out into the output buffers. */
+int zw_decode_stage_times(zw_ctx *ctx, float *ms);
 /* ... and of its k_yuv2rgb launch (0 when the batch returned planes). */
 int zw_decode_rgb_kernel_ms(zw_ctx *ctx, float *ms);
 
