@@ -327,9 +327,13 @@ struct PipeLane {
     // copies batch b's frames into input buffer b & 1 on `ustream`, one event
     // per chunk (uev); the kernel stream waits for it before rgb2yuv and records
     // rev once rgb2yuv has read the buffer, which the upload of batch b + 2 waits for.
-    hipStream_t ustream = nullptr;
+    // U uploaders per lane (frames i % U == u of every chunk), each with its own
+    // stream and events uev[parity][u * nch + c]: a pageable copy costs its
+    // calling thread about a millisecond per 1080p frame (pinning / staging).
+    std::vector<hipStream_t> ustreams;
     std::vector<hipEvent_t> uev[2], rev[2];
-    long long uploaded = 0, p1_queued = 0;  // chunks issued (over all batches), under sync->mu
+    std::vector<long long> uploaded;  // per uploader: chunks issued (over all batches), under sync->mu
+    long long p1_queued = 0;
     // Emission runs on its own thread, one batch behind the lane thread.
     // `fetched` counts the chunks whose pass-2 records it has copied out
     // (over all batches): pass 2 of the next batch may then reuse the chunk's
@@ -408,7 +412,7 @@ static void pipe_free(zw_pipe* p)
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
         if (L.stream2) (void)hipStreamDestroy(L.stream2);
-        if (L.ustream) (void)hipStreamDestroy(L.ustream);
+        for (hipStream_t u : L.ustreams) (void)hipStreamDestroy(u);
         for (int k = 0; k < 2; k++) {
             for (hipEvent_t e : L.uev[k])
                 if (e) (void)hipEventDestroy(e);
@@ -884,11 +888,19 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         const int b = qb++;
         for (int c = 0; c < nch; c++) {
             hipEvent_t ue = nullptr, re = nullptr;
-            if (host) {  // wait until the uploader has issued this chunk's copy
+            if (host) {  // wait until every uploader has issued its copies of this chunk
                 std::unique_lock<std::mutex> lk(L.sync->mu);
                 const long long need = (long long)b * nch + c + 1;
-                L.sync->cv.wait(lk, [&] { return L.uploaded >= need; });
-                if (L.uploaded == FAILED) return ZW_EDEVICE;
+                L.sync->cv.wait(lk, [&] {
+                    for (long long u : L.uploaded)
+                        if (u < need) return false;
+                    return true;
+                });
+                for (long long u : L.uploaded)
+                    if (u == FAILED) return ZW_EDEVICE;
+                lk.unlock();
+                for (size_t u = 1; u < L.ustreams.size(); u++)
+                    HIPOK(hipStreamWaitEvent(L.stream, L.uev[b & 1][u * nch + c], 0));
                 ue = L.uev[b & 1][c];
                 re = L.rev[b & 1][c];
             }
@@ -920,53 +932,61 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     {
         std::lock_guard<std::mutex> lk(L.sync->mu);
         L.sync->fetched = 0;
-        L.uploaded = L.p1_queued = 0;
+        L.uploaded.assign(host ? L.ustreams.size() : 0, 0);
+        L.p1_queued = 0;
     }
     // host-source uploads: batch b's chunks into input buffer b & 1, each once
     // rgb2yuv of batch b - 2 has read that buffer's chunk (the copies of batch
     // b + 1 run while batch b's passes hold the GPU)
-    int up_rc = ZW_OK;
-    std::thread up;
+    std::atomic<int> up_rc{ZW_OK};
+    std::vector<std::thread> up;
     if (host) {
-        up = std::thread([&]() {
-            (void)hipSetDevice(p->ctx->device);
-            for (int b = 0; b < nb && !up_rc; b++)
-                for (int c = 0; c < nch && !up_rc; c++) {
-                    if (b >= 2) {
-                        std::unique_lock<std::mutex> lk(L.sync->mu);
-                        const long long need = (long long)(b - 2) * nch + c + 1;
-                        L.sync->cv.wait(lk, [&] { return L.p1_queued >= need; });
-                        if (L.p1_queued == FAILED) {
-                            up_rc = ZW_EDEVICE;
-                            break;
+        const int U = (int)L.ustreams.size();
+        for (int u = 0; u < U; u++)
+            up.emplace_back([&, u]() {
+                (void)hipSetDevice(p->ctx->device);
+                hipStream_t us = L.ustreams[u];
+                for (int b = 0; b < nb && !up_rc; b++)
+                    for (int c = 0; c < nch && !up_rc; c++) {
+                        if (b >= 2) {
+                            std::unique_lock<std::mutex> lk(L.sync->mu);
+                            const long long need = (long long)(b - 2) * nch + c + 1;
+                            L.sync->cv.wait(lk, [&] { return L.p1_queued >= need; });
+                            if (L.p1_queued == FAILED) {
+                                up_rc = ZW_EDEVICE;
+                                L.uploaded[u] = FAILED;
+                                lk.unlock();
+                                L.sync->cv.notify_all();
+                                return;
+                            }
                         }
+                        int r = ZW_OK;
+                        if (b >= 2 && hipStreamWaitEvent(us, L.rev[b & 1][c], 0) != hipSuccess) r = ZW_EDEVICE;
+                        uint8_t* dst = p->img_buf(b & 1) + (size_t)ca(c) * p->img_stride;
+                        for (int i = u; i < cn(c) && !r; i += U)
+                            if (hipMemcpyAsync(dst + (size_t)i * p->img_stride,
+                                               p->host_src[(size_t)b * p->n + ca(c) + i], p->img_stride,
+                                               hipMemcpyHostToDevice, us) != hipSuccess)
+                                r = ZW_EDEVICE;
+                        if (!r && hipEventRecord(L.uev[b & 1][u * nch + c], us) != hipSuccess) r = ZW_EDEVICE;
+                        {
+                            std::lock_guard<std::mutex> lk(L.sync->mu);
+                            L.uploaded[u] = r ? FAILED : L.uploaded[u] + 1;
+                        }
+                        L.sync->cv.notify_all();
+                        if (r) up_rc = r;
                     }
-                    int r = ZW_OK;
-                    if (b >= 2 && hipStreamWaitEvent(L.ustream, L.rev[b & 1][c], 0) != hipSuccess) r = ZW_EDEVICE;
-                    uint8_t* dst = p->img_buf(b & 1) + (size_t)ca(c) * p->img_stride;
-                    for (int i = 0; i < cn(c) && !r; i++)
-                        if (hipMemcpyAsync(dst + (size_t)i * p->img_stride, p->host_src[(size_t)b * p->n + ca(c) + i],
-                                           p->img_stride, hipMemcpyHostToDevice, L.ustream) != hipSuccess)
-                            r = ZW_EDEVICE;
-                    if (!r && hipEventRecord(L.uev[b & 1][c], L.ustream) != hipSuccess) r = ZW_EDEVICE;
-                    {
-                        std::lock_guard<std::mutex> lk(L.sync->mu);
-                        L.uploaded = r ? FAILED : L.uploaded + 1;
-                    }
-                    L.sync->cv.notify_all();
-                    up_rc = r;
-                }
-        });
+            });
     }
     auto join_up = [&]() {
-        if (up.joinable()) {
-            if (up_rc == ZW_OK) {  // a lane failure: release the uploader's waits
-                std::lock_guard<std::mutex> lk(L.sync->mu);
-                if (L.p1_queued != FAILED && L.p1_queued < (long long)nb * nch) L.p1_queued = FAILED;
-            }
-            L.sync->cv.notify_all();
-            up.join();
+        if (up.empty()) return;
+        {  // a lane that stops early releases the uploaders' waits
+            std::lock_guard<std::mutex> lk(L.sync->mu);
+            if (L.p1_queued != FAILED && L.p1_queued < (long long)nb * nch) L.p1_queued = FAILED;
         }
+        L.sync->cv.notify_all();
+        for (auto& t : up) t.join();
+        up.clear();
     };
     struct UpGuard {  // every return path joins the uploader
         decltype(join_up)& f;
@@ -1053,7 +1073,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     }
     if ((r = join_emitter())) return r;
     join_up();
-    if (up_rc) return up_rc;
+    if (up_rc.load()) return up_rc.load();
     p->out_par = (nb - 1) & 1;
     HIPOK(hipStreamSynchronize(L.stream));
     if ((r = rows_check(p, L))) return r;
@@ -1159,22 +1179,43 @@ extern "C" int zw_pipe_encode_host(zw_pipe* p, int nb, const uint8_t* const* fra
     for (size_t i = 0; i < (size_t)nb * p->n; i++)
         if (!frames[i]) return ZW_EINVAL;
     HIPOK(hipSetDevice(p->ctx->device));
+    // uploaders per lane: ZW_UPLOAD_THREADS, else a quarter of the host threads
+    // over the lanes (the rest code the bitstreams), at least one
+    const char* ue = getenv("ZW_UPLOAD_THREADS");
+    int U = ue ? atoi(ue) : host_threads() / (4 * (int)p->lanes.size());
+    U = std::max(1, std::min(U, 16));
+    for (PipeLane& L : p->lanes)
+        if (!L.ustreams.empty() && (int)L.ustreams.size() != U) {  // a different count: rebuild the uev table
+            for (int k = 0; k < 2; k++) {
+                for (hipEvent_t e : L.uev[k]) (void)hipEventDestroy(e);
+                L.uev[k].clear();
+            }
+            while ((int)L.ustreams.size() > U) {
+                (void)hipStreamDestroy(L.ustreams.back());
+                L.ustreams.pop_back();
+            }
+        }
     if (nb > 1 && !p->d_img2 && hipMalloc(&p->d_img2, (size_t)p->n * p->img_stride + 64) != hipSuccess)
         return ZW_ENOMEM;
     for (PipeLane& L : p->lanes) {
         const int nch = (L.n + L.chunk - 1) / L.chunk;
-        if (!L.ustream) HIPOK(hipStreamCreateWithFlags(&L.ustream, hipStreamNonBlocking));
-        for (int k = 0; k < 2; k++)
-            while ((int)L.uev[k].size() < nch) {
-                hipEvent_t a = nullptr, b = nullptr;
+        while ((int)L.ustreams.size() < U) {
+            hipStream_t st;
+            HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            L.ustreams.push_back(st);
+        }
+        for (int k = 0; k < 2; k++) {
+            while ((int)L.uev[k].size() < U * nch) {
+                hipEvent_t a = nullptr;
                 HIPOK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
-                if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
-                    (void)hipEventDestroy(a);
-                    return ZW_EDEVICE;
-                }
                 L.uev[k].push_back(a);
-                L.rev[k].push_back(b);
             }
+            while ((int)L.rev[k].size() < nch) {
+                hipEvent_t a = nullptr;
+                HIPOK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+                L.rev[k].push_back(a);
+            }
+        }
     }
     p->host_src = frames;
     const int r = pipe_encode(p, nb);

@@ -210,8 +210,9 @@ def test_encode_webp_batch(ctx, color):
         assert outs[i] == want, f"frame {i}"
 
 
-@pytest.mark.parametrize("nb,lanes,chunk", [(1, "1", "4"), (3, "2", "2"), (4, "1", "3"), (5, "2", "4")])
-def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk):
+@pytest.mark.parametrize("nb,lanes,chunk,up", [(1, "1", "4", "1"), (3, "2", "2", "3"), (4, "1", "3", "2"),
+                                                (5, "2", "4", "1")])
+def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk, up):
     """zw_pipe_encode_host: nb batches streamed from host memory (batch b+1
     uploaded into the other input buffer while batch b encodes; lanes and chunks
     forced small so the uploads wait on rgb2yuv of batch b-2 per chunk).  Every
@@ -219,6 +220,7 @@ def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk):
     monkeypatch.setenv("ZW_PIPE_LANES", lanes)
     monkeypatch.setenv("ZW_PIPE_CHUNK", chunk)
     monkeypatch.setenv("ZW_ENC_ROWS", "0")
+    monkeypatch.setenv("ZW_UPLOAD_THREADS", up)
     w, h, n = 96, 64, 16  # (two lanes need >= 8 frames each)
     batches = [[synth_rgba(w, h, 0x5EED6000 + 16 * b + i, ("natural", "noise")[(b + i) % 2]) for i in range(n)]
                for b in range(nb)]
@@ -228,6 +230,12 @@ def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk):
         for i in range(n):
             rc, ref, _ = O.encode(batches[-1][i], w, h, 3, 75, 4)
             assert rc == 0 and p.output(i) == ref, f"frame {i} of the last batch"
+        # again on the same pipe with another uploader count, batches reversed
+        monkeypatch.setenv("ZW_UPLOAD_THREADS", "2" if up != "2" else "4")
+        p.encode_host(batches[::-1])
+        for i in (0, n - 1):
+            rc, ref, _ = O.encode(batches[0][i], w, h, 3, 75, 4)
+            assert p.output(i) == ref, f"frame {i}, second call"
         # the same pipe afterwards from device-resident input (the first buffer)
         for i in range(n):
             p.upload(i, batches[0][i])
