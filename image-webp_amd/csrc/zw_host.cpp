@@ -943,7 +943,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     if (host) {
         const int U = (int)L.ustreams.size();
         for (int u = 0; u < U; u++)
-            up.emplace_back([&, u]() {
+            up.emplace_back([&, u, U]() {  // (U by value: it goes out of scope before the threads end)
                 (void)hipSetDevice(p->ctx->device);
                 hipStream_t us = L.ustreams[u];
                 for (int b = 0; b < nb && !up_rc; b++)
