@@ -190,6 +190,34 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes)
     return ZW_OK;
 }
 
+// Host->device copy on a DMA engine, started (not waited for): `src` must be
+// pinned.  The caller waits on `sig` (value 1 -> 0) with sdma_wait.
+static int sdma_h2d_start(zw_ctx* c, void* dst, const void* src, size_t bytes, hsa_signal_t sig)
+{
+    if (c->poisoned.load(std::memory_order_acquire)) return ZW_EDEVICE;
+    hsa_signal_store_relaxed(sig, 1);
+    return hsa_amd_memory_async_copy(dst, c->gpu_agent, src, c->cpu_agent, bytes, 0, nullptr, sig) ==
+                   HSA_STATUS_SUCCESS
+               ? ZW_OK
+               : ZW_EDEVICE;
+}
+// Bounded wait for a DMA started by sdma_h2d_start; a copy that does not
+// complete poisons the context (its source staging stays allocated).
+static int sdma_wait(zw_ctx* c, hsa_signal_t sig)
+{
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    for (;;) {
+        const hsa_signal_value_t v =
+            hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 100000000ull, HSA_WAIT_STATE_BLOCKED);
+        if (v == 0) return ZW_OK;
+        if (std::chrono::steady_clock::now() > deadline) {
+            c->poisoned.store(true, std::memory_order_release);
+            g_dma_poisoned.store(true, std::memory_order_release);
+            return ZW_EDEVICE;
+        }
+    }
+}
+
 int ctx_d2h_stream(zw_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return ZW_OK;
@@ -334,6 +362,12 @@ struct PipeLane {
     std::vector<hipEvent_t> uev[2], rev[2];
     std::vector<long long> uploaded;  // per uploader: chunks issued (over all batches), under sync->mu
     long long p1_queued = 0;
+    // DMA-engine uploads (the default when the HSA agents resolve): per uploader
+    // two pinned frame slots and their completion signals.  HIP's own H2D of
+    // large copies runs as a blit kernel, which waits for CUs the encode
+    // launches hold, so it would not overlap them.
+    std::vector<uint8_t*> ustage;      // [2 * U]
+    std::vector<hsa_signal_t> usig;    // [2 * U]
     // Emission runs on its own thread, one batch behind the lane thread.
     // `fetched` counts the chunks whose pass-2 records it has copied out
     // (over all batches): pass 2 of the next batch may then reuse the chunk's
@@ -413,6 +447,9 @@ static void pipe_free(zw_pipe* p)
         if (L.stream) (void)hipStreamDestroy(L.stream);
         if (L.stream2) (void)hipStreamDestroy(L.stream2);
         for (hipStream_t u : L.ustreams) (void)hipStreamDestroy(u);
+        for (uint8_t* b : L.ustage) pinned_free(b);
+        if (!g_dma_poisoned.load())
+            for (hsa_signal_t sg : L.usig) (void)hsa_signal_destroy(sg);
         for (int k = 0; k < 2; k++) {
             for (hipEvent_t e : L.uev[k])
                 if (e) (void)hipEventDestroy(e);
@@ -961,13 +998,34 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                             }
                         }
                         int r = ZW_OK;
-                        if (b >= 2 && hipStreamWaitEvent(us, L.rev[b & 1][c], 0) != hipSuccess) r = ZW_EDEVICE;
                         uint8_t* dst = p->img_buf(b & 1) + (size_t)ca(c) * p->img_stride;
-                        for (int i = u; i < cn(c) && !r; i += U)
-                            if (hipMemcpyAsync(dst + (size_t)i * p->img_stride,
-                                               p->host_src[(size_t)b * p->n + ca(c) + i], p->img_stride,
-                                               hipMemcpyHostToDevice, us) != hipSuccess)
-                                r = ZW_EDEVICE;
+                        if (!L.ustage.empty()) {
+                            // staged through the uploader's two pinned slots onto a DMA
+                            // engine; the chunk is complete in HBM before it is published
+                            if (b >= 2 && hipEventSynchronize(L.rev[b & 1][c]) != hipSuccess) r = ZW_EDEVICE;
+                            bool busy[2] = {false, false};
+                            int k = 0;
+                            for (int i = u; i < cn(c) && !r; i += U, k++) {
+                                const int sl = k & 1;
+                                if (busy[sl] && (r = sdma_wait(p->ctx, L.usig[2 * u + sl]))) break;
+                                memcpy(L.ustage[2 * u + sl], p->host_src[(size_t)b * p->n + ca(c) + i], p->img_stride);
+                                r = sdma_h2d_start(p->ctx, dst + (size_t)i * p->img_stride, L.ustage[2 * u + sl],
+                                                   p->img_stride, L.usig[2 * u + sl]);
+                                busy[sl] = r == ZW_OK;
+                            }
+                            for (int sl = 0; sl < 2; sl++)
+                                if (busy[sl]) {
+                                    const int w = sdma_wait(p->ctx, L.usig[2 * u + sl]);
+                                    if (!r) r = w;
+                                }
+                        } else {
+                            if (b >= 2 && hipStreamWaitEvent(us, L.rev[b & 1][c], 0) != hipSuccess) r = ZW_EDEVICE;
+                            for (int i = u; i < cn(c) && !r; i += U)
+                                if (hipMemcpyAsync(dst + (size_t)i * p->img_stride,
+                                                   p->host_src[(size_t)b * p->n + ca(c) + i], p->img_stride,
+                                                   hipMemcpyHostToDevice, us) != hipSuccess)
+                                    r = ZW_EDEVICE;
+                        }
                         if (!r && hipEventRecord(L.uev[b & 1][u * nch + c], us) != hipSuccess) r = ZW_EDEVICE;
                         {
                             std::lock_guard<std::mutex> lk(L.sync->mu);
@@ -1203,6 +1261,28 @@ extern "C" int zw_pipe_encode_host(zw_pipe* p, int nb, const uint8_t* const* fra
             hipStream_t st;
             HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             L.ustreams.push_back(st);
+        }
+        // DMA staging (ZW_UPLOAD_SDMA=0: HIP copies instead)
+        const char* se = getenv("ZW_UPLOAD_SDMA");
+        const bool want = !(se && atoi(se) == 0) && sdma_probe(p->ctx);
+        if (!want || (int)L.ustage.size() != 2 * U) {
+            for (uint8_t* b : L.ustage) pinned_free(b);
+            for (hsa_signal_t sg : L.usig) (void)hsa_signal_destroy(sg);
+            L.ustage.clear();
+            L.usig.clear();
+        }
+        if (want && L.ustage.empty()) {
+            for (int k = 0; k < 2 * U; k++) {
+                void* b = nullptr;
+                hsa_signal_t sg;
+                if (hipHostMalloc(&b, p->img_stride, hipHostMallocDefault) != hipSuccess) return ZW_ENOMEM;
+                if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
+                    pinned_free(b);
+                    return ZW_EDEVICE;
+                }
+                L.ustage.push_back((uint8_t*)b);
+                L.usig.push_back(sg);
+            }
         }
         for (int k = 0; k < 2; k++) {
             while ((int)L.uev[k].size() < U * nch) {

@@ -32,8 +32,10 @@ for i in range(F):
     t = torch.empty(w * h * 4, dtype=torch.uint8, pin_memory=True)
     t.numpy()[:] = pageable[i]
     pinned.append(t.numpy())
-for name, frames in (("pageable", pageable), ("pinned", pinned)):
-    for u in ("1", "2", "4", "8"):
+for name, frames, sd in (("pageable sdma", pageable, "1"), ("pinned sdma", pinned, "1"),
+                         ("pageable hip", pageable, "0")):
+    os.environ["ZW_UPLOAD_SDMA"] = sd
+    for u in ("1", "2", "4"):
         os.environ["ZW_UPLOAD_THREADS"] = u
         p.encode_host([frames])
         t0 = time.perf_counter()
