@@ -137,14 +137,23 @@ DI void recon_words(int* c, const uint32_t* pw, uint32_t* rw)
         rw[i] = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
     }
 }
+// 32 bytes into LDS as two 16-byte writes, the second half first when `swap`:
+// lanes whose 32-byte slots are 256 bytes apart (the same 64 banks) then write
+// different halves in each instruction (no 2-way bank conflict)
+DI void lds_put32(uint32_t* o, const uint32_t* lw, bool swap)
+{
+    const v4u a = v4u{lw[0], lw[1], lw[2], lw[3]}, b = v4u{lw[4], lw[5], lw[6], lw[7]};
+    const int h = swap ? 4 : 0;
+    *(v4u*)(o + h) = swap ? b : a;
+    *(v4u*)(o + 4 - h) = swap ? a : b;
+}
 // a block's 16 levels in zigzag order as 8 words of i16 pairs, into LDS
-DI void stage_levels(uint32_t* o, const int* lv)
+DI void stage_levels(uint32_t* o, const int* lv, bool swap)
 {
     uint32_t lw[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) lw[q] = pack_lo(lv[kZZ(2 * q)], lv[kZZ(2 * q + 1)]);
-    *(v4u*)o = v4u{lw[0], lw[1], lw[2], lw[3]};
-    *(v4u*)(o + 4) = v4u{lw[4], lw[5], lw[6], lw[7]};
+    lds_put32(o, lw, swap);
 }
 DI void store_levels(int16_t* out, const int* lv)
 {
@@ -355,7 +364,10 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const uint8_t* img = Y + (size_t)f * img_stride;
 #pragma unroll
             for (int k = 0; k < 2; k++) {
-                const int item = lane + 64 * k, pr = item >> 4, xr = item & 15;
+                // chroma row pr of the item: pass k, 16-lane group g takes rows
+                // {0, 4, 2, 6} / {1, 5, 3, 7}, so the two groups of each half-wave
+                // write luma rows 2 pr 288 bytes apart (disjoint banks) instead of 144
+                const int g = lane >> 4, pr = (((g & 1) << 2) | ((g >> 1) << 1)) + k, xr = lane & 15;
                 if ((xr >> 1) < nact) {
                     uint32_t ya[2], yb[2], uw, vw;
                     rgb_item<SRC>(img, w, h, runs, (x0 + (xr >> 1)) * 16 + 8 * (xr & 1), mby * 8 + pr, ya, yb, uw, vw);
@@ -456,9 +468,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             // leave from the lanes (256 B a MB), so no level is held across the luma
             chroma();
             if (cm < XMB_MBS / 2) {
-                uint32_t* o = &L.lev[cm][136 + 8 * (4 * cplane + csub)];
-                *(v4u*)o = v4u{clw[0], clw[1], clw[2], clw[3]};
-                *(v4u*)(o + 4) = v4u{clw[4], clw[5], clw[6], clw[7]};
+                lds_put32(&L.lev[cm][136 + 8 * (4 * cplane + csub)], clw, cm & 1);
             } else if (cm < nact) {
                 v4u* o = (v4u*)(levels + ((mb0 + cm) * 25 + 17 + 4 * cplane + csub) * 16);
                 __builtin_nontemporal_store(v4u{clw[0], clw[1], clw[2], clw[3]}, o);
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                     c[k] = m24(lv[k], my1.q[1]);
                 }
                 c[0] = dcv;
-                if constexpr (STG) stage_levels(&L.lev[ml][8 * blk], lv);
+                if constexpr (STG) stage_levels(&L.lev[ml][8 * blk], lv, blk >= 8);
                 else if (m < nact) store_levels(levels + ((mb0 + m) * 25 + blk) * 16, lv);
                 uint32_t rw[4];
                 recon_words(c, pw, rw);
@@ -551,9 +561,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             chroma();
             const int m = cm;
             if constexpr (STG) {
-                uint32_t* o = &L.lev[m][136 + 8 * (4 * cplane + csub)];
-                *(v4u*)o = v4u{clw[0], clw[1], clw[2], clw[3]};
-                *(v4u*)(o + 4) = v4u{clw[4], clw[5], clw[6], clw[7]};
+                lds_put32(&L.lev[m][136 + 8 * (4 * cplane + csub)], clw, m & 1);
             } else if (m < nact) {
                 v4u* o = (v4u*)(levels + ((mb0 + m) * 25 + 17 + 4 * cplane + csub) * 16);
                 __builtin_nontemporal_store(v4u{clw[0], clw[1], clw[2], clw[3]}, o);
