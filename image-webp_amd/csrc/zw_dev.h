@@ -581,15 +581,12 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
     int c0 = ctx0, c1 = ctx0;  // ctx selecting the predecessor's cost table
     int bn = -1, bd = 0, bp = 0;
     unsigned prevbits = 0;
-    // the neutral-bias levels as i16 pairs and the signs as a mask (register
-    // pressure: the I16 caller runs this beside its 16-coefficient arrays)
-    uint32_t lvp[8];
-    unsigned sgm = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) lvp[i] = 0;
+    int lv0[16], sg[16];
     const uint32_t nbias = ((0u << 17) + 128) >> 8, tbias = ((0x80u << 17) + 128) >> 8;
 #pragma unroll
     for (int n = FIRST; n < 16; n++) {
+        lv0[n] = 0;
+        sg[n] = 0;
         if (n <= last) {
             const int j = kZZ(n);
             const int q = j == 0 ? (int)m.q[0] : qac;
@@ -641,8 +638,8 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
             s1 = ns1;
             c0 = nc0;
             c1 = nc1;
-            lvp[n >> 1] |= (uint32_t)l0 << (16 * (n & 1));
-            sgm |= (unsigned)sign << n;
+            lv0[n] = l0;
+            sg[n] = sign;
         }
     }
 #pragma unroll
@@ -656,8 +653,8 @@ DI int trellis(int* coeffs, int* out, const ZwMatrix& m, const uint16_t* sharpen
     for (int n = 15; n >= FIRST; n--) {
         if (n <= bn) {
             const int j = kZZ(n);
-            const int level = (int)((lvp[n >> 1] >> (16 * (n & 1))) & 0xffffu) + cd;
-            const int v = ((sgm >> n) & 1u) ? -level : level;
+            const int level = lv0[n] + cd;
+            const int v = sg[n] ? -level : level;
             out[n] = v;
             coeffs[j] = mul(v, (int)(j == 0 ? m.q[0] : m.q[1]));
             nz |= v != 0;

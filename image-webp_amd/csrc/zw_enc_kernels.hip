@@ -1837,34 +1837,26 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             const int shf = 3 + above + left;
             dcv = (!above && !left) ? 128 : ((su + (1 << (shf - 1))) >> shf);
         }
-        // the block's prediction from the border bytes (row 0 / column 0 of ws,
-        // which the reconstruction below never overwrites): formed here for the
-        // residual and again for the reconstruction, instead of holding 16
-        // values live across the trellis
-        auto pred16 = [&](int* pr) {
+        int c[16], pr[16];
+        {
+            // every 16-lane group computes its block's coefficients (lanes 16..47
+            // feed the ctx-parallel trellis)
             const int P0 = ws[0];
-            int L[4], Tp[4];
+            int L[4], Tp[4], r[16];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 L[i] = ws[(by * 4 + i + 1) * ZW_BPS];
                 Tp[i] = ws[1 + bx * 4 + i];
             }
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) pr[i * 4 + j] = sel4(mode, dcv, Tp[j], L[i], clamp255(L[i] + Tp[j] - P0));
-        };
-        int c[16];
-        {
-            // every 16-lane group computes its block's coefficients (lanes 16..47
-            // feed the ctx-parallel trellis)
-            int pr[16], r[16];
-            pred16(pr);
-#pragma unroll
             for (int i = 0; i < 4; i++) {
                 const uint32_t srow = *(const uint32_t*)(C.sY + (by * 4 + i) * 16 + bx * 4);
 #pragma unroll
-                for (int j = 0; j < 4; j++) r[i * 4 + j] = (int)((srow >> (8 * j)) & 255u) - pr[i * 4 + j];
+                for (int j = 0; j < 4; j++) {
+                    const int p = sel4(mode, dcv, Tp[j], L[i], clamp255(L[i] + Tp[j] - P0));
+                    pr[i * 4 + j] = p;
+                    r[i * 4 + j] = (int)((srow >> (8 * j)) & 255u) - p;
+                }
             }
             fdct16_pk(r, c);
         }
@@ -1951,8 +1943,6 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             for (int n = 0; n < 16; n++) W->lev[b][n] = (int16_t)lv[n];
             dq[0] = y2dq;
             idct16(dq);
-            int pr[16];
-            pred16(pr);
             uint8_t* wsp = W->ws;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
