@@ -218,6 +218,26 @@ static int sdma_wait(zw_ctx* c, hsa_signal_t sig)
     }
 }
 
+// Is [p, p + n) page-locked host memory the DMA engines can read (hipHostMalloc
+// or hipHostRegister)?  Such frames go to the engine directly, with no copy
+// through the uploader's staging slot.
+static bool host_pinned(const void* p, size_t n)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // (pageable memory: not an error worth keeping)
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost || !a.hostPointer) return false;
+    // the registration must cover the whole frame: its end must resolve too
+    hipPointerAttribute_t b;
+    if (hipPointerGetAttributes(&b, (const uint8_t*)p + n - 1) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return b.type == hipMemoryTypeHost;
+}
+
 int ctx_d2h_stream(zw_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return ZW_OK;
@@ -1008,9 +1028,13 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                             for (int i = u; i < cn(c) && !r; i += U, k++) {
                                 const int sl = k & 1;
                                 if (busy[sl] && (r = sdma_wait(p->ctx, L.usig[2 * u + sl]))) break;
-                                memcpy(L.ustage[2 * u + sl], p->host_src[(size_t)b * p->n + ca(c) + i], p->img_stride);
-                                r = sdma_h2d_start(p->ctx, dst + (size_t)i * p->img_stride, L.ustage[2 * u + sl],
-                                                   p->img_stride, L.usig[2 * u + sl]);
+                                const uint8_t* src = p->host_src[(size_t)b * p->n + ca(c) + i];
+                                if (!host_pinned(src, p->img_stride)) {  // pageable: through the slot
+                                    memcpy(L.ustage[2 * u + sl], src, p->img_stride);
+                                    src = L.ustage[2 * u + sl];
+                                }
+                                r = sdma_h2d_start(p->ctx, dst + (size_t)i * p->img_stride, src, p->img_stride,
+                                                   L.usig[2 * u + sl]);
                                 busy[sl] = r == ZW_OK;
                             }
                             for (int sl = 0; sl < 2; sl++)
