@@ -877,30 +877,25 @@ static void emit_vp8(zw_pipe* p, std::vector<uint8_t>& out, const uint8_t* rec, 
     }
 }
 
-// Frames are coded two at a time per host thread (zwh::emit_frame_pair: the
-// two token partitions' coder chains interleaved) when each has one token
-// partition; ZW_EMIT_PAIRS=0 codes one frame per task.
-static bool emit_pairs()
-{
-    static const bool on = []() {
-        const char* e = getenv("ZW_EMIT_PAIRS");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 static int chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
     const FetchBuf& B = L.fb[1];
     std::atomic<int> err{ZW_OK};
-    // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the VP8
-    // frame, and for alpha inputs the ALPH chunk (encode_alpha_lossless)
-    auto wrap = [&](size_t f, const std::vector<uint8_t>& vp8) {
+    parallel_for(na, [&](int i) {
+        const size_t f = F + i, hf = hidx(p, par, f);
         std::vector<uint8_t>& out = p->bitstreams[f];
-        thread_local std::vector<uint8_t> alph;
+        if (!p->container) {
+            emit_vp8(p, out, B.pack + B.finfo[2 * i], hf, na);
+            return;
+        }
+        // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the
+        // VP8 frame, and for alpha inputs the ALPH chunk (encode_alpha_lossless)
+        thread_local std::vector<uint8_t> vp8, alph;
+        vp8.clear();
         alph.clear();
+        emit_vp8(p, vp8, B.pack + B.finfo[2 * i], hf, na);
         out.clear();
         if (has_alpha) {
             if (const int r = zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph)) {
@@ -911,51 +906,6 @@ static int chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
         }
         const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
         zw_webp_wrap(out, vp8.data(), vp8.size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w, p->h, md);
-    };
-    if (p->nparts == 1 && na >= 2 && emit_pairs()) {
-        parallel_for((na + 1) / 2, [&](int k) {
-            const int i0 = 2 * k, i1 = 2 * k + 1;
-            if (i1 >= na) {  // the odd frame out
-                const size_t f = F + i0, hf = hidx(p, par, f);
-                if (!p->container) {
-                    emit_vp8(p, p->bitstreams[f], B.pack + B.finfo[2 * i0], hf, na);
-                } else {
-                    thread_local std::vector<uint8_t> vp8;
-                    vp8.clear();
-                    emit_vp8(p, vp8, B.pack + B.finfo[2 * i0], hf, na);
-                    wrap(f, vp8);
-                }
-                return;
-            }
-            const size_t f[2] = {F + i0, F + i1};
-            const size_t hf[2] = {hidx(p, par, f[0]), hidx(p, par, f[1])};
-            const ZwFrameParams* P[2] = {&p->h_params[hf[0]], &p->h_params[hf[1]]};
-            const uint8_t* rec[2] = {B.pack + B.finfo[2 * i0], B.pack + B.finfo[2 * i1]};
-            const bool have[2] = {p->h_have_upd[hf[0]] != 0, p->h_have_upd[hf[1]] != 0};
-            const uint8_t(*upd[2])[8][3][11] = {(const uint8_t(*)[8][3][11])(p->h_upd.data() + hf[0] * 4 * 8 * 3 * 11),
-                                                 (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf[1] * 4 * 8 * 3 * 11)};
-            thread_local zwh::FramePairScratch S;
-            thread_local std::vector<uint8_t> tmp[2];
-            std::vector<uint8_t>* out[2] = {&tmp[0], &tmp[1]};
-            if (!p->container) out[0] = &p->bitstreams[f[0]], out[1] = &p->bitstreams[f[1]];
-            zwh::emit_frame_pair(out, P, rec, p->w, p->h, have, upd, S);
-            if (p->container) {
-                wrap(f[0], tmp[0]);
-                wrap(f[1], tmp[1]);
-            }
-        });
-        return err.load();
-    }
-    parallel_for(na, [&](int i) {
-        const size_t f = F + i, hf = hidx(p, par, f);
-        if (!p->container) {
-            emit_vp8(p, p->bitstreams[f], B.pack + B.finfo[2 * i], hf, na);
-            return;
-        }
-        thread_local std::vector<uint8_t> vp8;
-        vp8.clear();
-        emit_vp8(p, vp8, B.pack + B.finfo[2 * i], hf, na);
-        wrap(f, vp8);
     });
     return err.load();
 }

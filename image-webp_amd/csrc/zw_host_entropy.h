@@ -102,58 +102,6 @@ struct BoolEncoder {
     }
 };
 
-// Token decisions recorded instead of coded: the walk over a frame's packed
-// records (token trees, extra bits, signs) runs first and leaves (probability,
-// bit) pairs here; code_pair then codes two frames' decisions interleaved.
-// Coding is one dependent chain per encoder (range, low, count), ~10 operations
-// per decision; two independent chains in one loop let the core overlap them
-// (measured 1.7x decisions/s on the GPU box's host, tools/ilp-style probe), and
-// the walk's branches no longer stall the chain.
-struct DecisionRecorder {
-    std::vector<uint8_t> p, b;
-    size_t n = 0;
-    void reset(size_t cap)
-    {
-        if (p.size() < cap) {
-            p.resize(cap);
-            b.resize(cap);
-        }
-        n = 0;
-    }
-    void grow()
-    {
-        const size_t c = p.size() * 2 + 4096;
-        p.resize(c);
-        b.resize(c);
-    }
-    inline void put(int bit, int prob)
-    {
-        if (__builtin_expect(n == p.size(), 0)) grow();
-        p[n] = (uint8_t)prob;
-        b[n] = (uint8_t)(bit != 0);
-        n++;
-    }
-    void flag(int f) { put(f, 128); }
-    inline void path(const uint8_t* bits, const uint8_t* pidx, int k, const uint8_t* probs)
-    {
-        for (int i = 0; i < k; i++) put(bits[i], probs[pidx[i]]);
-    }
-};
-
-// Codes two recorded decision streams into their encoders, interleaved
-// (byte-identical to coding each on its own: the encoders share nothing).
-inline void code_pair(BoolEncoder& A, const DecisionRecorder& ra, BoolEncoder& B, const DecisionRecorder& rb)
-{
-    const size_t n = ra.n < rb.n ? ra.n : rb.n;
-    const uint8_t *pa = ra.p.data(), *ba = ra.b.data(), *pb = rb.p.data(), *bb = rb.b.data();
-    for (size_t i = 0; i < n; i++) {
-        A.put(ba[i], pa[i]);
-        B.put(bb[i], pb[i]);
-    }
-    for (size_t i = n; i < ra.n; i++) A.put(ba[i], pa[i]);
-    for (size_t i = n; i < rb.n; i++) B.put(bb[i], pb[i]);
-}
-
 // The reference's bit-at-a-time form, kept for the equivalence test only.
 struct BoolEncoderRef {
     std::vector<uint8_t> buf;
@@ -523,8 +471,7 @@ inline bool updated_probs(const Stats& S, uint8_t out[4][8][3][11])
 
 // encode_coefficients token part (vp8.rs:845-958) for an already-quantized
 // packed block (eob = last nonzero + 1).
-template <class Enc>
-inline int emit_block(Enc& E, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first, int ctx)
+inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first, int ctx)
 {
     const TokenPaths& TP = token_paths();
     int skip_eob = 0;
@@ -638,8 +585,7 @@ inline void emit_mb_header(BoolEncoder& H, const ZwFrameParams& P, const PackedM
 // encode_residual_data (vp8.rs:650-800) of one MB with its left / top
 // complexity (non-zero) contexts.  Without an encoder (E == nullptr) only the
 // contexts advance: a block's context bit is eob > 0, as emit_block returns.
-template <class Enc>
-inline void emit_mb_tokens(Enc* E, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
+inline void emit_mb_tokens(BoolEncoder* E, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
 {
     const bool i4 = m.luma == 4;
     if (m.skip) {
@@ -744,49 +690,6 @@ inline void emit_frame(std::vector<uint8_t>& out, const ZwFrameParams& P, const 
     assemble_frame(out, H.buf, &T, 1, width, height);
 }
 
-// Two frames on one thread (one token partition each): headers coded as they
-// are walked, tokens recorded, then both token partitions coded interleaved by
-// code_pair.  Byte-identical to emit_frame on each.
-struct FramePairScratch {
-    DecisionRecorder r[2];
-};
-inline void emit_frame_pair(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
-                            int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11],
-                            FramePairScratch& S)
-{
-    BoolEncoder H[2], T[2];
-    for (int k = 0; k < 2; k++) {
-        const ZwFrameParams& Pk = *P[k];
-        const int mbw = Pk.mbw, mbh = Pk.mbh;
-        DecisionRecorder& R = S.r[k];
-        R.reset((size_t)mbw * mbh * 64 + 4096);
-        T[k].buf.reserve((size_t)mbw * mbh * 16 + 4096);
-        uint8_t probs[4][8][3][11];
-        emit_frame_header(H[k], Pk, have_updated[k], upd[k], 1, probs);
-        std::vector<Cplx> top(mbw);
-        memset(top.data(), 0, sizeof(Cplx) * mbw);
-        std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
-        const uint8_t* pk = packed[k];
-        PackedMb m;
-        for (int y = 0; y < mbh; y++) {
-            Cplx left;
-            memset(&left, 0, sizeof left);
-            uint8_t left_bp[4] = {0, 0, 0, 0};
-            for (int x = 0; x < mbw; x++) {
-                pk = view_mb(pk, m);
-                emit_mb_header(H[k], Pk, m, top_bp.data(), left_bp, x);
-                emit_mb_tokens(&R, probs, m, left, top[x]);
-            }
-        }
-        H[k].flush();
-    }
-    code_pair(T[0], S.r[0], T[1], S.r[1]);
-    for (int k = 0; k < 2; k++) {
-        T[k].flush();
-        assemble_frame(*out[k], H[k].buf, &T[k], 1, width, height);
-    }
-}
-
 // The same with nparts (2, 4, 8) token partitions: MB row y's tokens go to
 // partition y % nparts (vp8.rs:1419-1421).  A serial walk writes the MB headers
 // and records where each row's records start and the top contexts it begins
@@ -818,7 +721,7 @@ inline void emit_frame_parts(std::vector<uint8_t>& out, const ZwFrameParams& P, 
         for (int x = 0; x < mbw; x++) {
             packed = view_mb(packed, m);
             emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
-            emit_mb_tokens<BoolEncoder>(nullptr, probs, m, left, top[x]);
+            emit_mb_tokens(nullptr, probs, m, left, top[x]);
         }
     }
     H.flush();

@@ -34,29 +34,6 @@ int main(int argc, char** argv)
                    std::chrono::duration<double, std::nano>(t1 - t0).count() / m,
                    std::chrono::duration<double, std::nano>(t2 - t1).count() / m);
     }
-    // code_pair (two recorded streams coded interleaved) == each coded alone
-    for (int trial = 0; trial < 20; trial++) {
-        zwh::DecisionRecorder ra, rb;
-        ra.reset(16);
-        rb.reset(16);
-        const int na = (int)(rng() % 20000), nb = trial == 3 ? 0 : (int)(rng() % 20000);
-        for (int k = 0; k < 2; k++) {
-            zwh::DecisionRecorder& r = k ? rb : ra;
-            for (int i = 0; i < (k ? nb : na); i++) {
-                const int pr = 1 + (int)(rng() % 255);
-                r.put((int)(rng() % 256) >= pr || trial % 4 == 1, pr);
-            }
-        }
-        zwh::BoolEncoder A, B, A1, B1;
-        zwh::code_pair(A, ra, B, rb);
-        for (size_t i = 0; i < ra.n; i++) A1.put(ra.b[i], ra.p[i]);
-        for (size_t i = 0; i < rb.n; i++) B1.put(rb.b[i], rb.p[i]);
-        A.flush(); B.flush(); A1.flush(); B1.flush();
-        if (A.buf != A1.buf || B.buf != B1.buf) {
-            printf("PAIR MISMATCH trial %d\n", trial);
-            return 1;
-        }
-    }
     printf("equivalent\n");
     return 0;
 }
