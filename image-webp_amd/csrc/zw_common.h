@@ -89,6 +89,23 @@ struct ZwMbOut {
 #define ZW_DREC_HDR 80
 #define ZW_DREC_MAX (ZW_DREC_HDR + 25 * 16 * 2)  // 880 B = 55 lines
 
+// Device token parse (k_dec_tokens, zw_dec_tokens.hip).  The host parses the
+// frame header and the first partition's per-MB modes into ZW_TOK_MODE bytes
+// per MB (the record header's bytes 0..15: byte 0 luma mode | chroma mode << 3
+// | skip << 5, byte 1 segment, bytes 8..15 the I4 sub-modes; the rest 0); the
+// device parses the token partition into the records above.  Probabilities per
+// frame (ZW_TOK_PROBS bytes): 8 registers x 64 lanes of dwords, dword (k, l) at
+// byte (64 k + l) * 4; block type t's rows (the 11 node probabilities of (band
+// b, ctx c) in 3 dwords) in register 2t at lanes (3b + c) * 3 .. for b < 7,
+// band 7 in register 2t + 1 at lanes 3c ..
+struct ZwTokFrame {
+    uint64_t off;  // the token partition's byte offset in the uploaded blob
+    uint32_t len;  // its length (the blob holds >= 16 readable bytes past it)
+    uint32_t pad;
+};
+#define ZW_TOK_MODE 16
+#define ZW_TOK_PROBS 2048
+
 // Loop-filter parameters per segment x {i16, i4} (calculate_filter_parameters,
 // decoder/vp8.rs:1470): level, interior limit, hev threshold.
 struct ZwFilterParams {

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "../../include/zwebp.h"
@@ -34,6 +35,9 @@ size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
                           const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw, const uint8_t* tiles);
+hipError_t zwk_dec_tokens(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
+                          const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err, int mbw,
+                          int mbh, int n);
 }
 
 namespace {
@@ -408,6 +412,46 @@ static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
     return ZW_OK;
 }
 
+// The first partition's half of parse_mbs for the device token parse
+// (k_dec_tokens): each MB's modes, segment, skip flag and I4 sub-modes as the
+// first ZW_TOK_MODE bytes of its record header (decoder/vp8.rs:681-734), from
+// the same bool decoder in the same order, so the same streams fail.
+static int parse_modes(DecFrame& F, uint8_t* mrec)
+{
+    const int mbw = F.mbw, mbh = F.mbh;
+    std::vector<uint8_t> top_bp((size_t)mbw * 4, 0);
+    BitReader& b = F.hdr;
+    for (int mby = 0; mby < mbh; mby++) {
+        uint8_t left_bp[4] = {0};
+        for (int mbx = 0; mbx < mbw; mbx++) {
+            uint8_t* rec = mrec + ((size_t)mby * mbw + mbx) * ZW_TOK_MODE;
+            memset(rec, 0, ZW_TOK_MODE);
+            uint8_t* tbp = &top_bp[(size_t)mbx * 4];
+            int seg = 0;
+            if (F.segments_enabled && F.seg_update_map) seg = b.tree(SEGMENT_ID_TREE, F.seg_probs);
+            const int skip = F.skip_prob >= 0 ? b.bit(F.skip_prob) : 0;
+            const int lm = b.tree(YMODE_TREE, KEYFRAME_YMODE_PROBS);
+            if (lm == 4) {
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++) {
+                        const int m = b.tree(BMODE_TREE, KEYFRAME_BPRED_MODE_PROBS[tbp[x]][left_bp[y]]);
+                        rec[8 + ((x + y * 4) >> 1)] |= (uint8_t)(m << (4 * ((x + y * 4) & 1)));
+                        tbp[x] = (uint8_t)m;
+                        left_bp[y] = (uint8_t)m;
+                    }
+            } else {
+                static const uint8_t intra_of[4] = {0, 2, 3, 1};  // DC,V,H,TM -> B_DC,B_VE,B_HE,B_TM
+                for (int i = 0; i < 4; i++) tbp[i] = left_bp[i] = intra_of[lm];
+            }
+            const int cm = b.tree(UVMODE_TREE, KEYFRAME_UV_MODE_PROBS);
+            if (b.eof) return ZW_EBITSTREAM;
+            rec[0] = (uint8_t)(lm | (cm << 3) | (skip << 5));
+            rec[1] = (uint8_t)seg;
+        }
+    }
+    return ZW_OK;
+}
+
 // calculate_filter_parameters decoder/vp8.rs:1470-1523, tabulated per
 // (segment, is_i4).
 static void filter_table(ZwFilterParams& fp, int filter_type, int filter_level, int sharpness, int seg_enabled,
@@ -464,7 +508,14 @@ struct DecBatch {
     size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
     int mbw = 0, mbh = 0;
     const int* d_rs = nullptr;  // row-parallel kernels' per-frame sync words (null: workgroup-per-frame kernels)
+    const int* d_terr = nullptr;  // k_dec_tokens' per-frame error words (null: the host parsed the tokens)
     int n = 0;
+    // a chunk whose tokens the device parsed (DecTok): its records, MB offsets and
+    // frame bases are in device memory already; the kernels wait for x_done
+    const uint8_t* x_recs = nullptr;
+    const uint32_t* x_moff = nullptr;
+    const uint64_t* x_fbase = nullptr;
+    hipEvent_t x_done = nullptr;
     // host parse results waiting for dec_launch
     std::vector<DecQuant> quant;
     std::vector<ZwFilterParams> fps;
@@ -482,6 +533,17 @@ static bool dec_force_error() { return getenv("ZW_DEC_FORCE_ERROR") != nullptr; 
 // hanging the GPU; the planes of such a frame are incomplete.  Read the words
 // after the kernels completed (SDMA: the kernel stream may already run the next
 // chunk) and fail the call with ZW_EDEVICE.
+static int tokens_error(zw_ctx* ctx, const int* d_terr, int n)
+{
+    if (!d_terr) return ZW_OK;
+    int* e = (int*)ctx_pinned(ctx, 3, (size_t)n * sizeof(int));
+    if (!e) return ZW_ENOMEM;
+    if (int r = ctx_d2h(ctx, e, d_terr, (size_t)n * sizeof(int))) return r;
+    for (int f = 0; f < n; f++)
+        if (e[f]) return ZW_EBITSTREAM;  // a token partition ran out (parse_mbs: read_levels_into < 0)
+    return ZW_OK;
+}
+
 static int rows_error(zw_ctx* ctx, const int* d_rs, int n, int mbh)
 {
     if (!d_rs) return ZW_OK;
@@ -525,6 +587,8 @@ static int dec_parse(zw_ctx* ctx, int n, const uint8_t* const* data, const size_
     for (int i = 1; i < n; i++)
         if (F[i].mbw != mbw || F[i].mbh != mbh) return ZW_EINVAL;
     if (mbw == 0 || mbh == 0) return ZW_EINVALID_DIMENSIONS;
+    B.x_recs = nullptr;
+    B.d_terr = nullptr;
     const size_t nmb = (size_t)mbw * mbh;
     const size_t ysz = nmb * 256, csz = nmb * 64;
     // packed MB records (zw_common.h ZW_DREC_*): each frame is parsed into its
@@ -622,16 +686,31 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     hipStream_t s = ctx_stream(ctx);
     hipEvent_t* ev = bi ? ctx->dev_ev1 : ctx->dev_ev;
     B.ev = ev;
-    HIPOK(hipMemcpyAsync(d + o_mbs, stage, up_bytes, hipMemcpyHostToDevice, s));
+    if (up_bytes) HIPOK(hipMemcpyAsync(d + o_mbs, stage, up_bytes, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
     for (int e = 0; e < 4; e++)
         if (!ev[e]) HIPOK(hipEventCreate(&ev[e]));
-    HIPOK(hipEventRecord(ev[0], s));
-    // the kernels read the packed records straight from the upload
+    // the kernels read the packed records straight from the upload, or, for a
+    // chunk whose tokens the device parsed, from k_dec_tokens' output
     const uint8_t* recs = d + o_mbs;
     const uint32_t* moff = (const uint32_t*)(d + o_mbs + o_moff);
     const uint64_t* fbase = (const uint64_t*)(d + o_mbs + o_base);
+    if (B.x_recs) {
+        HIPOK(hipStreamWaitEvent(s, B.x_done, 0));
+        recs = B.x_recs;
+        moff = B.x_moff;
+        fbase = B.x_fbase;
+    } else if (const char* dump = getenv("ZW_DEC_TOKENS_DUMP")) {  // debug: frame 0's host records to <dump>.host
+        const uint32_t* mo = (const uint32_t*)(stage + o_moff);
+        std::string p0 = std::string(dump) + ".host";
+        if (FILE* fo = fopen(p0.c_str(), "wb")) {
+            fwrite(mo, 4, nmb + 1, fo);
+            fwrite(stage, 1, mo[nmb], fo);
+            fclose(fo);
+        }
+    }
+    HIPOK(hipEventRecord(ev[0], s));
     // two wavefront kernels (a fused recon + filter wavefront measured slower: the
     // per-MB latencies add up in one chain, and its registers spilled)
     if (rows) {
@@ -673,6 +752,169 @@ static int dec_chunk_frames()
     return c > 0 ? c : 128;
 }
 
+// ---------------------------------------------------------------------------
+// Device token parse (k_dec_tokens, zw_dec_tokens.hip) for the tail of a batch.
+// A frame's token partition is one serial chain of bool decisions: ≈2.9 ms on a
+// host core for a 1080p Q75 frame, far longer on one GPU wave, but the device
+// runs a wave per frame for hundreds of frames at once.  So a batch splits: the
+// frames [h0, n) are header/mode-parsed on the host up front (the first
+// partition, a short chain) and their tokens go to the device in one launch on
+// its own stream, while the chunk pipeline parses the frames [0, h0) on the
+// host as before; the device chunks' reconstruction waits for that launch.
+// ZW_DEC_TOKENS=host / device / mixed forces either or the split at any batch
+// size (device: every frame); ZW_DEC_TOKENS_HOST = the host's share of a split.
+// ---------------------------------------------------------------------------
+#ifndef ZW_DEC_TOKENS_MIN
+#define ZW_DEC_TOKENS_MIN (1 << 30)  // (auto split off until measured)
+#endif
+struct DecTok {
+    int h0 = 0, nd = 0;  // device frames [h0, h0 + nd)
+    std::vector<DecFrame> F;
+    std::vector<DecQuant> quant;
+    std::vector<ZwFilterParams> fps;
+    const uint8_t* recs = nullptr;
+    const uint32_t* moff = nullptr;
+    const uint64_t* fbase = nullptr;
+    const int* err = nullptr;
+    hipEvent_t done = nullptr;
+    size_t nmb = 0;
+};
+
+static int dec_tok_split(int n, int C)
+{
+    const char* e = getenv("ZW_DEC_TOKENS");
+    const int force = !e ? -1 : (!strcmp(e, "device") ? 1 : (!strcmp(e, "host") ? 0 : (!strcmp(e, "mixed") ? 2 : -1)));
+    if (force == 0 || (force < 0 && n < ZW_DEC_TOKENS_MIN)) return n;
+    if (force == 1) return 0;
+    const char* h = getenv("ZW_DEC_TOKENS_HOST");
+    const double frac = h ? atof(h) : 0.5;
+    int h0 = (int)(n * frac) / C * C;  // whole host chunks
+    return std::max(0, std::min(n, h0));
+}
+
+// Parses the headers and modes of frames [h0, n), stages them and launches
+// k_dec_tokens on the context's token stream.  Returns false (and leaves the
+// frames to the host chunks, which then report any error in frame order) when
+// a frame has several token partitions, another size, or a header / mode error.
+static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int h0, DecTok& T)
+{
+    const int nd = n - h0;
+    if (nd <= 0) return false;
+    T.F.assign(nd, DecFrame());
+    std::vector<DecFrame>& F = T.F;
+    std::vector<int> rc(nd, ZW_OK);
+    parallel_for(nd, [&](int i) { rc[i] = parse_header(F[i], data[h0 + i], lens[h0 + i]); });
+    for (int i = 0; i < nd; i++)
+        if (rc[i] != ZW_OK || F[i].nparts != 1 || F[i].mbw != F[0].mbw || F[i].mbh != F[0].mbh || F[i].mbw == 0 ||
+            F[i].mbh == 0)
+            return false;
+    const int mbw = F[0].mbw, mbh = F[0].mbh;
+    const size_t nmb = (size_t)mbw * mbh, slot = nmb * ZW_DREC_MAX;
+    std::vector<size_t> boff(nd);
+    size_t blob = 0;
+    for (int i = 0; i < nd; i++) {
+        boff[i] = blob;
+        blob += (F[i].part[0].len + 15) & ~(size_t)15;
+    }
+    blob += 16;  // k_dec_tokens reads up to 16 bytes past a partition
+    const size_t o_m = 0, o_p = al256(o_m + (size_t)nd * nmb * ZW_TOK_MODE);
+    const size_t o_tf = al256(o_p + (size_t)nd * ZW_TOK_PROBS), o_fb = al256(o_tf + (size_t)nd * sizeof(ZwTokFrame));
+    const size_t o_b = al256(o_fb + (size_t)nd * 8), up_bytes = al256(o_b + blob);
+    uint8_t* stage = (uint8_t*)ctx_pinned(ctx, 4, up_bytes);
+    if (!stage) return false;
+    T.quant.assign((size_t)nd * 4, DecQuant());
+    T.fps.assign(nd, ZwFilterParams());
+    parallel_for(nd, [&](int i) {
+        rc[i] = parse_modes(F[i], stage + o_m + (size_t)i * nmb * ZW_TOK_MODE);
+        // register layout (ZW_TOK_PROBS): dword (vgpr k, lane l) at (64 k + l) * 4; type t's
+        // rows (band b < 7, ctx c) in vgpr 2t at lanes (3b + c) * 3 + 0..2, band 7 in vgpr 2t + 1
+        uint8_t* pr = stage + o_p + (size_t)i * ZW_TOK_PROBS;
+        memset(pr, 0, ZW_TOK_PROBS);
+        for (int t = 0; t < 4; t++)
+            for (int b = 0; b < 8; b++)
+                for (int c = 0; c < 3; c++)
+                    for (int j = 0; j < 3; j++) {
+                        const int k = 2 * t + (b == 7), l = (b == 7 ? c : 3 * b + c) * 3 + j;
+                        for (int q = 0; q < 4 && 4 * j + q < 11; q++) pr[(64 * k + l) * 4 + q] = F[i].probs[t][b][c][4 * j + q];
+                    }
+        const ZwTokFrame tf = {boff[i], (uint32_t)F[i].part[0].len, 0};
+        memcpy(stage + o_tf + (size_t)i * sizeof(ZwTokFrame), &tf, sizeof tf);
+        ((uint64_t*)(stage + o_fb))[i] = (uint64_t)i * slot;
+        const size_t len = F[i].part[0].len, al = (len + 15) & ~(size_t)15;
+        memcpy(stage + o_b + boff[i], F[i].part[0].d, len);
+        memset(stage + o_b + boff[i] + len, 0, al - len);
+        for (int q = 0; q < 4; q++) T.quant[(size_t)i * 4 + q] = F[i].q[q];
+        filter_table(T.fps[i], F[i].filter_type, F[i].filter_level, F[i].sharpness, F[i].segments_enabled,
+                     F[i].seg_delta_values, F[i].seg_lf, F[i].lf_adj_enabled, F[i].ref_delta0, F[i].mode_delta0, mbw,
+                     mbh);
+    });
+    for (int i = 0; i < nd; i++)
+        if (rc[i] != ZW_OK) return false;
+    memset(stage + o_b + blob - 16, 0, 16);
+    const size_t o_rec = up_bytes, o_mo = al256(o_rec + (size_t)nd * slot);
+    const size_t o_te = al256(o_mo + (size_t)nd * (nmb + 1) * 4), total = al256(o_te + (size_t)nd * 4);
+    uint8_t* d = (uint8_t*)ctx_scratch_tok(ctx, total);
+    if (!d) return false;
+    if (!ctx->tok_ && hipStreamCreateWithFlags(&ctx->tok_, hipStreamNonBlocking) != hipSuccess) return false;
+    for (hipEvent_t& e : ctx->tok_ev)
+        if (!e && hipEventCreate(&e) != hipSuccess) return false;
+    hipStream_t s = ctx->tok_;
+    if (hipMemcpyAsync(d, stage, up_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return false;
+    if (hipEventRecord(ctx->tok_ev[0], s) != hipSuccess) return false;
+    if (zwk_dec_tokens(s, d + o_b, (const ZwTokFrame*)(d + o_tf), d + o_p, d + o_m, d + o_rec, slot,
+                       (uint32_t*)(d + o_mo), (int*)(d + o_te), mbw, mbh, nd) != hipSuccess)
+        return false;
+    if (hipEventRecord(ctx->tok_ev[1], s) != hipSuccess) {
+        (void)hipStreamSynchronize(s);  // (the launch is in flight: let it finish before the host takes over)
+        return false;
+    }
+    T.h0 = h0;
+    T.nd = nd;
+    T.nmb = nmb;
+    T.recs = d + o_rec;
+    T.moff = (const uint32_t*)(d + o_mo);
+    T.fbase = (const uint64_t*)(d + o_fb);
+    T.err = (const int*)(d + o_te);
+    T.done = ctx->tok_ev[1];
+    if (const char* dump = getenv("ZW_DEC_TOKENS_DUMP")) {  // debug: device frame 0's records to <dump>.dev
+        if (hipStreamSynchronize(s) == hipSuccess) {
+            std::vector<uint32_t> mo(nmb + 1);
+            (void)hipMemcpy(mo.data(), d + o_mo, (nmb + 1) * 4, hipMemcpyDeviceToHost);
+            std::vector<uint8_t> dev(mo[nmb]);
+            (void)hipMemcpy(dev.data(), d + o_rec, mo[nmb], hipMemcpyDeviceToHost);
+            std::string p0 = std::string(dump) + ".dev";
+            if (FILE* fo = fopen(p0.c_str(), "wb")) {
+                fwrite(mo.data(), 4, nmb + 1, fo);
+                fwrite(dev.data(), 1, dev.size(), fo);
+                fclose(fo);
+            }
+        }
+    }
+    return true;
+}
+
+// A chunk of device frames [first, first + cnt): no host parse; its records are k_dec_tokens'.
+static void dec_parse_dev(const DecTok& T, int first, int cnt, DecBatch& B)
+{
+    const int j0 = first - T.h0;
+    B.F.assign(T.F.begin() + j0, T.F.begin() + j0 + cnt);
+    B.quant.assign(T.quant.begin() + (size_t)j0 * 4, T.quant.begin() + (size_t)(j0 + cnt) * 4);
+    B.fps.assign(T.fps.begin() + j0, T.fps.begin() + j0 + cnt);
+    B.mbw = T.F[0].mbw;
+    B.mbh = T.F[0].mbh;
+    B.ysz = T.nmb * 256;
+    B.csz = T.nmb * 64;
+    B.n = cnt;
+    B.stage = nullptr;
+    B.up_bytes = B.o_moff = B.o_base = B.rec_bytes = 0;
+    B.x_recs = T.recs;
+    B.x_moff = T.moff + (size_t)j0 * (T.nmb + 1);
+    B.x_fbase = T.fbase + j0;
+    B.x_done = T.done;
+    B.d_terr = T.err + j0;
+    B.parse_ms = 0;
+}
+
 // Runs the batch in chunks, alternating the two buffer sets.  Per step c the
 // host parses chunk c while a second thread finishes chunk c-1 (waits for its
 // kernels, downloads and fans out -- mostly a DMA wait), then chunk c is
@@ -687,7 +929,16 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     const int C = dec_chunk_frames(), nch = (n + C - 1) / C;
     DecBatch B[2];
     ctx->dec_ms[0] = ctx->dec_ms[1] = ctx->dec_ms[2] = 0.f;
+    ctx->dec_tok_ms = 0.f;
     ctx->dec_host_ms[0] = ctx->dec_host_ms[1] = ctx->dec_host_ms[2] = 0;
+    // the device's share of the tokens first (its launch runs beside the host chunks)
+    DecTok T;
+    {
+        const double t0 = dec_now_ms();
+        const int h0 = dec_tok_split(n, C);
+        if (h0 >= n || !dec_tok_prepare(ctx, n, data, lens, h0, T)) T.h0 = n;
+        ctx->dec_host_ms[0] += dec_now_ms() - t0;
+    }
     auto first = [&](int c) { return c * C; };
     auto count = [&](int c) { return std::min(C, n - c * C); };
     int err = ZW_OK;
@@ -705,7 +956,8 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             });
         }
         if (c < nch) {
-            err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+            if (first(c) >= T.h0) dec_parse_dev(T, first(c), count(c), B[c & 1]);
+            else err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
             ctx->dec_host_ms[0] += B[c & 1].parse_ms;
         }
         if (fin.joinable()) fin.join();
@@ -715,6 +967,12 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             err = dec_launch(ctx, extra_per_frame * count(c), b, c & 1);
             if (!err) err = enqueue(b, first(c), count(c));
         }
+    }
+    if (T.nd > 0) {
+        float ms = 0.f;
+        if (hipEventSynchronize(T.done) == hipSuccess &&
+            hipEventElapsedTime(&ms, ctx->tok_ev[0], ctx->tok_ev[1]) == hipSuccess)
+            ctx->dec_tok_ms = ms;
     }
     if (err) (void)hipStreamSynchronize(ctx_stream(ctx));  // nothing queued may outlive the call
     return err;
@@ -738,6 +996,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fsz);
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[2]));
+        if (int r = tokens_error(ctx, B.d_terr, B.n)) return r;
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         const double td = dec_now_ms();
         {
@@ -834,6 +1093,7 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
         uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fbytes);
         if (!hout) return ZW_ENOMEM;
         HIPOK(hipEventSynchronize(B.ev[3]));
+        if (int r = tokens_error(ctx, B.d_terr, B.n)) return r;
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         const double td = dec_now_ms();
         if (int r = ctx_d2h_stream(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
@@ -938,6 +1198,13 @@ extern "C" int zw_decode_kernel_times(zw_ctx* ctx, float* ms)
     if (!ctx || !ms) return ZW_EINVAL;
     ms[0] = ctx->dec_ms[0];
     ms[1] = ctx->dec_ms[1];
+    return ZW_OK;
+}
+
+extern "C" int zw_decode_token_ms(zw_ctx* ctx, float* ms)
+{
+    if (!ctx || !ms) return ZW_EINVAL;
+    *ms = ctx->dec_tok_ms;
     return ZW_OK;
 }
 

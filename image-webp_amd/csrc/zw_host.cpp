@@ -260,13 +260,16 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     for (auto& v : c->dec_recs) std::vector<zw_ctx::RecBuf>().swap(v);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
-    c->dscratch = c->dscratch1 = nullptr;
+    if (c->tok_) (void)hipStreamSynchronize(c->tok_);
+    if (c->dscratch2) (void)hipFree(c->dscratch2);
+    c->dscratch = c->dscratch1 = c->dscratch2 = nullptr;
+    c->dscratch2_cap = 0;
     (void)hipDeviceSynchronize();  // queues may serve streams other than the context's
     for (auto& q : c->xmb_q)
         if (q.buf) (void)hipFree(q.buf);
     c->xmb_q.clear();
     c->dscratch_cap = c->dscratch1_cap = 0;
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < 5; i++) {
         pinned_free(c->hpin[i]);
         c->hpin[i] = nullptr;
         c->hpin_cap[i] = 0;
@@ -280,8 +283,12 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     zw_pipe_destroy(c->pipe1);
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
+    if (c->tok_) (void)hipStreamSynchronize(c->tok_);
+    if (c->dscratch2) (void)hipFree(c->dscratch2);
     for (auto& q : c->xmb_q)
         if (q.buf) (void)hipFree(q.buf);
+    for (hipEvent_t e : c->tok_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->dev_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->dev_ev1)
@@ -289,6 +296,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     for (void* h : c->hpin) pinned_free(h);
     if (c->stream_) (void)hipStreamDestroy(c->stream_);
     if (c->copy_) (void)hipStreamDestroy(c->copy_);
+    if (c->tok_) (void)hipStreamDestroy(c->tok_);
     delete c;
 }
 

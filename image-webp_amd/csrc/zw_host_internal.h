@@ -22,6 +22,10 @@ struct zw_ctx {
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
     void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
+    void* dscratch2 = nullptr;  // decode batches: the device token parse's upload and records
+    size_t dscratch2_cap = 0;
+    hipStream_t tok_ = nullptr;  // k_dec_tokens (runs beside the chunks' kernels), created on first use
+    hipEvent_t tok_ev[2] = {nullptr, nullptr};
     // zw_transform_quant_mbs*_device: the I4 queue of k_xform_mb / k_xform_mb_i4,
     // one per launch stream (launches on different streams may overlap; launches
     // on one stream are ordered), its counters reset on that stream per launch
@@ -46,14 +50,17 @@ struct zw_ctx {
     hsa_agent_t gpu_agent{}, cpu_agent{};
     // grow-only pinned host staging (decode batch: MB records up, planes down)
     // [0] / [2]: the two upload buffers of the pipelined decode, [1] downloads,
-    // [3] the row-parallel kernels' sync / error words
-    void* hpin[4] = {nullptr, nullptr, nullptr, nullptr};
-    size_t hpin_cap[4] = {0, 0, 0, 0};
+    // [3] the row-parallel kernels' sync / error words, [4] the device token
+    // parse's upload (modes, probabilities, token partitions)
+    void* hpin[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t hpin_cap[5] = {0, 0, 0, 0, 0};
     // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter,
     // [2] k_yuv2rgb (0 when the batch returned planes) (ms)
-    hipEvent_t dev_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t dev_ev1[4] = {nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
+    // ([4], [5]: around k_dec_tokens when the device parses the tokens)
+    hipEvent_t dev_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t dev_ev1[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
+    float dec_tok_ms = 0.f;  // k_dec_tokens, summed over the batch's chunks
     // host stages of the last decode batch, wall ms summed over its chunks:
     // [0] parse (bool decoder + records), [1] download, [2] fan-out / copy-out
     double dec_host_ms[3] = {0, 0, 0};
@@ -148,6 +155,18 @@ static inline void* ctx_scratch(zw_ctx* c, size_t bytes, int which = 0)
         cap = bytes;
     }
     return p;
+}
+
+static inline void* ctx_scratch_tok(zw_ctx* c, size_t bytes)
+{
+    if (c->dscratch2_cap < bytes) {
+        if (c->dscratch2) (void)hipFree(c->dscratch2);
+        c->dscratch2 = nullptr;
+        c->dscratch2_cap = 0;
+        if (hipMalloc(&c->dscratch2, bytes) != hipSuccess) return nullptr;
+        c->dscratch2_cap = bytes;
+    }
+    return c->dscratch2;
 }
 
 // The context's own stream (single-call entry points); created lazily so a

@@ -165,6 +165,7 @@ SIGNATURES = [
     ("zw_pipe_set_token_partitions", _I, [_VP, _I]),
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_decode_stage_times", _I, [_VP, _VP]),
+    ("zw_decode_token_ms", _I, [_VP, _VP]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_encode_host", _I, [_VP, _I, _VP]),
@@ -461,6 +462,15 @@ def decode_kernel_times(ctx=None):
     ms = (ctypes.c_float * 2)()
     _check(c._lib.zw_decode_kernel_times(c.handle, ms), "decode_kernel_times")
     return float(ms[0]), float(ms[1])
+
+
+def decode_token_ms(ctx=None):
+    """Device ms of the last decode batch's token parse (k_dec_tokens; 0 when
+    the host parsed the tokens)."""
+    c = _ctx(ctx)
+    ms = ctypes.c_float()
+    _check(c._lib.zw_decode_token_ms(c.handle, ctypes.byref(ms)), "decode_token_ms")
+    return float(ms.value)
 
 
 def decode_stage_times(ctx=None):

@@ -214,6 +214,12 @@ int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
  * ms[0] header/mode/token parse (bool decoder, all host threads), ms[1] planes
  * or images device->host, ms[2] fan-out into the output buffers. */
 int zw_decode_stage_times(zw_ctx *ctx, float *ms);
+/* Device time of the last decode batch's token parse (k_dec_tokens, summed over
+ * chunks; 0 when the host parsed the tokens).  Batches of >= 64 frames with one
+ * token partition each parse their tokens on the device (read_coefficients,
+ * decoder/vp8.rs:872-1058), the modes and headers on the host; ZW_DEC_TOKENS=
+ * host / device forces either. */
+int zw_decode_token_ms(zw_ctx *ctx, float *ms);
 /* ... and of its k_yuv2rgb launch (0 when the batch returned planes). */
 int zw_decode_rgb_kernel_ms(zw_ctx *ctx, float *ms);
 

@@ -320,16 +320,20 @@ def _manifest():
         return json.load(f)["streams"]
 
 
+@pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("rows", ["default", "0"])
 @pytest.mark.parametrize("entry", _manifest(), ids=lambda e: e["name"])
-def test_decode_goldens(ctx, monkeypatch, entry, rows):
+def test_decode_goldens(ctx, monkeypatch, entry, rows, tokens):
     """The committed streams' planes (SHA-256 from the reference's own decode
     fixtures / libwebp).  rows=0 forces the batch kernels (one workgroup per
     frame, reconstruction -> MB tiles -> loop filter), which otherwise only run
     for batches of 128+ frames: odd sizes and the gallery1 simple-filter
-    streams (chroma moved through the tiles unfiltered) go through them too."""
+    streams (chroma moved through the tiles unfiltered) go through them too.
+    tokens=device: the token partition parsed by k_dec_tokens (batches of 64+
+    frames otherwise), the modes on the host."""
     if rows != "default":
         monkeypatch.setenv("ZW_DEC_ROWS", rows)
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     vp8 = open(os.path.join(GOLD, entry["name"] + ".vp8"), "rb").read()
     fr = zwebp.vp8_decode_frame(vp8, ctx=ctx)
     w, h = entry["width"], entry["height"]
@@ -341,9 +345,12 @@ def test_decode_goldens(ctx, monkeypatch, entry, rows):
     assert got == entry["yuv_sha256"]
 
 
+@pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("w,h,kind,q,m", [(333, 211, "natural", 75, 4), (256, 256, "noise", 40, 6),
-                                          (96, 64, "flat", 75, 4), (512, 384, "natural", 90, 2)])
-def test_decode_oracle_streams(ctx, w, h, kind, q, m):
+                                          (96, 64, "flat", 75, 4), (512, 384, "natural", 90, 2),
+                                          (64, 48, "noise", 1, 4), (48, 32, "noise", 100, 6)])
+def test_decode_oracle_streams(ctx, monkeypatch, w, h, kind, q, m, tokens):
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     img = synth_rgba(w, h, 0x5EED0000 + h, kind)
     rc, vp8, _ = O.encode(img, w, h, 3, q, m)
     rc, r = O.decode(vp8)
@@ -362,12 +369,48 @@ def test_decode_batch(ctx):
         assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"])
 
 
+def test_decode_batch_device_tokens(ctx, monkeypatch):
+    """A batch of 80 frames of mixed content and quality, split as large batches
+    are (the first chunks parsed on the host, the rest's token partitions by
+    k_dec_tokens, one wave per frame, beside them) equals the oracle frame by
+    frame; with one frame's token partition cut short the batch fails with the
+    oracle's DecodingError variant for that frame, whichever side parses it."""
+    monkeypatch.setenv("ZW_DEC_TOKENS", "mixed")  # host chunks of 16 frames beside the device's 48 (+ 16)
+    monkeypatch.setenv("ZW_DEC_TOKENS_HOST", "0.4")
+    monkeypatch.setenv("ZW_DEC_CHUNK", "16")
+    w, h = 96, 64
+    kinds = ("natural", "noise", "flat")
+    streams = [O.encode(synth_rgba(w, h, 0x5EED6000 + i, kinds[i % 3]), w, h, 3, 5 + (i * 7) % 95, i % 7)[1]
+               for i in range(80)]
+    frames = zwebp.decode_batch(streams, ctx=ctx)
+    assert zwebp.decode_token_ms(ctx=ctx) > 0.0
+    for s, fr in zip(streams, frames):
+        rc, r = O.decode(s)
+        assert rc == 0
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+    bad = list(streams)
+    bad[17] = streams[17][: len(streams[17]) - max(8, len(streams[17]) // 3)]
+    rc, _ = O.decode(bad[17])
+    assert rc != 0
+    for tokens in ("host", "device", "mixed"):
+        monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
+        with pytest.raises(zwebp.DecodingError) as e:
+            zwebp.decode_batch(bad, ctx=ctx)
+        assert e.value.code == rc, (tokens, e.value.code, rc)
+    monkeypatch.setenv("ZW_DEC_TOKENS", "mixed")
+    frames = zwebp.decode_batch(streams, ctx=ctx)  # the context stays usable
+    rc, r = O.decode(streams[5])
+    assert np.array_equal(frames[5].ybuf, r["y"])
+
+
+@pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("chunk", ["1", "2", "4"])
-def test_decode_batch_chunked(ctx, monkeypatch, chunk):
+def test_decode_batch_chunked(ctx, monkeypatch, chunk, tokens):
     """The double-buffered chunk pipeline (ZW_DEC_CHUNK frames per chunk; the
     host parses chunk c+1 while chunk c runs): several chunks, a ragged last
     chunk, both buffer sets reused, every frame equal to the oracle."""
     monkeypatch.setenv("ZW_DEC_CHUNK", chunk)
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     w, h = 160, 112
     streams = [O.encode(synth_rgba(w, h, 0x5EED4000 + i, ("natural", "noise", "flat")[i % 3]), w, h, 3,
                         20 + 15 * i, 4)[1] for i in range(5)]
@@ -392,12 +435,15 @@ def test_decode_batch_chunked_size_mismatch(ctx, monkeypatch):
     assert all(np.array_equal(f.ybuf, r["y"]) for f in fr)
 
 
+@pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("rows", ["1", "0"])
-def test_decode_rows_and_frame_kernels(ctx, monkeypatch, rows):
+def test_decode_rows_and_frame_kernels(ctx, monkeypatch, rows, tokens):
     """Both reconstruction / loop-filter kernel families on the same 1080p streams
     (ZW_DEC_ROWS=1: one wave per MB row spread over the CUs, rows handed over
-    through global memory; 0: one workgroup per frame) equal the oracle."""
+    through global memory; 0: one workgroup per frame) equal the oracle, with
+    the tokens parsed on the host or by k_dec_tokens."""
     monkeypatch.setenv("ZW_DEC_ROWS", rows)
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     w, h = 1920, 1080
     streams = [O.encode(synth_rgba(w, h, 0x5EED3000 + i, "natural" if i else "noise"), w, h, 3, q, 4)[1]
                for i, q in enumerate((20, 75, 95))]
@@ -420,9 +466,11 @@ def _header_damage_cases(vp8):
     return out
 
 
-def test_decode_errors(ctx):
+@pytest.mark.parametrize("tokens", ["host", "device"])
+def test_decode_errors(ctx, monkeypatch, tokens):
     """Each failing header gives the oracle's DecodingError variant (codes 10-17 =
     decoder/api.rs:79-110 in declaration order)."""
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     vp8 = open(os.path.join(GOLD, "libwebp_natural_64x48_q75.vp8"), "rb").read()
     seen = set()
     for s in _header_damage_cases(vp8):
@@ -451,13 +499,15 @@ def test_encode_quality_method_sweep(ctx, m):
             assert bytes(got) == bytes(ref), f"q={q} m={m} color={color}"
 
 
+@pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("name", ["libwebp_natural_64x48_q75.vp8", "gallery1_1.vp8"])
-def test_decode_damaged_streams(ctx, name):
+def test_decode_damaged_streams(ctx, monkeypatch, name, tokens):
     """Truncated and byte-flipped streams (the header's 10 bytes kept, so the
     dimensions stay sane): wherever the oracle decodes (decode_frame,
     decoder/vp8.rs:1526, reading zeros past the end as bit_reader.rs does), the
     device path gives the same planes; wherever it fails, the product raises
     DecodingError.  Never a crash or a silent difference."""
+    monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     path = os.path.join(GOLD, name)
     if not os.path.exists(path):
         pytest.skip(f"{name} not in tests/golden")
