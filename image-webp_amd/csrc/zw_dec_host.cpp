@@ -744,6 +744,47 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     return ZW_OK;
 }
 
+// Parts a chunk's plane download is split into, each fanned out while the next
+// lands (ZW_DEC_DL_PARTS).
+static int dec_dl_parts()
+{
+    const char* e = getenv("ZW_DEC_DL_PARTS");
+    const int p = e ? atoi(e) : 1;  // (1 until measured on the box)
+    return p > 0 ? p : 1;
+}
+
+// A chunk's download in parts on a second thread, each part (frames [a, b))
+// handed to fan(a, b) as soon as copy(a, b) has landed it, so the fan-out into
+// the callers' buffers overlaps the rest of the download.  Returns the first
+// copy error; *dl_ms = the download's wall time.
+template <class CP, class FAN>
+static int dec_download_fan(zw_ctx* ctx, int cn, CP&& copy, FAN&& fan, double* dl_ms)
+{
+    const int parts = std::max(1, std::min(cn, dec_dl_parts()));
+    std::atomic<int> landed(0), err(ZW_OK);
+    const double t0 = dec_now_ms();
+    std::thread dl([&]() {
+        (void)hipSetDevice(ctx->device);
+        for (int p = 0; p < parts; p++) {
+            const int r = copy(cn * p / parts, cn * (p + 1) / parts);
+            if (r) {
+                err = r;
+                break;
+            }
+            landed.store(p + 1, std::memory_order_release);
+        }
+        *dl_ms = dec_now_ms() - t0;
+        landed.store(parts + 1, std::memory_order_release);  // (done, or stopped on an error)
+    });
+    for (int p = 0; p < parts; p++) {
+        while (landed.load(std::memory_order_acquire) <= p) std::this_thread::yield();
+        if (err.load() != ZW_OK) break;
+        fan(cn * p / parts, cn * (p + 1) / parts);
+    }
+    dl.join();
+    return err.load();
+}
+
 // Frames per pipelined chunk.  ZW_DEC_CHUNK overrides.
 static int dec_chunk_frames()
 {
@@ -991,7 +1032,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         const std::vector<DecFrame>& F = B.F;
         const size_t ysz = B.ysz, csz = B.csz;
         uint8_t* d = B.d;
-        // planes down through pinned staging (one DMA per plane set), then fanned out
+        // planes down through pinned staging, then fanned out into one buffer per frame
         const size_t fsz = ysz + 2 * csz;
         uint8_t* hout = (uint8_t*)ctx_pinned(ctx, 1, (size_t)cn * fsz);
         if (!hout) return ZW_ENOMEM;
@@ -999,26 +1040,37 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
         if (int r = tokens_error(ctx, B.d_terr, B.n)) return r;
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
         const double td = dec_now_ms();
-        {
-            int r = ctx_d2h_stream(ctx, hout, d + B.o_y, (size_t)cn * ysz);
-            if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * ysz, d + B.o_u, (size_t)cn * csz);
-            if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * (ysz + csz), d + B.o_v, (size_t)cn * csz);
-            if (r) return r;
-        }
+        // planes down in parts (three plane copies per frame range), each part
+        // fanned out into the frames' buffers while the next lands
         const double tf = dec_now_ms();
-        ctx->dec_host_ms[1] += tf - td;
         std::vector<int> oom(cn, 0);
-        parallel_for(cn, [&](int i) {
-            uint8_t* buf = (uint8_t*)malloc(fsz);
-            if (!buf) {
-                oom[i] = 1;
-                return;
-            }
-            memcpy(buf, hout + (size_t)i * ysz, ysz);
-            memcpy(buf + ysz, hout + (size_t)cn * ysz + (size_t)i * csz, csz);
-            memcpy(buf + ysz + csz, hout + (size_t)cn * (ysz + csz) + (size_t)i * csz, csz);
-            outs[f0 + i].y = buf;
-        });
+        double dl_ms = 0;
+        const int dr = dec_download_fan(
+            ctx, cn,
+            [&](int a, int b) {
+                const size_t A = (size_t)a, N = (size_t)(b - a);
+                int r = ctx_d2h_stream(ctx, hout + A * ysz, d + B.o_y + A * ysz, N * ysz);
+                if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * ysz + A * csz, d + B.o_u + A * csz, N * csz);
+                if (!r) r = ctx_d2h_stream(ctx, hout + (size_t)cn * (ysz + csz) + A * csz, d + B.o_v + A * csz, N * csz);
+                return r;
+            },
+            [&](int a, int b) {
+                parallel_for(b - a, [&](int k) {
+                    const int i = a + k;
+                    uint8_t* buf = (uint8_t*)malloc(fsz);
+                    if (!buf) {
+                        oom[i] = 1;
+                        return;
+                    }
+                    memcpy(buf, hout + (size_t)i * ysz, ysz);
+                    memcpy(buf + ysz, hout + (size_t)cn * ysz + (size_t)i * csz, csz);
+                    memcpy(buf + ysz + csz, hout + (size_t)cn * (ysz + csz) + (size_t)i * csz, csz);
+                    outs[f0 + i].y = buf;
+                });
+            },
+            &dl_ms);
+        ctx->dec_host_ms[1] += dl_ms;
+        if (dr) return dr;
         ctx->dec_host_ms[2] += dec_now_ms() - tf;
         if (dec_timing()) fprintf(stderr, "[dec] download+fanout %.2f ms\n", dec_now_ms() - td);
         int r = ZW_OK;
@@ -1095,32 +1147,42 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
         HIPOK(hipEventSynchronize(B.ev[3]));
         if (int r = tokens_error(ctx, B.d_terr, B.n)) return r;
         if (int r = rows_error(ctx, B.d_rs, B.n, B.mbh)) return r;
-        const double td = dec_now_ms();
-        if (int r = ctx_d2h_stream(ctx, hout, B.d + B.o_extra, (size_t)cn * fbytes)) return r;
         const double tf = dec_now_ms();
-        ctx->dec_host_ms[1] += tf - td;
         std::vector<int> oom(cn, 0);
-        parallel_for(cn, [&](int i) {
-            const uint8_t* src = hout + (size_t)i * fbytes;
-            if (dst) {
-                uint8_t* o = dst[f0 + i];
-                if (stride == row) {
-                    memcpy(o, src, fbytes);
-                } else {
-                    for (size_t y = 0; y < h; y++) memcpy(o + y * stride, src + y * row, row);
-                }
-                return;
-            }
-            uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
-            if (!buf) {
-                oom[i] = 1;
-                return;
-            }
-            memcpy(buf, src, fbytes);
-            outs[f0 + i].data = buf;
-            outs[f0 + i].len = fbytes;
-        });
+        double dl_ms = 0;
+        const int dr = dec_download_fan(
+            ctx, cn,
+            [&](int a, int b) {
+                return ctx_d2h_stream(ctx, hout + (size_t)a * fbytes, B.d + B.o_extra + (size_t)a * fbytes,
+                                      (size_t)(b - a) * fbytes);
+            },
+            [&](int a, int b) {
+                parallel_for(b - a, [&](int k) {
+                    const int i = a + k;
+                    const uint8_t* src = hout + (size_t)i * fbytes;
+                    if (dst) {
+                        uint8_t* o = dst[f0 + i];
+                        if (stride == row) {
+                            memcpy(o, src, fbytes);
+                        } else {
+                            for (size_t y = 0; y < h; y++) memcpy(o + y * stride, src + y * row, row);
+                        }
+                        return;
+                    }
+                    uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
+                    if (!buf) {
+                        oom[i] = 1;
+                        return;
+                    }
+                    memcpy(buf, src, fbytes);
+                    outs[f0 + i].data = buf;
+                    outs[f0 + i].len = fbytes;
+                });
+            },
+            &dl_ms);
+        ctx->dec_host_ms[1] += dl_ms;
         ctx->dec_host_ms[2] += dec_now_ms() - tf;
+        if (dr) return dr;
         for (int i = 0; i < cn; i++)
             if (oom[i]) return ZW_ENOMEM;
         float ms = 0.f;

@@ -212,7 +212,8 @@ int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
 /* Host stages of the last decode batch on ctx, wall ms summed over its chunks
  * (chunks overlap: parse of chunk c runs beside the download of chunk c-1):
  * ms[0] header/mode/token parse (bool decoder, all host threads), ms[1] planes
- * or images device->host, ms[2] fan-out into the output buffers. */
+ * or images device->host, ms[2] download + fan-out into the output buffers
+ * (a chunk's download runs in parts, each fanned out while the next lands). */
 int zw_decode_stage_times(zw_ctx *ctx, float *ms);
 /* Device time of the last decode batch's token parse (k_dec_tokens, summed over
  * chunks; 0 when the host parsed the tokens).  Batches of >= 64 frames with one
