@@ -416,6 +416,7 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     decb = zwebp.decode_batch(pbatch, ctx=ctx)  # pipelined chunks (parse / device / download overlap)
     el = time.perf_counter() - t0
     st = zwebp.decode_stage_times(ctx=ctx)
+    tok_ms = zwebp.decode_token_ms(ctx=ctx)
     thr = zwebp.host_threads()
     fbytes = len(decb[0].ybuf) + len(decb[0].ubuf) + len(decb[0].vbuf)
     stages = {"host_parse_ms": st[0], "download_ms": st[1], "fanout_ms": st[2], "host_threads": thr,
@@ -423,8 +424,10 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
               "parse_bound_decodes_per_s": pipe_frames / (st[0] * 1e-3) if st[0] > 0 else None,
               "download_gbs": pipe_frames * fbytes / (st[1] * 1e-3) / 1e9 if st[1] > 0 else None,
               "download_bound_decodes_per_s": pipe_frames / (st[1] * 1e-3) if st[1] > 0 else None,
+              "device_token_ms": tok_ms, "token_split": os.environ.get("ZW_DEC_TOKENS", "auto"),
               "note": "wall ms summed over chunks; the parse (the host bool decoder's serial chain, every "
-                      "host thread) of chunk c overlaps the download + fan-out of chunk c-1"}
+                      "host thread) of chunk c overlaps the download + fan-out of chunk c-1; device_token_ms: "
+                      "k_dec_tokens' launch for the frames whose tokens the device parsed (0: none)"}
     batch = pbatch[:frames]
     vy = [0, 0, 0]  # matched, mismatched, no digest
 

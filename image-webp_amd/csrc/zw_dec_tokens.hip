@@ -252,47 +252,34 @@ extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __r
                 used += ZW_DREC_HDR;
             } else {
                 uint32_t nzm = 0;
-                int nlv = 0, stv = 0, y2v = 0, y2eob = 0, first = 0, lvv, eob;
-                if (lm != 4) {
-                    const int nz = tok_block(b, sbuf, P[2], P[3], 0, (int)(T & 1u) + (int)(L & 1u), y2v, y2eob);
-                    T = (T & ~1u) | (uint32_t)nz;
-                    L = (L & ~1u) | (uint32_t)nz;
-                    first = 1;
-                    bad = bad || b.eof;
-                }
+                int nlv = 0, stv = 0, y2v = 0, y2eob = 0, lvv, eob;
                 const uint32_t YA = lm != 4 ? P[0] : P[6], YB = lm != 4 ? P[1] : P[7];  // type 0 (after Y2) or 3 (I4)
                 auto put = [&](int blk) {  // the block's levels after the previous blocks'
-                    bad = bad || b.eof;
                     stv = lane == blk ? nlv : stv;
                     if (lane < eob) lv[nlv + lane] = (int16_t)lvv;
                     nlv += eob;
                 };
+                // the MB's blocks in the reference's order, through one call site (one copy
+                // of the token walk in the code): k = 0 Y2 (I16 MBs only), 1..16 Y, 17..20 U,
+                // 21..24 V; tb / lb = the block's bit in the top / left context words
 #pragma unroll 1
-                for (int y = 0; y < 4; y++) {
-#pragma unroll 1
-                    for (int x = 0; x < 4; x++) {
-                        const int ctx = (int)((T >> (x + 1)) & 1u) + (int)((L >> (y + 1)) & 1u);
-                        const int nz = tok_block(b, sbuf, YA, YB, first, ctx, lvv, eob);
-                        put(x + 4 * y);
-                        nzm |= (uint32_t)nz << (x + 4 * y);
-                        T = (T & ~(2u << x)) | ((uint32_t)nz << (x + 1));
-                        L = (L & ~(2u << y)) | ((uint32_t)nz << (y + 1));
-                    }
-                }
-#pragma unroll 1
-                for (int j = 5; j <= 7; j += 2) {
-#pragma unroll 1
-                    for (int y = 0; y < 2; y++) {
-#pragma unroll 1
-                        for (int x = 0; x < 2; x++) {
-                            const int blk = x + 2 * y + (j == 5 ? 16 : 20);
-                            const int ctx = (int)((T >> (x + j)) & 1u) + (int)((L >> (y + j)) & 1u);
-                            const int nz = tok_block(b, sbuf, P[4], P[5], 0, ctx, lvv, eob);
-                            put(blk);
-                            nzm |= (uint32_t)nz << blk;
-                            T = (T & ~(1u << (x + j))) | ((uint32_t)nz << (x + j));
-                            L = (L & ~(1u << (y + j))) | ((uint32_t)nz << (y + j));
-                        }
+                for (int k = lm != 4 ? 0 : 1; k < 25; k++) {
+                    const int q = k - 17, pl = q >> 2;
+                    const int tb = k == 0 ? 0 : (k <= 16 ? ((k - 1) & 3) + 1 : (q & 1) + 5 + 2 * pl);
+                    const int lb = k == 0 ? 0 : (k <= 16 ? ((k - 1) >> 2) + 1 : ((q >> 1) & 1) + 5 + 2 * pl);
+                    const uint32_t A = k == 0 ? P[2] : (k <= 16 ? YA : P[4]), B = k == 0 ? P[3] : (k <= 16 ? YB : P[5]);
+                    const int first = k >= 1 && k <= 16 && lm != 4 ? 1 : 0;
+                    const int ctx = (int)((T >> tb) & 1u) + (int)((L >> lb) & 1u);
+                    const int nz = tok_block(b, sbuf, A, B, first, ctx, lvv, eob);
+                    T = (T & ~(1u << tb)) | ((uint32_t)nz << tb);
+                    L = (L & ~(1u << lb)) | ((uint32_t)nz << lb);
+                    bad = bad || b.eof;
+                    if (k == 0) {
+                        y2v = lvv;
+                        y2eob = eob;
+                    } else {
+                        put(k - 1);
+                        nzm |= (uint32_t)nz << (k - 1);
                     }
                 }
                 lvv = y2v;  // Y2 (parsed first) goes last
