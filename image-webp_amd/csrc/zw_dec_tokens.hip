@@ -230,6 +230,7 @@ extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __r
     // read_levels_into fails a frame when a block read ends with eof set (an
     // empty partition is fine while every MB is skipped)
     bool bad = false;
+    uint32_t mdone = 0;  // MBs whose offset is written
     wsync();
     for (int mby = 0; mby < mbh && !bad; mby++) {
         uint32_t L = 0;  // left contexts, the same 9 bits
@@ -239,6 +240,7 @@ extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __r
             const int lm = (int)(mr.x & 7u), skip = (int)((mr.x >> 5) & 1u);
             uint32_t T = rfl(tcx[mbx]);
             bst32(used, rm, lane == 0 ? (uint32_t)i * 4u : ZW_OOB);
+            mdone = (uint32_t)i + 1u;
             if (skip) {
                 // header only: the modes, no levels (every start 0)
                 if (lm != 4) {
@@ -302,7 +304,11 @@ extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __r
             if (lane == 0) tcx[mbx] = (uint16_t)T;
         }
     }
-    bst32(used, rm, lane == 0 ? (uint32_t)nmb * 4u : ZW_OOB);
+    // a frame that failed stopped early: its remaining MBs get empty records at
+    // the end (offsets = the bytes used), so the reconstruction that still runs
+    // before the host sees the error reads inside the frame's records
+    const uint32_t from = bad ? (uint32_t)rfl(mdone) : (uint32_t)nmb;
+    for (uint32_t j = from + (uint32_t)lane; j <= (uint32_t)nmb; j += 64) bst32(used, rm, j * 4u);
     if (lane == 0) err[f] = bad ? 1 : 0;
 #ifdef ZW_TOK_PROF
     if (lane == 0 && (f == 0 || f == (int)gridDim.x - 1))
