@@ -36,7 +36,7 @@ struct TokBD {
 
 DI void tok_fetch(TokBD& b, uint8_t* sbuf)
 {
-    if (threadIdx.x == 0)
+    if ((threadIdx.x & 63) == 0)
         __builtin_amdgcn_global_load_lds((const void*)(b.p + (b.pos & ~3u)), (void*)(sbuf + 16 * b.slot), 16, 0, 0);
 }
 
@@ -117,6 +117,21 @@ struct TokRow {
     uint32_t r0, r1, r2;
 };
 DI uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+#ifdef ZW_TOK_SMEM
+// (experiment: the rows as scalar loads from the frame's table in memory, A = the type's first register index)
+DI TokRow prow_m(const uint8_t* __restrict__ Pf, uint32_t A, int n, int ctx)
+{
+    const uint32_t k = A + (n == 15 ? 1u : 0u);
+    const int l = n < 15 ? (band_of(n) * 3 + ctx) * 3 : ctx * 3;
+    const uint4 w = *(const uint4*)(Pf + (64 * k + l) * 4);
+    TokRow r;
+    r.r0 = w.x;
+    r.r1 = w.y;
+    r.r2 = w.z;
+    return r;
+}
+#define prow(A, B, n, ctx) prow_m(Pf, A, n, ctx)
+#else
 DI TokRow prow(uint32_t A, uint32_t B, int n, int ctx)
 {
     TokRow r;
@@ -133,6 +148,7 @@ DI TokRow prow(uint32_t A, uint32_t B, int n, int ctx)
     }
     return r;
 }
+#endif
 // Byte k of a probability row (k constant at every call site).
 DI uint32_t pb(const TokRow& r, int k)
 {
@@ -145,7 +161,11 @@ DI uint32_t pb(const TokRow& r, int k)
 // (positions < first and the zeros stay 0); eob = last nonzero position + 1.
 // Returns the block's non-zero flag (n > first at the end of block; a zero run
 // to position 16 counts as non-zero, as in the reference).
-DI int tok_block(TokBD& b, uint8_t* sbuf, uint32_t A, uint32_t B, int first, int ctx, int& lvv, int& eob)
+DI int tok_block(TokBD& b, uint8_t* sbuf, uint32_t A, uint32_t B, int first, int ctx, int& lvv, int& eob
+#ifdef ZW_TOK_SMEM
+                 , const uint8_t* __restrict__ Pf
+#endif
+)
 {
     int n = first;
     eob = 0;
@@ -186,7 +206,7 @@ DI int tok_block(TokBD& b, uint8_t* sbuf, uint32_t A, uint32_t B, int first, int
             v = 3 + (8 << cat) + extra;
         }
         const int s = tok_bit(b, 128, sbuf);
-        lvv = (int)threadIdx.x == n ? (s ? -v : v) : lvv;
+        lvv = (int)(threadIdx.x & 63) == n ? (s ? -v : v) : lvv;
         eob = ++n;
         if (n == 16) break;
         row = prow(A, B, n, nctx);
@@ -201,16 +221,24 @@ DI int tok_block(TokBD& b, uint8_t* sbuf, uint32_t A, uint32_t B, int first, int
 // Out: frame f's records at recs + f * slot, their offsets at moff + f * (nmb
 // + 1) (moff[nmb] = the used bytes), err[f] = 1 when the partition ran out
 // (the host then fails the call with ZW_EBITSTREAM, as parse_mbs does).
-extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __restrict__ blob,
+#ifndef ZW_TOK_WAVES
+#define ZW_TOK_WAVES 1  // frames (waves) per workgroup: more confine the launch to fewer CUs
+#endif
+extern "C" __global__ __launch_bounds__(64 * ZW_TOK_WAVES) void k_dec_tokens(const uint8_t* __restrict__ blob,
                                                               const ZwTokFrame* __restrict__ tf,
                                                               const uint8_t* __restrict__ probs,
                                                               const uint8_t* __restrict__ modes, uint8_t* recs,
-                                                              uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh)
+                                                              uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh,
+                                                              int nframes)
 {
-    __shared__ uint16_t tcx[(ZW_MAX_W + 15) / 16];  // 9-bit top contexts per MB column (Y2, Y 1-4, U 5-6, V 7-8)
-    __shared__ __attribute__((aligned(16))) uint8_t rec[ZW_DREC_MAX + 16];
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[32];  // the stream's two 16-byte fetch slots
-    const int f = blockIdx.x, lane = threadIdx.x;
+    __shared__ uint16_t tcx_all[ZW_TOK_WAVES][(ZW_MAX_W + 15) / 16];  // 9-bit top contexts per MB column (Y2, Y 1-4, U 5-6, V 7-8)
+    __shared__ __attribute__((aligned(16))) uint8_t rec_all[ZW_TOK_WAVES][ZW_DREC_MAX + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf_all[ZW_TOK_WAVES][32];  // the stream's two 16-byte fetch slots
+    const int wv = (int)(threadIdx.x >> 6), f = blockIdx.x * ZW_TOK_WAVES + wv, lane = (int)(threadIdx.x & 63);
+    if (f >= nframes) return;  // (no workgroup barrier below: every wave runs alone)
+    uint16_t* tcx = tcx_all[wv];
+    uint8_t* rec = rec_all[wv];
+    uint8_t* sbuf = sbuf_all[wv];
     const size_t nmb = (size_t)mbw * mbh;
     for (int i = lane; i < mbw; i += 64) tcx[i] = 0;
     // the frame's probabilities: 8 VGPRs (type t: A = P[2 t], B = P[2 t + 1]; ZW_TOK_PROBS layout)
@@ -269,10 +297,18 @@ extern "C" __global__ __launch_bounds__(64) void k_dec_tokens(const uint8_t* __r
                     const int q = k - 17, pl = q >> 2;
                     const int tb = k == 0 ? 0 : (k <= 16 ? ((k - 1) & 3) + 1 : (q & 1) + 5 + 2 * pl);
                     const int lb = k == 0 ? 0 : (k <= 16 ? ((k - 1) >> 2) + 1 : ((q >> 1) & 1) + 5 + 2 * pl);
+#ifdef ZW_TOK_SMEM
+                    const uint32_t A = k == 0 ? 2u : (k <= 16 ? (lm != 4 ? 0u : 6u) : 4u), B = 0;
+#else
                     const uint32_t A = k == 0 ? P[2] : (k <= 16 ? YA : P[4]), B = k == 0 ? P[3] : (k <= 16 ? YB : P[5]);
+#endif
                     const int first = k >= 1 && k <= 16 && lm != 4 ? 1 : 0;
                     const int ctx = (int)((T >> tb) & 1u) + (int)((L >> lb) & 1u);
-                    const int nz = tok_block(b, sbuf, A, B, first, ctx, lvv, eob);
+                    const int nz = tok_block(b, sbuf, A, B, first, ctx, lvv, eob
+#ifdef ZW_TOK_SMEM
+                                             , probs + (size_t)f * ZW_TOK_PROBS
+#endif
+                    );
                     T = (T & ~(1u << tb)) | ((uint32_t)nz << tb);
                     L = (L & ~(1u << lb)) | ((uint32_t)nz << lb);
                     bad = bad || b.eof;
@@ -323,6 +359,7 @@ extern "C" hipError_t zwk_dec_tokens(hipStream_t s, const uint8_t* blob, const Z
                                      const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err,
                                      int mbw, int mbh, int n)
 {
-    hipLaunchKernelGGL(k_dec_tokens, dim3(n), dim3(64), 0, s, blob, tf, probs, modes, recs, slot, moff, err, mbw, mbh);
+    hipLaunchKernelGGL(k_dec_tokens, dim3((n + ZW_TOK_WAVES - 1) / ZW_TOK_WAVES), dim3(64 * ZW_TOK_WAVES), 0, s, blob, tf,
+                       probs, modes, recs, slot, moff, err, mbw, mbh, n);
     return hipGetLastError();
 }
