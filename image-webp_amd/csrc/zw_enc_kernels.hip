@@ -2847,10 +2847,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_P1_SLOWSKIP 1
 #endif
 #ifndef ZW_P1_SLOW_NUM
-#define ZW_P1_SLOW_NUM 3
-#endif
+#define ZW_P1_SLOW_NUM 1  // re-tuned in round 4 (1080p, 256 frames, one lane): 1/1 28.2-28.3 ms, 3/2 28.8-29.0,
+#endif                    // 2/3 29.0-29.1, 1/2 29.2, 4/3 29.8, 0/1 29.9, 2/1 31.7
 #ifndef ZW_P1_SLOW_DEN
-#define ZW_P1_SLOW_DEN 2
+#define ZW_P1_SLOW_DEN 1
 #endif
     constexpr bool skip_mode = ZW_P1_SLOWSKIP && PASS == 1 && !ROWS && NCH == 1 && NW > 4;
     constexpr int nslow = (NW - 1) / 4 > 0 ? (NW - 1) / 4 : 1;  // luma waves on SIMD 0: 4, 8, ..

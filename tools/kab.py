@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One-lane encode kernel times of the library ZWEBP_LIB names (for A/B runs):
 256 1080p frames, one launch per pass, best of R runs (ms per launch).
-usage: ZWEBP_LIB=... python tools/kab.py [R]"""
+usage: ZWEBP_LIB=... python tools/kab.py [R] [W H]"""
 import json
 import os
 import sys
@@ -13,7 +13,7 @@ import zwebp  # noqa: E402
 from zwebp.synth import synth_rgba  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-w, h, n = 1920, 1080, 256
+w, h, n = (int(sys.argv[2]), int(sys.argv[3]), 256) if len(sys.argv) > 3 else (1920, 1080, 256)
 ctx = zwebp.Context(0)
 imgs = [synth_rgba(w, h, 0x5EED0000 + i) for i in range(4)]
 p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
@@ -28,5 +28,5 @@ for _ in range(R):
 p.encode()
 import hashlib  # noqa: E402
 dig = hashlib.sha256(b"".join(p.output(i) for i in range(4))).hexdigest()[:16]
-print(json.dumps({"lib": os.path.basename(os.environ.get("ZWEBP_LIB", "libzwebp.so")), "rgb2yuv": best[0],
+print(json.dumps({"lib": os.path.basename(os.environ.get("ZWEBP_LIB", "libzwebp.so")), "size": f"{w}x{h}", "rgb2yuv": best[0],
                   "analysis": best[1], "pass1": best[2], "pass2": best[3], "digest4": dig}), flush=True)
