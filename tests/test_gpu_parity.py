@@ -403,6 +403,28 @@ def test_decode_batch_device_tokens(ctx, monkeypatch):
     assert np.array_equal(frames[5].ybuf, r["y"])
 
 
+def test_decode_device_tokens_edge_streams(ctx, monkeypatch):
+    """Device-token batches with the streams the kernel must not mishandle: frames
+    with 2 / 4 / 8 token partitions (the whole batch then stays on the host
+    parse), a flat frame whose MBs are all skipped (a near-empty token
+    partition), and the lowest and highest quality settings; every frame equals
+    the oracle's decode."""
+    monkeypatch.setenv("ZW_DEC_TOKENS", "device")
+    w, h = 80, 48
+    flat = np.full((h, w, 3), 128, np.uint8)
+    img = np.ascontiguousarray(synth_rgba(w, h, 0x5EED7000, "noise")[..., :3])
+    cases = [[O.encode(img, w, h, 2, 75, 4, nparts=k)[1] for k in (2, 4, 8)],
+             [O.encode(img, w, h, 2, 75, 4, nparts=k)[1] for k in (1, 4, 1)],
+             [O.encode(flat, w, h, 2, q, 4)[1] for q in (0, 75, 100)],
+             [O.encode(img, w, h, 2, q, m)[1] for q, m in ((0, 0), (100, 6), (1, 2), (99, 5))]]
+    for streams in cases:
+        frames = zwebp.decode_batch(streams, ctx=ctx)
+        for s, fr in zip(streams, frames):
+            rc, r = O.decode(s)
+            assert rc == 0
+            assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+
+
 @pytest.mark.parametrize("tokens", ["host", "device"])
 @pytest.mark.parametrize("chunk", ["1", "2", "4"])
 def test_decode_batch_chunked(ctx, monkeypatch, chunk, tokens):
