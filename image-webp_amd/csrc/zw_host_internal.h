@@ -189,6 +189,10 @@ static inline hipStream_t ctx_stream(zw_ctx* c)
 // (hipHostMalloc): the DMA engine cannot reach pageable memory.
 int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
 
+// Decoded-frame buffer pool (zw_dec_host.cpp): takes back a buffer it handed
+// out (returns false for any other pointer, which the caller frees).
+bool zw_dec_pool_put(void* p);
+
 // Set (process-wide) once an SDMA copy timed out with the engine possibly
 // still writing its destination: from then on pinned host buffers, which are
 // the destinations of those copies, are leaked instead of freed, so a late

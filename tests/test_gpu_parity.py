@@ -369,6 +369,41 @@ def test_decode_batch(ctx):
         assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"])
 
 
+def test_decode_batch_recycled_buffers(ctx):
+    """Decoded frame buffers go back to the library's pool when freed
+    (zw_frame_free) and the next batch of that size fills them: a batch decoded
+    into recycled buffers equals the oracle, and frames still held are never
+    handed out again (a later batch leaves them unchanged)."""
+    import gc
+    w, h = 112, 80
+    kinds = ("natural", "noise", "flat")
+    sets = [[O.encode(synth_rgba(w, h, 0x5EED7000 + 16 * k + i, kinds[(i + k) % 3]), w, h, 3, 20 + 25 * i, 4)[1]
+             for i in range(3)] for k in range(3)]
+    first = zwebp.decode_batch(sets[0], ctx=ctx)
+    del first
+    gc.collect()
+    held = zwebp.decode_batch(sets[1], ctx=ctx)
+    copies = [(bytes(f.ybuf), bytes(f.ubuf), bytes(f.vbuf)) for f in held]
+    later = zwebp.decode_batch(sets[2], ctx=ctx)
+    for streams, frames in ((sets[1], held), (sets[2], later)):
+        for s, fr in zip(streams, frames):
+            rc, r = O.decode(s)
+            assert rc == 0
+            assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+    assert [(bytes(f.ybuf), bytes(f.ubuf), bytes(f.vbuf)) for f in held] == copies
+    # RGBA buffers (zw_bytes) through the same pool, beside the encoder's
+    # outputs (plain malloc) freed by the same zw_bytes_free
+    rgb0 = zwebp.decode_rgb_batch(sets[0], 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    del rgb0
+    gc.collect()
+    enc = zwebp.encode_batch([synth_rgba(w, h, 0x5EED7100)], w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    rgb1 = zwebp.decode_rgb_batch(sets[1], 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    for s, b in zip(sets[1], rgb1):
+        rc, r = O.decode(s)
+        assert np.array_equal(b.reshape(-1), O.yuv_to_rgb_fancy(r["y"], r["u"], r["v"], w, h, 4))
+    del enc
+
+
 def test_decode_batch_device_tokens(ctx, monkeypatch):
     """A batch of 80 frames of mixed content and quality, split as large batches
     are (the first chunks parsed on the host, the rest's token partitions by
