@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -838,28 +839,51 @@ template <class CP, class FAN>
 static int dec_download_fan(zw_ctx* ctx, int cn, CP&& copy, FAN&& fan, double* dl_ms)
 {
     const int parts = std::max(1, std::min(cn, dec_dl_parts()));
-    std::atomic<int> landed(0), err(ZW_OK);
+    std::mutex mu;
+    std::condition_variable cv;
+    int landed = 0, err = ZW_OK;
     const double t0 = dec_now_ms();
     std::thread dl([&]() {
         (void)hipSetDevice(ctx->device);
         for (int p = 0; p < parts; p++) {
             const int r = copy(cn * p / parts, cn * (p + 1) / parts);
+            std::lock_guard<std::mutex> g(mu);
             if (r) {
                 err = r;
                 break;
             }
-            landed.store(p + 1, std::memory_order_release);
+            landed = p + 1;
+            cv.notify_one();
         }
         *dl_ms = dec_now_ms() - t0;
-        landed.store(parts + 1, std::memory_order_release);  // (done, or stopped on an error)
+        std::lock_guard<std::mutex> g(mu);
+        landed = parts + 1;  // (done, or stopped on an error)
+        cv.notify_one();
     });
+    // the waiting thread sleeps (a spinning one took a CPU from the parse threads)
     for (int p = 0; p < parts; p++) {
-        while (landed.load(std::memory_order_acquire) <= p) std::this_thread::yield();
-        if (err.load() != ZW_OK) break;
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return landed > p || err != ZW_OK; });
+            if (err != ZW_OK) break;
+        }
         fan(cn * p / parts, cn * (p + 1) / parts);
     }
     dl.join();
-    return err.load();
+    return err;
+}
+
+// Threads of a fan-out part (ZW_DEC_FAN_THREADS; 0 = every host thread).  The
+// copies into recycled buffers run beside the next chunk's parse; capping them
+// did not help it (1 024 1080p frames: all 16 threads 5 061-5 120 decodes/s,
+// 8: 5 018-5 107, 4: 4 753-4 873; profiles/r04_dec_fan_ab.txt).
+static int dec_fan_threads()
+{
+    static const int t = [] {
+        const char* e = getenv("ZW_DEC_FAN_THREADS");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    return t;
 }
 
 // Frames per pipelined chunk.  ZW_DEC_CHUNK overrides.
@@ -1143,7 +1167,7 @@ extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* dat
                     memcpy(buf + ysz, hout + (size_t)cn * ysz + (size_t)i * csz, csz);
                     memcpy(buf + ysz + csz, hout + (size_t)cn * (ysz + csz) + (size_t)i * csz, csz);
                     outs[f0 + i].y = buf;
-                });
+                }, dec_fan_threads());
             },
             &dl_ms);
         ctx->dec_host_ms[1] += dl_ms;
@@ -1254,7 +1278,7 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
                     memcpy(buf, src, fbytes);
                     outs[f0 + i].data = buf;
                     outs[f0 + i].len = fbytes;
-                });
+                }, dec_fan_threads());
             },
             &dl_ms);
         ctx->dec_host_ms[1] += dl_ms;

@@ -121,9 +121,9 @@ static inline int host_threads()
 }
 
 template <class F>
-static inline void parallel_for(int n, F fn)
+static inline void parallel_for(int n, F fn, int max_threads = 0)
 {
-    int nt = std::min(host_threads(), n);
+    int nt = std::min(max_threads > 0 ? std::min(max_threads, host_threads()) : host_threads(), n);
     if (nt <= 1) {
         for (int i = 0; i < n; i++) fn(i);
         return;
