@@ -767,8 +767,8 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     if (up_bytes) HIPOK(hipMemcpyAsync(d + o_mbs, stage, up_bytes, hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_q, quant.data(), quant.size() * sizeof(DecQuant), hipMemcpyHostToDevice, s));
     HIPOK(hipMemcpyAsync(d + o_fp, fps.data(), fps.size() * sizeof(ZwFilterParams), hipMemcpyHostToDevice, s));
-    for (int e = 0; e < 4; e++)
-        if (!ev[e]) HIPOK(hipEventCreate(&ev[e]));
+    for (int e = 0; e < 4; e++)  // blocking sync: finish() sleeps on them (ctx_d2h_stream)
+        if (!ev[e]) HIPOK(hipEventCreateWithFlags(&ev[e], hipEventBlockingSync));
     // the kernels read the packed records straight from the upload, or, for a
     // chunk whose tokens the device parsed, from k_dec_tokens' output
     const uint8_t* recs = d + o_mbs;

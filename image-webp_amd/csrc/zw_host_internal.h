@@ -18,6 +18,7 @@ struct zw_ctx {
     int device;
     hipStream_t stream_ = nullptr;  // created on first use (hardware queues are scarce)
     hipStream_t copy_ = nullptr;    // decode downloads (ctx_d2h_stream), created on first use
+    hipEvent_t copy_ev = nullptr;   // its completion, waited on without spinning
     // grow-only device scratch for the single-call decode / filter entry points
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
