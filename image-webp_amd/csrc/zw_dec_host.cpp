@@ -529,6 +529,19 @@ struct FramePool {
         live[p] = n;
         return p;
     }
+    // frees every buffer the pool holds (those handed out stay tracked)
+    void trim()
+    {
+        std::vector<uint8_t*> drop;
+        {
+            std::lock_guard<std::mutex> g(m);
+            for (auto& kv : free_)
+                for (uint8_t* b : kv.second) drop.push_back(b);
+            free_.clear();
+            bytes = 0;
+        }
+        for (uint8_t* b : drop) free(b);
+    }
     // false: p did not come from the pool.  Over the cap, buffers of other
     // sizes are dropped first (the latest frame size is the one reused).
     bool put(void* q)
@@ -569,6 +582,7 @@ static FramePool& frame_pool()
 }  // namespace
 
 bool zw_dec_pool_put(void* p) { return frame_pool().put(p); }
+void zw_dec_pool_trim() { frame_pool().trim(); }
 
 extern "C" void zw_frame_free(zw_frame* f)
 {

@@ -263,6 +263,7 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
         c->pipe1 = nullptr;
     }
     for (auto& v : c->dec_recs) std::vector<zw_ctx::RecBuf>().swap(v);
+    zw_dec_pool_trim();  // the decoded-frame buffers callers have already freed
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     if (c->tok_) (void)hipStreamSynchronize(c->tok_);

@@ -193,6 +193,8 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
 // Decoded-frame buffer pool (zw_dec_host.cpp): takes back a buffer it handed
 // out (returns false for any other pointer, which the caller frees).
 bool zw_dec_pool_put(void* p);
+// Frees the buffers the pool holds (zw_ctx_release_buffers).
+void zw_dec_pool_trim();
 
 // Set (process-wide) once an SDMA copy timed out with the engine possibly
 // still writing its destination: from then on pinned host buffers, which are

@@ -402,6 +402,15 @@ def test_decode_batch_recycled_buffers(ctx):
         rc, r = O.decode(s)
         assert np.array_equal(b.reshape(-1), O.yuv_to_rgb_fancy(r["y"], r["u"], r["v"], w, h, 4))
     del enc
+    # release_buffers empties the pool; frames still held stay valid, later batches decode as before
+    del later, rgb1
+    gc.collect()
+    ctx.release_buffers()
+    again = zwebp.decode_batch(sets[2], ctx=ctx)
+    for s, fr in zip(sets[2], again):
+        rc, r = O.decode(s)
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.vbuf, r["v"])
+    assert [(bytes(f.ybuf), bytes(f.ubuf), bytes(f.vbuf)) for f in held] == copies
 
 
 def test_decode_batch_device_tokens(ctx, monkeypatch):
