@@ -72,3 +72,27 @@ def test_product_does_not_link_oracle():
     assert " or_" not in out
     deps = subprocess.run(["ldd", LIB], capture_output=True, text=True).stdout
     assert "oracle" not in deps
+
+
+def test_free_functions_take_plain_malloc_buffers(lib):
+    """zw_bytes_free / zw_frame_free keep the C contract for buffers that did
+    not come from the decoded-frame pool (the encoder's outputs, a binding's
+    own malloc): they are free()d and the fields cleared; a null frame is a
+    no-op.  No device is touched."""
+    import zwebp
+    L = zwebp.load_library()
+    libc = ctypes.CDLL(None)
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    for _ in range(4):
+        b = zwebp._Bytes()
+        b.data = libc.malloc(1 << 20)
+        b.len = 1 << 20
+        L.zw_bytes_free(ctypes.byref(b))
+        assert not b.data and b.len == 0
+        f = zwebp._Frame()
+        f.y = libc.malloc(3 << 20)
+        L.zw_frame_free(ctypes.byref(f))
+        assert not f.y and not f.u and not f.v
+    L.zw_frame_free(ctypes.byref(zwebp._Frame()))
+    L.zw_bytes_free(ctypes.byref(zwebp._Bytes()))
