@@ -76,10 +76,12 @@ struct ZwMbOut {
 // Packed decode record (what crosses PCIe): 16-byte aligned, per MB
 //   [0] luma_mode | chroma_mode << 3 | skip << 5   [1] segment   [2..3] pad
 //   [4..7] nz_mask   [8..15] bpred, 4 bits each
-//   [16..67] start[26] (u16): block b's levels are entries start[b] ..
-//            start[b+1]-1 of the level array (its zigzag prefix up to the last
-//            nonzero); blocks 0..23, then 24 = Y2   [68..79] pad
-//   [80..] int16 levels, zigzag order; pad to 16.
+//   [16..65] start[25] (u16): block b's levels (b = Y 0..15, U 0..3, V 0..3)
+//            are entries start[b] .. start[b+1]-1 of the level array (its
+//            zigzag prefix up to the last nonzero); start[24] = the total.
+//            Y2's levels (I16 MBs) come first, entries 0 .. start[0]-1, in the
+//            order the token partition holds them   [66..79] pad (0)
+//   [80..] int16 levels, zigzag order; pad to 16 (0).
 // k_dec_recon / k_dec_recon_rows read it straight from the upload (one MB
 // ahead, staged in LDS); a level is start[b] + zigzag position < start[b+1].
 // k_pack_scan's per-chunk counter words: [0] running offset, [1] frames done,
@@ -89,22 +91,18 @@ struct ZwMbOut {
 #define ZW_DREC_HDR 80
 #define ZW_DREC_MAX (ZW_DREC_HDR + 25 * 16 * 2)  // 880 B = 55 lines
 
-// Device token parse (k_dec_tokens, zw_dec_tokens.hip).  The host parses the
+// Device token parse (k_dec_tokl, zw_dec_tokens.hip).  The host parses the
 // frame header and the first partition's per-MB modes into ZW_TOK_MODE bytes
 // per MB (the record header's bytes 0..15: byte 0 luma mode | chroma mode << 3
 // | skip << 5, byte 1 segment, bytes 8..15 the I4 sub-modes; the rest 0); the
-// device parses the token partition into the records above.  Probabilities per
-// frame (ZW_TOK_PROBS bytes): 8 registers x 64 lanes of dwords, dword (k, l) at
-// byte (64 k + l) * 4; block type t's rows (the 11 node probabilities of (band
-// b, ctx c) in 3 dwords) in register 2t at lanes (3b + c) * 3 .. for b < 7,
-// band 7 in register 2t + 1 at lanes 3c ..
+// device parses the token partition into the records above.  Probabilities
+// per frame: tokl::PROBS (1056) bytes, [type][band][ctx][node] as parsed.
 struct ZwTokFrame {
-    uint64_t off;  // the token partition's byte offset in the uploaded blob
-    uint32_t len;  // its length (the blob holds >= 16 readable bytes past it)
+    uint64_t off;  // the token partition's byte offset in the uploaded blob (16-aligned)
+    uint32_t len;  // its length (the blob holds it zero-padded to 16, plus 16 zero bytes at the end)
     uint32_t pad;
 };
 #define ZW_TOK_MODE 16
-#define ZW_TOK_PROBS 2048
 
 // Loop-filter parameters per segment x {i16, i4} (calculate_filter_parameters,
 // decoder/vp8.rs:1470): level, interior limit, hev threshold.

@@ -38,10 +38,12 @@ size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
                           const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw, const uint8_t* tiles);
-hipError_t zwk_dec_tokens(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
-                          const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err, int mbw,
-                          int mbh, int n);
+hipError_t zwk_dec_tokl(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
+                        const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh,
+                        int n);
+size_t zw_tokl_lds_bytes(int mbw);
 }
+#include "zw_tokl.h"
 
 namespace {
 
@@ -319,7 +321,6 @@ static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
     const int mbw = F.mbw, mbh = F.mbh;
     std::vector<uint8_t> top_cx((size_t)mbw * 9, 0), top_bp((size_t)mbw * 4, 0);
     BitReader& b = F.hdr;
-    int16_t y2[16];
     for (int mby = 0; mby < mbh; mby++) {
         BitReader& pr = F.part[mby % F.nparts];
         uint8_t left_cx[9] = {0}, left_bp[4] = {0};
@@ -360,9 +361,8 @@ static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
             }
             uint32_t nzm = 0;
             int first = 0, eob, nlv = 0;
-            int y2eob = 0;
-            if (lm != 4) {
-                const int nz = read_levels_into(pr, F.probs[1], y2, 0, tcx[0] + left_cx[0], &y2eob);
+            if (lm != 4) {  // Y2 (parsed first) goes first
+                const int nz = read_levels_into(pr, F.probs[1], lv, 0, tcx[0] + left_cx[0], &nlv);
                 if (nz < 0) return ZW_EBITSTREAM;
                 left_cx[0] = tcx[0] = (uint8_t)nz;
                 first = 1;
@@ -401,10 +401,7 @@ static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
                     left_cx[y + j] = (uint8_t)left;
                 }
             }
-            start[24] = (uint16_t)nlv;  // Y2 (parsed first) goes last
-            memcpy(lv + nlv, y2, (size_t)y2eob * 2);
-            nlv += y2eob;
-            start[25] = (uint16_t)nlv;
+            start[24] = (uint16_t)nlv;  // the end of block 23
             memcpy(rec + 4, &nzm, 4);
             const size_t bytes = ZW_DREC_HDR + (size_t)nlv * 2, padded = (bytes + 15) & ~(size_t)15;
             memset(rec + bytes, 0, padded - bytes);
@@ -416,7 +413,7 @@ static int parse_mbs(DecFrame& F, uint8_t* recs, uint32_t* moff)
 }
 
 // The first partition's half of parse_mbs for the device token parse
-// (k_dec_tokens): each MB's modes, segment, skip flag and I4 sub-modes as the
+// (k_dec_tokl): each MB's modes, segment, skip flag and I4 sub-modes as the
 // first ZW_TOK_MODE bytes of its record header (decoder/vp8.rs:681-734), from
 // the same bool decoder in the same order, so the same streams fail.
 static int parse_modes(DecFrame& F, uint8_t* mrec)
@@ -600,7 +597,7 @@ struct DecBatch {
     size_t o_y = 0, o_u = 0, o_v = 0, o_extra = 0, ysz = 0, csz = 0;
     int mbw = 0, mbh = 0;
     const int* d_rs = nullptr;  // row-parallel kernels' per-frame sync words (null: workgroup-per-frame kernels)
-    const int* d_terr = nullptr;  // k_dec_tokens' per-frame error words (null: the host parsed the tokens)
+    const int* d_terr = nullptr;  // k_dec_tokl's per-frame error words (null: the host parsed the tokens)
     int n = 0;
     // a chunk whose tokens the device parsed (DecTok): its records, MB offsets and
     // frame bases are in device memory already; the kernels wait for x_done
@@ -631,8 +628,13 @@ static int tokens_error(zw_ctx* ctx, const int* d_terr, int n)
     int* e = (int*)ctx_pinned(ctx, 3, (size_t)n * sizeof(int));
     if (!e) return ZW_ENOMEM;
     if (int r = ctx_d2h(ctx, e, d_terr, (size_t)n * sizeof(int))) return r;
-    for (int f = 0; f < n; f++)
-        if (e[f]) return ZW_EBITSTREAM;  // a token partition ran out (parse_mbs: read_levels_into < 0)
+    for (int f = 0; f < n; f++) {
+        if (e[f] == 1) return ZW_EBITSTREAM;  // a token partition ran out (parse_mbs: read_levels_into < 0)
+        if (e[f]) {
+            fprintf(stderr, "zwebp: device token parse gave up waiting on frame %d of %d\n", f, n);
+            return ZW_EDEVICE;
+        }
+    }
     return ZW_OK;
 }
 
@@ -784,7 +786,7 @@ static int dec_launch(zw_ctx* ctx, size_t extra_bytes, DecBatch& B, int bi)
     for (int e = 0; e < 4; e++)  // blocking sync: finish() sleeps on them (ctx_d2h_stream)
         if (!ev[e]) HIPOK(hipEventCreateWithFlags(&ev[e], hipEventBlockingSync));
     // the kernels read the packed records straight from the upload, or, for a
-    // chunk whose tokens the device parsed, from k_dec_tokens' output
+    // chunk whose tokens the device parsed, from k_dec_tokl's output
     const uint8_t* recs = d + o_mbs;
     const uint32_t* moff = (const uint32_t*)(d + o_mbs + o_moff);
     const uint64_t* fbase = (const uint64_t*)(d + o_mbs + o_base);
@@ -909,20 +911,20 @@ static int dec_chunk_frames()
 }
 
 // ---------------------------------------------------------------------------
-// Device token parse (k_dec_tokens, zw_dec_tokens.hip) for the tail of a batch.
+// Device token parse (k_dec_tokl, zw_dec_tokens.hip) for the tail of a batch.
 // A frame's token partition is one serial chain of bool decisions: ≈2.9 ms on a
-// host core for a 1080p Q75 frame, far longer on one GPU wave, but the device
-// runs a wave per frame for hundreds of frames at once.  So a batch splits: the
-// frames [h0, n) are header/mode-parsed on the host up front (the first
-// partition, a short chain) and their tokens go to the device in one launch on
-// its own stream, while the chunk pipeline parses the frames [0, h0) on the
-// host as before; the device chunks' reconstruction waits for that launch.
-// ZW_DEC_TOKENS=host / device / mixed forces either or the split at any batch
-// size (device: every frame); ZW_DEC_TOKENS_HOST = the host's share of a split.
+// host core for a 1080p Q75 frame, ≈250 ms on one GPU lane, but one launch runs
+// 64 frames per wave side by side, so its time hardly depends on how many
+// frames it holds.  So a batch splits: the frames [h0, n) are header/mode-parsed
+// on the host up front (the first partition, a short chain) and their tokens go
+// to the device in one launch on its own stream, while the chunk pipeline
+// parses the frames [0, h0) on the host as before; the device chunks'
+// reconstruction waits for that launch.  By default (auto) the host keeps as
+// many whole chunks as it parses in the launch's time, from the rates the last
+// batches measured, and the device takes the rest (none when the host alone
+// would finish first).  ZW_DEC_TOKENS=host / device / mixed forces the host,
+// the device or a split at ZW_DEC_TOKENS_HOST (the host's share, 0.5).
 // ---------------------------------------------------------------------------
-#ifndef ZW_DEC_TOKENS_MIN
-#define ZW_DEC_TOKENS_MIN (1 << 30)  // off: measured slower than the host parse for 1 024-frame batches
-#endif
 struct DecTok {
     int h0 = 0, nd = 0;  // device frames [h0, h0 + nd)
     std::vector<DecFrame> F;
@@ -936,15 +938,27 @@ struct DecTok {
     size_t nmb = 0;
 };
 
-static int dec_tok_split(int n, int C)
+// The host's frames [0, h0) of a batch of n frames of nmb MBs (C frames per chunk).
+static int dec_tok_split(zw_ctx* ctx, int n, int C, size_t nmb)
 {
     const char* e = getenv("ZW_DEC_TOKENS");
     const int force = !e ? -1 : (!strcmp(e, "device") ? 1 : (!strcmp(e, "host") ? 0 : (!strcmp(e, "mixed") ? 2 : -1)));
-    if (force == 0 || (force < 0 && n < ZW_DEC_TOKENS_MIN)) return n;
+    if (force == 0) return n;
     if (force == 1) return 0;
-    const char* h = getenv("ZW_DEC_TOKENS_HOST");
-    const double frac = h ? atof(h) : 0.5;
-    int h0 = (int)(n * frac) / C * C;  // whole host chunks
+    if (force == 2) {
+        const char* h = getenv("ZW_DEC_TOKENS_HOST");
+        const double frac = h ? atof(h) : 0.5;
+        return std::max(0, std::min(n, (int)(n * frac) / C * C));  // whole host chunks
+    }
+    // auto.  Defaults until measured: 0.19 ms of chunk time per 1080p frame (16 host
+    // threads) and a 250 ms launch for 1080p frames (measured: 1 024 / 2 048 / 4 096
+    // frames host-only 3 331 / 3 836 / 4 448, best split 3 331 / 4 614 / 4 977 decodes/s)
+    const double host_f = ctx->dec_host_ms_per_frame > 0 ? ctx->dec_host_ms_per_frame : 0.19 * (double)nmb / 8160.0;
+    const double tok = (ctx->dec_tok_ms_per_mb > 0 ? ctx->dec_tok_ms_per_mb : 250.0 / 8160.0) * (double)nmb;
+    const double tail = 0.06 * tok;  // the device frames' reconstruction and download after the launch, per frame of
+                                     // host work that the launch's length leaves (an estimate; errs toward the host)
+    if (n * host_f <= tok + tail) return n;  // the host alone finishes first
+    const int h0 = (int)(tok / host_f) / C * C;
     return std::max(0, std::min(n, h0));
 }
 
@@ -965,16 +979,20 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
             F[i].mbh == 0)
             return false;
     const int mbw = F[0].mbw, mbh = F[0].mbh;
-    const size_t nmb = (size_t)mbw * mbh, slot = nmb * ZW_DREC_MAX;
+    // k_dec_tokl keeps per-lane top contexts in LDS (very wide frames stay on the host) and
+    // addresses a wave's 64 record slots through one buffer (< 2 GB)
+    const size_t nmb = (size_t)mbw * mbh, slot = nmb * ZW_DREC_MAX + 64;  // (+64: the pad store past a full record)
+    if (zw_tokl_lds_bytes(mbw) > 160 * 1024 || 64 * slot >= ((size_t)1 << 31)) return false;
+    const size_t probs_b = (size_t)tokl::PROBS;
     std::vector<size_t> boff(nd);
     size_t blob = 0;
     for (int i = 0; i < nd; i++) {
         boff[i] = blob;
         blob += (F[i].part[0].len + 15) & ~(size_t)15;
     }
-    blob += 16;  // k_dec_tokens reads up to 16 bytes past a partition
+    blob += 16;  // (16 zero bytes at the end)
     const size_t o_m = 0, o_p = al256(o_m + (size_t)nd * nmb * ZW_TOK_MODE);
-    const size_t o_tf = al256(o_p + (size_t)nd * ZW_TOK_PROBS), o_fb = al256(o_tf + (size_t)nd * sizeof(ZwTokFrame));
+    const size_t o_tf = al256(o_p + (size_t)nd * probs_b), o_fb = al256(o_tf + (size_t)nd * sizeof(ZwTokFrame));
     const size_t o_b = al256(o_fb + (size_t)nd * 8), up_bytes = al256(o_b + blob);
     uint8_t* stage = (uint8_t*)ctx_pinned(ctx, 4, up_bytes);
     if (!stage) return false;
@@ -982,17 +1000,7 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     T.fps.assign(nd, ZwFilterParams());
     parallel_for(nd, [&](int i) {
         rc[i] = parse_modes(F[i], stage + o_m + (size_t)i * nmb * ZW_TOK_MODE);
-        // register layout (ZW_TOK_PROBS): dword (vgpr k, lane l) at (64 k + l) * 4; type t's
-        // rows (band b < 7, ctx c) in vgpr 2t at lanes (3b + c) * 3 + 0..2, band 7 in vgpr 2t + 1
-        uint8_t* pr = stage + o_p + (size_t)i * ZW_TOK_PROBS;
-        memset(pr, 0, ZW_TOK_PROBS);
-        for (int t = 0; t < 4; t++)
-            for (int b = 0; b < 8; b++)
-                for (int c = 0; c < 3; c++)
-                    for (int j = 0; j < 3; j++) {
-                        const int k = 2 * t + (b == 7), l = (b == 7 ? c : 3 * b + c) * 3 + j;
-                        for (int q = 0; q < 4 && 4 * j + q < 11; q++) pr[(64 * k + l) * 4 + q] = F[i].probs[t][b][c][4 * j + q];
-                    }
+        memcpy(stage + o_p + (size_t)i * probs_b, F[i].probs, tokl::PROBS);  // [type][band][ctx][node]
         const ZwTokFrame tf = {boff[i], (uint32_t)F[i].part[0].len, 0};
         memcpy(stage + o_tf + (size_t)i * sizeof(ZwTokFrame), &tf, sizeof tf);
         ((uint64_t*)(stage + o_fb))[i] = (uint64_t)i * slot;
@@ -1017,8 +1025,8 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     hipStream_t s = ctx->tok_;
     if (hipMemcpyAsync(d, stage, up_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return false;
     if (hipEventRecord(ctx->tok_ev[0], s) != hipSuccess) return false;
-    if (zwk_dec_tokens(s, d + o_b, (const ZwTokFrame*)(d + o_tf), d + o_p, d + o_m, d + o_rec, slot,
-                       (uint32_t*)(d + o_mo), (int*)(d + o_te), mbw, mbh, nd) != hipSuccess)
+    if (zwk_dec_tokl(s, d + o_b, (const ZwTokFrame*)(d + o_tf), d + o_p, d + o_m, d + o_rec, slot,
+                     (uint32_t*)(d + o_mo), (int*)(d + o_te), mbw, mbh, nd) != hipSuccess)
         return false;
     if (hipEventRecord(ctx->tok_ev[1], s) != hipSuccess) {
         (void)hipStreamSynchronize(s);  // (the launch is in flight: let it finish before the host takes over)
@@ -1091,10 +1099,17 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     DecTok T;
     {
         const double t0 = dec_now_ms();
-        const int h0 = dec_tok_split(n, C);
+        size_t nmb = 0;
+        if (n > 0 && lens[0] >= 10) {  // (the first frame's dimensions; dec_tok_prepare checks every frame)
+            const uint8_t* d = data[0];
+            nmb = (size_t)((((d[6] | (d[7] << 8)) & 0x3fff) + 15) / 16) * (size_t)((((d[8] | (d[9] << 8)) & 0x3fff) + 15) / 16);
+        }
+        const int h0 = nmb ? dec_tok_split(ctx, n, C, nmb) : n;
         if (h0 >= n || !dec_tok_prepare(ctx, n, data, lens, h0, T)) T.h0 = n;
         ctx->dec_host_ms[0] += dec_now_ms() - t0;
     }
+    double host_parse_ms = 0;
+    int host_frames = 0;
     auto first = [&](int c) { return c * C; };
     auto count = [&](int c) { return std::min(C, n - c * C); };
     int err = ZW_OK;
@@ -1112,8 +1127,13 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             });
         }
         if (c < nch) {
-            if (first(c) >= T.h0) dec_parse_dev(T, first(c), count(c), B[c & 1]);
-            else err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+            if (first(c) >= T.h0) {
+                dec_parse_dev(T, first(c), count(c), B[c & 1]);
+            } else {
+                err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
+                host_parse_ms += B[c & 1].parse_ms;
+                host_frames += count(c);
+            }
             ctx->dec_host_ms[0] += B[c & 1].parse_ms;
         }
         if (fin.joinable()) fin.join();
@@ -1127,9 +1147,13 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     if (T.nd > 0) {
         float ms = 0.f;
         if (hipEventSynchronize(T.done) == hipSuccess &&
-            hipEventElapsedTime(&ms, ctx->tok_ev[0], ctx->tok_ev[1]) == hipSuccess)
+            hipEventElapsedTime(&ms, ctx->tok_ev[0], ctx->tok_ev[1]) == hipSuccess) {
             ctx->dec_tok_ms = ms;
+            if (!err && ms > 0) ctx->dec_tok_ms_per_mb = ms / (double)T.nmb;
+        }
     }
+    // (a chunk's parse runs while the previous chunk downloads: the chunk time is its share of the pipe)
+    if (!err && host_frames >= C && host_parse_ms > 0) ctx->dec_host_ms_per_frame = host_parse_ms / host_frames;
     if (err) (void)hipStreamSynchronize(ctx_stream(ctx));  // nothing queued may outlive the call
     return err;
 }
@@ -1445,6 +1469,105 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
     HIPOK(hipMemcpyAsync(v, d + o_v, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
     return rows_env != 0 ? rows_error(ctx, (const int*)(d + o_rs), 1, (int)mbh) : ZW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// CPU check of the device token parse's state machine (zw_tokl.h, the code
+// k_dec_tokl runs per lane): the same functions step one frame here over host
+// memory, and the records must equal parse_mbs's byte for byte (or both fail).
+// Test hook only (tests/test_tokl.py); no device work.
+// ---------------------------------------------------------------------------
+namespace {
+struct HostTokMem {
+    static constexpr uint32_t U = 1;
+    static constexpr uint32_t lane0 = 0;
+    const uint32_t* TT;
+    const uint8_t* P;
+    const uint8_t* stream;
+    size_t len;
+    const uint8_t* modes;
+    uint8_t* rec;
+    uint32_t* mo;
+    uint32_t nmb, mbw;
+    std::vector<uint16_t> tcxv;
+
+    void tt(uint32_t st, uint32_t& t0, uint32_t& t1) const
+    {
+        t0 = TT[2 * st];
+        t1 = TT[2 * st + 1];
+    }
+    void desc(uint32_t i, uint32_t* d) const { tokl::desc(i / tokl::NDESC, i % tokl::NDESC, d); }
+    uint32_t prob_at(uint32_t i) const { return P[i]; }
+    uint64_t bits64(uint32_t bp) const
+    {
+        uint64_t v = 0;
+        const size_t b0 = bp >> 3;
+        for (int i = 0; i < 9; i++) {
+            const uint64_t byte = b0 + i < len ? stream[b0 + i] : 0;
+            if (i < 8) v = (v << 8) | byte;
+            else v = (bp & 7) ? (v << (bp & 7)) | (byte >> (8 - (bp & 7))) : v;
+        }
+        return v;
+    }
+    void mode(uint32_t mbi, uint32_t* r) const { memcpy(r, modes + (size_t)mbi * ZW_TOK_MODE, 16); }
+    uint32_t tcx(uint32_t mbx) const { return tcxv[mbx]; }
+    void set_tcx(uint32_t mbx, uint32_t v) { tcxv[mbx] = (uint16_t)v; }
+    void st16c(bool c, uint32_t off, uint32_t v)
+    {
+        const uint16_t h = (uint16_t)v;
+        if (c) memcpy(rec + off, &h, 2);
+    }
+    void st128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+    {
+        const uint32_t w[4] = {a, b, c, d};
+        memcpy(rec + off, w, 16);
+    }
+    void st128u(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) { st128(off, a, b, c, d); }
+    void moff(uint32_t i, uint32_t v) { mo[i] = v; }
+};
+}  // namespace
+
+extern "C" int zw_dbg_tokl_frame(const uint8_t* vp8, size_t len, int* match)
+{
+    if (!match || (!vp8 && len)) return ZW_EINVAL;
+    *match = -1;
+    DecFrame A, B;
+    if (int r = parse_header(A, vp8, len)) return r;
+    (void)parse_header(B, vp8, len);
+    const size_t nmb = (size_t)A.mbw * A.mbh;
+    if (nmb == 0) return ZW_EINVALID_DIMENSIONS;
+    std::vector<uint8_t> ref(nmb * ZW_DREC_MAX), modes(nmb * ZW_TOK_MODE), rec(nmb * ZW_DREC_MAX + 64);
+    std::vector<uint32_t> moff_ref(nmb + 1), moff(nmb + 1);
+    const int rc = parse_mbs(A, ref.data(), moff_ref.data());
+    if (B.nparts != 1 || parse_modes(B, modes.data()) != ZW_OK) return rc;  // the host keeps such frames
+    static const uint32_t TT[2 * tokl::NST] = ZW_TOKL_TT_INIT;
+    HostTokMem m;
+    m.TT = TT;
+    m.P = &B.probs[0][0][0][0];
+    m.stream = B.part[0].d;
+    m.len = B.part[0].len;
+    m.modes = modes.data();
+    m.rec = rec.data();
+    m.mo = moff.data();
+    m.nmb = (uint32_t)nmb;
+    m.mbw = (uint32_t)B.mbw;
+    m.tcxv.assign(B.mbw, 0);
+    tokl::Lane L;
+    tokl::init(L, (uint32_t)m.len, true);
+    while (L.phase != tokl::PH_DONE) {
+        if (L.phase == tokl::PH_MB) {
+            tokl::mb_phase(L, m);
+            continue;
+        }
+        if (L.vb < 8) tokl::topup(L, m);
+        tokl::step(L, m);
+    }
+    if (rc != ZW_OK || L.bad) {
+        *match = (rc == ZW_EBITSTREAM && L.bad) ? 1 : 0;
+        return rc;
+    }
+    *match = moff == moff_ref && !memcmp(rec.data(), ref.data(), moff_ref[nmb]) ? 1 : 0;
+    return rc;
 }
 
 // ---------------------------------------------------------------------------

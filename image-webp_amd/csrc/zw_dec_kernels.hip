@@ -65,12 +65,12 @@ DI int i4_eoff(int j) { return j < 4 ? (3 - j) * ZW_BPS - 1 : (j == 4 ? -ZW_BPS 
 
 
 // Packed MB record (zw_common.h ZW_DREC_*, written by zw_dec_host.cpp
-// PackedMb): byte 0 luma mode (bits 0-2), chroma mode (3-4), skip (5); byte 1
-// segment; bytes 4-7 the non-zero mask; 8-15 the I4 sub-modes as nibbles;
-// halfwords 8.. the level start of each block (0-23, 24 = Y2) and the end;
-// from byte ZW_DREC_HDR each block's levels in zigzag order up to its last
-// non-zero one.  drec_lv: the level at natural index n of the block whose
-// levels are [s0, s1).
+// parse_mbs or k_dec_tokl): byte 0 luma mode (bits 0-2), chroma mode (3-4),
+// skip (5); byte 1 segment; bytes 4-7 the non-zero mask; 8-15 the I4 sub-modes
+// as nibbles; halfwords 8.. the level start of each block 0-23 and (24) the
+// end; from byte ZW_DREC_HDR the levels in zigzag order up to each block's last
+// non-zero one, Y2's first ([0, start[0])).  drec_lv: the level at natural
+// index n of the block whose levels are [s0, s1).
 DI int drec_lv(const uint8_t* rb, int s0, int s1, int n)
 {
     const int idx = s0 + izz_of(n);
@@ -509,10 +509,10 @@ __device__ __forceinline__ void dec_recon_row(const uint8_t* __restrict__ recs, 
 #endif
             // Y2 in group form (lane k = block k's DC after the iWHT), moved to the quads
             const int k = lane & 15;
-            const int y2s = __builtin_amdgcn_readfirstlane(drec_start(rb, 24)), y2e = __builtin_amdgcn_readfirstlane(drec_start(rb, 25));
+            const int y2e = __builtin_amdgcn_readfirstlane(drec_start(rb, 0));  // Y2's levels come first: [0, start[0])
             int dc = 0;
-            if (!skip && y2e > y2s) {
-                const int y2v = drec_lv(rb, y2s, y2e, k) * (k ? Q.y2ac : Q.y2dc);
+            if (!skip && y2e > 0) {
+                const int y2v = drec_lv(rb, 0, y2e, k) * (k ? Q.y2ac : Q.y2dc);
                 dc = __builtin_amdgcn_ds_bpermute(4 * b, iwht_g(y2v, k));
             }
             const int s0 = drec_start(rb, b), s1 = drec_start(rb, b + 1);

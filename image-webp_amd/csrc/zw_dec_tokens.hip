@@ -1,365 +1,358 @@
-// zw_dec_tokens.hip -- the VP8 token partition parsed on the device (gfx950).
+// zw_dec_tokens.hip -- the VP8 token partition parsed on the device (gfx950),
+// one frame per LANE (k_dec_tokl).
 //
 // read_coefficients (decoder/vp8.rs:872-1058) over the boolean decoder of
 // bit_reader.rs:254-640.  A frame's token partition is one serial chain of
 // binary decisions (each one's range and value depend on the one before), so a
-// frame cannot be split; a batch parses its frames side by side, one wave per
-// frame.  All control state is wave-uniform, so it lives in scalar registers
-// and branches on the scalar unit; the lanes hold the current block's levels
-// (lane n = zigzag position n) and copy each MB's packed
-// record (zw_common.h ZW_DREC_*) out in one pass.  The records are
-// byte-identical to the host parser's (zw_dec_host.cpp parse_mbs), and
-// k_dec_recon reads them unchanged.  The host keeps the frame header and the
-// first partition's per-MB modes (ZW_TOK_MODE bytes per MB, a short chain).
+// frame cannot be split; a batch parses its frames side by side.  The host
+// keeps the frame header and the first partition's per-MB modes (ZW_TOK_MODE
+// bytes per MB, a short chain); the records written here are byte-identical to
+// the host parser's (zw_dec_host.cpp parse_mbs), and k_dec_recon reads them
+// unchanged.
 #include "zw_dev.h"
+
+// ---------------------------------------------------------------------------
+// Lane-parallel form (k_dec_tokl): one frame per LANE, 64 frames per wave.
+//
+// Every lane runs zw_tokl.h's state machine for its own frame: one decision per
+// step, written branch-free (a branch any lane takes costs the whole wave, and
+// some lane ends a token or a block at almost every step), the MB bookkeeping
+// in an MB phase.  Round 4's form, one frame per wave on the scalar unit, ran
+// ≈517 cycles per decision and held a wave per frame.  The decoder wave issues
+// no global loads (its stores never have to be waited for); a second wave of the
+// workgroup, the feeder, copies each lane's stream bytes and per-MB mode records
+// from HBM into LDS rings ahead of use and publishes fill counters that the
+// decoder lanes read (LDS operations of a CU complete in issue order; every
+// spin is bounded and a lane that gives up reports a device error).
+//
+// LDS per workgroup (dwords): probabilities [264][64] (lane l's dword j at
+// j * 64 + l: a lane-varying row index never makes two lanes of a group hit one
+// bank), stream ring [16][64] (64 bytes per lane), mode ring [32 slots][4][64],
+// sync words, the transition and descriptor tables, and the top contexts
+// [mbw][64] u16.  ≈122 KB at 1080p: one workgroup per CU.  Record stores are
+// raw buffer stores over the wave's 64 frame slots, with an out-of-range offset
+// for a lane that stores nothing (no branch).
+// ---------------------------------------------------------------------------
+#include "zw_tokl.h"
 
 namespace {
 
-DI uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__constant__ uint32_t d_TOKL_TT[2 * tokl::NST] = ZW_TOKL_TT_INIT;
 
-// BitReader (bit_reader.rs; zw_dec_host.cpp BitReader) with the same loads:
-// 7 bytes while at least 7 remain, then one byte at a time, then one zero byte
-// and eof.  The 16 bytes holding the next 7-byte load are fetched into LDS by
-// an LDS-DMA load as soon as the previous load is consumed (no register
-// destination, so nothing on the decision chain waits for it until the next
-// load; two slots alternate so a read never meets the DMA writing).
-struct TokBD {
-#ifdef ZW_TOK_PROF
-    uint32_t ndec, nload;  // profiling build: decisions and 7-byte loads
-#endif
-    const uint8_t* p;
-    uint64_t value;
-    uint32_t range, pos, len, slot;
-    int bits;
-    bool eof;
-};
+constexpr int TKL_P = 264 * 64, TKL_SR = 16 * 64, TKL_MRS = 32, TKL_MR = TKL_MRS * 4 * 64, TKL_SY = 4 * 64 + 4,
+              TKL_TT = 2 * tokl::NST, TKL_DS = 2 * 4 * tokl::NDESC;
+constexpr int TKL_FIXED = TKL_P + TKL_SR + TKL_MR + TKL_SY + TKL_TT + TKL_DS;  // dwords before the top contexts
+constexpr uint32_t TKL_SPIN = 1u << 22;
 
-DI void tok_fetch(TokBD& b, uint8_t* sbuf)
-{
-    if ((threadIdx.x & 63) == 0)
-        __builtin_amdgcn_global_load_lds((const void*)(b.p + (b.pos & ~3u)), (void*)(sbuf + 16 * b.slot), 16, 0, 0);
-}
+typedef __attribute__((address_space(3))) uint32_t lds_u32;  // (a generic volatile pointer would become a flat access)
 
-DI void tok_load(TokBD& b, uint8_t* sbuf)
-{
-    const uint32_t rem = b.len - b.pos;
-    if (rem >= 7) {
-#ifdef ZW_TOK_PROF
-        b.nload++;
-#endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fetch has landed
-        const uint4 w = *(const uint4*)(sbuf + 16 * b.slot);
-        const uint32_t o = b.pos & 3u;
-        const uint64_t lo = ((uint64_t)rfl(w.y) << 32) | rfl(w.x);
-        const uint64_t hi = ((uint64_t)rfl(w.w) << 32) | rfl(w.z);
-        const uint64_t x = o ? (lo >> (8 * o)) | (hi << (64 - 8 * o)) : lo;  // bytes pos..pos+7, first in the low byte
-        b.value = (__builtin_bswap64(x) >> 8) | (b.value << 56);
-        b.bits += 56;
-        b.pos += 7;
-        b.slot ^= 1u;
-        tok_fetch(b, sbuf);
-    } else if (rem > 0) {
-        const uint32_t w = rfl(*(const uint32_t*)(b.p + (b.pos & ~3u)));
-        b.value = (uint64_t)((w >> (8 * (b.pos & 3u))) & 255u) | (b.value << 8);
-        b.bits += 8;
-        b.pos++;
-    } else {
-        // past the end: the reference shifts in one zero byte and sets eof, and
-        // read_coefficients then fails the frame (vp8.rs; parse_mbs returns
-        // ZW_EBITSTREAM) -- the device flags the frame the same way
-        b.eof = true;
-        b.value <<= 8;
-        b.bits += 8;
+struct TokDev {
+    static constexpr uint32_t U = 64;  // probability table [entry][lane] bytes
+    uint32_t* P;
+    const uint32_t* TT;
+    const uint32_t* DS;
+    const uint32_t* SR;
+    const uint32_t* MR;
+    uint16_t* TCX;
+    volatile lds_u32* sfill;
+    volatile lds_u32* mfill;
+    volatile lds_u32* scons;
+    volatile lds_u32* mcons;
+    __amdgpu_buffer_rsrc_t rr;  // the wave's 64 record slots
+    uint32_t rbase;             // this lane's slot in rr
+    uint32_t* mo;
+    uint32_t lane, lane0, nmb, mbw, tmo;
+
+    DI void tt(uint32_t st, uint32_t& t0, uint32_t& t1) const
+    {
+        t0 = TT[2 * st];
+        t1 = TT[2 * st + 1];
     }
-}
-
-DI void tok_init(TokBD& b, const uint8_t* p, uint32_t len, uint8_t* sbuf)
-{
-    b.p = p;  // (the blob has 16 readable bytes past every partition)
-    b.len = len;
-    b.pos = 0;
-    b.value = 0;
-    b.range = 254;
-    b.bits = -8;
-    b.eof = false;
-    b.slot = 0;
-#ifdef ZW_TOK_PROF
-    b.ndec = b.nload = 0;
-#endif
-    tok_fetch(b, sbuf);
-    tok_load(b, sbuf);
-}
-
-// read_bool: split = range * prob >> 8 on range - 1 (bit_reader.rs), the
-// update by selects (no branch on the decoded bit)
-DI int tok_bit(TokBD& b, uint32_t prob, uint8_t* sbuf)
-{
-    if (b.bits < 0) tok_load(b, sbuf);
-#ifdef ZW_TOK_PROF
-    b.ndec++;
-#endif
-    const uint32_t split = (b.range * prob) >> 8;
-    const uint32_t v = (uint32_t)(b.value >> b.bits);
-    const bool bit = v > split;
-    const uint32_t nr = bit ? b.range - split : split + 1;
-    b.value = bit ? b.value - ((uint64_t)(split + 1) << b.bits) : b.value;
-    const int shift = __builtin_clz(nr) - 24;
-    b.bits -= shift;
-    b.range = (nr << shift) - 1;
-    return bit ? 1 : 0;
-}
-
-// The frame's coefficient probabilities live in registers: per block type t,
-// VGPR A holds the rows of bands 0..6 (row (band, ctx) = dwords 0..2 at lanes
-// (3 band + ctx) * 3 ..), VGPR B the rows of band 7 (lanes 3 ctx ..); a row is
-// read with three v_readlane (no memory access on the decision chain).
-struct TokRow {
-    uint32_t r0, r1, r2;
-};
-DI uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-#ifdef ZW_TOK_SMEM
-// (experiment: the rows as scalar loads from the frame's table in memory, A = the type's first register index)
-DI TokRow prow_m(const uint8_t* __restrict__ Pf, uint32_t A, int n, int ctx)
-{
-    const uint32_t k = A + (n == 15 ? 1u : 0u);
-    const int l = n < 15 ? (band_of(n) * 3 + ctx) * 3 : ctx * 3;
-    const uint4 w = *(const uint4*)(Pf + (64 * k + l) * 4);
-    TokRow r;
-    r.r0 = w.x;
-    r.r1 = w.y;
-    r.r2 = w.z;
-    return r;
-}
-#define prow(A, B, n, ctx) prow_m(Pf, A, n, ctx)
-#else
-DI TokRow prow(uint32_t A, uint32_t B, int n, int ctx)
-{
-    TokRow r;
-    if (n < 15) {
-        const int l = (band_of(n) * 3 + ctx) * 3;
-        r.r0 = rdl(A, l);
-        r.r1 = rdl(A, l + 1);
-        r.r2 = rdl(A, l + 2);
-    } else {
-        const int l = ctx * 3;
-        r.r0 = rdl(B, l);
-        r.r1 = rdl(B, l + 1);
-        r.r2 = rdl(B, l + 2);
+    DI void desc(uint32_t i, uint32_t* d) const
+    {
+        const uint4 v = *(const uint4*)(DS + 4 * i);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
     }
-    return r;
-}
-#endif
-// Byte k of a probability row (k constant at every call site).
-DI uint32_t pb(const TokRow& r, int k)
-{
-    const uint32_t w = k < 4 ? r.r0 : (k < 8 ? r.r1 : r.r2);
-    return (w >> (8 * (k & 3))) & 255u;
-}
-
-// One block's tokens (read_coefficients vp8.rs:872-1058; zw_dec_host.cpp
-// read_levels_into): lane n of lvv gets the level at zigzag position n
-// (positions < first and the zeros stay 0); eob = last nonzero position + 1.
-// Returns the block's non-zero flag (n > first at the end of block; a zero run
-// to position 16 counts as non-zero, as in the reference).
-DI int tok_block(TokBD& b, uint8_t* sbuf, uint32_t A, uint32_t B, int first, int ctx, int& lvv, int& eob
-#ifdef ZW_TOK_SMEM
-                 , const uint8_t* __restrict__ Pf
-#endif
-)
-{
-    int n = first;
-    eob = 0;
-    lvv = 0;
-    TokRow row = prow(A, B, n, ctx);
-    for (;;) {
-        if (!tok_bit(b, pb(row, 0), sbuf)) break;  // end of block
-        while (!tok_bit(b, pb(row, 1), sbuf)) {    // DCT_0
-            if (++n == 16) return 1;
-            row = prow(A, B, n, 0);
-        }
-        int v, nctx = 2;
-        if (!tok_bit(b, pb(row, 2), sbuf)) {
-            v = 1;
-            nctx = 1;
-        } else if (!tok_bit(b, pb(row, 3), sbuf)) {
-            if (!tok_bit(b, pb(row, 4), sbuf)) v = 2;
-            else v = 3 + tok_bit(b, pb(row, 5), sbuf);
-        } else if (!tok_bit(b, pb(row, 6), sbuf)) {
-            if (!tok_bit(b, pb(row, 7), sbuf)) {
-                v = 5 + tok_bit(b, 159, sbuf);
-            } else {
-                v = 7 + 2 * tok_bit(b, 165, sbuf);
-                v += tok_bit(b, 145, sbuf);
+    DI uint32_t prob_at(uint32_t a) const { return ((const uint8_t*)P)[a]; }
+    // 64 stream bits from bit bp on, MSB first (dwords hold 4 stream bytes, the
+    // first in the low byte)
+    DI uint64_t bits64(uint32_t bp)
+    {
+        const uint32_t dw = bp >> 5, need = ((4u * dw + 11u) >> 4) + 1u;
+        for (uint32_t i = 0; sfill[lane] < need; i++) {
+            if (i > TKL_SPIN) {
+                tmo = 1;
+                break;
             }
-        } else {
-            const int b1 = tok_bit(b, pb(row, 8), sbuf);
-            const int b0 = tok_bit(b, b1 ? pb(row, 10) : pb(row, 9), sbuf);
-            const int cat = 2 * b1 + b0;  // DCT_CAT3..6: 3, 4, 5, 11 extra bits
-            // PROB_DCT_CAT[2 + cat] as byte immediates (no memory load on the chain)
-            const uint64_t lo = cat == 0 ? 0x8c94adull : (cat == 1 ? 0x878c9bb0ull : (cat == 2 ? 0x82868d9db4ull : 0x8c99b1c4e6f3fefeull));
-            const int nb = cat == 3 ? 11 : 3 + cat;
-            int extra = 0;
-            for (int k = 0; k < nb; k++) {
-                const uint32_t p = k < 8 ? (uint32_t)(lo >> (8 * k)) & 255u : (0x818285u >> (8 * (k - 8))) & 255u;
-                extra = extra + extra + tok_bit(b, p, sbuf);
-            }
-            v = 3 + (8 << cat) + extra;
+            __builtin_amdgcn_s_sleep(1);
         }
-        const int s = tok_bit(b, 128, sbuf);
-        lvv = (int)(threadIdx.x & 63) == n ? (s ? -v : v) : lvv;
-        eob = ++n;
-        if (n == 16) break;
-        row = prow(A, B, n, nctx);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t d0 = SR[((dw) & 15u) * 64u + lane], d1 = SR[((dw + 1u) & 15u) * 64u + lane],
+                       d2 = SR[((dw + 2u) & 15u) * 64u + lane];
+        scons[lane] = 4u * dw;  // (issued after the reads: the feeder may now refill older chunks)
+        const uint32_t b0 = __builtin_bswap32(d0), b1 = __builtin_bswap32(d1), b2 = __builtin_bswap32(d2);
+        const uint32_t o = bp & 31u;
+        return ((((uint64_t)b0) << 32 | b1) << o) | (uint32_t)((((uint64_t)b2) << o) >> 32);
     }
-    return n > first;
-}
+    DI void mode(uint32_t mbi, uint32_t* r)
+    {
+        for (uint32_t i = 0; mfill[lane] <= mbi; i++) {
+            if (i > TKL_SPIN) {
+                tmo = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t s = (mbi & (TKL_MRS - 1)) * 4u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) r[j] = MR[(s + j) * 64u + lane];
+        mcons[lane] = mbi + 1u;
+    }
+    DI uint32_t tcx(uint32_t mbx) const { return TCX[mbx * 64u + lane]; }
+    DI void set_tcx(uint32_t mbx, uint32_t v) { TCX[mbx * 64u + lane] = (uint16_t)v; }
+    DI void st16c(bool c, uint32_t off, uint32_t v)
+    {
+#ifndef ZW_TOKL_EXP_NOSTORE  // (timing experiment: no level / start stores, wrong records)
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rr, (int)(c ? rbase + off : ZW_OOB), 0, 0);
+#endif
+    }
+    DI void st128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+    {
+        const zu4 v = {a, b, c, d};
+        bst128(v, rr, rbase + off);
+    }
+    DI void st128u(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) { st128(off, a, b, c, d); }
+    DI void moff(uint32_t i, uint32_t v) { mo[i] = v; }
+};
 
 }  // namespace
 
-// One wave per frame.  tf[f]: the frame's token partition in blob; probs:
-// ZW_TOK_PROBS bytes per frame; modes: ZW_TOK_MODE bytes per MB per frame.
-// Out: frame f's records at recs + f * slot, their offsets at moff + f * (nmb
-// + 1) (moff[nmb] = the used bytes), err[f] = 1 when the partition ran out
-// (the host then fails the call with ZW_EBITSTREAM, as parse_mbs does).
-#ifndef ZW_TOK_WAVES
-#define ZW_TOK_WAVES 1  // frames (waves) per workgroup: more confine the launch to fewer CUs
+#ifndef ZW_TOKL_TK
+#define ZW_TOKL_TK 8  // steps between top-ups (one decision per step: <= 8 keeps >= 8 valid bits)
 #endif
-extern "C" __global__ __launch_bounds__(64 * ZW_TOK_WAVES) void k_dec_tokens(const uint8_t* __restrict__ blob,
-                                                              const ZwTokFrame* __restrict__ tf,
-                                                              const uint8_t* __restrict__ probs,
-                                                              const uint8_t* __restrict__ modes, uint8_t* recs,
-                                                              uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh,
-                                                              int nframes)
+#ifndef ZW_TOKL_MK
+#define ZW_TOKL_MK 1  // steps between MB phases
+#endif
+#ifndef ZW_TOKL_MBRUN
+#define ZW_TOKL_MBRUN 8  // MBs one MB phase may start (skipped MBs need no decisions)
+#endif
+
+// One workgroup = a decoder wave (64 frames, lane l = frame blockIdx.x * 64 + l)
+// and a feeder wave.  Same arguments and outputs as k_dec_tokens, except
+// probs: tokl::PROBS bytes per frame in [type][band][ctx][node] order.  err[f]:
+// 1 = the partition ran out (ZW_EBITSTREAM), 2 = a bounded wait gave up.
+extern "C" __global__ __launch_bounds__(128) void k_dec_tokl(const uint8_t* __restrict__ blob,
+                                                            const ZwTokFrame* __restrict__ tf,
+                                                            const uint8_t* __restrict__ probs,
+                                                            const uint8_t* __restrict__ modes, uint8_t* recs,
+                                                            uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh,
+                                                            int nframes)
 {
-    __shared__ uint16_t tcx_all[ZW_TOK_WAVES][(ZW_MAX_W + 15) / 16];  // 9-bit top contexts per MB column (Y2, Y 1-4, U 5-6, V 7-8)
-    __shared__ __attribute__((aligned(16))) uint8_t rec_all[ZW_TOK_WAVES][ZW_DREC_MAX + 16];
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf_all[ZW_TOK_WAVES][32];  // the stream's two 16-byte fetch slots
-    const int wv = (int)(threadIdx.x >> 6), f = blockIdx.x * ZW_TOK_WAVES + wv, lane = (int)(threadIdx.x & 63);
-    if (f >= nframes) return;  // (no workgroup barrier below: every wave runs alone)
-    uint16_t* tcx = tcx_all[wv];
-    uint8_t* rec = rec_all[wv];
-    uint8_t* sbuf = sbuf_all[wv];
-    const size_t nmb = (size_t)mbw * mbh;
-    for (int i = lane; i < mbw; i += 64) tcx[i] = 0;
-    // the frame's probabilities: 8 VGPRs (type t: A = P[2 t], B = P[2 t + 1]; ZW_TOK_PROBS layout)
-    uint32_t P[8];
+    extern __shared__ uint32_t sm[];
+    uint32_t* P = sm;
+    uint32_t* SR = P + TKL_P;
+    uint32_t* MR = SR + TKL_SR;
+    uint32_t* SY = MR + TKL_MR;
+    uint32_t* TT = SY + TKL_SY;
+    uint32_t* DS = TT + TKL_TT;
+    uint16_t* TCX = (uint16_t*)(DS + TKL_DS);
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int f = (int)blockIdx.x * 64 + lane;
+    const bool act = f < nframes;
+    const uint32_t nmb = (uint32_t)mbw * (uint32_t)mbh;
+    // tables, zeroed state, the lanes' probabilities (both waves)
+    for (int i = tid; i < TKL_TT; i += 128) TT[i] = d_TOKL_TT[i];
+    for (int i = tid; i < 2 * tokl::NDESC; i += 128) tokl::desc((uint32_t)(i / tokl::NDESC), (uint32_t)(i % tokl::NDESC), DS + 4 * i);
+    for (int i = tid; i < TKL_SY; i += 128) SY[i] = 0u;
+    for (int i = tid; i < mbw * 32; i += 128) ((uint32_t*)TCX)[i] = 0u;
+    {
+        const uint4* pr = (const uint4*)(probs + (size_t)(act ? f : 0) * tokl::PROBS);
+        uint8_t* P8 = (uint8_t*)P;  // entry i of lane l at byte i * 64 + l
+#pragma unroll 11
+        for (int q = wv; q < tokl::PROBS / 16; q += 2) {
+            const uint4 v = act ? pr[q] : make_uint4(0, 0, 0, 0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int k = 0; k < 8; k++) P[k] = ((const uint32_t*)(probs + (size_t)f * ZW_TOK_PROBS))[k * 64 + lane];
-    TokBD b;
-#ifdef ZW_TOK_PROF
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
-    tok_init(b, blob + tf[f].off, tf[f].len, sbuf);
-    const uint4* __restrict__ M = (const uint4*)(modes + (size_t)f * nmb * ZW_TOK_MODE);
-    const __amdgpu_buffer_rsrc_t ro = brsrc(recs + (size_t)f * slot, (uint32_t)slot);
-    const __amdgpu_buffer_rsrc_t rm = brsrc(moff + (size_t)f * (nmb + 1), (uint32_t)(nmb + 1) * 4u);
-    int16_t* lv = (int16_t*)(rec + ZW_DREC_HDR);
-    uint32_t used = 0;
-    // read_levels_into fails a frame when a block read ends with eof set (an
-    // empty partition is fine while every MB is skipped)
-    bool bad = false;
-    uint32_t mdone = 0;  // MBs whose offset is written
-    wsync();
-    for (int mby = 0; mby < mbh && !bad; mby++) {
-        uint32_t L = 0;  // left contexts, the same 9 bits
-        for (int mbx = 0; mbx < mbw; mbx++) {
-            const size_t i = (size_t)mby * mbw + mbx;
-            const uint4 mr = M[i];
-            const int lm = (int)(mr.x & 7u), skip = (int)((mr.x >> 5) & 1u);
-            uint32_t T = rfl(tcx[mbx]);
-            bst32(used, rm, lane == 0 ? (uint32_t)i * 4u : ZW_OOB);
-            mdone = (uint32_t)i + 1u;
-            if (skip) {
-                // header only: the modes, no levels (every start 0)
-                if (lm != 4) {
-                    T &= ~1u;
-                    L &= ~1u;
-                }
-                T &= 1u;
-                L &= 1u;
-                const zu4 h = {mr.x, 0u, mr.z, mr.w}, z = {0u, 0u, 0u, 0u};
-                bst128(lane == 0 ? h : z, ro, lane < 5 ? used + 16u * (uint32_t)lane : ZW_OOB);
-                used += ZW_DREC_HDR;
-            } else {
-                uint32_t nzm = 0;
-                int nlv = 0, stv = 0, y2v = 0, y2eob = 0, lvv, eob;
-                const uint32_t YA = lm != 4 ? P[0] : P[6], YB = lm != 4 ? P[1] : P[7];  // type 0 (after Y2) or 3 (I4)
-                auto put = [&](int blk) {  // the block's levels after the previous blocks'
-                    stv = lane == blk ? nlv : stv;
-                    if (lane < eob) lv[nlv + lane] = (int16_t)lvv;
-                    nlv += eob;
-                };
-                // the MB's blocks in the reference's order, through one call site (one copy
-                // of the token walk in the code): k = 0 Y2 (I16 MBs only), 1..16 Y, 17..20 U,
-                // 21..24 V; tb / lb = the block's bit in the top / left context words
-#pragma unroll 1
-                for (int k = lm != 4 ? 0 : 1; k < 25; k++) {
-                    const int q = k - 17, pl = q >> 2;
-                    const int tb = k == 0 ? 0 : (k <= 16 ? ((k - 1) & 3) + 1 : (q & 1) + 5 + 2 * pl);
-                    const int lb = k == 0 ? 0 : (k <= 16 ? ((k - 1) >> 2) + 1 : ((q >> 1) & 1) + 5 + 2 * pl);
-#ifdef ZW_TOK_SMEM
-                    const uint32_t A = k == 0 ? 2u : (k <= 16 ? (lm != 4 ? 0u : 6u) : 4u), B = 0;
-#else
-                    const uint32_t A = k == 0 ? P[2] : (k <= 16 ? YA : P[4]), B = k == 0 ? P[3] : (k <= 16 ? YB : P[5]);
-#endif
-                    const int first = k >= 1 && k <= 16 && lm != 4 ? 1 : 0;
-                    const int ctx = (int)((T >> tb) & 1u) + (int)((L >> lb) & 1u);
-                    const int nz = tok_block(b, sbuf, A, B, first, ctx, lvv, eob
-#ifdef ZW_TOK_SMEM
-                                             , probs + (size_t)f * ZW_TOK_PROBS
-#endif
-                    );
-                    T = (T & ~(1u << tb)) | ((uint32_t)nz << tb);
-                    L = (L & ~(1u << lb)) | ((uint32_t)nz << lb);
-                    bad = bad || b.eof;
-                    if (k == 0) {
-                        y2v = lvv;
-                        y2eob = eob;
-                    } else {
-                        put(k - 1);
-                        nzm |= (uint32_t)nz << (k - 1);
-                    }
-                }
-                lvv = y2v;  // Y2 (parsed first) goes last
-                eob = y2eob;
-                put(24);
-                stv = lane == 25 ? nlv : stv;
-                // header dwords: modes, nzm, I4 modes, the 26 level starts as halfword pairs, pad
-                const int s0 = __shfl(stv, 2 * (lane - 4)), s1 = __shfl(stv, 2 * (lane - 4) + 1);
-                uint32_t hd = (uint32_t)(s0 & 0xffff) | ((uint32_t)s1 << 16);
-                hd = lane == 0 ? mr.x : (lane == 1 ? nzm : (lane == 2 ? mr.z : (lane == 3 ? mr.w : hd)));
-                if (lane < ZW_DREC_HDR / 4) ((uint32_t*)rec)[lane] = lane < 17 ? hd : 0u;
-                const uint32_t bytes = ZW_DREC_HDR + 2u * (uint32_t)nlv, padded = (bytes + 15u) & ~15u;
-                if (lane < 8 && ZW_DREC_HDR + 2u * (uint32_t)(nlv + lane) < padded) lv[nlv + lane] = 0;
-                wsync();
-                const zu4 w = *(const zu4*)(rec + 16 * (lane < 55 ? lane : 0));
-                bst128(w, ro, 16u * (uint32_t)lane < padded ? used + 16u * (uint32_t)lane : ZW_OOB);
-                wsync();
-                used += padded;
-            }
-            if (lane == 0) tcx[mbx] = (uint16_t)T;
+            for (int j = 0; j < 16; j++) P8[(16 * q + j) * 64 + lane] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
         }
     }
-    // a frame that failed stopped early: its remaining MBs get empty records at
-    // the end (offsets = the bytes used), so the reconstruction that still runs
-    // before the host sees the error reads inside the frame's records
-    const uint32_t from = bad ? (uint32_t)rfl(mdone) : (uint32_t)nmb;
-    for (uint32_t j = from + (uint32_t)lane; j <= (uint32_t)nmb; j += 64) bst32(used, rm, j * 4u);
-    if (lane == 0) err[f] = bad ? 1 : 0;
+    __syncthreads();
+    volatile lds_u32* sfill = (volatile lds_u32*)SY;
+    volatile lds_u32* mfill = sfill + 64;
+    volatile lds_u32* scons = sfill + 128;
+    volatile lds_u32* mcons = sfill + 192;
+    volatile lds_u32* done = sfill + 256;
+    if (wv == 1) {
+        // feeder: lane l keeps frame l's stream ring (4 chunks of 16 bytes) and
+        // mode ring (TKL_MRS MBs) full; stream bytes past the partition are 0
+        const uint8_t* src = act ? blob + tf[f].off : blob;
+        const uint32_t len = act ? tf[f].len : 0u, nch = (len + 15u) >> 4;
+        const uint4* mrec = (const uint4*)(modes + (size_t)(act ? f : 0) * nmb * ZW_TOK_MODE);
+        uint32_t sf = 0, mf = 0;
+        while (!*done) {
+            const uint32_t sc = scons[lane], mc = mcons[lane];
+            uint4 s[2], m[8];
+            uint32_t ns = 0, nm = 0;
+            // every load unconditional at a clamped (valid) address, so the ten are in
+            // flight together; the lanes keep what is theirs
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t c = sf + (uint32_t)u;
+                const bool ok = act && c < (sc >> 4) + 4u;
+                const uint4 v = ((const uint4*)src)[c < nch ? c : 0u];
+                s[u] = c < nch ? v : make_uint4(0, 0, 0, 0);
+                ns += ok ? 1u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t k = mf + (uint32_t)u;
+                const bool ok = act && k < nmb && k < mc + (uint32_t)TKL_MRS;
+                m[u] = mrec[k < nmb ? k : 0u];
+                nm += ok ? 1u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if ((uint32_t)u < ns) {
+                    const uint32_t b = ((sf + (uint32_t)u) & 3u) * 4u;
+                    SR[(b + 0) * 64 + lane] = s[u].x;
+                    SR[(b + 1) * 64 + lane] = s[u].y;
+                    SR[(b + 2) * 64 + lane] = s[u].z;
+                    SR[(b + 3) * 64 + lane] = s[u].w;
+                }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if ((uint32_t)u < nm) {
+                    const uint32_t b = ((mf + (uint32_t)u) & (TKL_MRS - 1)) * 4u;
+                    MR[(b + 0) * 64 + lane] = m[u].x;
+                    MR[(b + 1) * 64 + lane] = m[u].y;
+                    MR[(b + 2) * 64 + lane] = m[u].z;
+                    MR[(b + 3) * 64 + lane] = m[u].w;
+                }
+            sf += ns;
+            mf += nm;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // ring data before the fill counters
+            sfill[lane] = sf;
+            mfill[lane] = mf;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
+    // decoder
+    TokDev m;
+    m.P = P;
+    m.TT = TT;
+    m.DS = DS;
+    m.SR = SR;
+    m.MR = MR;
+    m.TCX = TCX;
+    m.sfill = sfill;
+    m.mfill = mfill;
+    m.scons = scons;
+    m.mcons = mcons;
+    {
+        const int f0 = (int)blockIdx.x * 64, nw = nframes - f0 < 64 ? nframes - f0 : 64;
+        m.rr = brsrc(recs + (size_t)f0 * slot, (uint32_t)(nw * slot));
+        m.rbase = (uint32_t)(lane * slot);
+    }
+    m.mo = moff + (size_t)(act ? f : 0) * (nmb + 1);
+    m.lane = m.lane0 = (uint32_t)lane;
+    m.nmb = nmb;
+    m.mbw = (uint32_t)mbw;
+    m.tmo = 0;
+    tokl::Lane L;
+    tokl::init(L, act ? tf[f].len : 0u, act);
 #ifdef ZW_TOK_PROF
-    if (lane == 0 && (f == 0 || f == (int)gridDim.x - 1))
-        printf("[k_dec_tokens] frame %d: %u decisions, %u loads, %llu cycles (%.1f per decision)\n", f, b.ndec, b.nload,
-               (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start),
-               (double)(__builtin_amdgcn_s_memtime() - t_start) / (double)b.ndec);
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    uint32_t ndec = 0, nstep = 0;
+#endif
+#ifdef ZW_TOK_PROF
+    uint64_t c_top = 0, c_step = 0, c_mb = 0, t_a, t_b;
+    uint32_t n_mb = 0;
+#define TKL_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define TKL_STAMP(v)
+#endif
+    for (uint32_t step = 0;; step++) {
+        // every live lane, whatever its phase: then no lane makes more than
+        // ZW_TOKL_TK decisions between two top-ups (step 0 fills the windows)
+        TKL_STAMP(t_a);
+        if (step % ZW_TOKL_TK == 0 && L.phase != tokl::PH_DONE) tokl::topup(L, m);
+        TKL_STAMP(t_b);
+#ifdef ZW_TOK_PROF
+        c_top += t_b - t_a;
+#endif
+        if (L.phase == tokl::PH_DECIDE) {
+#ifdef ZW_TOK_PROF
+            ndec++;
+#endif
+            tokl::step(L, m);
+        }
+        TKL_STAMP(t_a);
+#ifdef ZW_TOK_PROF
+        c_step += t_a - t_b;
+#endif
+        if (step % ZW_TOKL_MK == 0) {
+#ifdef ZW_TOK_PROF
+            n_mb += __builtin_amdgcn_ballot_w64(L.phase == tokl::PH_MB) != 0;
+#endif
+#pragma unroll 1
+            for (int r = 0; r < ZW_TOKL_MBRUN && L.phase == tokl::PH_MB; r++) tokl::mb_phase(L, m);
+        }
+        TKL_STAMP(t_b);
+#ifdef ZW_TOK_PROF
+        c_mb += t_b - t_a;
+#endif
+        if (m.tmo) L.phase = tokl::PH_DONE;
+#ifdef ZW_TOK_PROF
+        nstep++;
+#endif
+        if (__builtin_amdgcn_ballot_w64(L.phase != tokl::PH_DONE) == 0) break;
+    }
+    if (lane == 0) *done = 1u;
+    if (act) {
+        if (L.bad || m.tmo) {
+            // the frame stopped early: its MB and the rest get empty records at the
+            // bytes used, so the reconstruction that still runs before the host
+            // reads err stays inside the frame's records
+            m.st128(L.hb, 0u, 0u, 0u, 0u);
+            m.st128(L.hb + 16u, 0u, 0u, 0u, 0u);
+            m.st128(L.hb + 32u, 0u, 0u, 0u, 0u);
+            m.st128(L.hb + 48u, 0u, 0u, 0u, 0u);
+            m.st128(L.hb + 64u, 0u, 0u, 0u, 0u);
+            for (uint32_t j = L.mbi; j <= nmb; j++) m.mo[j] = L.hb;
+        }
+        err[f] = m.tmo ? 2 : (L.bad ? 1 : 0);
+    }
+#ifdef ZW_TOK_PROF
+    if (f == 0 || f == nframes - 1)
+        printf("[k_dec_tokl] frame %d: %u decisions in %u steps, %llu cycles (%.1f per step: top-up %.1f, step %.1f, "
+               "MB phase %.1f in %u steps)\n",
+               f, ndec, nstep, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start),
+               (double)(__builtin_amdgcn_s_memtime() - t_start) / (double)nstep, (double)c_top / nstep,
+               (double)c_step / nstep, (double)c_mb / nstep, n_mb);
 #endif
 }
 
-// n frames, one wave each.
-extern "C" hipError_t zwk_dec_tokens(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
-                                     const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err,
-                                     int mbw, int mbh, int n)
+extern "C" size_t zw_tokl_lds_bytes(int mbw) { return (size_t)(TKL_FIXED + mbw * 32) * 4; }
+
+extern "C" hipError_t zwk_dec_tokl(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
+                                   const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err, int mbw,
+                                   int mbh, int n)
 {
-    hipLaunchKernelGGL(k_dec_tokens, dim3((n + ZW_TOK_WAVES - 1) / ZW_TOK_WAVES), dim3(64 * ZW_TOK_WAVES), 0, s, blob, tf,
-                       probs, modes, recs, slot, moff, err, mbw, mbh, n);
+    const size_t lds = zw_tokl_lds_bytes(mbw);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k_dec_tokl, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_dec_tokl, dim3((n + 63) / 64), dim3(128), lds, s, blob, tf, probs, modes, recs, slot, moff, err,
+                       mbw, mbh, n);
     return hipGetLastError();
 }

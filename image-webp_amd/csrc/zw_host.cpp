@@ -219,23 +219,26 @@ static int sdma_wait(zw_ctx* c, hsa_signal_t sig)
 }
 
 // Is [p, p + n) page-locked host memory the DMA engines can read (hipHostMalloc
-// or hipHostRegister)?  Such frames go to the engine directly, with no copy
-// through the uploader's staging slot.
-static bool host_pinned(const void* p, size_t n)
+// or hipHostRegister)?  Then the address the agents use for p (the
+// allocation's device pointer at p's offset: for registered memory it need not
+// equal p), and such a frame goes to the engine directly, with no copy through
+// the uploader's staging slot; else nullptr.
+static const void* host_pinned(const void* p, size_t n)
 {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();  // (pageable memory: not an error worth keeping)
-        return false;
+        return nullptr;
     }
-    if (a.type != hipMemoryTypeHost || !a.hostPointer) return false;
-    // the registration must cover the whole frame: its end must resolve too
+    if (a.type != hipMemoryTypeHost || !a.hostPointer || !a.devicePointer) return nullptr;
+    // the registration must cover the whole frame: its end must resolve too, to the same allocation
     hipPointerAttribute_t b;
     if (hipPointerGetAttributes(&b, (const uint8_t*)p + n - 1) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return nullptr;
     }
-    return b.type == hipMemoryTypeHost;
+    if (b.type != hipMemoryTypeHost || b.hostPointer != a.hostPointer) return nullptr;
+    return (const uint8_t*)a.devicePointer + ((const uint8_t*)p - (const uint8_t*)a.hostPointer);
 }
 
 int ctx_d2h_stream(zw_ctx* c, void* dst, const void* src, size_t bytes)
@@ -465,6 +468,9 @@ struct zw_pipe {
 static void pipe_free(zw_pipe* p)
 {
     if (!p) return;
+    // an upload DMA that timed out (the context is poisoned) may still write the
+    // input buffers: they are leaked rather than handed back to the allocator
+    if (p->ctx && p->ctx->poisoned.load(std::memory_order_acquire)) p->d_img = p->d_img2 = nullptr;
     void* ptrs[] = {p->d_img, p->d_img2, p->d_Y, p->d_U, p->d_V, p->d_ry, p->d_ru, p->d_rv, p->d_alpha, p->d_histo,
                     p->d_tmpl, p->d_params, p->d_lcost, p->d_derr, p->d_out1, p->d_out2, p->d_dbg,
                     p->d_eobs, p->d_sizes, p->d_finfo, p->d_pack, p->d_finfo2, p->d_pack2, p->d_stats, p->d_stats_tmp};
@@ -1044,7 +1050,9 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                                 const int sl = k & 1;
                                 if (busy[sl] && (r = sdma_wait(p->ctx, L.usig[2 * u + sl]))) break;
                                 const uint8_t* src = p->host_src[(size_t)b * p->n + ca(c) + i];
-                                if (!host_pinned(src, p->img_stride)) {  // pageable: through the slot
+                                if (const void* dp = host_pinned(src, p->img_stride)) {
+                                    src = (const uint8_t*)dp;
+                                } else {  // pageable: through the slot
                                     memcpy(L.ustage[2 * u + sl], src, p->img_stride);
                                     src = L.ustage[2 * u + sl];
                                 }

@@ -61,7 +61,11 @@ struct zw_ctx {
     hipEvent_t dev_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     hipEvent_t dev_ev1[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
-    float dec_tok_ms = 0.f;  // k_dec_tokens, summed over the batch's chunks
+    float dec_tok_ms = 0.f;  // k_dec_tokl of the last batch (0: the host parsed every frame)
+    // measured rates for the host / device split of the token parse (dec_tok_split):
+    // host chunk parse ms per frame (the whole chunk over all threads), device launch ms
+    // per MB of a frame (the launch runs its frames side by side), 0 = not measured yet
+    double dec_host_ms_per_frame = 0, dec_tok_ms_per_mb = 0;
     // host stages of the last decode batch, wall ms summed over its chunks:
     // [0] parse (bool decoder + records), [1] download, [2] fan-out / copy-out
     double dec_host_ms[3] = {0, 0, 0};

@@ -166,6 +166,7 @@ SIGNATURES = [
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_decode_stage_times", _I, [_VP, _VP]),
     ("zw_decode_token_ms", _I, [_VP, _VP]),
+    ("zw_dbg_tokl_frame", _I, [_VP, _SZ, ctypes.POINTER(_I)]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_encode_host", _I, [_VP, _I, _VP]),
@@ -471,6 +472,18 @@ def decode_token_ms(ctx=None):
     ms = ctypes.c_float()
     _check(c._lib.zw_decode_token_ms(c.handle, ctypes.byref(ms)), "decode_token_ms")
     return float(ms.value)
+
+
+def dbg_tokl_frame(vp8):
+    """Test hook (CPU only): (host parse code, match) for the device token
+    parse's state machine stepped on the host over one VP8 frame; match 1 =
+    records equal to the host parser's (or both failed), 0 = differ, -1 = a
+    frame the device parse does not take."""
+    L = load_library()
+    a = _as_u8(vp8)
+    m = ctypes.c_int(-1)
+    rc = L.zw_dbg_tokl_frame(_ptr(a) if a.size else None, a.size, ctypes.byref(m))
+    return rc, m.value
 
 
 def decode_stage_times(ctx=None):

@@ -215,12 +215,20 @@ int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
  * or images device->host, ms[2] download + fan-out into the output buffers
  * (a chunk's download runs in parts, each fanned out while the next lands). */
 int zw_decode_stage_times(zw_ctx *ctx, float *ms);
-/* Device time of the last decode batch's token parse (k_dec_tokens, summed over
- * chunks; 0 when the host parsed the tokens).  Batches of >= 64 frames with one
- * token partition each parse their tokens on the device (read_coefficients,
- * decoder/vp8.rs:872-1058), the modes and headers on the host; ZW_DEC_TOKENS=
- * host / device forces either. */
+/* Device time of the last decode batch's token parse (k_dec_tokl, one frame per
+ * lane; 0 when the host parsed every frame's tokens).  The device parses the
+ * token partitions (read_coefficients, decoder/vp8.rs:872-1058) of a batch's
+ * later frames while the host parses the earlier chunks; headers and modes stay
+ * on the host.  ZW_DEC_TOKENS=host|device|mixed forces the host, the device or a
+ * split (ZW_DEC_TOKENS_HOST = the host's share); frames with several token
+ * partitions always parse on the host. */
 int zw_decode_token_ms(zw_ctx *ctx, float *ms);
+/* Test hook, host only (no device work): steps the device token parse's
+ * per-lane state machine (k_dec_tokl) over one VP8 frame on the CPU and compares
+ * its packed MB records with the host parser's.  Returns the host parse's code;
+ * *match = 1 (records equal, or both failed), 0 (they differ), -1 (a frame the
+ * device parse never takes: several partitions, or a header / mode error). */
+int zw_dbg_tokl_frame(const uint8_t *vp8, size_t len, int *match);
 /* ... and of its k_yuv2rgb launch (0 when the batch returned planes). */
 int zw_decode_rgb_kernel_ms(zw_ctx *ctx, float *ms);
 
@@ -344,7 +352,12 @@ int zw_pipe_encode_repeat(zw_pipe *p, int n);
  * passes run, so the host->device copies overlap the kernels.  The outputs
  * (zw_pipe_output) are the last batch's.  Not with container output (ZW_EINVAL).
  * Replaces the caller-side loop WebPEncoder::encode(&[u8]) per frame
- * (encoder/api.rs:1291) for a stream of host frames. */
+ * (encoder/api.rs:1291) for a stream of host frames.  Page-locked frames
+ * (hipHostMalloc / hipHostRegister) are read by the DMA engines directly.
+ * After ZW_EDEVICE (a copy that did not complete in time) a DMA engine may
+ * still read the caller's frames: keep them allocated for the process's
+ * lifetime, and destroy the context (its device buffers are then leaked, not
+ * reused). */
 int zw_pipe_encode_host(zw_pipe *p, int nb, const uint8_t *const *frames);
 /* Device-only passes (rgb2yuv, analysis, segments, pass 1, stats, pass 2) without
  * token emission, for kernel timing.  Returns 0 or an error. */

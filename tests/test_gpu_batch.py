@@ -324,3 +324,64 @@ def test_single_colour_files_decode(ctx, n):
     ref = O.yuv_to_rgb_fancy(r["y"].reshape(-1, ys)[:n, :n].reshape(-1), r["u"].reshape(-1, cs)[:c, :c].reshape(-1),
                              r["v"].reshape(-1, cs)[:c, :c].reshape(-1), n, n).reshape(-1, 3)
     assert np.array_equal(rgb, ref)
+
+
+def _hip():
+    import ctypes
+    import ctypes.util
+    name = ctypes.util.find_library("amdhip64") or "libamdhip64.so"
+    h = ctypes.CDLL(name)
+    h.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    h.hipHostFree.argtypes = [ctypes.c_void_p]
+    h.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    h.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    return h
+
+
+@pytest.mark.parametrize("kind", ["hostmalloc", "registered"])
+def test_pipe_encode_host_pinned(ctx, monkeypatch, kind):
+    """zw_pipe_encode_host from page-locked frames, which go to the DMA engines
+    without the staging copy: hipHostMalloc memory (what torch pin_memory
+    gives) and pageable memory registered with hipHostRegister (the engines
+    read it through the allocation's device pointer).  Bitstreams equal the
+    oracle's; every frame sits at an offset inside one allocation."""
+    import ctypes
+    monkeypatch.setenv("ZW_PIPE_LANES", "1")
+    monkeypatch.setenv("ZW_ENC_ROWS", "0")
+    w, h, n, nb = 96, 64, 8, 2
+    fb = w * h * 4
+    hip = _hip()
+    total = nb * n * fb + 4096
+    if kind == "hostmalloc":
+        ptr = ctypes.c_void_p()
+        assert hip.hipHostMalloc(ctypes.byref(ptr), total, 0) == 0
+        base = ptr.value
+        keep = None
+    else:
+        keep = np.zeros(total, np.uint8)
+        base = keep.ctypes.data
+        assert hip.hipHostRegister(ctypes.c_void_p(base), total, 0) == 0
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(base))
+        batches = []
+        for b in range(nb):
+            fr = []
+            for i in range(n):
+                off = 1024 + (b * n + i) * fb  # (not at the allocation's start)
+                a = buf[off:off + fb]
+                a[:] = synth_rgba(w, h, 0x5EED7000 + 16 * b + i, "natural").reshape(-1)
+                fr.append(a)
+            batches.append(fr)
+        p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+        try:
+            p.encode_host(batches)
+            for i in range(n):
+                rc, ref, _ = O.encode(np.array(batches[-1][i]).reshape(h, w, 4), w, h, 3, 75, 4)
+                assert rc == 0 and p.output(i) == ref, f"frame {i}"
+        finally:
+            p.close()
+    finally:
+        if kind == "hostmalloc":
+            hip.hipHostFree(ctypes.c_void_p(base))
+        else:
+            hip.hipHostUnregister(ctypes.c_void_p(base))
