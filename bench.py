@@ -389,6 +389,55 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
     return out
 
 
+def device_tokens_leg(ctx, streams, frames, tags, digests):
+    """Batch decode where the device token parse takes part (k_dec_tokl, one
+    frame per lane): one launch parses a share of the batch's token partitions
+    in ≈250 ms whatever its frame count, so the auto split hands it the frames
+    the host would not finish in that time -- none at 1 024 1080p frames, most
+    of them here.  The same batch with ZW_DEC_TOKENS=host for comparison.
+    Planes of a sample of frames across the host and device shares (every 61st)
+    are hashed against the oracle's decode digests."""
+    import zwebp
+    batch = [streams[i % len(streams)] for i in range(frames)]
+    res = {}
+    vy = [0, 0, 0]
+    for mode in ("host", "auto"):
+        old = os.environ.get("ZW_DEC_TOKENS")
+        if mode == "host":
+            os.environ["ZW_DEC_TOKENS"] = "host"
+        else:
+            os.environ.pop("ZW_DEC_TOKENS", None)
+        try:
+            zwebp.decode_batch(batch[:256], ctx=ctx)  # (warm-up: pool, staging)
+            t0 = time.perf_counter()
+            dec = zwebp.decode_batch(batch, ctx=ctx)
+            el = time.perf_counter() - t0
+            st = zwebp.decode_stage_times(ctx=ctx)
+            res[mode] = {"decodes_per_s": frames / el, "device_token_ms": zwebp.decode_token_ms(ctx=ctx),
+                         "host_parse_ms": st[0], "download_ms": st[1], "fanout_ms": st[2]}
+            if mode == "auto" and tags is not None:
+                for i in range(0, frames, 61):
+                    want = digests.get("dec_yuv/" + tags[i % len(streams)])
+                    if want is None:
+                        vy[2] += 1
+                        continue
+                    hsh = hashlib.sha256()
+                    for a in (dec[i].ybuf, dec[i].ubuf, dec[i].vbuf):
+                        hsh.update(bytes(a))
+                    vy[0 if hsh.hexdigest() == want else 1] += 1
+            del dec
+        finally:
+            if old is None:
+                os.environ.pop("ZW_DEC_TOKENS", None)
+            else:
+                os.environ["ZW_DEC_TOKENS"] = old
+    return {"batch_frames": frames, "auto": res["auto"], "host_only": res["host"],
+            "speedup": res["auto"]["decodes_per_s"] / res["host"]["decodes_per_s"],
+            "verified": vy[1] + vy[2] == 0 and vy[0] > 0,
+            "verification": {"sampled_frames": vy[0] + vy[1] + vy[2], "matched": vy[0], "mismatched": vy[1],
+                             "no_digest": vy[2], "against": "dec_yuv/ oracle digests"}}
+
+
 def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     """SURVEY config 3: the decode path on this GPU.  Host bool decoding + MB
     records up, k_dec_recon (dequant, iWHT/iDCT, prediction) + k_loopfilter,
@@ -430,7 +479,8 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
               "device_token_ms": tok_ms, "token_split": os.environ.get("ZW_DEC_TOKENS", "auto"),
               "note": "wall ms summed over chunks; the parse (the host bool decoder's serial chain, every "
                       "host thread) of chunk c overlaps the download + fan-out of chunk c-1; device_token_ms: "
-                      "k_dec_tokens' launch for the frames whose tokens the device parsed (0: none)"}
+                      "k_dec_tokl's launch for the frames whose tokens the device parsed (0: none; the auto split "
+                      "leaves a batch to the host when the host alone finishes first)"}
     batch = pbatch[:frames]
     vy = [0, 0, 0]  # matched, mismatched, no digest
 
@@ -450,6 +500,7 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
             j = 0 if i == 0 else (i - 1) % len(streams)
             tally(vy, "dec_yuv/" + tags[j], fr.ybuf, fr.ubuf, fr.vbuf)
     del decb, dec1
+    dev_tok = device_tokens_leg(ctx, streams, 16 * frames, tags, digests)
     # kernel throughput: the whole batch as one launch of the per-frame kernels
     env0 = {k: os.environ.get(k) for k in ("ZW_DEC_CHUNK", "ZW_DEC_ROWS")}
     os.environ["ZW_DEC_CHUNK"], os.environ["ZW_DEC_ROWS"] = str(frames), "0"
@@ -470,7 +521,8 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
            "batch_kernel_ms": {"k_dec_recon": rk, "k_loopfilter": lf, "launch": "whole batch, one workgroup per frame"},
            "kernel_frames_per_s": frames / ((rk + lf) * 1e-3),
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                        "alg_bytes_per_mb": 1208}}
+                        "alg_bytes_per_mb": 1208},
+           "device_tokens": dev_tok}
     # decode to packed RGBA (fancy upsampling on the device, k_yuv2rgb) into the
     # caller's reused buffers (decode_rgba_into, api.rs:1004), and into fresh
     # per-frame buffers (decode_rgba's Vec per call: page faults on 8 MB each);
@@ -486,7 +538,8 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
         for i, b in enumerate(bufs):
             tally(vr, "dec_rgba/" + tags[i % len(streams)], b)
     del bufs
-    out["verified"] = tags is not None and vy[1] + vy[2] + vr[1] + vr[2] == 0 and vy[0] > 0 and vr[0] > 0
+    out["verified"] = tags is not None and vy[1] + vy[2] + vr[1] + vr[2] == 0 and vy[0] > 0 and vr[0] > 0 and \
+        dev_tok["verified"]
     out["verification"] = {"yuv": {"matched": vy[0], "mismatched": vy[1], "no_digest": vy[2]},
                            "rgba": {"matched": vr[0], "mismatched": vr[1], "no_digest": vr[2]},
                            "against": "dec_yuv/ and dec_rgba/ oracle digests (decode_frame, fill_rgba fancy)"}
@@ -662,6 +715,63 @@ def container_rgba(pipe, host_imgs, steps, w, h, q, m, seeds, digests):
             "verification": {"files_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss,
                              "against": "riff/... oracle digests (RIFF + VP8X + ALPH + VP8)"},
             "note": "RIFF + VP8X + ALPH + VP8 per frame; inputs resident in HBM, alpha planes read from host memory"}
+
+
+def container_alpha(ctx, w, h, q, m, frames, steps, seeds, digests):
+    """The container leg on frames with a real alpha plane (synth_rgba kind
+    "alpha": a cut-out with a soft noisy edge and a ramp band; the headline's
+    frames have alpha = 255, whose ALPH chunk is ~0.9 KB): every emission
+    thread codes each frame's ALPH (encode_alpha_lossless, api.rs:1175-1221)
+    beside its VP8 tokens.  Own `frames`-frame pipe, device-resident input;
+    whole RIFF files hashed against the oracle's riffa/ digests.  alph_ms_per_frame
+    times zw_encode_alpha alone on one host thread."""
+    import struct
+    import zwebp
+    from zwebp.synth import synth_rgba
+    imgs = [synth_rgba(w, h, sd, "alpha") for sd in seeds]
+    p = zwebp.Pipeline(frames, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    try:
+        for i in range(frames):
+            p.upload(i, imgs[i % len(imgs)])
+        p.set_container([imgs[i % len(imgs)] for i in range(frames)])
+        p.encode_repeat(1)
+        t0 = time.perf_counter()
+        p.encode_repeat(steps)
+        el = time.perf_counter() - t0
+        k = p.kernel_times()
+        ok = bad = miss = 0
+        alph_bytes = 0
+        for i in range(frames):
+            c = p.output(i)
+            if i == 0:
+                off = 12
+                while off + 8 <= len(c):
+                    tag, ln = c[off:off + 4], struct.unpack("<I", c[off + 4:off + 8])[0]
+                    if tag == b"ALPH":
+                        alph_bytes = ln
+                    off += 8 + ln + (ln & 1)
+            want = digests.get(f"riffa/{w}x{h}/q{q}m{m}/{seeds[i % len(seeds)]:#010x}")
+            if want is None:
+                miss += 1
+            elif hashlib.sha256(c).hexdigest() == want:
+                ok += 1
+            else:
+                bad += 1
+    finally:
+        p.close()
+    zwebp.encode_alpha(imgs[0], w, h, zwebp.ColorType.Rgba8)
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        zwebp.encode_alpha(imgs[0], w, h, zwebp.ColorType.Rgba8)
+    alph_ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"encodes_per_s": frames * steps / el, "frames": frames * steps, "ms_per_batch": el / steps * 1e3,
+            "host_emit_ms_per_batch": float(k[7]), "alph_bytes_frame0": alph_bytes, "alph_ms_per_frame": alph_ms,
+            "verified": bad == 0 and miss == 0 and ok == frames,
+            "verification": {"files_checked": ok + bad + miss, "matched": ok, "mismatched": bad, "no_digest": miss,
+                             "against": "riffa/... oracle digests (RIFF + VP8X + ALPH + VP8)"},
+            "note": "RGBA frames with a cut-out alpha plane (synth_rgba kind 'alpha'); emission threads code VP8 tokens "
+                    "and the ALPH chunk per frame"}
 
 
 def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0):
@@ -953,6 +1063,7 @@ def main():
             line["single_frame"] = single_frame(ctx, imgs[0], w, h, q, m, seeds[0], digests)
             streams = [bytes(pipes[0][0].output(i)) for i in range(min(B, D))]  # VP8 frames, before container mode
             line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, q, m, seeds, digests)
+            line["container_rgba"]["real_alpha"] = container_alpha(ctx, w, h, q, m, 256, 3, seeds, digests)
             line["host_resident"] = host_resident(pipes[0][0], imgs, 3, w, h, q, m, seeds, digests)
             line["seam_threads"] = seam_threads()
             line["decode_path"] = decode_path(ctx, streams, 256, w, h, not a.no_cpu_baseline, tags, digests)
@@ -988,6 +1099,7 @@ def main():
                 "3_1080p_decode_path": {"verified": line["decode_path"]["verified"], "see": "decode_path"},
                 "4_1080p_batch_encode": {"verified": line["verified"] and line["single_frame"]["verified"] and
                                          line["container_rgba"]["verified"] and line["host_resident"]["verified"]
+                                         and line["container_rgba"]["real_alpha"]["verified"]
                                          and line["seam_threads"]["verified"],
                                          "see": "value, single_frame, container_rgba, host_resident, seam_threads"},
                 "5_4k_batch_n1": {"verified": line["config5_4k_n1"]["verified"], "see": "config5_4k_n1 (N=1 anchor "

@@ -2,7 +2,10 @@
 
 synth_rgba(w, h, seed): per-channel gradient + 8x8 checker (amplitude 32) +
 approximately Gaussian noise (sigma ~6, Irwin-Hall of 4 hashed uniforms),
-alpha = 255.  Counter-based hashing (PCG-style output permutation of the
+alpha = 255.  kind="alpha": the same colours with a real alpha plane, a
+cut-out: transparent background, an opaque disc with a soft 32-pixel edge
+carrying noise (sigma ~6), and a smooth ramp across the top eighth -- the
+content encode_alpha_lossless codes for a product shot or a sticker.  Counter-based hashing (PCG-style output permutation of the
 pixel index mixed with the seed) so any frame can be generated independently,
 vectorised with numpy.  Seed convention from BASELINE.md: 0x5EED0000 + index.
 """
@@ -48,5 +51,21 @@ def synth_rgba(w, h, seed=0x5EED0000, kind="natural"):
         # sum of 4 U(0,65535): mean 131070, sd ~37837 -> scale to sigma 6
         noise = ((acc - 131070) * 6) // 37837
         out[..., c] = np.clip(grads[c] + checker + noise, 0, 255).astype(np.uint8)
-    out[..., 3] = 255
+    out[..., 3] = 255 if kind != "alpha" else _alpha_plane(w, h, base, yy, xx, idx)
     return out
+
+
+def _alpha_plane(w, h, base, yy, xx, idx):
+    # a cut-out: transparent background, an opaque disc whose 32-pixel soft edge
+    # carries noise (sigma ~6), and a smooth horizontal ramp across the top eighth
+    cy, cx, r = h / 2.0, w / 2.0, 0.35 * min(w, h)
+    d = np.sqrt((yy - cy) ** 2 + (xx - cx) ** 2)
+    a = np.clip((r + 16 - d) * (255.0 / 32.0), 0, 255).astype(np.int64)
+    acc = np.zeros((h, w), np.int64)
+    for k in range(4):
+        acc += (_hash32(base + idx + np.uint64(3) + np.uint64((k + 8) << 20)) & np.uint64(0xFFFF)).astype(np.int64)
+    noise = ((acc - 131070) * 6) // 37837
+    a = np.where((a > 0) & (a < 255), a + noise, a)
+    top = yy * 8 < h
+    a = np.where(top, (xx * 255) // max(w - 1, 1), a)
+    return np.clip(a, 0, 255).astype(np.uint8)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Device token parse (k_dec_tokens) against the host parse: the same batch
+"""Device token parse (k_dec_tokl) against the host parse: the same batch
 decoded with ZW_DEC_TOKENS=host and =device must give identical planes; prints
 both wall times, the token kernel time and the per-stage breakdown.
 usage: python tools/dec_tokens.py [frames] [reps]"""

@@ -11,6 +11,7 @@ Keys (synth_rgba natural frames, RGBA8, Q75 method 4; seed = frame_seed(i)):
       768x512   (config 1): frame_seed(i)
   p8/1920x1080/q75m4/seed   the same frame with 8 token partitions (single_frame leg)
   riff/1920x1080/q75m4/seed RIFF + VP8X + ALPH + VP8 (WebPEncoder::encode of the RGBA frame)
+  riffa/1920x1080/q75m4/seed the same for synth_rgba(..., kind="alpha") frames (a real alpha plane)
   dec_yuv/1920x1080/q75m4/seed   Y || U || V (MB-padded) of decode_frame of the VP8 frame
   dec_rgba/1920x1080/q75m4/seed  fill_rgba (fancy upsampling) of that decode
   xmb/1920x1080/q75m4/seed  levels || ry || ru || rv of the streaming DCT+quant pass
@@ -39,7 +40,8 @@ OUT = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
 JOBS = [("vp8", 1920, 1080, k * 256 + i) for k in range(32) for i in range(4)] + \
        [("vp8", 3840, 2160, k * 512 + i) for k in range(8) for i in range(4)] + \
        [("vp8", 768, 512, i) for i in range(4)] + \
-       [("full", 1920, 1080, i) for i in range(4)]
+       [("full", 1920, 1080, i) for i in range(4)] + \
+       [("riffa", 1920, 1080, i) for i in range(4)]
 
 
 def sha(*arrs):
@@ -64,7 +66,14 @@ def one(job):
     kind, w, h, idx = job
     seed = frame_seed(idx)
     tag = f"{w}x{h}/q75m4/{seed:#010x}"
-    img = synth_rgba(w, h, seed)
+    img = synth_rgba(w, h, seed, "alpha" if kind == "riffa" else "natural")
+    if kind == "riffa":
+        rc, bs, _ = O.encode(img, w, h, 3, 75, 4)
+        assert rc == 0
+        rc, alph = O.encode_alpha(img, w, h, 3)
+        assert rc == 0
+        riff = riff_rgba(w, h, bs, alph)
+        return [("riffa/" + tag, sha(riff), len(riff)), ("riffa_alph/" + tag, "", len(alph))]
     if kind == "vp8":
         rc, bs, _ = O.encode(img, w, h, 3, 75, 4)
         assert rc == 0
@@ -99,11 +108,21 @@ def one(job):
 
 
 def main():
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None  # e.g. "riffa": add those kinds to the file
+    jobs = [j for j in JOBS if only is None or j[0] in only]
     with ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
-        res = [r for rs in ex.map(one, JOBS) for r in rs]
+        res = [r for rs in ex.map(one, jobs) for r in rs]
+    if only is not None:
+        old = json.load(open(OUT))
+        old["digests"].update({k: v for k, v, _ in res if v})
+        old["bytes"].update({k: n for k, _, n in res if n})
+        with open(OUT, "w") as f:
+            json.dump(old, f, indent=0, sort_keys=True)
+        print(f"{len(res)} digests added -> {OUT}")
+        return
     d = {"generator": "tools/make_bench_digests.py (oracle/ C restatement of the reference encoder)",
          "key": "see tools/make_bench_digests.py: kind/WxH/qQmM/seed -> sha256 of the oracle's output",
-         "digests": {k: v for k, v, _ in res}, "bytes": {k: n for k, _, n in res if n}}
+         "digests": {k: v for k, v, _ in res if v}, "bytes": {k: n for k, _, n in res if n}}
     with open(OUT, "w") as f:
         json.dump(d, f, indent=0, sort_keys=True)
     print(f"{len(res)} digests -> {OUT}")
