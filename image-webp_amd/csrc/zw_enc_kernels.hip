@@ -2600,6 +2600,24 @@ template <int PASS> struct RowsShape {
     static constexpr int NW = PASS == 1 ? ChainShape<true>::NCH : 1;
 };
 
+// Bytes of the frame-wide row arrays a workgroup keeps in LDS: top_y, top_u,
+// top_v, top_c, top_derr.  The batch kernels (one workgroup per frame) keep all
+// of them; in the row-parallel kernels the luma waves work from per-MB windows
+// of the global row state, and only pass 1's chroma chain keeps top_u / top_v /
+// top_derr, so their LDS no longer grows with the width (which is what bounded
+// the encodable width: 1 568 MBs with the batch shapes, any u16 width here).
+struct TopLds {
+    size_t y, u, v, c, d;
+    __host__ __device__ TopLds(int mbw, bool rows, int pass)
+    {
+        const bool all = !rows, chain = rows && pass == 1;
+        y = all ? (((size_t)mbw * 16 + 48 + 15) & ~(size_t)15) : 0;
+        u = v = all || chain ? (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15) : 0;
+        c = all ? (((size_t)mbw * 12 + 15) & ~(size_t)15) : 0;
+        d = all || chain ? (((size_t)mbw * 4 + 15) & ~(size_t)15) : 0;
+    }
+};
+
 template <int PASS, bool ROWS>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
 {
@@ -2625,14 +2643,15 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     int* xch = (int*)(smem + off);  // two-wave chroma chain: [plane][2][12] exchange words, then 2 flags
     int* xflag = xch + 48;
     off += 256;
+    const TopLds TS(mbw, ROWS, PASS);
     uint8_t* top_y = smem + off;
-    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
+    off += TS.y;
     uint8_t* top_u = smem + off;
-    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    off += TS.u;
     uint8_t* top_v = smem + off;
-    off += ((size_t)mbw * 8 + 48 + 15) & ~(size_t)15;
+    off += TS.v;
     uint8_t* top_c = smem + off;  // [mbw][12]: y2, y[4], u[2], v[2]
-    off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
+    off += TS.c;
     int8_t* top_derr = (int8_t*)(smem + off);  // [mbw][4]
     WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
     // row-parallel: is this workgroup pass 1's chroma chain (it keeps the
@@ -2657,12 +2676,14 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     for (int i = threadIdx.x; i < 256; i += WG) seg_lut[i] = P->seg_enabled ? P->seg_map_lut[i] : 0;
     load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
     if (!ROWS || chain_wg) {
-        for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
+        if (!ROWS) {
+            for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
+            for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
+        }
         for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
             top_u[i] = 127;
             top_v[i] = 127;
         }
-        for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
         for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     }
     if (threadIdx.x < NW) progress[threadIdx.x] = -1;
@@ -3222,7 +3243,7 @@ extern "C" hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const u
     return hipGetLastError();
 }
 
-static size_t encode_lds_bytes(int mbw, int nw)
+static size_t encode_lds_bytes(int mbw, int nw, bool rows, int pass)
 {
     size_t off = 0;
     off += (sizeof(LdsTables) + 15) & ~(size_t)15;
@@ -3231,11 +3252,8 @@ static size_t encode_lds_bytes(int mbw, int nw)
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * nw;
     off += 64;
     off += 256;
-    off += ((size_t)mbw * 16 + 48 + 15) & ~(size_t)15;
-    off += 2 * (((size_t)mbw * 8 + 48 + 15) & ~(size_t)15);
-    off += ((size_t)mbw * 12 + 15) & ~(size_t)15;
-    off += (size_t)mbw * 4;
-    return off;
+    const TopLds t(mbw, rows, pass);
+    return off + t.y + t.u + t.v + t.c + t.d;
 }
 
 
@@ -3282,18 +3300,20 @@ extern "C" hipError_t zwk_segments(hipStream_t s, uint32_t* histo, const ZwFrame
     return hipGetLastError();
 }
 
-// The widest frame (in MBs) whose per-frame LDS arrays (top rows, contexts)
-// fit the 160 KiB of a CU in every encode kernel shape.  encode_frame_lossy
-// takes any u16 width (vp8.rs:3143-3148); wider frames than this return
-// ZW_EINVALID_DIMENSIONS (boundary).
-extern "C" int zwk_encode_max_mbw(void)
+// The widest frame (in MBs) whose LDS fits the 160 KiB of a CU in the batch
+// shapes (rows = false: every row array of the frame in LDS) or in the
+// row-parallel shapes (rows = true: only pass 1's chroma chain keeps rows).
+// encode_frame_lossy takes any u16 width (vp8.rs:3143-3148): 4 096 MBs, which
+// the row-parallel kernels hold; wider frames than the batch shapes take go to them.
+extern "C" int zwk_encode_max_mbw(int rows)
 {
-    const int nws[4] = {PassShape<1>::NW, PassShape<2>::NW, RowsShape<1>::NW, 1};
     int lo = 1, hi = 65536 / 16;
     while (lo < hi) {
         const int mid = (lo + hi + 1) / 2;
-        bool ok = true;
-        for (int i = 0; i < 4; i++) ok = ok && encode_lds_bytes(mid, nws[i]) <= 160 * 1024;
+        const bool ok = rows ? encode_lds_bytes(mid, RowsShape<1>::NW, true, 1) <= 160 * 1024 &&
+                                   encode_lds_bytes(mid, RowsShape<2>::NW, true, 2) <= 160 * 1024
+                             : encode_lds_bytes(mid, PassShape<1>::NW, false, 1) <= 160 * 1024 &&
+                                   encode_lds_bytes(mid, PassShape<2>::NW, false, 2) <= 160 * 1024;
         if (ok) lo = mid;
         else hi = mid - 1;
     }
@@ -3332,13 +3352,14 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
         if (pass == 1) {
             constexpr int nw = RowsShape<1>::NW;
             hipLaunchKernelGGL(k_encode_rows_pass1, dim3(1 + (mbh + nw - 1) / nw, nframes), dim3(64 * nw),
-                               encode_lds_bytes(mbw, nw), s, a);
+                               encode_lds_bytes(mbw, nw, true, 1), s, a);
         } else {
-            hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), encode_lds_bytes(mbw, 1), s, a);
+            hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), encode_lds_bytes(mbw, 1, true, 2), s,
+                               a);
         }
         return hipGetLastError();
     }
-    const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW);
+    const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW, false, pass);
     if (pass == 1) hipLaunchKernelGGL(k_encode_pass1, dim3(nframes), dim3(PassShape<1>::WG), lds, s, a);
     else hipLaunchKernelGGL(k_encode_pass2, dim3(nframes), dim3(PassShape<2>::WG), lds, s, a);
     return hipGetLastError();

@@ -53,7 +53,7 @@ hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* 
                       ZwMbOut* out, uint8_t* ry, uint8_t* ru, uint8_t* rv, size_t ysz, size_t csz, int mbw, int mbh,
                       int nframes, int* dbg, uint8_t* rows, uint32_t* sizes = nullptr);
 size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
-int zwk_encode_max_mbw(void);
+int zwk_encode_max_mbw(int rows);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -543,8 +543,10 @@ static int pipe_chunk_for(int lane_frames, int device)
 // Row-parallel encode kernels (one wave per MB row, spread over the CUs) for
 // chunks too small to fill the device with one 12-wave workgroup per frame.
 // ZW_ENC_ROWS=0/1 forces either shape.
-static bool pipe_rows_for(int chunk, int mbh, int device)
+static bool pipe_rows_for(int chunk, int mbw, int mbh, int device)
 {
+    static const int batch_max_mbw = zwk_encode_max_mbw(0);
+    if (mbw > batch_max_mbw) return true;  // the batch shapes cannot hold the frame's rows in LDS
     const char* e = getenv("ZW_ENC_ROWS");
     if (e && *e) return atoi(e) != 0;
     hipDeviceProp_t prop;
@@ -556,13 +558,13 @@ static bool pipe_rows_for(int chunk, int mbh, int device)
 
 // encode_frame_lossy's dimension rule (vp8.rs:3143-3148): any u16, the header
 // keeping the low 14 bits (vp8.rs:326-327; zwh::emit_frame does the same).
-// Zero is refused (the reference has no meaningful zero-MB frame), and so is a
-// width whose per-frame LDS rows exceed a CU (zwk_encode_max_mbw MBs, about
-// 27 000 pixels): the one divergence, documented in INTEGRATION.md.
+// Zero is refused (the reference has no meaningful zero-MB frame).  Frames
+// wider than the batch kernels' LDS takes (zwk_encode_max_mbw(0), 1 568 MBs)
+// run the row-parallel kernels, whose LDS holds any u16 width.
 static bool encode_dims_ok(uint32_t width, uint32_t height)
 {
     if (width == 0 || height == 0 || width > 65535 || height > 65535) return false;
-    static const int max_mbw = zwk_encode_max_mbw();
+    static const int max_mbw = zwk_encode_max_mbw(1);
     return (int)((width + 15) / 16) <= max_mbw;
 }
 
@@ -635,7 +637,7 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
              hipStreamCreateWithFlags(&L.stream2, hipStreamNonBlocking) == hipSuccess &&
              hipMalloc(&L.d_ctr, 2 * (size_t)nch * ZW_PACK_CTR_WORDS * sizeof(unsigned long long)) == hipSuccess &&
              hipMemset(L.d_ctr, 0, 2 * (size_t)nch * ZW_PACK_CTR_WORDS * sizeof(unsigned long long)) == hipSuccess;
-        if (ok && pipe_rows_for(L.chunk, p->mbh, ctx->device)) {
+        if (ok && pipe_rows_for(L.chunk, p->mbw, p->mbh, ctx->device)) {
             const size_t rb = zwk_encode_rows_bytes(p->mbw, p->mbh, L.chunk);
             ok = hipMalloc(&L.d_rows, rb) == hipSuccess && hipMemset(L.d_rows, 0, rb) == hipSuccess;
             // test hook (ZW_ENC_FORCE_ERROR=1): pre-set the launch error word, as a

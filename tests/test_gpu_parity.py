@@ -289,15 +289,18 @@ def test_encode_beyond_14bit_dims(ctx, w, h):
     assert int.from_bytes(out[6:8], "little") == w & 0x3FFF and int.from_bytes(out[8:10], "little") == h & 0x3FFF
 
 
-def test_encode_width_beyond_lds_is_refused(ctx):
-    """The documented divergence: wider than 1568 MBs the
-    product returns InvalidDimensions where the reference would encode."""
-    w, h = 25089, 1
-    img = np.zeros(w * h * 3, np.uint8)
-    with pytest.raises(zwebp.EncodingError) as e:
-        zwebp.encode_frame_lossy(img, w, h, 2, 75, 4, ctx=ctx)
-    assert e.value.code == 1
-    assert O.encode(img, w, h, 2, 75, 4)[0] == 0
+@pytest.mark.parametrize("w,h", [(25089, 1), (25600, 16), (65535, 16), (40000, 33)])
+def test_encode_wide_frames(ctx, w, h):
+    """encode_frame_lossy takes any u16 width (vp8.rs:3143-3148).  Frames wider
+    than the batch kernels' LDS holds (1 568 MBs) run the row-parallel kernels,
+    whose LDS no longer grows with the width: the bitstream equals the oracle's
+    (the header keeps the low 14 bits of the width, vp8.rs:326-327).  A width of
+    65 536 is not a u16: InvalidDimensions, as the reference's try_into."""
+    img = np.ascontiguousarray(synth_rgba(w, h, 0x5EED7700 + w, "natural")[..., :3])
+    rc, ref, _ = O.encode(img, w, h, 2, 75, 4)
+    assert rc == 0
+    got = zwebp.encode_frame_lossy(img, w, h, 2, 75, 4, ctx=ctx)
+    assert bytes(got) == bytes(ref)
     with pytest.raises(zwebp.EncodingError) as e:
         zwebp.encode_frame_lossy(np.zeros(65536 * 3, np.uint8), 65536, 1, 2, 75, 4, ctx=ctx)
     assert e.value.code == 1
