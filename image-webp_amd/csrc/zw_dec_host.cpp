@@ -963,7 +963,7 @@ static int dec_tok_split(zw_ctx* ctx, int n, int C, size_t nmb)
 }
 
 // Parses the headers and modes of frames [h0, n), stages them and launches
-// k_dec_tokens on the context's token stream.  Returns false (and leaves the
+// k_dec_tokl on the context's token stream.  Returns false (and leaves the
 // frames to the host chunks, which then report any error in frame order) when
 // a frame has several token partitions, another size, or a header / mode error.
 static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int h0, DecTok& T)
@@ -1057,7 +1057,7 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     return true;
 }
 
-// A chunk of device frames [first, first + cnt): no host parse; its records are k_dec_tokens'.
+// A chunk of device frames [first, first + cnt): no host parse; its records are k_dec_tokl'.
 static void dec_parse_dev(const DecTok& T, int first, int cnt, DecBatch& B)
 {
     const int j0 = first - T.h0;
@@ -1158,9 +1158,44 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     return err;
 }
 
+// A batch's frames in runs of one size: each run decodes as a batch of its own
+// (the device buffers and the packed images of a run are per size), in frame
+// order, so the first failing frame's error is the one returned, as a sequence
+// of decode_frame calls (decoder/vp8.rs:1526) would report it.  Returns the
+// end of the run starting at i0 (frames too short for dimensions stand alone).
+static int dec_run_end(int n, const uint8_t* const* data, const size_t* lens, int i0)
+{
+    auto key = [&](int i) -> uint32_t {
+        if (!data[i] || lens[i] < 10) return 0xffffffffu;
+        const uint8_t* d = data[i];
+        return (uint32_t)((d[6] | (d[7] << 8)) & 0x3fff) | ((uint32_t)((d[8] | (d[9] << 8)) & 0x3fff) << 16);
+    };
+    const uint32_t k0 = key(i0);
+    int i1 = i0 + 1;
+    if (k0 != 0xffffffffu)
+        while (i1 < n && key(i1) == k0) i1++;
+    return i1;
+}
+
+static int dec_batch_one(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs);
+
 extern "C" int zw_vp8_decode_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
 {
     if (!ctx || n <= 0 || !data || !lens || !outs) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
+    for (int i0 = 0; i0 < n;) {
+        const int i1 = dec_run_end(n, data, lens, i0);
+        if (const int r = dec_batch_one(ctx, i1 - i0, data + i0, lens + i0, outs + i0)) {
+            for (int k = 0; k < i0; k++) zw_frame_free(&outs[k]);
+            return r;
+        }
+        i0 = i1;
+    }
+    return ZW_OK;
+}
+
+static int dec_batch_one(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, zw_frame* outs)
+{
     for (int i = 0; i < n; i++) memset(&outs[i], 0, sizeof(zw_frame));
     int mbw0 = -1, mbh0 = -1;
     auto enqueue = [&](DecBatch& B, int, int) -> int {
@@ -1344,16 +1379,34 @@ static int dec_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const s
 extern "C" int zw_vp8_decode_rgb_batch(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int bpp,
                                        int upsampling, zw_bytes* outs, uint32_t* widths, uint32_t* heights)
 {
-    if (!outs) return ZW_EINVAL;
-    return dec_rgb_batch(ctx, n, data, lens, bpp, upsampling, outs, nullptr, nullptr, 0, widths, heights);
+    if (!outs || n <= 0 || !data || !lens) return ZW_EINVAL;
+    for (int i = 0; i < n; i++) outs[i].data = nullptr, outs[i].len = 0;
+    for (int i0 = 0; i0 < n;) {  // runs of one size (dec_run_end)
+        const int i1 = dec_run_end(n, data, lens, i0);
+        if (const int r = dec_rgb_batch(ctx, i1 - i0, data + i0, lens + i0, bpp, upsampling, outs + i0, nullptr,
+                                        nullptr, 0, widths ? widths + i0 : nullptr, heights ? heights + i0 : nullptr)) {
+            for (int k = 0; k < i0; k++) zw_bytes_free(&outs[k]);
+            return r;
+        }
+        i0 = i1;
+    }
+    return ZW_OK;
 }
 
 extern "C" int zw_vp8_decode_rgb_batch_into(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens,
                                             int bpp, int upsampling, uint8_t* const* outs, const size_t* out_lens,
                                             uint32_t stride_bytes, uint32_t* widths, uint32_t* heights)
 {
-    if (!outs) return ZW_EINVAL;
-    return dec_rgb_batch(ctx, n, data, lens, bpp, upsampling, nullptr, outs, out_lens, stride_bytes, widths, heights);
+    if (!outs || n <= 0 || !data || !lens || !out_lens) return ZW_EINVAL;
+    for (int i0 = 0; i0 < n;) {  // runs of one size (dec_run_end)
+        const int i1 = dec_run_end(n, data, lens, i0);
+        if (const int r = dec_rgb_batch(ctx, i1 - i0, data + i0, lens + i0, bpp, upsampling, nullptr, outs + i0,
+                                        out_lens + i0, stride_bytes, widths ? widths + i0 : nullptr,
+                                        heights ? heights + i0 : nullptr))
+            return r;
+        i0 = i1;
+    }
+    return ZW_OK;
 }
 
 extern "C" int zw_vp8_decode_rgb(zw_ctx* ctx, const uint8_t* vp8, size_t len, int bpp, int upsampling, zw_bytes* out,

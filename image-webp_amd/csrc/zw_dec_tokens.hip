@@ -142,8 +142,7 @@ struct TokDev {
 #endif
 
 // One workgroup = a decoder wave (64 frames, lane l = frame blockIdx.x * 64 + l)
-// and a feeder wave.  Same arguments and outputs as k_dec_tokens, except
-// probs: tokl::PROBS bytes per frame in [type][band][ctx][node] order.  err[f]:
+// and a feeder wave.  probs: tokl::PROBS bytes per frame in [type][band][ctx][node] order.  err[f]:
 // 1 = the partition ran out (ZW_EBITSTREAM), 2 = a bounded wait gave up.
 extern "C" __global__ __launch_bounds__(128) void k_dec_tokl(const uint8_t* __restrict__ blob,
                                                             const ZwTokFrame* __restrict__ tf,

@@ -25,7 +25,7 @@ struct zw_ctx {
     void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
     void* dscratch2 = nullptr;  // decode batches: the device token parse's upload and records
     size_t dscratch2_cap = 0;
-    hipStream_t tok_ = nullptr;  // k_dec_tokens (runs beside the chunks' kernels), created on first use
+    hipStream_t tok_ = nullptr;  // k_dec_tokl (runs beside the chunks' kernels), created on first use
     hipEvent_t tok_ev[2] = {nullptr, nullptr};
     // zw_transform_quant_mbs*_device: the I4 queue of k_xform_mb / k_xform_mb_i4,
     // one per launch stream (launches on different streams may overlap; launches
@@ -57,7 +57,7 @@ struct zw_ctx {
     size_t hpin_cap[5] = {0, 0, 0, 0, 0};
     // device time of the last decode batch: [0] k_dec_recon, [1] k_loopfilter,
     // [2] k_yuv2rgb (0 when the batch returned planes) (ms)
-    // ([4], [5]: around k_dec_tokens when the device parses the tokens)
+    // ([4], [5]: around k_dec_tokl when the device parses the tokens)
     hipEvent_t dev_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     hipEvent_t dev_ev1[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};

@@ -466,7 +466,7 @@ def decode_kernel_times(ctx=None):
 
 
 def decode_token_ms(ctx=None):
-    """Device ms of the last decode batch's token parse (k_dec_tokens; 0 when
+    """Device ms of the last decode batch's token parse (k_dec_tokl; 0 when
     the host parsed the tokens)."""
     c = _ctx(ctx)
     ms = ctypes.c_float()
@@ -524,7 +524,7 @@ def vp8_decode_rgb(data, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
 
 
 def decode_rgb_batch(frames, bpp=3, upsampling=UpsamplingMethod.Bilinear, ctx=None):
-    """vp8_decode_rgb over frames of identical dimensions, one device pass."""
+    """vp8_decode_rgb over a batch (runs of frames of one size, one device pass each)."""
     c = _ctx(ctx)
     L = c._lib
     arrs = [_as_u8(d) for d in frames]

@@ -177,7 +177,9 @@ int zw_encode_webp_batch(zw_ctx *ctx, int n, const zw_image *imgs, uint8_t quali
 
 /* Vp8Decoder::decode_frame */
 int zw_vp8_decode_frame(zw_ctx *ctx, const uint8_t *vp8, size_t len, zw_frame *out);
-/* n independent decode_frame calls on frames of identical dimensions (new: batch). */
+/* n independent decode_frame calls (new: batch).  Frames may differ in size:
+ * each run of consecutive frames of one size decodes as a batch of its own, in
+ * order; the first failing frame's error is returned (no outputs are kept). */
 int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, zw_frame *outs);
 /* decode_frame + Frame::fill_rgb (bpp 3) / fill_rgba (bpp 4, alpha 255 as
  * decode_rgba) (decoder/vp8.rs:200-258, yuv.rs:82 / :402) on the device: the
@@ -185,7 +187,8 @@ int zw_vp8_decode_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const si
  * upsampling: ZW_UPSAMPLE_BILINEAR (fancy) or ZW_UPSAMPLE_SIMPLE. */
 int zw_vp8_decode_rgb(zw_ctx *ctx, const uint8_t *vp8, size_t len, int bpp, int upsampling, zw_bytes *out,
                       uint32_t *width, uint32_t *height);
-/* n frames of identical dimensions (new: batch); widths/heights may be NULL. */
+/* n frames (new: batch; runs of one size as zw_vp8_decode_batch); widths /
+ * heights may be NULL. */
 int zw_vp8_decode_rgb_batch(zw_ctx *ctx, int n, const uint8_t *const *data, const size_t *lens, int bpp,
                             int upsampling, zw_bytes *outs, uint32_t *widths, uint32_t *heights);
 /* The same into the caller's buffers (decode_rgba_into / decode_rgb_into,

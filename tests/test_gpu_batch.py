@@ -385,3 +385,37 @@ def test_pipe_encode_host_pinned(ctx, monkeypatch, kind):
             hip.hipHostFree(ctypes.c_void_p(base))
         else:
             hip.hipHostUnregister(ctypes.c_void_p(base))
+
+
+def test_decode_batch_mixed_sizes(ctx):
+    """Frames of several sizes in one batch decode as runs of one size, each
+    equal to the oracle's decode_frame (decoder/vp8.rs:1526), as a sequence of
+    decode_frame calls would; RGBA batches (fresh and caller buffers) likewise.
+    A damaged frame mid-batch fails the call with the oracle's variant."""
+    sizes = [(64, 48), (64, 48), (96, 80), (33, 17), (33, 17), (33, 17), (64, 48)]
+    streams = []
+    for k, (w, h) in enumerate(sizes):
+        rc, s, _ = O.encode(synth_rgba(w, h, 0x5EED7800 + k, "natural"), w, h, 3, 60 + k, 4)
+        assert rc == 0
+        streams.append(s)
+    frames = zwebp.decode_batch(streams, ctx=ctx)
+    for s, fr in zip(streams, frames):
+        rc, r = O.decode(s)
+        assert rc == 0
+        assert np.array_equal(fr.ybuf, r["y"]) and np.array_equal(fr.ubuf, r["u"]) and np.array_equal(fr.vbuf, r["v"])
+    imgs = zwebp.decode_rgb_batch(streams, 4, zwebp.UpsamplingMethod.Bilinear, ctx=ctx)
+    stride = 4 * max(w for w, _ in sizes)  # (one row stride for every caller buffer)
+    bufs = [np.zeros(stride * h, np.uint8) for (w, h) in sizes]
+    zwebp.decode_rgb_batch_into(streams, bufs, 4, zwebp.UpsamplingMethod.Bilinear, stride_bytes=stride, ctx=ctx)
+    for (w, h), s, im, b in zip(sizes, streams, imgs, bufs):
+        rc, r = O.decode(s)
+        want = np.asarray(O.yuv_to_rgb_fancy(r["y"], r["u"], r["v"], w, h, 4)).reshape(h, w * 4)
+        assert bytes(im) == want.tobytes()
+        assert np.array_equal(b.reshape(h, stride)[:, :w * 4], want)
+    bad = list(streams)
+    bad[3] = bad[3][:40]
+    rc, _ = O.decode(bad[3])
+    assert rc != 0
+    with pytest.raises(zwebp.DecodingError) as e:
+        zwebp.decode_batch(bad, ctx=ctx)
+    assert e.value.code == rc
