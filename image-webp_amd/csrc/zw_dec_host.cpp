@@ -497,7 +497,9 @@ static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 // 5 022 decodes/s with fresh buffers, 5 132-5 221 recycled).  zw_frame_free /
 // zw_bytes_free hand a buffer back to this process-wide pool (keyed by size,
 // bounded by ZW_DEC_POOL_MB, default 4096; 0 = off) and the next batch of that
-// size takes it.  Buffers the pool handed out are tracked, so zw_bytes_free
+// size takes it.  Only while a context is alive: the last zw_ctx_destroy (and
+// every zw_ctx_release_buffers) frees what the pool holds, and buffers freed
+// after that go straight back to free().  Buffers the pool handed out are tracked, so zw_bytes_free
 // still free()s the encoder's outputs.  (bench decode_path, 1024 1080p
 // frames: fan-out 96 -> 67 ms, 5 013 -> 5 289 decodes/s.)
 struct FramePool {
@@ -551,6 +553,10 @@ struct FramePool {
             if (it == live.end()) return false;
             const size_t n = it->second;
             live.erase(it);
+            if (!zw_ctx_any_alive()) {
+                free(p);
+                return true;
+            }
             for (auto& kv : free_) {
                 while (bytes + n > cap && kv.first != n && !kv.second.empty()) {
                     drop.push_back(kv.second.back());

@@ -42,7 +42,8 @@ hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size
                           void* levels, void* recon, int cus);
 hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp, int w,
                         int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw, int mbh, int nframes,
-                        int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, uint32_t* queue, int variant);
+                        int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, uint32_t* queue, uint32_t* qerr,
+                        int variant);
 size_t zwk_xform_mb_seg_bytes(void);
 size_t zwk_xform_mb_queue_bytes(int mbw, int mbh, int nframes);
 void zwk_xform_mb_pack_segs(const ZwMatrix* m, int n, void* out);
@@ -83,6 +84,12 @@ extern "C" const char* zw_strerror(int code)
     }
 }
 
+// Contexts alive in the process: the decoded-frame pool (zw_dec_host.cpp) keeps
+// freed frame buffers only while some context is, and the last zw_ctx_destroy
+// trims it.
+static std::atomic<int> g_ctx_alive{0};
+bool zw_ctx_any_alive() { return g_ctx_alive.load(std::memory_order_acquire) > 0; }
+
 extern "C" int zw_ctx_create(int device, zw_ctx** out)
 {
     if (!out) return ZW_EINVAL;
@@ -92,7 +99,7 @@ extern "C" int zw_ctx_create(int device, zw_ctx** out)
     HIPOK(hipSetDevice(device));
     zw_ctx* c = new zw_ctx();
     c->device = device;
-
+    g_ctx_alive.fetch_add(1, std::memory_order_acq_rel);
     *out = c;
     return ZW_OK;
 }
@@ -296,6 +303,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (c->dscratch2) (void)hipFree(c->dscratch2);
     for (auto& q : c->xmb_q)
         if (q.buf) (void)hipFree(q.buf);
+    if (c->xmb_err) (void)hipHostFree((void*)c->xmb_err);
     for (hipEvent_t e : c->tok_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->dev_ev)
@@ -308,6 +316,7 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
     if (c->tok_) (void)hipStreamDestroy(c->tok_);
     delete c;
+    if (g_ctx_alive.fetch_sub(1, std::memory_order_acq_rel) == 1) zw_dec_pool_trim();
 }
 
 extern "C" void zw_bytes_free(zw_bytes* b)
@@ -1777,19 +1786,38 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
     // new buffer, or one whose last launch pair failed to queue, is reset on the
     // launch stream first.  So neither an overlapping launch on another stream
     // nor a launch that stopped partway can leave a stale count.
+    // At most XMB_QUEUES streams keep a queue: a new stream takes the least
+    // recently used one's entry (hipFree of its buffer waits for the device).
+    // An overflow any launch reports through the context's host-visible error
+    // word (k_xform_mb, never expected) fails this and every later call.
     const hipStream_t ls = stream ? (hipStream_t)stream : ctx_stream(ctx);
     const size_t qb = zwk_xform_mb_queue_bytes((int)mbw, (int)mbh, nframes);
     void* q = nullptr;
     zw_ctx::XmbQueue* qe = nullptr;
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
+        if (!ctx->xmb_err) {
+            void* h = nullptr;
+            if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) return ZW_ENOMEM;
+            ctx->xmb_err = (volatile uint32_t*)h;
+            *ctx->xmb_err = 0;
+        }
+        if (*ctx->xmb_err) return ZW_EDEVICE;
+        constexpr size_t XMB_QUEUES = 8;
         zw_ctx::XmbQueue* e = nullptr;
         for (auto& x : ctx->xmb_q)
             if (x.stream == ls) e = &x;
+        if (!e && ctx->xmb_q.size() >= XMB_QUEUES) {
+            for (auto& x : ctx->xmb_q)
+                if (!e || x.used < e->used) e = &x;
+            if (e->buf) (void)hipFree(e->buf);
+            *e = {ls, nullptr, 0};
+        }
         if (!e) {
             ctx->xmb_q.push_back({ls, nullptr, 0});
             e = &ctx->xmb_q.back();
         }
+        e->used = ++ctx->xmb_clock;
         if (e->cap < qb) {
             if (e->buf) (void)hipFree(e->buf);
             e->buf = nullptr;
@@ -1805,7 +1833,8 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
     }
     HIPOK(zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp, (int)w, (int)h,
                        img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes, (int16_t*)d_levels,
-                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, xmb_variant()));
+                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, (uint32_t*)ctx->xmb_err,
+                       xmb_variant()));
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
         qe->dirty = false;  // both kernels queued: the pair leaves the counters zero
@@ -1866,7 +1895,7 @@ extern "C" int zw_transform_quant_mbs(zw_ctx* ctx, int nframes, uint32_t mbw, ui
     HIPOK(hipMemcpyAsync(ru, d + o_ru, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(rv, d + o_rv, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
-    return ZW_OK;
+    return *ctx->xmb_err ? ZW_EDEVICE : ZW_OK;
 }
 
 extern "C" int zw_transform_quant_mbs_rgb(zw_ctx* ctx, int nframes, uint32_t width, uint32_t height, int bpp,
@@ -1902,5 +1931,5 @@ extern "C" int zw_transform_quant_mbs_rgb(zw_ctx* ctx, int nframes, uint32_t wid
     HIPOK(hipMemcpyAsync(ru, d + o_ru, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(rv, d + o_rv, csz, hipMemcpyDeviceToHost, s));
     HIPOK(hipStreamSynchronize(s));
-    return ZW_OK;
+    return *ctx->xmb_err ? ZW_EDEVICE : ZW_OK;
 }

@@ -35,8 +35,11 @@ struct zw_ctx {
         void* buf = nullptr;
         size_t cap = 0;
         bool dirty = true;  // counters not known to be zero: reset on the stream first
+        uint64_t used = 0;  // xmb_clock at the last launch (LRU eviction past 8 streams)
     };
     std::deque<XmbQueue> xmb_q;  // (a deque: entries stay put while others are added)
+    uint64_t xmb_clock = 0;
+    volatile uint32_t* xmb_err = nullptr;  // host-mapped: k_xform_mb sets it on a queue overflow
     std::mutex xmb_mu;
     size_t dscratch1_cap = 0;
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy
@@ -199,6 +202,8 @@ int ctx_d2h(zw_ctx* c, void* dst, const void* src, size_t bytes);
 bool zw_dec_pool_put(void* p);
 // Frees the buffers the pool holds (zw_ctx_release_buffers).
 void zw_dec_pool_trim();
+// Is some zw_ctx alive (zw_host.cpp)?  The frame pool keeps buffers only then.
+bool zw_ctx_any_alive();
 
 // Set (process-wide) once an SDMA copy timed out with the engine possibly
 // still writing its destination: from then on pinned host buffers, which are

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U, const uint8_t* __restrict__ V, int w, int h,
     size_t img_stride, bool runs, const uint8_t* __restrict__ recs, const XmbSeg* __restrict__ segs, int mbw, int mbh, int nframes,
     int16_t* __restrict__ levels, uint8_t* __restrict__ RY, uint8_t* __restrict__ RU, uint8_t* __restrict__ RV,
-    uint32_t* __restrict__ i4q)
+    uint32_t* __restrict__ i4q, uint32_t* __restrict__ qerr)
 {
     // (the copy calibration always stages: the same bytes in and out, levels as one
     // contiguous run -- the ceiling for moving them)
@@ -410,10 +410,14 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
                                                   __HIP_MEMORY_SCOPE_AGENT);
                 base = (uint32_t)__shfl((int)base, 0);
                 const int rank = __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u);
-                // bounded: the queue holds one launch's MBs (a count past that
-                // would mean a shared or stale queue, which the host rules out)
+                // bounded: the queue holds one launch's MBs.  A count past that
+                // would mean a shared or stale queue, which the host rules out;
+                // should it happen, the MB's luma is not transformed and the
+                // host-visible error word makes the context's calls fail
                 if (i4 && base + rank < (uint32_t)nframes * (uint32_t)(mbw * mbh))
                     i4q[XI4_LIST + base + rank] = (uint32_t)(mb0 + lane);
+                else if (i4)
+                    __hip_atomic_store(qerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         // ---- chroma: lane = 8*mb + 4*plane + block (quad = one plane of one MB);
@@ -777,12 +781,13 @@ extern "C" void zwk_xform_mb_pack_segs(const ZwMatrix* m /* [n][4][3] */, int n,
 }
 
 // queue: zwk_xform_mb_queue_bytes of device memory whose two counters are zero
-// (as every launch leaves them).  src_bpp: 0 = Y/U/V planes; 3 / 4 = RGB / RGBA
+// (as every launch leaves them); qerr: a host-visible word the kernel sets to 1
+// if the queue overflowed (never cleared here).  src_bpp: 0 = Y/U/V planes; 3 / 4 = RGB / RGBA
 // pixels at Y (frame stride img_stride, image w x h).
 extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp,
                                    int w, int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw,
                                    int mbh, int nframes, int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV,
-                                   uint32_t* queue, int variant)
+                                   uint32_t* queue, uint32_t* qerr, int variant)
 {
     const long long waves = (long long)nframes * mbh * ((mbw + XMB_MBS - 1) / XMB_MBS);
     const unsigned grid = (unsigned)((waves + XMB_WAVES - 1) / XMB_WAVES);
@@ -794,7 +799,7 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     const bool runs = src_bpp != 0 && (uintptr_t)Y % ra == 0 && img_stride % ra == 0 && ((size_t)w * src_bpp) % ra == 0;
 #define XMB_LAUNCH(SRC, CP)                                                                                         \
     hipLaunchKernelGGL((k_xform_mb<SRC, CP>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, w, h, img_stride, runs,  \
-                       recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue)
+                       recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue, qerr)
     if (src_bpp == 0) {
         if (copy) XMB_LAUNCH(0, true);
         else XMB_LAUNCH(0, false);

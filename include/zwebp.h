@@ -101,6 +101,9 @@ typedef struct {
 } zw_image;
 
 int zw_ctx_create(int device, zw_ctx **out);
+/* The last zw_ctx_destroy of the process also frees the decoded-frame buffers
+ * zw_frame_free / zw_bytes_free handed back to the reuse pool (which keeps up to
+ * ZW_DEC_POOL_MB, default 4096, MB of them while any context is alive). */
 void zw_ctx_destroy(zw_ctx *ctx);
 /* Frees the context's grow-only device scratch and pinned host staging (the
  * single-call and batch decode / filter entry points keep them between calls);

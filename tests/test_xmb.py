@@ -175,6 +175,20 @@ for rep in range(3):
         want2 = O.xform_mbs(c[0], c[1], c[2], c[3], c[4], nf2, w2, h2)
         assert np.array_equal(outs[0].cpu().numpy().reshape(-1, 25, 16), want2[0]), "levels, two streams"
         assert np.array_equal(outs[1].cpu().numpy(), want2[1]), "ry, two streams"
+# more launch streams than the context keeps I4 queues for (8): the least
+# recently used stream's queue is handed over, every launch still exact
+nf2, w2, h2, c, tt, outs, _ = cases[0]
+want2 = O.xform_mbs(c[0], c[1], c[2], c[3], c[4], nf2, w2, h2)
+streams = [torch.cuda.Stream(dev) for _ in range(11)]
+for rep in range(2):
+    for st in streams:
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        zwebp.transform_quant_mbs_device(nf2, w2, h2, *[x.data_ptr() for x in tt], *[o.data_ptr() for o in outs],
+                                         stream=st.cuda_stream, ctx=ctx)
+        st.synchronize()
+        assert np.array_equal(outs[0].cpu().numpy().reshape(-1, 25, 16), want2[0]), "levels, stream rotation"
 bad = list(args)
 bad[3] += 4  # misaligned records
 try:
