@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <memory>
 #include <thread>
@@ -262,6 +263,8 @@ int ctx_d2h_stream(zw_ctx* c, void* dst, const void* src, size_t bytes)
     return ZW_OK;
 }
 
+static void seam_trim(bool all);
+
 extern "C" void zw_ctx_release_buffers(zw_ctx* c)
 {
     if (!c) return;
@@ -274,6 +277,7 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     }
     for (auto& v : c->dec_recs) std::vector<zw_ctx::RecBuf>().swap(v);
     zw_dec_pool_trim();  // the decoded-frame buffers callers have already freed
+    seam_trim(false);    // the idle pipelines concurrent single-frame calls shared
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     if (c->tok_) (void)hipStreamSynchronize(c->tok_);
@@ -295,6 +299,17 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
 extern "C" void zw_ctx_destroy(zw_ctx* c)
 {
     if (!c) return;
+    zw_ctx_free_internal(c);
+    if (g_ctx_alive.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        seam_trim(true);
+        zw_dec_pool_trim();
+    }
+}
+
+// Everything a context holds (the user contexts' zw_ctx_destroy, and the seam's
+// internal contexts, which are not counted as alive).
+void zw_ctx_free_internal(zw_ctx* c)
+{
     (void)hipSetDevice(c->device);
     zw_pipe_destroy(c->pipe1);
     if (c->dscratch) (void)hipFree(c->dscratch);
@@ -316,7 +331,6 @@ extern "C" void zw_ctx_destroy(zw_ctx* c)
     if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
     if (c->tok_) (void)hipStreamDestroy(c->tok_);
     delete c;
-    if (g_ctx_alive.fetch_sub(1, std::memory_order_acq_rel) == 1) zw_dec_pool_trim();
 }
 
 extern "C" void zw_bytes_free(zw_bytes* b)
@@ -1559,6 +1573,187 @@ extern "C" int zw_encode_webp_batch(zw_ctx* ctx, int n, const zw_image* imgs, ui
     return r;
 }
 
+// --------------------------------------------------------------------------
+// Seam batching of concurrent single-frame calls.  Callers of
+// zw_encode_frame_lossy(_ex) on one device -- any contexts, any threads --
+// queue their frame; up to SEAM_LEADERS of them at a time take the queue's
+// front shape (size, colour, quality, method, partitions) and encode up to
+// SEAM_MAX_BATCH queued frames of it as one pipeline batch (a power of two of
+// them, so a few cached pipelines serve every load), then wake the callers whose
+// frames they carried.  A frame's bitstream does not depend on the other
+// frames of its batch, so every caller gets exactly what a call of its own
+// returns, while concurrent callers share launches (one CU per frame) instead
+// of each allocating a pipeline and queueing its own kernels.  Each leader slot
+// has an internal context of its own (streams, scratch, cached pipelines); the
+// last zw_ctx_destroy frees them.  ZW_SEAM=0: every call encodes on its own.
+// --------------------------------------------------------------------------
+namespace {
+constexpr int SEAM_LEADERS = 8, SEAM_MAX_BATCH = 64, SEAM_PIPES = 6;
+int seam_knob(const char* name, int def)
+{
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : def;
+}
+struct SeamReq {
+    const uint8_t* data;
+    size_t len;
+    int key[6];
+    zw_bytes* out;
+    int rc = ZW_OK;
+    bool done = false;
+};
+struct SeamPipe {
+    int key[6];
+    int n;
+    zw_pipe* p;
+    uint64_t used;
+};
+struct SeamSlot {
+    bool busy = false;
+    zw_ctx* ctx = nullptr;
+    std::vector<SeamPipe> pipes;  // idle pipelines by (shape, frames), LRU beyond SEAM_PIPES
+};
+struct Seam {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<SeamReq*> q;
+    SeamSlot slot[SEAM_LEADERS];
+    uint64_t clock = 0;
+};
+std::mutex g_seam_mu;
+std::vector<std::pair<int, Seam*>> g_seams;  // by device; never freed (pointers stay valid)
+Seam& seam_of(int device)
+{
+    std::lock_guard<std::mutex> g(g_seam_mu);
+    for (auto& d : g_seams)
+        if (d.first == device) return *d.second;
+    g_seams.push_back({device, new Seam()});
+    return *g_seams.back().second;
+}
+bool seam_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("ZW_SEAM");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+}  // namespace
+
+// Frees the idle cached pipelines (all=true: and the internal contexts) of
+// every device's seam; slots a leader holds are left alone.
+static void seam_trim(bool all)
+{
+    std::vector<zw_pipe*> drop;
+    std::vector<zw_ctx*> ctxs;
+    {
+        std::lock_guard<std::mutex> g(g_seam_mu);
+        for (auto& d : g_seams) {
+            Seam& S = *d.second;
+            std::lock_guard<std::mutex> lk(S.mu);
+            for (SeamSlot& sl : S.slot) {
+                if (sl.busy) continue;
+                for (SeamPipe& sp : sl.pipes) drop.push_back(sp.p);
+                sl.pipes.clear();
+                if (all && sl.ctx) {
+                    ctxs.push_back(sl.ctx);
+                    sl.ctx = nullptr;
+                }
+            }
+        }
+    }
+    for (zw_pipe* p : drop) zw_pipe_destroy(p);
+    for (zw_ctx* c : ctxs) zw_ctx_free_internal(c);
+}
+
+static int seam_encode(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height, int color,
+                       uint8_t quality, uint8_t method, int nparts, zw_bytes* out)
+{
+    Seam& S = seam_of(ctx->device);
+    SeamReq r{data, len, {(int)width, (int)height, color, quality, method, nparts}, out};
+    std::unique_lock<std::mutex> lk(S.mu);
+    S.q.push_back(&r);
+    while (!r.done) {
+        static const int leaders = std::max(1, std::min(SEAM_LEADERS, seam_knob("ZW_SEAM_LEADERS", 2)));
+        static const bool pow2 = seam_knob("ZW_SEAM_POW2", 1) != 0;
+        int k = 0;
+        while (k < leaders && S.slot[k].busy) k++;
+        if (k == leaders || S.q.empty()) {
+            S.cv.wait(lk);
+            continue;
+        }
+        // lead: the front shape's queued frames, a power of two of them
+        SeamSlot& sl = S.slot[k];
+        sl.busy = true;
+        const int* key = S.q.front()->key;
+        int avail = 0;
+        for (SeamReq* x : S.q)
+            if (!memcmp(x->key, key, sizeof x->key) && ++avail == SEAM_MAX_BATCH) break;
+        int n = 1;
+        while (2 * n <= avail) n *= 2;
+        if (!pow2) n = avail;
+        std::vector<SeamReq*> b;
+        b.reserve(n);
+        int kk[6];
+        memcpy(kk, key, sizeof kk);
+        for (auto it = S.q.begin(); it != S.q.end() && (int)b.size() < n;) {
+            if (!memcmp((*it)->key, kk, sizeof kk)) {
+                b.push_back(*it);
+                it = S.q.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        zw_pipe* p = nullptr;
+        for (size_t i = 0; i < sl.pipes.size(); i++)
+            if (sl.pipes[i].n == n && !memcmp(sl.pipes[i].key, kk, sizeof kk)) {
+                p = sl.pipes[i].p;
+                sl.pipes.erase(sl.pipes.begin() + (long)i);
+                break;
+            }
+        lk.unlock();
+        int rc = ZW_OK;
+        if (!sl.ctx) {
+            sl.ctx = new zw_ctx();
+            sl.ctx->device = ctx->device;
+        }
+        if (!p) rc = zw_pipe_create(sl.ctx, n, (uint32_t)kk[0], (uint32_t)kk[1], kk[2], (uint8_t)kk[3], (uint8_t)kk[4], &p);
+        if (!rc) rc = zw_pipe_set_token_partitions(p, kk[5]);
+        for (int i = 0; i < n && !rc; i++) rc = zw_pipe_upload(p, i, b[i]->data, b[i]->len);
+        if (!rc) rc = zw_pipe_encode(p);
+        std::vector<int> frc(n, rc);
+        for (int i = 0; i < n && !rc; i++) frc[i] = zw_pipe_output(p, i, b[i]->out);
+        zw_pipe* drop = nullptr;
+        if (rc) {  // a pipeline that failed is not kept
+            drop = p;
+            p = nullptr;
+        }
+        lk.lock();
+        if (p) {
+            sl.pipes.push_back({{kk[0], kk[1], kk[2], kk[3], kk[4], kk[5]}, n, p, ++S.clock});
+            if ((int)sl.pipes.size() > SEAM_PIPES) {
+                size_t lru = 0;
+                for (size_t i = 1; i < sl.pipes.size(); i++)
+                    if (sl.pipes[i].used < sl.pipes[lru].used) lru = i;
+                drop = sl.pipes[lru].p;
+                sl.pipes.erase(sl.pipes.begin() + (long)lru);
+            }
+        }
+        for (int i = 0; i < n; i++) {
+            b[i]->rc = frc[i];
+            b[i]->done = true;
+        }
+        sl.busy = false;
+        S.cv.notify_all();
+        if (drop) {
+            lk.unlock();
+            zw_pipe_destroy(drop);
+            lk.lock();
+        }
+    }
+    return r.rc;
+}
+
 extern "C" int zw_encode_frame_lossy(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
                                      int color, uint8_t quality, uint8_t method, zw_bytes* out)
 {
@@ -1574,6 +1769,18 @@ extern "C" int zw_encode_frame_lossy_ex(zw_ctx* ctx, const uint8_t* data, size_t
     out->len = 0;
     int r = check_encode_args(data, len, width, height, color, quality);
     if (r) return r;
+    if (token_partitions != 1 && token_partitions != 2 && token_partitions != 4 && token_partitions != 8)
+        return ZW_EINVAL;
+    // Up to ZW_SEAM_SOLO calls in flight encode on their own (each context's
+    // cached one-frame pipeline); calls beyond that join the seam.
+    static std::atomic<int> inflight{0};
+    static const int solo = seam_knob("ZW_SEAM_SOLO", 16);
+    struct Count {
+        Count() { inflight.fetch_add(1, std::memory_order_acq_rel); }
+        ~Count() { inflight.fetch_sub(1, std::memory_order_acq_rel); }
+    } count;
+    if (seam_enabled() && inflight.load(std::memory_order_acquire) > solo)
+        return seam_encode(ctx, data, len, width, height, color, quality, method, token_partitions, out);
     zw_image im = {data, len, width, height, color};
     return zw_encode_batch_ex(ctx, 1, &im, quality, method, token_partitions, out);
 }

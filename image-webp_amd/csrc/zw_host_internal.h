@@ -204,6 +204,8 @@ bool zw_dec_pool_put(void* p);
 void zw_dec_pool_trim();
 // Is some zw_ctx alive (zw_host.cpp)?  The frame pool keeps buffers only then.
 bool zw_ctx_any_alive();
+// Frees a context's resources and the context (zw_ctx_destroy minus the count).
+void zw_ctx_free_internal(zw_ctx* c);
 
 // Set (process-wide) once an SDMA copy timed out with the engine possibly
 // still writing its destination: from then on pinned host buffers, which are

@@ -132,7 +132,15 @@ typedef struct {
     size_t xmp_len;
 } zw_metadata;
 
-/* encode_frame_lossy: raw VP8 frame bytes ("VP8 " chunk payload). */
+/* encode_frame_lossy: raw VP8 frame bytes ("VP8 " chunk payload).  Thread-safe;
+ * concurrent calls on one device (any contexts) are batched: while at most
+ * ZW_SEAM_SOLO (default 16) calls are in flight each encodes on its own (its
+ * context's cached one-frame pipeline); calls beyond that queue, and up to two
+ * of them at a time encode the queue's frames of their shape (size, colour,
+ * quality, method, partitions) as one batch of up to 64 (a power of two) and
+ * hand every caller its own bitstream -- byte-identical to a call of its own.
+ * The batches run on internal contexts that the last zw_ctx_destroy frees
+ * (zw_ctx_release_buffers frees their idle pipelines).  ZW_SEAM=0: no batching. */
 int zw_encode_frame_lossy(zw_ctx *ctx, const uint8_t *data, size_t len, uint32_t width, uint32_t height,
                           int color, uint8_t quality, uint8_t method, zw_bytes *out);
 

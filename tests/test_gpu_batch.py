@@ -419,3 +419,47 @@ def test_decode_batch_mixed_sizes(ctx):
     with pytest.raises(zwebp.DecodingError) as e:
         zwebp.decode_batch(bad, ctx=ctx)
     assert e.value.code == rc
+
+
+@pytest.mark.gpu
+def test_seam_concurrent_single_frame_calls(ctx):
+    """encode_frame_lossy from 12 threads, each with a context of its own, over
+    three shapes (sizes, quality, method, partitions): the seam batches the
+    concurrent calls of one shape into shared launches, and every call returns
+    exactly the oracle's bitstream for its own frame."""
+    import threading
+    shapes = [(96, 64, 75, 4, 1), (96, 64, 40, 2, 1), (48, 80, 75, 4, 2)]
+    imgs = {s: [synth_rgba(s[0], s[1], 0x5EA0 + 7 * i + s[2]) for i in range(4)] for s in shapes}
+    want = {}
+    for s in shapes:
+        for i, im in enumerate(imgs[s]):
+            rc, b, _ = O.encode(im, s[0], s[1], 3, s[2], s[3], nparts=s[4])
+            assert rc == 0
+            want[(s, i)] = b
+    T, calls = 12, 6
+    bad, errs = [], []
+
+    def work(t):
+        c = zwebp.Context(0)
+        try:
+            for k in range(calls):
+                s = shapes[(t + k) % len(shapes)]
+                i = (t * 5 + k) % 4
+                got = zwebp.encode_frame_lossy(imgs[s][i], s[0], s[1], zwebp.ColorType.Rgba8, s[2], s[3], ctx=c,
+                                               token_partitions=s[4])
+                if bytes(got) != want[(s, i)]:
+                    bad.append((t, k, s, i))
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+        finally:
+            c.close()
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=240)
+    assert not errs and not bad, (errs, bad[:4])
+    # an invalid call fails on its own without joining (or stalling) a batch
+    with pytest.raises(zwebp.ZwError):
+        zwebp.encode_frame_lossy(imgs[shapes[0]][0].reshape(-1)[:100], 96, 64, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
