@@ -303,8 +303,13 @@ DI void rgb_item(const uint8_t* __restrict__ img, int w, int h, bool runs, int p
 // SRC: 0 = Y/U/V planes (MB-padded), 3 / 4 = RGB / RGBA pixels at Y (frame f at
 // Y + f * img_stride; w, h the image size; runs: every 8-pixel run is aligned
 // for its 16-byte (RGBA) / 8-byte (RGB) loads, else all pixels go the per-pixel
-// way).  COPY: the calibration variant -- the same loads and stores, no arithmetic.
-template <int SRC, bool COPY>
+// way).  CV: 0 = the pass; 99 = the copy calibration (the same loads and
+// stores, no arithmetic); the per-stream calibrations move one stream alone:
+// 94 the records in, 92 / 97 the RGB(A) pixels in (92 raw, folded into LDS with
+// no conversion; 97 converted into the tiles as the pass does), 93 the same
+// pixels in with every load instruction reading 64 x 16 contiguous bytes, 96
+// the levels out, 95 the reconstruction out.
+template <int SRC, int CV>
 __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U, const uint8_t* __restrict__ V, int w, int h,
     size_t img_stride, bool runs, const uint8_t* __restrict__ recs, const XmbSeg* __restrict__ segs, int mbw, int mbh, int nframes,
@@ -313,6 +318,11 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 {
     // (the copy calibration always stages: the same bytes in and out, levels as one
     // contiguous run -- the ceiling for moving them)
+    constexpr bool COPY = CV != 0;
+    constexpr bool REC_IN = CV == 0 || CV == 99 || CV == 94;
+    constexpr bool PIX_IN = CV == 0 || CV == 99 || CV == 97;
+    constexpr bool LEV_OUT = CV == 0 || CV == 99 || CV == 96;
+    constexpr bool REC_OUT = CV == 0 || CV == 99 || CV == 95;
     constexpr bool STG = COPY || (XMB_STAGE_LEV < 0 ? (SRC != 0 || XMB_PLANES_HALF) : XMB_STAGE_LEV != 0);
     constexpr bool HALF = STG && !COPY && XMB_HALF_STAGE;
     constexpr int NL = !STG ? 0 : (HALF ? XMB_MBS / 2 : XMB_MBS);
@@ -338,10 +348,39 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     {
         const int rm = lane / 6, rq = lane % 6;
         v4u r4 = {0u, 0u, 0u, 0u};
-        if (lane < 48 && rm < nact) r4 = __builtin_nontemporal_load((const v4u*)(recs + (mb0 + rm) * 96) + rq);
+        if (REC_IN && lane < 48 && rm < nact) r4 = __builtin_nontemporal_load((const v4u*)(recs + (mb0 + rm) * 96) + rq);
         v4u s4 = {0u, 0u, 0u, 0u};
         if (!COPY && lane >= 40) s4 = *((const v4u*)(segs + (size_t)f * 4) + (lane - 40));
-        if (SRC == 0) {
+        if (SRC != 0 && (CV == 92 || CV == 93)) {
+            // raw pixel reads, folded into one word per lane (kept in LDS so they stay)
+            const uint8_t* img = Y + (size_t)f * img_stride + ((size_t)mby * 16 * w + (size_t)x0 * 16) * SRC;
+            const int rowb = nact * 16 * SRC;  // bytes of the group's row
+            uint32_t acc = 0;
+            if (CV == 92) {  // the pass's item pattern: lane = 8 px x 2 rows, 32 B per row
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const int g = lane >> 4, pr = (((g & 1) << 2) | ((g >> 1) << 1)) + k, xr = lane & 15;
+                    if ((xr >> 1) < nact && mby * 16 + 2 * pr + 1 < h) {
+                        const uint8_t* ra = img + ((size_t)(2 * pr) * w) * SRC + (size_t)xr * 32;
+                        const v4u a0 = __builtin_nontemporal_load((const v4u*)ra), a1 = __builtin_nontemporal_load((const v4u*)ra + 1);
+                        const v4u b0 = __builtin_nontemporal_load((const v4u*)(ra + (size_t)w * SRC));
+                        const v4u b1 = __builtin_nontemporal_load((const v4u*)(ra + (size_t)w * SRC) + 1);
+                        acc ^= a0.x ^ a0.y ^ a0.z ^ a0.w ^ a1.x ^ a1.y ^ a1.z ^ a1.w ^ b0.x ^ b0.y ^ b0.z ^ b0.w ^ b1.x ^ b1.y ^ b1.z ^ b1.w;
+                    }
+                }
+            } else {  // contiguous: instruction j reads rows 2j, 2j+1, 32 lanes x 16 B each
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int r = 2 * j + (lane >> 5), c = (lane & 31) * 16;
+                    if (c < rowb && mby * 16 + r < h) {
+                        const v4u a = __builtin_nontemporal_load((const v4u*)(img + (size_t)r * w * SRC + c));
+                        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+                    }
+                }
+            }
+            (&L.yt[0][0])[lane] = acc;
+        } else if (!PIX_IN) {
+        } else if (SRC == 0) {
             const uint8_t* Yf = Y + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
             const int yc = lane & 7, yr = lane >> 3;
             v4u y0 = {0u, 0u, 0u, 0u}, y1 = y0;
@@ -386,7 +425,8 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 
     if (COPY) {
         // calibration: levels staged from the records, no arithmetic
-        if constexpr (STG) {
+        if constexpr (!LEV_OUT) {
+        } else if constexpr (STG) {
             for (int i = lane; i < XMB_MBS * XMB_LEVW; i += 64) (&L.lev[0][0])[i] = (&L.rec[0][0])[i % (XMB_MBS * 24)];
         } else {
             for (int k = 0; k < 3; k++) {
@@ -580,7 +620,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     // row-coalesced (an I4 MB's luma tile still holds its source: k_xform_mb_i4,
     // next on the stream, reads it there and overwrites it with the reconstruction)
     {
-        if constexpr (STG && !HALF) {
+        if constexpr (STG && !HALF && LEV_OUT) {
             const int nch = nact * (XMB_LEVW / 4);
             v4u* lo = (v4u*)(levels + mb0 * 400);
 #pragma unroll
@@ -591,14 +631,14 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
         }
         uint8_t* RYf = RY + f * ysz + (size_t)mby * 16 * ys + x0 * 16;
         const int yc = lane & 7, yr = lane >> 3;
-        if (yc < nact) {
+        if (REC_OUT && yc < nact) {
             __builtin_nontemporal_store(*(const v4u*)&L.yt[yr][4 * yc], (v4u*)(RYf + yr * ys + yc * 16));
             __builtin_nontemporal_store(*(const v4u*)&L.yt[yr + 8][4 * yc], (v4u*)(RYf + (yr + 8) * ys + yc * 16));
         }
         uint8_t* Cf = (cp ? RV : RU) + f * csz + (size_t)(mby * 8 + cr) * cs + (x0 + 2 * cq) * 8;
         const v4u c4 = *(const v4u*)&L.ct[cp][cr][4 * cq];
-        if (cn == 2) __builtin_nontemporal_store(c4, (v4u*)Cf);
-        else if (cn == 1) __builtin_nontemporal_store(v2u{c4.x, c4.y}, (v2u*)Cf);
+        if (REC_OUT && cn == 2) __builtin_nontemporal_store(c4, (v4u*)Cf);
+        else if (REC_OUT && cn == 1) __builtin_nontemporal_store(v2u{c4.x, c4.y}, (v2u*)Cf);
     }
 }
 
@@ -794,21 +834,31 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     if (grid == 0) return hipSuccess;
     if (src_bpp != 0 && src_bpp != 3 && src_bpp != 4) return hipErrorInvalidValue;
     const XmbSeg* sg = (const XmbSeg*)segs;
-    const bool copy = variant == 99;
+    const bool copy = variant != 0;
+    if (copy && variant != 99 && (src_bpp == 0 || (variant != 92 && variant != 93 && (variant < 94 || variant > 97))))
+        return hipErrorInvalidValue;
     const int ra = src_bpp == 4 ? 16 : 8;
     const bool runs = src_bpp != 0 && (uintptr_t)Y % ra == 0 && img_stride % ra == 0 && ((size_t)w * src_bpp) % ra == 0;
 #define XMB_LAUNCH(SRC, CP)                                                                                         \
     hipLaunchKernelGGL((k_xform_mb<SRC, CP>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, w, h, img_stride, runs,  \
                        recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue, qerr)
     if (src_bpp == 0) {
-        if (copy) XMB_LAUNCH(0, true);
-        else XMB_LAUNCH(0, false);
+        if (copy) XMB_LAUNCH(0, 99);
+        else XMB_LAUNCH(0, 0);
     } else if (src_bpp == 3) {
-        if (copy) XMB_LAUNCH(3, true);
-        else XMB_LAUNCH(3, false);
+        if (copy) XMB_LAUNCH(3, 99);
+        else XMB_LAUNCH(3, 0);
     } else {
-        if (copy) XMB_LAUNCH(4, true);
-        else XMB_LAUNCH(4, false);
+        switch (variant) {
+        case 0: XMB_LAUNCH(4, 0); break;
+        case 92: XMB_LAUNCH(4, 92); break;
+        case 93: XMB_LAUNCH(4, 93); break;
+        case 94: XMB_LAUNCH(4, 94); break;
+        case 95: XMB_LAUNCH(4, 95); break;
+        case 96: XMB_LAUNCH(4, 96); break;
+        case 97: XMB_LAUNCH(4, 97); break;
+        default: XMB_LAUNCH(4, 99); break;
+        }
     }
 #undef XMB_LAUNCH
     if (copy) return hipGetLastError();
