@@ -35,7 +35,7 @@ stream.  The 96-byte record is traffic the pass moves but 8(d) does not count
 (achieved_incl_records).  `yuv_planes_form` is the same pass from Y/U/V planes
 at 1568 B/MB.  `copy_ceiling` runs the same loads and stores with no transform
 arithmetic (ZW_XMB_VARIANT=99).  `traffic` is the PMC-measured HBM bytes per
-launch from profiles/r04_xmb_pmc.json scaled to this launch.  Every frame's
+launch from profiles/r05_xmb_pmc.json scaled to this launch.  Every frame's
 levels and reconstruction are hashed against the oracle's digests.
 `roofline_blocks`: k_fdct_quant, the same arithmetic on 4x4 blocks with the
 prediction materialised (64 B per block counted, 16 B of prediction moved).
@@ -44,7 +44,7 @@ fused with the final DCT+quant+recon), against the VALU issue peak of 2
 wave-instructions per CU-cycle (4 SIMD32, a wave64 VALU op every 2 cycles per
 SIMD): `frac` from one rocprofv3 --pmc dispatch (SQ_INSTS_VALU over that
 dispatch's GRBM_GUI_ACTIVE cycles, clock_ghz from its timestamps;
-profiles/r04_encode_pmc.json), `frac_live` the same instruction count over this
+profiles/r05_encode_pmc.json), `frac_live` the same instruction count over this
 run's launch time at that clock.
 cpu_baseline times the C restatement of the reference encoder (oracle/, -O3)
 on a bounded sample of the same frames.
@@ -71,9 +71,9 @@ HBM_PEAK_GBS = 8000.0
 VALU_PEAK_PER_CU_CYCLE = 2.0      # wave64 VALU instructions: 4 SIMD32 x 1 per 2 cycles
 CLOCK_GHZ = 2.4
 XFORM_PMC = os.path.join(ROOT, "profiles", "r04_xform_pmc_traffic.json")
-ENCODE_PMC = os.path.join(ROOT, "profiles", "r04_encode_pmc.json")
+ENCODE_PMC = os.path.join(ROOT, "profiles", "r05_encode_pmc.json")
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
-XMB_PMC = os.path.join(ROOT, "profiles", "r04_xmb_pmc.json")
+XMB_PMC = os.path.join(ROOT, "profiles", "r05_xmb_pmc.json")
 
 
 def pmc_traffic(path, units):
@@ -837,7 +837,7 @@ def encode_roofline(p2_ms, launch_frames, nmb):
             "valu_insts_per_mb": d["valu_insts_per_mb"], "mbs_per_launch": mbs,
             "hbm_achieved": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9,
             "hbm_frac": ALG_BYTES_PER_MB * mbs / (p2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "source": "profiles/r04_encode_pmc.json (rocprofv3 --pmc SQ_INSTS_VALU + GRBM_GUI_ACTIVE in one "
+            "source": "profiles/r05_encode_pmc.json (rocprofv3 --pmc SQ_INSTS_VALU + GRBM_GUI_ACTIVE in one "
                       "pass, one dispatch; clock from its timestamps; tools/gpu_pmc_encode.sh)"}
 
 
@@ -1047,7 +1047,7 @@ def main():
                                 "achieved_incl_records": xm["achieved_incl_records"],
                                 "copy_ceiling": xm["copy_ceiling"], "verified": xm["verified"],
                                 "verification": xm["verification"],
-                                "traffic_source": "profiles/r04_xmb_pmc.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)",
+                                "traffic_source": "profiles/r05_xmb_pmc.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)",
                                 "yuv_planes_form": xa["yuv"],
                                 "fused_path": {"kernel": "k_encode_pass2 (RD search fused with the final "
                                                          "DCT+quant+recon, the timed step's dominant kernel)",
