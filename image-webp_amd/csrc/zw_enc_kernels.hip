@@ -1401,7 +1401,7 @@ DI int quad_sum(int v)
 // 0: lane q holds column q, av[r] = |level| at natural index n = 4 r + q.
 // Uniform in the quad.  LC = false: pass 1 (zero LevelCosts, quirk A2).
 template <bool LC>
-DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* T, int& last_o)
+DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* T, int& last_o, int head_none[2])
 {
     unsigned nz = 0, big = 0, sc = 0;
 #pragma unroll
@@ -1411,11 +1411,9 @@ DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* 
         big |= (unsigned)(av[r] >= 2) << n;
         sc |= (unsigned)min(av[r], 2) << (2 * r);
     }
-    nz = (unsigned)quad_or((int)nz);
-    big = (unsigned)quad_or((int)big);
-    const int last = 31 - __clz((int)nz);
-    last_o = last;
-    int part = 0;
+    // every table read of the block issued before any is used (one LDS round
+    // trip): the level costs, then the end-of-block cost at last + 1
+    int tl[4];
     if (LC) {
         // the context of position n is min(|level[n - 1]|, 2): lane q - 1 of the
         // same row, for q = 0 lane 3 of the row above (ctx0 at n = 0)
@@ -1427,18 +1425,23 @@ DI int rcost_quad(const int av[4], int q, int ctx0, int ctype, const LdsTables* 
             const int c_q0 = r == 0 ? ctx0 : (int)((pv >> (2 * r - 2)) & 3u);
             const int ctx = csel(q == 0, c_q0, c_same);
             const int a = av[r];
-            const int tl = T->lfc[min(a, 2047)] + T->lc[ctype][band_of(n)][ctx][min(a, 67)];
-            part += tl & -(int)(n <= last);
+            tl[r] = T->lfc[min(a, 2047)] + T->lc[ctype][band_of(n)][ctx][min(a, 67)];
         }
     } else {
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += T->lfc[min(av[r], 2047)];
+        for (int r = 0; r < 4; r++) tl[r] = T->lfc[min(av[r], 2047)];
     }
-    const int sum = quad_sum(part);
+    nz = (unsigned)quad_or((int)nz);
+    big = (unsigned)quad_or((int)big);
+    const int last = 31 - __clz((int)nz);
+    last_o = last;
     const int ctx_t = ((big >> max(last, 0)) & 1u) ? 2 : 1;
     const int tail = (int)T->beob[ctype][band_of(min(last + 1, 15))][ctx_t] & -(int)(last < 15);
-    const int head = (int)T->binit[ctype][0][ctx0] & -(int)(ctx0 == 0);
-    return csel(last < 0, (int)T->beob[ctype][0][ctx0], head + sum + tail);  // (no divergent branch)
+    int part = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) part += LC ? tl[r] & -(int)(4 * r + q <= last) : tl[r];
+    const int sum = quad_sum(part);
+    return csel(last < 0, head_none[1], head_none[0] + sum + tail);  // (no divergent branch)
 }
 
 // Candidate evaluation of an I4 step in quad form (K <= 4: methods 0-4).  The
@@ -1476,6 +1479,15 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
     const int bx = csel(slot, sbx[sl], sbx[0]), by = csel(slot, sby[sl], sby[0]);
     const int ctx0 = csel(slot, nzc[sl], nzc[0]);
     const int mcost = T->fci4[csel(slot, tctx[sl], tctx[0])][csel(slot, lctx[sl], lctx[0])][mv];
+    // read up front, off the transform's chain: the quantiser of this lane's
+    // coefficients and the block's costs that depend only on ctx0 (the first
+    // coefficient's "more tokens" bit, and the empty block's end of block)
+    const uint32_t iq0 = q ? S.y1.iq[1] : S.y1.iq[0], bs0 = q ? S.y1.bias[1] : S.y1.bias[0];
+    const uint32_t iq1 = S.y1.iq[1], bs1 = S.y1.bias[1];
+    const int q0 = q ? (int)S.y1.q[1] : (int)S.y1.q[0], qa = (int)S.y1.q[1];
+    int hn[2];
+    hn[0] = (int)T->binit[3][0][ctx0] & -(int)(ctx0 == 0);
+    hn[1] = (int)T->beob[3][0][ctx0];
     // prediction of row q: V indices of its four pixels (254: TrueMotion,
     // V[3 - q] + the top offsets; 255: the DC entry V[38])
     uint32_t p01, p32;
@@ -1498,25 +1510,25 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
         s01 = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
         s32 = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
     }
+    PH_MARK_L(22, l, 0);
     const uint32_t R01 = sub_pk(s01, p01), R32 = sub_pk(s32, p32);
     int cf[4];
     uvq_fdct(add_pk(R01, R32), sub_pk(R01, R32), q, cf);
     int av[4], dq[4], lv[4];
     {
-        const uint32_t iq0 = q ? S.y1.iq[1] : S.y1.iq[0], bs0 = q ? S.y1.bias[1] : S.y1.bias[0];
-        const int q0 = q ? (int)S.y1.q[1] : (int)S.y1.q[0];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const bool dcs = r == 0;  // (0, q): the DC for q = 0
             const int v = cf[r];
-            const int a = (int)((__umul24((uint32_t)iabs(v), dcs ? iq0 : S.y1.iq[1]) + (dcs ? bs0 : S.y1.bias[1])) >> 17);
+            const int a = (int)((__umul24((uint32_t)iabs(v), dcs ? iq0 : iq1) + (dcs ? bs0 : bs1)) >> 17);
             av[r] = a;
             lv[r] = v < 0 ? -a : a;
-            dq[r] = m24(lv[r], dcs ? q0 : (int)S.y1.q[1]);
+            dq[r] = m24(lv[r], dcs ? q0 : qa);
         }
     }
     int last;
-    const int cost = rcost_quad<PASS == 2>(av, q, ctx0, 3, T, last);  // get_cost_luma4 (ctype 3, first 0)
+    const int cost = rcost_quad<PASS == 2>(av, q, ctx0, 3, T, last, hn);  // get_cost_luma4 (ctype 3, first 0)
+    PH_MARK_L(23, l, 0);
     uint32_t r01, r32;
     uvq_idct_recon(dq, p01, p32, q, r01, r32);
     int sse = 0;

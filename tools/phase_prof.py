@@ -25,7 +25,8 @@ NAMES = {0: "wait(row above)", 1: "border+pick_i16", 2: "pick_i4", 3: "pick_uv",
          7: "  (count of I4 MBs)", 14: "  final: I16 MBs", 15: "  final: I4 MBs",
          16: "    i16: fdct+y2", 17: "    i16: quant check+trellis", 18: "    i16: ctx resolve+gather",
          19: "  (I4 search steps run)", 20: "  (I4 searches)",
-         21: "wait(above-right)+border"}
+         21: "wait(above-right)+border",
+         22: "  i4q: modes+pred+src", 23: "  i4q: fdct+quant+cost"}
 
 
 def main():
