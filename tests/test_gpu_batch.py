@@ -387,11 +387,15 @@ def test_pipe_encode_host_pinned(ctx, monkeypatch, kind):
             hip.hipHostUnregister(ctypes.c_void_p(base))
 
 
-def test_decode_batch_mixed_sizes(ctx):
+@pytest.mark.parametrize("tokens", ["auto", "device"])
+def test_decode_batch_mixed_sizes(ctx, monkeypatch, tokens):
     """Frames of several sizes in one batch decode as runs of one size, each
     equal to the oracle's decode_frame (decoder/vp8.rs:1526), as a sequence of
     decode_frame calls would; RGBA batches (fresh and caller buffers) likewise.
-    A damaged frame mid-batch fails the call with the oracle's variant."""
+    A damaged frame mid-batch fails the call with the oracle's variant.
+    tokens=device: every run's token partitions parsed by k_dec_tokl."""
+    if tokens != "auto":
+        monkeypatch.setenv("ZW_DEC_TOKENS", tokens)
     sizes = [(64, 48), (64, 48), (96, 80), (33, 17), (33, 17), (33, 17), (64, 48)]
     streams = []
     for k, (w, h) in enumerate(sizes):
