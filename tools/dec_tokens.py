@@ -17,7 +17,10 @@ from zwebp.synth import synth_rgba  # noqa: E402
 def run(vp8, ctx, mode, reps):
     os.environ["ZW_DEC_TOKENS"] = mode
     best = None
+    fr = None
     for _ in range(reps):
+        hs = [hashlib.sha256(bytes(f.ybuf) + bytes(f.ubuf) + bytes(f.vbuf)).hexdigest() for f in fr[:8]] if fr else None
+        fr = None  # the previous batch's frames go back to the library (as a decode loop frees them)
         t0 = time.perf_counter()
         fr = zwebp.decode_batch(vp8, ctx=ctx)
         el = time.perf_counter() - t0
