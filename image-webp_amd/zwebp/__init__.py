@@ -548,8 +548,9 @@ def _writable_u8(buf):
 def decode_rgb_batch_into(frames, outs, bpp=3, upsampling=UpsamplingMethod.Bilinear, stride_bytes=None, ctx=None):
     """decode_rgb_batch into the caller's buffers (decode_rgba_into / decode_rgb_into,
     decoder/api.rs:1004-1128): outs[i] is a writable uint8 array of at least
-    stride * height bytes, rows stride_bytes (default width * bpp) apart.
-    Returns [(width, height)] per frame."""
+    stride * height bytes, rows stride_bytes apart (one stride for every
+    buffer; default the widest frame's width * bpp).  Returns [(width, height)]
+    per frame."""
     c = _ctx(ctx)
     L = c._lib
     arrs = [_as_u8(d) for d in frames]
@@ -558,8 +559,7 @@ def decode_rgb_batch_into(frames, outs, bpp=3, upsampling=UpsamplingMethod.Bilin
     if len(dst) != n or n == 0:
         raise ValueError("one output buffer per frame")
     if stride_bytes is None:
-        w0 = webp_frame_width(arrs[0])
-        stride_bytes = w0 * bpp
+        stride_bytes = max(webp_frame_width(a) for a in arrs) * bpp
     ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
     lens = (ctypes.c_size_t * n)(*[a.size for a in arrs])
     optr = (ctypes.c_void_p * n)(*[o.ctypes.data for o in dst])
