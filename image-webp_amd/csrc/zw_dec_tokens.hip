@@ -137,6 +137,10 @@ struct TokDev {
 #ifndef ZW_TOKL_MK
 #define ZW_TOKL_MK 1  // steps between MB phases
 #endif
+#ifndef ZW_TOKL_FSLEEP
+#define ZW_TOKL_FSLEEP 32  // feeder pause between ring refills (64 cycles each; 2: +1.4 % launch time, the feeder
+                           // wave's loads and VALU beside the decoder)
+#endif
 #ifndef ZW_TOKL_MBRUN
 #define ZW_TOKL_MBRUN 8  // MBs one MB phase may start (skipped MBs need no decisions)
 #endif
@@ -236,7 +240,7 @@ extern "C" __global__ __launch_bounds__(128) void k_dec_tokl(const uint8_t* __re
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // ring data before the fill counters
             sfill[lane] = sf;
             mfill[lane] = mf;
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(ZW_TOKL_FSLEEP);
         }
         return;
     }
