@@ -2005,8 +2005,14 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
         if (!ctx->xmb_err) {
             void* h = nullptr;
+            void* dp = nullptr;
             if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) return ZW_ENOMEM;
+            if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+                (void)hipHostFree(h);
+                return ZW_EDEVICE;
+            }
             ctx->xmb_err = (volatile uint32_t*)h;
+            ctx->xmb_err_dev = (uint32_t*)dp;
             *ctx->xmb_err = 0;
         }
         if (*ctx->xmb_err) return ZW_EDEVICE;
@@ -2037,10 +2043,16 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
         qe = e;
         if (qe->dirty) HIPOK(hipMemsetAsync(q, 0, 16, ls));
         qe->dirty = true;
+        // test hook: a stale count past this launch's MBs, as a shared queue would leave
+        if (getenv("ZW_XMB_FORCE_OVERFLOW")) {
+            const uint32_t stale = (uint32_t)((size_t)nframes * mbw * mbh);
+            HIPOK(hipMemcpyAsync(q, &stale, 4, hipMemcpyHostToDevice, ls));
+            HIPOK(hipStreamSynchronize(ls));  // (the source is on this stack)
+        }
     }
     HIPOK(zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp, (int)w, (int)h,
                        img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes, (int16_t*)d_levels,
-                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, (uint32_t*)ctx->xmb_err,
+                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, ctx->xmb_err_dev,
                        xmb_variant()));
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);

@@ -40,6 +40,7 @@ struct zw_ctx {
     std::deque<XmbQueue> xmb_q;  // (a deque: entries stay put while others are added)
     uint64_t xmb_clock = 0;
     volatile uint32_t* xmb_err = nullptr;  // host-mapped: k_xform_mb sets it on a queue overflow
+    uint32_t* xmb_err_dev = nullptr;       // the same word as the device addresses it
     std::mutex xmb_mu;
     size_t dscratch1_cap = 0;
     // SDMA copy engine path (HSA) for device->host fetches: ROCclr's hipMemcpy

@@ -664,13 +664,17 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* _
     const uint8_t* vvb = (const uint8_t*)&vvs[wv][0][0];
     const int nmb = mbw * mbh;
     const uint32_t cap = (uint32_t)((long long)nframes * nmb);
-    const uint32_t n = min(__hip_atomic_load(&i4q[XI4_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), cap);
+    // an overflowed count (a stale or shared queue: k_xform_mb flagged it) or an
+    // entry outside this launch is not trusted: nothing is read through it
+    const uint32_t cnt = __hip_atomic_load(&i4q[XI4_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = cnt > cap ? 0u : cnt;
     const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
     const uint32_t nwaves = gridDim.x * XMB_WAVES;
 #pragma unroll 1
     for (uint32_t k = 64 * (blockIdx.x * XMB_WAVES + wv); k < n; k += 64 * nwaves) {
         if (k + lane >= n) continue;  // (no cross-lane operations below)
         const size_t gm = i4q[XI4_LIST + k + lane];
+        if (gm >= cap) continue;
         const int f = (int)(gm / nmb), rr = (int)(gm % nmb), mby = rr / mbw, x = rr % mbw;
         // record words 0..15: modes/segment, bpred, corner, top 16 + top-right 4, left 16
         uint32_t R[16];

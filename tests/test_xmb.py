@@ -226,6 +226,36 @@ def test_gpu_xform_mbs_errors(ctx):
 
 
 @pytest.mark.gpu
+def test_gpu_xform_mbs_queue_overflow_reported(monkeypatch):
+    """An I4 queue whose count is stale (test hook: preset past the launch's
+    MBs, as a shared queue would leave it) makes k_xform_mb flag the context's
+    error word instead of writing past the queue, k_xform_mb_i4 read nothing
+    through it, and the call -- and every later one on that context -- fail
+    with DeviceError; other contexts are unaffected."""
+    import zwebp
+    mbw, mbh, nf = 9, 3, 2
+    y, u, v, recs, sq = _random_case(np.random.default_rng(9), nf, mbw, mbh, 0.5)
+    bad = zwebp.Context(0)
+    try:
+        monkeypatch.setenv("ZW_XMB_FORCE_OVERFLOW", "1")
+        with pytest.raises(zwebp.ZwError) as e:
+            zwebp.transform_quant_mbs(y, u, v, recs, sq, nf, mbw, mbh, ctx=bad)
+        assert e.value.code == 4
+        monkeypatch.delenv("ZW_XMB_FORCE_OVERFLOW")
+        with pytest.raises(zwebp.ZwError):
+            zwebp.transform_quant_mbs(y, u, v, recs, sq, nf, mbw, mbh, ctx=bad)
+    finally:
+        bad.close()
+    good = zwebp.Context(0)
+    try:
+        got = zwebp.transform_quant_mbs(y, u, v, recs, sq, nf, mbw, mbh, ctx=good)
+        want = O.xform_mbs(y, u, v, recs, sq, nf, mbw, mbh)
+        assert all(np.array_equal(a, b) for a, b in zip(got, want))
+    finally:
+        good.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("w,h,bpp,nframes", [(1920, 1080, 4, 2), (97, 33, 4, 2), (200, 136, 3, 1), (15, 7, 4, 1),
                                              (64, 48, 3, 2), (130, 17, 3, 1), (257, 255, 4, 1)])
 def test_gpu_xform_mbs_rgb(ctx, w, h, bpp, nframes):
