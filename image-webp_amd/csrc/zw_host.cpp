@@ -8,6 +8,7 @@
 //   -> H2D params/costs -> k_encode(pass 2) -> D2H pass-2 MB records
 //   -> host: header + token emission (one thread per frame).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -223,6 +224,46 @@ static int sdma_wait(zw_ctx* c, hsa_signal_t sig)
             g_dma_poisoned.store(true, std::memory_order_release);
             return ZW_EDEVICE;
         }
+    }
+}
+
+// RGBA -> RGB for the host-resident upload (zw_pipe_encode_host): the VP8
+// payload reads only R, G, B (convert_image_yuv, yuv.rs:656-804; the alpha
+// plane goes to ALPH, which that entry point does not write), so an RGBA frame
+// crosses PCIe as 3/4 of its bytes and rgb2yuv reads it as RGB.  16 pixels a
+// step: four in-lane byte shuffles, spliced into three 16-byte streaming
+// stores (`d` 16-byte aligned: the pinned staging slot).
+__attribute__((target("ssse3"))) static void pack_rgb_ssse3(uint8_t* d, const uint8_t* s, size_t npx)
+{
+    const __m128i sh = _mm_setr_epi8(0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -128, -128, -128, -128);
+    size_t i = 0;
+    for (; i + 16 <= npx; i += 16, s += 64, d += 48) {
+        const __m128i a = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)s), sh);
+        const __m128i b = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(s + 16)), sh);
+        const __m128i c = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(s + 32)), sh);
+        const __m128i e = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(s + 48)), sh);
+        _mm_stream_si128((__m128i*)d, _mm_or_si128(a, _mm_slli_si128(b, 12)));
+        _mm_stream_si128((__m128i*)(d + 16), _mm_or_si128(_mm_srli_si128(b, 4), _mm_slli_si128(c, 8)));
+        _mm_stream_si128((__m128i*)(d + 32), _mm_or_si128(_mm_srli_si128(c, 8), _mm_slli_si128(e, 4)));
+    }
+    _mm_sfence();
+    for (; i < npx; i++, s += 4, d += 3) {
+        d[0] = s[0];
+        d[1] = s[1];
+        d[2] = s[2];
+    }
+}
+static void pack_rgb(uint8_t* d, const uint8_t* s, size_t npx)
+{
+    static const bool ssse3 = __builtin_cpu_supports("ssse3");
+    if (ssse3 && ((uintptr_t)d & 15) == 0) {
+        pack_rgb_ssse3(d, s, npx);
+        return;
+    }
+    for (size_t i = 0; i < npx; i++) {
+        d[3 * i] = s[4 * i];
+        d[3 * i + 1] = s[4 * i + 1];
+        d[3 * i + 2] = s[4 * i + 2];
     }
 }
 
@@ -485,6 +526,9 @@ struct zw_pipe {
     // (batch b, frame i at host_src[b * n + i]); null outside such a call
     uint8_t* d_img2 = nullptr;
     const uint8_t* const* host_src = nullptr;
+    // RGBA frames staged as RGB (pack_rgb) and converted from that: set for a
+    // zw_pipe_encode_host call on the DMA-staging path (ZW_UPLOAD_PACK=0: off)
+    bool up_pack = false;
     uint8_t* img_buf(int parity) const { return parity ? d_img2 : d_img; }
 };
 
@@ -778,7 +822,8 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
     const int n = na;
     if (uploaded) HIPOK(hipStreamWaitEvent(s, uploaded, 0));
     if (timed) HIPOK(hipEventRecord(L.ev[0], s));
-    HIPOK(zwk_rgb2yuv(s, p->img_buf(parity) + F * p->img_stride, p->w, p->h, p->bpp, p->mbw, p->mbh,
+    const bool packed = uploaded && p->up_pack;  // (this chunk's frames arrived as RGB)
+    HIPOK(zwk_rgb2yuv(s, p->img_buf(parity) + F * p->img_stride, p->w, p->h, packed ? 3 : p->bpp, p->mbw, p->mbh,
                       p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->img_stride, p->ysz, p->csz,
                       n));
     if (read) HIPOK(hipEventRecord(read, s));
@@ -1075,13 +1120,18 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
                                 const int sl = k & 1;
                                 if (busy[sl] && (r = sdma_wait(p->ctx, L.usig[2 * u + sl]))) break;
                                 const uint8_t* src = p->host_src[(size_t)b * p->n + ca(c) + i];
-                                if (const void* dp = host_pinned(src, p->img_stride)) {
+                                size_t bytes = p->img_stride;
+                                if (p->up_pack) {  // RGBA -> RGB through the slot, pinned source or not
+                                    pack_rgb(L.ustage[2 * u + sl], src, (size_t)p->w * p->h);
+                                    src = L.ustage[2 * u + sl];
+                                    bytes = (size_t)p->w * p->h * 3;
+                                } else if (const void* dp = host_pinned(src, p->img_stride)) {
                                     src = (const uint8_t*)dp;
                                 } else {  // pageable: through the slot
                                     memcpy(L.ustage[2 * u + sl], src, p->img_stride);
                                     src = L.ustage[2 * u + sl];
                                 }
-                                r = sdma_h2d_start(p->ctx, dst + (size_t)i * p->img_stride, src, p->img_stride,
+                                r = sdma_h2d_start(p->ctx, dst + (size_t)i * p->img_stride, src, bytes,
                                                    L.usig[2 * u + sl]);
                                 busy[sl] = r == ZW_OK;
                             }
@@ -1369,9 +1419,14 @@ extern "C" int zw_pipe_encode_host(zw_pipe* p, int nb, const uint8_t* const* fra
             }
         }
     }
+    {
+        const char* pe = getenv("ZW_UPLOAD_PACK");
+        p->up_pack = p->bpp == 4 && !p->lanes.empty() && !p->lanes[0].ustage.empty() && !(pe && atoi(pe) == 0);
+    }
     p->host_src = frames;
     const int r = pipe_encode(p, nb);
     p->host_src = nullptr;
+    p->up_pack = false;
     return r;
 }
 

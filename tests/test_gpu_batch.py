@@ -210,20 +210,28 @@ def test_encode_webp_batch(ctx, color):
         assert outs[i] == want, f"frame {i}"
 
 
-@pytest.mark.parametrize("nb,lanes,chunk,up", [(1, "1", "4", "1"), (3, "2", "2", "3"), (4, "1", "3", "2"),
-                                                (5, "2", "4", "1")])
-def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk, up):
+@pytest.mark.parametrize("nb,lanes,chunk,up,pack,w,h", [(1, "1", "4", "1", "1", 96, 64), (3, "2", "2", "3", "0", 96, 64),
+                                                         (4, "1", "3", "2", "1", 96, 64), (5, "2", "4", "1", "1", 96, 64),
+                                                         (3, "1", "4", "2", "1", 101, 37)])
+def test_pipe_encode_host(ctx, monkeypatch, nb, lanes, chunk, up, pack, w, h):
     """zw_pipe_encode_host: nb batches streamed from host memory (batch b+1
     uploaded into the other input buffer while batch b encodes; lanes and chunks
     forced small so the uploads wait on rgb2yuv of batch b-2 per chunk).  Every
-    batch holds different frames; the last batch's bitstreams equal the oracle's."""
+    batch holds different frames; the last batch's bitstreams equal the oracle's.
+    pack = 1 (the default): the RGBA frames cross as RGB (alpha dropped on the
+    host, rgb2yuv reading 3 bytes a pixel; the 101-wide frames take its
+    per-sample path); pack = 0: as RGBA."""
     monkeypatch.setenv("ZW_PIPE_LANES", lanes)
     monkeypatch.setenv("ZW_PIPE_CHUNK", chunk)
     monkeypatch.setenv("ZW_ENC_ROWS", "0")
     monkeypatch.setenv("ZW_UPLOAD_THREADS", up)
-    w, h, n = 96, 64, 16  # (two lanes need >= 8 frames each)
+    monkeypatch.setenv("ZW_UPLOAD_PACK", pack)
+    n = 16  # (two lanes need >= 8 frames each)
     batches = [[synth_rgba(w, h, 0x5EED6000 + 16 * b + i, ("natural", "noise")[(b + i) % 2]) for i in range(n)]
                for b in range(nb)]
+    for b in range(nb):  # a varying alpha plane: the VP8 payload does not depend on it
+        for i in range(n):
+            batches[b][i].reshape(-1, 4)[:, 3] = (np.arange(w * h) * (7 + b + i)) & 255
     p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
     try:
         p.encode_host(batches)
@@ -338,14 +346,16 @@ def _hip():
     return h
 
 
-@pytest.mark.parametrize("kind", ["hostmalloc", "registered"])
-def test_pipe_encode_host_pinned(ctx, monkeypatch, kind):
-    """zw_pipe_encode_host from page-locked frames, which go to the DMA engines
-    without the staging copy: hipHostMalloc memory (what torch pin_memory
-    gives) and pageable memory registered with hipHostRegister (the engines
-    read it through the allocation's device pointer).  Bitstreams equal the
+@pytest.mark.parametrize("kind,pack", [("hostmalloc", "0"), ("registered", "0"), ("hostmalloc", "1")])
+def test_pipe_encode_host_pinned(ctx, monkeypatch, kind, pack):
+    """zw_pipe_encode_host from page-locked frames: with ZW_UPLOAD_PACK=0 they
+    go to the DMA engines without the staging copy -- hipHostMalloc memory (what
+    torch pin_memory gives) and pageable memory registered with hipHostRegister
+    (the engines read it through the allocation's device pointer); packed (the
+    default) they are staged as RGB like pageable frames.  Bitstreams equal the
     oracle's; every frame sits at an offset inside one allocation."""
     import ctypes
+    monkeypatch.setenv("ZW_UPLOAD_PACK", pack)
     monkeypatch.setenv("ZW_PIPE_LANES", "1")
     monkeypatch.setenv("ZW_ENC_ROWS", "0")
     w, h, n, nb = 96, 64, 8, 2

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host-resident (PCIe-inclusive) encode rate: zw_pipe_encode_host over 1024
 1080p frames x 3 batches, pageable frames and pinned frames, per uploader count.
-usage: python tools/host_res.py [frames] [batches]"""
+usage: python tools/host_res.py [frames] [batches] [hip]
+Legs: RGBA frames packed to RGB on the host (ZW_UPLOAD_PACK=1, the default) or sent as RGBA."""
 import os
 import sys
 import time
@@ -32,13 +33,18 @@ for i in range(F):
     t = torch.empty(w * h * 4, dtype=torch.uint8, pin_memory=True)
     t.numpy()[:] = pageable[i]
     pinned.append(t.numpy())
-for name, frames, sd in (("pageable sdma", pageable, "1"), ("pinned sdma", pinned, "1"),
-                         ("pageable hip", pageable, "0")):
+legs = (("pageable packed", pageable, "1", "1"), ("pinned packed", pinned, "1", "1"),
+        ("pageable rgba", pageable, "1", "0"), ("pinned rgba", pinned, "1", "0"))
+if len(sys.argv) > 3 and sys.argv[3] == "hip":
+    legs += (("pageable hip", pageable, "0", "0"),)
+for name, frames, sd, pk in legs:
     os.environ["ZW_UPLOAD_SDMA"] = sd
+    os.environ["ZW_UPLOAD_PACK"] = pk
     for u in ("1", "2", "4"):
         os.environ["ZW_UPLOAD_THREADS"] = u
         p.encode_host([frames])
         t0 = time.perf_counter()
         p.encode_host([frames] * NB)
         el = time.perf_counter() - t0
-        print(f"{name} U={u}: {F * NB / el:.0f} encodes/s ({F * NB * w * h * 4 / el / 1e9:.1f} GB/s H2D)", flush=True)
+        bpp = 3 if pk == "1" else 4
+        print(f"{name} U={u}: {F * NB / el:.0f} encodes/s ({F * NB * w * h * bpp / el / 1e9:.1f} GB/s H2D)", flush=True)
