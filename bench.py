@@ -613,7 +613,8 @@ def host_resident(pipe, host_imgs, nb, w, h, q, m, seeds, digests):
     host memory, as WebPEncoder::encode(&[u8]) callers hand frames over
     (encoder/api.rs:1291).  Each of the batch's frames is its own pageable host
     buffer (frame i holds the synthetic frame seeds[i % D]); per batch every
-    frame crosses PCIe again.  Each lane's uploader thread copies batch b+1 into
+    frame crosses PCIe again; nb is the headline's batch count (--steps), so the
+    pipeline's fill and drain weigh as they do in `value`.  Each lane's uploader thread copies batch b+1 into
     the second device input buffer while batch b's passes run.  RGBA frames
     cross as RGB by default (the uploader drops the alpha bytes, which the VP8
     payload does not read, while staging; rgb2yuv reads 3 bytes a pixel):
@@ -1071,7 +1072,7 @@ def main():
             streams = [bytes(pipes[0][0].output(i)) for i in range(min(B, D))]  # VP8 frames, before container mode
             line["container_rgba"] = container_rgba(pipes[0][0], imgs, 2, w, h, q, m, seeds, digests)
             line["container_rgba"]["real_alpha"] = container_alpha(ctx, w, h, q, m, 256, 3, seeds, digests)
-            line["host_resident"] = host_resident(pipes[0][0], imgs, 3, w, h, q, m, seeds, digests)
+            line["host_resident"] = host_resident(pipes[0][0], imgs, max(3, a.steps), w, h, q, m, seeds, digests)
             for k in ("pageable", "pinned", "pinned_rgba"):  # against the HBM-resident headline
                 line["host_resident"][k]["of_value"] = line["host_resident"][k]["encodes_per_s"] / line["value"]
             line["seam_threads"] = seam_threads()

@@ -253,9 +253,45 @@ __attribute__((target("ssse3"))) static void pack_rgb_ssse3(uint8_t* d, const ui
         d[2] = s[2];
     }
 }
+// 32 pixels a step: in-lane shuffles, each 32-byte register compacted to its 24
+// bytes, three 32-byte streaming stores (`d` 32-byte aligned)
+__attribute__((target("avx2"))) static void pack_rgb_avx2(uint8_t* d, const uint8_t* s, size_t npx)
+{
+    const __m256i sh = _mm256_setr_epi8(0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -128, -128, -128, -128, 0, 1, 2, 4, 5,
+                                        6, 8, 9, 10, 12, 13, 14, -128, -128, -128, -128);
+    const __m256i cp = _mm256_setr_epi32(0, 1, 2, 4, 5, 6, 3, 7);  // dwords 0-5 valid
+    const __m256i ib0 = _mm256_setr_epi32(0, 0, 0, 0, 0, 0, 0, 1), ib1 = _mm256_setr_epi32(2, 3, 4, 5, 0, 0, 0, 0);
+    const __m256i ic1 = _mm256_setr_epi32(0, 0, 0, 0, 0, 1, 2, 3), ic2 = _mm256_setr_epi32(4, 5, 0, 0, 0, 0, 0, 0);
+    const __m256i ie2 = _mm256_setr_epi32(0, 0, 0, 1, 2, 3, 4, 5);
+    size_t i = 0;
+    for (; i + 32 <= npx; i += 32, s += 128, d += 96) {
+        const __m256i a = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)s), sh), cp);
+        const __m256i b =
+            _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(s + 32)), sh), cp);
+        const __m256i c =
+            _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(s + 64)), sh), cp);
+        const __m256i e =
+            _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(s + 96)), sh), cp);
+        _mm256_stream_si256((__m256i*)d, _mm256_blend_epi32(a, _mm256_permutevar8x32_epi32(b, ib0), 0xC0));
+        _mm256_stream_si256((__m256i*)(d + 32), _mm256_blend_epi32(_mm256_permutevar8x32_epi32(b, ib1),
+                                                                   _mm256_permutevar8x32_epi32(c, ic1), 0xF0));
+        _mm256_stream_si256((__m256i*)(d + 64), _mm256_blend_epi32(_mm256_permutevar8x32_epi32(c, ic2),
+                                                                   _mm256_permutevar8x32_epi32(e, ie2), 0xFC));
+    }
+    _mm_sfence();
+    for (; i < npx; i++, s += 4, d += 3) {
+        d[0] = s[0];
+        d[1] = s[1];
+        d[2] = s[2];
+    }
+}
 static void pack_rgb(uint8_t* d, const uint8_t* s, size_t npx)
 {
-    static const bool ssse3 = __builtin_cpu_supports("ssse3");
+    static const bool avx2 = __builtin_cpu_supports("avx2"), ssse3 = __builtin_cpu_supports("ssse3");
+    if (avx2 && ((uintptr_t)d & 31) == 0) {
+        pack_rgb_avx2(d, s, npx);
+        return;
+    }
     if (ssse3 && ((uintptr_t)d & 15) == 0) {
         pack_rgb_ssse3(d, s, npx);
         return;

@@ -366,8 +366,11 @@ int zw_pipe_encode_repeat(zw_pipe *p, int n);
  * passes run, so the host->device copies overlap the kernels.  The outputs
  * (zw_pipe_output) are the last batch's.  Not with container output (ZW_EINVAL).
  * Replaces the caller-side loop WebPEncoder::encode(&[u8]) per frame
- * (encoder/api.rs:1291) for a stream of host frames.  Page-locked frames
- * (hipHostMalloc / hipHostRegister) are read by the DMA engines directly.
+ * (encoder/api.rs:1291) for a stream of host frames.  RGBA frames cross
+ * PCIe as RGB: the uploader drops the alpha bytes (which the VP8 payload
+ * does not read) while staging each frame in pinned memory.  With
+ * ZW_UPLOAD_PACK=0 they cross as RGBA, and page-locked frames (hipHostMalloc
+ * / hipHostRegister) are then read by the DMA engines directly.
  * After ZW_EDEVICE (a copy that did not complete in time) a DMA engine may
  * still read the caller's frames: keep them allocated for the process's
  * lifetime, and destroy the context (its device buffers are then leaked, not

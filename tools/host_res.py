@@ -40,7 +40,7 @@ if len(sys.argv) > 3 and sys.argv[3] == "hip":
 for name, frames, sd, pk in legs:
     os.environ["ZW_UPLOAD_SDMA"] = sd
     os.environ["ZW_UPLOAD_PACK"] = pk
-    for u in ("1", "2", "4"):
+    for u in os.environ.get("HR_UPLOADERS", "1,2,4").split(","):
         os.environ["ZW_UPLOAD_THREADS"] = u
         p.encode_host([frames])
         t0 = time.perf_counter()
