@@ -90,6 +90,24 @@ struct XmbLds : XmbLev<NL> {
 #define XI4_COUNT 0
 #define XI4_DONE 1
 #define XI4_LIST 64
+// Orderings of the queue counters.  Relaxed is enough: the queue entries come
+// from the previous kernel on the stream (the launch boundary makes them
+// visible), a workgroup reads the count before its own done-increment in
+// program order, and nothing this kernel writes is published through the
+// counters.  Acquire / release at agent scope cost an L2 invalidate / write-back
+// (buffer_inv / buffer_wbl2) in each of up to 1 024 workgroups.
+#ifndef XI4_STRICT
+#define XI4_STRICT 0
+#endif
+#if XI4_STRICT
+#define XI4_ACQ __ATOMIC_ACQUIRE
+#define XI4_ACQREL __ATOMIC_ACQ_REL
+#define XI4_REL __ATOMIC_RELEASE
+#else
+#define XI4_ACQ __ATOMIC_RELAXED
+#define XI4_ACQREL __ATOMIC_RELAXED
+#define XI4_REL __ATOMIC_RELAXED
+#endif
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
 DI uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
@@ -666,7 +684,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* _
     const uint32_t cap = (uint32_t)((long long)nframes * nmb);
     // an overflowed count (a stale or shared queue: k_xform_mb flagged it) or an
     // entry outside this launch is not trusted: nothing is read through it
-    const uint32_t cnt = __hip_atomic_load(&i4q[XI4_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cnt = __hip_atomic_load(&i4q[XI4_COUNT], XI4_ACQ, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t n = cnt > cap ? 0u : cnt;
     const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
     const uint32_t nwaves = gridDim.x * XMB_WAVES;
@@ -789,10 +807,10 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* _
     // the last workgroup out zeroes the queue counters for the next launch
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t d = __hip_atomic_fetch_add(&i4q[XI4_DONE], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t d = __hip_atomic_fetch_add(&i4q[XI4_DONE], 1u, XI4_ACQREL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == gridDim.x - 1) {
             __hip_atomic_store(&i4q[XI4_COUNT], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&i4q[XI4_DONE], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&i4q[XI4_DONE], 0u, XI4_REL, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
