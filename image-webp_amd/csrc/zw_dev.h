@@ -1009,3 +1009,68 @@ DI int idct_g_exact(int x, int k)
         return w16(csel(j == 3, -base, base) + csel(j == 2, -nb, nb)) >> 3;
     }
 }
+
+// ---- quad-form 4x4 transform (lane q of a quad: row q of the pixels, column q of
+// the coefficients); the encoder's I4 candidates and k_xform_mb_i4
+DI int dot2v(uint32_t a, uint32_t b, int acc)  // v_dot2_i32_i16, both operands in VGPRs
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(acc));
+    return d;
+}
+// The quad's row-transform inputs broadcast to every lane: lane q forms
+// column q of the row stage (dct4x4 transform.rs:176) for rows 0..3, then the
+// column stage: c[r] = coefficient (r, q), natural index 4 r + q.
+DI void uvq_fdct(uint32_t A, uint32_t D, int q, int c[4])
+{
+    const bool odd = q & 1;
+    const zs2 k0 = {8, 8}, k2 = {8, -8}, k1 = {10704, 4434}, k3 = {4434, -10704};
+    // (arithmetic selects: lane-dependent ?: chains became divergent branches)
+    const uint32_t k = (uint32_t)sel4(q, (int)as_zu(k0), (int)as_zu(k1), (int)as_zu(k2), (int)as_zu(k3));
+    const int rnd = sel4(q, 0, 3625, 0, 1875);
+    const int sh = csel(odd, 10, 0);
+    // (csel, not ?: -- a select of two DPP results may be folded into one DPP
+    // of a select, which would take the source lane's choice)
+    int t[4];
+    t[0] = dot2v((uint32_t)csel(odd, qb0((int)D), qb0((int)A)), k, rnd) >> sh;
+    t[1] = dot2v((uint32_t)csel(odd, qb1((int)D), qb1((int)A)), k, rnd) >> sh;
+    t[2] = dot2v((uint32_t)csel(odd, qb2((int)D), qb2((int)A)), k, rnd) >> sh;
+    t[3] = dot2v((uint32_t)csel(odd, qb3((int)D), qb3((int)A)), k, rnd) >> sh;
+    const uint32_t X01 = pack_lo(t[0], t[1]), X32 = pack_lo(t[3], t[2]);
+    const zs2 XA = as_zs2(X01) + as_zs2(X32), XD = as_zs2(X01) - as_zs2(X32);
+    const zs2 k1p = {1, 1}, k1m = {1, -1}, k2a = {5352, 2217}, k2b = {2217, -5352};
+    c[0] = dot2(XA, k1p, 7) >> 4;
+    c[2] = dot2(XA, k1m, 7) >> 4;
+    c[1] = (dot2(XD, k2a, 12000) >> 16) + ((as_zu(XD) & 0xffffu) != 0u ? 1 : 0);
+    c[3] = dot2(XD, k2b, 51000) >> 16;
+}
+
+// idct4x4 (transform.rs:19) of the quad's dequantised columns (lane q holds
+// column q, rows 0..3), then the reconstruction clamp(pred + residual) of row q
+// as i16 pairs (x0, x1), (x3, x2).
+DI void uvq_idct_recon(const int dq[4], uint32_t p01, uint32_t p32, int q, uint32_t& r01, uint32_t& r32)
+{
+    uint32_t lo, hi;
+    {
+        const int x0 = dq[0], x1 = dq[1], x2 = dq[2], x3 = dq[3];
+        const int a1 = x0 + x2, b1 = x0 - x2;
+        const int c1 = (m24(x1, 35468) >> 16) - (x3 + (m24(x3, 20091) >> 16));
+        const int d1 = (x1 + (m24(x1, 20091) >> 16)) + (m24(x3, 35468) >> 16);
+        lo = pack_lo(a1 + d1, b1 + c1);
+        hi = pack_lo(b1 - c1, a1 - d1);
+    }
+    // row q of every column: the lane of column j holds it in lo (rows 0, 1) or hi (rows 2, 3)
+    const bool upper = q >= 2;
+    const uint32_t off = 16u * (uint32_t)(q & 1);
+    const int y0 = __builtin_amdgcn_sbfe(csel(upper, qb0((int)hi), qb0((int)lo)), off, 16);
+    const int y1 = __builtin_amdgcn_sbfe(csel(upper, qb1((int)hi), qb1((int)lo)), off, 16);
+    const int y2 = __builtin_amdgcn_sbfe(csel(upper, qb2((int)hi), qb2((int)lo)), off, 16);
+    const int y3 = __builtin_amdgcn_sbfe(csel(upper, qb3((int)hi), qb3((int)lo)), off, 16);
+    const int a1 = y0 + y2, b1 = y0 - y2;
+    const int c1 = (m24(y1, 35468) >> 16) - (y3 + (m24(y3, 20091) >> 16));
+    const int d1 = (y1 + (m24(y1, 20091) >> 16)) + (m24(y3, 35468) >> 16);
+    const int o0 = (a1 + d1 + 4) >> 3, o1 = (b1 + c1 + 4) >> 3, o2 = (b1 - c1 + 4) >> 3, o3 = (a1 - d1 + 4) >> 3;
+    r01 = clamp_pk(add_pk(pack_lo(o0, o1), p01));
+    r32 = clamp_pk(add_pk(pack_lo(o3, o2), p32));
+}
+

@@ -44,8 +44,8 @@ hipError_t zwk_fdct_quant(hipStream_t s, const void* src, const void* pred, size
                           void* levels, void* recon, int cus);
 hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp, int w,
                         int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw, int mbh, int nframes,
-                        int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, uint32_t* queue, uint32_t* qerr,
-                        int variant);
+                        int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV, uint32_t* queue, int qp,
+                        uint32_t* qerr, int variant);
 size_t zwk_xform_mb_seg_bytes(void);
 size_t zwk_xform_mb_queue_bytes(int mbw, int mbh, int nframes);
 void zwk_xform_mb_pack_segs(const ZwMatrix* m, int n, void* out);
@@ -2092,6 +2092,7 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
     const size_t qb = zwk_xform_mb_queue_bytes((int)mbw, (int)mbh, nframes);
     void* q = nullptr;
     zw_ctx::XmbQueue* qe = nullptr;
+    int qp = 0;
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
         if (!ctx->xmb_err) {
@@ -2134,20 +2135,23 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
         qe = e;
         if (qe->dirty) HIPOK(hipMemsetAsync(q, 0, 16, ls));
         qe->dirty = true;
+        qp = qe->parity;
         // test hook: a stale count past this launch's MBs, as a shared queue would leave
         if (getenv("ZW_XMB_FORCE_OVERFLOW")) {
             const uint32_t stale = (uint32_t)((size_t)nframes * mbw * mbh);
-            HIPOK(hipMemcpyAsync(q, &stale, 4, hipMemcpyHostToDevice, ls));
+            HIPOK(hipMemcpyAsync((uint32_t*)q + qp, &stale, 4, hipMemcpyHostToDevice, ls));
             HIPOK(hipStreamSynchronize(ls));  // (the source is on this stack)
         }
     }
     HIPOK(zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp, (int)w, (int)h,
                        img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes, (int16_t*)d_levels,
-                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, ctx->xmb_err_dev,
+                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, qp, ctx->xmb_err_dev,
                        xmb_variant()));
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
-        qe->dirty = false;  // both kernels queued: the pair leaves the counters zero
+        // both kernels queued: the pair leaves count qp ^ 1 zero for the next launch
+        qe->dirty = false;
+        qe->parity ^= 1;
     }
     return ZW_OK;
 }

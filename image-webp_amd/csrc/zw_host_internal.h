@@ -35,6 +35,7 @@ struct zw_ctx {
         void* buf = nullptr;
         size_t cap = 0;
         bool dirty = true;  // counters not known to be zero: reset on the stream first
+        int parity = 0;     // the count the next launch appends to (k_xform_mb's qp)
         uint64_t used = 0;  // xmb_clock at the last launch (LRU eviction past 8 streams)
     };
     std::deque<XmbQueue> xmb_q;  // (a deque: entries stay put while others are added)

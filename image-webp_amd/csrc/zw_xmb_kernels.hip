@@ -84,29 +84,20 @@ struct XmbLds : XmbLev<NL> {
 };
 
 // k_xform_mb_i4: one I4 MB per lane.  Queue
-// layout (u32 words): [0] count (k_xform_mb appends), [1] workgroups done,
-// [64..] global MB indexes.  Zero counters on entry; k_xform_mb_i4's last
-// workgroup zeroes them for the next launch.
-#define XI4_COUNT 0
-#define XI4_DONE 1
+// layout (u32 words): [0], [1] the counts of the queue's even / odd launches
+// (k_xform_mb appends to count qp), [64..] global MB indexes.  Both counts
+// are zero before a queue's first launch; each launch's drain kernel zeroes
+// the other parity's count -- the previous launch's, whose drain has finished
+// (stream order) and which the next launch uses -- so no kernel needs to
+// know when every workgroup of the launch is done.
 #define XI4_LIST 64
-// Orderings of the queue counters.  Relaxed is enough: the queue entries come
-// from the previous kernel on the stream (the launch boundary makes them
-// visible), a workgroup reads the count before its own done-increment in
-// program order, and nothing this kernel writes is published through the
-// counters.  Acquire / release at agent scope cost an L2 invalidate / write-back
-// (buffer_inv / buffer_wbl2) in each of up to 1 024 workgroups.
-#ifndef XI4_STRICT
-#define XI4_STRICT 0
-#endif
-#if XI4_STRICT
-#define XI4_ACQ __ATOMIC_ACQUIRE
-#define XI4_ACQREL __ATOMIC_ACQ_REL
-#define XI4_REL __ATOMIC_RELEASE
-#else
+// The drain kernel's count read is relaxed: the queue entries come from the
+// previous kernel on the stream, whose writes the launch boundary makes
+// visible (an acquire at agent scope costs an L2 invalidate in every
+// workgroup).
 #define XI4_ACQ __ATOMIC_RELAXED
-#define XI4_ACQREL __ATOMIC_RELAXED
-#define XI4_REL __ATOMIC_RELAXED
+#ifndef XI4_QUAD
+#define XI4_QUAD 1  // 1: k_xform_mb_i4q drains the queue; 0: k_xform_mb_i4 (one MB per lane)
 #endif
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
@@ -332,7 +323,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U, const uint8_t* __restrict__ V, int w, int h,
     size_t img_stride, bool runs, const uint8_t* __restrict__ recs, const XmbSeg* __restrict__ segs, int mbw, int mbh, int nframes,
     int16_t* __restrict__ levels, uint8_t* __restrict__ RY, uint8_t* __restrict__ RU, uint8_t* __restrict__ RV,
-    uint32_t* __restrict__ i4q, uint32_t* __restrict__ qerr)
+    uint32_t* __restrict__ i4q, int qp, uint32_t* __restrict__ qerr)
 {
     // (the copy calibration always stages: the same bytes in and out, levels as one
     // contiguous run -- the ceiling for moving them)
@@ -464,7 +455,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             if (b) {
                 uint32_t base = 0;
                 if (lane == 0)
-                    base = __hip_atomic_fetch_add(&i4q[XI4_COUNT], (uint32_t)__popcll(b), __ATOMIC_RELAXED,
+                    base = __hip_atomic_fetch_add(&i4q[qp], (uint32_t)__popcll(b), __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
                 base = (uint32_t)__shfl((int)base, 0);
                 const int rank = __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u);
@@ -672,7 +663,7 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
 __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* __restrict__ recs,
                                                               const XmbSeg* __restrict__ segs, int mbw, int mbh,
                                                               int nframes, int16_t* __restrict__ levels,
-                                                              uint8_t* __restrict__ RY, uint32_t* __restrict__ i4q)
+                                                              uint8_t* __restrict__ RY, uint32_t* __restrict__ i4q, int qp)
 {
     __shared__ uint32_t vvs[XMB_WAVES][10][64];  // per lane: the 39-value vector (word q of lane l at [q][l])
     __shared__ uint8_t i4idx[10][16];            // d_I4_IDX
@@ -684,7 +675,8 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* _
     const uint32_t cap = (uint32_t)((long long)nframes * nmb);
     // an overflowed count (a stale or shared queue: k_xform_mb flagged it) or an
     // entry outside this launch is not trusted: nothing is read through it
-    const uint32_t cnt = __hip_atomic_load(&i4q[XI4_COUNT], XI4_ACQ, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cnt = __hip_atomic_load(&i4q[qp], XI4_ACQ, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&i4q[qp ^ 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t n = cnt > cap ? 0u : cnt;
     const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
     const uint32_t nwaves = gridDim.x * XMB_WAVES;
@@ -804,14 +796,182 @@ __global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4(const uint8_t* _
             lc[2] = lc[3];
         }
     }
-    // the last workgroup out zeroes the queue counters for the next launch
+}
+
+// The same I4 MBs in quad form (the default, XI4_QUAD): 8 MBs a wave, 8 lanes
+// an MB -- two quads, one per block of the current x+2y anti-diagonal, lane q
+// of a quad holding row q of the block's pixels and column q of its
+// coefficients (uvq_fdct / uvq_idct_recon, the encoder's I4 candidate form).
+// An MB's chain is 10 steps of a quarter block each instead of 16 whole
+// blocks, and the queue's MBs spread over 8x the waves: the one-MB-per-lane
+// form above is bound by that chain (one wave a SIMD issuing a serial
+// 16-block walk), this one by issue.  Per MB in LDS: the reconstruction with
+// its borders (row 0 the pixels above, byte column 8 + x for pixel x, so a
+// block's row is one aligned word and its left neighbour byte 3 of the word
+// before), the source luma, the 16 blocks' levels as they leave, the record.
+#define XQ_MBS 8
+struct XqMb {
+    uint32_t buf[17][8];  // cols 7 (left / corner), 8..23 (the MB), 24..27 (above-right)
+    uint32_t src[16][4];
+    uint32_t lev[16][8];  // blocks 0..15, zigzag i16 pairs (the first 512 B of the MB's levels)
+    uint32_t rec[16];     // record words 0..15
+};
+__global__ __launch_bounds__(64 * XMB_WAVES) void k_xform_mb_i4q(const uint8_t* __restrict__ recs,
+                                                               const XmbSeg* __restrict__ segs, int mbw, int mbh,
+                                                               int nframes, int16_t* __restrict__ levels,
+                                                               uint8_t* __restrict__ RY, uint32_t* __restrict__ i4q, int qp)
+{
+    __shared__ XqMb qm[XMB_WAVES][XQ_MBS];
+    __shared__ uint32_t vvs[XMB_WAVES][10][64];  // per lane: the 39-value vector (word w of lane l at [w][l])
+    __shared__ uint8_t i4idx[10][16];            // d_I4_IDX
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < 40) ((uint32_t*)i4idx)[threadIdx.x] = ((const uint32_t*)d_I4_IDX)[threadIdx.x];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t d = __hip_atomic_fetch_add(&i4q[XI4_DONE], 1u, XI4_ACQREL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == gridDim.x - 1) {
-            __hip_atomic_store(&i4q[XI4_COUNT], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&i4q[XI4_DONE], 0u, XI4_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint8_t* vvb = (const uint8_t*)&vvs[wv][0][0];
+    const int mi = lane >> 3, j8 = lane & 7, slot = (lane >> 2) & 1, q = lane & 3;
+    XqMb& M = qm[wv][mi];
+    const int nmb = mbw * mbh;
+    const uint32_t cap = (uint32_t)((long long)nframes * nmb);
+    const uint32_t cnt = __hip_atomic_load(&i4q[qp], XI4_ACQ, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(&i4q[qp ^ 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = cnt > cap ? 0u : cnt;
+    const size_t ys = (size_t)mbw * 16, ysz = ys * mbh * 16;
+    const uint32_t nwaves = gridDim.x * XMB_WAVES;
+#pragma unroll 1
+    for (uint32_t k = XQ_MBS * (blockIdx.x * XMB_WAVES + wv); k < n; k += XQ_MBS * nwaves) {
+        // every lane runs every step (the quads' DPP reads need their whole quad);
+        // an MB slot past the queue's end or with an entry outside the launch
+        // computes on zeros and stores nothing
+        const bool have = k + mi < n;
+        uint32_t gm = have ? i4q[XI4_LIST + k + mi] : 0u;
+        const bool valid = have && gm < cap;
+        gm = valid ? gm : 0u;
+        const int f = (int)(gm / nmb), rr = (int)(gm % nmb), mby = rr / mbw, x = rr % mbw;
+        uint8_t* ymb = RY + f * ysz + (size_t)mby * 16 * ys + (size_t)x * 16;
+        {
+            v4u r4 = {0u, 0u, 0u, 0u}, s0 = r4, s1 = r4;
+            if (valid) {
+                if (j8 < 4) r4 = *((const v4u*)(recs + (size_t)gm * 96) + j8);
+                s0 = *(const v4u*)(ymb + (size_t)(2 * j8) * ys);  // (k_xform_mb left the source luma here)
+                s1 = *(const v4u*)(ymb + (size_t)(2 * j8 + 1) * ys);
+            }
+            if (j8 < 4) *(v4u*)&M.rec[4 * j8] = r4;
+            *(v4u*)M.src[2 * j8] = s0;
+            *(v4u*)M.src[2 * j8 + 1] = s1;
         }
+        wsync();
+        // borders: row 0 = corner, the 16 pixels above, the 4 above-right; the
+        // left column down col 7; blocks (3, by > 0) read the above-right 4 too
+        // (rows 4, 8, 12), as the reference's top-right of the right column
+        if (j8 == 0) M.buf[0][1] = (M.rec[5] & 255u) << 24;
+        if (j8 < 4) M.buf[0][2 + j8] = M.rec[6 + j8];
+        if (j8 == 4) M.buf[0][6] = M.rec[10];
+        if (j8 > 4) M.buf[4 * (j8 - 4)][6] = M.rec[10];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int r = 2 * j8 + t;
+            M.buf[1 + r][1] = ((M.rec[11 + (r >> 2)] >> (8 * (r & 3))) & 255u) << 24;
+        }
+        const int seg = (int)((M.rec[0] >> 16) & 3u);
+        XmbMat my1;
+        {
+            const v4u m0 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1), m1 = *((const v4u*)&segs[(size_t)f * 4 + seg].y1 + 1);
+            my1.iq[0] = (int)m0.x; my1.iq[1] = (int)m0.y; my1.bp[0] = (int)m0.z; my1.bp[1] = (int)m0.w;
+            my1.bn[0] = (int)m1.x; my1.bn[1] = (int)m1.y; my1.q[0] = (int)m1.z; my1.q[1] = (int)m1.w;
+        }
+        const uint32_t bp01 = M.rec[1], bp23 = M.rec[2];
+        wsync();
+#pragma unroll 1
+        for (int s = 0; s < 10; s++) {
+            const int sbyA = s < 4 ? 0 : (s - 2) >> 1, sbxA = s - 2 * sbyA;
+            const bool act = slot == 0 || (s >= 2 && s <= 7);
+            const int bx = act ? (slot ? sbxA - 2 : sbxA) : 0, by = act ? (slot ? sbyA + 1 : sbyA) : 0;
+            const int sm = (int)((((by < 2 ? bp01 : bp23) >> (16 * (by & 1))) >> (4 * bx)) & 15u);
+            // the 13 edges: left column bottom-up, corner, top 4 + top-right 4
+            const uint32_t* ra = M.buf[4 * by];
+            const uint32_t wc = ra[1 + bx], T = ra[2 + bx], TR = ra[3 + bx];
+            uint32_t Lr[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) Lr[r] = M.buf[1 + 4 * by + r][1 + bx] >> 24;
+            const uint32_t sw = M.src[4 * by + q][bx];
+            int E[13];
+#pragma unroll
+            for (int t = 0; t < 4; t++) E[t] = (int)Lr[3 - t];
+            E[4] = (int)(wc >> 24);
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                E[5 + t] = (int)byte_of(T, t);
+                E[9 + t] = (int)byte_of(TR, t);
+            }
+#pragma unroll
+            for (int w = 0; w < 10; w++) {
+                uint32_t wd = 0;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int i = 4 * w + t;
+                    int v;
+                    if (i < 13) v = E[i];
+                    else if (i < 24) v = (E[i - 13] + 2 * E[i - 12] + E[i - 11] + 2) >> 2;
+                    else if (i < 36) v = (E[i - 24] + E[i - 23] + 1) >> 1;
+                    else if (i == 36) v = (E[11] + 3 * E[12] + 2) >> 2;
+                    else if (i == 37) v = (E[1] + 3 * E[0] + 2) >> 2;
+                    else if (i == 38) v = (4 + E[0] + E[1] + E[2] + E[3] + E[5] + E[6] + E[7] + E[8]) >> 3;
+                    else v = 0;
+                    wd |= (uint32_t)v << (8 * t);
+                }
+                vvs[wv][w][lane] = wd;
+            }
+            // row q of the prediction (TrueMotion: clamp(L[q] + T[t] - corner))
+            const int Lq = sel4(q, (int)Lr[0], (int)Lr[1], (int)Lr[2], (int)Lr[3]);
+            uint32_t pw = 0;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int idx = i4idx[sm][4 * q + t];
+                int v;
+                if (idx == 254) v = clamp255(Lq + E[5 + t] - E[4]);
+                else {
+                    const int ii = idx == 255 ? 38 : idx;
+                    v = vvb[((ii >> 2) * 64 + lane) * 4 + (ii & 3)];
+                }
+                pw |= (uint32_t)v << (8 * t);
+            }
+            const uint32_t p01 = __builtin_amdgcn_perm(0u, pw, 0x0c010c00u), p32 = __builtin_amdgcn_perm(0u, pw, 0x0c020c03u);
+            const uint32_t R01 = sub_pk(pr01(sw), p01), R32 = sub_pk(pr32(sw), p32);
+            int cf[4];
+            uvq_fdct(add_pk(R01, R32), sub_pk(R01, R32), q, cf);  // cf[r]: coefficient (r, q), natural index 4 r + q
+            int lv[4], dq[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                // (selects, not my1.x[tk]: a lane-varying index would put my1 in scratch)
+                const bool dc = r == 0 && q == 0;
+                const int c = cf[r];
+                const int iq = dc ? my1.iq[0] : my1.iq[1], bp = dc ? my1.bp[0] : my1.bp[1];
+                const int bn = dc ? my1.bn[0] : my1.bn[1], qq = dc ? my1.q[0] : my1.q[1];
+                lv[r] = (__mul24(c, iq) + (c < 0 ? bn : bp)) >> 17;
+                dq[r] = m24(lv[r], qq);
+            }
+            uint32_t r01, r32;
+            uvq_idct_recon(dq, p01, p32, q, r01, r32);
+            if (act) {
+                M.buf[1 + 4 * by + q][2 + bx] = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
+                int16_t* lp = (int16_t*)M.lev[4 * by + bx];
+#pragma unroll
+                for (int r = 0; r < 4; r++) lp[izz_of(4 * r + q)] = (int16_t)lv[r];
+            }
+            wsync();
+        }
+        if (valid) {
+            v4u* lo = (v4u*)(levels + (size_t)gm * 400);
+#pragma unroll
+            for (int t = 0; t < 4; t++) __builtin_nontemporal_store(*((const v4u*)&M.lev[0][0] + 4 * j8 + t), lo + 4 * j8 + t);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const int r = 2 * j8 + t;
+                const v2u a = *(const v2u*)&M.buf[1 + r][2], b = *(const v2u*)&M.buf[1 + r][4];
+                __builtin_nontemporal_store(v4u{a.x, a.y, b.x, b.y}, (v4u*)(ymb + (size_t)r * ys));
+            }
+        }
+        wsync();
     }
 }
 
@@ -849,7 +1009,7 @@ extern "C" void zwk_xform_mb_pack_segs(const ZwMatrix* m /* [n][4][3] */, int n,
 extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_t* U, const uint8_t* V, int src_bpp,
                                    int w, int h, size_t img_stride, const uint8_t* recs, const void* segs, int mbw,
                                    int mbh, int nframes, int16_t* levels, uint8_t* RY, uint8_t* RU, uint8_t* RV,
-                                   uint32_t* queue, uint32_t* qerr, int variant)
+                                   uint32_t* queue, int qp, uint32_t* qerr, int variant)
 {
     const long long waves = (long long)nframes * mbh * ((mbw + XMB_MBS - 1) / XMB_MBS);
     const unsigned grid = (unsigned)((waves + XMB_WAVES - 1) / XMB_WAVES);
@@ -863,7 +1023,7 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     const bool runs = src_bpp != 0 && (uintptr_t)Y % ra == 0 && img_stride % ra == 0 && ((size_t)w * src_bpp) % ra == 0;
 #define XMB_LAUNCH(SRC, CP)                                                                                         \
     hipLaunchKernelGGL((k_xform_mb<SRC, CP>), dim3(grid), dim3(64 * XMB_WAVES), 0, s, Y, U, V, w, h, img_stride, runs,  \
-                       recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue, qerr)
+                       recs, sg, mbw, mbh, nframes, levels, RY, RU, RV, queue, qp, qerr)
     if (src_bpp == 0) {
         if (copy) XMB_LAUNCH(0, 99);
         else XMB_LAUNCH(0, 0);
@@ -884,11 +1044,17 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     }
 #undef XMB_LAUNCH
     if (copy) return hipGetLastError();
-    // the I4 queue: waves of 64 MBs; one per 64 x 16 MBs of the launch (an I4
-    // share up to 1/16 runs in one pass over the grid), at most 1024 workgroups
+    // the I4 queue: waves of XQ_MBS (quad form) / 64 MBs; grid for an I4 share up
+    // to 1/16 in one pass over it, at most 4096 / 1024 workgroups
     const long long nmbs = (long long)nframes * mbw * mbh;
-    const unsigned g4 = (unsigned)min((nmbs + 64 * 16 * XMB_WAVES - 1) / (64 * 16 * XMB_WAVES), 1024LL);
-    hipLaunchKernelGGL(k_xform_mb_i4, dim3(g4), dim3(64 * XMB_WAVES), 0, s, recs, sg, mbw, mbh, nframes, levels, RY,
-                       queue);
+    if (XI4_QUAD) {
+        const unsigned g4 = (unsigned)min((nmbs + XQ_MBS * 16 * XMB_WAVES - 1) / (XQ_MBS * 16 * XMB_WAVES), 4096LL);
+        hipLaunchKernelGGL(k_xform_mb_i4q, dim3(g4), dim3(64 * XMB_WAVES), 0, s, recs, sg, mbw, mbh, nframes, levels,
+                           RY, queue, qp);
+    } else {
+        const unsigned g4 = (unsigned)min((nmbs + 64 * 16 * XMB_WAVES - 1) / (64 * 16 * XMB_WAVES), 1024LL);
+        hipLaunchKernelGGL(k_xform_mb_i4, dim3(g4), dim3(64 * XMB_WAVES), 0, s, recs, sg, mbw, mbh, nframes, levels,
+                           RY, queue, qp);
+    }
     return hipGetLastError();
 }
