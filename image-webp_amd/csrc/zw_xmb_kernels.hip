@@ -336,14 +336,17 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
     constexpr bool HALF = STG && !COPY && XMB_HALF_STAGE;
     constexpr int NL = !STG ? 0 : (HALF ? XMB_MBS / 2 : XMB_MBS);
     __shared__ XmbLds<NL> lds[XMB_WAVES];
+    // (the wave's group index made wave-uniform, so its decomposition runs on the
+    // scalar unit in 32 bits: as per-lane 64-bit divisions it cost ~180 VALU a wave)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     XmbLds<NL>& L = lds[wv];
-    const int ngx = (mbw + XMB_MBS - 1) / XMB_MBS;
-    const long long id = (long long)blockIdx.x * XMB_WAVES + wv;
-    if (id >= (long long)nframes * mbh * ngx) return;
+    const uint32_t ngx = (uint32_t)(mbw + XMB_MBS - 1) / XMB_MBS;
+    // (< 2^31: the host checks the group count)
+    const uint32_t id = blockIdx.x * XMB_WAVES + (uint32_t)wv;
+    if (id >= (uint32_t)nframes * (uint32_t)mbh * ngx) return;
     const int gx = (int)(id % ngx);
-    const long long rest = id / ngx;
-    const int mby = (int)(rest % mbh), f = (int)(rest / mbh);
+    const uint32_t rest = id / ngx;
+    const int mby = (int)(rest % (uint32_t)mbh), f = (int)(rest / (uint32_t)mbh);
     const int x0 = gx * XMB_MBS, nact = min(XMB_MBS, mbw - x0);
     const int nmb = mbw * mbh;
     const size_t ys = (size_t)mbw * 16, cs = (size_t)mbw * 8;
@@ -1014,6 +1017,7 @@ extern "C" hipError_t zwk_xform_mb(hipStream_t s, const uint8_t* Y, const uint8_
     const long long waves = (long long)nframes * mbh * ((mbw + XMB_MBS - 1) / XMB_MBS);
     const unsigned grid = (unsigned)((waves + XMB_WAVES - 1) / XMB_WAVES);
     if (grid == 0) return hipSuccess;
+    if (waves >= (1LL << 31)) return hipErrorInvalidValue;  // (k_xform_mb indexes its groups in 32 bits)
     if (src_bpp != 0 && src_bpp != 3 && src_bpp != 4) return hipErrorInvalidValue;
     const XmbSeg* sg = (const XmbSeg*)segs;
     const bool copy = variant != 0;
