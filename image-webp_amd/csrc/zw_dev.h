@@ -97,6 +97,22 @@ __device__ __forceinline__ uint32_t pk_y2(uint32_t p)
     const uint32_t rg = __builtin_amdgcn_perm(0u, p, 0x0c010c00u);  // (R, G)
     return udot2(rg, 0x812341c7u /* (16839, 33059) */, ((p >> 16) & 255u) * 6420u + (1u << 15) + (16u << 16)) >> 16;
 }
+// Y of four pixels (0x..BBGGRR words) as one packed word.  Each coefficient
+// split into high and low bytes (16839 = 65:199, 33059 = 129:35, 6420 = 25:20)
+// makes the sum two v_dot4_u32_u8 and a shift-add; it stays below 2^24, so the
+// Y byte is byte 2 of it and two v_perm gather the four (equal to pk_y for
+// every (R, G, B): checked exhaustively).
+__device__ __forceinline__ uint32_t pk_y4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3)
+{
+    auto y = [](uint32_t p) {
+        const uint32_t hi = __builtin_amdgcn_udot4(p, 0x00198141u, 0u, false);
+        const uint32_t lo = __builtin_amdgcn_udot4(p, 0x001423c7u, (1u << 15) + (16u << 16), false);
+        return (hi << 8) + lo;
+    };
+    const uint32_t lo = __builtin_amdgcn_perm(y(p1), y(p0), 0x0c0c0602u);  // Y0, Y1 in bytes 0, 1
+    const uint32_t hi = __builtin_amdgcn_perm(y(p3), y(p2), 0x06020c0cu);  // Y2, Y3 in bytes 2, 3
+    return lo | hi;
+}
 // (U, V) bytes of the 2x2 of pixels a, b (row 0) and c, d (row 1): (s + 2^17) >> 18
 // of s = sum of pk_u / pk_v + (512 << 16)
 __device__ __forceinline__ void pk_uv4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t& u, uint32_t& v)

@@ -149,12 +149,9 @@ __global__ __launch_bounds__(256) void k_rgb2yuv_rows(const uint8_t* __restrict_
         uint32_t a[8], b[8];
         rgb_run8<BPP>(im + ((size_t)r0 * w + px0) * BPP, a);
         rgb_run8<BPP>(im + ((size_t)r1 * w + px0) * BPP, b);
-        uint32_t ya[2] = {0, 0}, yb[2] = {0, 0}, uw = 0, vw = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            ya[i >> 2] |= (uint32_t)pk_y(a[i]) << (8 * (i & 3));
-            yb[i >> 2] |= (uint32_t)pk_y(b[i]) << (8 * (i & 3));
-        }
+        const uint32_t ya[2] = {pk_y4(a[0], a[1], a[2], a[3]), pk_y4(a[4], a[5], a[6], a[7])};
+        const uint32_t yb[2] = {pk_y4(b[0], b[1], b[2], b[3]), pk_y4(b[4], b[5], b[6], b[7])};
+        uint32_t uw = 0, vw = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int su = pk_u(a[2 * j]) + pk_u(a[2 * j + 1]) + pk_u(b[2 * j]) + pk_u(b[2 * j + 1]) + (512 << 16);

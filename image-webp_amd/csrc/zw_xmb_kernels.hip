@@ -294,12 +294,11 @@ DI void rgb_item(const uint8_t* __restrict__ img, int w, int h, bool runs, int p
             cb[i] = px_at<BPP>(img, w, cxx, cy1);
         }
     }
-    ya[0] = ya[1] = yb[0] = yb[1] = uw = vw = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        ya[i >> 2] |= pk_y2(a[i]) << (8 * (i & 3));
-        yb[i >> 2] |= pk_y2(b[i]) << (8 * (i & 3));
-    }
+    uw = vw = 0;
+    ya[0] = pk_y4(a[0], a[1], a[2], a[3]);
+    ya[1] = pk_y4(a[4], a[5], a[6], a[7]);
+    yb[0] = pk_y4(b[0], b[1], b[2], b[3]);
+    yb[1] = pk_y4(b[4], b[5], b[6], b[7]);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         uint32_t u, v;
