@@ -101,6 +101,18 @@ struct XmbLds : XmbLev<NL> {
 #endif
 
 DI int qz(int c, const XmbMat& m, int t) { return (__mul24(c, m.iq[t]) + (c < 0 ? m.bn[t] : m.bp[t])) >> 17; }
+// A lane's quantiser matrix from LDS into registers (two 16-byte reads, pinned):
+// read through the reference, each coefficient's bias became a load at a
+// selected address (an LDS round trip per coefficient) instead of a select
+DI XmbMat ld_mat(const XmbMat& m)
+{
+    v4u a = *(const v4u*)&m, b = *((const v4u*)&m + 1);
+    asm volatile("" : "+v"(a), "+v"(b));
+    XmbMat r;
+    r.iq[0] = (int)a.x; r.iq[1] = (int)a.y; r.bp[0] = (int)a.z; r.bp[1] = (int)a.w;
+    r.bn[0] = (int)b.x; r.bn[1] = (int)b.y; r.q[0] = (int)b.z; r.q[1] = (int)b.w;
+    return r;
+}
 DI uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
 
 // byte pairs (b0, b1) and (b3, b2) of a row word as i16 pairs
@@ -482,7 +494,10 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const int mode = (int)((R[0] >> 8) & 255u);
             const int seg = (int)((R[0] >> 16) & 3u);
             const int has_top = (int)((R[0] >> 24) & 1u), has_left = (int)((R[0] >> 25) & 1u);
-            const XmbMat& muv = S[seg].uv;
+            // (in registers for the RGB(A) forms; the planes form keeps its 5 waves a SIMD)
+            XmbMat muv_r;
+            if constexpr (SRC != 0) muv_r = ld_mat(S[seg].uv);
+            const XmbMat& muv = SRC != 0 ? muv_r : S[seg].uv;
             const uint32_t* Tw = R + 16 + 4 * plane;  // top 8 at bytes 64 + 16*plane, left 8 right after
             const uint32_t st = bsum(Tw[0]) + bsum(Tw[1]), sl = bsum(Tw[2]) + bsum(Tw[3]);
             uint32_t pw[4], sw[4];
@@ -541,7 +556,9 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
             const int mode = (int)(R[0] & 255u);
             const int seg = (int)((R[0] >> 16) & 3u);
             const int has_top = (int)((R[0] >> 24) & 1u), has_left = (int)((R[0] >> 25) & 1u);
-            const XmbMat& my1 = S[seg].y1;
+            XmbMat my1_r;
+            if constexpr (SRC != 0) my1_r = ld_mat(S[seg].y1);
+            const XmbMat& my1 = SRC != 0 ? my1_r : S[seg].y1;
             int y2l = 0;
             if (mode != 4) {
                 uint32_t sw[4];
