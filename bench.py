@@ -26,7 +26,7 @@ timed region and the max time is taken with an all-reduce.
                    shard_range(T, r, N), in device batches of `--batch` frames.
 
 `roofline`: SURVEY.md 8(d)'s designated HBM-bound pass, the streaming
-DCT+quant pass over per-MB records (k_xform_mb + k_xform_mb_i4) on 256 frames
+DCT+quant pass over per-MB records (k_xform_mb + k_xform_mb_i4q) on 256 frames
 resident in HBM, BASELINE config 2's form: the synthetic RGBA frames in
 (convert_image_yuv fused), levels + reconstructed YUV out.  ALGORITHMIC bytes =
 the RGBA read (w*h*4 per frame) + levels 800 + recon 384 per MB (8(d)'s
@@ -279,7 +279,7 @@ def dct_quant_pass(ctx, torch, dev, frames, nmb, reps=5):
 
 def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, digests=None, imgs=None):
     """SURVEY 8(d)'s HBM-roofline pass: the streaming DCT+quant pass over per-MB
-    records (k_xform_mb + k_xform_mb_i4) on `frames` frames resident in HBM, in
+    records (k_xform_mb + k_xform_mb_i4q) on `frames` frames resident in HBM, in
     both source forms:
       "rgba": BASELINE config 2 -- the synthetic RGBA frames in, convert_image_yuv
               fused into the pass (zw_transform_quant_mbs_rgb_device); algorithmic
@@ -352,7 +352,7 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
         moved = src_moved + mbs * (1184 + XMB_RECORD_BYTES)
         ach = alg / (ms * 1e-3) / 1e9
         copy_gbs = moved / (ms_copy * 1e-3) / 1e9
-        return {"kernel": "k_xform_mb + k_xform_mb_i4", "source": name,
+        return {"kernel": "k_xform_mb + k_xform_mb_i4q", "source": name,
                 "workload": f"{frames} frames x {nmb} MBs ({w}x{h}), the timed encode's modes",
                 "mbs_per_launch": mbs, "alg_bytes_per_launch": alg, "alg_bytes_per_mb": alg / mbs,
                 "record_bytes_per_mb": XMB_RECORD_BYTES, "ms_per_launch": ms, "achieved": ach,
@@ -1042,7 +1042,7 @@ def main():
             xm = xa["rgba"]
             line["roofline"] = {"bound": "hbm", "achieved": xm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": xm["frac"], "traffic": pmc_traffic(XMB_PMC, xm["mbs_per_launch"]),
-                                "kernel": "k_xform_mb<RGBA> + k_xform_mb_i4 (BASELINE config 2: RGBA in, "
+                                "kernel": "k_xform_mb<RGBA> + k_xform_mb_i4q (BASELINE config 2: RGBA in, "
                                           "DCT/quant/IDCT, levels + reconstructed YUV out)",
                                 "workload": xm["workload"], "mbs_per_launch": xm["mbs_per_launch"],
                                 "alg_bytes_per_mb": xm["alg_bytes_per_mb"],
