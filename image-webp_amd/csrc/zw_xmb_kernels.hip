@@ -665,8 +665,18 @@ __global__ __launch_bounds__(64 * XMB_WAVES) XMB_ATTR void k_xform_mb(
         }
         uint8_t* Cf = (cp ? RV : RU) + f * csz + (size_t)(mby * 8 + cr) * cs + (x0 + 2 * cq) * 8;
         const v4u c4 = *(const v4u*)&L.ct[cp][cr][4 * cq];
-        if (REC_OUT && cn == 2) __builtin_nontemporal_store(c4, (v4u*)Cf);
-        else if (REC_OUT && cn == 1) __builtin_nontemporal_store(v2u{c4.x, c4.y}, (v2u*)Cf);
+#ifndef XMB_CHROMA_NT
+#define XMB_CHROMA_NT (SRC == 0)  // measured: RGBA 1.300-1.303 vs 1.310-1.316 ms plain; planes 1.04 vs 1.06-1.08 NT
+#endif
+        if (XMB_CHROMA_NT) {
+            if (REC_OUT && cn == 2) __builtin_nontemporal_store(c4, (v4u*)Cf);
+            else if (REC_OUT && cn == 1) __builtin_nontemporal_store(v2u{c4.x, c4.y}, (v2u*)Cf);
+        } else {
+            // (64-byte row pieces: the other half of each 128-byte line is the
+            // neighbouring group's, so the stores may merge in L2)
+            if (REC_OUT && cn == 2) *(v4u*)Cf = c4;
+            else if (REC_OUT && cn == 1) *(v2u*)Cf = v2u{c4.x, c4.y};
+        }
     }
 }
 
