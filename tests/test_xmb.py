@@ -226,6 +226,24 @@ def test_gpu_xform_mbs_errors(ctx):
 
 
 @pytest.mark.gpu
+def test_gpu_xform_mbs_i4_drain_at_scale(ctx):
+    """k_xform_mb_i4q over more I4 MBs than its grid takes in one pass (16
+    frames of 120 x 68 MBs, every MB I4: 130 560 queue entries; the grid is
+    sized for an I4 share of 1/16, 8 160 MBs a pass), then launches back to back on the same queue with
+    other I4 shares: each launch appends to its own parity's count and the
+    drain zeroes the other's, so every launch equals the oracle."""
+    import zwebp
+    for nf, mbw, mbh, i4, seed in ((16, 120, 68, 1.0, 1), (2, 120, 68, 0.0, 2), (3, 33, 17, 0.6, 3),
+                                   (1, 120, 68, 1.0, 4)):
+        y, u, v, recs, sq = _random_case(np.random.default_rng(seed), nf, mbw, mbh, i4)
+        got = zwebp.transform_quant_mbs(y, u, v, recs, sq, nf, mbw, mbh, ctx=ctx)
+        want = O.xform_mbs(y, u, v, recs, sq, nf, mbw, mbh)
+        for name, a, b in zip(("levels", "ry", "ru", "rv"), got, want):
+            bad = np.argwhere(a != b)
+            assert bad.size == 0, f"case {seed} {name}: {len(bad)} differences, first {bad[:4].tolist()}"
+
+
+@pytest.mark.gpu
 def test_gpu_xform_mbs_queue_overflow_reported(monkeypatch):
     """An I4 queue whose count is stale (test hook: preset past the launch's
     MBs, as a shared queue would leave it) makes k_xform_mb flag the context's
