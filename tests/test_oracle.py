@@ -522,3 +522,16 @@ def test_single_colour_file_kat(n):
     W.WebPFree.argtypes = [ctypes.c_void_p]
     W.WebPFree(p)
     assert np.array_equal(lw, rgb)
+
+
+def test_luma_dot4_split_equals_convert_image_yuv():
+    """The device's luma (pk_y4, zw_dev.h): each coefficient of yuv.rs's
+    (16839 R + 33059 G + 6420 B + 2^15 + (16 << 16)) >> 16 split into high and
+    low bytes for two v_dot4_u32_u8, the sum kept below 2^24 so its byte 2 is
+    Y -- equal for every (R, G, B)."""
+    v = np.arange(1 << 24, dtype=np.uint32)
+    r, g, b = v & 255, (v >> 8) & 255, (v >> 16) & 255
+    ref = (16839 * r + 33059 * g + 6420 * b + (1 << 15) + (16 << 16)) >> 16
+    s = ((65 * r + 129 * g + 25 * b) << 8) + (199 * r + 35 * g + 20 * b + (1 << 15) + (16 << 16))
+    assert (s < (1 << 24)).all()
+    assert np.array_equal((s >> 16) & 255, ref)
