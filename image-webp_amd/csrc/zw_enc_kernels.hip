@@ -431,6 +431,219 @@ extern "C" __global__ __launch_bounds__(256) void k_analysis(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// The same analysis, four MBs a wave (ZW_AN_FORM 4): 16 lanes an MB, lane j
+// working three of the MB's 48 (block, mode) items -- luma block j under DC
+// and under TM, chroma block j & 7 (U 0-3, V 4-7) under mode j >> 3 -- so every
+// lane has work and the four MBs' chains overlap.  Items, histograms and the
+// alpha are those of k_analysis above, computed in the same order.
+// ---------------------------------------------------------------------------
+// One item: its 16 coefficient bins (min(|c| >> 3, 31)), the count of bin 0 and the largest bin.
+DI void an_item(const AnalysisTile* A, bool luma, int mode, int b, bool ht, bool hl, int bins[16], int& z, int& vmax)
+{
+    const int pl = b >> 2;  // chroma plane
+    const int bb = luma ? b : (b & 3);
+    const int bx = luma ? (bb & 3) : (bb & 1), by = luma ? (bb >> 2) : (bb >> 1);
+    uint32_t st = 0, sl = 0;
+    if (luma) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            st = __builtin_amdgcn_sad_u8(A->ytop[w], 0u, st);
+            sl = __builtin_amdgcn_sad_u8(((const uint32_t*)A->yleft)[w], 0u, sl);
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            st = __builtin_amdgcn_sad_u8(A->ctop[pl][w], 0u, st);
+            sl = __builtin_amdgcn_sad_u8(((const uint32_t*)A->cleft[pl])[w], 0u, sl);
+        }
+    }
+    const uint32_t s2 = ht && hl ? st + sl : (ht ? 2 * st : 2 * sl);
+    const int dcv = (ht || hl) ? (luma ? (int)((s2 + 16) >> 5) : (int)((s2 + 8) >> 4)) : 0x80;
+    const int corner = A->corner[luma ? 0 : 1 + pl];
+    int d[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = by * 4 + i;
+        const uint32_t srow = luma ? A->y[r][bx] : A->c[pl][r][bx];
+        const int L = luma ? A->yleft[r] : A->cleft[pl][r];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int cidx = bx * 4 + j;
+            const uint32_t tw = luma ? A->ytop[cidx >> 2] : A->ctop[pl][cidx >> 2];
+            const int T = (int)((tw >> (8 * (cidx & 3))) & 255u);
+            const int tm = (ht && hl) ? clamp255(L + T - corner) : (hl ? L : (ht ? T : 129));
+            const int p = mode == 0 ? dcv : tm;
+            d[i * 4 + j] = (int)((srow >> (8 * j)) & 255u) - p;
+        }
+    }
+    int o[16];
+    fdct16_pk(d, o);
+    z = 0;
+    vmax = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        bins[k] = min(iabs(o[k]) >> 3, 31);
+        z += bins[k] == 0;
+        vmax = max(vmax, bins[k]);
+    }
+}
+DI int max8(int v)  // max within aligned 8-lane groups
+{
+    v = max(v, DPP(v, 0xB1));
+    v = max(v, DPP(v, 0x4E));
+    return max(v, DPP(v, 0x141));
+}
+DI int an_red8(int v)  // sum within aligned 8-lane groups
+{
+    v += DPP(v, 0xB1);
+    v += DPP(v, 0x4E);
+    return v + DPP(v, 0x141);
+}
+DI int max16(int v)
+{
+    v = max8(v);
+    return max(v, DPP(v, 0x140));
+}
+typedef unsigned an_v4u __attribute__((ext_vector_type(4)));
+typedef unsigned an_v2u __attribute__((ext_vector_type(2)));
+#ifndef ZW_AN4_GPW
+#define ZW_AN4_GPW 2  // 4-MB groups per wave
+#endif
+extern "C" __global__ __launch_bounds__(256) void k_analysis4(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
+                                                              const uint8_t* __restrict__ V, int mbw, int mbh,
+                                                              size_t ysz, size_t csz, uint8_t* __restrict__ alpha,
+                                                              uint32_t* __restrict__ histo)
+{
+    __shared__ AnalysisTile tile[4][4];   // [wave][MB]
+    __shared__ uint32_t hist[4][4][4][32];  // [wave][MB][histogram][bin] (only when some bin 0 is short)
+    __shared__ uint32_t ahist[256];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, mi = lane >> 4, j = lane & 15;
+    const int f = blockIdx.y;
+    const int nmb = mbw * mbh;
+    ahist[threadIdx.x] = 0;
+    __syncthreads();
+    const int ys = mbw * 16, cs = mbw * 8;
+    const uint8_t* Yf = Y + (size_t)f * ysz;
+    const uint8_t* Uf = U + (size_t)f * csz;
+    const uint8_t* Vf = V + (size_t)f * csz;
+    AnalysisTile* A = &tile[wv][mi];
+#pragma unroll 1
+    for (int it = 0; it < ZW_AN4_GPW; it++) {
+        const int mb = ((blockIdx.x * ZW_AN4_GPW + it) * 4 + wv) * 4 + mi;
+        const bool in = mb < nmb;
+        const int mbx = in ? mb % mbw : 0, mby = in ? mb / mbw : 0;
+        const bool ht = mby > 0, hl = mbx > 0;
+        // ---- stage the MB and its edges (lane j: luma row j, chroma row j & 7 of plane j >> 3)
+        {
+            const int pl = j >> 3, cr = j & 7;
+            const uint8_t* Cf = pl ? Vf : Uf;
+            an_v4u yr = {0u, 0u, 0u, 0u};
+            an_v2u cw = {0u, 0u};
+            uint32_t yl = 0, cl = 0;
+            if (in) {
+                const uint8_t* yp = Yf + (size_t)(mby * 16 + j) * ys + mbx * 16;
+                const uint8_t* cp = Cf + (size_t)(mby * 8 + cr) * cs + mbx * 8;
+                yr = *(const an_v4u*)yp;
+                cw = *(const an_v2u*)cp;
+                if (hl) {
+                    yl = yp[-1];
+                    cl = cp[-1];
+                }
+            }
+            wsync();  // (the previous group's reads of the tile are done)
+            *(an_v4u*)A->y[j] = yr;
+            *(an_v2u*)A->c[pl][cr] = cw;
+            A->yleft[j] = (uint8_t)yl;
+            A->cleft[pl][cr] = (uint8_t)cl;
+            if (j < 6) {
+                uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+                if (in && ht) {
+                    if (j == 0) {
+                        const an_v4u t = *(const an_v4u*)(Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16);
+                        t0 = t.x; t1 = t.y; t2 = t.z; t3 = t.w;
+                    } else if (j < 3) {
+                        const an_v2u t = *(const an_v2u*)((j == 1 ? Uf : Vf) + (size_t)(mby * 8 - 1) * cs + mbx * 8);
+                        t0 = t.x; t1 = t.y;
+                    } else if (hl) {
+                        const uint8_t* cp = j == 3 ? Yf + (size_t)(mby * 16 - 1) * ys + mbx * 16 - 1
+                                                   : (j == 4 ? Uf : Vf) + (size_t)(mby * 8 - 1) * cs + mbx * 8 - 1;
+                        t0 = *cp;
+                    }
+                }
+                if (j == 0) {
+                    A->ytop[0] = t0; A->ytop[1] = t1; A->ytop[2] = t2; A->ytop[3] = t3;
+                } else if (j < 3) {
+                    A->ctop[j - 1][0] = t0;
+                    A->ctop[j - 1][1] = t1;
+                } else {
+                    A->corner[j - 3] = (uint8_t)t0;
+                }
+            }
+            wsync();
+        }
+        // ---- the three items: luma block j under DC (A) and TM (B), chroma block j & 7 under mode j >> 3 (C)
+        int bins[16], zA, vA, zB, vB, zC, vC;
+        an_item(A, true, 0, j, ht, hl, bins, zA, vA);
+        an_item(A, true, 1, j, ht, hl, bins, zB, vB);
+        an_item(A, false, j >> 3, j & 7, ht, hl, bins, zC, vC);
+        // per histogram (luma DC, luma TM, chroma DC in lanes j < 8, chroma TM in j >= 8):
+        // the bin-0 count and the largest bin
+        const int z0 = red16(zA), z1 = red16(zB), z23 = an_red8(zC);
+        const int v0 = max16(vA), v1 = max16(vB), v23 = max8(vC);
+        // fast path (k_analysis): bin 0 holding at least half of a histogram's
+        // coefficients is its largest count, and the last non-empty bin is the largest bin
+        const bool ok = 2 * z0 >= 256 && 2 * z1 >= 256 && 2 * z23 >= 128;
+        int a0, a1, a23;
+        if (__ballot(in && !ok) == 0ull) {
+            a0 = z0 > 1 ? (int)(510u * (uint32_t)v0 / (uint32_t)z0) : 0;
+            a1 = z1 > 1 ? (int)(510u * (uint32_t)v1 / (uint32_t)z1) : 0;
+            a23 = z23 > 1 ? (int)(510u * (uint32_t)v23 / (uint32_t)z23) : 0;
+        } else {
+            // exact histograms: bin 0 counted in the lane, the other bins by LDS atomics
+            uint32_t* H = &hist[wv][mi][0][0];
+#pragma unroll
+            for (int k = 0; k < 8; k++) (&hist[wv][0][0][0])[64 * k + lane] = 0;
+            wsync();
+#pragma unroll 1
+            for (int t = 0; t < 3; t++) {
+                int zz, vv;
+                const int h = t < 2 ? t : 2 + (j >> 3);
+                an_item(A, t < 2, t < 2 ? t : j >> 3, t < 2 ? j : j & 7, ht, hl, bins, zz, vv);
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (bins[k]) atomicAdd(&H[h * 32 + bins[k]], 1u);
+                if (zz) atomicAdd(&H[h * 32], (uint32_t)zz);
+            }
+            wsync();
+            int av[4];
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const uint32_t c0 = H[h * 32 + 2 * j], c1 = H[h * 32 + 2 * j + 1];
+                const int mx = max16((int)max(c0, c1));
+                const int lnz = max16(c1 ? 2 * j + 1 : (c0 ? 2 * j : -1));
+                av[h] = mx > 1 ? (int)(510u * (uint32_t)max(lnz, 0) / (uint32_t)mx) : 0;
+            }
+            a0 = av[0];
+            a1 = av[1];
+            a23 = j < 8 ? av[2] : av[3];
+        }
+        const int a3 = __shfl(a23, (lane & ~15) | 8);  // chroma TM's, from lane 8 of the MB
+        if (j == 0 && in) {
+            const int best = max(-1, max(a0, a1));
+            const int buv = max(-1, max(a23, a3));
+            int al = (3 * best + buv + 2) >> 2;
+            al = 255 - al;
+            al = al < 0 ? 0 : (al > 255 ? 255 : al);
+            alpha[(size_t)f * nmb + mb] = (uint8_t)al;
+            atomicAdd(&ahist[al], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t c = ahist[threadIdx.x];
+    if (c) atomicAdd(&histo[(size_t)f * 256 + threadIdx.x], c);
+}
+
+// ---------------------------------------------------------------------------
 // Segments: one thread per frame.  k-means over the alpha histogram
 // (assign_segments_kmeans analysis.rs:1029), per-segment quant via the
 // reference's f64 fast_math pow (compute_segment_quant :1145; this file is
@@ -3234,9 +3447,15 @@ extern "C" hipError_t zwk_analysis(hipStream_t s, const uint8_t* Y, const uint8_
                                    int mbh, size_t ysz, size_t csz, uint8_t* alpha, uint32_t* histo, int nframes)
 {
     const int nmb = mbw * mbh;
-    hipLaunchKernelGGL(k_analysis, dim3((nmb + 4 * ZW_AN_MPW - 1) / (4 * ZW_AN_MPW), nframes), dim3(256), 0, s, Y, U, V,
-                       mbw, mbh, ysz, csz, alpha,
-                       histo);
+#ifndef ZW_AN_FORM
+#define ZW_AN_FORM 4  // 4: k_analysis4 (four MBs a wave); 1: k_analysis (one MB a wave)
+#endif
+    if (ZW_AN_FORM == 4)
+        hipLaunchKernelGGL(k_analysis4, dim3((nmb + 16 * ZW_AN4_GPW - 1) / (16 * ZW_AN4_GPW), nframes), dim3(256), 0, s, Y,
+                           U, V, mbw, mbh, ysz, csz, alpha, histo);
+    else
+        hipLaunchKernelGGL(k_analysis, dim3((nmb + 4 * ZW_AN_MPW - 1) / (4 * ZW_AN_MPW), nframes), dim3(256), 0, s, Y, U,
+                           V, mbw, mbh, ysz, csz, alpha, histo);
     return hipGetLastError();
 }
 
