@@ -507,7 +507,7 @@ DI int max16(int v)
 typedef unsigned an_v4u __attribute__((ext_vector_type(4)));
 typedef unsigned an_v2u __attribute__((ext_vector_type(2)));
 #ifndef ZW_AN4_GPW
-#define ZW_AN4_GPW 2  // 4-MB groups per wave
+#define ZW_AN4_GPW 1  // 4-MB groups per wave (measured, analysis + segments per 256 1080p frames: 1 1.375, 2 1.47, 4 1.41 ms)
 #endif
 extern "C" __global__ __launch_bounds__(256) void k_analysis4(const uint8_t* __restrict__ Y, const uint8_t* __restrict__ U,
                                                               const uint8_t* __restrict__ V, int mbw, int mbh,
