@@ -38,10 +38,14 @@ size_t zw_dec_rows_sync_bytes(int mbh, int nframes);
 size_t zw_dec_rows_border_bytes(int mbw, int nframes);
 hipError_t zwk_loopfilter(hipStream_t s, uint8_t* Y, uint8_t* U, uint8_t* V, const uint8_t* flags,
                           const ZwFilterParams* fp, size_t ysz, size_t csz, int nframes, int mbw, const uint8_t* tiles);
-hipError_t zwk_dec_tokl(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
-                        const uint8_t* modes, uint8_t* recs, uint64_t slot, uint32_t* moff, int* err, int mbw, int mbh,
-                        int n);
-size_t zw_tokl_lds_bytes(int mbw);
+hipError_t zwk_dec_tok_count(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
+                             const uint8_t* modes, const uint32_t* cls, uint8_t* snaps, int* err1, uint32_t* sizes,
+                             int* err2, uint32_t* moff, uint64_t* fbase, int* terr, uint64_t* d_total,
+                             uint64_t* host_total, int mbw, int mbh, int n, hipEvent_t stage1_done);
+hipError_t zwk_dec_tok_write(hipStream_t s, const uint8_t* blob, const ZwTokFrame* tf, const uint8_t* probs,
+                             const uint8_t* modes, const uint8_t* snaps, const int* err1, const uint32_t* moff,
+                             const uint64_t* fbase, uint8_t* recs, int nmb, int n);
+size_t zw_tok1_lds_bytes(int mbw);
 }
 #include "zw_tokl.h"
 
@@ -917,31 +921,45 @@ static int dec_chunk_frames()
 }
 
 // ---------------------------------------------------------------------------
-// Device token parse (k_dec_tokl, zw_dec_tokens.hip) for the tail of a batch.
-// A frame's token partition is one serial chain of bool decisions: ≈2.9 ms on a
-// host core for a 1080p Q75 frame, ≈250 ms on one GPU lane, but one launch runs
-// 64 frames per wave side by side, so its time hardly depends on how many
-// frames it holds.  So a batch splits: the frames [h0, n) are header/mode-parsed
-// on the host up front (the first partition, a short chain) and their tokens go
-// to the device in one launch on its own stream, while the chunk pipeline
-// parses the frames [0, h0) on the host as before; the device chunks'
-// reconstruction waits for that launch.  By default (auto) the host keeps as
-// many whole chunks as it parses in the launch's time, from the rates the last
-// batches measured, and the device takes the rest (none when the host alone
-// would finish first).  ZW_DEC_TOKENS=host / device / mixed forces the host,
-// the device or a split at ZW_DEC_TOKENS_HOST (the host's share, 0.5).
+// Device token parse (zw_dec_tokens.hip) for the tail of a batch.  A frame's
+// token partition is one serial chain of bool decisions: ≈2.7 ms on a host core
+// for a 1080p Q75 frame, much longer on one GPU lane, but one launch runs 64
+// frames per wave side by side, so its time hardly depends on how many frames it
+// holds.  So a batch splits: the frames [h0, n) are header/mode-parsed on the
+// host up front (the first partition, a short chain) and their tokens go to the
+// device on its own stream, while the chunk pipeline parses the frames [0, h0)
+// on the host as before; the device chunks' reconstruction waits for the
+// device's records.  The device parse runs in two stages: k_dec_tok1 (the
+// decision chains alone, a snapshot per MB) and k_dec_tok2 (every MB replayed
+// from its snapshot in parallel: a count pass, offsets, then the records into a
+// buffer sized from the count, so the records take what they use -- ≈1 MB per
+// 1080p Q75 frame -- and no worst-case slots).  By default (auto) the host keeps
+// as many whole chunks as it parses in the device's time, from the rates the
+// last batches measured, and the device takes the rest (none when the host
+// alone would finish first).  ZW_DEC_TOKENS=host / device / mixed forces the
+// host, the device or a split at ZW_DEC_TOKENS_HOST (the host's share, 0.5).
+//
+// Device memory the parse keeps in the context after a batch (freed by
+// zw_ctx_release_buffers / zw_ctx_destroy; grow-only between): per device frame
+// its partition, modes (16 B per MB), probabilities, a 16-byte snapshot and a
+// 4-byte size and offset per MB (≈0.4 MB per 1080p frame) plus its records.
 // ---------------------------------------------------------------------------
 struct DecTok {
     int h0 = 0, nd = 0;  // device frames [h0, h0 + nd)
     std::vector<DecFrame> F;
     std::vector<DecQuant> quant;
     std::vector<ZwFilterParams> fps;
-    const uint8_t* recs = nullptr;
+    size_t nmb = 0;
+    // device buffers of the write pass (ctx_scratch_tok)
+    uint8_t* d = nullptr;
+    size_t o_b = 0, o_tf = 0, o_p = 0, o_m = 0, o_sn = 0, o_e1 = 0;
     const uint32_t* moff = nullptr;
     const uint64_t* fbase = nullptr;
     const int* err = nullptr;
+    // set by dec_tok_finish
+    const uint8_t* recs = nullptr;
     hipEvent_t done = nullptr;
-    size_t nmb = 0;
+    int state = 0;  // 0 launched (count), 1 records queued, -1 failed (the host parses the rest)
 };
 
 // The host's frames [0, h0) of a batch of n frames of nmb MBs (C frames per chunk).
@@ -957,21 +975,21 @@ static int dec_tok_split(zw_ctx* ctx, int n, int C, size_t nmb)
         return std::max(0, std::min(n, (int)(n * frac) / C * C));  // whole host chunks
     }
     // auto.  Defaults until measured: 0.19 ms of chunk time per 1080p frame (16 host
-    // threads) and a 250 ms launch for 1080p frames (measured: 1 024 / 2 048 / 4 096
-    // frames host-only 3 331 / 3 836 / 4 448, best split 3 331 / 4 614 / 4 977 decodes/s)
+    // threads) and a 100 ms device parse for 1080p frames
     const double host_f = ctx->dec_host_ms_per_frame > 0 ? ctx->dec_host_ms_per_frame : 0.19 * (double)nmb / 8160.0;
-    const double tok = (ctx->dec_tok_ms_per_mb > 0 ? ctx->dec_tok_ms_per_mb : 250.0 / 8160.0) * (double)nmb;
-    const double tail = 0.06 * tok;  // the device frames' reconstruction and download after the launch, per frame of
-                                     // host work that the launch's length leaves (an estimate; errs toward the host)
+    const double tok = (ctx->dec_tok_ms_per_mb > 0 ? ctx->dec_tok_ms_per_mb : 100.0 / 8160.0) * (double)nmb;
+    const double tail = 0.06 * tok;  // the device frames' reconstruction and download after the parse, per frame of
+                                     // host work that the parse's length leaves (an estimate; errs toward the host)
     if (n * host_f <= tok + tail) return n;  // the host alone finishes first
     const int h0 = (int)(tok / host_f) / C * C;
     return std::max(0, std::min(n, h0));
 }
 
-// Parses the headers and modes of frames [h0, n), stages them and launches
-// k_dec_tokl on the context's token stream.  Returns false (and leaves the
-// frames to the host chunks, which then report any error in frame order) when
-// a frame has several token partitions, another size, or a header / mode error.
+// Parses the headers and modes of frames [h0, n), stages them and launches the
+// device parse's first half (stage 1, the count pass, offsets) on the context's
+// token stream.  Returns false (and leaves the frames to the host chunks, which
+// then report any error in frame order) when a frame has several token
+// partitions, another size, or a header / mode error.
 static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, int h0, DecTok& T)
 {
     const int nd = n - h0;
@@ -985,10 +1003,10 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
             F[i].mbh == 0)
             return false;
     const int mbw = F[0].mbw, mbh = F[0].mbh;
-    // k_dec_tokl keeps per-lane top contexts in LDS (very wide frames stay on the host) and
-    // addresses a wave's 64 record slots through one buffer (< 2 GB)
-    const size_t nmb = (size_t)mbw * mbh, slot = nmb * ZW_DREC_MAX + 64;  // (+64: the pad store past a full record)
-    if (zw_tokl_lds_bytes(mbw) > 160 * 1024 || 64 * slot >= ((size_t)1 << 31)) return false;
+    // stage 1 keeps per-lane top contexts in LDS (very wide frames stay on the host) and
+    // addresses a wave's 64 frames of snapshots through one buffer (< 2 GB)
+    const size_t nmb = (size_t)mbw * mbh, ncw = (nmb + 15) / 16;
+    if (mbw < 2 || zw_tok1_lds_bytes(mbw) > 160 * 1024 || 64 * nmb * 16 >= ((size_t)1 << 31)) return false;
     const size_t probs_b = (size_t)tokl::PROBS;
     std::vector<size_t> boff(nd);
     size_t blob = 0;
@@ -997,19 +1015,25 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
         blob += (F[i].part[0].len + 15) & ~(size_t)15;
     }
     blob += 16;  // (16 zero bytes at the end)
-    const size_t o_m = 0, o_p = al256(o_m + (size_t)nd * nmb * ZW_TOK_MODE);
-    const size_t o_tf = al256(o_p + (size_t)nd * probs_b), o_fb = al256(o_tf + (size_t)nd * sizeof(ZwTokFrame));
-    const size_t o_b = al256(o_fb + (size_t)nd * 8), up_bytes = al256(o_b + blob);
+    const size_t o_m = 0, o_c = al256(o_m + (size_t)nd * nmb * ZW_TOK_MODE), o_p = al256(o_c + (size_t)nd * ncw * 4);
+    const size_t o_tf = al256(o_p + (size_t)nd * probs_b), o_b = al256(o_tf + (size_t)nd * sizeof(ZwTokFrame));
+    const size_t up_bytes = al256(o_b + blob);
     uint8_t* stage = (uint8_t*)ctx_pinned(ctx, 4, up_bytes);
     if (!stage) return false;
     T.quant.assign((size_t)nd * 4, DecQuant());
     T.fps.assign(nd, ZwFilterParams());
     parallel_for(nd, [&](int i) {
-        rc[i] = parse_modes(F[i], stage + o_m + (size_t)i * nmb * ZW_TOK_MODE);
+        uint8_t* mr = stage + o_m + (size_t)i * nmb * ZW_TOK_MODE;
+        rc[i] = parse_modes(F[i], mr);
+        uint32_t* cw = (uint32_t*)(stage + o_c) + (size_t)i * ncw;  // 2 bits per MB: I4, skipped
+        memset(cw, 0, ncw * 4);
+        for (size_t j = 0; j < nmb; j++) {
+            const uint8_t b0 = mr[j * ZW_TOK_MODE];
+            cw[j >> 4] |= ((uint32_t)((b0 & 7) == 4) | (uint32_t)((b0 >> 5) & 1) << 1) << (2 * (j & 15));
+        }
         memcpy(stage + o_p + (size_t)i * probs_b, F[i].probs, tokl::PROBS);  // [type][band][ctx][node]
         const ZwTokFrame tf = {boff[i], (uint32_t)F[i].part[0].len, 0};
         memcpy(stage + o_tf + (size_t)i * sizeof(ZwTokFrame), &tf, sizeof tf);
-        ((uint64_t*)(stage + o_fb))[i] = (uint64_t)i * slot;
         const size_t len = F[i].part[0].len, al = (len + 15) & ~(size_t)15;
         memcpy(stage + o_b + boff[i], F[i].part[0].d, len);
         memset(stage + o_b + boff[i] + len, 0, al - len);
@@ -1021,40 +1045,80 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     for (int i = 0; i < nd; i++)
         if (rc[i] != ZW_OK) return false;
     memset(stage + o_b + blob - 16, 0, 16);
-    const size_t o_rec = up_bytes, o_mo = al256(o_rec + (size_t)nd * slot);
-    const size_t o_te = al256(o_mo + (size_t)nd * (nmb + 1) * 4), total = al256(o_te + (size_t)nd * 4);
+    const size_t o_sn = up_bytes, o_sz = al256(o_sn + (size_t)nd * nmb * 16), o_mo = al256(o_sz + (size_t)nd * nmb * 4);
+    const size_t o_fb = al256(o_mo + (size_t)nd * (nmb + 1) * 4), o_e1 = al256(o_fb + (size_t)nd * 8);
+    const size_t o_e2 = al256(o_e1 + (size_t)nd * 4), o_te = al256(o_e2 + (size_t)nd * 4);
+    const size_t o_tot = al256(o_te + (size_t)nd * 4), total = al256(o_tot + 8);
     uint8_t* d = (uint8_t*)ctx_scratch_tok(ctx, total);
     if (!d) return false;
+    if (!ctx->tok_total && hipHostMalloc((void**)&ctx->tok_total, 256, hipHostMallocDefault) != hipSuccess) {
+        ctx->tok_total = nullptr;
+        return false;
+    }
     if (!ctx->tok_ && hipStreamCreateWithFlags(&ctx->tok_, hipStreamNonBlocking) != hipSuccess) return false;
     for (hipEvent_t& e : ctx->tok_ev)
         if (!e && hipEventCreate(&e) != hipSuccess) return false;
     hipStream_t s = ctx->tok_;
     if (hipMemcpyAsync(d, stage, up_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return false;
     if (hipEventRecord(ctx->tok_ev[0], s) != hipSuccess) return false;
-    if (zwk_dec_tokl(s, d + o_b, (const ZwTokFrame*)(d + o_tf), d + o_p, d + o_m, d + o_rec, slot,
-                     (uint32_t*)(d + o_mo), (int*)(d + o_te), mbw, mbh, nd) != hipSuccess)
-        return false;
-    if (hipEventRecord(ctx->tok_ev[1], s) != hipSuccess) {
-        (void)hipStreamSynchronize(s);  // (the launch is in flight: let it finish before the host takes over)
+    if (zwk_dec_tok_count(s, d + o_b, (const ZwTokFrame*)(d + o_tf), d + o_p, d + o_m, (const uint32_t*)(d + o_c),
+                          d + o_sn, (int*)(d + o_e1), (uint32_t*)(d + o_sz), (int*)(d + o_e2), (uint32_t*)(d + o_mo),
+                          (uint64_t*)(d + o_fb), (int*)(d + o_te), (uint64_t*)(d + o_tot), ctx->tok_total, mbw, mbh,
+                          nd, ctx->tok_ev[3]) != hipSuccess ||
+        hipEventRecord(ctx->tok_ev[2], s) != hipSuccess) {
+        (void)hipStreamSynchronize(s);  // (work may be in flight: let it finish before the host takes over)
         return false;
     }
     T.h0 = h0;
     T.nd = nd;
     T.nmb = nmb;
-    T.recs = d + o_rec;
+    T.d = d;
+    T.o_b = o_b;
+    T.o_tf = o_tf;
+    T.o_p = o_p;
+    T.o_m = o_m;
+    T.o_sn = o_sn;
+    T.o_e1 = o_e1;
     T.moff = (const uint32_t*)(d + o_mo);
     T.fbase = (const uint64_t*)(d + o_fb);
     T.err = (const int*)(d + o_te);
+    T.state = 0;
+    return true;
+}
+
+// The device parse's second half, once, before the first device chunk: waits
+// for the count (the host thread blocks; the previous chunk's download and
+// fan-out run on their own thread meanwhile), sizes the record buffer and
+// queues the record pass.  false: the host parses the device frames instead.
+static bool dec_tok_finish(zw_ctx* ctx, DecTok& T)
+{
+    if (T.state != 0) return T.state > 0;
+    T.state = -1;
+    if (hipEventSynchronize(ctx->tok_ev[2]) != hipSuccess) return false;
+    const size_t bytes = std::max<size_t>(256, (size_t)*ctx->tok_total);
+    uint8_t* recs = (uint8_t*)ctx_scratch_rec(ctx, bytes);
+    if (!recs) return false;
+    hipStream_t s = ctx->tok_;
+    if (zwk_dec_tok_write(s, T.d + T.o_b, (const ZwTokFrame*)(T.d + T.o_tf), T.d + T.o_p, T.d + T.o_m, T.d + T.o_sn,
+                          (const int*)(T.d + T.o_e1), T.moff, T.fbase, recs, (int)T.nmb, T.nd) != hipSuccess ||
+        hipEventRecord(ctx->tok_ev[1], s) != hipSuccess) {
+        (void)hipStreamSynchronize(s);
+        return false;
+    }
+    T.recs = recs;
     T.done = ctx->tok_ev[1];
+    T.state = 1;
     if (const char* dump = getenv("ZW_DEC_TOKENS_DUMP")) {  // debug: device frame 0's records to <dump>.dev
         if (hipStreamSynchronize(s) == hipSuccess) {
-            std::vector<uint32_t> mo(nmb + 1);
-            (void)hipMemcpy(mo.data(), d + o_mo, (nmb + 1) * 4, hipMemcpyDeviceToHost);
-            std::vector<uint8_t> dev(mo[nmb]);
-            (void)hipMemcpy(dev.data(), d + o_rec, mo[nmb], hipMemcpyDeviceToHost);
+            std::vector<uint32_t> mo(T.nmb + 1);
+            uint64_t fb0 = 0;
+            (void)hipMemcpy(mo.data(), T.moff, (T.nmb + 1) * 4, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(&fb0, T.fbase, 8, hipMemcpyDeviceToHost);
+            std::vector<uint8_t> dev(mo[T.nmb]);
+            (void)hipMemcpy(dev.data(), recs + fb0, mo[T.nmb], hipMemcpyDeviceToHost);
             std::string p0 = std::string(dump) + ".dev";
             if (FILE* fo = fopen(p0.c_str(), "wb")) {
-                fwrite(mo.data(), 4, nmb + 1, fo);
+                fwrite(mo.data(), 4, T.nmb + 1, fo);
                 fwrite(dev.data(), 1, dev.size(), fo);
                 fclose(fo);
             }
@@ -1063,7 +1127,7 @@ static bool dec_tok_prepare(zw_ctx* ctx, int n, const uint8_t* const* data, cons
     return true;
 }
 
-// A chunk of device frames [first, first + cnt): no host parse; its records are k_dec_tokl'.
+// A chunk of device frames [first, first + cnt): no host parse; its records are the device parse's.
 static void dec_parse_dev(const DecTok& T, int first, int cnt, DecBatch& B)
 {
     const int j0 = first - T.h0;
@@ -1100,6 +1164,7 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     DecBatch B[2];
     ctx->dec_ms[0] = ctx->dec_ms[1] = ctx->dec_ms[2] = 0.f;
     ctx->dec_tok_ms = 0.f;
+    ctx->dec_tok_stage_ms[0] = ctx->dec_tok_stage_ms[1] = ctx->dec_tok_stage_ms[2] = 0.f;
     ctx->dec_host_ms[0] = ctx->dec_host_ms[1] = ctx->dec_host_ms[2] = 0;
     // the device's share of the tokens first (its launch runs beside the host chunks)
     DecTok T;
@@ -1133,7 +1198,7 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             });
         }
         if (c < nch) {
-            if (first(c) >= T.h0) {
+            if (first(c) >= T.h0 && dec_tok_finish(ctx, T)) {
                 dec_parse_dev(T, first(c), count(c), B[c & 1]);
             } else {
                 err_p = dec_parse(ctx, count(c), data + first(c), lens + first(c), B[c & 1], c & 1);
@@ -1151,10 +1216,16 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
         }
     }
     if (T.nd > 0) {
+        if (T.state == 0) (void)hipStreamSynchronize(ctx->tok_);  // (an error before the first device chunk)
         float ms = 0.f;
-        if (hipEventSynchronize(T.done) == hipSuccess &&
+        if (T.state > 0 && hipEventSynchronize(T.done) == hipSuccess &&
             hipEventElapsedTime(&ms, ctx->tok_ev[0], ctx->tok_ev[1]) == hipSuccess) {
             ctx->dec_tok_ms = ms;
+            for (int k = 0; k < 3; k++) {
+                float m = 0.f;
+                static const int e0[3] = {0, 3, 2}, e1[3] = {3, 2, 1};
+                if (hipEventElapsedTime(&m, ctx->tok_ev[e0[k]], ctx->tok_ev[e1[k]]) == hipSuccess) ctx->dec_tok_stage_ms[k] = m;
+            }
             if (!err && ms > 0) ctx->dec_tok_ms_per_mb = ms / (double)T.nmb;
         }
     }
@@ -1468,6 +1539,13 @@ extern "C" int zw_decode_token_ms(zw_ctx* ctx, float* ms)
     return ZW_OK;
 }
 
+extern "C" int zw_decode_token_stages(zw_ctx* ctx, float* ms)
+{
+    if (!ctx || !ms) return ZW_EINVAL;
+    for (int i = 0; i < 3; i++) ms[i] = ctx->dec_tok_stage_ms[i];
+    return ZW_OK;
+}
+
 extern "C" int zw_decode_stage_times(zw_ctx* ctx, float* ms)
 {
     if (!ctx || !ms) return ZW_EINVAL;
@@ -1531,24 +1609,70 @@ extern "C" int zw_loop_filter_frame(zw_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t
 }
 
 // ---------------------------------------------------------------------------
-// CPU check of the device token parse's state machine (zw_tokl.h, the code
-// k_dec_tokl runs per lane): the same functions step one frame here over host
-// memory, and the records must equal parse_mbs's byte for byte (or both fail).
-// Test hook only (tests/test_tokl.py); no device work.
+// CPU check of the device token parse (zw_tokl.h, the code k_dec_tok1 and
+// k_dec_tok2 run per lane): the same functions step one frame here over host
+// memory -- stage 1 over the whole frame (snapshots), stage 2 per MB from each
+// snapshot (count, offsets, records) -- and the records must equal parse_mbs's
+// byte for byte (or both fail).  Test hook only (tests/test_tokl.py); no device work.
 // ---------------------------------------------------------------------------
 namespace {
-struct HostTokMem {
+static uint64_t host_bits64(const uint8_t* stream, size_t len, uint32_t bp)
+{
+    uint64_t v = 0;
+    const size_t b0 = bp >> 3;
+    for (int i = 0; i < 9; i++) {
+        const uint64_t byte = b0 + i < len ? stream[b0 + i] : 0;
+        if (i < 8) v = (v << 8) | byte;
+        else v = (bp & 7) ? (v << (bp & 7)) | (byte >> (8 - (bp & 7))) : v;
+    }
+    return v;
+}
+
+struct HostTok1Mem {
+    static constexpr uint32_t U = 1;
+    const uint32_t* T1;
+    const uint8_t* P;
+    const uint8_t* stream;
+    size_t len;
+    const uint8_t* modes;
+    uint32_t nmb, mbw;
+    std::vector<uint16_t> tcxv;
+    std::vector<uint32_t> snaps;  // 4 words per MB
+    uint32_t prob_at(uint32_t a) const { return P[a]; }
+    void tt1(uint32_t s8, uint32_t& t0, uint32_t& t1) const
+    {
+        t0 = T1[s8 / 4];
+        t1 = T1[s8 / 4 + 1];
+    }
+    void desc1(uint32_t i, uint32_t* d) const { tok1::desc1<1>(i / tok1::NDESC1, i % tok1::NDESC1, d); }
+    uint64_t bits64(uint32_t bp) const { return host_bits64(stream, len, bp); }
+    uint32_t cls(uint32_t mbi) const
+    {
+        const uint8_t b0 = modes[(size_t)mbi * ZW_TOK_MODE];
+        return (uint32_t)((b0 & 7) == 4) | ((uint32_t)((b0 >> 5) & 1) << 1);
+    }
+    uint32_t tcx(uint32_t mbx) const { return tcxv[mbx]; }
+    void set_tcx(uint32_t mbx, uint32_t v) { tcxv[mbx] = (uint16_t)v; }
+    void snap(bool c, uint32_t mbi, uint32_t s0, uint32_t s1, uint32_t tl)
+    {
+        if (!c) return;
+        uint32_t* w = &snaps[(size_t)mbi * 4];
+        w[0] = s0;
+        w[1] = s1;
+        w[2] = tl;
+        w[3] = 0;
+    }
+};
+
+struct HostTok2Mem {
     static constexpr uint32_t U = 1;
     static constexpr uint32_t lane0 = 0;
     const uint32_t* TT;
     const uint8_t* P;
     const uint8_t* stream;
     size_t len;
-    const uint8_t* modes;
-    uint8_t* rec;
-    uint32_t* mo;
-    uint32_t nmb, mbw;
-    std::vector<uint16_t> tcxv;
+    uint8_t* rec = nullptr;  // null: count only
+    uint32_t lim = 0;        // the MB's record end (stores past it belong to the next MB)
 
     void tt(uint32_t st, uint32_t& t0, uint32_t& t1) const
     {
@@ -1557,33 +1681,40 @@ struct HostTokMem {
     }
     void desc(uint32_t i, uint32_t* d) const { tokl::desc(i / tokl::NDESC, i % tokl::NDESC, d); }
     uint32_t prob_at(uint32_t i) const { return P[i]; }
-    uint64_t bits64(uint32_t bp) const
-    {
-        uint64_t v = 0;
-        const size_t b0 = bp >> 3;
-        for (int i = 0; i < 9; i++) {
-            const uint64_t byte = b0 + i < len ? stream[b0 + i] : 0;
-            if (i < 8) v = (v << 8) | byte;
-            else v = (bp & 7) ? (v << (bp & 7)) | (byte >> (8 - (bp & 7))) : v;
-        }
-        return v;
-    }
-    void mode(uint32_t mbi, uint32_t* r) const { memcpy(r, modes + (size_t)mbi * ZW_TOK_MODE, 16); }
-    uint32_t tcx(uint32_t mbx) const { return tcxv[mbx]; }
-    void set_tcx(uint32_t mbx, uint32_t v) { tcxv[mbx] = (uint16_t)v; }
+    uint64_t bits64(uint32_t bp) const { return host_bits64(stream, len, bp); }
     void st16c(bool c, uint32_t off, uint32_t v)
     {
         const uint16_t h = (uint16_t)v;
-        if (c) memcpy(rec + off, &h, 2);
+        if (rec && c && off < lim) memcpy(rec + off, &h, 2);
     }
     void st128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
     {
         const uint32_t w[4] = {a, b, c, d};
-        memcpy(rec + off, w, 16);
+        if (rec) memcpy(rec + off, w, 16);
     }
-    void st128u(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) { st128(off, a, b, c, d); }
-    void moff(uint32_t i, uint32_t v) { mo[i] = v; }
 };
+
+// stage 2 for MB i of a frame (its record at hb); returns the record's bytes, *bad = the eof rule failed
+static uint32_t host_tok2_mb(HostTok2Mem& m, const uint8_t* modes, const uint32_t* snap, uint32_t hb, bool* bad)
+{
+    uint32_t mr[4];
+    memcpy(mr, modes, 16);
+    if ((mr[0] >> 5) & 1u) {
+        tokl::mb_skip(m, hb, mr);
+        return ZW_DREC_HDR;
+    }
+    tokl::Lane L;
+    tokl::from_snapshot(L, m, snap[0], snap[1], (uint32_t)m.len);
+    L.hb = hb;
+    tokl::mb_begin(L, m, mr, snap[2]);
+    while (L.phase == tokl::PH_DECIDE) {
+        if (L.vb < 8) tokl::topup(L, m);
+        tokl::step(L, m);
+    }
+    tokl::mb_end(L, m);
+    *bad = *bad || L.bad;
+    return L.hb - hb;
+}
 }  // namespace
 
 extern "C" int zw_dbg_tokl_frame(const uint8_t* vp8, size_t len, int* match)
@@ -1595,34 +1726,51 @@ extern "C" int zw_dbg_tokl_frame(const uint8_t* vp8, size_t len, int* match)
     (void)parse_header(B, vp8, len);
     const size_t nmb = (size_t)A.mbw * A.mbh;
     if (nmb == 0) return ZW_EINVALID_DIMENSIONS;
-    std::vector<uint8_t> ref(nmb * ZW_DREC_MAX), modes(nmb * ZW_TOK_MODE), rec(nmb * ZW_DREC_MAX + 64);
+    std::vector<uint8_t> ref(nmb * ZW_DREC_MAX), modes(nmb * ZW_TOK_MODE);
     std::vector<uint32_t> moff_ref(nmb + 1), moff(nmb + 1);
     const int rc = parse_mbs(A, ref.data(), moff_ref.data());
-    if (B.nparts != 1 || parse_modes(B, modes.data()) != ZW_OK) return rc;  // the host keeps such frames
-    static const uint32_t TT[2 * tokl::NST] = ZW_TOKL_TT_INIT;
-    HostTokMem m;
-    m.TT = TT;
-    m.P = &B.probs[0][0][0][0];
-    m.stream = B.part[0].d;
-    m.len = B.part[0].len;
-    m.modes = modes.data();
-    m.rec = rec.data();
-    m.mo = moff.data();
-    m.nmb = (uint32_t)nmb;
-    m.mbw = (uint32_t)B.mbw;
-    m.tcxv.assign(B.mbw, 0);
-    tokl::Lane L;
-    tokl::init(L, (uint32_t)m.len, true);
-    while (L.phase != tokl::PH_DONE) {
-        if (L.phase == tokl::PH_MB) {
-            tokl::mb_phase(L, m);
-            continue;
-        }
-        if (L.vb < 8) tokl::topup(L, m);
-        tokl::step(L, m);
+    if (B.nparts != 1 || B.mbw < 2 || parse_modes(B, modes.data()) != ZW_OK) return rc;  // the host keeps such frames
+    // stage 1
+    static const tok1::Table<1> T1;
+    HostTok1Mem m1;
+    m1.T1 = T1.e;
+    m1.P = &B.probs[0][0][0][0];
+    m1.stream = B.part[0].d;
+    m1.len = B.part[0].len;
+    m1.modes = modes.data();
+    m1.nmb = (uint32_t)nmb;
+    m1.mbw = (uint32_t)B.mbw;
+    m1.tcxv.assign(B.mbw + 1, 0);
+    m1.snaps.assign(nmb * 4, 0);
+    tok1::Lane1 L1;
+    tok1::init1(L1, true);
+    for (uint64_t st = 0; L1.k != tok1::K_DONE; st++) {
+        if ((st & 7) == 0) tok1::topup1(L1, m1);  // (the device's schedule)
+        tok1::step1(L1, m1);  // (as the device: a lane waiting for its MB phase steps in SINK)
+        if ((st & 3) == 3)
+            for (int r = 0; r < 8 && L1.k == tok1::K_MB; r++) tok1::mb1(L1, m1);
     }
-    if (rc != ZW_OK || L.bad) {
-        *match = (rc == ZW_EBITSTREAM && L.bad) ? 1 : 0;
+    // stage 2: count, offsets, records
+    static const uint32_t TT[2 * tokl::NST] = ZW_TOKL_TT_INIT;
+    HostTok2Mem m2;
+    m2.TT = TT;
+    m2.P = &B.probs[0][0][0][0];
+    m2.stream = B.part[0].d;
+    m2.len = B.part[0].len;
+    bool bad = false;
+    moff[0] = 0;
+    for (size_t i = 0; i < nmb; i++)
+        moff[i + 1] = moff[i] + host_tok2_mb(m2, modes.data() + i * ZW_TOK_MODE, &m1.snaps[i * 4], 0, &bad);
+    std::vector<uint8_t> rec(moff[nmb] + 16);
+    m2.rec = rec.data();
+    bool bad2 = false;
+    for (size_t i = 0; i < nmb; i++) {
+        m2.lim = moff[i + 1];
+        const uint32_t sz = host_tok2_mb(m2, modes.data() + i * ZW_TOK_MODE, &m1.snaps[i * 4], moff[i], &bad2);
+        if (sz != moff[i + 1] - moff[i]) return ZW_EINVAL;  // (the two passes must agree)
+    }
+    if (rc != ZW_OK || bad) {
+        *match = (rc == ZW_EBITSTREAM && bad) ? 1 : 0;
         return rc;
     }
     *match = moff == moff_ref && !memcmp(rec.data(), ref.data(), moff_ref[nmb]) ? 1 : 0;

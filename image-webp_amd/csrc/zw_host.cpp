@@ -359,8 +359,9 @@ extern "C" void zw_ctx_release_buffers(zw_ctx* c)
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     if (c->tok_) (void)hipStreamSynchronize(c->tok_);
     if (c->dscratch2) (void)hipFree(c->dscratch2);
-    c->dscratch = c->dscratch1 = c->dscratch2 = nullptr;
-    c->dscratch2_cap = 0;
+    if (c->dscratch3) (void)hipFree(c->dscratch3);
+    c->dscratch = c->dscratch1 = c->dscratch2 = c->dscratch3 = nullptr;
+    c->dscratch2_cap = c->dscratch3_cap = 0;
     (void)hipDeviceSynchronize();  // queues may serve streams other than the context's
     for (auto& q : c->xmb_q)
         if (q.buf) (void)hipFree(q.buf);
@@ -393,6 +394,8 @@ void zw_ctx_free_internal(zw_ctx* c)
     if (c->dscratch1) (void)hipFree(c->dscratch1);
     if (c->tok_) (void)hipStreamSynchronize(c->tok_);
     if (c->dscratch2) (void)hipFree(c->dscratch2);
+    if (c->dscratch3) (void)hipFree(c->dscratch3);
+    pinned_free(c->tok_total);
     for (auto& q : c->xmb_q)
         if (q.buf) (void)hipFree(q.buf);
     if (c->xmb_err) (void)hipHostFree((void*)c->xmb_err);

@@ -23,10 +23,14 @@ struct zw_ctx {
     void* dscratch = nullptr;
     size_t dscratch_cap = 0;
     void* dscratch1 = nullptr;  // second buffer of the pipelined decode batches
-    void* dscratch2 = nullptr;  // decode batches: the device token parse's upload and records
+    void* dscratch2 = nullptr;  // decode batches: the device token parse's upload, snapshots and offsets
     size_t dscratch2_cap = 0;
-    hipStream_t tok_ = nullptr;  // k_dec_tokl (runs beside the chunks' kernels), created on first use
-    hipEvent_t tok_ev[2] = {nullptr, nullptr};
+    void* dscratch3 = nullptr;  // decode batches: the device token parse's records (sized by its count pass)
+    size_t dscratch3_cap = 0;
+    uint64_t* tok_total = nullptr;  // pinned: the count pass's record bytes
+    hipStream_t tok_ = nullptr;  // the device token parse (runs beside the chunks' kernels), created on first use
+    // [0] before stage 1, [1] the records written, [2] the count pass and scans done, [3] stage 1 done
+    hipEvent_t tok_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // zw_transform_quant_mbs*_device: the I4 queue of k_xform_mb / k_xform_mb_i4,
     // one per launch stream (launches on different streams may overlap; launches
     // on one stream are ordered), its counters reset on that stream per launch
@@ -66,7 +70,8 @@ struct zw_ctx {
     hipEvent_t dev_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     hipEvent_t dev_ev1[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // second buffer of the pipelined decode
     float dec_ms[3] = {0.f, 0.f, 0.f};
-    float dec_tok_ms = 0.f;  // k_dec_tokl of the last batch (0: the host parsed every frame)
+    float dec_tok_ms = 0.f;  // the device token parse of the last batch (0: the host parsed every frame)
+    float dec_tok_stage_ms[3] = {0.f, 0.f, 0.f};  // its stage 1, count pass + offsets (+ the host's wait), record pass
     // measured rates for the host / device split of the token parse (dec_tok_split):
     // host chunk parse ms per frame (the whole chunk over all threads), device launch ms
     // per MB of a frame (the launch runs its frames side by side), 0 = not measured yet
@@ -165,6 +170,18 @@ static inline void* ctx_scratch(zw_ctx* c, size_t bytes, int which = 0)
         cap = bytes;
     }
     return p;
+}
+
+static inline void* ctx_scratch_rec(zw_ctx* c, size_t bytes)
+{
+    if (c->dscratch3_cap < bytes) {
+        if (c->dscratch3) (void)hipFree(c->dscratch3);
+        c->dscratch3 = nullptr;
+        c->dscratch3_cap = 0;
+        if (hipMalloc(&c->dscratch3, bytes) != hipSuccess) return nullptr;
+        c->dscratch3_cap = bytes;
+    }
+    return c->dscratch3;
 }
 
 static inline void* ctx_scratch_tok(zw_ctx* c, size_t bytes)

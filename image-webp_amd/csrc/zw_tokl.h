@@ -118,7 +118,7 @@ TKL_HD uint32_t mul24(uint32_t a, uint32_t b)
 }
 
 // COEFF_BANDS (vp8.rs) as nibbles: positions 0..7 in the low word, 8..15 in the high one
-TKL_HD uint32_t band(uint32_t n)
+TKL_HD constexpr uint32_t band(uint32_t n)
 {
     const uint32_t w = n < 8u ? 0x65463210u : 0x76666666u;
     return (w >> (4u * (n & 7u))) & 15u;
@@ -132,11 +132,11 @@ TKL_HD uint32_t band(uint32_t n)
 // Blocks: k = 0 Y2 (type 1), 1..16 Y (type 0 after Y2, else 3; first 1 after
 // Y2), 17..20 U, 21..24 V (type 2); the context bits follow parse_mbs (top:
 // 0 Y2, 1..4 Y columns, 5..6 U, 7..8 V; left the same with rows).
-TKL_HD void desc(uint32_t c, uint32_t k, uint32_t* d)
+TKL_HD constexpr void desc(uint32_t c, uint32_t k, uint32_t* d)
 {
     d[0] = d[1] = d[2] = d[3] = 0;
     if (k > 24 || (k == 0 && c == 1)) return;
-    uint32_t tb, lb, t, first = 0;
+    uint32_t tb = 0, lb = 0, t = 0, first = 0;
     if (k == 0) {
         tb = lb = 0;
         t = 1;
@@ -290,71 +290,34 @@ TKL_HD void step(Lane& L, M& m)
     L.p = (be || ev || ((e >> 26) & 1u)) ? pt : ((e >> 6) & 255u);
 }
 
+// Stage 2's MB boundaries (one MB per lane, started from stage 1's snapshot).
+// mb_begin: the record starts at L.hb; mr = the MB's ZW_TOK_MODE bytes (as
+// words), TL = its block contexts at its start (top bits 0..8 from the MB
+// above, left bits 16..24 from the MB to the left).  Not for skipped MBs (a
+// header-only record, written by the caller).
 template <class M>
-TKL_HD void next_mb(Lane& L, M& m)
-{
-    L.mbi++;
-    if (++L.mbx == m.mbw) L.mbx = 0;
-}
-
-// The MB phase: finish the MB whose last block ended (its header and the zero
-// pad after its levels), then start the next MB or finish the frame.  A skipped
-// MB (mb_no_coeff_skip) is a header-only record; it returns with the lane still
-// at PH_MB.
-template <class M>
-TKL_HD void mb_phase(Lane& L, M& m)
+TKL_HD void mb_begin(Lane& L, M& m, const uint32_t* mr, uint32_t TL)
 {
     constexpr uint32_t U = M::U;
-    if (L.k == 25u) {
-        m.st128(L.hb, L.w0, L.nzm2 >> 1, L.w2, L.w3);
-        m.st128(L.hb + 64u, L.nlv, 0u, 0u, 0u);
-        m.st128(L.lvb, 0u, 0u, 0u, 0u);  // (2-byte aligned)
-        L.hb = (L.lvb + 15u) & ~15u;
-        m.set_tcx(L.mbx, L.TL & 511u);
-        next_mb(L, m);
-        L.k = 0;
-    }
-    if (L.mbi == m.nmb) {
-        m.moff(m.nmb, L.hb);
-        L.phase = PH_DONE;
-        return;
-    }
-    m.moff(L.mbi, L.hb);
-    uint32_t mr[4];
-    m.mode(L.mbi, mr);
     L.w0 = mr[0];
     L.w2 = mr[2];
     L.w3 = mr[3];
-    const uint32_t lm = mr[0] & 7u, skip = (mr[0] >> 5) & 1u;
-    L.TL = (L.mbx == 0 ? 0u : (L.TL & 0x01FF0000u)) | m.tcx(L.mbx);
-    if (skip) {
-        // parse_mbs: every context but Y2's (kept for I4 MBs) becomes 0
-        L.TL &= lm != 4u ? 0u : 0x00010001u;
-        m.st128(L.hb, mr[0], 0u, mr[2], mr[3]);
-        m.st128(L.hb + 16u, 0u, 0u, 0u, 0u);
-        m.st128(L.hb + 32u, 0u, 0u, 0u, 0u);
-        m.st128(L.hb + 48u, 0u, 0u, 0u, 0u);
-        m.st128(L.hb + 64u, 0u, 0u, 0u, 0u);
-        L.hb += 80u;
-        m.set_tcx(L.mbx, L.TL & 511u);
-        next_mb(L, m);
-        return;
-    }
+    const uint32_t lm = mr[0] & 7u;
+    L.TL = TL;
     const uint32_t c = lm == 4u ? 1u : 0u;
     L.dsb = c * NDESC;
     L.k = c;
     L.nzm2 = L.nlv = 0;
     L.lvb = L.hb + 80u;
     uint32_t d[4];
-    m.desc(L.dsb + L.k, d);
-    L.dx = d[0];
-    L.dy = d[1];
     m.desc(L.dsb + L.k + 1u, d);
     L.dnx = d[0];
     L.dny = d[1];
     L.dnz = d[2];
     L.dnw = d[3];
     m.desc(L.dsb + L.k, d);
+    L.dx = d[0];
+    L.dy = d[1];
     const uint32_t ctx = ((L.TL >> (L.dy & 15u)) & 1u) + ((L.TL >> ((L.dy >> 4) & 31u)) & 1u);
     L.first = (L.dy >> 9) & 1u;
     L.n = L.first;
@@ -364,9 +327,358 @@ TKL_HD void mb_phase(Lane& L, M& m)
     if (c) m.st16c(true, L.hb + 16u, 0u);  // start[0] of an I4 MB
     if (L.first) m.st16c(true, L.lvb, 0u);
     L.st = 0;
+    L.acc = 0;
     L.p = m.prob_at(L.rbl);
     m.tt(0, L.t0, L.t1);
     L.phase = PH_DECIDE;
 }
 
+// mb_end: the MB's last block ended (k == 25): its header, the total level
+// count and the zero pad after its levels; L.hb = the end of the record.
+// (step()'s stores can fall past the record's end -- a ZERO run's zeros after
+// the last nonzero level, position 0 of an empty luma block -- so a memory
+// interface whose MBs are written in parallel drops stores past the MB's end.)
+template <class M>
+TKL_HD void mb_end(Lane& L, M& m)
+{
+    m.st128(L.hb, L.w0, L.nzm2 >> 1, L.w2, L.w3);
+    m.st128(L.hb + 64u, L.nlv, 0u, 0u, 0u);
+    const uint32_t end = (L.lvb + 15u) & ~15u;
+    for (uint32_t a = L.lvb; a < end; a += 2u) m.st16c(true, a, 0u);  // the zero pad (not past the record)
+    L.hb = end;
+}
+
+// A header-only record (a skipped MB, mb_no_coeff_skip): every start 0.
+template <class M>
+TKL_HD void mb_skip(M& m, uint32_t hb, const uint32_t* mr)
+{
+    m.st128(hb, mr[0], 0u, mr[2], mr[3]);
+    m.st128(hb + 16u, 0u, 0u, 0u, 0u);
+    m.st128(hb + 32u, 0u, 0u, 0u, 0u);
+    m.st128(hb + 48u, 0u, 0u, 0u, 0u);
+    m.st128(hb + 64u, 0u, 0u, 0u, 0u);
+}
+
+// Stage 2's lane from stage 1's MB snapshot: s0 = bits shifted out at the MB's
+// start, s1 = the window's top byte | rm1 << 8 | min(vb, 8) << 16 (the top
+// min(vb, 8) bits of that byte are valid, the rest not yet loaded), len = the
+// partition's bytes.  The window is refilled from the stream at s0 + that
+// count, so the MB's decisions are the ones stage 1 made.
+template <class M>
+TKL_HD void from_snapshot(Lane& L, M& m, uint32_t s0, uint32_t s1, uint32_t len)
+{
+    init(L, len, true);
+    const uint32_t vbs = (s1 >> 16) & 15u;
+    const uint64_t top = (uint64_t)(s1 & 255u) << 56;
+    L.V = vbs ? (top | (m.bits64(s0 + vbs) >> vbs)) : m.bits64(s0);
+    L.vb = 64u;
+    L.bp = s0 + 64u;
+    L.rm1 = (s1 >> 8) & 255u;
+}
+
 }  // namespace tokl
+
+// ===========================================================================
+// Stage 1: the serial decision chain alone (the device's k_dec_tok1).
+//
+// A frame's decisions cannot be split (each one's range and value depend on the
+// one before), so the chain's length per decision is what a batch waits for.
+// Stage 1 carries only what the next decision needs: the bool decoder, one
+// state index S and the block contexts.  S folds the tree node, the position n
+// and the row context into one transition table T1[S][bit] (982 states per
+// block type; the same for every frame), whose entry also holds the next
+// state's probability source (a row entry of the frame's table, or a fixed
+// probability), so a decision is the arithmetic, one table select and two LDS
+// reads (probability, T1 entry) for the next.  Levels, starts and records are
+// not built here: at each MB start the lane stores a 16-byte snapshot (stream
+// position, the window's top byte, range, block contexts), and stage 2
+// (k_dec_tok2, one MB per lane, thousands of MBs in parallel) replays each MB
+// from its snapshot with step() above and writes the packed records.
+//
+// States (n = position 0..15, c = row context 0..2):
+//   TN(n, c, node)  tree node 0..10 of the token at n, row (band(n), c)
+//   FR(first, c)    node 0 of a block's first token (EOB here: the block is empty)
+//   SG(n, c')       the sign of the token at n; c' = the next row context (1 after a ONE, else 2)
+//   XS(n, j)        extra bit j of a category token at n (tokl states 12 + j), fixed probabilities
+// Entry (state, bit): next state * 8 (its T1 row's byte offset, bits 0..12) |
+// its probability source << 13 (a row entry e as e * U, or the fixed
+// probability) | fixed << 29 | the block's non-zero flag << 30 | block end << 31.
+// A block-end entry's next state is the next block's FR(first, ctx), which the
+// lane computes from the contexts (popcount of its two context bits).
+// ===========================================================================
+namespace tok1 {
+using namespace tokl;
+
+// SINK (982): the state of a lane that makes no decision (waiting for the MB
+// phase, or done): both entries lead back to it and leave everything but the
+// decoder unchanged, so the wave steps every lane without a branch.
+constexpr uint32_t FR0 = 528, SG0 = 534, XS0 = 566, SINK = 982, NS = 983;
+constexpr uint32_t E_BE = 1u << 31, E_NZ = 1u << 30, E_FX = 1u << 29, E_S = 0x1FFFu, E_PV = 13;
+constexpr uint32_t E_SINK = SINK * 8u | (128u << E_PV) | E_FX;
+constexpr uint32_t NDESC1 = 27;
+// the lane's k: 0..24 a block of the MB (decisions), 25 the MB phase is due, 26 done
+constexpr uint32_t K_MB = 25, K_DONE = 26;
+
+TKL_HD constexpr uint32_t tn(uint32_t n, uint32_t c, uint32_t node) { return n * 33u + c * 11u + node; }
+TKL_HD constexpr uint32_t fr(uint32_t first, uint32_t c) { return FR0 + first * 3u + c; }
+TKL_HD constexpr uint32_t sg(uint32_t n, uint32_t c1) { return SG0 + n * 2u + (c1 - 1u); }
+TKL_HD constexpr uint32_t xs(uint32_t n, uint32_t j) { return XS0 + n * 26u + j; }
+
+// tokl states 12..37 (the categories' extra bits): probability and successor (11 = the sign)
+TKL_HD constexpr uint32_t cat_prob(uint32_t s)
+{
+    constexpr uint8_t P[26] = {159, 165, 145, 173, 148, 140, 176, 155, 140, 135, 180, 157, 141,
+                               134, 130, 254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129};
+    return P[s - 12u];
+}
+TKL_HD constexpr uint32_t cat_next(uint32_t s)
+{
+    return (s == 12u || s == 14u || s == 17u || s == 21u || s == 26u || s == 37u) ? 11u : s + 1u;
+}
+
+template <uint32_t U>
+struct Table {
+    uint32_t e[2 * NS];
+    // an entry going to state s (its probability source with it)
+    static constexpr uint32_t to(uint32_t s)
+    {
+        if (s < FR0) {
+            const uint32_t n = s / 33u, c = (s % 33u) / 11u, node = s % 11u;
+            return s * 8u | ((band(n) * 33u + c * 11u + node) * U) << E_PV;
+        }
+        if (s < XS0) return s * 8u | (128u << E_PV) | E_FX;  // a sign (FR states are never a direct target)
+        const uint32_t j = (s - XS0) % 26u;
+        return s * 8u | (cat_prob(12u + j) << E_PV) | E_FX;
+    }
+    // the token at n ended (a ZERO goes on at node 1 with context 0, a token at node 0)
+    static constexpr uint32_t next_pos(uint32_t n, uint32_t c1, uint32_t node)
+    {
+        return n + 1u == 16u ? (E_BE | E_NZ) : to(tn(n + 1u, c1, node));
+    }
+    constexpr Table() : e()
+    {
+        for (uint32_t n = 0; n < 16; n++)
+            for (uint32_t c = 0; c < 3; c++) {
+                uint32_t* t = e + 2 * tn(n, c, 0);
+                t[0] = E_BE | E_NZ;                       // node 0: EOB
+                t[1] = to(tn(n, c, 1));
+                t[2] = next_pos(n, 0, 1);                 // node 1: ZERO
+                t[3] = to(tn(n, c, 2));
+                t[4] = to(sg(n, 1));                      // node 2: ONE
+                t[5] = to(tn(n, c, 3));
+                t[6] = to(tn(n, c, 4));                   // node 3
+                t[7] = to(tn(n, c, 6));
+                t[8] = to(sg(n, 2));                      // node 4: TWO
+                t[9] = to(tn(n, c, 5));
+                t[10] = t[11] = to(sg(n, 2));             // node 5: THREE / FOUR
+                t[12] = to(tn(n, c, 7));                  // node 6
+                t[13] = to(tn(n, c, 8));
+                t[14] = to(xs(n, 0));                     // node 7: cat1 / cat2
+                t[15] = to(xs(n, 1));
+                t[16] = to(tn(n, c, 9));                  // node 8
+                t[17] = to(tn(n, c, 10));
+                t[18] = to(xs(n, 3));                     // node 9: cat3 / cat4
+                t[19] = to(xs(n, 6));
+                t[20] = to(xs(n, 10));                    // node 10: cat5 / cat6
+                t[21] = to(xs(n, 15));
+            }
+        for (uint32_t first = 0; first < 2; first++)
+            for (uint32_t c = 0; c < 3; c++) {
+                e[2 * fr(first, c)] = E_BE;  // EOB first: an empty block
+                e[2 * fr(first, c) + 1] = to(tn(first, c, 1));
+            }
+        e[2 * SINK] = e[2 * SINK + 1] = E_SINK;
+        for (uint32_t n = 0; n < 16; n++) {
+            for (uint32_t c1 = 1; c1 < 3; c1++) e[2 * sg(n, c1)] = e[2 * sg(n, c1) + 1] = next_pos(n, c1, 0);
+            for (uint32_t j = 0; j < 26; j++) {
+                const uint32_t ns = cat_next(12u + j);
+                e[2 * xs(n, j)] = e[2 * xs(n, j) + 1] = ns == 11u ? to(sg(n, 2)) : to(xs(n, ns - 12u));
+            }
+        }
+    }
+};
+
+// Descriptor of block k in MB class c (tokl::desc's blocks): its two context
+// bits in TL, its type's row base (type * 264 * U), FR(first, 0) * 8, and the
+// probability source of FR(first, 0) (band(first) * 33 * U); k = 25, 26 and
+// (c = 1, k = 0) lead to SINK (no context bits, FR = SINK).
+template <uint32_t U>
+TKL_HD constexpr void desc1(uint32_t c, uint32_t k, uint32_t* d)
+{
+    uint32_t q[4] = {0, 0, 0, 0};
+    tokl::desc(c, k, q);
+    d[0] = q[0];
+    d[1] = q[3] * U;
+    const uint32_t first = (q[1] >> 9) & 1u;
+    d[2] = q[0] ? fr(first, 0) * 8u : SINK * 8u;
+    d[3] = band(first) * 33u * U;
+}
+
+struct Lane1 {
+    uint64_t V;
+    uint32_t vb, bp, rm1;
+    uint32_t pr, pv, pf;       // this decision's probability: pf ? pv : pr (pr read from the frame's table)
+    uint32_t t0, t1;           // its T1 entries
+    uint32_t tbl, TL, dx, k, dsb;
+    uint32_t dnx, dnt, dnf, dnp;  // the next block's descriptor
+    uint32_t mbi, mbx, sk;        // sk: the MB phase continues a run of skipped MBs
+    uint32_t tcn;                 // the top contexts of the next MB's column (read ahead)
+};
+
+TKL_HD void init1(Lane1& L, bool active)
+{
+    L.V = 0;
+    L.vb = L.bp = 0;
+    L.rm1 = 254;
+    L.pr = L.pv = L.pf = 0;
+    L.t0 = L.t1 = E_SINK;
+    L.tbl = L.TL = L.dx = L.dsb = 0;
+    L.k = active ? K_MB : K_DONE;
+    L.dnx = L.dnt = L.dnf = L.dnp = 0;
+    L.mbi = L.mbx = 0;
+    L.sk = 1;  // (nothing to finish before MB 0)
+    L.tcn = 0;
+}
+
+template <class M>
+TKL_HD void topup1(Lane1& L, M& m)
+{
+    if (L.vb < 64u) {
+        const uint64_t s = m.bits64(L.bp);
+        L.V |= s >> L.vb;
+        L.bp += 64u - L.vb;
+        L.vb = 64u;
+    }
+}
+
+TKL_HD uint32_t popc(uint32_t x)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_popcount(x);
+#else
+    return (uint32_t)__builtin_popcount(x);
+#endif
+}
+
+// bfi(m, a, b) = (a & m) | (b & ~m): a per-lane select by a mask (v_bfi_b32),
+// which the compiler keeps as one instruction instead of an exec-mask branch
+TKL_HD uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+// One decision (tokl::step's arithmetic), the transition and, at a block's end,
+// the next block's first state from its contexts.  A lane in SINK (k >= 25)
+// keeps its decoder state; the rest of its state stays by SINK's entries.
+template <class M>
+TKL_HD void step1(Lane1& L, M& m)
+{
+    constexpr uint32_t U = M::U;
+    const bool fz = L.k >= K_MB;
+    const uint32_t p = L.pf ? L.pv : L.pr;
+    const uint32_t sm1 = mul24(L.rm1, p) >> 8;  // split - 1
+    const uint32_t big = (sm1 << 24) + (1u << 24);
+    uint32_t vh = (uint32_t)(L.V >> 32);
+    const bool bit = vh >= big;
+    // the next decision's state first: its probability and T1 reads go out
+    // before the rest of the step, which runs while they are in flight
+    const uint32_t e = bit ? L.t1 : L.t0;
+    const uint32_t bm = (uint32_t)((int32_t)e >> 31);                       // all ones at a block end
+    const uint32_t nzm = (uint32_t)((int32_t)(e << 1) >> 31) & L.dx;        // the ended block's bits if non-zero
+    const uint32_t TL = bfi(bm, (L.TL & ~L.dx) | nzm, L.TL);
+    const uint32_t bctx = popc(TL & L.dnx);
+    const uint32_t S8 = bfi(bm, L.dnf + bctx * 8u, e & E_S);
+    const uint32_t pv = bfi(bm, L.dnp + mul24(bctx, 11u * U), (e >> E_PV) & 0xFFFFu);
+    const uint32_t tbl = bfi(bm, L.dnt, L.tbl);
+    L.pr = m.prob_at(tbl + pv);
+    m.tt1(S8, L.t0, L.t1);
+#ifdef __HIP_DEVICE_COMPILE__
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    L.TL = TL;
+    L.tbl = tbl;
+    L.pv = pv;
+    L.pf = e & E_FX;  // (block-end entries have E_FX clear)
+    // the block bookkeeping (the next descriptor's read goes out next)
+    L.dx = bfi(bm, L.dnx, L.dx);
+    const uint32_t k = L.k - bm;
+    L.k = k;
+    uint32_t dn[4];
+    m.desc1(L.dsb + k + 1u, dn);
+#ifdef __HIP_DEVICE_COMPILE__
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    // the decoder's update
+    const uint32_t r = bit ? L.rm1 - sm1 : sm1 + 1u;
+    vh -= bit ? big : 0u;
+    const uint32_t sh = (uint32_t)__builtin_clz(r) - 24u;
+    L.rm1 = fz ? L.rm1 : (r << sh) - 1u;
+    L.V = fz ? L.V : ((((uint64_t)vh) << 32) | (uint32_t)L.V) << sh;
+    L.vb = fz ? L.vb : L.vb - sh;
+    L.dnx = dn[0];
+    L.dnt = dn[1];
+    L.dnf = dn[2];
+    L.dnp = dn[3];
+#ifdef __HIP_DEVICE_COMPILE__
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// The MB phase (lanes with k = 25): finish the MB whose last block ended (its
+// top contexts), then start the next MB (a skipped one is context bookkeeping
+// only: the lane stays at k = 25) or finish the frame (k = 26).  m.cls(i): bit 0 = MB i is I4, bit 1 = skipped.
+// m.snap(c, i, s0, s1, TL): if c, MB i's snapshot (from_snapshot above).  The
+// next column's top contexts are read when an MB starts (the row above wrote
+// them long before), so the MB phase waits for no context read.  (Frames of one
+// MB column, whose next MB's top contexts are the MB's own, parse on the host.)
+// m.set_tcx(mbw, v) writes a dummy column.
+template <class M>
+TKL_HD void mb1(Lane1& L, M& m)
+{
+    constexpr uint32_t U = M::U;
+    // (written branch-free: at 64 lanes some lane is at an MB boundary in most
+    // MB phases, and every branch costs the whole wave)
+    const bool fin = L.sk == 0u;  // the MB's last block ended: its column's top contexts, then the next MB
+    m.set_tcx(fin ? L.mbx : m.mbw, L.TL & 511u);  // (column mbw: a dummy)
+    const uint32_t mbi = L.mbi + (fin ? 1u : 0u);
+    const uint32_t mbx = fin ? (L.mbx + 1u == m.mbw ? 0u : L.mbx + 1u) : L.mbx;
+    const bool done = mbi == m.nmb;
+    const uint32_t cs = m.cls(done ? mbi - 1u : mbi);
+    const bool skip = (cs & 2u) != 0u, i4 = (cs & 1u) != 0u;
+    const uint32_t TL = (mbx == 0 ? 0u : (L.TL & 0x01FF0000u)) | L.tcn;
+    const uint32_t mbxn = mbx + 1u == m.mbw ? 0u : mbx + 1u;
+    const uint32_t tcn = m.tcx(mbxn);  // (the row above wrote it; with mbw = 2 and fin, the write above)
+    // a skipped MB: parse_mbs's contexts (every one but Y2's, kept for I4 MBs, becomes 0)
+    const uint32_t TLs = i4 ? (TL & 0x00010001u) : 0u;
+    m.set_tcx(skip && !done ? mbx : m.mbw, TLs & 511u);
+    // an MB with tokens: its snapshot and first block
+    const bool start = !done && !skip;
+    const uint32_t vbs = L.vb < 8u ? L.vb : 8u;
+    m.snap(start, mbi, L.bp - L.vb, (uint32_t)(L.V >> 56) | (L.rm1 << 8) | (vbs << 16), TL);
+    // the class's first two blocks (constants: I16 starts at Y2, I4 at Y 0)
+    uint32_t a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0}, b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};
+    desc1<U>(0, 0, a0);
+    desc1<U>(0, 1, a1);
+    desc1<U>(1, 1, b0);
+    desc1<U>(1, 2, b1);
+    const uint32_t dx = i4 ? b0[0] : a0[0], tbl = i4 ? b0[1] : a0[1];
+    const uint32_t bctx = popc(TL & dx);
+    const uint32_t S8 = start ? (i4 ? b0[2] : a0[2]) + bctx * 8u : SINK * 8u;
+    const uint32_t pv = (i4 ? b0[3] : a0[3]) + mul24(bctx, 11u * U);
+    L.pv = pv;
+    L.pf = 0;
+    L.pr = m.prob_at(tbl + pv);
+    m.tt1(S8, L.t0, L.t1);
+    L.dx = dx;
+    L.tbl = tbl;
+    L.dsb = i4 ? NDESC1 : 0u;
+    L.dnx = i4 ? b1[0] : a1[0];
+    L.dnt = i4 ? b1[1] : a1[1];
+    L.dnf = i4 ? b1[2] : a1[2];
+    L.dnp = i4 ? b1[3] : a1[3];
+    L.k = done ? K_DONE : (skip ? K_MB : (i4 ? 1u : 0u));
+    L.sk = skip ? 1u : 0u;
+    L.TL = skip ? TLs : TL;
+    L.tcn = tcn;
+    L.mbi = skip ? mbi + 1u : mbi;
+    L.mbx = skip ? mbxn : mbx;
+}
+
+}  // namespace tok1

@@ -166,6 +166,7 @@ SIGNATURES = [
     ("zw_decode_kernel_times", _I, [_VP, _VP]),
     ("zw_decode_stage_times", _I, [_VP, _VP]),
     ("zw_decode_token_ms", _I, [_VP, _VP]),
+    ("zw_decode_token_stages", _I, [_VP, _VP]),
     ("zw_dbg_tokl_frame", _I, [_VP, _SZ, ctypes.POINTER(_I)]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
@@ -484,6 +485,16 @@ def dbg_tokl_frame(vp8):
     m = ctypes.c_int(-1)
     rc = L.zw_dbg_tokl_frame(_ptr(a) if a.size else None, a.size, ctypes.byref(m))
     return rc, m.value
+
+
+def decode_token_stages(ctx=None):
+    """Device time of the last batch's token parse by stage (ms): stage 1
+    (k_dec_tok1, the decision chains), the count pass + offsets (k_dec_tok2
+    count, scans, and the host's wait for the total), the record pass."""
+    c = _ctx(ctx)
+    ms = (ctypes.c_float * 3)()
+    _check(c._lib.zw_decode_token_stages(c.handle, ms), "decode_token_stages")
+    return float(ms[0]), float(ms[1]), float(ms[2])
 
 
 def decode_stage_times(ctx=None):

@@ -229,14 +229,20 @@ int zw_decode_kernel_times(zw_ctx *ctx, float *ms);
  * or images device->host, ms[2] download + fan-out into the output buffers
  * (a chunk's download runs in parts, each fanned out while the next lands). */
 int zw_decode_stage_times(zw_ctx *ctx, float *ms);
-/* Device time of the last decode batch's token parse (k_dec_tokl, one frame per
- * lane; 0 when the host parsed every frame's tokens).  The device parses the
+/* Device time of the last decode batch's token parse (k_dec_tok1 + k_dec_tok2:
+ * one frame per lane, then one MB per lane; 0 when the host parsed every
+ * frame's tokens).  The device parses the
  * token partitions (read_coefficients, decoder/vp8.rs:872-1058) of a batch's
  * later frames while the host parses the earlier chunks; headers and modes stay
  * on the host.  ZW_DEC_TOKENS=host|device|mixed forces the host, the device or a
  * split (ZW_DEC_TOKENS_HOST = the host's share); frames with several token
  * partitions always parse on the host. */
 int zw_decode_token_ms(zw_ctx *ctx, float *ms);
+/* The same by stage (ms): ms[0] stage 1 (k_dec_tok1: each frame's decision
+ * chain on one lane, a snapshot per MB), ms[1] the count pass (k_dec_tok2 over
+ * every MB from its snapshot) + record offsets + the host's wait for the total,
+ * ms[2] the record pass (k_dec_tok2 writing the packed records). */
+int zw_decode_token_stages(zw_ctx *ctx, float *ms);
 /* Test hook, host only (no device work): steps the device token parse's
  * per-lane state machine (k_dec_tokl) over one VP8 frame on the CPU and compares
  * its packed MB records with the host parser's.  Returns the host parse's code;
