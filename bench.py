@@ -803,8 +803,13 @@ def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0
         nbytes = sum(len(p.output(i)) for i in range(min(frames, len(seeds))))
         threads = zwebp.host_threads()
         emit_s = float(k[7]) * 1e-3
+        # the pass kernels' time per batch (launches of launch_frames frames run back to
+        # back on the kernel stream): the GPU-side bound of ms_per_batch
+        kspan = (float(k[2]) + float(k[3])) * frames / max(1, p.launch_frames)
         return {"workload": f"{w}x{h} RGBA Q{q} m{m}, {frames} frames per device batch, {steps} pipelined batches",
                 "encodes_per_s": frames * steps / el, "ms_per_batch": el / steps * 1e3,
+                "pass_kernels_ms_per_batch": kspan, "ms_per_batch_over_pass_kernels": (el / steps * 1e3) / kspan
+                if kspan > 0 else None,
                 "frames_per_step": frames, "launch_frames": p.launch_frames,
                 "kernel_ms_per_launch_span": {"encode_pass1": float(k[2]), "encode_pass2": float(k[3])},
                 "host_emit_ms_per_batch": float(k[7]), "host_threads": threads,
@@ -1082,8 +1087,9 @@ def main():
                 pipe.close()
             pipes = []
             s4 = [frame_seed(i) for i in range(4)]
-            line["config5_4k_n1"] = batch_leg(ctx, 3840, 2160, q, m, 256, 2, s4, digests)
-            line["config1_768x512_gpu"] = batch_leg(ctx, 768, 512, q, m, 256, 4, s4, digests)
+            # (8 pipelined batches each: a 2-batch leg measured mostly the pipeline's fill and drain)
+            line["config5_4k_n1"] = batch_leg(ctx, 3840, 2160, q, m, 256, 8, s4, digests)
+            line["config1_768x512_gpu"] = batch_leg(ctx, 768, 512, q, m, 256, 8, s4, digests)
             c5 = line["config5_4k_n1"]
             fpc = c5.get("host_emit_frames_per_s_per_core")
             line["host_budget"] = {

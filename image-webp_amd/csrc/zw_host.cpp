@@ -1716,6 +1716,8 @@ struct Seam {
 };
 std::mutex g_seam_mu;
 std::vector<std::pair<int, Seam*>> g_seams;  // by device; never freed (pointers stay valid)
+// process-wide seam counters (zw_dbg_seam_stats): batches led, frames they held, the largest
+std::atomic<uint64_t> g_seam_batches{0}, g_seam_frames{0}, g_seam_max{0};
 Seam& seam_of(int device)
 {
     std::lock_guard<std::mutex> g(g_seam_mu);
@@ -1822,7 +1824,21 @@ static int seam_encode(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t wi
             drop = p;
             p = nullptr;
         }
+        g_seam_batches.fetch_add(1, std::memory_order_relaxed);
+        g_seam_frames.fetch_add((uint64_t)n, std::memory_order_relaxed);
+        for (uint64_t m = g_seam_max.load(); (uint64_t)n > m && !g_seam_max.compare_exchange_weak(m, (uint64_t)n);) {
+        }
         lk.lock();
+        if (sl.ctx && sl.ctx->poisoned.load()) {
+            // an SDMA copy of this slot's context timed out: its pinned buffers may
+            // still be written, so the context and its pipelines are leaked (the
+            // poisoning policy) and the slot's next batch gets a fresh context
+            // instead of failing every caller in it with ZW_EDEVICE
+            sl.ctx = nullptr;
+            sl.pipes.clear();
+            p = nullptr;
+            drop = nullptr;
+        }
         if (p) {
             sl.pipes.push_back({{kk[0], kk[1], kk[2], kk[3], kk[4], kk[5]}, n, p, ++S.clock});
             if ((int)sl.pipes.size() > SEAM_PIPES) {
@@ -1846,6 +1862,22 @@ static int seam_encode(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t wi
         }
     }
     return r.rc;
+}
+
+// Test hook: the seam's process-wide counters (batches led, frames in them,
+// the largest batch); reset = 1 clears them.
+extern "C" int zw_dbg_seam_stats(uint64_t* out, int reset)
+{
+    if (!out) return ZW_EINVAL;
+    out[0] = g_seam_batches.load();
+    out[1] = g_seam_frames.load();
+    out[2] = g_seam_max.load();
+    if (reset) {
+        g_seam_batches = 0;
+        g_seam_frames = 0;
+        g_seam_max = 0;
+    }
+    return ZW_OK;
 }
 
 extern "C" int zw_encode_frame_lossy(zw_ctx* ctx, const uint8_t* data, size_t len, uint32_t width, uint32_t height,
@@ -2083,12 +2115,16 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
     HIPOK(hipSetDevice(ctx->device));
     // The I4 queue k_xform_mb fills and k_xform_mb_i4 drains: one per launch
     // stream, grow-only (a regrow frees the old buffer, which hipFree orders
-    // after queued work).  A completed launch pair leaves its counters zero; a
-    // new buffer, or one whose last launch pair failed to queue, is reset on the
-    // launch stream first.  So neither an overlapping launch on another stream
-    // nor a launch that stopped partway can leave a stale count.
+    // after queued work).  The queue keeps one count per launch parity: a launch
+    // appends to count qp and its drain zeroes count qp ^ 1 (the previous
+    // launch's, drained earlier in stream order), so a launch pair leaves its own
+    // count nonzero and the next launch, of the other parity, starts from zero.
+    // A new buffer, or one whose last launch pair failed to queue, is reset on
+    // the launch stream first.  So neither an overlapping launch on another
+    // stream nor a launch that stopped partway can leave a stale count.
     // At most XMB_QUEUES streams keep a queue: a new stream takes the least
-    // recently used one's entry (hipFree of its buffer waits for the device).
+    // recently used idle one's entry (hipFree of its buffer waits for the
+    // device); an entry whose launch another thread is queueing is never taken.
     // An overflow any launch reports through the context's host-visible error
     // word (k_xform_mb, never expected) fails this and every later call.
     const hipStream_t ls = stream ? (hipStream_t)stream : ctx_stream(ctx);
@@ -2115,11 +2151,14 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
         zw_ctx::XmbQueue* e = nullptr;
         for (auto& x : ctx->xmb_q)
             if (x.stream == ls) e = &x;
+        if (e && e->inflight && e->cap < qb) e = nullptr;  // (another thread queues on it: a new entry to regrow)
         if (!e && ctx->xmb_q.size() >= XMB_QUEUES) {
             for (auto& x : ctx->xmb_q)
-                if (!e || x.used < e->used) e = &x;
-            if (e->buf) (void)hipFree(e->buf);
-            *e = {ls, nullptr, 0};
+                if (x.inflight == 0 && (!e || x.used < e->used)) e = &x;
+            if (e) {
+                if (e->buf) (void)hipFree(e->buf);
+                *e = {ls, nullptr, 0};
+            }
         }
         if (!e) {
             ctx->xmb_q.push_back({ls, nullptr, 0});
@@ -2139,6 +2178,7 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
         if (qe->dirty) HIPOK(hipMemsetAsync(q, 0, 16, ls));
         qe->dirty = true;
         qp = qe->parity;
+        qe->inflight++;
         // test hook: a stale count past this launch's MBs, as a shared queue would leave
         if (getenv("ZW_XMB_FORCE_OVERFLOW")) {
             const uint32_t stale = (uint32_t)((size_t)nframes * mbw * mbh);
@@ -2146,16 +2186,21 @@ static int xmb_launch(zw_ctx* ctx, void* stream, int nframes, uint32_t mbw, uint
             HIPOK(hipStreamSynchronize(ls));  // (the source is on this stack)
         }
     }
-    HIPOK(zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp, (int)w, (int)h,
-                       img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh, nframes, (int16_t*)d_levels,
-                       (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, (uint32_t*)q, qp, ctx->xmb_err_dev,
-                       xmb_variant()));
+    const hipError_t le = zwk_xform_mb(ls, (const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, src_bpp,
+                                       (int)w, (int)h, img_stride, (const uint8_t*)d_recs, d_segs, (int)mbw, (int)mbh,
+                                       nframes, (int16_t*)d_levels, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv,
+                                       (uint32_t*)q, qp, ctx->xmb_err_dev, xmb_variant());
     {
         std::lock_guard<std::mutex> lk(ctx->xmb_mu);
+        qe->inflight--;
         // both kernels queued: the pair leaves count qp ^ 1 zero for the next launch
-        qe->dirty = false;
-        qe->parity ^= 1;
+        // (a failed launch leaves the entry dirty: reset before its next use)
+        if (le == hipSuccess) {
+            qe->dirty = false;
+            qe->parity ^= 1;
+        }
     }
+    HIPOK(le);
     return ZW_OK;
 }
 

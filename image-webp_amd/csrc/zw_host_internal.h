@@ -41,6 +41,7 @@ struct zw_ctx {
         bool dirty = true;  // counters not known to be zero: reset on the stream first
         int parity = 0;     // the count the next launch appends to (k_xform_mb's qp)
         uint64_t used = 0;  // xmb_clock at the last launch (LRU eviction past 8 streams)
+        int inflight = 0;   // launches being queued on it (between the two locked sections): not evictable
     };
     std::deque<XmbQueue> xmb_q;  // (a deque: entries stay put while others are added)
     uint64_t xmb_clock = 0;

@@ -168,6 +168,7 @@ SIGNATURES = [
     ("zw_decode_token_ms", _I, [_VP, _VP]),
     ("zw_decode_token_stages", _I, [_VP, _VP]),
     ("zw_dbg_tokl_frame", _I, [_VP, _SZ, ctypes.POINTER(_I)]),
+    ("zw_dbg_seam_stats", _I, [_VP, _I]),
     ("zw_pipe_encode", _I, [_VP]),
     ("zw_pipe_encode_repeat", _I, [_VP, _I]),
     ("zw_pipe_encode_host", _I, [_VP, _I, _VP]),
@@ -485,6 +486,15 @@ def dbg_tokl_frame(vp8):
     m = ctypes.c_int(-1)
     rc = L.zw_dbg_tokl_frame(_ptr(a) if a.size else None, a.size, ctypes.byref(m))
     return rc, m.value
+
+
+def dbg_seam_stats(reset=False):
+    """Test hook: the encode seam's counters (batches led, frames in them, the
+    largest batch) since the last reset."""
+    L = load_library()
+    out = (ctypes.c_uint64 * 3)()
+    _check(L.zw_dbg_seam_stats(out, 1 if reset else 0), "dbg_seam_stats")
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def decode_token_stages(ctx=None):

@@ -244,11 +244,16 @@ int zw_decode_token_ms(zw_ctx *ctx, float *ms);
  * ms[2] the record pass (k_dec_tok2 writing the packed records). */
 int zw_decode_token_stages(zw_ctx *ctx, float *ms);
 /* Test hook, host only (no device work): steps the device token parse's
- * per-lane state machine (k_dec_tokl) over one VP8 frame on the CPU and compares
- * its packed MB records with the host parser's.  Returns the host parse's code;
+ * state machines (k_dec_tok1's decision chain, then k_dec_tok2's per-MB replay
+ * from each MB's snapshot) over one VP8 frame on the CPU and compares the
+ * packed MB records with the host parser's.  Returns the host parse's code;
  * *match = 1 (records equal, or both failed), 0 (they differ), -1 (a frame the
- * device parse never takes: several partitions, or a header / mode error). */
+ * device parse never takes: several partitions, one MB column, or a header /
+ * mode error). */
 int zw_dbg_tokl_frame(const uint8_t *vp8, size_t len, int *match);
+/* Test hook: the encode seam's process-wide counters -- out[0] batches led,
+ * out[1] frames in them, out[2] the largest batch; reset != 0 clears them. */
+int zw_dbg_seam_stats(uint64_t *out, int reset);
 /* ... and of its k_yuv2rgb launch (0 when the batch returned planes). */
 int zw_decode_rgb_kernel_ms(zw_ctx *ctx, float *ms);
 

@@ -10,6 +10,7 @@ row-parallel decode.
   (+ ICCP / EXIF / XMP) byte-equal to the oracle's pieces in the reference's
   chunk order; libwebp round trip when the system library is present.
 """
+import os
 import ctypes
 import struct
 
@@ -435,11 +436,81 @@ def test_decode_batch_mixed_sizes(ctx, monkeypatch, tokens):
     assert e.value.code == rc
 
 
+_SEAM_CHILD = r"""
+import os, sys, threading
+sys.path[:0] = [os.path.join(sys.argv[1], "image-webp_amd"), os.path.join(sys.argv[1], "tests")]
+import numpy as np
+import zwebp
+import oracle_lib as O
+from zwebp.synth import synth_rgba
+shapes = [(96, 64, 75, 4, 1), (96, 64, 40, 2, 1), (48, 80, 75, 4, 2)]
+imgs = {s: [synth_rgba(s[0], s[1], 0x5EA0 + 7 * i + s[2]) for i in range(4)] for s in shapes}
+want = {}
+for s in shapes:
+    for i, im in enumerate(imgs[s]):
+        rc, b, _ = O.encode(im, s[0], s[1], 3, s[2], s[3], nparts=s[4])
+        assert rc == 0
+        want[(s, i)] = b
+zwebp.dbg_seam_stats(reset=True)
+T, calls = 24, 6
+bad, errs = [], []
+def work(t):
+    c = zwebp.Context(0)
+    try:
+        for k in range(calls):
+            s = shapes[(t + k) % len(shapes)]
+            i = (t * 5 + k) % 4
+            got = zwebp.encode_frame_lossy(imgs[s][i], s[0], s[1], zwebp.ColorType.Rgba8, s[2], s[3], ctx=c,
+                                           token_partitions=s[4])
+            if bytes(got) != want[(s, i)]:
+                bad.append((t, k, s, i))
+    except Exception as e:
+        errs.append(repr(e))
+    finally:
+        c.close()
+th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+for x in th:
+    x.start()
+for x in th:
+    x.join(timeout=240)
+st = zwebp.dbg_seam_stats()
+print("seam", st, "bad", bad[:4], "errs", errs[:4], flush=True)
+assert not errs and not bad, (errs, bad[:4])
+assert st[1] == T * calls and st[2] >= 2, st  # every call went through the seam, some in shared batches
+# an invalid call fails on its own without joining (or stalling) a batch
+c = zwebp.Context(0)
+try:
+    zwebp.encode_frame_lossy(imgs[shapes[0]][0].reshape(-1)[:100], 96, 64, zwebp.ColorType.Rgba8, 75, 4, ctx=c)
+    raise SystemExit("an invalid call succeeded")
+except zwebp.ZwError:
+    pass
+c.close()
+print("ok", flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_seam_batches_concurrent_calls():
+    """The seam itself (zw_host.cpp seam_encode): in a fresh process with
+    ZW_SEAM_SOLO=0 (read once, at the first call) every encode_frame_lossy call
+    joins the seam; 24 threads with contexts of their own over three shapes
+    (sizes, quality, method, partitions) form shared batches of mixed callers
+    (the counters show frames per batch > 1), each caller gets exactly the
+    oracle's bitstream for its own frame, and an invalid call fails alone."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ZW_SEAM_SOLO="0")
+    r = subprocess.run([sys.executable, "-c", _SEAM_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
 @pytest.mark.gpu
 def test_seam_concurrent_single_frame_calls(ctx):
     """encode_frame_lossy from 12 threads, each with a context of its own, over
-    three shapes (sizes, quality, method, partitions): the seam batches the
-    concurrent calls of one shape into shared launches, and every call returns
+    three shapes (sizes, quality, method, partitions): below ZW_SEAM_SOLO calls
+    in flight each encodes on its own (the solo path), and every call returns
     exactly the oracle's bitstream for its own frame."""
     import threading
     shapes = [(96, 64, 75, 4, 1), (96, 64, 40, 2, 1), (48, 80, 75, 4, 2)]
