@@ -390,13 +390,13 @@ def xmb_pass(ctx, torch, dev, pipe, nd, seeds, w, h, q, m, frames=256, reps=10, 
 
 
 def device_tokens_leg(ctx, streams, frames, tags, digests):
-    """Batch decode where the device token parse takes part (k_dec_tokl, one
-    frame per lane): one launch parses a share of the batch's token partitions
-    in ≈250 ms whatever its frame count, so the auto split hands it the frames
-    the host would not finish in that time -- none at 1 024 1080p frames, most
-    of them here.  The same batch with ZW_DEC_TOKENS=host for comparison.
-    Planes of a sample of frames across the host and device shares (every 61st)
-    are hashed against the oracle's decode digests."""
+    """Batch decode where the device token parse takes part (k_dec_tok1, one
+    frame's decision chain per lane, then k_dec_tok2, every MB replayed from its
+    snapshot): the chain of one frame takes about as long as the whole launch,
+    whatever its frame count, so the auto split hands the device the frames the
+    host would not finish in that time.  The same batch with ZW_DEC_TOKENS=host
+    for comparison.  Planes of a sample of frames across the host and device
+    shares (every 61st) are hashed against the oracle's decode digests."""
     import zwebp
     batch = [streams[i % len(streams)] for i in range(frames)]
     res = {}
@@ -413,7 +413,10 @@ def device_tokens_leg(ctx, streams, frames, tags, digests):
             dec = zwebp.decode_batch(batch, ctx=ctx)
             el = time.perf_counter() - t0
             st = zwebp.decode_stage_times(ctx=ctx)
+            ts = zwebp.decode_token_stages(ctx=ctx)
             res[mode] = {"decodes_per_s": frames / el, "device_token_ms": zwebp.decode_token_ms(ctx=ctx),
+                         "device_token_stages_ms": {"k_dec_tok1": ts[0], "count_and_offsets": ts[1],
+                                                    "records": ts[2]},
                          "host_parse_ms": st[0], "download_ms": st[1], "fanout_ms": st[2]}
             if mode == "auto" and tags is not None:
                 for i in range(0, frames, 61):
@@ -469,17 +472,24 @@ def decode_path(ctx, streams, frames, w, h, with_cpu, tags=None, digests=None):
     el = time.perf_counter() - t0
     st = zwebp.decode_stage_times(ctx=ctx)
     tok_ms = zwebp.decode_token_ms(ctx=ctx)
+    tok_st = zwebp.decode_token_stages(ctx=ctx)
     thr = zwebp.host_threads()
     fbytes = len(decb[0].ybuf) + len(decb[0].ubuf) + len(decb[0].vbuf)
     stages = {"host_parse_ms": st[0], "download_ms": st[1], "fanout_ms": st[2], "host_threads": thr,
-              "parse_ms_per_frame_per_thread": st[0] * thr / pipe_frames,
-              "parse_bound_decodes_per_s": pipe_frames / (st[0] * 1e-3) if st[0] > 0 else None,
+              "parse_ms_per_frame_per_thread": st[0] * thr / pipe_frames,  # (over every frame of the batch)
+              # the host chunks' parse and the device token parse run side by side
+              "parse_bound_decodes_per_s": pipe_frames / (max(st[0], tok_ms) * 1e-3) if max(st[0], tok_ms) > 0
+              else None,
               "download_gbs": pipe_frames * fbytes / (st[1] * 1e-3) / 1e9 if st[1] > 0 else None,
               "download_bound_decodes_per_s": pipe_frames / (st[1] * 1e-3) if st[1] > 0 else None,
-              "device_token_ms": tok_ms, "token_split": os.environ.get("ZW_DEC_TOKENS", "auto"),
+              "device_token_ms": tok_ms, "device_token_stages_ms": {"k_dec_tok1": tok_st[0],
+                                                                      "count_and_offsets": tok_st[1],
+                                                                      "records": tok_st[2]},
+              "token_split": os.environ.get("ZW_DEC_TOKENS", "auto"),
               "note": "wall ms summed over chunks; the parse (the host bool decoder's serial chain, every "
-                      "host thread) of chunk c overlaps the download + fan-out of chunk c-1; device_token_ms: "
-                      "k_dec_tokl's launch for the frames whose tokens the device parsed (0: none; the auto split "
+                      "host thread) of chunk c overlaps the download + fan-out of chunk c-1; host_parse_ms counts "
+                      "the host-parsed frames only; device_token_ms: the device token parse (k_dec_tok1 + "
+                      "k_dec_tok2) for the frames whose tokens the device parsed (0: none; the auto split "
                       "leaves a batch to the host when the host alone finishes first)"}
     batch = pbatch[:frames]
     vy = [0, 0, 0]  # matched, mismatched, no digest

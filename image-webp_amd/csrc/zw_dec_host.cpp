@@ -1747,7 +1747,7 @@ extern "C" int zw_dbg_tokl_frame(const uint8_t* vp8, size_t len, int* match)
     for (uint64_t st = 0; L1.k != tok1::K_DONE; st++) {
         if ((st & 7) == 0) tok1::topup1(L1, m1);  // (the device's schedule)
         tok1::step1(L1, m1);  // (as the device: a lane waiting for its MB phase steps in SINK)
-        if ((st & 3) == 3)
+        if ((st & 15) == 15)
             for (int r = 0; r < 8 && L1.k == tok1::K_MB; r++) tok1::mb1(L1, m1);
     }
     // stage 2: count, offsets, records

@@ -29,12 +29,12 @@ namespace {
 __constant__ uint32_t d_TOKL_TT[2 * tokl::NST] = ZW_TOKL_TT_INIT;
 __constant__ tok1::Table<64> d_T1 = tok1::Table<64>();
 
-// stage-1 LDS (dwords): T1, probabilities [264][64] (entry i of lane l at byte i * 64 + l),
+// stage-1 LDS (dwords): T1 (static), then dynamic: probabilities [264][64] (entry i of lane l at byte i * 64 + l),
 // stream ring [16][64] (64 bytes per lane), class ring [4][64] (16 MBs a word), sync
 // words, stage-1 descriptors, then the top contexts [mbw + 1][64] u16 (column mbw: a dummy)
 constexpr int TK1_P = 264 * 64, TK1_SR = 16 * 64, TK1_CR = 4 * 64, TK1_SY = 4 * 64 + 4, TK1_T = 2 * tok1::NS,
               TK1_D = 2 * 4 * tok1::NDESC1;
-constexpr int TK1_FIXED = TK1_P + TK1_SR + TK1_CR + TK1_SY + TK1_T + TK1_D + 32;  // (+ the dummy column)
+constexpr int TK1_FIXED = TK1_P + TK1_SR + TK1_CR + TK1_SY + TK1_D + 32;  // dynamic (+ the dummy column); T1 is static
 constexpr uint32_t TKL_SPIN = 1u << 22;
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;  // (a generic volatile pointer would become a flat access)
@@ -59,7 +59,7 @@ struct Tok1Dev {
     DI uint32_t prob_at(uint32_t a) const { return P8[a + lane]; }
     DI void tt1(uint32_t s8, uint32_t& t0, uint32_t& t1) const
     {
-        const uint2 v = *(const uint2*)((const uint8_t*)T1 + s8);  // (T1 at LDS address 0: no add)
+        const uint2 v = *(const uint2*)((const uint8_t*)T1 + s8);
         t0 = v.x;
         t1 = v.y;
     }
@@ -134,7 +134,7 @@ struct Tok1Dev {
 }  // namespace
 
 #ifndef ZW_TOK1_MK
-#define ZW_TOK1_MK 4  // steps between MB phases (a lane at an MB's end idles until the next one; 1, 2, 4 or 8)
+#define ZW_TOK1_MK 16  // steps between MB phases (a lane at an MB's end idles until the next one; a power of 2: 8 / 16 / 32 measured 433 / 390 / 399 cycles a decision)
 #endif
 #ifndef ZW_TOK1_MBRUN
 #define ZW_TOK1_MBRUN 8  // MBs one MB phase may start (skipped MBs need no decisions)
@@ -156,8 +156,8 @@ extern "C" __global__ __launch_bounds__(128) void k_dec_tok1(const uint8_t* __re
                                                             int* err1, int mbw, int mbh, int nframes)
 {
     extern __shared__ uint32_t sm[];
-    uint32_t* T1 = sm;  // (first: its reads need no base)
-    uint32_t* P = T1 + TK1_T;
+    __shared__ uint32_t T1[TK1_T];  // (static: its reads fold the base into the offset)
+    uint32_t* P = sm;
     uint32_t* SR = P + TK1_P;
     uint32_t* CR = SR + TK1_SR;
     uint32_t* SY = CR + TK1_CR;
@@ -265,7 +265,7 @@ extern "C" __global__ __launch_bounds__(128) void k_dec_tok1(const uint8_t* __re
     // rounds of 8 steps: a top-up first (every live lane, whatever its phase:
     // then no lane makes more than 8 decisions between two top-ups), an MB phase
     // every ZW_TOK1_MK steps, the exit test once a round
-    for (;;) {
+    for (uint32_t rnd = 0;; rnd++) {
         if (L.k != tok1::K_DONE) tok1::topup1(L, m);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -273,7 +273,8 @@ extern "C" __global__ __launch_bounds__(128) void k_dec_tok1(const uint8_t* __re
             ndec += L.k < tok1::K_MB;
 #endif
             tok1::step1(L, m);  // (every lane: SINK keeps the waiting ones)
-            if (j % ZW_TOK1_MK == ZW_TOK1_MK - 1) {
+            if ((ZW_TOK1_MK <= 8 && j % ZW_TOK1_MK == ZW_TOK1_MK - 1) ||
+                (ZW_TOK1_MK > 8 && j == 7 && (rnd % (ZW_TOK1_MK / 8)) == ZW_TOK1_MK / 8 - 1)) {
 #ifdef ZW_TOK_PROF
                 n_mb += __builtin_amdgcn_ballot_w64(L.k == tok1::K_MB) != 0;
 #endif
@@ -472,7 +473,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dec_tok_fbase(const uint32_
     if (tid == 1023) *total = s[1023];
 }
 
-extern "C" size_t zw_tok1_lds_bytes(int mbw) { return (size_t)(TK1_FIXED + mbw * 32) * 4; }
+extern "C" size_t zw_tok1_lds_bytes(int mbw) { return (size_t)(TK1_FIXED + TK1_T + mbw * 32) * 4; }  // (static + dynamic)
 
 // Stage 1, then stage 2's count, the scans, and the total's copy to host_total
 // (pinned), all on stream s.  Buffers as the kernels above describe them.
@@ -482,12 +483,12 @@ extern "C" hipError_t zwk_dec_tok_count(hipStream_t s, const uint8_t* blob, cons
                                         uint64_t* d_total, uint64_t* host_total, int mbw, int mbh, int n,
                                         hipEvent_t stage1_done)
 {
-    const size_t lds = zw_tok1_lds_bytes(mbw);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds = zw_tok1_lds_bytes(mbw) - (size_t)TK1_T * 4;  // (the dynamic part)
+    if (lds + (size_t)TK1_T * 4 > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
         const hipError_t e = hipFuncSetAttribute((const void*)k_dec_tok1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 160 * 1024);
+                                                 160 * 1024 - TK1_T * 4);
         if (e != hipSuccess) return e;
         attr = true;
     }

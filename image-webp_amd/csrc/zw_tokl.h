@@ -572,7 +572,7 @@ TKL_HD void step1(Lane1& L, M& m)
 {
     constexpr uint32_t U = M::U;
     const bool fz = L.k >= K_MB;
-    const uint32_t p = L.pf ? L.pv : L.pr;
+    const uint32_t p = bfi(L.pf, L.pv, L.pr);  // (pf: all ones for a fixed probability)
     const uint32_t sm1 = mul24(L.rm1, p) >> 8;  // split - 1
     const uint32_t big = (sm1 << 24) + (1u << 24);
     uint32_t vh = (uint32_t)(L.V >> 32);
@@ -595,7 +595,7 @@ TKL_HD void step1(Lane1& L, M& m)
     L.TL = TL;
     L.tbl = tbl;
     L.pv = pv;
-    L.pf = e & E_FX;  // (block-end entries have E_FX clear)
+    L.pf = (uint32_t)((int32_t)(e << 2) >> 31);  // E_FX as a mask (block-end entries have it clear)
     // the block bookkeeping (the next descriptor's read goes out next)
     L.dx = bfi(bm, L.dnx, L.dx);
     const uint32_t k = L.k - bm;
@@ -610,7 +610,11 @@ TKL_HD void step1(Lane1& L, M& m)
     vh -= bit ? big : 0u;
     const uint32_t sh = (uint32_t)__builtin_clz(r) - 24u;
     L.rm1 = fz ? L.rm1 : (r << sh) - 1u;
-    L.V = fz ? L.V : ((((uint64_t)vh) << 32) | (uint32_t)L.V) << sh;
+    {
+        const uint64_t Vn = ((((uint64_t)vh) << 32) | (uint32_t)L.V) << sh;  // (halves selected: no exec branch)
+        const uint32_t lo = fz ? (uint32_t)L.V : (uint32_t)Vn, hi = fz ? (uint32_t)(L.V >> 32) : (uint32_t)(Vn >> 32);
+        L.V = ((uint64_t)hi << 32) | lo;
+    }
     L.vb = fz ? L.vb : L.vb - sh;
     L.dnx = dn[0];
     L.dnt = dn[1];

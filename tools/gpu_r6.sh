@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU session steps (each under its own time limit; stops at the first
+# Round-6 GPU session steps (each under its own time limit; stops at the first
 # time-limit / fault exit).  STEPS selects, e.g. STEPS="smoke pytest bench".
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 fatal() { case $1 in 124|137|134|139|135|132) return 0;; *) return 1;; esac; }
