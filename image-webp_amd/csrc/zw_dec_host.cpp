@@ -1160,7 +1160,7 @@ template <class ENQ, class FIN>
 static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const size_t* lens, size_t extra_per_frame,
                         ENQ&& enqueue, FIN&& finish)
 {
-    const int C = dec_chunk_frames(), nch = (n + C - 1) / C;
+    const int C = dec_chunk_frames();
     DecBatch B[2];
     ctx->dec_ms[0] = ctx->dec_ms[1] = ctx->dec_ms[2] = 0.f;
     ctx->dec_tok_ms = 0.f;
@@ -1181,22 +1181,47 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
     }
     double host_parse_ms = 0;
     int host_frames = 0;
-    auto first = [&](int c) { return c * C; };
-    auto count = [&](int c) { return std::min(C, n - c * C); };
+    // chunks: C frames while the host parses, then the device-parsed frames in chunks
+    // of up to ZW_DEC_DEV_CHUNK (512): their records are all ready at once when the
+    // device parse ends, so fewer, longer chunks download back to back behind it
+    // (1 024 1080p frames: the tail after the device parse 68 -> ~45 ms)
+    std::vector<int> cb;
+    {
+        static const int DC = [] {
+            const char* e = getenv("ZW_DEC_DEV_CHUNK");
+            const int v = e ? atoi(e) : 512;
+            return v > 0 ? v : 512;
+        }();
+        for (int f = 0; f < n;) {
+            cb.push_back(f);
+            f += f < T.h0 ? std::min(C, T.h0 - f) : DC;
+        }
+        cb.push_back(n);
+    }
+    const int nch = (int)cb.size() - 1;
+    auto first = [&](int c) { return cb[c]; };
+    auto count = [&](int c) { return std::min(cb[c + 1], n) - cb[c]; };
     int err = ZW_OK;
+    // ZW_DEC_TRACE: the chunk timeline (ms from the batch start) on stderr
+    static const bool trace = getenv("ZW_DEC_TRACE") != nullptr;
+    const double tb = dec_now_ms();
     for (int c = 0; c <= nch && !err; c++) {
         int err_f = ZW_OK, err_p = ZW_OK;
         std::thread fin;
+        double tf0 = 0, tf1 = 0, tp0 = 0, tp1 = 0;
         if (c >= 1) {
             fin = std::thread([&, c]() {
                 (void)hipSetDevice(ctx->device);
                 DecBatch& b = B[(c - 1) & 1];
+                tf0 = dec_now_ms() - tb;
                 err_f = finish(b, first(c - 1), count(c - 1));
+                tf1 = dec_now_ms() - tb;
                 float ms = 0.f;
                 if (hipEventElapsedTime(&ms, b.ev[0], b.ev[1]) == hipSuccess) ctx->dec_ms[0] += ms;
                 if (hipEventElapsedTime(&ms, b.ev[1], b.ev[2]) == hipSuccess) ctx->dec_ms[1] += ms;
             });
         }
+        tp0 = dec_now_ms() - tb;
         if (c < nch) {
             if (first(c) >= T.h0 && dec_tok_finish(ctx, T)) {
                 dec_parse_dev(T, first(c), count(c), B[c & 1]);
@@ -1207,6 +1232,7 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             }
             ctx->dec_host_ms[0] += B[c & 1].parse_ms;
         }
+        tp1 = dec_now_ms() - tb;
         if (fin.joinable()) fin.join();
         err = err_f ? err_f : err_p;
         if (c < nch && !err) {
@@ -1214,6 +1240,9 @@ static int dec_pipeline(zw_ctx* ctx, int n, const uint8_t* const* data, const si
             err = dec_launch(ctx, extra_per_frame * count(c), b, c & 1);
             if (!err) err = enqueue(b, first(c), count(c));
         }
+        if (trace)
+            fprintf(stderr, "[dec trace] c=%d %s parse %.1f-%.1f, finish(c-1) %.1f-%.1f, launched %.1f ms\n", c,
+                    c < nch && first(c) >= T.h0 ? "dev " : "host", tp0, tp1, tf0, tf1, dec_now_ms() - tb);
     }
     if (T.nd > 0) {
         if (T.state == 0) (void)hipStreamSynchronize(ctx->tok_);  // (an error before the first device chunk)
