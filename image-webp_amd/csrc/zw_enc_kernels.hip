@@ -841,24 +841,34 @@ struct EncArgs {
     int* dbg;                   // optional pass-2 I4 dump (16*34 ints per MB), may be null
     uint8_t* rows;              // row-parallel kernels: zero-filled ZW_ROWS_HDR + nframes * RowsLayout::frame
     uint32_t* sizes;            // pass 2, may be null: per MB its packed record size (zw_pack_kernels.hip)
+    int nframes;                // frames of the launch (the frame-pair kernel's last workgroup may hold one)
+};
+
+// Per-MB LDS state: what lives from an MB's first search to its stores (the
+// staged source, the luma work buffer with the I4 search's reconstruction, the
+// levels and sub-modes) and the MB row's left contexts.  A wave working two
+// rows at once (the paired kernels) keeps one per row.
+struct MbLds {
+    uint8_t sy[256], su[64], sv[64];  // source MB (staged per MB)
+    uint8_t ws[17 * ZW_BPS];      // luma work buffer (create_border_luma layout)
+    uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
+    int8_t left_derr[4];
+    uint8_t modes[16];
+    int16_t lev[25][16];
 };
 
 // per-wave LDS scratch
 struct WaveLds {
-    uint8_t sy[256], su[64], sv[64];  // source MB (staged per MB)
-    uint8_t ws[17 * ZW_BPS];      // luma work buffer (create_border_luma layout)
+    MbLds mb;                     // the wave's (first) row
     uint8_t cu[9 * ZW_BPS], cv[9 * ZW_BPS];
-    uint8_t left_y[20], left_u[12], left_v[12], left_c[12];
-    int8_t left_derr[4];
     uint32_t uvc[64][8];          // pick_uv -> final_chroma, per lane: its coefficients (i16 pairs) + rows' pred
     int dc[64];
     int y2d[64];
     int y2cost[4];
     int V[2][40];                 // I4 value vectors of the (up to) two sub-blocks of a search step
     int nzt[4], nzl[4];
-    uint8_t modes[16];
-    int16_t lev[25][16];
     int misc[16];
+    uint32_t pst[2][4];           // paired kernels: per MB {lm | need << 4 | seg << 8, i16 score lo, hi, i4 nz | win << 16}
     // row-parallel kernels: this MB's slice of the row above's state (top_y of
     // the MB and of the MB above-right, top_u/v, top_c, top_derr), pulled from
     // and pushed to global memory around each MB
@@ -878,6 +888,7 @@ struct Ctx {
     const ZwSegment* Sl;  // the frame's 4 segments, in LDS
     const LdsTables* T;
     WaveLds* W;
+    MbLds* M;             // the MB's per-row state (&W->mb, or the paired row's)
     uint8_t *top_y, *top_u, *top_v, *top_c;
     int8_t* top_derr;
     const uint8_t *srcY, *srcU, *srcV;  // MB origin (HBM)
@@ -890,14 +901,14 @@ struct Ctx {
                             // top_* point at the wave's per-MB window)
 };
 
-// create_border_luma (prediction.rs:15) into W->ws
+// create_border_luma (prediction.rs:15) into C.M->ws
 // part 0: corner, top and left (everything the I16 search reads: available once
 // the MB above is done); part 1: the top-right pixels (row 0 columns 17..31 and
 // their copies at rows 4, 8, 12; the I4 search needs the MB above-right);
 // part 2: both.
 __device__ void build_luma_border(const Ctx& C, int part = 2)
 {
-    uint8_t* ws = C.W->ws;
+    uint8_t* ws = C.M->ws;
     const int l = C.lane;
     const int mbw = C.a->mbw;
     const bool want = part == 2 || (part == 0 ? (l < 17 || l >= 32) : (l >= 17 && l < 32));
@@ -905,7 +916,7 @@ __device__ void build_luma_border(const Ctx& C, int part = 2)
     if (!want) {
     } else if (l < 32) {
         int v;
-        if (l == 0) v = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : C.W->left_y[0]);
+        if (l == 0) v = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : C.M->left_y[0]);
         else if (C.mby == 0) v = 127;
         else if (l <= 16) v = C.top_y[C.oy + l - 1];
         else if (C.mbx == mbw - 1) v = C.top_y[C.oy + 15];
@@ -918,7 +929,7 @@ __device__ void build_luma_border(const Ctx& C, int part = 2)
         }
     } else if (l < 48) {
         int i = l - 32;
-        ws[(i + 1) * ZW_BPS] = C.mbx == 0 ? 129 : C.W->left_y[1 + i];
+        ws[(i + 1) * ZW_BPS] = C.mbx == 0 ? 129 : C.M->left_y[1 + i];
     }
     wsync();
 }
@@ -932,7 +943,7 @@ __device__ void build_chroma_border(const Ctx& C)
         const int i = pl ? l - 17 : l;
         uint8_t* w = pl ? C.W->cv : C.W->cu;
         const uint8_t* top = pl ? C.top_v : C.top_u;
-        const uint8_t* left = pl ? C.W->left_v : C.W->left_u;
+        const uint8_t* left = pl ? C.M->left_v : C.M->left_u;
         if (i == 0) w[0] = C.mby == 0 ? 127 : (C.mbx == 0 ? 129 : left[0]);
         else if (i <= 8) w[i] = C.mby == 0 ? 127 : top[C.oc + i - 1];
         else w[(i - 8) * ZW_BPS] = C.mbx == 0 ? 129 : left[i - 8];
@@ -945,8 +956,7 @@ template <int PASS>
 __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_score)
 {
     const int lane = C.lane, m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
-    WaveLds* W = C.W;
-    const uint8_t* ws = W->ws;
+    const uint8_t* ws = C.M->ws;
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
     const int above = C.mby != 0, left = C.mbx != 0;
@@ -1054,6 +1064,7 @@ __device__ void pick_i16(const Ctx& C, int& best_mode, unsigned long long& best_
 __device__ unsigned long long zw_phase_cycles_dev[2][24];
 __device__ unsigned long long zw_wave_cycles_dev[2][16][24];  // the same per wave index
 #define PH_START() long long ph_t_ = clock64()
+#define PH_RESET() (ph_t_ = clock64())
 #define PH_MARK(k) PH_MARK_L(k, lane, PASS)
 // accumulate in the wave's LDS slot; flushed once per kernel (ph_flush)
 #define PH_MARK_L(k, ln, ps)                                                        \
@@ -1088,17 +1099,19 @@ extern "C" int zw_phase_cycles(unsigned long long* out, int reset)
 #define PH_COUNT(k) (void)0
 // ISA inspection builds: phase boundaries as assembly comments
 #define PH_START() asm volatile("; ZWMARK start" ::: "memory")
+#define PH_RESET() (void)0
 #define PH_MARK(k) asm volatile("; ZWMARK " #k ::: "memory")
 #define PH_MARK_L(k, ln, ps) asm volatile("; ZWMARK " #k ::: "memory")
 #else
 #define PH_COUNT(k) (void)0
 #define PH_START() (void)0
+#define PH_RESET() (void)0
 #define PH_MARK(k) (void)0
 #define PH_MARK_L(k, ln, ps) (void)0
 #endif
 
 // Fill the I4 value vectors V[h] for the NB sub-blocks (x0[h], y0[h]) of
-// W->ws (branch-free: every lane reads up to three edge pixels and forms an
+// C.M->ws (branch-free: every lane reads up to three edge pixels and forms an
 // avg2/avg3/copy; the lane -> (edge indices, weights) map is block invariant).
 //   V[0..12]  E = [L3 L2 L1 L0 P A0..A7]      V[13..23] avg3(E[k], E[k+1], E[k+2])
 //   V[24..35] avg2(E[k], E[k+1])              V[36] avg3(A6,A7,A7)  V[37] avg3(L2,L3,L3)
@@ -1107,7 +1120,7 @@ template <int NB>
 __device__ __forceinline__ void i4_values_n(const Ctx& C, const int* x0, const int* y0)
 {
     WaveLds* W = C.W;
-    const uint8_t* ws = W->ws;
+    const uint8_t* ws = C.M->ws;
     const int l = C.lane;
     // lane -> (ka, kb, kc) and weights; t: 0 copy, 1 avg3, 2 avg2, 3/4 special avg3
     // (arithmetic only: lane-dependent selects must not become branches)
@@ -1490,7 +1503,7 @@ struct I4Lane {
 template <int NB>
 __device__ __forceinline__ uint32_t i4_values_pk(const Ctx& C, const int* x0, const int* y0)
 {
-    const uint8_t* ws = C.W->ws;
+    const uint8_t* ws = C.M->ws;
     const int l = C.lane;
     const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
     const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
@@ -1607,7 +1620,6 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
                      I4State& st, bool keep)
 {
     PH_START();
-    WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
     const int l = C.lane, m = l & 15, hf = l >> 5;
@@ -1710,7 +1722,7 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
         st.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);
         st.running += rdscore(bsse, brate, S.l_mode);
         st.mpack |= (unsigned long long)bmode << (4 * i);
-        if (l == h) W->modes[i] = (uint8_t)bmode;
+        if (l == h) C.M->modes[i] = (uint8_t)bmode;
     }
     // the winners' quads write their rows of the reconstruction (and, when the
     // final pass reuses them, their columns of levels in zigzag order)
@@ -1718,11 +1730,11 @@ DI void i4_cand_quad(const Ctx& C, const int* sbx, const int* sby, const int* x0
     if (k == bks && l < 16 * NB) {
         const int xo = csel(slot, x0[sl], x0[0]), yo = csel(slot, y0[sl], y0[0]);
         const uint32_t wd = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
-        uint8_t* p = W->ws + (yo + q) * ZW_BPS + xo;
+        uint8_t* p = C.M->ws + (yo + q) * ZW_BPS + xo;
 #pragma unroll
         for (int j = 0; j < 4; j++) p[j] = (uint8_t)(wd >> (8 * j));
         if (keep) {
-            int16_t* lvp = W->lev[by * 4 + bx];
+            int16_t* lvp = C.M->lev[by * 4 + bx];
 #pragma unroll
             for (int r = 0; r < 4; r++) lvp[izz_of(4 * r + q)] = (int16_t)lv[r];
         }
@@ -1735,7 +1747,6 @@ template <int PASS, int NB>
 __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int* sby, int K, const I4Lane& LC,
                                         I4State& st, bool keep)
 {
-    WaveLds* W = C.W;
     const ZwSegment& S = *C.S;
     const LdsTables* T = C.T;
     const int l = C.lane, hf = l >> 5, m = l & 15;
@@ -1893,7 +1904,7 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
         st.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);  // (lane wl's mode is bmode[h])
         st.running += rdscore(bsse, brate, S.l_mode);
         st.mpack |= (unsigned long long)bmode[h] << (4 * i);
-        if (l == h) W->modes[i] = (uint8_t)bmode[h];
+        if (l == h) C.M->modes[i] = (uint8_t)bmode[h];
     }
     // the winners' two lanes write their rows of the reconstruction (and, when
     // the final pass reuses them, the levels in zigzag order)
@@ -1903,12 +1914,12 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
 #pragma unroll
         for (int r = 0; r < 2; r++) {
             const uint32_t wd = __builtin_amdgcn_perm(r32[r], r01[r], 0x04060200u);
-            uint8_t* p = W->ws + (yo + 2 * hf + r) * ZW_BPS + xo;
+            uint8_t* p = C.M->ws + (yo + 2 * hf + r) * ZW_BPS + xo;
 #pragma unroll
             for (int j = 0; j < 4; j++) p[j] = (uint8_t)(wd >> (8 * j));
         }
         if (keep) {
-            int16_t* lv = W->lev[by * 4 + bx];
+            int16_t* lv = C.M->lev[by * 4 + bx];
 #pragma unroll
             for (int c = 0; c < 2; c++)
 #pragma unroll
@@ -1922,7 +1933,7 @@ __device__ __forceinline__ void i4_step(const Ctx& C, const int* sbx, const int*
     PH_MARK_L(13, l, 0);
 }
 
-// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in W->modes.
+// pick_best_intra4 (vp8.rs:1790-2040).  Returns true when I4 wins; modes in C.M->modes.
 // Each block's choice depends only on its left / top / top-right neighbours,
 // which every earlier anti-diagonal holds, so every choice equals the
 // raster-order one.  The reference's early exits (running score >= the I16
@@ -1961,8 +1972,320 @@ __device__ bool pick_i4(const Ctx& C, unsigned long long i16_score, bool keep, u
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Paired I4 search: one wave searches the MBs of two rows at once.  The paired
+// kernels give a wave two MB rows, y and y + 1, the second two columns behind
+// (the x + 2y wavefront's lag), so MB A = (x, y) and MB B = (x - 2, y + 1) reach
+// their I4 searches together; both visit the same anti-diagonal steps.  Lanes
+// 0..31 work A and lanes 32..63 work B (hm = lane >> 5): the candidate phase
+// keeps the quad form (lane = 32 hm + 16 slot + 4 k + q), the ranking works
+// all four rows of a (slot, mode) in one lane (lane = 32 hm + 16 slot + mode).
+// The value vectors of the four (MB, slot) blocks are packed one byte each
+// (byte 2 hm + slot) in lanes 0..38.  Every per-MB decision (winners, early
+// exits, running scores) is the single search's, per MB: a search that ends
+// early leaves its lanes computing on, with their stores masked.
+// ---------------------------------------------------------------------------
+struct I4PLane {
+    uint32_t ix[4];  // bperm byte addresses (4 x V index) of the lane's pixels in rows 0..3, one per byte
+    uint32_t psel;   // v_perm selector taking the lane's (MB, slot) byte of two gathered words
+    int tm;          // mode is TrueMotion
+};
+
+DI uint32_t i4p_psel(int hm, int slot)
+{
+    const uint32_t b = (uint32_t)(2 * hm + slot);
+    return 0x0c000c00u | ((4u + b) << 16) | b;
+}
+
+DI void i4p_lane_init(const Ctx& C, I4PLane& L)
+{
+    const int l = C.lane, m = l & 15, mv = m < 10 ? m : 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) w |= (uint32_t)(4 * (i4_src_index(C.T, mv, 4 * r + j) & 255)) << (8 * j);
+        L.ix[r] = w;
+    }
+    L.psel = i4p_psel(l >> 5, (l >> 4) & 1);
+    L.tm = mv == 1;
+}
+
+// Value vectors (see i4_values_pk) of both MBs' step blocks: lane v < 39 holds
+// V[v] of (A slot 0, A slot 1, B slot 0, B slot 1) in bytes 0..3.
+template <int NB>
+DI uint32_t i4p_values(const Ctx& CA, const Ctx& CB, const int* x0, const int* y0)
+{
+    const int l = CA.lane;
+    const int t = (int)(l >= 13) + (int)(l >= 24) + (int)(l >= 36) + (int)(l >= 37);
+    const int k = min(l - 13 * (int)(l >= 13) - 11 * (int)(l >= 24), 12);
+    const int t3 = (int)(t == 3), t4 = (int)(t >= 4), t12 = (int)(t == 1 || t == 2);
+    const int ka = k + t3 * (11 - k) + t4 * (1 - k);
+    const int kb = k + t12 + t3 * (12 - k) - t4 * k;
+    const int kc = min(k + 2 * (int)(t == 1), 12);
+    const int wb = 2 * (int)(t == 1) + (int)(t == 2) + 3 * (t3 + t4);
+    const int wc = (int)(t == 1);
+    const int sh = (int)(t != 0) + (int)(t != 0 && t != 2);
+    const int oa = csel(ka < 4, -ka * ZW_BPS, ka - 4 - 4 * ZW_BPS);
+    const int ob = csel(kb < 4, -kb * ZW_BPS, kb - 4 - 4 * ZW_BPS);
+    const int oc = csel(kc < 4, -kc * ZW_BPS, kc - 4 - 4 * ZW_BPS);
+    const bool dcl = l < 4 || (l >= 5 && l < 9);
+    uint32_t v[2], ea[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; mb++) {
+        const uint8_t* ws = (mb ? CB : CA).M->ws;
+        v[mb] = ea[mb] = 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int hh = NB == 2 ? h : 0;
+            const int rowL = (y0[hh] + 3) * ZW_BPS + x0[hh] - 1;
+            const int a = ws[rowL + oa], eb = ws[rowL + ob], ec = ws[rowL + oc];
+            v[mb] |= (uint32_t)((a + wb * eb + wc * ec + ((1 << sh) >> 1)) >> sh) << (16 * h);
+            ea[mb] |= (uint32_t)a << (16 * h);
+        }
+    }
+    // the DCs of the four blocks (sums < 2^16 per slot)
+    const uint32_t da = (uint32_t)__builtin_amdgcn_readfirstlane(red16((int)(dcl ? ea[0] : 0u)));
+    const uint32_t db = (uint32_t)__builtin_amdgcn_readfirstlane(red16((int)(dcl ? ea[1] : 0u)));
+    const uint32_t dcv = (((da & 0xffffu) + 4) >> 3) | ((((da >> 16) + 4) >> 3) << 8) |
+                         ((((db & 0xffffu) + 4) >> 3) << 16) | ((((db >> 16) + 4) >> 3) << 24);
+    return l == 38 ? dcv : __builtin_amdgcn_perm(v[1], v[0], 0x06040200u);
+}
+
+template <int PASS, int NB>
+DI void i4p_step(const Ctx& CA, const Ctx& CB, const int* sbx, const int* sby, int K, const I4PLane& LC,
+                 I4State st[2], const bool act[2], bool keep)
+{
+    [[maybe_unused]] const Ctx& C = CA;  // (the phase counters)
+    const int l = CA.lane, m = l & 15, hm = l >> 5;
+    const int slot = NB == 2 ? (l >> 4) & 1 : 0;
+    const int sl = NB == 2 ? 1 : 0;
+    // per (MB, slot) contexts, wave-uniform, then the lane's
+    int x0[NB], y0[NB], tc[2][NB], lc[2][NB], nc[2][NB];
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int i = sby[h] * 4 + sbx[h];
+        x0[h] = sbx[h] * 4 + 1;
+        y0[h] = sby[h] * 4 + 1;
+#pragma unroll
+        for (int mb = 0; mb < 2; mb++) {
+            tc[mb][h] = sby[h] == 0 ? 0 : (int)((st[mb].mpack >> (4 * (i - 4))) & 15);
+            lc[mb][h] = sbx[h] == 0 ? 0 : (int)((st[mb].mpack >> (4 * (i - 1))) & 15);
+            nc[mb][h] = (sby[h] == 0 ? 0 : (int)((st[mb].tnz >> sbx[h]) & 1)) +
+                        (sbx[h] == 0 ? 0 : (int)((st[mb].lnz >> sby[h]) & 1));
+        }
+    }
+    auto pick = [&](const int (&v)[2][NB]) {
+        const int a = csel(slot, v[0][sl], v[0][0]), b = csel(slot, v[1][sl], v[1][0]);
+        return csel(hm, b, a);
+    };
+    const int tctx = pick(tc), lctx = pick(lc), ctx0 = pick(nc);
+    const int bx = csel(slot, sbx[sl], sbx[0]), by = csel(slot, sby[sl], sby[0]);
+    const uint8_t* sYh = hm ? CB.sY : CA.sY;
+    const ZwSegment* Sh = hm ? CB.S : CA.S;
+    const LdsTables* Th = hm ? CB.T : CA.T;  // the lane's frame's tables (costs, probabilities)
+    PH_START();
+    const uint32_t vp = i4p_values<NB>(CA, CB, x0, y0);
+    // TrueMotion offsets V[5 + j] - V[4] of the lane's (MB, slot), as (x0, x1), (x3, x2) pairs
+    uint32_t ap01, ap32;
+    {
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)vp, 4);
+        uint32_t a[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) a[j] = (uint32_t)__builtin_amdgcn_readlane((int)vp, 5 + j);
+        const int sh = 8 * (2 * hm + slot);
+        const int p_ = (int)((P >> sh) & 255u);
+        const int d0 = (int)((a[0] >> sh) & 255u) - p_, d1 = (int)((a[1] >> sh) & 255u) - p_;
+        const int d2 = (int)((a[2] >> sh) & 255u) - p_, d3 = (int)((a[3] >> sh) & 255u) - p_;
+        ap01 = pack_lo(d0, d1);
+        ap32 = pack_lo(d3, d2);
+    }
+    PH_MARK_L(10, l, 0);
+    // ranking: the four rows of (MB, slot, mode) in one lane
+    int pse = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t ix = LC.ix[r];
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ix & 255u), (int)vp);
+        const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ix >> 8) & 255u), (int)vp);
+        const uint32_t v2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ix >> 16) & 255u), (int)vp);
+        const uint32_t v3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ix >> 24), (int)vp);
+        const uint32_t q01 = __builtin_amdgcn_perm(v1, v0, LC.psel), q32 = __builtin_amdgcn_perm(v2, v3, LC.psel);
+        const uint32_t p01 = LC.tm ? clamp_pk(add_pk(q01, ap01)) : q01;
+        const uint32_t p32 = LC.tm ? clamp_pk(add_pk(q32, ap32)) : q32;
+        const uint32_t sw = *(const uint32_t*)(sYh + (by * 4 + r) * 16 + bx * 4);
+        const uint32_t d01 = sub_pk(__builtin_amdgcn_perm(0u, sw, 0x0c010c00u), p01);
+        const uint32_t d32 = sub_pk(__builtin_amdgcn_perm(0u, sw, 0x0c020c03u), p32);
+        pse = dot2v(d01, d01, pse);
+        pse = dot2v(d32, d32, pse);
+    }
+    const int key = m < 10 ? (pse << 4) | m : 0x7fffffff;
+    int rank = 0, scratch_;
+#define ZW_RANK_STEP(R) "v_sub_co_u32_dpp %1, vcc, %2, %2 row_ror:" #R " row_mask:0xf bank_mask:0xf\n" \
+                        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+    asm volatile("s_nop 1\n" ZW_RANK_STEP(1) ZW_RANK_STEP(2) ZW_RANK_STEP(3) ZW_RANK_STEP(4) ZW_RANK_STEP(5)
+                     ZW_RANK_STEP(6) ZW_RANK_STEP(7) ZW_RANK_STEP(8) ZW_RANK_STEP(9) ZW_RANK_STEP(10)
+                         ZW_RANK_STEP(11) ZW_RANK_STEP(12) ZW_RANK_STEP(13) ZW_RANK_STEP(14) ZW_RANK_STEP(15)
+                 : "+v"(rank), "=&v"(scratch_)
+                 : "v"(key)
+                 : "vcc");
+#undef ZW_RANK_STEP
+    PH_MARK_L(11, l, 0);
+    // candidate modes: k-th of each (MB, slot) group, four bits each, group g at bit 16 g
+    unsigned long long modes = 0;
+    for (int k = 0; k < K; k++) {
+        const unsigned long long b = __ballot(m < 10 && rank == k);
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+            modes |= (unsigned long long)__builtin_ctz((uint32_t)(b >> (16 * g)) | 0x10000u) << (16 * g + 4 * k);
+    }
+    const int k = (l >> 2) & 3, q = l & 3;
+    const int g = 2 * hm + slot;
+    const int mq = (int)((modes >> (16 * g + 4 * k)) & 15ull);
+    const int mv = k < K ? mq : 0;  // (k >= K: a valid mode, never eligible)
+    const int mcost = Th->fci4[tctx][lctx][mv];
+    const uint32_t iq0 = q ? Sh->y1.iq[1] : Sh->y1.iq[0], bs0 = q ? Sh->y1.bias[1] : Sh->y1.bias[0];
+    const uint32_t iq1 = Sh->y1.iq[1], bs1 = Sh->y1.bias[1];
+    const int q0 = q ? (int)Sh->y1.q[1] : (int)Sh->y1.q[0], qa = (int)Sh->y1.q[1];
+    int hn[2];
+    hn[0] = (int)Th->binit[3][0][ctx0] & -(int)(ctx0 == 0);
+    hn[1] = (int)Th->beob[3][0][ctx0];
+    uint32_t p01, p32;
+    {
+        const uint32_t iw = *(const uint32_t*)&Th->i4qa[mv][4 * q];
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            v[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((iw >> (8 * j)) & 255u), (int)vp);
+        const uint32_t q01 = __builtin_amdgcn_perm(v[1], v[0], LC.psel), q32 = __builtin_amdgcn_perm(v[2], v[3], LC.psel);
+        const bool tm = mv == 1;
+        p01 = tm ? clamp_pk(add_pk(q01, ap01)) : q01;
+        p32 = tm ? clamp_pk(add_pk(q32, ap32)) : q32;
+    }
+    uint32_t s01, s32;
+    {
+        const uint32_t sw = *(const uint32_t*)(sYh + (by * 4 + q) * 16 + bx * 4);
+        s01 = __builtin_amdgcn_perm(0u, sw, 0x0c010c00u);
+        s32 = __builtin_amdgcn_perm(0u, sw, 0x0c020c03u);
+    }
+    PH_MARK_L(22, l, 0);
+    const uint32_t R01 = sub_pk(s01, p01), R32 = sub_pk(s32, p32);
+    int cf[4];
+    uvq_fdct(add_pk(R01, R32), sub_pk(R01, R32), q, cf);
+    int av[4], dq[4], lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool dcs = r == 0;  // (0, q): the DC for q = 0
+        const int v = cf[r];
+        const int a = (int)((__umul24((uint32_t)iabs(v), dcs ? iq0 : iq1) + (dcs ? bs0 : bs1)) >> 17);
+        av[r] = a;
+        lv[r] = v < 0 ? -a : a;
+        dq[r] = m24(lv[r], dcs ? q0 : qa);
+    }
+    int last;
+    const int cost = rcost_quad<PASS == 2>(av, q, ctx0, 3, Th, last, hn);
+    PH_MARK_L(23, l, 0);
+    uint32_t r01, r32;
+    uvq_idct_recon(dq, p01, p32, q, r01, r32);
+    int sse = 0;
+    {
+        const uint32_t d01 = sub_pk(s01, r01), d32 = sub_pk(s32, r32);
+        sse = dot2v(d01, d01, sse);
+        sse = dot2v(d32, d32, sse);
+    }
+    sse = quad_sum(sse);
+    const uint32_t rate = (uint32_t)(mcost + cost);
+    const uint32_t score = (uint32_t)sse * 256u + (rate & 0xffffu) * Sh->l_i4;
+    const uint32_t key2 = k < K ? (score << 2) | (uint32_t)k : 0xffffffffu;
+    const uint32_t kmin = min16u(key2);
+    const unsigned long long win = __ballot(key2 == kmin);
+    PH_MARK_L(12, l, 0);
+#pragma unroll
+    for (int mb = 0; mb < 2; mb++) {
+        const ZwSegment& S = *(mb ? CB : CA).S;
+        MbLds* M = (mb ? CB : CA).M;
+#pragma unroll
+        for (int h = 0; h < NB; h++) {
+            const int gg = 2 * mb + h;
+            const int bk = __builtin_ctz((uint32_t)(win >> (16 * gg)) & 0xffffu) >> 2;
+            const int bmode = (int)((modes >> (16 * gg + 4 * bk)) & 15ull);
+            const int wl = 16 * gg + 4 * bk;
+            const uint32_t bsse = (uint32_t)__builtin_amdgcn_readlane(sse, wl);
+            const uint32_t brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, wl);
+            const int bnz = __builtin_amdgcn_readlane((int)(last >= 0), wl);
+            const int i = sby[h] * 4 + sbx[h];
+            I4State& s = st[mb];
+            s.tnz = (s.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
+            s.lnz = (s.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
+            s.nzm |= (uint32_t)bnz << i;
+            s.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);
+            s.running += rdscore(bsse, brate, S.l_mode);
+            s.mpack |= (unsigned long long)bmode << (4 * i);
+            if (act[mb] && l == gg) M->modes[i] = (uint8_t)bmode;
+        }
+    }
+    // the winners' quads write their rows of the reconstruction (and levels)
+    const int bks = __builtin_ctz((uint32_t)(win >> (16 * g)) & 0xffffu) >> 2;
+    if (k == bks && ((l >> 4) & 1) < NB && (hm ? act[1] : act[0])) {
+        MbLds* M = hm ? CB.M : CA.M;
+        const int xo = csel(slot, x0[sl], x0[0]), yo = csel(slot, y0[sl], y0[0]);
+        const uint32_t wd = __builtin_amdgcn_perm(r32, r01, 0x04060200u);
+        uint8_t* p = M->ws + (yo + q) * ZW_BPS + xo;
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[j] = (uint8_t)(wd >> (8 * j));
+        if (keep) {
+            int16_t* lvp = M->lev[by * 4 + bx];
+#pragma unroll
+            for (int r = 0; r < 4; r++) lvp[izz_of(4 * r + q)] = (int16_t)lv[r];
+        }
+    }
+    wsync();
+    PH_MARK_L(13, l, 0);
+}
+
+// pick_best_intra4 (vp8.rs:1790-2040) of two MBs at once (K <= 4): bit mb of
+// the result is set when I4 wins MB mb (A, B); each MB's early exits are the
+// single search's (pick_i4).  An MB with act* false is not searched (its
+// lanes compute on its work buffer with every store masked).
+template <int PASS>
+__device__ uint32_t pick_i4_pair(const Ctx& CA, const Ctx& CB, unsigned long long i16A, unsigned long long i16B,
+                                 bool actA, bool actB, bool keep, uint32_t& nzA, uint32_t& nzB)
+{
+    const int K = CA.method <= 3 ? 3 : 4;
+    I4State st[2];
+    st[0].running = 211ull * CA.S->l_mode;
+    st[1].running = 211ull * CB.S->l_mode;
+#pragma unroll
+    for (int mb = 0; mb < 2; mb++) {
+        st[mb].total_mc = 0;
+        st[mb].mpack = 0;
+        st[mb].tnz = st[mb].lnz = st[mb].nzm = 0;
+    }
+    bool act[2] = {actA, actB};  // (an MB without a search: its lanes run masked)
+    const unsigned long long lim[2] = {i16A, i16B};
+    I4PLane LC;
+    i4p_lane_init(CA, LC);
+    for (int s = 0; s < 10; s++) {
+        const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
+        const int sbxA = s - 2 * sbyA;
+        if (s >= 2 && s <= 7) {
+            const int bx[2] = {sbxA, sbxA - 2}, by[2] = {sbyA, sbyA + 1};
+            i4p_step<PASS, 2>(CA, CB, bx, by, K, LC, st, act, keep);
+        } else {
+            i4p_step<PASS, 1>(CA, CB, &sbxA, &sbyA, K, LC, st, act, keep);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; mb++)
+            if (st[mb].running >= lim[mb] || st[mb].total_mc > 256u * 16u * 16u / 4u) act[mb] = false;
+        if (!act[0] && !act[1]) return 0;
+    }
+    nzA = st[0].nzm;
+    nzB = st[1].nzm;
+    return (uint32_t)act[0] | ((uint32_t)act[1] << 1);
+}
+
 // Final luma transform (transform_luma_block vp8.rs:2647 / _4x4 :2785).
-// Writes zigzag levels to W->lev[0..16], recon into W->ws.  Returns the
+// Writes zigzag levels to C.M->lev[0..16], recon into C.M->ws.  Returns the
 // simple-quant "any nonzero" flag for skip detection (check_all_coeffs_zero).
 __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], int i4_nzm)
 {
@@ -1974,10 +2297,10 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
     if (mode == 4 && i4_nzm >= 0) {
         // simple quantisation: the search's winners are the final blocks (same
         // prediction, transform and quantize_coeff); their levels are in
-        // W->lev, their reconstruction in W->ws
+        // C.M->lev, their reconstruction in C.M->ws
 #pragma unroll
         for (int i = 0; i < 16; i++) y_nz_out[i] = (i4_nzm >> i) & 1;
-        if (l < 16) W->lev[16][l] = 0;
+        if (l < 16) C.M->lev[16][l] = 0;
         wsync();
         PH_MARK_L(15, l, 0);
         PH_COUNT(7);
@@ -1985,7 +2308,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
     }
     if (mode != 4) {
         build_luma_border(C);
-        const uint8_t* ws = W->ws;
+        const uint8_t* ws = C.M->ws;
         const int above = C.mby != 0, left = C.mbx != 0;
         const int b = l & 15, bx = b & 3, by = b >> 2;
         int dcv;
@@ -2026,7 +2349,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             const int d = wht_g(c[0], b);
             const int t = b > 0;
             const int y2q = quantz(d, S.y2.iq[t], S.y2.bias[t]);
-            if (l < 16) W->lev[16][izz_of(b)] = (int16_t)y2q;
+            if (l < 16) C.M->lev[16][izz_of(b)] = (int16_t)y2q;
             if (gmask(y2q != 0)) anynz = 1;
             y2dq = iwht_g(m24(y2q, (int)S.y2.q[t]), b);
         }
@@ -2058,7 +2381,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 nt[q] = __builtin_amdgcn_readfirstlane(C.top_c[C.ocx + 1 + q]);
-                nl[q] = __builtin_amdgcn_readfirstlane(W->left_c[1 + q]);
+                nl[q] = __builtin_amdgcn_readfirstlane(C.M->left_c[1 + q]);
             }
             unsigned code = 0, nzbits = 0;
 #pragma unroll
@@ -2100,10 +2423,10 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
         if (l < 16) {
             lv[0] = 0;
 #pragma unroll
-            for (int n = 0; n < 16; n++) W->lev[b][n] = (int16_t)lv[n];
+            for (int n = 0; n < 16; n++) C.M->lev[b][n] = (int16_t)lv[n];
             dq[0] = y2dq;
             idct16(dq);
-            uint8_t* wsp = W->ws;
+            uint8_t* wsp = C.M->ws;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const int y = by * 4 + (k >> 2), x = bx * 4 + (k & 3);
@@ -2119,11 +2442,11 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
         int top_nz[4], left_nz[4];
         for (int k = 0; k < 4; k++) {
             top_nz[k] = C.top_c[C.ocx + 1 + k];
-            left_nz[k] = W->left_c[1 + k];
+            left_nz[k] = C.M->left_c[1 + k];
         }
         for (int i = 0; i < 16; i++) {
             const int sby = i >> 2, sbx = i & 3, x0 = sbx * 4 + 1, y0 = sby * 4 + 1;
-            const int bm = W->modes[i];
+            const int bm = C.M->modes[i];
             i4_values(C, x0, y0);
             // 16-lane group form: every group computes the same block; group 0 stores
             const int k = l & 15;
@@ -2148,15 +2471,15 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
                 const int cn = gget(ck, zz_of(k));
                 int lvn;
                 nzq = trellis_g<0>(cn, k, S.y1, S.sharpen, S.lt_i4, C.T, 3, ctx0, lvn);
-                if (l < 16) W->lev[i][k] = (int16_t)lvn;
+                if (l < 16) C.M->lev[i][k] = (int16_t)lvn;
                 dqk = m24(gget(lvn, izz_of(k)), (int)S.y1.q[k > 0]);
             } else {
-                if (l < 16) W->lev[i][izz_of(k)] = (int16_t)qs;
+                if (l < 16) C.M->lev[i][izz_of(k)] = (int16_t)qs;
                 nzq = snz;
                 dqk = m24(qs, (int)S.y1.q[k > 0]);
             }
             const int rk = idct_g(dqk, k);
-            if (l < 16) W->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pk + rk);
+            if (l < 16) C.M->ws[(y0 + (k >> 2)) * ZW_BPS + x0 + (k & 3)] = (uint8_t)clamp255(pk + rk);
             wsync();
             if (l == 0) {
                 W->misc[1] = nzq;
@@ -2170,7 +2493,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
             y_nz_out[i] = nz;
             wsync();
         }
-        if (l < 16) W->lev[16][l] = 0;
+        if (l < 16) C.M->lev[16][l] = 0;
         wsync();
         PH_MARK_L(15, l, 0);
         PH_COUNT(7);
@@ -2181,7 +2504,7 @@ __device__ int final_luma(const Ctx& C, int mode, bool trel, int y_nz_out[16], i
 // Final chroma transform with error diffusion (transform_chroma_blocks
 // vp8.rs:3039, apply_chroma_error_diffusion :572), lane-pair form: lanes b and
 // 32 + b work block b (U 0..3, V 4..7) from the coefficients pick_uv left for
-// the chosen mode.  Levels to W->lev[17..24], recon into cu / cv.  Returns the
+// the chosen mode.  Levels to C.M->lev[17..24], recon into cu / cv.  Returns the
 // simple-quant "any nonzero" flag; uv_nz[8] receives per-block has-coefficients.
 __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[8])
 {
@@ -2228,7 +2551,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
 #pragma unroll
         for (int ch = 0; ch < 2; ch++) {
             int8_t* top = top_derr + ch * 2;
-            int8_t* lft = W->left_derr + ch * 2;
+            int8_t* lft = C.M->left_derr + ch * 2;
             const int t0 = __builtin_amdgcn_readfirstlane((int)top[0]), t1 = __builtin_amdgcn_readfirstlane((int)top[1]);
             const int l0 = __builtin_amdgcn_readfirstlane((int)lft[0]), l1 = __builtin_amdgcn_readfirstlane((int)lft[1]);
             int* d = dcs + ch * 4;
@@ -2262,7 +2585,7 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
             const int q_ = dcs ? (int)(h ? S.uv.q[1] : S.uv.q[0]) : (int)S.uv.q[1];
             const int lv = quantz(cf[c][r], iq, bias);
             nz |= lv;
-            if (act) W->lev[17 + b][izz_of(4 * r + 2 * h + c)] = (int16_t)lv;
+            if (act) C.M->lev[17 + b][izz_of(4 * r + 2 * h + c)] = (int16_t)lv;
             dq[c][r] = m24(lv, q_);
         }
     uint32_t r01[2], r32[2];
@@ -2293,12 +2616,11 @@ __device__ int final_chroma(const Ctx& C, int mode, int8_t* top_derr, int uv_nz[
 __device__ void store_luma_borders(const Ctx& C)
 {
     const int l = C.lane;
-    WaveLds* W = C.W;
-    if (l < 17) W->left_y[l] = W->ws[l * ZW_BPS + 16];
-    else if (l < 33) C.top_y[C.oy + (l - 17)] = W->ws[16 * ZW_BPS + (l - 17) + 1];
+    if (l < 17) C.M->left_y[l] = C.M->ws[l * ZW_BPS + 16];
+    else if (l < 33) C.top_y[C.oy + (l - 17)] = C.M->ws[16 * ZW_BPS + (l - 17) + 1];
     if (C.a->ry && l < 64) {
         uint8_t* ry = C.a->ry + (size_t)C.f * C.a->ysz + (size_t)C.mby * 16 * C.ys + C.mbx * 16;
-        for (int k = l; k < 256; k += 64) ry[(size_t)(k >> 4) * C.ys + (k & 15)] = W->ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
+        for (int k = l; k < 256; k += 64) ry[(size_t)(k >> 4) * C.ys + (k & 15)] = C.M->ws[((k >> 4) + 1) * ZW_BPS + 1 + (k & 15)];
     }
     wsync();
 }
@@ -2307,8 +2629,8 @@ __device__ void store_chroma_borders(const Ctx& C)
     const int l = C.lane;
     WaveLds* W = C.W;
     if (l < 9) {
-        W->left_u[l] = W->cu[l * ZW_BPS + 8];
-        W->left_v[l] = W->cv[l * ZW_BPS + 8];
+        C.M->left_u[l] = W->cu[l * ZW_BPS + 8];
+        C.M->left_v[l] = W->cv[l * ZW_BPS + 8];
     } else if (l < 17) {
         C.top_u[C.oc + (l - 9)] = W->cu[8 * ZW_BPS + (l - 9) + 1];
         C.top_v[C.oc + (l - 9)] = W->cv[8 * ZW_BPS + (l - 9) + 1];
@@ -2328,7 +2650,7 @@ __device__ void write_levels(const Ctx& C, int first_blk, int nblk, bool zero)
     ZwMbOut* o = C.a->out + (size_t)C.f * C.a->mbw * C.a->mbh + (size_t)C.mby * C.a->mbw + C.mbx;
     // as words (ZwMbOut records and the LDS levels are 4-byte aligned)
     uint32_t* dst = (uint32_t*)&o->levels[first_blk][0];
-    const uint32_t* srcl = (const uint32_t*)&C.W->lev[first_blk][0];
+    const uint32_t* srcl = (const uint32_t*)&C.M->lev[first_blk][0];
     for (int k = C.lane; k < nblk * 8; k += 64) dst[k] = zero ? 0u : srcl[k];
 }
 
@@ -2500,7 +2822,7 @@ DI int uvq_pick(const Ctx& C, const UvQ& U, int* xch, int* xflag, int seq)
 
 // transform_chroma_blocks (vp8.rs:3039-3121) of one plane under mode cm:
 // the DC error diffusion of channel U.pl (vp8.rs:572-647), quantisation,
-// levels into W->lev[17 + 4 pl + b], reconstruction into the work buffer.
+// levels into C.M->lev[17 + 4 pl + b], reconstruction into the work buffer.
 DI void uvq_final(const Ctx& C, const UvQ& U, int cm, int8_t* top_derr)
 {
     WaveLds* W = C.W;
@@ -2536,7 +2858,7 @@ DI void uvq_final(const Ctx& C, const UvQ& U, int cm, int8_t* top_derr)
             return (int)(int8_t)(v < -127 ? -127 : (v > 127 ? 127 : v));
         };
         int8_t* top = top_derr + U.pl * 2;
-        int8_t* lft = W->left_derr;
+        int8_t* lft = C.M->left_derr;
         const int t0 = __builtin_amdgcn_readfirstlane((int)top[0]), t1 = __builtin_amdgcn_readfirstlane((int)top[1]);
         const int l0 = __builtin_amdgcn_readfirstlane((int)lft[0]), l1 = __builtin_amdgcn_readfirstlane((int)lft[1]);
         const int e0 = diffuse(d[0], t0, l0);
@@ -2562,7 +2884,7 @@ DI void uvq_final(const Ctx& C, const UvQ& U, int cm, int8_t* top_derr)
     for (int r = 0; r < 4; r++) {
         const bool dcs = r == 0 && q == 0;
         const int lv = quantz(cf[r], dcs ? S.uv.iq[0] : S.uv.iq[1], dcs ? S.uv.bias[0] : S.uv.bias[1]);
-        if (act) W->lev[17 + 4 * U.pl + b][izz_of(4 * r + q)] = (int16_t)lv;
+        if (act) C.M->lev[17 + 4 * U.pl + b][izz_of(4 * r + q)] = (int16_t)lv;
         dq[r] = m24(lv, dcs ? (int)S.uv.q[0] : (int)S.uv.q[1]);
     }
     uint32_t r01, r32;
@@ -2630,11 +2952,11 @@ __device__ void setup_ctx(Ctx& C, const EncArgs* a, const uint8_t* seg_lut, Wave
     // stage the source MB in LDS: 64 lanes x 4 B luma, 32 lanes x 4 B chroma
     {
         const int l = C.lane;
-        ((uint32_t*)W->sy)[l] = m.y;
-        if (l < 32) ((uint32_t*)((l >> 4) ? W->sv : W->su))[l & 15] = m.c;
-        C.sY = W->sy;
-        C.sU = W->su;
-        C.sV = W->sv;
+        ((uint32_t*)C.M->sy)[l] = m.y;
+        if (l < 32) ((uint32_t*)((l >> 4) ? C.M->sv : C.M->su))[l & 15] = m.c;
+        C.sY = C.M->sy;
+        C.sU = C.M->su;
+        C.sV = C.M->sv;
     }
     wsync();
     // wave-uniform: the segment's matrices / lambdas / sharpening come from LDS;
@@ -2756,6 +3078,16 @@ DI void row_publish(int* prog, int val)
 template <bool ROWS> struct ChainShape {
     static constexpr int NCH = (ROWS ? ZW_UVQ_CHAIN_ROWS : ZW_UVQ_CHAIN_BATCH) ? 2 : 1;
 };
+// the per-MB stage loops of the frame-pair kernel: ZW_PAIR_UNROLL 1 emits
+// each stage twice (constant frame index), 0 once (a two-trip loop)
+#ifndef ZW_PAIR_UNROLL
+#define ZW_PAIR_UNROLL 0
+#endif
+#if ZW_PAIR_UNROLL
+#define ZW_PAIR_LOOP _Pragma("unroll")
+#else
+#define ZW_PAIR_LOOP _Pragma("nounroll")
+#endif
 template <int PASS> struct RowsShape {
     static constexpr int NW = PASS == 1 ? ChainShape<true>::NCH : 1;
 };
@@ -2778,26 +3110,33 @@ struct TopLds {
     }
 };
 
-template <int PASS, bool ROWS>
+template <int PASS, bool ROWS, int FP = 1>
 __device__ __forceinline__ void encode_body(const EncArgs& a)
 {
     constexpr int NW = ROWS ? RowsShape<PASS>::NW : PassShape<PASS>::NW, WG = NW * 64;
     constexpr int NCH = PASS == 1 ? ChainShape<ROWS>::NCH : 0;  // chain waves (pass 1)
+    constexpr bool PAIR = FP == 2;  // frame pairs: the workgroup encodes frames f and f + 1
+    static_assert(FP == 1 || (FP == 2 && PASS == 2 && !ROWS), "frame pairs: the batch pass-2 kernel");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int f = ROWS ? blockIdx.y : blockIdx.x;
+    const int f = ROWS ? blockIdx.y : blockIdx.x * FP;
+    const int nf = PAIR ? min(2, a.nframes - f) : 1;  // frames of this workgroup
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int mbw = a.mbw, mbh = a.mbh;
     const ZwFrameParams* P = a.params + f;
     // carve LDS
     size_t off = 0;
+    // (per frame of the workgroup: the tables, segments, alpha map and the top rows)
+    constexpr size_t sT = (sizeof(LdsTables) + 15) & ~(size_t)15, sS = (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
     LdsTables* T = (LdsTables*)(smem + off);
-    off += (sizeof(LdsTables) + 15) & ~(size_t)15;
+    off += sT * FP;
     ZwSegment* Sl = (ZwSegment*)(smem + off);  // the frame's 4 segments (matrices, lambdas, sharpening)
-    off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
+    off += sS * FP;
     uint8_t* seg_lut = smem + off;  // alpha -> segment (zeros when segmentation is off)
-    off += 256;
+    off += 256 * FP;
     WaveLds* Wall = (WaveLds*)(smem + off);
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * NW;
+    MbLds* Mall2 = (MbLds*)(smem + off);  // frame pairs: the second frame's per-MB state
+    off += PAIR ? ((sizeof(MbLds) + 15) & ~(size_t)15) * NW : 0;
     int* progress = (int*)(smem + off);
     off += 64;
     int* xch = (int*)(smem + off);  // two-wave chroma chain: [plane][2][12] exchange words, then 2 flags
@@ -2805,13 +3144,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     off += 256;
     const TopLds TS(mbw, ROWS, PASS);
     uint8_t* top_y = smem + off;
-    off += TS.y;
+    off += TS.y * FP;
     uint8_t* top_u = smem + off;
-    off += TS.u;
+    off += TS.u * FP;
     uint8_t* top_v = smem + off;
-    off += TS.v;
+    off += TS.v * FP;
     uint8_t* top_c = smem + off;  // [mbw][12]: y2, y[4], u[2], v[2]
-    off += TS.c;
+    off += TS.c * FP;
     int8_t* top_derr = (int8_t*)(smem + off);  // [mbw][4]
     WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
     // row-parallel: is this workgroup pass 1's chroma chain (it keeps the
@@ -2822,29 +3161,43 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     int* rerr = ROWS ? (int*)a.rows : nullptr;
     int* rsync = (int*)rb;
 
-    // init shared state
-    for (int i = threadIdx.x; i < (int)(sizeof(T->lc) / 2); i += WG)
-        (&T->lc[0][0][0][0])[i] = a.lcost ? (&a.lcost[f].lc[0][0][0][0])[i] : 0;
-    for (int i = threadIdx.x; i < 96; i += WG) {
-        (&T->eob[0][0][0])[i] = a.lcost ? (&a.lcost[f].eob[0][0][0])[i] : 0;
-        (&T->init[0][0][0])[i] = a.lcost ? (&a.lcost[f].init[0][0][0])[i] : 0;
-    }
-    for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&T->probs[0][0][0][0])[i] = (&P->probs[0][0][0][0])[i];
-    static_assert(sizeof(ZwSegment) % 4 == 0, "segment copy by dwords");
-    for (int i = threadIdx.x; i < (int)(4 * sizeof(ZwSegment) / 4); i += WG)
-        ((uint32_t*)Sl)[i] = ((const uint32_t*)P->seg)[i];
-    for (int i = threadIdx.x; i < 256; i += WG) seg_lut[i] = P->seg_enabled ? P->seg_map_lut[i] : 0;
-    load_static_tables(T, threadIdx.x, WG, &P->probs[0][0][0][0]);
-    if (!ROWS || chain_wg) {
-        if (!ROWS) {
-            for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) top_y[i] = 127;
-            for (int i = threadIdx.x; i < mbw * 12; i += WG) top_c[i] = 0;
+    // init shared state (each frame of the workgroup)
+#pragma unroll
+    for (int fr = 0; fr < FP; fr++) {
+        if (fr >= nf) break;
+        const int ff = f + fr;
+        const ZwFrameParams* Pf = a.params + ff;
+        LdsTables* Tf = (LdsTables*)((uint8_t*)T + sT * fr);
+        ZwSegment* Sf = (ZwSegment*)((uint8_t*)Sl + sS * fr);
+        uint8_t* lut = seg_lut + 256 * fr;
+        for (int i = threadIdx.x; i < (int)(sizeof(Tf->lc) / 2); i += WG)
+            (&Tf->lc[0][0][0][0])[i] = a.lcost ? (&a.lcost[ff].lc[0][0][0][0])[i] : 0;
+        for (int i = threadIdx.x; i < 96; i += WG) {
+            (&Tf->eob[0][0][0])[i] = a.lcost ? (&a.lcost[ff].eob[0][0][0])[i] : 0;
+            (&Tf->init[0][0][0])[i] = a.lcost ? (&a.lcost[ff].init[0][0][0])[i] : 0;
         }
-        for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
-            top_u[i] = 127;
-            top_v[i] = 127;
+        for (int i = threadIdx.x; i < 4 * 8 * 3 * 11; i += WG) (&Tf->probs[0][0][0][0])[i] = (&Pf->probs[0][0][0][0])[i];
+        static_assert(sizeof(ZwSegment) % 4 == 0, "segment copy by dwords");
+        for (int i = threadIdx.x; i < (int)(4 * sizeof(ZwSegment) / 4); i += WG)
+            ((uint32_t*)Sf)[i] = ((const uint32_t*)Pf->seg)[i];
+        for (int i = threadIdx.x; i < 256; i += WG) lut[i] = Pf->seg_enabled ? Pf->seg_map_lut[i] : 0;
+        load_static_tables(Tf, threadIdx.x, WG, &Pf->probs[0][0][0][0]);
+        if (!ROWS || chain_wg) {
+            uint8_t* ty = top_y + TS.y * fr;
+            uint8_t* tu = top_u + TS.u * fr;
+            uint8_t* tv = top_v + TS.v * fr;
+            uint8_t* tcx = top_c + TS.c * fr;
+            int8_t* td = top_derr + TS.d * fr;
+            if (!ROWS) {
+                for (int i = threadIdx.x; i < mbw * 16 + 48; i += WG) ty[i] = 127;
+                for (int i = threadIdx.x; i < mbw * 12; i += WG) tcx[i] = 0;
+            }
+            for (int i = threadIdx.x; i < mbw * 8 + 48; i += WG) {
+                tu[i] = 127;
+                tv[i] = 127;
+            }
+            for (int i = threadIdx.x; i < mbw * 4; i += WG) td[i] = PASS == 2 ? a.derr[(size_t)ff * mbw * 4 + i] : 0;
         }
-        for (int i = threadIdx.x; i < mbw * 4; i += WG) top_derr[i] = PASS == 2 ? a.derr[(size_t)f * mbw * 4 + i] : 0;
     }
     if (threadIdx.x < NW) progress[threadIdx.x] = -1;
     if (threadIdx.x < 2) xflag[threadIdx.x] = 0;
@@ -2856,6 +3209,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.P = P;
     C.T = T;
     C.W = W;
+    C.M = &W->mb;
     C.lane = lane;
     C.f = f;
     C.Sl = Sl;
@@ -2868,7 +3222,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     C.oy = C.oc = C.ocx = C.od = 0;
     const bool trel = PASS == 2 && __builtin_amdgcn_readfirstlane(P->do_trellis);
     // without trellis (and without the pass-2 I4 dump) the final I4 blocks are
-    // the search's winners, which the search leaves in W->lev / W->ws
+    // the search's winners, which the search leaves in C.M->lev / C.M->ws
     const bool keep_i4 = !trel && (PASS == 1 || a.dbg == nullptr);
     const size_t nmb = (size_t)mbw * mbh;
 #ifdef ZW_PHASE_PROF
@@ -2891,16 +3245,16 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_CHAIN_PRIO 3
 #endif
         __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
-        if (lane < 4) W->left_derr[lane] = 0;
+        if (lane < 4) C.M->left_derr[lane] = 0;
         if (NCH == 2) {
             // quad form: wave 0 the U plane, wave 1 the V plane
             const int pl = wv;
             UvQ U;
             U.pl = pl;
             U.w = W->cu;
-            U.sp = W->su;
+            U.sp = C.M->su;
             U.top = pl ? top_v : top_u;
-            U.left = W->left_u;
+            U.left = C.M->left_u;
             const uint8_t* const P0 = (pl ? a.V : a.U) + (size_t)f * a.csz;
             const int cs = mbw * 8;
             auto fetch_uv = [&](int mbx, int mby) {
@@ -2916,7 +3270,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             MbFetch nx = fetch_uv(0, 0);
             int seq = 0;
             for (int mby = 0; mby < mbh; mby++) {
-                if (lane < 12) W->left_u[lane] = 129;
+                if (lane < 12) C.M->left_u[lane] = 129;
                 wsync();
                 for (int mbx = 0; mbx < mbw; mbx++) {
                     PH_START();
@@ -2927,7 +3281,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                     else if (mby + 1 < mbh) nx = fetch_uv(0, mby + 1);
                     C.mbx = mbx;
                     C.mby = mby;
-                    if (lane < 16) ((uint32_t*)W->su)[lane] = cur.y;
+                    if (lane < 16) ((uint32_t*)C.M->su)[lane] = cur.y;
                     wsync();
                     const int seg = __builtin_amdgcn_readfirstlane((int)seg_lut[cur.alpha]);
                     C.seg = seg;
@@ -2954,8 +3308,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         MbFetch nx = fetch_mb(&a, f, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
-                W->left_u[lane] = 129;
-                W->left_v[lane] = 129;
+                C.M->left_u[lane] = 129;
+                C.M->left_v[lane] = 129;
             }
             wsync();
             for (int mbx = 0; mbx < mbw; mbx++) {
@@ -3066,6 +3420,250 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         C.top_c = W->win_c;
         C.top_derr = W->win_d;
     }
+    // everything of an MB after its searches: the final transforms, the
+    // complexity contexts (pass 2), the levels, the MB record and the borders
+    auto mb_store = [&](Ctx& C, int lm, int cm, bool i4reuse, uint32_t i4nz, bool trel) __attribute__((always_inline)) {
+        const int lane = C.lane;
+        PH_START();
+        int ynz[16];
+        const int lnz = final_luma(C, lm, trel, ynz, i4reuse ? (int)i4nz : -1);
+        PH_MARK(4);
+        int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int cnz = 0;
+        if (PASS == 2) cnz = final_chroma(C, cm, C.top_derr + C.od, uvnz);
+        PH_MARK(5);
+        ZwMbOut* o = a.out + (size_t)C.f * nmb + (size_t)C.mby * mbw + C.mbx;
+        if (PASS == 2) {
+            const int skip = !(lnz | cnz);
+            // complexity (encode_residual_data semantics / skip clearing)
+            if (lane == 0) {
+                uint8_t* tc = C.top_c + C.ocx;
+                uint8_t* lc = C.M->left_c;
+                if (skip) {
+                    for (int k = 1; k < 9; k++) tc[k] = lc[k] = 0;
+                    if (lm != 4) tc[0] = lc[0] = 0;
+                } else {
+                    if (lm != 4) {
+                        int y2nz = 0;
+                        for (int n = 0; n < 16; n++) y2nz |= C.M->lev[16][n] != 0;
+                        tc[0] = lc[0] = (uint8_t)y2nz;
+                    }
+                    for (int x = 0; x < 4; x++) tc[1 + x] = (uint8_t)ynz[12 + x];
+                    for (int y = 0; y < 4; y++) lc[1 + y] = (uint8_t)ynz[y * 4 + 3];
+                    tc[5] = (uint8_t)uvnz[2];
+                    tc[6] = (uint8_t)uvnz[3];
+                    lc[5] = (uint8_t)uvnz[1];
+                    lc[6] = (uint8_t)uvnz[3];
+                    tc[7] = (uint8_t)uvnz[6];
+                    tc[8] = (uint8_t)uvnz[7];
+                    lc[7] = (uint8_t)uvnz[5];
+                    lc[8] = (uint8_t)uvnz[7];
+                }
+                o->skip = (uint8_t)skip;
+                o->chroma_mode = (uint8_t)cm;
+            }
+            store_chroma_borders(C);
+            write_levels(C, 0, 25, skip);
+            if (a.sizes) {
+                // the packed record size k_pack_size would compute from these
+                // levels: header, eob bytes and every block's levels up to its eob
+                int e = 0;
+                if (lane < 25 && !skip) {
+                    const uint32_t* lw = (const uint32_t*)C.M->lev[lane];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const uint32_t v = lw[q];
+                        e = (v >> 16) ? 2 * q + 2 : ((v & 0xffffu) ? 2 * q + 1 : e);
+                    }
+                }
+                // lanes 0..24 hold the eobs: DPP sums per 16-lane row, rows 0 and 1 added
+                const int r16 = red16(e);
+                const int es = __builtin_amdgcn_readlane(r16, 0) + __builtin_amdgcn_readlane(r16, 16);
+                if (lane == 0)
+                    a.sizes[(size_t)C.f * nmb + (size_t)C.mby * mbw + C.mbx] = (uint32_t)(1 + (lm == 4 ? 8 : 0) + 25 + 2 * es);
+            }
+        } else {
+            write_levels(C, 0, 17, false);
+            if (lane == 0) o->skip = 0;  // pass-1 skip is decided on the host from the levels
+        }
+        if (lane == 0) {
+            o->luma_mode = (uint8_t)lm;
+            o->segment = (uint8_t)C.seg;
+        }
+        if (lane < 16) o->bpred[lane] = lm == 4 ? C.M->modes[lane] : 0;
+        store_luma_borders(C);
+    };
+    if constexpr (PAIR) {
+        // ---- frame pairs: every wave works MB row y of both frames of the
+        // workgroup (the rows of a frame go to the waves as in the one-frame
+        // kernel), MB (x, y) of frame 0 and of frame 1 per iteration.  Both
+        // frames' rows advance together, so one progress word per wave serves
+        // both.  The two MBs' I4 searches run in one wave (pick_i4_pair): lanes
+        // 0..31 frame 0, lanes 32..63 frame 1.  The other per-MB stages run in
+        // loops over the frames (not unrolled: one copy of their code), and what
+        // an MB's stages hand on goes through LDS (W->pst), not registers.
+        MbLds* const Mp[2] = {&W->mb, Mall2 + wv};
+        const int meth0 = C.method;
+        const int K = C.method <= 3 ? 3 : (C.method == 4 ? 4 : 10);
+        // per-frame encoder settings (a launch's frames normally share them)
+        const int meth1 = nf == 2 ? __builtin_amdgcn_readfirstlane(a.params[f + 1].method) : C.method;
+        const bool trel1 = nf == 2 && __builtin_amdgcn_readfirstlane(a.params[f + 1].do_trellis);
+        const bool keep1 = !trel1 && a.dbg == nullptr;
+        const bool same_k = nf == 1 || (meth1 == C.method && trel1 == trel);
+        for (int it = 0;; it++) {
+            const int mby = wv + it * NW;
+            if (mby >= mbh) break;
+#pragma unroll
+            for (int fr = 0; fr < 2; fr++) {
+                MbLds* M = Mp[fr];
+                if (lane < 20) M->left_y[lane] = 129;
+                if (lane < 12) {
+                    M->left_u[lane] = M->left_v[lane] = 129;
+                    M->left_c[lane] = 0;
+                }
+                if (lane < 4) M->left_derr[lane] = 0;
+            }
+            wsync();
+            const int prevw = mby > 0 ? (mby - 1) % NW : 0;
+            auto wait_above = [&](int need) {
+                if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + need);
+            };
+            for (int mbx = 0; mbx < mbw; mbx++) {
+                PH_START();
+                const int lane = opaque_lane(threadIdx.x & 63);
+                C.lane = lane;
+                // point C at frame fr's MB (x, y)
+                auto enter = [&](int fr) {
+                    // a fresh opaque lane per MB stage: lane-derived constants are
+                    // recomputed, not held across the other frame's stages
+                    C.lane = opaque_lane(threadIdx.x & 63);
+                    C.f = f + fr;
+                    C.P = a.params + C.f;
+                    C.T = (const LdsTables*)((const uint8_t*)T + sT * fr);
+                    C.Sl = (const ZwSegment*)((const uint8_t*)Sl + sS * fr);
+                    C.top_y = top_y + TS.y * fr;
+                    C.top_u = top_u + TS.u * fr;
+                    C.top_v = top_v + TS.v * fr;
+                    C.top_c = top_c + TS.c * fr;
+                    C.top_derr = top_derr + TS.d * fr;
+                    C.M = fr ? Mp[1] : Mp[0];
+                    C.method = fr ? meth1 : meth0;
+                    C.mbx = mbx;
+                    C.mby = mby;
+                    C.oy = mbx * 16;
+                    C.oc = mbx * 8;
+                    C.ocx = mbx * 12;
+                    C.od = mbx * 4;
+                    C.sY = C.M->sy;
+                    C.sU = C.M->su;
+                    C.sV = C.M->sv;
+                };
+                auto pst = [&](int fr, int k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)W->pst[fr][k]); };
+                wait_above(min(mbx + 1, mbw));
+#if ZW_DYN_PRIO > 0
+                {
+                    int slack = mbw;
+                    if (mby > 0) {
+                        const int v = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(&progress[prevw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        if ((v >> 16) == mby - 1) slack = (v & 0xffff) - mbx - 1;
+                    }
+                    constexpr int dp = ZW_DYN_PRIO;
+                    set_prio(slack >= dp * 3 ? 3 : (slack >= dp * 2 ? 2 : (slack >= dp ? 1 : 0)));
+                }
+#endif
+                PH_MARK(0);
+ZW_PAIR_LOOP
+                for (int fr = 0; fr < 2; fr++) {
+                    if (fr >= nf) {
+                        if (lane == 0) W->pst[fr][0] = 0;  // (no frame 1: no search)
+                        continue;
+                    }
+                    enter(fr);
+                    const MbFetch fm = fetch_mb(&a, C.f, lane, mbx, mby);
+                    setup_ctx(C, &a, seg_lut + 256 * fr, W, mbx, mby, fm);
+                    build_luma_border(C, 0);
+                    int l_;
+                    unsigned long long s_;
+                    pick_i16<PASS>(C, l_, s_);
+                    const bool n_ = C.method > 1 && (C.method >= 5 || s_ > 211ull * C.S->l_mode || l_ != 0);
+                    if (lane == 0) {
+                        W->pst[fr][0] = (uint32_t)l_ | ((uint32_t)n_ << 4) | ((uint32_t)C.seg << 8);
+                        W->pst[fr][1] = (uint32_t)s_;
+                        W->pst[fr][2] = (uint32_t)(s_ >> 32);
+                        W->pst[fr][3] = 0;
+                    }
+                    wsync();
+                }
+                wsync();
+                PH_MARK(1);
+                const uint32_t s0 = pst(0, 0), s1 = pst(1, 0);
+                const bool n0 = (s0 >> 4) & 1u, n1 = (s1 >> 4) & 1u;
+                if (n0 || n1) wait_above(min(mbx + 2, mbw));
+ZW_PAIR_LOOP
+                for (int fr = 0; fr < 2; fr++) {
+                    if (!((pst(fr, 0) >> 4) & 1u)) continue;
+                    enter(fr);
+                    build_luma_border(C, 1);
+                }
+                PH_MARK(21);
+                if (K <= 4 && same_k && (n0 || n1)) {
+                    Ctx CA = C, CB = C;
+                    CA.lane = CB.lane = opaque_lane(threadIdx.x & 63);
+                    CA.T = T;
+                    CB.T = (const LdsTables*)((const uint8_t*)T + sT);
+                    CA.M = Mp[0];
+                    CB.M = Mp[1];
+                    CA.S = Sl + (s0 >> 8);
+                    CB.S = (const ZwSegment*)((const uint8_t*)Sl + sS) + (s1 >> 8);
+                    CA.sY = Mp[0]->sy;
+                    CB.sY = Mp[1]->sy;
+                    const unsigned long long i0 = pst(0, 1) | ((unsigned long long)pst(0, 2) << 32);
+                    const unsigned long long i1 = pst(1, 1) | ((unsigned long long)pst(1, 2) << 32);
+                    uint32_t z0 = 0, z1 = 0;
+                    const uint32_t r = pick_i4_pair<PASS>(CA, CB, i0, i1, n0, n1, keep_i4, z0, z1);
+                    if (lane == 0) {
+                        W->pst[0][3] = (r & 1u) ? (z0 | 0x10000u) : 0u;
+                        W->pst[1][3] = (r & 2u) ? (z1 | 0x10000u) : 0u;
+                    }
+                } else if (n0 || n1) {
+ZW_PAIR_LOOP
+                    for (int fr = 0; fr < 2; fr++) {
+                        const uint32_t sm = pst(fr, 0);
+                        if (!((sm >> 4) & 1u)) continue;
+                        enter(fr);
+                        C.seg = (int)(sm >> 8);
+                        C.S = C.Sl + C.seg;
+                        uint32_t z = 0;
+                        const bool w4 = pick_i4<PASS>(C, pst(fr, 1) | ((unsigned long long)pst(fr, 2) << 32),
+                                                      fr ? keep1 : keep_i4, z);
+                        if (lane == 0) W->pst[fr][3] = w4 ? (z | 0x10000u) : 0u;
+                    }
+                }
+                wsync();
+                PH_MARK(2);
+ZW_PAIR_LOOP
+                for (int fr = 0; fr < 2; fr++) {
+                    if (fr >= nf) continue;
+                    enter(fr);
+                    const uint32_t sm = pst(fr, 0), r4 = pst(fr, 3);
+                    C.seg = (int)(sm >> 8);
+                    C.S = C.Sl + C.seg;
+                    build_chroma_border(C);
+                    const int cm = pick_uv<PASS>(C);
+                    PH_MARK(3);
+                    const bool w4 = (r4 >> 16) & 1u;
+                    mb_store(C, w4 ? 4 : (int)(sm & 15u), cm, w4 && (fr ? keep1 : keep_i4), r4 & 0xffffu,
+                             fr ? trel1 : trel);
+                    PH_RESET();
+                }
+                publish(progress, wv, mby * 65536 + mbx + 1);
+                PH_MARK(6);
+            }
+        }
+        ph_flush();
+        return;
+    }
     uint8_t* const gty = ROWS ? rb + RL.ty : nullptr;
     uint8_t* const gtu = ROWS ? rb + RL.tu : nullptr;
     uint8_t* const gtv = ROWS ? rb + RL.tv : nullptr;
@@ -3075,13 +3673,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         const int mby = ROWS ? row_ticket(&rsync[0]) : (skip_mode ? yk : rw + it * nrw);
         if (skip_mode) yk = next_row(yk);
         if (mby >= mbh) break;
-        if (lane < 20) W->left_y[lane] = 129;
+        if (lane < 20) C.M->left_y[lane] = 129;
         if (lane < 12) {
-            W->left_u[lane] = 129;
-            W->left_v[lane] = 129;
-            W->left_c[lane] = 0;
+            C.M->left_u[lane] = 129;
+            C.M->left_v[lane] = 129;
+            C.M->left_c[lane] = 0;
         }
-        if (lane < 4) W->left_derr[lane] = 0;
+        if (lane < 4) C.M->left_derr[lane] = 0;
         wsync();
         const int prevw = (!ROWS && mby > 0) ? wave_of_row(mby - 1) : 0;
         int seen = -1;  // ROWS: last progress value read of the row above
@@ -3210,73 +3808,8 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 }
             }
             PH_MARK(2);
-            int ynz[16];
-            const int lnz = final_luma(C, lm, trel, ynz, i4reuse ? (int)i4nz : -1);
-            PH_MARK(4);
-            int uvnz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            int cnz = 0;
-            if (PASS == 2) cnz = final_chroma(C, cm, C.top_derr + C.od, uvnz);
-            PH_MARK(5);
-            ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
-            if (PASS == 2) {
-                const int skip = !(lnz | cnz);
-                // complexity (encode_residual_data semantics / skip clearing)
-                if (lane == 0) {
-                    uint8_t* tc = C.top_c + C.ocx;
-                    uint8_t* lc = W->left_c;
-                    if (skip) {
-                        for (int k = 1; k < 9; k++) tc[k] = lc[k] = 0;
-                        if (lm != 4) tc[0] = lc[0] = 0;
-                    } else {
-                        if (lm != 4) {
-                            int y2nz = 0;
-                            for (int n = 0; n < 16; n++) y2nz |= W->lev[16][n] != 0;
-                            tc[0] = lc[0] = (uint8_t)y2nz;
-                        }
-                        for (int x = 0; x < 4; x++) tc[1 + x] = (uint8_t)ynz[12 + x];
-                        for (int y = 0; y < 4; y++) lc[1 + y] = (uint8_t)ynz[y * 4 + 3];
-                        tc[5] = (uint8_t)uvnz[2];
-                        tc[6] = (uint8_t)uvnz[3];
-                        lc[5] = (uint8_t)uvnz[1];
-                        lc[6] = (uint8_t)uvnz[3];
-                        tc[7] = (uint8_t)uvnz[6];
-                        tc[8] = (uint8_t)uvnz[7];
-                        lc[7] = (uint8_t)uvnz[5];
-                        lc[8] = (uint8_t)uvnz[7];
-                    }
-                    o->skip = (uint8_t)skip;
-                    o->chroma_mode = (uint8_t)cm;
-                }
-                store_chroma_borders(C);
-                write_levels(C, 0, 25, skip);
-                if (a.sizes) {
-                    // the packed record size k_pack_size would compute from these
-                    // levels: header, eob bytes and every block's levels up to its eob
-                    int e = 0;
-                    if (lane < 25 && !skip) {
-                        const uint32_t* lw = (const uint32_t*)W->lev[lane];
-#pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            const uint32_t v = lw[q];
-                            e = (v >> 16) ? 2 * q + 2 : ((v & 0xffffu) ? 2 * q + 1 : e);
-                        }
-                    }
-                    // lanes 0..24 hold the eobs: DPP sums per 16-lane row, rows 0 and 1 added
-                    const int r16 = red16(e);
-                    const int es = __builtin_amdgcn_readlane(r16, 0) + __builtin_amdgcn_readlane(r16, 16);
-                    if (lane == 0)
-                        a.sizes[(size_t)f * nmb + (size_t)mby * mbw + mbx] = (uint32_t)(1 + (lm == 4 ? 8 : 0) + 25 + 2 * es);
-                }
-            } else {
-                write_levels(C, 0, 17, false);
-                if (lane == 0) o->skip = 0;  // pass-1 skip is decided on the host from the levels
-            }
-            if (lane == 0) {
-                o->luma_mode = (uint8_t)lm;
-                o->segment = (uint8_t)C.seg;
-            }
-            if (lane < 16) o->bpred[lane] = lm == 4 ? W->modes[lane] : 0;
-            store_luma_borders(C);
+            mb_store(C, lm, cm, i4reuse, i4nz, trel);
+            PH_RESET();
             if (ROWS) {
                 // push this MB's state for the row below (sc1), then publish
                 if (mby + 1 < mbh) {
@@ -3298,6 +3831,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 
 extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1, false>(a); }
 extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2, false>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2_fp(EncArgs a) { encode_body<2, false, 2>(a); }
 extern "C" __global__ __launch_bounds__(64 * RowsShape<1>::NW) void k_encode_rows_pass1(EncArgs a) { encode_body<1, true>(a); }
 extern "C" __global__ __launch_bounds__(64) void k_encode_rows_pass2(EncArgs a) { encode_body<2, true>(a); }
 
@@ -3403,18 +3937,39 @@ extern "C" hipError_t zwk_quant_blocks(hipStream_t s, const int* coeffs, const u
     return hipGetLastError();
 }
 
-static size_t encode_lds_bytes(int mbw, int nw, bool rows, int pass)
+static size_t encode_lds_bytes(int mbw, int nw, bool rows, int pass, int fp = 1)
 {
     size_t off = 0;
-    off += (sizeof(LdsTables) + 15) & ~(size_t)15;
-    off += (4 * sizeof(ZwSegment) + 15) & ~(size_t)15;
-    off += 256;
+    off += ((sizeof(LdsTables) + 15) & ~(size_t)15) * fp;
+    off += ((4 * sizeof(ZwSegment) + 15) & ~(size_t)15) * fp;
+    off += 256 * fp;
     off += ((sizeof(WaveLds) + 15) & ~(size_t)15) * nw;
+    if (fp == 2) off += ((sizeof(MbLds) + 15) & ~(size_t)15) * nw;
     off += 64;
     off += 256;
     const TopLds t(mbw, rows, pass);
-    return off + t.y + t.u + t.v + t.c + t.d;
+    return off + (t.y + t.u + t.v + t.c + t.d) * fp;
 }
+
+// Pass 2 in frame pairs (k_encode_pass2_fp) for launches of at least two
+// frames per CU whose pair shape fits in LDS; ZW_ENC_FP=0/1 forces it off/on
+// (where it fits).
+static bool encode_fp_for(int mbw, int nframes)
+{
+    static const int mode = [] { const char* e = getenv("ZW_ENC_FP"); return e && *e ? atoi(e) : -1; }();
+    static const int cus = [] {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        return hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                       prop.multiProcessorCount > 0
+                   ? prop.multiProcessorCount
+                   : 256;
+    }();
+    if (mode == 0 || nframes < 2) return false;
+    if (encode_lds_bytes(mbw, PassShape<2>::NW, false, 2, 2) > 160 * 1024) return false;
+    return mode == 1 || nframes >= 2 * cus;
+}
+extern "C" int zwk_encode_fp(int mbw, int nframes) { return encode_fp_for(mbw, nframes) ? 1 : 0; }
 
 
 // ---------------------------------------------------------------------------
@@ -3505,9 +4060,11 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
     a.Y = Y; a.U = U; a.V = V; a.alpha = alpha; a.params = params; a.lcost = lcost; a.derr = derr; a.out = out;
     a.ry = ry; a.ru = ru; a.rv = rv; a.ysz = ysz; a.csz = csz; a.mbw = mbw; a.mbh = mbh; a.pass = pass;
     a.rows = rows;
+    a.nframes = nframes;
     static const bool attr_set = []() {
         (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_pass2_fp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_rows_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_rows_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
@@ -3523,6 +4080,11 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
             hipLaunchKernelGGL(k_encode_rows_pass2, dim3(mbh, nframes), dim3(64), encode_lds_bytes(mbw, 1, true, 2), s,
                                a);
         }
+        return hipGetLastError();
+    }
+    if (pass == 2 && encode_fp_for(mbw, nframes)) {
+        hipLaunchKernelGGL(k_encode_pass2_fp, dim3((nframes + 1) / 2), dim3(PassShape<2>::WG),
+                           encode_lds_bytes(mbw, PassShape<2>::NW, false, 2, 2), s, a);
         return hipGetLastError();
     }
     const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW, false, pass);

@@ -57,6 +57,7 @@ hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* 
                       int nframes, int* dbg, uint8_t* rows, uint32_t* sizes = nullptr);
 size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
 int zwk_encode_max_mbw(int rows);
+int zwk_encode_fp(int mbw, int nframes);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -491,6 +492,11 @@ struct PipeLane {
     Pinned<ZwStatsOut> h_stats;          // [chunk] pass-1 statistics from k_stats
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
+    // Pass 2 in frame pairs (k_encode_pass2_fp: two frames a workgroup, so a
+    // launch fills the CUs with two frames per CU): chunks 2k and 2k + 1 take
+    // pass 2 in one launch, pass 1 and the statistics stay per chunk.
+    bool pair2 = false;
+    int p2_frames = 0;  // frames of the timed pass-2 launch (kms[3] is scaled to one chunk)
     int rc = 0;
     // Host-source streaming (zw_pipe_encode_host): the lane's uploader thread
     // copies batch b's frames into input buffer b & 1 on `ustream`, one event
@@ -632,8 +638,9 @@ static int pipe_lanes_for(int n, int device)
     return g;
 }
 // Frames per kernel launch inside a lane: one encode workgroup occupies a
-// whole CU (512 threads x 256 VGPRs), so a launch of one frame per CU fills
+// whole CU (768 threads x 168 VGPRs), so a launch of one frame per CU fills
 // the device; the lane runs pass 1 of chunk c+1 while the host works on chunk c.
+// (Pass 2 may take two chunks in one launch: PipeLane::pair2.)
 static int pipe_chunk_for(int lane_frames, int device)
 {
     const char* e = getenv("ZW_PIPE_CHUNK");
@@ -750,6 +757,8 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
             // wave that gave up waiting would, so the host-side check is exercised
             if (ok && getenv("ZW_ENC_FORCE_ERROR")) ok = hipMemset(L.d_rows, 1, 1) == hipSuccess;
         }
+        // pass 2 of chunks (2k, 2k + 1) in one launch where it runs in frame pairs
+        L.pair2 = ok && !L.d_rows && nch >= 2 && zwk_encode_fp(p->mbw, 2 * L.chunk);
         for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
         for (size_t i = 0; ok && i < L.cev.size(); i++)
             ok = hipEventCreateWithFlags(&L.cev[i], hipEventDisableTiming) == hipSuccess;
@@ -977,7 +986,10 @@ static int chunk_pass2(zw_pipe* p, PipeLane& L, int fa, int na, bool timed)
 {
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa;
-    if (timed) HIPOK(hipEventRecord(L.ev[4], s));
+    if (timed) {
+        HIPOK(hipEventRecord(L.ev[4], s));
+        L.p2_frames = na;
+    }
     HIPOK(rows_reset(p, L, na));
     HIPOK(zwk_encode(s, 2, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
                      p->d_params + F, p->d_lcost + F, p->d_derr + F * p->mbw * 4, p->d_out2 + F * p->nmb,
@@ -1046,7 +1058,8 @@ static void lane_times(PipeLane& L)
     (void)hipEventElapsedTime(&L.kms[0], L.ev[0], L.ev[1]);  // rgb2yuv
     (void)hipEventElapsedTime(&L.kms[1], L.ev[1], L.ev[2]);  // analysis + segments
     (void)hipEventElapsedTime(&L.kms[2], L.ev[2], L.ev[3]);  // pass 1
-    (void)hipEventElapsedTime(&L.kms[3], L.ev[4], L.ev[5]);  // pass 2
+    (void)hipEventElapsedTime(&L.kms[3], L.ev[4], L.ev[5]);  // pass 2 (per chunk of frames)
+    if (L.p2_frames > 0 && L.p2_frames != L.chunk) L.kms[3] *= (float)L.chunk / (float)L.p2_frames;
 }
 
 // Software-pipelined encode of one lane.  Per batch: pass 1 of every chunk is
@@ -1255,31 +1268,38 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     if (r) return fail(r);
     for (int b = 0; b < nb; b++) {
         for (int c = 0; c < nch; c++) {
-            const double t0 = now_ms();
-            r = p->host_stats ? chunk_fetch(p, L, L.fb[0], ca(c), cn(c), 2 * c, L.cev[2 * c])
-                              : chunk_fetch_stats(p, L, ca(c), cn(c), L.cev[2 * c]);
-            if (r) return fail(r);
-            const double t1 = now_ms();
-            if ((r = chunk_stats(p, L, ca(c), cn(c), b & 1))) return fail(r);
-            stats += now_ms() - t1;
-            fetch += t1 - t0;
-            if (g_trace)
-                fprintf(stderr, "  lane %d batch %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, b, c,
-                        t1 - g_trace_t0, now_ms() - g_trace_t0);
-            if (emit && b > 0) {  // the emitter has copied out chunk c of batch b-1
-                std::unique_lock<std::mutex> lk(L.sync->mu);
-                const long long need = (long long)(b - 1) * nch + c + 1;
-                L.sync->cv.wait(lk, [&] { return L.sync->fetched >= need; });
-                if (L.sync->fetched == FAILED) {
-                    lk.unlock();
-                    const int re = join_emitter();
-                    return re ? re : ZW_EDEVICE;
+            // pass 2 of chunk c alone, or of chunks c and c + 1 in one launch (pair2)
+            const int c1 = (L.pair2 && (c & 1) == 0 && c + 1 < nch) ? c + 1 : c;
+            for (int k = c; k <= c1; k++) {
+                const double t0 = now_ms();
+                r = p->host_stats ? chunk_fetch(p, L, L.fb[0], ca(k), cn(k), 2 * k, L.cev[2 * k])
+                                  : chunk_fetch_stats(p, L, ca(k), cn(k), L.cev[2 * k]);
+                if (r) return fail(r);
+                const double t1 = now_ms();
+                if ((r = chunk_stats(p, L, ca(k), cn(k), b & 1))) return fail(r);
+                stats += now_ms() - t1;
+                fetch += t1 - t0;
+                if (g_trace)
+                    fprintf(stderr, "  lane %d batch %d chunk %d: p1 fetched %.1f stats done %.1f\n", L.f0, b, k,
+                            t1 - g_trace_t0, now_ms() - g_trace_t0);
+                if (emit && b > 0) {  // the emitter has copied out chunk k of batch b-1
+                    std::unique_lock<std::mutex> lk(L.sync->mu);
+                    const long long need = (long long)(b - 1) * nch + k + 1;
+                    L.sync->cv.wait(lk, [&] { return L.sync->fetched >= need; });
+                    if (L.sync->fetched == FAILED) {
+                        lk.unlock();
+                        const int re = join_emitter();
+                        return re ? re : ZW_EDEVICE;
+                    }
                 }
             }
-            r = chunk_pass2(p, L, ca(c), cn(c), c == 0);
-            if (!r && emit) r = chunk_pack(p, L, ca(c), cn(c), p->d_out2, 2 * c + 1);
-            if (!r && hipEventRecord(L.cev[2 * c + 1], L.stream) != hipSuccess) r = ZW_EDEVICE;
+            r = chunk_pass2(p, L, ca(c), ca(c1) + cn(c1) - ca(c), c == 0);
+            for (int k = c; k <= c1 && !r; k++) {
+                if (emit) r = chunk_pack(p, L, ca(k), cn(k), p->d_out2, 2 * k + 1);
+                if (!r && hipEventRecord(L.cev[2 * k + 1], L.stream) != hipSuccess) r = ZW_EDEVICE;
+            }
             if (r) return fail(r);
+            c = c1;
         }
         if (b + 1 < nb && (r = queue_pass1())) return fail(r);
         if (emit) {

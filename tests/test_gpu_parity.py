@@ -242,6 +242,44 @@ def test_encode_rows_multi_frame(ctx, monkeypatch, chunk):
         p.close()
 
 
+@pytest.mark.parametrize("chunk,n", [("2", 5), ("3", 7), ("4", 4)])
+def test_encode_frame_pairs(ctx, monkeypatch, chunk, n):
+    """Pass 2 in frame pairs (k_encode_pass2_fp: two frames per workgroup, the
+    two MBs' I4 searches in one wave), forced on at small sizes: pass 2 of
+    chunks (2k, 2k + 1) in one launch, odd frame counts (a workgroup with one
+    frame), ragged last chunks, per-frame segments and content; several batches
+    (encode_repeat).  Every frame must equal the reference's stream."""
+    monkeypatch.setenv("ZW_ENC_FP", "1")
+    monkeypatch.setenv("ZW_ENC_ROWS", "0")
+    monkeypatch.setenv("ZW_PIPE_CHUNK", chunk)
+    w, h = 208, 144
+    imgs = [synth_rgba(w, h, 0x5EED3000 + i, ("natural", "noise", "flat")[i % 3]) for i in range(n)]
+    p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+    try:
+        for i, img in enumerate(imgs):
+            p.upload(i, img)
+        p.encode_repeat(2)
+        for i, img in enumerate(imgs):
+            rc, ref, _ = O.encode(img, w, h, 3, 75, 4)
+            assert p.output(i) == ref, f"frame {i}"
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("m,q", [(2, 40), (3, 90), (5, 75), (6, 30)])
+def test_encode_frame_pairs_methods(ctx, monkeypatch, m, q):
+    """Frame-pair pass 2 at other methods: K = 3 candidates (methods 2-3), the
+    ten-candidate search (methods 5-6, each frame's own search) and trellis."""
+    monkeypatch.setenv("ZW_ENC_FP", "1")
+    monkeypatch.setenv("ZW_ENC_ROWS", "0")
+    w, h = 144, 96
+    imgs = [synth_rgba(w, h, 0x5EED4000 + i, ("natural", "noise")[i % 2]) for i in range(3)]
+    outs = zwebp.encode_batch(imgs, w, h, zwebp.ColorType.Rgba8, q, m, ctx=ctx)
+    for i, img in enumerate(imgs):
+        rc, ref, _ = O.encode(img, w, h, 3, q, m)
+        assert outs[i] == ref, f"frame {i}"
+
+
 def test_encode_repeat_streaming(ctx, monkeypatch):
     """encode_repeat: batch k+1's pass 1 overlaps batch k's emission (separate
     pass-1 / pass-2 pack buffers); several chunks per lane; every batch's

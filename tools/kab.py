@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One-lane encode kernel times of the library ZWEBP_LIB names (for A/B runs):
-256 1080p frames, one launch per pass, best of R runs (ms per launch).
+KAB_FRAMES (256) 1080p frames per chunk, best of R runs (ms per launch).
 usage: ZWEBP_LIB=... python tools/kab.py [R] [W H]"""
 import json
 import os
@@ -13,7 +13,9 @@ import zwebp  # noqa: E402
 from zwebp.synth import synth_rgba  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-w, h, n = (int(sys.argv[2]), int(sys.argv[3]), 256) if len(sys.argv) > 3 else (1920, 1080, 256)
+n = int(os.environ.get("KAB_FRAMES", "256"))  # frames per launch (512: pass 2 in frame pairs)
+os.environ.setdefault("ZW_PIPE_CHUNK", str(n))
+w, h = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
 ctx = zwebp.Context(0)
 imgs = [synth_rgba(w, h, 0x5EED0000 + i) for i in range(4)]
 p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
