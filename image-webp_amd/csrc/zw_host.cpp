@@ -1019,35 +1019,85 @@ static void emit_vp8(zw_pipe* p, std::vector<uint8_t>& out, const uint8_t* rec, 
     }
 }
 
+// ZW_DUMP_EMIT=<path>: the emission input of the pipe's frame 0 (its
+// parameters, probability updates and packed records) for tools/emit_bench.cpp.
+static void dump_emit_input(zw_pipe* p, const uint8_t* rec, size_t bytes, size_t hf)
+{
+    static const char* path = getenv("ZW_DUMP_EMIT");
+    static std::atomic<int> done{0};
+    if (!path || done.exchange(1)) return;
+    FILE* fp = fopen(path, "wb");
+    if (!fp) return;
+    const uint32_t hdr[4] = {0x4d45575au, (uint32_t)sizeof(ZwFrameParams), (uint32_t)p->w, (uint32_t)p->h};
+    const uint8_t have = p->h_have_upd[hf];
+    const unsigned long long n = bytes;
+    bool ok = fwrite(hdr, sizeof hdr, 1, fp) == 1 && fwrite(&p->h_params[hf], sizeof(ZwFrameParams), 1, fp) == 1 &&
+              fwrite(&have, 1, 1, fp) == 1 && fwrite(p->h_upd.data() + hf * 4 * 8 * 3 * 11, 4 * 8 * 3 * 11, 1, fp) == 1 &&
+              fwrite(&n, sizeof n, 1, fp) == 1 && fwrite(rec, 1, bytes, fp) == bytes;
+    (void)ok;
+    fclose(fp);
+}
+
 static int chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
     const FetchBuf& B = L.fb[1];
+    if (fa == 0) dump_emit_input(p, B.pack + B.finfo[0], (size_t)B.finfo[1], hidx(p, par, 0));
     std::atomic<int> err{ZW_OK};
-    parallel_for(na, [&](int i) {
-        const size_t f = F + i, hf = hidx(p, par, f);
-        std::vector<uint8_t>& out = p->bitstreams[f];
-        if (!p->container) {
-            emit_vp8(p, out, B.pack + B.finfo[2 * i], hf, na);
-            return;
+    // One token partition (the default): the frames go out in groups of up to
+    // ZW_EMIT_GROUP (4), whose boolean coders run interleaved in one thread
+    // (zwh::emit_frames); with token partitions, one frame per task.
+    static const int group = [] {
+        const char* e = getenv("ZW_EMIT_GROUP");
+        const int g = e && *e ? atoi(e) : 4;
+        return g < 1 ? 1 : (g > 4 ? 4 : g);
+    }();
+    const int G = p->nparts == 1 ? group : 1;
+    parallel_for((na + G - 1) / G, [&](int g) {
+        const int i0 = g * G, K = std::min(G, na - i0);
+        thread_local std::vector<uint8_t> vp8[4], alph;
+        std::vector<uint8_t>* outs[4];
+        for (int k = 0; k < K; k++) {
+            const size_t f = F + i0 + k;
+            // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398) wraps
+            // the VP8 frame (and for alpha inputs the ALPH chunk) in a container
+            outs[k] = p->container ? &vp8[k] : &p->bitstreams[f];
+            outs[k]->clear();
         }
-        // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398): the
-        // VP8 frame, and for alpha inputs the ALPH chunk (encode_alpha_lossless)
-        thread_local std::vector<uint8_t> vp8, alph;
-        vp8.clear();
-        alph.clear();
-        emit_vp8(p, vp8, B.pack + B.finfo[2 * i], hf, na);
-        out.clear();
-        if (has_alpha) {
-            if (const int r = zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph)) {
-                int ok = ZW_OK;
-                err.compare_exchange_strong(ok, r);
-                return;
+        if (p->nparts == 1) {
+            const ZwFrameParams* Pk[4];
+            const uint8_t* rk[4];
+            bool hk[4];
+            const uint8_t(*uk[4])[8][3][11];
+            for (int k = 0; k < K; k++) {
+                const size_t hf = hidx(p, par, F + i0 + k);
+                Pk[k] = &p->h_params[hf];
+                rk[k] = B.pack + B.finfo[2 * (i0 + k)];
+                hk[k] = p->h_have_upd[hf] != 0;
+                uk[k] = (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11);
             }
+            zwh::emit_frames(outs, Pk, rk, K, p->w, p->h, hk, uk);
+        } else {
+            emit_vp8(p, *outs[0], B.pack + B.finfo[2 * i0], hidx(p, par, F + i0), na);
         }
-        const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
-        zw_webp_wrap(out, vp8.data(), vp8.size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w, p->h, md);
+        if (!p->container) return;
+        for (int k = 0; k < K; k++) {
+            const size_t f = F + i0 + k;
+            std::vector<uint8_t>& out = p->bitstreams[f];
+            alph.clear();
+            out.clear();
+            if (has_alpha) {
+                if (const int r = zw_alph_encode(p->host_frames[f], p->img_stride, p->w, p->h, p->color, alph)) {
+                    int ok = ZW_OK;
+                    err.compare_exchange_strong(ok, r);
+                    return;
+                }
+            }
+            const zw_metadata md = {nullptr, 0, nullptr, 0, nullptr, 0};
+            zw_webp_wrap(out, outs[k]->data(), outs[k]->size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w,
+                         p->h, md);
+        }
     });
     return err.load();
 }

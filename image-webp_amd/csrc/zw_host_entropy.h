@@ -193,7 +193,11 @@ struct TreePaths {
     {
         for (int v = 0; v < nsym; v++) n[v] = (uint8_t)tree_path(t, tlen, v, 0, bits[v], pidx[v]);
     }
-    void put(BoolEncoder& E, const uint8_t* probs, int v) const { E.path(bits[v], pidx[v], n[v], probs); }
+    template <class Enc>
+    void put(Enc& E, const uint8_t* probs, int v) const
+    {
+        E.path(bits[v], pidx[v], n[v], probs);
+    }
 };
 
 // TOKEN_TREE paths for tokens 0..11 from start index 0 / 2 (after a zero token)
@@ -471,7 +475,8 @@ inline bool updated_probs(const Stats& S, uint8_t out[4][8][3][11])
 
 // encode_coefficients token part (vp8.rs:845-958) for an already-quantized
 // packed block (eob = last nonzero + 1).
-inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first, int ctx)
+template <class Enc>
+inline int emit_block(Enc& E, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first, int ctx)
 {
     const TokenPaths& TP = token_paths();
     int skip_eob = 0;
@@ -504,7 +509,8 @@ inline int emit_block(BoolEncoder& E, const uint8_t (*P)[3][11], const uint8_t* 
 
 // Compressed frame header (encode_compressed_frame_header vp8.rs:332-372) with
 // log2(nparts) token partitions; `probs` leaves with the probabilities in force.
-inline void emit_frame_header(BoolEncoder& H, const ZwFrameParams& P, bool have_updated,
+template <class Enc>
+inline void emit_frame_header(Enc& H, const ZwFrameParams& P, bool have_updated,
                               const uint8_t upd[4][8][3][11], int nparts, uint8_t probs[4][8][3][11])
 {
     memcpy(probs, COEFF_PROBS, sizeof(COEFF_PROBS));
@@ -556,8 +562,8 @@ inline void emit_frame_header(BoolEncoder& H, const ZwFrameParams& P, bool have_
 }
 
 // write_macroblock_header (vp8.rs:498-560) of MB x of the current row.
-inline void emit_mb_header(BoolEncoder& H, const ZwFrameParams& P, const PackedMb& m, uint8_t* top_bp, uint8_t left_bp[4],
-                           int x)
+template <class Enc>
+inline void emit_mb_header(Enc& H, const ZwFrameParams& P, const PackedMb& m, uint8_t* top_bp, uint8_t left_bp[4], int x)
 {
     static const TreePaths seg_t(SEGMENT_ID_TREE, 6, 4), ymode_t(YMODE_TREE, 8, 5), bmode_t(BMODE_TREE, 18, 10),
         uvmode_t(UVMODE_TREE, 6, 4);
@@ -585,7 +591,8 @@ inline void emit_mb_header(BoolEncoder& H, const ZwFrameParams& P, const PackedM
 // encode_residual_data (vp8.rs:650-800) of one MB with its left / top
 // complexity (non-zero) contexts.  Without an encoder (E == nullptr) only the
 // contexts advance: a block's context bit is eob > 0, as emit_block returns.
-inline void emit_mb_tokens(BoolEncoder* E, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
+template <class Enc>
+inline void emit_mb_tokens(Enc* E, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
 {
     const bool i4 = m.luma == 4;
     if (m.skip) {
@@ -721,7 +728,7 @@ inline void emit_frame_parts(std::vector<uint8_t>& out, const ZwFrameParams& P, 
         for (int x = 0; x < mbw; x++) {
             packed = view_mb(packed, m);
             emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
-            emit_mb_tokens(nullptr, probs, m, left, top[x]);
+            emit_mb_tokens<BoolEncoder>(nullptr, probs, m, left, top[x]);
         }
     }
     H.flush();
@@ -742,6 +749,363 @@ inline void emit_frame_parts(std::vector<uint8_t>& out, const ZwFrameParams& P, 
         E.flush();
     });
     assemble_frame(out, H.buf, T, nparts, width, height);
+}
+
+// ---------------------------------------------------------------------------
+// Split emission: the token walk records each MB's decisions (bit, probability)
+// and a tight loop codes them.  The boolean coder's cost is its serial
+// dependence through `range` (multiply, select, count-leading-zeros, shift per
+// decision); with the token logic out of that loop, the coder of two frames can
+// run interleaved in one thread (emit_frames2), so the two independent chains
+// overlap.  Byte-identical to emit_frame (tools/emit_bench.cpp, the equivalence
+// tests): the same arithmetic in the same order per stream.
+// ---------------------------------------------------------------------------
+struct DecRec {  // BoolEncoder's interface; each decision appended as prob | bit << 8
+    uint16_t* p;
+    inline void put(int bit, int prob) { *p++ = (uint16_t)((uint32_t)prob | ((uint32_t)(bit != 0) << 8)); }
+    void flag(int f) { put(f, 128); }
+    void literal(int nbits, int v)
+    {
+        for (int b = nbits - 1; b >= 0; b--) put(((1 << b) & v) > 0, 128);
+    }
+    inline void path(const uint8_t* bits, const uint8_t* pidx, int n, const uint8_t* probs)
+    {
+        for (int i = 0; i < n; i++) put(bits[i], probs[pidx[i]]);
+    }
+};
+// decisions of one MB's tokens: at most 25 blocks x 16 positions x (11 tree +
+// 11 extra + 1 sign) + 25 end-of-block decisions
+constexpr int kMbDecisionsMax = 25 * 16 * 23 + 25;
+
+// BoolEncoder's arithmetic into a caller-sized byte buffer (one spare byte in
+// front for a carry out of the first byte).
+struct RawBool {
+    std::vector<uint8_t> buf;
+    size_t lo = 1, pos = 1;  // first byte, next byte
+    uint32_t low = 0, range = 255;
+    int count = -24;
+    void reserve_more(size_t n)
+    {
+        if (pos + n + 8 > buf.size()) buf.resize((pos + n + 8) * 2);
+    }
+    void carry(uint8_t* b)
+    {
+        size_t i = pos;
+        while (i > lo) {
+            i--;
+            if (b[i] < 255) {
+                b[i]++;
+                return;
+            }
+            b[i] = 0;
+        }
+        b[--lo] = 1;
+    }
+    void flush()
+    {
+        reserve_more(8);
+        uint8_t* b = buf.data();
+        const int bit_num = -count;
+        int c = bit_num;
+        uint32_t v = low;
+        if (low & (1u << (32 - bit_num))) carry(b);
+        v <<= (c & 7);
+        c = (c >> 3) - 1;
+        while (c >= 0) {
+            v <<= 8;
+            c--;
+        }
+        for (c = 3; c >= 0; c--) {
+            b[pos++] = (uint8_t)(v >> 24);
+            v <<= 8;
+        }
+    }
+    const uint8_t* data() const { return buf.data() + lo; }
+    size_t size() const { return pos - lo; }
+};
+
+// One decision of stream S (state in locals the caller keeps in registers).
+#define ZW_RAW_PUT(D, LOW, RANGE, COUNT, BUF, POS, S)                            \
+    do {                                                                          \
+        const uint32_t prob_ = (D) & 255u, m_ = 0u - ((D) >> 8);                  \
+        const uint32_t split_ = 1 + (((RANGE - 1) * prob_) >> 8);                 \
+        LOW += split_ & m_;                                                       \
+        const uint32_t r_ = split_ ^ ((split_ ^ (RANGE - split_)) & m_);          \
+        const int shift_ = __builtin_clz(r_) - 24;                                \
+        RANGE = r_ << shift_;                                                     \
+        COUNT += shift_;                                                          \
+        if (COUNT >= 0) {                                                         \
+            const int offset_ = shift_ - COUNT;                                   \
+            if ((LOW << (offset_ - 1)) & 0x80000000u) {                           \
+                S.pos = POS;                                                      \
+                S.carry(BUF);                                                     \
+            }                                                                     \
+            BUF[POS++] = (uint8_t)(LOW >> (24 - offset_));                        \
+            LOW = (LOW << offset_) & 0xffffffu;                                   \
+            LOW <<= COUNT;                                                        \
+            COUNT -= 8;                                                           \
+        } else {                                                                  \
+            LOW <<= shift_;                                                       \
+        }                                                                         \
+    } while (0)
+
+// M streams, n decisions each, interleaved (M independent dependency chains)
+template <int M>
+inline void raw_codeM(RawBool* const* S, const uint16_t* const* d, int n)
+{
+    uint8_t* b[M];
+    uint32_t lo[M], ra[M];
+    int co[M];
+    size_t po[M];
+#pragma GCC unroll 4
+    for (int k = 0; k < M; k++) {
+        S[k]->reserve_more((size_t)n);
+        b[k] = S[k]->buf.data();
+        lo[k] = S[k]->low, ra[k] = S[k]->range, co[k] = S[k]->count, po[k] = S[k]->pos;
+    }
+    for (int i = 0; i < n; i++) {
+#pragma GCC unroll 4
+        for (int k = 0; k < M; k++) ZW_RAW_PUT((uint32_t)d[k][i], lo[k], ra[k], co[k], b[k], po[k], (*S[k]));
+    }
+#pragma GCC unroll 4
+    for (int k = 0; k < M; k++) S[k]->low = lo[k], S[k]->range = ra[k], S[k]->count = co[k], S[k]->pos = po[k];
+}
+
+// K (<= 4) streams of different lengths: interleaved over the common length,
+// then over the longer ones' remainders.
+inline void raw_code_multi(RawBool* const* S, const uint16_t* const* d, const int* n, int K)
+{
+    const uint16_t* dd[4];
+    int nn[4];
+    for (int k = 0; k < K; k++) dd[k] = d[k], nn[k] = n[k];
+    for (;;) {
+        RawBool* as[4];
+        const uint16_t* ad[4];
+        int ai[4], m = 0, mn = 1 << 30;
+        for (int k = 0; k < K; k++)
+            if (nn[k] > 0) {
+                as[m] = S[k];
+                ad[m] = dd[k];
+                ai[m++] = k;
+                mn = nn[k] < mn ? nn[k] : mn;
+            }
+        if (m == 0) return;
+        switch (m) {
+        case 4: raw_codeM<4>(as, ad, mn); break;
+        case 3: raw_codeM<3>(as, ad, mn); break;
+        case 2: raw_codeM<2>(as, ad, mn); break;
+        default: raw_codeM<1>(as, ad, mn); break;
+        }
+        for (int j = 0; j < m; j++) dd[ai[j]] += mn, nn[ai[j]] -= mn;
+    }
+}
+
+// The token tree paths as decision templates: per (after-a-zero, token) the
+// decisions bit << 8 | probability index, padded to 12 with index 0.
+struct TokTmpl {
+    uint8_t n[2][12];
+    uint16_t d[2][12][12];
+    TokTmpl()
+    {
+        const TokenPaths& TP = token_paths();
+        for (int s = 0; s < 2; s++)
+            for (int v = 0; v < 12; v++) {
+                n[s][v] = TP.n[s][v];
+                for (int i = 0; i < 12; i++)
+                    d[s][v][i] = i < TP.n[s][v] ? (uint16_t)((TP.bits[s][v][i] << 8) | TP.pidx[s][v][i]) : 0;
+            }
+    }
+};
+inline const TokTmpl& tok_tmpl()
+{
+    static const TokTmpl T;
+    return T;
+}
+
+// emit_block's decisions (the same sequence) recorded at o.
+inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first,
+                     int ctx)
+{
+    if (eobi <= first) {  // no coefficient: the end of block at `first` (bit 0)
+        *o++ = P[COEFF_BANDS[first]][ctx][0];
+        return eobi > 0;
+    }
+    int s = 0;
+    uint16_t* q = o;
+    for (int idx = first; idx < eobi; idx++) {
+        const int coeff = lv_at(lv, idx);
+        const uint8_t* pr = P[COEFF_BANDS[idx]][ctx];
+        const int a = coeff < 0 ? -coeff : coeff;
+        const int token = token_of(a);
+        const uint16_t* t = TT.d[s][token];
+        const int n = TT.n[s][token];
+        // the first three decisions unconditionally (paths of tokens 0 and 1
+        // are at most three long), the rest of longer paths after
+        q[0] = (uint16_t)((t[0] & 0xff00u) | pr[t[0] & 0xffu]);
+        q[1] = (uint16_t)((t[1] & 0xff00u) | pr[t[1] & 0xffu]);
+        q[2] = (uint16_t)((t[2] & 0xff00u) | pr[t[2] & 0xffu]);
+        if (n > 3)
+            for (int i = 3; i < n; i++) q[i] = (uint16_t)((t[i] & 0xff00u) | pr[t[i] & 0xffu]);
+        q += n;
+        if (token >= 5) {
+            const uint8_t* cp = PROB_DCT_CAT[token - 5];
+            const int extra = a - DCT_CAT_BASE[token - 5];
+            int mask = token == 10 ? 1 << 10 : 1 << (token - 5);
+            for (int k = 0; k < 12 && cp[k]; k++) {
+                *q++ = (uint16_t)(cp[k] | ((extra & mask) ? 0x100 : 0));
+                mask >>= 1;
+            }
+        }
+        if (token != 0) *q++ = (uint16_t)(128 | (coeff < 0 ? 0x100 : 0));
+        s = token == 0;
+        ctx = token == 0 ? 0 : (token == 1 ? 1 : 2);
+    }
+    if (eobi < 16) *q++ = P[COEFF_BANDS[eobi]][ctx][0];
+    o = q;
+    return 1;
+}
+
+// emit_mb_tokens' decisions (rec_block per block), the same contexts.
+inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
+{
+    const TokTmpl& TT = tok_tmpl();
+    const bool i4 = m.luma == 4;
+    if (m.skip) {
+        left.clear(!i4);
+        top.clear(!i4);
+        return;
+    }
+    const int plane = i4 ? 3 : 0;
+    if (!i4) {
+        const int hc = rec_block(o, TT, probs[1], m.lv[16], m.eob[16], 0, left.y2 + top.y2);
+        left.y2 = top.y2 = (uint8_t)hc;
+    }
+    const int first = i4 ? 0 : 1;
+    for (int by = 0; by < 4; by++) {
+        int l = left.y[by];
+        for (int bx = 0; bx < 4; bx++) {
+            const int b = by * 4 + bx;
+            const int hc = rec_block(o, TT, probs[plane], m.lv[b], m.eob[b], first, l + top.y[bx]);
+            l = hc;
+            top.y[bx] = (uint8_t)hc;
+        }
+        left.y[by] = (uint8_t)l;
+    }
+    for (int pl = 0; pl < 2; pl++) {
+        uint8_t* lc = pl ? left.v : left.u;
+        uint8_t* tc = pl ? top.v : top.u;
+        for (int by = 0; by < 2; by++) {
+            int l = lc[by];
+            for (int bx = 0; bx < 2; bx++) {
+                const int b = 17 + 4 * pl + by * 2 + bx;
+                const int hc = rec_block(o, TT, probs[2], m.lv[b], m.eob[b], 0, l + tc[bx]);
+                l = hc;
+                tc[bx] = (uint8_t)hc;
+            }
+            lc[by] = (uint8_t)l;
+        }
+    }
+}
+
+inline void assemble_frame1(std::vector<uint8_t>& out, const RawBool& H, const RawBool& T, int width, int height)
+{
+    const size_t hs = H.size(), ts = T.size();
+    out.resize(10 + hs + ts);
+    uint8_t* o = out.data();
+    const uint32_t tag = ((uint32_t)hs << 5) | (1u << 4);
+    o[0] = (uint8_t)tag;
+    o[1] = (uint8_t)(tag >> 8);
+    o[2] = (uint8_t)(tag >> 16);
+    o[3] = 0x9d;
+    o[4] = 0x01;
+    o[5] = 0x2a;
+    o[6] = (uint8_t)(width & 0xff);
+    o[7] = (uint8_t)((width >> 8) & 0x3f);
+    o[8] = (uint8_t)(height & 0xff);
+    o[9] = (uint8_t)((height >> 8) & 0x3f);
+    memcpy(o + 10, H.data(), hs);
+    memcpy(o + 10 + hs, T.data(), ts);
+}
+
+// emit_frame of K (1..4) frames of one size at once (one token partition):
+// each MB row's header and token decisions are recorded per frame, then the
+// K frames' coders run interleaved.  Byte-identical to emit_frame per frame.
+inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
+                        int K, int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11])
+{
+    struct Fr {
+        std::vector<uint16_t> hd, td;
+        RawBool H, T;
+        std::vector<Cplx> top;
+        std::vector<uint8_t> top_bp;
+        uint8_t probs[4][8][3][11];
+    };
+    thread_local Fr F[4];
+    const int mbw = P[0]->mbw, mbh = P[0]->mbh;
+    const uint8_t* q[4];
+    for (int k = 0; k < K; k++) {
+        Fr& f = F[k];
+        for (RawBool* r : {&f.H, &f.T}) {
+            r->lo = r->pos = 1;
+            r->low = 0;
+            r->range = 255;
+            r->count = -24;
+        }
+        f.T.reserve_more((size_t)mbw * mbh * 16 + 4096);
+        f.top.assign(mbw, Cplx{});
+        f.top_bp.assign((size_t)mbw * 4, 0);
+        // the frame header's decisions (at most 4 x 8 x 3 x 11 x 9 probability
+        // updates and ~100 others), then the MB headers' (whole frame; at most
+        // 2 + 1 + 4 + 16 x 9 + 3 per MB)
+        const size_t hcap = 4 * 8 * 3 * 11 * 9 + 256 + (size_t)mbw * mbh * 160;
+        if (f.hd.size() < hcap) f.hd.resize(hcap);
+        DecRec R{f.hd.data()};
+        emit_frame_header(R, *P[k], have_updated[k], upd[k], 1, f.probs);
+        q[k] = packed[k];
+        f.H.pos = (size_t)(R.p - f.hd.data());  // (decisions so far, until coded)
+    }
+    const size_t tcap = (size_t)mbw * kMbDecisionsMax;
+    for (int y = 0; y < mbh; y++) {
+        const uint16_t* td[4] = {};
+        int tn[4] = {};
+        RawBool* ts[4] = {};
+        for (int k = 0; k < K; k++) {
+            Fr& f = F[k];
+            if (f.td.size() < tcap) f.td.resize(tcap);
+            Cplx left;
+            memset(&left, 0, sizeof left);
+            uint8_t left_bp[4] = {0, 0, 0, 0};
+            DecRec R{f.hd.data() + f.H.pos};
+            uint16_t* o = f.td.data();
+            for (int x = 0; x < mbw; x++) {
+                PackedMb m;
+                q[k] = view_mb(q[k], m);
+                emit_mb_header(R, *P[k], m, f.top_bp.data(), left_bp, x);
+                rec_mb_tokens(o, f.probs, m, left, f.top[x]);
+            }
+            f.H.pos = (size_t)(R.p - f.hd.data());
+            td[k] = f.td.data();
+            tn[k] = (int)(o - f.td.data());
+            ts[k] = &f.T;
+        }
+        raw_code_multi(ts, td, tn, K);
+    }
+    // the header partitions
+    const uint16_t* hd[4] = {};
+    int hn[4] = {};
+    RawBool* hs[4] = {};
+    for (int k = 0; k < K; k++) {
+        hd[k] = F[k].hd.data();
+        hn[k] = (int)F[k].H.pos;
+        F[k].H.pos = 1;
+        hs[k] = &F[k].H;
+    }
+    raw_code_multi(hs, hd, hn, K);
+    for (int k = 0; k < K; k++) {
+        F[k].H.flush();
+        F[k].T.flush();
+        assemble_frame1(*out[k], F[k].H, F[k].T, width, height);
+    }
 }
 
 // quality_to_quant_index (vp8.rs:37-55) with fast_math::cbrt/round (fast_math.rs:15-42).
