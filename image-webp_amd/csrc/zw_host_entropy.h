@@ -922,7 +922,9 @@ inline const TokTmpl& tok_tmpl()
     return T;
 }
 
-// emit_block's decisions (the same sequence) recorded at o.
+// emit_block's decisions (the same sequence) recorded at o.  (A branch-free
+// form -- whole padded templates, sign and end of block always written --
+// measured slower on the GPU box's host: 1.73 vs 1.20 ms per 1080p frame.)
 inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first,
                      int ctx)
 {

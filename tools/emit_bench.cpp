@@ -94,6 +94,33 @@ int main(int argc, char** argv)
         }
         nd = (size_t)(o - all.data());
     });
+    // the walk's parts: record parsing alone, + MB headers
+    volatile int sink = 0;
+    const double t_view = best_ms(reps, [&] {
+        zwh::PackedMb m;
+        const uint8_t* q = rec.data();
+        int acc = 0;
+        for (int i = 0; i < P.mbw * P.mbh; i++) {
+            q = zwh::view_mb(q, m);
+            acc += m.eob[3];
+        }
+        sink = acc;
+    });
+    const double t_hdr = best_ms(reps, [&] {
+        zwh::PackedMb m;
+        zwh::DecRec H{hd.data()};
+        std::vector<uint8_t> top_bp((size_t)P.mbw * 4, 0);
+        const uint8_t* q = rec.data();
+        for (int y = 0; y < P.mbh; y++) {
+            uint8_t left_bp[4] = {0, 0, 0, 0};
+            for (int x = 0; x < P.mbw; x++) {
+                q = zwh::view_mb(q, m);
+                zwh::emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
+            }
+        }
+    });
+    printf("  walk parts: record views %.3f ms, + MB headers %.3f ms\n", t_view, t_hdr);
+    (void)sink;
     auto reset = [](zwh::RawBool& S) {
         S.lo = S.pos = 1;
         S.low = 0;
