@@ -3116,7 +3116,10 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     constexpr int NW = ROWS ? RowsShape<PASS>::NW : PassShape<PASS>::NW, WG = NW * 64;
     constexpr int NCH = PASS == 1 ? ChainShape<ROWS>::NCH : 0;  // chain waves (pass 1)
     constexpr bool PAIR = FP == 2;  // frame pairs: the workgroup encodes frames f and f + 1
-    static_assert(FP == 1 || (FP == 2 && PASS == 2 && !ROWS), "frame pairs: the batch pass-2 kernel");
+    static_assert(FP == 1 || (FP == 2 && !ROWS), "frame pairs: the batch kernels");
+    // pass 1's chroma chain waves: in frame pairs one per frame (the one-wave
+    // form), else NCH (the quad form's two waves in the row kernels)
+    constexpr int NCW = PASS == 1 ? (PAIR ? 2 : NCH) : 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int f = ROWS ? blockIdx.y : blockIdx.x * FP;
     const int nf = PAIR ? min(2, a.nframes - f) : 1;  // frames of this workgroup
@@ -3155,7 +3158,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
     WaveLds* W = (WaveLds*)((uint8_t*)Wall + ((sizeof(WaveLds) + 15) & ~(size_t)15) * wv);
     // row-parallel: is this workgroup pass 1's chroma chain (it keeps the
     // frame-wide top_u/v/derr in LDS), and the frame's global row state
-    const bool chain_wg = PASS == 1 && (ROWS ? blockIdx.x == 0 : wv < NCH);
+    const bool chain_wg = PASS == 1 && (ROWS ? blockIdx.x == 0 : wv < NCW);
     const RowsLayout RL(mbw, mbh);
     uint8_t* rb = ROWS ? a.rows + ZW_ROWS_HDR + (size_t)f * RL.frame : nullptr;
     int* rerr = ROWS ? (int*)a.rows : nullptr;
@@ -3245,8 +3248,27 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
 #define ZW_CHAIN_PRIO 3
 #endif
         __builtin_amdgcn_s_setprio(ZW_CHAIN_PRIO);
+        // frame pairs: chain wave k works frame f + k
+        const int cfr = PAIR ? wv : 0;
+        if (PAIR && cfr >= nf) {
+            ph_flush();
+            return;
+        }
+        const int fc = f + cfr;
+        const uint8_t* const lutc = seg_lut + 256 * cfr;
+        int8_t* const tdc = top_derr + TS.d * cfr;
+        if (PAIR) {
+            C.f = fc;
+            C.P = a.params + fc;
+            C.T = (const LdsTables*)((const uint8_t*)T + sT * cfr);
+            C.Sl = (const ZwSegment*)((const uint8_t*)Sl + sS * cfr);
+            C.top_u = top_u + TS.u * cfr;
+            C.top_v = top_v + TS.v * cfr;
+            C.top_derr = tdc;
+            C.method = __builtin_amdgcn_readfirstlane(C.P->method);
+        }
         if (lane < 4) C.M->left_derr[lane] = 0;
-        if (NCH == 2) {
+        if (NCH == 2 && !PAIR) {
             // quad form: wave 0 the U plane, wave 1 the V plane
             const int pl = wv;
             UvQ U;
@@ -3305,7 +3327,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
             ph_flush();
             return;
         }
-        MbFetch nx = fetch_mb(&a, f, lane, 0, 0);
+        MbFetch nx = fetch_mb(&a, fc, lane, 0, 0);
         for (int mby = 0; mby < mbh; mby++) {
             if (lane < 12) {
                 C.M->left_u[lane] = 129;
@@ -3317,25 +3339,25 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 const int lane = opaque_lane(threadIdx.x & 63);
                 C.lane = lane;
                 const MbFetch cur = nx;
-                if (mbx + 1 < mbw) nx = fetch_mb(&a, f, lane, mbx + 1, mby);
-                else if (mby + 1 < mbh) nx = fetch_mb(&a, f, lane, 0, mby + 1);
-                setup_ctx(C, &a, seg_lut, W, mbx, mby, cur);
+                if (mbx + 1 < mbw) nx = fetch_mb(&a, fc, lane, mbx + 1, mby);
+                else if (mby + 1 < mbh) nx = fetch_mb(&a, fc, lane, 0, mby + 1);
+                setup_ctx(C, &a, lutc, W, mbx, mby, cur);
                 C.oc = mbx * 8;
                 C.ocx = mbx * 12;
                 build_chroma_border(C);
                 const int cm = pick_uv<PASS>(C);
                 PH_MARK(8);
                 int uvnz[8];
-                final_chroma(C, cm, top_derr + mbx * 4, uvnz);
+                final_chroma(C, cm, tdc + mbx * 4, uvnz);
                 PH_MARK(9);
                 store_chroma_borders(C);
-                ZwMbOut* o = a.out + (size_t)f * nmb + (size_t)mby * mbw + mbx;
+                ZwMbOut* o = a.out + (size_t)fc * nmb + (size_t)mby * mbw + mbx;
                 if (lane == 0) o->chroma_mode = (uint8_t)cm;
                 write_levels(C, 17, 8, false);
                 wsync();
             }
         }
-        for (int i = lane; i < mbw * 4; i += 64) a.derr[(size_t)f * mbw * 4 + i] = top_derr[i];
+        for (int i = lane; i < mbw * 4; i += 64) a.derr[(size_t)fc * mbw * 4 + i] = tdc[i];
         ph_flush();
         return;
     }
@@ -3507,11 +3529,13 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
         const int K = C.method <= 3 ? 3 : (C.method == 4 ? 4 : 10);
         // per-frame encoder settings (a launch's frames normally share them)
         const int meth1 = nf == 2 ? __builtin_amdgcn_readfirstlane(a.params[f + 1].method) : C.method;
-        const bool trel1 = nf == 2 && __builtin_amdgcn_readfirstlane(a.params[f + 1].do_trellis);
-        const bool keep1 = !trel1 && a.dbg == nullptr;
+        const bool trel1 = PASS == 2 && nf == 2 && __builtin_amdgcn_readfirstlane(a.params[f + 1].do_trellis);
+        const bool keep1 = !trel1 && (PASS == 1 || a.dbg == nullptr);
+        // the luma waves (pass 1: after the chain waves) take the rows in turn
+        constexpr int NL = NW - NCW;
         const bool same_k = nf == 1 || (meth1 == C.method && trel1 == trel);
         for (int it = 0;; it++) {
-            const int mby = wv + it * NW;
+            const int mby = (wv - NCW) + it * NL;
             if (mby >= mbh) break;
 #pragma unroll
             for (int fr = 0; fr < 2; fr++) {
@@ -3524,7 +3548,7 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                 if (lane < 4) M->left_derr[lane] = 0;
             }
             wsync();
-            const int prevw = mby > 0 ? (mby - 1) % NW : 0;
+            const int prevw = mby > 0 ? NCW + (mby - 1) % NL : 0;
             auto wait_above = [&](int need) {
                 if (mby > 0) wait_row(progress, prevw, (mby - 1) * 65536 + need);
             };
@@ -3568,8 +3592,9 @@ __device__ __forceinline__ void encode_body(const EncArgs& a)
                             __hip_atomic_load(&progress[prevw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                         if ((v >> 16) == mby - 1) slack = (v & 0xffff) - mbx - 1;
                     }
-                    constexpr int dp = ZW_DYN_PRIO;
-                    set_prio(slack >= dp * 3 ? 3 : (slack >= dp * 2 ? 2 : (slack >= dp ? 1 : 0)));
+                    constexpr int dp = PASS == 1 ? ZW_DYN_PRIO1 : ZW_DYN_PRIO;
+                    const int pr_ = slack >= dp * 3 ? 3 : (slack >= dp * 2 ? 2 : (slack >= dp ? 1 : 0));
+                    set_prio(PASS == 1 ? min(pr_, ZW_P1_LUMA_MAX) : pr_);
                 }
 #endif
                 PH_MARK(0);
@@ -3649,8 +3674,11 @@ ZW_PAIR_LOOP
                     const uint32_t sm = pst(fr, 0), r4 = pst(fr, 3);
                     C.seg = (int)(sm >> 8);
                     C.S = C.Sl + C.seg;
-                    build_chroma_border(C);
-                    const int cm = pick_uv<PASS>(C);
+                    int cm = 0;  // (pass 1: the chain waves work the chroma)
+                    if (PASS == 2) {
+                        build_chroma_border(C);
+                        cm = pick_uv<PASS>(C);
+                    }
                     PH_MARK(3);
                     const bool w4 = (r4 >> 16) & 1u;
                     mb_store(C, w4 ? 4 : (int)(sm & 15u), cm, w4 && (fr ? keep1 : keep_i4), r4 & 0xffffu,
@@ -3830,6 +3858,7 @@ ZW_PAIR_LOOP
 }
 
 extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1(EncArgs a) { encode_body<1, false>(a); }
+extern "C" __global__ __launch_bounds__(PassShape<1>::WG) void k_encode_pass1_fp(EncArgs a) { encode_body<1, false, 2>(a); }
 extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2(EncArgs a) { encode_body<2, false>(a); }
 extern "C" __global__ __launch_bounds__(PassShape<2>::WG) void k_encode_pass2_fp(EncArgs a) { encode_body<2, false, 2>(a); }
 extern "C" __global__ __launch_bounds__(64 * RowsShape<1>::NW) void k_encode_rows_pass1(EncArgs a) { encode_body<1, true>(a); }
@@ -3951,12 +3980,14 @@ static size_t encode_lds_bytes(int mbw, int nw, bool rows, int pass, int fp = 1)
     return off + (t.y + t.u + t.v + t.c + t.d) * fp;
 }
 
-// Pass 2 in frame pairs (k_encode_pass2_fp) for launches of at least two
-// frames per CU whose pair shape fits in LDS; ZW_ENC_FP=0/1 forces it off/on
-// (where it fits).
-static bool encode_fp_for(int mbw, int nframes)
+// Frame pairs (k_encode_pass1_fp / k_encode_pass2_fp) for launches of at
+// least two frames per CU whose pair shape fits in LDS; ZW_ENC_FP=0/1 forces
+// them off/on (where they fit), ZW_ENC_FP1 the same for pass 1 alone.
+static bool encode_fp_for(int pass, int mbw, int nframes)
 {
-    static const int mode = [] { const char* e = getenv("ZW_ENC_FP"); return e && *e ? atoi(e) : -1; }();
+    static const int mode2 = [] { const char* e = getenv("ZW_ENC_FP"); return e && *e ? atoi(e) : -1; }();
+    static const int mode1 = [] { const char* e = getenv("ZW_ENC_FP1"); return e && *e ? atoi(e) : mode2; }();
+    const int mode = pass == 1 ? mode1 : mode2;
     static const int cus = [] {
         int dev = 0;
         hipDeviceProp_t prop;
@@ -3966,10 +3997,10 @@ static bool encode_fp_for(int mbw, int nframes)
                    : 256;
     }();
     if (mode == 0 || nframes < 2) return false;
-    if (encode_lds_bytes(mbw, PassShape<2>::NW, false, 2, 2) > 160 * 1024) return false;
+    if (encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW, false, pass, 2) > 160 * 1024) return false;
     return mode == 1 || nframes >= 2 * cus;
 }
-extern "C" int zwk_encode_fp(int mbw, int nframes) { return encode_fp_for(mbw, nframes) ? 1 : 0; }
+extern "C" int zwk_encode_fp(int pass, int mbw, int nframes) { return encode_fp_for(pass, mbw, nframes) ? 1 : 0; }
 
 
 // ---------------------------------------------------------------------------
@@ -4065,6 +4096,7 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
         (void)hipFuncSetAttribute((const void*)k_encode_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_pass2_fp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode_pass1_fp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_rows_pass1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_encode_rows_pass2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
@@ -4082,9 +4114,13 @@ extern "C" hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, cons
         }
         return hipGetLastError();
     }
-    if (pass == 2 && encode_fp_for(mbw, nframes)) {
-        hipLaunchKernelGGL(k_encode_pass2_fp, dim3((nframes + 1) / 2), dim3(PassShape<2>::WG),
-                           encode_lds_bytes(mbw, PassShape<2>::NW, false, 2, 2), s, a);
+    if (encode_fp_for(pass, mbw, nframes)) {
+        if (pass == 1)
+            hipLaunchKernelGGL(k_encode_pass1_fp, dim3((nframes + 1) / 2), dim3(PassShape<1>::WG),
+                               encode_lds_bytes(mbw, PassShape<1>::NW, false, 1, 2), s, a);
+        else
+            hipLaunchKernelGGL(k_encode_pass2_fp, dim3((nframes + 1) / 2), dim3(PassShape<2>::WG),
+                               encode_lds_bytes(mbw, PassShape<2>::NW, false, 2, 2), s, a);
         return hipGetLastError();
     }
     const size_t lds = encode_lds_bytes(mbw, pass == 1 ? PassShape<1>::NW : PassShape<2>::NW, false, pass);

@@ -13,6 +13,9 @@
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <condition_variable>
 #include <mutex>
 #include <cstdio>
@@ -57,7 +60,7 @@ hipError_t zwk_encode(hipStream_t s, int pass, const uint8_t* Y, const uint8_t* 
                       int nframes, int* dbg, uint8_t* rows, uint32_t* sizes = nullptr);
 size_t zwk_encode_rows_bytes(int mbw, int mbh, int nframes);
 int zwk_encode_max_mbw(int rows);
-int zwk_encode_fp(int mbw, int nframes);
+int zwk_encode_fp(int pass, int mbw, int nframes);
 }
 
 extern "C" const char* zw_strerror(int code)
@@ -488,7 +491,10 @@ struct PipeLane {
     hipEvent_t ev[8] = {};
     unsigned long long* d_ctr = nullptr;
     uint8_t* d_rows = nullptr;  // row-parallel encode scratch (small chunks), else null
-    FetchBuf fb[2];  // [0] pass-1 records (host stats replay), [1] pass-2 records (emission thread)
+    // [0] pass-1 records (host stats replay), [1], [2] pass-2 records of the
+    // emission thread (chunk c in fb[1 + (c & 1)]: with pass 2 of two chunks in
+    // one launch, both are copied out before either is emitted)
+    FetchBuf fb[3];
     Pinned<ZwStatsOut> h_stats;          // [chunk] pass-1 statistics from k_stats
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
@@ -497,6 +503,8 @@ struct PipeLane {
     // pass 2 in one launch, pass 1 and the statistics stay per chunk.
     bool pair2 = false;
     int p2_frames = 0;  // frames of the timed pass-2 launch (kms[3] is scaled to one chunk)
+    bool pair1 = false;  // the same for pass 1 (k_encode_pass1_fp)
+    int p1_frames = 0;
     int rc = 0;
     // Host-source streaming (zw_pipe_encode_host): the lane's uploader thread
     // copies batch b's frames into input buffer b & 1 on `ustream`, one event
@@ -562,6 +570,16 @@ struct zw_pipe {
     std::vector<const uint8_t*> host_frames;
     int nparts = 1;  // token partitions per frame (zw_pipe_set_token_partitions)
     std::vector<PipeLane> lanes;
+    // Cross-lane order of the pass-1 launches (lane_encode, ZW_P1_ORDER): lane
+    // g's pass 1 of a batch waits for lane g - 1's statistics kernels of that
+    // batch (lane 0: of the previous batch).  Otherwise a lane's statistics,
+    // queued behind its own pass 1, wait for CUs until the other lane's whole
+    // pass-1 launch ends, and its pass 2 after them (measured: ~30 ms of idle
+    // GPU a step).  p1_stats[g]: batches whose statistics lane g has queued
+    // (its event L.ev[6] recorded after them); INT64_MAX once the lane stopped.
+    std::mutex p1_mu;
+    std::condition_variable p1_cv;
+    std::vector<long long> p1_stats;
     float kms[8];
     // Set when a run stops partway: k_segments' histograms and k_pack_scan's
     // counters, which the kernels clear themselves, may then be left nonzero,
@@ -591,8 +609,7 @@ static void pipe_free(zw_pipe* p)
     for (PipeLane& L : p->lanes) {
         if (L.d_ctr) (void)hipFree(L.d_ctr);
         if (L.d_rows) (void)hipFree(L.d_rows);
-        L.fb[0].release();
-        L.fb[1].release();
+        for (FetchBuf& b : L.fb) b.release();
         for (int i = 0; i < 8; i++)
             if (L.ev[i]) (void)hipEventDestroy(L.ev[i]);
         for (hipEvent_t e : L.cev)
@@ -742,8 +759,8 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
         L.f0 = (int)((long long)n * g / G);
         L.n = (int)((long long)n * (g + 1) / G) - L.f0;
         L.chunk = pipe_chunk_for(L.n, ctx->device);
-        ok = L.fb[0].finfo.alloc(2 * (size_t)L.chunk) && L.fb[1].finfo.alloc(2 * (size_t)L.chunk) &&
-             L.fb[0].total.alloc(1) && L.fb[1].total.alloc(1) && (p->host_stats || L.h_stats.alloc((size_t)L.n));
+        for (FetchBuf& b : L.fb) ok = ok && b.finfo.alloc(2 * (size_t)L.chunk) && b.total.alloc(1);
+        ok = ok && (p->host_stats || L.h_stats.alloc((size_t)L.n));
         const int nch = (L.n + L.chunk - 1) / L.chunk;
         L.cev.assign(2 * (size_t)nch, nullptr);
         ok = ok && hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) == hipSuccess &&
@@ -758,7 +775,8 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
             if (ok && getenv("ZW_ENC_FORCE_ERROR")) ok = hipMemset(L.d_rows, 1, 1) == hipSuccess;
         }
         // pass 2 of chunks (2k, 2k + 1) in one launch where it runs in frame pairs
-        L.pair2 = ok && !L.d_rows && nch >= 2 && zwk_encode_fp(p->mbw, 2 * L.chunk);
+        L.pair2 = ok && !L.d_rows && nch >= 2 && zwk_encode_fp(2, p->mbw, 2 * L.chunk);
+        L.pair1 = ok && !L.d_rows && nch >= 2 && zwk_encode_fp(1, p->mbw, 2 * L.chunk);
         for (int i = 0; ok && i < 8; i++) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
         for (size_t i = 0; ok && i < L.cev.size(); i++)
             ok = hipEventCreateWithFlags(&L.cev[i], hipEventDisableTiming) == hipSuccess;
@@ -862,8 +880,28 @@ static int rows_check(zw_pipe* p, PipeLane& L)
 }
 
 // ---- per-chunk stages (frames [fa, fa + na) of a lane) ----
+// Pass 1 of frames [fa, fa + na): the encode launch alone (chunk_pass1 queues
+// the steps before it; a paired lane launches two chunks' pass 1 at once).
+static int chunk_pass1_encode(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false)
+{
+    hipStream_t s = L.stream;
+    const size_t F = (size_t)fa;
+    if (timed) {
+        HIPOK(hipEventRecord(L.ev[2], s));
+        L.p1_frames = na;
+    }
+    HIPOK(rows_reset(p, L, na));
+    HIPOK(zwk_encode(s, 1, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
+                     p->d_params + F, nullptr, p->d_derr + F * p->mbw * 4, p->d_out1 + F * p->nmb,
+                     write_recon ? p->d_ry + F * p->ysz : nullptr, write_recon ? p->d_ru + F * p->csz : nullptr,
+                     write_recon ? p->d_rv + F * p->csz : nullptr, p->ysz, p->csz, p->mbw, p->mbh, na, nullptr,
+                     L.d_rows));
+    if (timed) HIPOK(hipEventRecord(L.ev[3], s));
+    return ZW_OK;
+}
+
 static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool write_recon = false,
-                       int parity = 0, hipEvent_t uploaded = nullptr, hipEvent_t read = nullptr)
+                       int parity = 0, hipEvent_t uploaded = nullptr, hipEvent_t read = nullptr, bool encode = true)
 {
     hipStream_t s = L.stream;
     const size_t F = (size_t)fa;
@@ -879,15 +917,8 @@ static int chunk_pass1(zw_pipe* p, PipeLane& L, int fa, int na, bool timed, bool
     HIPOK(zwk_analysis(s, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->mbw, p->mbh, p->ysz,
                        p->csz, p->d_alpha + F * p->nmb, p->d_histo + F * 256, n));
     HIPOK(zwk_segments(s, p->d_histo + F * 256, p->d_tmpl, p->d_params + F, n));
-    if (timed) HIPOK(hipEventRecord(L.ev[2], s));
-    HIPOK(rows_reset(p, L, n));
-    HIPOK(zwk_encode(s, 1, p->d_Y + F * p->ysz, p->d_U + F * p->csz, p->d_V + F * p->csz, p->d_alpha + F * p->nmb,
-                     p->d_params + F, nullptr, p->d_derr + F * p->mbw * 4, p->d_out1 + F * p->nmb,
-                     write_recon ? p->d_ry + F * p->ysz : nullptr, write_recon ? p->d_ru + F * p->csz : nullptr,
-                     write_recon ? p->d_rv + F * p->csz : nullptr, p->ysz, p->csz, p->mbw, p->mbh, n, nullptr,
-                     L.d_rows));
-    if (timed) HIPOK(hipEventRecord(L.ev[3], s));
-    return ZW_OK;
+    if (!encode) return ZW_OK;
+    return chunk_pass1_encode(p, L, fa, na, timed, write_recon);
 }
 
 // Pass 2 writes each MB's packed record size (EncArgs::sizes), so packing
@@ -1038,11 +1069,10 @@ static void dump_emit_input(zw_pipe* p, const uint8_t* rec, size_t bytes, size_t
     fclose(fp);
 }
 
-static int chunk_emit(zw_pipe* p, PipeLane& L, int fa, int na, int par)
+static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
-    const FetchBuf& B = L.fb[1];
     if (fa == 0) dump_emit_input(p, B.pack + B.finfo[0], (size_t)B.finfo[1], hidx(p, par, 0));
     std::atomic<int> err{ZW_OK};
     // One token partition (the default): the frames go out in groups of up to
@@ -1107,7 +1137,8 @@ static void lane_times(PipeLane& L)
     for (int i = 0; i < 4; i++) L.kms[i] = 0.f;
     (void)hipEventElapsedTime(&L.kms[0], L.ev[0], L.ev[1]);  // rgb2yuv
     (void)hipEventElapsedTime(&L.kms[1], L.ev[1], L.ev[2]);  // analysis + segments
-    (void)hipEventElapsedTime(&L.kms[2], L.ev[2], L.ev[3]);  // pass 1
+    (void)hipEventElapsedTime(&L.kms[2], L.ev[2], L.ev[3]);  // pass 1 (per chunk of frames)
+    if (L.p1_frames > 0 && L.p1_frames != L.chunk) L.kms[2] *= (float)L.chunk / (float)L.p1_frames;
     (void)hipEventElapsedTime(&L.kms[3], L.ev[4], L.ev[5]);  // pass 2 (per chunk of frames)
     if (L.p2_frames > 0 && L.p2_frames != L.chunk) L.kms[3] *= (float)L.chunk / (float)L.p2_frames;
 }
@@ -1134,46 +1165,101 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     const bool host = p->host_src != nullptr;
     const long long FAILED = std::numeric_limits<long long>::max();
     int qb = 0;  // batch whose pass 1 queue_pass1 queues next
+    // cross-lane order of the pass-1 launches (zw_pipe::p1_stats)
+    static const bool p1_order_env = [] { const char* e = getenv("ZW_P1_ORDER"); return !e || atoi(e) != 0; }();
+    const int G = (int)p->lanes.size();
+    const int lane_id = (int)(&L - p->lanes.data());
+    const bool p1_order = p1_order_env && G > 1 && emit;
+    struct OrderGuard {  // a lane that stops releases the lanes waiting on it
+        zw_pipe* p;
+        int g;
+        bool on;
+        ~OrderGuard()
+        {
+            if (!on) return;
+            {
+                std::lock_guard<std::mutex> lk(p->p1_mu);
+                p->p1_stats[g] = std::numeric_limits<long long>::max();
+            }
+            p->p1_cv.notify_all();
+        }
+    } order_guard{p, lane_id, p1_order};
+    auto p1_order_wait = [&](int b) -> int {
+        if (!p1_order) return ZW_OK;
+        const int prev = (lane_id + G - 1) % G;
+        const long long need = lane_id == 0 ? b : b + 1;
+        if (need <= 0) return ZW_OK;
+        {
+            std::unique_lock<std::mutex> lk(p->p1_mu);
+            p->p1_cv.wait(lk, [&] { return p->p1_stats[prev] >= need; });
+            if (p->p1_stats[prev] == std::numeric_limits<long long>::max()) return ZW_OK;  // (it stopped)
+        }
+        HIPOK(hipStreamWaitEvent(L.stream, p->lanes[prev].ev[6], 0));
+        return ZW_OK;
+    };
     auto queue_pass1 = [&]() -> int {
         const int b = qb++;
         for (int c = 0; c < nch; c++) {
-            hipEvent_t ue = nullptr, re = nullptr;
-            if (host) {  // wait until every uploader has issued its copies of this chunk
-                std::unique_lock<std::mutex> lk(L.sync->mu);
-                const long long need = (long long)b * nch + c + 1;
-                L.sync->cv.wait(lk, [&] {
+            // pass 1 of chunk c alone, or of chunks c and c + 1 in one launch (pair1)
+            const int c1 = (L.pair1 && (c & 1) == 0 && c + 1 < nch) ? c + 1 : c;
+            int r = ZW_OK;
+            for (int k = c; k <= c1 && !r; k++) {
+                hipEvent_t ue = nullptr, re = nullptr;
+                if (host) {  // wait until every uploader has issued its copies of this chunk
+                    std::unique_lock<std::mutex> lk(L.sync->mu);
+                    const long long need = (long long)b * nch + k + 1;
+                    L.sync->cv.wait(lk, [&] {
+                        for (long long u : L.uploaded)
+                            if (u < need) return false;
+                        return true;
+                    });
                     for (long long u : L.uploaded)
-                        if (u < need) return false;
-                    return true;
-                });
-                for (long long u : L.uploaded)
-                    if (u == FAILED) return ZW_EDEVICE;
-                lk.unlock();
-                for (size_t u = 1; u < L.ustreams.size(); u++)
-                    HIPOK(hipStreamWaitEvent(L.stream, L.uev[b & 1][u * nch + c], 0));
-                ue = L.uev[b & 1][c];
-                re = L.rev[b & 1][c];
-            }
-            int r = chunk_pass1(p, L, ca(c), cn(c), c == 0, false, host ? (b & 1) : 0, ue, re);
-            if (host) {
-                {
-                    std::lock_guard<std::mutex> lk(L.sync->mu);
-                    L.p1_queued = r ? FAILED : L.p1_queued + 1;
+                        if (u == FAILED) return ZW_EDEVICE;
+                    lk.unlock();
+                    for (size_t u = 1; u < L.ustreams.size(); u++)
+                        HIPOK(hipStreamWaitEvent(L.stream, L.uev[b & 1][u * nch + k], 0));
+                    ue = L.uev[b & 1][k];
+                    re = L.rev[b & 1][k];
                 }
-                L.sync->cv.notify_all();
+                // (the pre-pass kernels; an unpaired chunk also its pass 1, after the
+                // cross-lane wait below for chunk 0)
+                const bool enc = c1 == c && !(k == 0 && p1_order);
+                r = chunk_pass1(p, L, ca(k), cn(k), k == 0, false, host ? (b & 1) : 0, ue, re, enc);
+                if (!r && c1 == c && !enc) {
+                    r = p1_order_wait(b);
+                    if (!r) r = chunk_pass1_encode(p, L, ca(k), cn(k), k == 0);
+                }
+                if (host) {
+                    {
+                        std::lock_guard<std::mutex> lk(L.sync->mu);
+                        L.p1_queued = r ? FAILED : L.p1_queued + 1;
+                    }
+                    L.sync->cv.notify_all();
+                }
             }
-            if (!r) {
+            if (!r && c == 0 && c1 != c) r = p1_order_wait(b);
+            if (!r && c1 != c) r = chunk_pass1_encode(p, L, ca(c), ca(c1) + cn(c1) - ca(c), c == 0);
+            for (int k = c; k <= c1 && !r; k++) {
                 if (p->host_stats) {
-                    r = chunk_pack(p, L, ca(c), cn(c), p->d_out1, 2 * c);
+                    r = chunk_pack(p, L, ca(k), cn(k), p->d_out1, 2 * k);
                 } else {
-                    const size_t F = (size_t)ca(c);
+                    const size_t F = (size_t)ca(k);
                     HIPOK(zwk_stats(L.stream, p->d_out1 + F * p->nmb, p->mbw, p->mbh,
                                     (uint8_t*)p->d_stats_tmp + zw_stats_scratch_bytes(p->nmb, (int)F),
-                                    p->d_stats + F, cn(c)));
+                                    p->d_stats + F, cn(k)));
                 }
+                if (!r) HIPOK(hipEventRecord(L.cev[2 * k], L.stream));
             }
             if (r) return r;
-            HIPOK(hipEventRecord(L.cev[2 * c], L.stream));
+            c = c1;
+        }
+        if (p1_order) {  // this batch's statistics are queued: the next lane's pass 1 may follow
+            HIPOK(hipEventRecord(L.ev[6], L.stream));
+            {
+                std::lock_guard<std::mutex> lk(p->p1_mu);
+                p->p1_stats[lane_id] = b + 1;
+            }
+            p->p1_cv.notify_all();
         }
         return ZW_OK;
     };
@@ -1277,32 +1363,39 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     // emission of batch b (runs on `em`)
     auto emitter = [&](int b) {
         for (int c = 0; c < nch; c++) {
+            // the chunks of one pass-2 launch: copied out first (pass 2 of the
+            // next batch may then reuse their device buffers), then emitted
+            const int c1 = (L.pair2 && (c & 1) == 0 && c + 1 < nch) ? c + 1 : c;
             const double t0 = now_ms();
-            const int r = chunk_fetch(p, L, L.fb[1], ca(c), cn(c), 2 * c + 1, L.cev[2 * c + 1]);
-            {
-                std::lock_guard<std::mutex> lk(L.sync->mu);
-                L.sync->fetched = r ? FAILED : L.sync->fetched + 1;
-            }
-            L.sync->cv.notify_all();
-            if (r) {
-                emit_rc = r;
-                return;
-            }
-            const double t1 = now_ms();
-            if (const int re = chunk_emit(p, L, ca(c), cn(c), b & 1)) {
-                {  // the lane thread may wait for later chunks: release it
+            for (int k = c; k <= c1; k++) {
+                const int r = chunk_fetch(p, L, L.fb[1 + (k & 1)], ca(k), cn(k), 2 * k + 1, L.cev[2 * k + 1]);
+                {
                     std::lock_guard<std::mutex> lk(L.sync->mu);
-                    L.sync->fetched = FAILED;
+                    L.sync->fetched = r ? FAILED : L.sync->fetched + 1;
                 }
                 L.sync->cv.notify_all();
-                emit_rc = re;
-                return;
+                if (r) {
+                    emit_rc = r;
+                    return;
+                }
             }
+            const double t1 = now_ms();
+            for (int k = c; k <= c1; k++)
+                if (const int re = chunk_emit(p, L.fb[1 + (k & 1)], ca(k), cn(k), b & 1)) {
+                    {  // the lane thread may wait for later chunks: release it
+                        std::lock_guard<std::mutex> lk(L.sync->mu);
+                        L.sync->fetched = FAILED;
+                    }
+                    L.sync->cv.notify_all();
+                    emit_rc = re;
+                    return;
+                }
             tok += now_ms() - t1;
             fetch2 += t1 - t0;
             if (g_trace)
-                fprintf(stderr, "  lane %d batch %d chunk %d: p2 fetched %.1f emit done %.1f\n", L.f0, b, c,
+                fprintf(stderr, "  lane %d batch %d chunks %d-%d: p2 fetched %.1f emit done %.1f\n", L.f0, b, c, c1,
                         t1 - g_trace_t0, now_ms() - g_trace_t0);
+            c = c1;
         }
     };
     std::thread em;
@@ -1356,6 +1449,14 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
             if ((r = join_emitter())) return r;
             em = std::thread([&, b]() {
                 (void)hipSetDevice(p->ctx->device);
+                // Emission is throughput work beside the lanes' latency-critical
+                // steps (the statistics that release pass 2, the queueing): its
+                // thread and the workers it spawns (they inherit the nice value)
+                // yield the CPU to them.  Measured: the statistics of a chunk took
+                // up to 45 ms instead of ~2 behind two lanes' emission workers,
+                // with the GPU idle meanwhile.
+                static const int nice_em = [] { const char* e = getenv("ZW_EMIT_NICE"); return e ? atoi(e) : 5; }();
+                if (nice_em > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_em);
                 emitter(b);
             });
         }
@@ -1440,6 +1541,7 @@ static int pipe_encode(zw_pipe* p, int nb)
     const double T0 = now_ms();
     g_trace = trace;
     g_trace_t0 = T0;
+    p->p1_stats.assign(p->lanes.size(), 0);
     int r = run_lanes(p, [&](PipeLane& L) -> int {
         const int q = lane_encode(p, L, true, nb);
         if (trace)
