@@ -29,6 +29,17 @@
 #define ZW_NW2 12
 #endif
 #define NW_MAX (ZW_NW1 > ZW_NW2 ? ZW_NW1 : ZW_NW2)
+// Issue priority of a luma wave from its slack to the row above (encode_body):
+// slack (MBs) per priority level, 0: off; pass 1's level width and cap.
+#ifndef ZW_DYN_PRIO
+#define ZW_DYN_PRIO 1
+#endif
+#ifndef ZW_DYN_PRIO1
+#define ZW_DYN_PRIO1 2  // (1: 28.86, 2: 28.74 ms per 256 1080p frames, one-frame kernel)
+#endif
+#ifndef ZW_P1_LUMA_MAX
+#define ZW_P1_LUMA_MAX 3  // (2 kept the luma waves below the chroma chain: 0.7 % slower)
+#endif
 template <int PASS> struct PassShape {
     static constexpr int NW = PASS == 1 ? ZW_NW1 : ZW_NW2;
     static constexpr int WG = NW * 64;
@@ -3772,9 +3783,6 @@ ZW_PAIR_LOOP
                 C.ocx = mbx * 12;
                 C.od = mbx * 4;
             }
-#ifndef ZW_DYN_PRIO
-#define ZW_DYN_PRIO 1  // slack (MBs) per priority level; 0: off
-#endif
 #if ZW_DYN_PRIO > 0
             if (!ROWS) {
                 // Issue priority from the slack to the row above.  VALU issue is
@@ -3789,14 +3797,8 @@ ZW_PAIR_LOOP
                         __hip_atomic_load(&progress[prevw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                     if ((v >> 16) == mby - 1) slack = (v & 0xffff) - mbx - 1;
                 }
-#ifndef ZW_DYN_PRIO1
-#define ZW_DYN_PRIO1 2  // pass 1's slack per level (1: 28.86, 2: 28.74 ms per 256 1080p frames)
-#endif
                 constexpr int dp = PASS == 1 ? ZW_DYN_PRIO1 : ZW_DYN_PRIO;
                 const int p = slack >= dp * 3 ? 3 : (slack >= dp * 2 ? 2 : (slack >= dp ? 1 : 0));
-#ifndef ZW_P1_LUMA_MAX
-#define ZW_P1_LUMA_MAX 3  // pass 1: the luma waves' cap (2 kept them below the chroma chain: 0.7 % slower)
-#endif
                 set_prio(PASS == 1 ? min(p, ZW_P1_LUMA_MAX) : p);
             }
 #endif
