@@ -1126,9 +1126,11 @@ def main():
                 pipe.close()
             pipes = []
             s4 = [frame_seed(i) for i in range(4)]
-            # (8 pipelined batches each: a 2-batch leg measured mostly the pipeline's fill and drain)
-            line["config5_4k_n1"] = batch_leg(ctx, 3840, 2160, q, m, 256, 8, s4, digests)
-            line["config1_768x512_gpu"] = batch_leg(ctx, 768, 512, q, m, 256, 8, s4, digests)
+            # (8 pipelined batches each: a 2-batch leg measured mostly the pipeline's fill and
+            # drain; 512 frames a batch, so the passes run in frame pairs as in the headline:
+            # at 4K the leg is config 5's whole 4 096-frame job at N = 1)
+            line["config5_4k_n1"] = batch_leg(ctx, 3840, 2160, q, m, 512, 8, s4, digests)
+            line["config1_768x512_gpu"] = batch_leg(ctx, 768, 512, q, m, 512, 8, s4, digests)
             c5 = line["config5_4k_n1"]
             fpc = c5.get("host_emit_frames_per_s_per_core")
             line["host_budget"] = {

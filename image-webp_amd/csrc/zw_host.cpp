@@ -636,7 +636,7 @@ static void pipe_free(zw_pipe* p)
 // free start the other lane's work instead of idling until its slowest frame
 // ends (measured, 1024 1080p frames: 3 015 -> 3 087 encodes/s; three lanes no
 // better).  ZW_PIPE_LANES overrides.
-static int pipe_lanes_for(int n, int device)
+static int pipe_lanes_for(int n, int device, int mbw)
 {
     const char* e = getenv("ZW_PIPE_LANES");
     int g;
@@ -647,7 +647,10 @@ static int pipe_lanes_for(int n, int device)
         const int cus = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
                             ? prop.multiProcessorCount
                             : 256;
-        g = n >= 2 * cus ? 2 : 1;
+        // where the passes run in frame pairs a lane needs two chunks (two
+        // frames per CU) for them: a second lane only from four chunks
+        const bool fp = zwk_encode_fp(2, mbw, 2 * cus) != 0;
+        g = n >= (fp ? 4 : 2) * cus ? 2 : 1;
     }
     if (g < 1) g = 1;
     if (g > 16) g = 16;
@@ -752,7 +755,7 @@ extern "C" int zw_pipe_create(zw_ctx* ctx, int n, uint32_t width, uint32_t heigh
     p->host_stats = getenv("ZW_HOST_STATS") != nullptr;
     ok = ok && (p->host_stats || (hipMalloc(&p->d_stats, N * sizeof(ZwStatsOut)) == hipSuccess &&
                                   hipMalloc(&p->d_stats_tmp, zw_stats_scratch_bytes(p->nmb, n)) == hipSuccess));
-    const int G = pipe_lanes_for(n, ctx->device);
+    const int G = pipe_lanes_for(n, ctx->device, p->mbw);
     p->lanes.resize(G);
     for (int g = 0; ok && g < G; g++) {
         PipeLane& L = p->lanes[g];
