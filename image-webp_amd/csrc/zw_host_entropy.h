@@ -967,7 +967,10 @@ inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11],
     return 1;
 }
 
-// emit_mb_tokens' decisions (rec_block per block), the same contexts.
+// emit_mb_tokens' decisions (rec_block per block), the same contexts.  A
+// block's context bit is eob > 0 (what emit_block returns), so every block's
+// context is taken from the eobs up front: the blocks' walks do not wait on
+// each other.
 inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
 {
     const TokTmpl& TT = tok_tmpl();
@@ -978,34 +981,40 @@ inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const 
         return;
     }
     const int plane = i4 ? 3 : 0;
+    const uint8_t* e = m.eob;
     if (!i4) {
-        const int hc = rec_block(o, TT, probs[1], m.lv[16], m.eob[16], 0, left.y2 + top.y2);
-        left.y2 = top.y2 = (uint8_t)hc;
+        const int c = left.y2 + top.y2;
+        left.y2 = top.y2 = (uint8_t)(e[16] > 0);
+        rec_block(o, TT, probs[1], m.lv[16], e[16], 0, c);
     }
     const int first = i4 ? 0 : 1;
-    for (int by = 0; by < 4; by++) {
-        int l = left.y[by];
+    int ctx[16];
+    for (int by = 0; by < 4; by++)
         for (int bx = 0; bx < 4; bx++) {
             const int b = by * 4 + bx;
-            const int hc = rec_block(o, TT, probs[plane], m.lv[b], m.eob[b], first, l + top.y[bx]);
-            l = hc;
-            top.y[bx] = (uint8_t)hc;
+            const int l = bx ? (int)(e[b - 1] > 0) : left.y[by];
+            const int t = by ? (int)(e[b - 4] > 0) : top.y[bx];
+            ctx[b] = l + t;
         }
-        left.y[by] = (uint8_t)l;
+    for (int k = 0; k < 4; k++) {
+        left.y[k] = (uint8_t)(e[4 * k + 3] > 0);
+        top.y[k] = (uint8_t)(e[12 + k] > 0);
     }
+    for (int b = 0; b < 16; b++) rec_block(o, TT, probs[plane], m.lv[b], e[b], first, ctx[b]);
     for (int pl = 0; pl < 2; pl++) {
         uint8_t* lc = pl ? left.v : left.u;
         uint8_t* tc = pl ? top.v : top.u;
-        for (int by = 0; by < 2; by++) {
-            int l = lc[by];
-            for (int bx = 0; bx < 2; bx++) {
-                const int b = 17 + 4 * pl + by * 2 + bx;
-                const int hc = rec_block(o, TT, probs[2], m.lv[b], m.eob[b], 0, l + tc[bx]);
-                l = hc;
-                tc[bx] = (uint8_t)hc;
-            }
-            lc[by] = (uint8_t)l;
-        }
+        const int b0 = 17 + 4 * pl;
+        const int c0 = lc[0] + tc[0], c1 = (e[b0] > 0) + tc[1], c2 = lc[1] + (e[b0] > 0),
+                  c3 = (e[b0 + 2] > 0) + (e[b0 + 1] > 0);
+        lc[0] = (uint8_t)(e[b0 + 1] > 0);
+        lc[1] = (uint8_t)(e[b0 + 3] > 0);
+        tc[0] = (uint8_t)(e[b0 + 2] > 0);
+        tc[1] = (uint8_t)(e[b0 + 3] > 0);
+        rec_block(o, TT, probs[2], m.lv[b0], e[b0], 0, c0);
+        rec_block(o, TT, probs[2], m.lv[b0 + 1], e[b0 + 1], 0, c1);
+        rec_block(o, TT, probs[2], m.lv[b0 + 2], e[b0 + 2], 0, c2);
+        rec_block(o, TT, probs[2], m.lv[b0 + 3], e[b0 + 3], 0, c3);
     }
 }
 
