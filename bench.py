@@ -112,7 +112,7 @@ def parse():
                     help="frames per rank per step (weak scaling)")
     ap.add_argument("--total-frames", type=int, default=0,
                     help="strong scaling: frames per step over all ranks (BASELINE config 5: 4096)")
-    ap.add_argument("--batch", type=int, default=256, help="device batch in --total-frames mode")
+    ap.add_argument("--batch", type=int, default=512, help="device batch in --total-frames mode (512: frame pairs)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--quality", type=int, default=75)

@@ -2000,6 +2000,11 @@ struct I4PLane {
     uint32_t ix[4];  // bperm byte addresses (4 x V index) of the lane's pixels in rows 0..3, one per byte
     uint32_t psel;   // v_perm selector taking the lane's (MB, slot) byte of two gathered words
     int tm;          // mode is TrueMotion
+    // the candidate step's quantiser of the lane's coefficient column q (its MB's
+    // segment, fixed for the search): read once instead of every step
+    uint32_t iq0, bs0, iq1, bs1;
+    int q0, qa;
+    uint32_t l_i4;
 };
 
 DI uint32_t i4p_psel(int hm, int slot)
@@ -2008,9 +2013,20 @@ DI uint32_t i4p_psel(int hm, int slot)
     return 0x0c000c00u | ((4u + b) << 16) | b;
 }
 
-DI void i4p_lane_init(const Ctx& C, I4PLane& L)
+DI void i4p_lane_init(const Ctx& C, const Ctx& CB, I4PLane& L)
 {
     const int l = C.lane, m = l & 15, mv = m < 10 ? m : 0;
+    {
+        const ZwSegment* Sh = (l >> 5) ? CB.S : C.S;
+        const int q = l & 3;
+        L.iq0 = q ? Sh->y1.iq[1] : Sh->y1.iq[0];
+        L.bs0 = q ? Sh->y1.bias[1] : Sh->y1.bias[0];
+        L.iq1 = Sh->y1.iq[1];
+        L.bs1 = Sh->y1.bias[1];
+        L.q0 = q ? (int)Sh->y1.q[1] : (int)Sh->y1.q[0];
+        L.qa = (int)Sh->y1.q[1];
+        L.l_i4 = Sh->l_i4;
+    }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         uint32_t w = 0;
@@ -2093,7 +2109,6 @@ DI void i4p_step(const Ctx& CA, const Ctx& CB, const int* sbx, const int* sby, i
     const int tctx = pick(tc), lctx = pick(lc), ctx0 = pick(nc);
     const int bx = csel(slot, sbx[sl], sbx[0]), by = csel(slot, sby[sl], sby[0]);
     const uint8_t* sYh = hm ? CB.sY : CA.sY;
-    const ZwSegment* Sh = hm ? CB.S : CA.S;
     const LdsTables* Th = hm ? CB.T : CA.T;  // the lane's frame's tables (costs, probabilities)
     PH_START();
     const uint32_t vp = i4p_values<NB>(CA, CB, x0, y0);
@@ -2155,9 +2170,8 @@ DI void i4p_step(const Ctx& CA, const Ctx& CB, const int* sbx, const int* sby, i
     const int mq = (int)((modes >> (16 * g + 4 * k)) & 15ull);
     const int mv = k < K ? mq : 0;  // (k >= K: a valid mode, never eligible)
     const int mcost = Th->fci4[tctx][lctx][mv];
-    const uint32_t iq0 = q ? Sh->y1.iq[1] : Sh->y1.iq[0], bs0 = q ? Sh->y1.bias[1] : Sh->y1.bias[0];
-    const uint32_t iq1 = Sh->y1.iq[1], bs1 = Sh->y1.bias[1];
-    const int q0 = q ? (int)Sh->y1.q[1] : (int)Sh->y1.q[0], qa = (int)Sh->y1.q[1];
+    const uint32_t iq0 = LC.iq0, bs0 = LC.bs0, iq1 = LC.iq1, bs1 = LC.bs1;
+    const int q0 = LC.q0, qa = LC.qa;
     int hn[2];
     hn[0] = (int)Th->binit[3][0][ctx0] & -(int)(ctx0 == 0);
     hn[1] = (int)Th->beob[3][0][ctx0];
@@ -2206,10 +2220,13 @@ DI void i4p_step(const Ctx& CA, const Ctx& CB, const int* sbx, const int* sby, i
     }
     sse = quad_sum(sse);
     const uint32_t rate = (uint32_t)(mcost + cost);
-    const uint32_t score = (uint32_t)sse * 256u + (rate & 0xffffu) * Sh->l_i4;
+    const uint32_t score = (uint32_t)sse * 256u + (rate & 0xffffu) * LC.l_i4;
     const uint32_t key2 = k < K ? (score << 2) | (uint32_t)k : 0xffffffffu;
     const uint32_t kmin = min16u(key2);
     const unsigned long long win = __ballot(key2 == kmin);
+    // the winner's u16 rate, mode cost (< 2^15) and nonzero flag in one word: one
+    // readlane for them instead of three
+    const uint32_t pk = (rate & 0xffffu) | ((uint32_t)mcost << 16) | ((uint32_t)(last >= 0) << 31);
     PH_MARK_L(12, l, 0);
 #pragma unroll
     for (int mb = 0; mb < 2; mb++) {
@@ -2222,14 +2239,15 @@ DI void i4p_step(const Ctx& CA, const Ctx& CB, const int* sbx, const int* sby, i
             const int bmode = (int)((modes >> (16 * gg + 4 * bk)) & 15ull);
             const int wl = 16 * gg + 4 * bk;
             const uint32_t bsse = (uint32_t)__builtin_amdgcn_readlane(sse, wl);
-            const uint32_t brate = (uint32_t)__builtin_amdgcn_readlane((int)rate, wl);
-            const int bnz = __builtin_amdgcn_readlane((int)(last >= 0), wl);
+            const uint32_t bpk = (uint32_t)__builtin_amdgcn_readlane((int)pk, wl);
+            const uint32_t brate = bpk & 0xffffu;
+            const int bnz = (int)(bpk >> 31);
             const int i = sby[h] * 4 + sbx[h];
             I4State& s = st[mb];
             s.tnz = (s.tnz & ~(1u << sbx[h])) | ((uint32_t)bnz << sbx[h]);
             s.lnz = (s.lnz & ~(1u << sby[h])) | ((uint32_t)bnz << sby[h]);
             s.nzm |= (uint32_t)bnz << i;
-            s.total_mc += (uint32_t)__builtin_amdgcn_readlane(mcost, wl);
+            s.total_mc += (bpk >> 16) & 0x7fffu;
             s.running += rdscore(bsse, brate, S.l_mode);
             s.mpack |= (unsigned long long)bmode << (4 * i);
             if (act[mb] && l == gg) M->modes[i] = (uint8_t)bmode;
@@ -2275,7 +2293,7 @@ __device__ uint32_t pick_i4_pair(const Ctx& CA, const Ctx& CB, unsigned long lon
     bool act[2] = {actA, actB};  // (an MB without a search: its lanes run masked)
     const unsigned long long lim[2] = {i16A, i16B};
     I4PLane LC;
-    i4p_lane_init(CA, LC);
+    i4p_lane_init(CA, CB, LC);
     for (int s = 0; s < 10; s++) {
         const int sbyA = s < 4 ? 0 : (s - 2) >> 1;
         const int sbxA = s - 2 * sbyA;
