@@ -818,6 +818,7 @@ def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0
         nbytes = sum(len(p.output(i)) for i in range(min(frames, len(seeds))))
         threads = zwebp.host_threads()
         emit_s = float(k[7]) * 1e-3
+        emit_cpu_s = float(k[8]) * 1e-3
         # the pass kernels' time per batch (launches of launch_frames frames run back to
         # back on the kernel stream): the GPU-side bound of ms_per_batch
         kspan = (float(k[2]) + float(k[3])) * frames / max(1, p.launch_frames)
@@ -827,8 +828,10 @@ def batch_leg(ctx, w, h, q, m, frames, steps, seeds, digests, first_seed_index=0
                 if kspan > 0 else None,
                 "frames_per_step": frames, "launch_frames": p.launch_frames,
                 "kernel_ms_per_launch_span": {"encode_pass1": float(k[2]), "encode_pass2": float(k[3])},
-                "host_emit_ms_per_batch": float(k[7]), "host_threads": threads,
-                "host_emit_frames_per_s_per_core": frames / (emit_s * threads) if emit_s > 0 else None,
+                "host_emit_ms_per_batch": float(k[7]), "host_emit_cpu_ms_per_batch": float(k[8]),
+                "host_threads": threads,
+                "host_emit_frames_per_s_per_core": frames / emit_cpu_s if emit_cpu_s > 0 else None,
+                "host_emit_frames_per_s_per_core_wall": frames / (emit_s * threads) if emit_s > 0 else None,
                 "avg_frame_bytes": nbytes / max(1, min(frames, len(seeds))),
                 "verified": bad == 0 and miss == 0 and ok == frames,
                 "verification": {"frames_checked": ok + bad + miss, "matched": ok, "mismatched": bad,
@@ -985,7 +988,7 @@ def main():
         for pipe, nb in pipes:
             pipe.encode_repeat(nb)
     barrier()
-    kt = np.zeros(8)
+    kt = np.zeros(9)
     t0 = time.perf_counter()
     if a.sequential:
         for _ in range(a.steps):
@@ -1022,6 +1025,7 @@ def main():
         per_launch = pipes[0][0].launch_frames
         threads = zwebp.host_threads()
         emit_s = float(k[7]) * 1e-3
+        emit_cpu_s = float(k[8]) * 1e-3  # the emission workers' thread CPU time per batch
         line = {
             "metric": f"{w}x{h} lossy encodes/s (Q{a.quality}, method {a.method})",
             "value": total_frames / el,
@@ -1051,8 +1055,13 @@ def main():
                                        "run: a span includes waiting for the other lane's kernels, so the phases "
                                        "do not add up to the step; kernel_ms_per_launch has one-lane kernel times",
             "host_ms_per_step": {"fetch_pass1": float(k[4]), "stats_probs": float(k[5]),
-                                 "fetch_pass2": float(k[6]), "emit": float(k[7]), "threads": threads},
-            "host_emit_frames_per_s_per_core": B / (emit_s * threads) if emit_s > 0 else None,
+                                 "fetch_pass2": float(k[6]), "emit": float(k[7]), "threads": threads,
+                                 "emit_cpu": float(k[8])},
+            # frames per second of CPU time the emission workers ran (thread CPU clocks):
+            # what one core sustains; the wall form (emit wall x threads) also counts the
+            # workers' waits for a CPU while the two lanes' emissions overlap
+            "host_emit_frames_per_s_per_core": B / emit_cpu_s if emit_cpu_s > 0 else None,
+            "host_emit_frames_per_s_per_core_wall": B / (emit_s * threads) if emit_s > 0 else None,
             "avg_frame_bytes": bytes_out / max(1, min(B, D)),
         }
         # the extra legs are single-GPU measurements: only the N=1 run carries them
@@ -1140,7 +1149,8 @@ def main():
                 "cores_for_8x_this_gpu_1080p": 8 * line["value"] / line["host_emit_frames_per_s_per_core"]
                 if line["host_emit_frames_per_s_per_core"] else None,
                 "cores_for_8x_this_gpu_4k": 8 * c5["encodes_per_s"] / fpc if fpc else None,
-                "note": "host cores the bool coder needs to keep 8 GPUs at this GPU's measured rate; "
+                "note": "host cores the bool coder needs to keep 8 GPUs at this GPU's measured rate, from the "
+                        "emission workers' thread CPU time (the CPU the entropy stage consumes per frame); "
                         "threads per rank = affinity CPUs / LOCAL_WORLD_SIZE, capped by OMP_NUM_THREADS"}
         line["cpu_baseline"] = None
         if not a.no_cpu_baseline and world == 1:

@@ -16,6 +16,7 @@
 #include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <time.h>
 #include <condition_variable>
 #include <mutex>
 #include <cstdio>
@@ -498,6 +499,7 @@ struct PipeLane {
     Pinned<ZwStatsOut> h_stats;          // [chunk] pass-1 statistics from k_stats
     float kms[4] = {0, 0, 0, 0};
     double hms[4] = {0, 0, 0, 0};  // host ms: fetch1, stats, fetch2, emit
+    double emit_cpu_ms = 0;        // thread CPU ms of the emission workers per batch
     // Pass 2 in frame pairs (k_encode_pass2_fp: two frames a workgroup, so a
     // launch fills the CUs with two frames per CU): chunks 2k and 2k + 1 take
     // pass 2 in one launch, pass 1 and the statistics stay per chunk.
@@ -580,7 +582,10 @@ struct zw_pipe {
     std::mutex p1_mu;
     std::condition_variable p1_cv;
     std::vector<long long> p1_stats;
-    float kms[8];
+    float kms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // emission workspaces (chunk_emit): one per concurrent group task at most
+    std::mutex ews_mu;
+    std::vector<std::unique_ptr<zwh::EmitWs>> ews;
     // Set when a run stops partway: k_segments' histograms and k_pack_scan's
     // counters, which the kernels clear themselves, may then be left nonzero,
     // so every later run of this pipe fails instead of reading them.
@@ -864,6 +869,13 @@ static double now_ms()
 {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// CPU time the calling thread has run (ns)
+static long long thread_cpu_ns()
+{
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (long long)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
 
 // Zero the row-parallel kernels' per-frame tickets, progress and row state
 // before a launch of n frames.  The launch header (error word) is not cleared:
@@ -1072,7 +1084,8 @@ static void dump_emit_input(zw_pipe* p, const uint8_t* rec, size_t bytes, size_t
     fclose(fp);
 }
 
-static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par)
+// cpu_ns: the workers' thread CPU time is added to it (the host budget per frame)
+static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, std::atomic<long long>& cpu_ns)
 {
     const size_t F = (size_t)fa;
     const bool has_alpha = p->color == ZW_COLOR_LA8 || p->color == ZW_COLOR_RGBA8;
@@ -1087,9 +1100,40 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par)
         return g < 1 ? 1 : (g > 4 ? 4 : g);
     }();
     const int G = p->nparts == 1 ? group : 1;
+    // workers per lane (ZW_EMIT_THREADS; default every host thread: with 8 a lane, the
+    // two lanes' emissions used 2 % less CPU but the step was 2 % slower)
+    static const int per_lane_env = [] { const char* e = getenv("ZW_EMIT_THREADS"); return e ? atoi(e) : 0; }();
+    const int nt = per_lane_env > 0 ? per_lane_env : host_threads();
     parallel_for((na + G - 1) / G, [&](int g) {
+        const long long c0 = thread_cpu_ns();
+        // a workspace from the pipe's pool (its buffers stay allocated and faulted
+        // in across chunks and batches; the workers are new threads per chunk)
+        std::unique_ptr<zwh::EmitWs> ws;
+        {
+            std::lock_guard<std::mutex> lk(p->ews_mu);
+            if (!p->ews.empty()) {
+                ws = std::move(p->ews.back());
+                p->ews.pop_back();
+            }
+        }
+        if (!ws) ws.reset(new zwh::EmitWs);
+        struct Done {
+            zw_pipe* p;
+            std::unique_ptr<zwh::EmitWs>& ws;
+            std::atomic<long long>& to;
+            long long c0;
+            ~Done()
+            {
+                {
+                    std::lock_guard<std::mutex> lk(p->ews_mu);
+                    p->ews.push_back(std::move(ws));
+                }
+                to.fetch_add(thread_cpu_ns() - c0, std::memory_order_relaxed);
+            }
+        } done{p, ws, cpu_ns, c0};
         const int i0 = g * G, K = std::min(G, na - i0);
-        thread_local std::vector<uint8_t> vp8[4], alph;
+        std::vector<uint8_t>* vp8 = ws->out;
+        std::vector<uint8_t>& alph = ws->alph;
         std::vector<uint8_t>* outs[4];
         for (int k = 0; k < K; k++) {
             const size_t f = F + i0 + k;
@@ -1110,7 +1154,7 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par)
                 hk[k] = p->h_have_upd[hf] != 0;
                 uk[k] = (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11);
             }
-            zwh::emit_frames(outs, Pk, rk, K, p->w, p->h, hk, uk);
+            zwh::emit_frames(outs, Pk, rk, K, p->w, p->h, hk, uk, ws.get());
         } else {
             emit_vp8(p, *outs[0], B.pack + B.finfo[2 * i0], hidx(p, par, F + i0), na);
         }
@@ -1131,7 +1175,7 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par)
             zw_webp_wrap(out, outs[k]->data(), outs[k]->size(), "VP8 ", has_alpha ? &alph : nullptr, has_alpha, p->w,
                          p->h, md);
         }
-    });
+    }, nt);
     return err.load();
 }
 
@@ -1267,6 +1311,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
         return ZW_OK;
     };
     double fetch = 0, stats = 0, fetch2 = 0, tok = 0;
+    std::atomic<long long> emit_cpu{0};
     int emit_rc = ZW_OK;
     {
         std::lock_guard<std::mutex> lk(L.sync->mu);
@@ -1384,7 +1429,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
             }
             const double t1 = now_ms();
             for (int k = c; k <= c1; k++)
-                if (const int re = chunk_emit(p, L.fb[1 + (k & 1)], ca(k), cn(k), b & 1)) {
+                if (const int re = chunk_emit(p, L.fb[1 + (k & 1)], ca(k), cn(k), b & 1, emit_cpu)) {
                     {  // the lane thread may wait for later chunks: release it
                         std::lock_guard<std::mutex> lk(L.sync->mu);
                         L.sync->fetched = FAILED;
@@ -1474,6 +1519,7 @@ static int lane_encode(zw_pipe* p, PipeLane& L, bool emit, int nb = 1)
     L.hms[1] = stats / nb;
     L.hms[2] = fetch2 / nb;
     L.hms[3] = tok / nb;
+    L.emit_cpu_ms = 1e-6 * (double)emit_cpu.load() / nb;
     lane_times(L);
     return ZW_OK;
 }
@@ -1499,12 +1545,15 @@ static int run_lanes(zw_pipe* p, F fn)
 static void pipe_collect_times(zw_pipe* p)
 {
     // per-kernel: mean over lanes of each lane's launch duration; host: max over lanes
-    for (int i = 0; i < 8; i++) p->kms[i] = 0.f;
-    for (PipeLane& L : p->lanes)
+    // ms[8]: the emission workers' CPU ms per batch, summed over lanes
+    for (int i = 0; i < 9; i++) p->kms[i] = 0.f;
+    for (PipeLane& L : p->lanes) {
         for (int i = 0; i < 4; i++) {
             p->kms[i] += L.kms[i] / (float)p->lanes.size();
             p->kms[4 + i] = std::max(p->kms[4 + i], (float)L.hms[i]);
         }
+        p->kms[8] += (float)L.emit_cpu_ms;
+    }
 }
 
 extern "C" int zw_pipe_run_pass1(zw_pipe* p, int write_recon)
@@ -1655,7 +1704,7 @@ extern "C" int zw_pipe_lanes(zw_pipe* p) { return p ? (int)p->lanes.size() : 0; 
 extern "C" int zw_pipe_kernel_times(zw_pipe* p, float* ms, int n)
 {
     if (!p || !ms) return ZW_EINVAL;
-    for (int i = 0; i < n && i < 8; i++) ms[i] = p->kms[i];
+    for (int i = 0; i < n && i < 9; i++) ms[i] = p->kms[i];
     return ZW_OK;
 }
 

@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#include <memory>
 #include <vector>
 #include "zw_common.h"
 
@@ -922,11 +923,34 @@ inline const TokTmpl& tok_tmpl()
     return T;
 }
 
-// emit_block's decisions (the same sequence) recorded at o.  (A branch-free
-// form -- whole padded templates, sign and end of block always written --
-// measured slower on the GPU box's host: 1.73 vs 1.20 ms per 1080p frame.)
-inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11], const uint8_t* lv, int eobi, int first,
-                     int ctx)
+// The token paths with the frame's probabilities filled in: per (type, band,
+// ctx, after-a-zero, token) the path's decisions (bit << 8 | probability),
+// its length in entry 15.  Built once per frame (the probabilities are fixed
+// for the frame's tokens), so a token's decisions are one 32-byte copy.
+struct TokRes {
+    alignas(32) uint16_t d[4][8][3][2][12][16];
+};
+inline void tok_resolve(TokRes& R, const uint8_t (*probs)[8][3][11])
+{
+    const TokTmpl& TT = tok_tmpl();
+    for (int t = 0; t < 4; t++)
+        for (int b = 0; b < 8; b++)
+            for (int c = 0; c < 3; c++)
+                for (int s = 0; s < 2; s++)
+                    for (int v = 0; v < 12; v++) {
+                        uint16_t* o = R.d[t][b][c][s][v];
+                        const int n = TT.n[s][v];
+                        for (int i = 0; i < 16; i++)
+                            o[i] = i < n ? (uint16_t)((TT.d[s][v][i] & 0xff00u) | probs[t][b][c][TT.d[s][v][i] & 0xffu]) : 0;
+                        o[15] = (uint16_t)n;
+                    }
+}
+
+// emit_block's decisions (the same sequence) recorded at o (which has 16
+// entries of slack: a path is copied whole).  Rt: the block type's resolved
+// paths, P its probabilities.
+inline int rec_block(uint16_t*& o, const uint16_t (*Rt)[3][2][12][16], const uint8_t (*P)[3][11], const uint8_t* lv,
+                     int eobi, int first, int ctx)
 {
     if (eobi <= first) {  // no coefficient: the end of block at `first` (bit 0)
         *o++ = P[COEFF_BANDS[first]][ctx][0];
@@ -936,19 +960,11 @@ inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11],
     uint16_t* q = o;
     for (int idx = first; idx < eobi; idx++) {
         const int coeff = lv_at(lv, idx);
-        const uint8_t* pr = P[COEFF_BANDS[idx]][ctx];
         const int a = coeff < 0 ? -coeff : coeff;
         const int token = token_of(a);
-        const uint16_t* t = TT.d[s][token];
-        const int n = TT.n[s][token];
-        // the first three decisions unconditionally (paths of tokens 0 and 1
-        // are at most three long), the rest of longer paths after
-        q[0] = (uint16_t)((t[0] & 0xff00u) | pr[t[0] & 0xffu]);
-        q[1] = (uint16_t)((t[1] & 0xff00u) | pr[t[1] & 0xffu]);
-        q[2] = (uint16_t)((t[2] & 0xff00u) | pr[t[2] & 0xffu]);
-        if (n > 3)
-            for (int i = 3; i < n; i++) q[i] = (uint16_t)((t[i] & 0xff00u) | pr[t[i] & 0xffu]);
-        q += n;
+        const uint16_t* t = Rt[COEFF_BANDS[idx]][ctx][s][token];
+        memcpy(q, t, 32);
+        q += t[15];
         if (token >= 5) {
             const uint8_t* cp = PROB_DCT_CAT[token - 5];
             const int extra = a - DCT_CAT_BASE[token - 5];
@@ -958,9 +974,11 @@ inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11],
                 mask >>= 1;
             }
         }
-        if (token != 0) *q++ = (uint16_t)(128 | (coeff < 0 ? 0x100 : 0));
+        // the sign (token != 0), written always and kept only for a nonzero
+        *q = (uint16_t)(128u | (((uint32_t)coeff >> 31) << 8));
+        q += token != 0;
         s = token == 0;
-        ctx = token == 0 ? 0 : (token == 1 ? 1 : 2);
+        ctx = token >= 2 ? 2 : token;
     }
     if (eobi < 16) *q++ = P[COEFF_BANDS[eobi]][ctx][0];
     o = q;
@@ -971,9 +989,9 @@ inline int rec_block(uint16_t*& o, const TokTmpl& TT, const uint8_t (*P)[3][11],
 // block's context bit is eob > 0 (what emit_block returns), so every block's
 // context is taken from the eobs up front: the blocks' walks do not wait on
 // each other.
-inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left, Cplx& top)
+inline void rec_mb_tokens(uint16_t*& o, const TokRes& R, const uint8_t (*probs)[8][3][11], const PackedMb& m, Cplx& left,
+                          Cplx& top)
 {
-    const TokTmpl& TT = tok_tmpl();
     const bool i4 = m.luma == 4;
     if (m.skip) {
         left.clear(!i4);
@@ -985,7 +1003,7 @@ inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const 
     if (!i4) {
         const int c = left.y2 + top.y2;
         left.y2 = top.y2 = (uint8_t)(e[16] > 0);
-        rec_block(o, TT, probs[1], m.lv[16], e[16], 0, c);
+        rec_block(o, R.d[1], probs[1], m.lv[16], e[16], 0, c);
     }
     const int first = i4 ? 0 : 1;
     int ctx[16];
@@ -1000,7 +1018,7 @@ inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const 
         left.y[k] = (uint8_t)(e[4 * k + 3] > 0);
         top.y[k] = (uint8_t)(e[12 + k] > 0);
     }
-    for (int b = 0; b < 16; b++) rec_block(o, TT, probs[plane], m.lv[b], e[b], first, ctx[b]);
+    for (int b = 0; b < 16; b++) rec_block(o, R.d[plane], probs[plane], m.lv[b], e[b], first, ctx[b]);
     for (int pl = 0; pl < 2; pl++) {
         uint8_t* lc = pl ? left.v : left.u;
         uint8_t* tc = pl ? top.v : top.u;
@@ -1011,10 +1029,10 @@ inline void rec_mb_tokens(uint16_t*& o, const uint8_t (*probs)[8][3][11], const 
         lc[1] = (uint8_t)(e[b0 + 3] > 0);
         tc[0] = (uint8_t)(e[b0 + 2] > 0);
         tc[1] = (uint8_t)(e[b0 + 3] > 0);
-        rec_block(o, TT, probs[2], m.lv[b0], e[b0], 0, c0);
-        rec_block(o, TT, probs[2], m.lv[b0 + 1], e[b0 + 1], 0, c1);
-        rec_block(o, TT, probs[2], m.lv[b0 + 2], e[b0 + 2], 0, c2);
-        rec_block(o, TT, probs[2], m.lv[b0 + 3], e[b0 + 3], 0, c3);
+        rec_block(o, R.d[2], probs[2], m.lv[b0], e[b0], 0, c0);
+        rec_block(o, R.d[2], probs[2], m.lv[b0 + 1], e[b0 + 1], 0, c1);
+        rec_block(o, R.d[2], probs[2], m.lv[b0 + 2], e[b0 + 2], 0, c2);
+        rec_block(o, R.d[2], probs[2], m.lv[b0 + 3], e[b0 + 3], 0, c3);
     }
 }
 
@@ -1038,20 +1056,36 @@ inline void assemble_frame1(std::vector<uint8_t>& out, const RawBool& H, const R
     memcpy(o + 10 + hs, T.data(), ts);
 }
 
-// emit_frame of K (1..4) frames of one size at once (one token partition):
-// each MB row's header and token decisions are recorded per frame, then the
-// K frames' coders run interleaved.  Byte-identical to emit_frame per frame.
-inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
-                        int K, int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11])
-{
+// The buffers of emit_frames (decision records, coders, row state) for up to
+// four frames.  Kept between calls (a caller's pool, or one per thread): the
+// record buffers are sized for the worst case, and allocating and faulting
+// them in afresh cost more than the emission of a frame.
+struct EmitWs {
     struct Fr {
         std::vector<uint16_t> hd, td;
         RawBool H, T;
         std::vector<Cplx> top;
         std::vector<uint8_t> top_bp;
         uint8_t probs[4][8][3][11];
-    };
-    thread_local Fr F[4];
+        TokRes res;
+    } F[4];
+    std::vector<uint8_t> out[4], alph;  // (for the caller: container assembly)
+};
+
+// emit_frame of K (1..4) frames of one size at once (one token partition):
+// each MB row's header and token decisions are recorded per frame, then the
+// K frames' coders run interleaved.  Byte-identical to emit_frame per frame.
+inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
+                        int K, int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11],
+                        EmitWs* ws = nullptr)
+{
+    using Fr = EmitWs::Fr;
+    thread_local std::unique_ptr<EmitWs> own;
+    if (!ws) {
+        if (!own) own.reset(new EmitWs);
+        ws = own.get();
+    }
+    Fr* F = ws->F;
     const int mbw = P[0]->mbw, mbh = P[0]->mbh;
     const uint8_t* q[4];
     for (int k = 0; k < K; k++) {
@@ -1072,10 +1106,11 @@ inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* c
         if (f.hd.size() < hcap) f.hd.resize(hcap);
         DecRec R{f.hd.data()};
         emit_frame_header(R, *P[k], have_updated[k], upd[k], 1, f.probs);
+        tok_resolve(f.res, f.probs);
         q[k] = packed[k];
         f.H.pos = (size_t)(R.p - f.hd.data());  // (decisions so far, until coded)
     }
-    const size_t tcap = (size_t)mbw * kMbDecisionsMax;
+    const size_t tcap = (size_t)mbw * kMbDecisionsMax + 16;  // (+ rec_block's slack)
     for (int y = 0; y < mbh; y++) {
         const uint16_t* td[4] = {};
         int tn[4] = {};
@@ -1092,7 +1127,7 @@ inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* c
                 PackedMb m;
                 q[k] = view_mb(q[k], m);
                 emit_mb_header(R, *P[k], m, f.top_bp.data(), left_bp, x);
-                rec_mb_tokens(o, f.probs, m, left, f.top[x]);
+                rec_mb_tokens(o, f.res, f.probs, m, left, f.top[x]);
             }
             f.H.pos = (size_t)(R.p - f.hd.data());
             td[k] = f.td.data();

@@ -972,10 +972,12 @@ class Pipeline:
         return self._lib.zw_pipe_launch_frames(self._h)
 
     def kernel_times(self):
-        ms = (ctypes.c_float * 8)()
-        n = self._lib.zw_pipe_kernel_times(self._h, ms, 8)
+        ms = (ctypes.c_float * 9)()
+        n = self._lib.zw_pipe_kernel_times(self._h, ms, 9)
         _check(n, "zw_pipe_kernel_times")
-        return list(ms)  # ms: rgb2yuv, analysis+segments, pass1, pass2 (device); fetch1, stats, fetch2, emit (host)
+        # ms: rgb2yuv, analysis+segments, pass1, pass2 (device); fetch1, stats, fetch2, emit (host wall);
+        # emission CPU ms per batch (all lanes' workers)
+        return list(ms)
 
     def close(self):
         if self._h:

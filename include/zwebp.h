@@ -414,7 +414,8 @@ int zw_pipe_read_probs(zw_pipe *p, int frame, uint8_t *probs, int *skip_prob);
  * run the row-parallel encode kernels (one wave per MB row; env ZW_ENC_ROWS=0/1
  * forces either shape).  zw_pipe_kernel_times: ms[0..3] = mean per-launch device time of
  * rgb2yuv, analysis+segments, pass 1, pass 2 (each launch covers one lane's
- * frames); ms[4..7] = host ms of fetch1, stats, fetch2, emit (max over lanes). */
+ * frames); ms[4..7] = host ms of fetch1, stats, fetch2, emit (wall, max over lanes);
+ * ms[8] = the emission workers' thread CPU ms per batch, summed over lanes (n >= 9). */
 int zw_pipe_lanes(zw_pipe *p);
 /* frames covered by one encode-kernel launch (a lane's chunk) */
 int zw_pipe_launch_frames(zw_pipe *p);

@@ -79,6 +79,8 @@ int main(int argc, char** argv)
         uint8_t probs[4][8][3][11];
         zwh::DecRec H{hd.data()};
         zwh::emit_frame_header(H, P, have != 0, upd, 1, probs);
+        static zwh::TokRes res;
+        zwh::tok_resolve(res, probs);
         std::vector<zwh::Cplx> top(P.mbw, zwh::Cplx{});
         std::vector<uint8_t> top_bp((size_t)P.mbw * 4, 0);
         const uint8_t* q = rec.data();
@@ -89,7 +91,7 @@ int main(int argc, char** argv)
             for (int x = 0; x < P.mbw; x++) {
                 q = zwh::view_mb(q, m);
                 zwh::emit_mb_header(H, P, m, top_bp.data(), left_bp, x);
-                zwh::rec_mb_tokens(o, probs, m, left, top[x]);
+                zwh::rec_mb_tokens(o, res, probs, m, left, top[x]);
             }
         }
         nd = (size_t)(o - all.data());
