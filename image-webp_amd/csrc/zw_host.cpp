@@ -1092,12 +1092,13 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
     if (fa == 0) dump_emit_input(p, B.pack + B.finfo[0], (size_t)B.finfo[1], hidx(p, par, 0));
     std::atomic<int> err{ZW_OK};
     // One token partition (the default): the frames go out in groups of up to
-    // ZW_EMIT_GROUP (4), whose boolean coders run interleaved in one thread
-    // (zwh::emit_frames); with token partitions, one frame per task.
+    // ZW_EMIT_GROUP (16 on a host with AVX-512: their boolean coders run as the
+    // lanes of one vector coder, zwh::raw_code16; else 4, interleaved), in one
+    // thread each (zwh::emit_frames); with token partitions, one frame per task.
     static const int group = [] {
         const char* e = getenv("ZW_EMIT_GROUP");
-        const int g = e && *e ? atoi(e) : 4;
-        return g < 1 ? 1 : (g > 4 ? 4 : g);
+        const int g = e && *e ? atoi(e) : (zwh::have_code16() ? 16 : 4);
+        return g < 1 ? 1 : (g > zwh::EmitWs::kMax ? zwh::EmitWs::kMax : g);
     }();
     const int G = p->nparts == 1 ? group : 1;
     // workers per lane (ZW_EMIT_THREADS; default every host thread: with 8 a lane, the
@@ -1134,7 +1135,7 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
         const int i0 = g * G, K = std::min(G, na - i0);
         std::vector<uint8_t>* vp8 = ws->out;
         std::vector<uint8_t>& alph = ws->alph;
-        std::vector<uint8_t>* outs[4];
+        std::vector<uint8_t>* outs[zwh::EmitWs::kMax];
         for (int k = 0; k < K; k++) {
             const size_t f = F + i0 + k;
             // WebPEncoder::encode with EncoderParams::lossy (api.rs:1291-1398) wraps
@@ -1143,10 +1144,10 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
             outs[k]->clear();
         }
         if (p->nparts == 1) {
-            const ZwFrameParams* Pk[4];
-            const uint8_t* rk[4];
-            bool hk[4];
-            const uint8_t(*uk[4])[8][3][11];
+            const ZwFrameParams* Pk[zwh::EmitWs::kMax];
+            const uint8_t* rk[zwh::EmitWs::kMax];
+            bool hk[zwh::EmitWs::kMax];
+            const uint8_t(*uk[zwh::EmitWs::kMax])[8][3][11];
             for (int k = 0; k < K; k++) {
                 const size_t hf = hidx(p, par, F + i0 + k);
                 Pk[k] = &p->h_params[hf];

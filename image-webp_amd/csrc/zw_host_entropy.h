@@ -8,7 +8,10 @@
 //   headers                         encoder/vp8.rs:315-560
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+#include <immintrin.h>
+#include <algorithm>
 #include <memory>
 #include <vector>
 #include "zw_common.h"
@@ -892,6 +895,125 @@ inline void raw_codeM(RawBool* const* S, const uint16_t* const* d, int n)
     }
 }
 
+// Up to 16 streams at once, one per lane of AVX-512 vectors: raw_codeM's
+// arithmetic (low end in 64 bits, 48 pending bits out at a time) on 16 lanes,
+// each lane's decision fetched by a gather from the shared arena `base` at
+// element offset off[k] + i; lanes past their stream's length n[k] are masked.
+// The rare events -- a carry, 48 bits due -- are handled per lane in scalar
+// code.  Same bytes as raw_codeM (one independent coder per lane).
+__attribute__((target("avx512f,avx512cd,avx512vl,avx512dq,avx512bw"))) inline void raw_code16(
+    RawBool* const* S, const uint16_t* base, const uint32_t* off, const int* n, int K)
+{
+    alignas(64) uint64_t lo[16];
+    alignas(64) uint32_t ra[16], ix[16], nn[16];
+    alignas(64) int32_t co[16];
+    uint8_t* b[16];
+    size_t po[16];
+    int nmax = 0;
+    for (int k = 0; k < 16; k++) {
+        if (k < K) {
+            S[k]->reserve_more((size_t)n[k]);
+            b[k] = S[k]->buf.data();
+            lo[k] = S[k]->low, ra[k] = S[k]->range, co[k] = S[k]->count + 24, po[k] = S[k]->pos;
+            if (lo[k] >> (8 + co[k])) {
+                S[k]->carry(b[k]);
+                lo[k] &= (1ull << (8 + co[k])) - 1;
+            }
+            ix[k] = off[k];
+            nn[k] = (uint32_t)n[k];
+            nmax = n[k] > nmax ? n[k] : nmax;
+        } else {
+            b[k] = nullptr;
+            lo[k] = 0, ra[k] = 255, co[k] = 0, po[k] = 0, ix[k] = 0, nn[k] = 0;
+        }
+    }
+    __m512i vlo0 = _mm512_load_si512(lo), vlo1 = _mm512_load_si512(lo + 8);
+    __m512i vra = _mm512_load_si512(ra), vco = _mm512_load_si512(co), vix = _mm512_load_si512(ix);
+    const __m512i vnn = _mm512_load_si512(nn), one = _mm512_set1_epi32(1), c255 = _mm512_set1_epi32(255);
+    const __m512i c256 = _mm512_set1_epi32(0x100), c24 = _mm512_set1_epi32(24), c8 = _mm512_set1_epi32(8);
+    const __m512i c48 = _mm512_set1_epi32(48);
+    __m512i vi = _mm512_setzero_si512();
+    for (int i = 0; i < nmax; i++) {
+        const __mmask16 act = _mm512_cmpgt_epu32_mask(vnn, vi);
+        vi = _mm512_add_epi32(vi, one);
+        const __m512i d = _mm512_mask_i32gather_epi32(_mm512_setzero_si512(), act, vix, (const void*)base, 2);
+        vix = _mm512_add_epi32(vix, one);
+        const __m512i prob = _mm512_and_si512(d, c255);
+        const __mmask16 bit = _mm512_mask_test_epi32_mask(act, d, c256);
+        const __m512i split = _mm512_add_epi32(one, _mm512_srli_epi32(_mm512_mullo_epi32(_mm512_sub_epi32(vra, one), prob), 8));
+        const __m512i r = _mm512_mask_sub_epi32(split, bit, vra, split);
+        const __m512i sh = _mm512_maskz_sub_epi32(act, _mm512_lzcnt_epi32(r), c24);
+        vra = _mm512_mask_sllv_epi32(vra, act, r, sh);
+        // low += split (bit lanes), in two halves of 8 x 64 bits
+        const __m512i add = _mm512_maskz_mov_epi32(bit, split);
+        vlo0 = _mm512_add_epi64(vlo0, _mm512_cvtepu32_epi64(_mm512_castsi512_si256(add)));
+        vlo1 = _mm512_add_epi64(vlo1, _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(add, 1)));
+        const __m512i w = _mm512_add_epi32(vco, c8);  // the bits L may hold
+        const __m512i w0 = _mm512_cvtepu32_epi64(_mm512_castsi512_si256(w)), w1 = _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(w, 1));
+        const __mmask8 cy0 = _mm512_test_epi64_mask(_mm512_srlv_epi64(vlo0, w0), _mm512_srlv_epi64(vlo0, w0));
+        const __mmask8 cy1 = _mm512_test_epi64_mask(_mm512_srlv_epi64(vlo1, w1), _mm512_srlv_epi64(vlo1, w1));
+        if (__builtin_expect((cy0 | cy1) != 0, 0)) {
+            _mm512_store_si512(lo, vlo0);
+            _mm512_store_si512(lo + 8, vlo1);
+            const unsigned cm = (unsigned)cy0 | ((unsigned)cy1 << 8);
+            for (int k = 0; k < 16; k++)
+                if ((cm >> k) & 1u) {
+                    S[k]->pos = po[k];
+                    S[k]->carry(b[k]);
+                    lo[k] &= (1ull << (8 + co[k])) - 1;
+                }
+            vlo0 = _mm512_load_si512(lo);
+            vlo1 = _mm512_load_si512(lo + 8);
+        }
+        vlo0 = _mm512_sllv_epi64(vlo0, _mm512_cvtepu32_epi64(_mm512_castsi512_si256(sh)));
+        vlo1 = _mm512_sllv_epi64(vlo1, _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(sh, 1)));
+        vco = _mm512_add_epi32(vco, sh);
+        _mm512_store_si512(co, vco);  // (co[] stays current for the scalar paths)
+        const __mmask16 fm = _mm512_cmpge_epi32_mask(vco, c48);
+        if (fm) {
+            _mm512_store_si512(lo, vlo0);
+            _mm512_store_si512(lo + 8, vlo1);
+            for (unsigned m = fm; m; m &= m - 1) {
+                const int k = __builtin_ctz(m);
+                const uint64_t be = __builtin_bswap64(lo[k] << (56 - co[k]));
+                memcpy(b[k] + po[k], &be, 8);
+                po[k] += 6;
+                co[k] -= 48;
+                lo[k] &= (1ull << (8 + co[k])) - 1;
+            }
+            vlo0 = _mm512_load_si512(lo);
+            vlo1 = _mm512_load_si512(lo + 8);
+            vco = _mm512_load_si512(co);
+        }
+    }
+    _mm512_store_si512(lo, vlo0);
+    _mm512_store_si512(lo + 8, vlo1);
+    _mm512_store_si512(ra, vra);
+    _mm512_store_si512(co, vco);
+    for (int k = 0; k < K; k++) {
+        while (co[k] >= 24) {
+            b[k][po[k]++] = (uint8_t)(lo[k] >> co[k]);
+            lo[k] &= (1ull << co[k]) - 1;
+            co[k] -= 8;
+        }
+        while (co[k] < 16 && po[k] > S[k]->lo) {
+            lo[k] |= (uint64_t)b[k][--po[k]] << (8 + co[k]);
+            co[k] += 8;
+        }
+        S[k]->low = (uint32_t)lo[k], S[k]->range = ra[k], S[k]->count = co[k] - 24, S[k]->pos = po[k];
+    }
+}
+inline bool have_code16()
+{
+    static const bool ok = [] {
+        if (const char* e = getenv("ZW_CODE16")) return atoi(e) != 0 && __builtin_cpu_supports("avx512f");
+        return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512cd") &&
+               __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512dq") &&
+               __builtin_cpu_supports("avx512bw");
+    }();
+    return ok;
+}
+
 // K (<= 4) streams of different lengths: interleaved over the common length,
 // then over the longer ones' remainders.
 inline void raw_code_multi(RawBool* const* S, const uint16_t* const* d, const int* n, int K)
@@ -1081,20 +1203,46 @@ inline void assemble_frame1(std::vector<uint8_t>& out, const RawBool& H, const R
 // record buffers are sized for the worst case, and allocating and faulting
 // them in afresh cost more than the emission of a frame.
 struct EmitWs {
+    static constexpr int kMax = 16;
     struct Fr {
-        std::vector<uint16_t> hd, td;
         RawBool H, T;
         std::vector<Cplx> top;
         std::vector<uint8_t> top_bp;
         uint8_t probs[4][8][3][11];
         TokRes res;
-    } F[4];
-    std::vector<uint8_t> out[4], alph;  // (for the caller: container assembly)
+    } F[kMax];
+    // decision records, kMax frames' each in one arena (the 16-lane coder gathers
+    // from it by 32-bit offsets); sized for the worst case and left uninitialised,
+    // so only the pages a frame writes are ever touched
+    std::unique_ptr<uint16_t[]> hd, td;
+    size_t hcap = 0, tcap = 0;
+    std::vector<uint8_t> out[kMax], alph;  // (for the caller: container assembly)
 };
 
-// emit_frame of K (1..4) frames of one size at once (one token partition):
+// K coders over their decision runs d[k] (n[k] decisions each): the 16-lane
+// coder when the host has AVX-512, there are more than four and the runs lie
+// within 2^31 elements of `base` (its gather offsets), else four at a time.
+inline void code_streams(RawBool* const* S, const uint16_t* base, const uint16_t* const* d, const int* n, int K)
+{
+    if (K > 4 && have_code16()) {
+        uint32_t off[16];
+        bool fit = true;
+        for (int k = 0; k < K; k++) {
+            const size_t o = (size_t)(d[k] - base);
+            fit = fit && o + (size_t)n[k] < ((size_t)1 << 31);
+            off[k] = (uint32_t)o;
+        }
+        if (fit) {
+            raw_code16(S, base, off, n, K);
+            return;
+        }
+    }
+    for (int k0 = 0; k0 < K; k0 += 4) raw_code_multi(S + k0, d + k0, n + k0, std::min(4, K - k0));
+}
+
+// emit_frame of K (1..16) frames of one size at once (one token partition):
 // each MB row's header and token decisions are recorded per frame, then the
-// K frames' coders run interleaved.  Byte-identical to emit_frame per frame.
+// K frames' coders run side by side.  Byte-identical to emit_frame per frame.
 inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
                         int K, int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11],
                         EmitWs* ws = nullptr)
@@ -1107,7 +1255,24 @@ inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* c
     }
     Fr* F = ws->F;
     const int mbw = P[0]->mbw, mbh = P[0]->mbh;
-    const uint8_t* q[4];
+    // the frame header's decisions (at most 4 x 8 x 3 x 11 x 9 probability updates
+    // and ~100 others), then the MB headers' (whole frame; at most 2 + 1 + 4 + 16 x 9
+    // + 3 per MB); a row's token decisions (+ rec_block's slack, + the gather's)
+    const size_t hcap = 4 * 8 * 3 * 11 * 9 + 256 + (size_t)mbw * mbh * 160;
+    const size_t tcap = (size_t)mbw * kMbDecisionsMax + 32;
+    if (ws->hcap < hcap) {
+        ws->hd.reset(new uint16_t[hcap * EmitWs::kMax + 32]);
+        ws->hcap = hcap;
+    }
+    if (ws->tcap < tcap) {
+        ws->td.reset(new uint16_t[tcap * EmitWs::kMax + 32]);
+        ws->tcap = tcap;
+    }
+    uint16_t* const hd = ws->hd.get();
+    uint16_t* const td = ws->td.get();
+    const size_t hst = ws->hcap, tst = ws->tcap;
+    const uint8_t* q[EmitWs::kMax];
+    size_t hn[EmitWs::kMax];
     for (int k = 0; k < K; k++) {
         Fr& f = F[k];
         for (RawBool* r : {&f.H, &f.T}) {
@@ -1119,54 +1284,47 @@ inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* c
         f.T.reserve_more((size_t)mbw * mbh * 16 + 4096);
         f.top.assign(mbw, Cplx{});
         f.top_bp.assign((size_t)mbw * 4, 0);
-        // the frame header's decisions (at most 4 x 8 x 3 x 11 x 9 probability
-        // updates and ~100 others), then the MB headers' (whole frame; at most
-        // 2 + 1 + 4 + 16 x 9 + 3 per MB)
-        const size_t hcap = 4 * 8 * 3 * 11 * 9 + 256 + (size_t)mbw * mbh * 160;
-        if (f.hd.size() < hcap) f.hd.resize(hcap);
-        DecRec R{f.hd.data()};
+        DecRec R{hd + (size_t)k * hst};
         emit_frame_header(R, *P[k], have_updated[k], upd[k], 1, f.probs);
         tok_resolve(f.res, f.probs);
         q[k] = packed[k];
-        f.H.pos = (size_t)(R.p - f.hd.data());  // (decisions so far, until coded)
+        hn[k] = (size_t)(R.p - (hd + (size_t)k * hst));
     }
-    const size_t tcap = (size_t)mbw * kMbDecisionsMax + 16;  // (+ rec_block's slack)
+    RawBool* ts[EmitWs::kMax];
+    const uint16_t* tp[EmitWs::kMax];
+    int tn[EmitWs::kMax];
     for (int y = 0; y < mbh; y++) {
-        const uint16_t* td[4] = {};
-        int tn[4] = {};
-        RawBool* ts[4] = {};
         for (int k = 0; k < K; k++) {
             Fr& f = F[k];
-            if (f.td.size() < tcap) f.td.resize(tcap);
             Cplx left;
             memset(&left, 0, sizeof left);
             uint8_t left_bp[4] = {0, 0, 0, 0};
-            DecRec R{f.hd.data() + f.H.pos};
-            uint16_t* o = f.td.data();
+            DecRec R{hd + (size_t)k * hst + hn[k]};
+            uint16_t* const o0 = td + (size_t)k * tst;
+            uint16_t* o = o0;
             for (int x = 0; x < mbw; x++) {
                 PackedMb m;
                 q[k] = view_mb(q[k], m);
                 emit_mb_header(R, *P[k], m, f.top_bp.data(), left_bp, x);
                 rec_mb_tokens(o, f.res, f.probs, m, left, f.top[x]);
             }
-            f.H.pos = (size_t)(R.p - f.hd.data());
-            td[k] = f.td.data();
-            tn[k] = (int)(o - f.td.data());
+            hn[k] = (size_t)(R.p - (hd + (size_t)k * hst));
+            tp[k] = o0;
+            tn[k] = (int)(o - o0);
             ts[k] = &f.T;
         }
-        raw_code_multi(ts, td, tn, K);
+        code_streams(ts, td, tp, tn, K);
     }
     // the header partitions
-    const uint16_t* hd[4] = {};
-    int hn[4] = {};
-    RawBool* hs[4] = {};
+    RawBool* hs[EmitWs::kMax];
+    const uint16_t* hp[EmitWs::kMax];
+    int hl[EmitWs::kMax];
     for (int k = 0; k < K; k++) {
-        hd[k] = F[k].hd.data();
-        hn[k] = (int)F[k].H.pos;
-        F[k].H.pos = 1;
+        hp[k] = hd + (size_t)k * hst;
+        hl[k] = (int)hn[k];
         hs[k] = &F[k].H;
     }
-    raw_code_multi(hs, hd, hn, K);
+    code_streams(hs, hd, hp, hl, K);
     for (int k = 0; k < K; k++) {
         F[k].H.flush();
         F[k].T.flush();

@@ -177,7 +177,7 @@ int main(int argc, char** argv)
     // frame four times lets the branch predictor learn each row's branches):
     // copy k has the MB rows rotated by 17 k rows (a valid record stream, not
     // the same bitstream), the caches swept (256 MB) before every rep
-    std::vector<uint8_t> cp[4];
+    std::vector<uint8_t> cp[16];
     {
         std::vector<size_t> row_off((size_t)P.mbh + 1);
         {
@@ -189,31 +189,33 @@ int main(int argc, char** argv)
             }
             row_off[P.mbh] = (size_t)(q - rec.data());
         }
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < 16; k++)
             for (int y = 0; y < P.mbh; y++) {
-                const int ry = (y + 17 * k) % P.mbh;
+                const int ry = (y + 17 * k + (k >= 4 ? 5 : 0)) % P.mbh;
                 cp[k].insert(cp[k].end(), rec.begin() + (long)row_off[ry], rec.begin() + (long)row_off[ry + 1]);
             }
         std::vector<uint8_t> sweep((size_t)256 << 20, 1);
-        std::vector<uint8_t> o[4];
-        std::vector<uint8_t>* op[4] = {&o[0], &o[1], &o[2], &o[3]};
-        const ZwFrameParams* Ps[4] = {&P, &P, &P, &P};
-        const uint8_t* recs[4] = {cp[0].data(), cp[1].data(), cp[2].data(), cp[3].data()};
-        const bool haves[4] = {have != 0, have != 0, have != 0, have != 0};
-        const uint8_t(*upds[4])[8][3][11] = {upd, upd, upd, upd};
-        double best = 1e30, sum = 0;
-        const int nr = reps < 10 ? reps : 10;
-        for (int r = 0; r < nr; r++) {
-            for (size_t i = 0; i < sweep.size(); i += 64) sweep[i]++;
-            for (auto& c : cp) c[r % c.size()] ^= 0;  // (the copies stay live)
-            const auto t0 = std::chrono::steady_clock::now();
-            zwh::emit_frames(op, Ps, recs, 4, w, h, haves, upds);
-            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            best = ms < best ? ms : best;
-            sum += ms;
+        for (int K : {4, 16}) {
+            std::vector<uint8_t> o[16];
+            std::vector<uint8_t>* op[16];
+            const ZwFrameParams* Ps[16];
+            const uint8_t* recs[16];
+            bool haves[16];
+            const uint8_t(*upds[16])[8][3][11];
+            for (int k = 0; k < 16; k++) op[k] = &o[k], Ps[k] = &P, recs[k] = cp[k].data(), haves[k] = have != 0, upds[k] = upd;
+            double best = 1e30, sum = 0;
+            const int nr = reps < 10 ? reps : 10;
+            for (int r = 0; r < nr; r++) {
+                for (size_t i = 0; i < sweep.size(); i += 64) sweep[i]++;
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int k0 = 0; k0 < 16; k0 += K) zwh::emit_frames(op + k0, Ps + k0, recs + k0, K, w, h, haves + k0, upds + k0);
+                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                best = ms < best ? ms : best;
+                sum += ms;
+            }
+            printf("  distinct K=%d (16 row-rotated frames, caches swept): best %.3f, mean %.3f ms per frame%s\n", K,
+                   best / 16, sum / nr / 16, K > 4 && zwh::have_code16() ? " (16-lane coder)" : "");
         }
-        printf("  distinct K=4 (4 row-rotated frames, caches swept): best %.3f, mean %.3f ms per frame\n", best / 4,
-               sum / nr / 4);
     }
     // breakdown: the walk recording every token decision of the frame (and
     // the headers'), then the coder alone over the token decisions

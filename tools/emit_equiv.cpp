@@ -6,6 +6,7 @@
 // and random decision streams with long carry runs.
 //   g++ -O2 -std=c++17 -I image-webp_amd/csrc tools/emit_equiv.cpp
 #include <cstdio>
+#include <algorithm>
 #include <random>
 #include "zw_host_entropy.h"
 
@@ -90,14 +91,69 @@ int main()
             }
         }
     }
-    // 2) emit_frames (K = 1..4 frames of mixed content) against emit_frame
-    for (int trial = 0; trial < 24; trial++) {
-        const int K = 1 + trial % 4;
+    // 1b) the 16-lane coder (on a host with AVX-512): 5..16 streams of different
+    // lengths, in pieces, against the bit-at-a-time reference
+    if (zwh::have_code16()) {
+        for (int trial = 0; trial < 20; trial++) {
+            const int K = 5 + trial % 12;
+            std::vector<uint16_t> arena;
+            std::vector<size_t> at(K);
+            std::vector<std::vector<uint8_t>> want(K);
+            std::vector<int> len(K);
+            for (int k = 0; k < K; k++) {
+                const int m = rnd(12000);
+                zwh::BoolEncoderRef R;
+                at[k] = arena.size();
+                for (int i = 0; i < m; i++) {
+                    const int p = trial % 3 == 0 ? 1 + rnd(255) : (rnd(2) ? 1 + rnd(8) : 247 + rnd(9));
+                    int bit = rnd(256) >= p;
+                    if (trial % 5 == 1) bit = 1;
+                    arena.push_back((uint16_t)(p | bit << 8));
+                    R.put(bit, p);
+                }
+                arena.push_back(0);
+                R.flush();
+                want[k] = R.buf;
+                len[k] = m;
+            }
+            arena.resize(arena.size() + 32);
+            std::vector<zwh::RawBool> S(K);
+            std::vector<zwh::RawBool*> sp(K);
+            for (int k = 0; k < K; k++) sp[k] = &S[k];
+            std::vector<int> done(K, 0);
+            while (true) {
+                std::vector<const uint16_t*> pp(K);
+                std::vector<int> piece(K);
+                int any = 0;
+                for (int k = 0; k < K; k++) {
+                    piece[k] = std::min(len[k] - done[k], rnd(3000));
+                    pp[k] = arena.data() + at[k] + done[k];
+                    any |= len[k] - done[k];
+                }
+                if (!any) break;
+                zwh::code_streams(sp.data(), arena.data(), pp.data(), piece.data(), K);
+                for (int k = 0; k < K; k++) done[k] += piece[k];
+            }
+            for (int k = 0; k < K; k++) {
+                S[k].flush();
+                if (std::vector<uint8_t>(S[k].data(), S[k].data() + S[k].size()) != want[k]) {
+                    printf("coder16 MISMATCH trial %d stream %d\n", trial, k);
+                    return 1;
+                }
+            }
+        }
+        printf("16-lane coder checked\n");
+    } else {
+        printf("(no AVX-512 here: the 16-lane coder not checked)\n");
+    }
+    // 2) emit_frames (K = 1..16 frames of mixed content) against emit_frame
+    for (int trial = 0; trial < 40; trial++) {
+        const int K = 1 + trial % 16;
         const int mbw = 1 + rnd(9), mbh = 1 + rnd(7);
         std::vector<ZwFrameParams> P(K);
         std::vector<std::vector<uint8_t>> rec(K);
-        static uint8_t upd[4][4][8][3][11];
-        bool have[4];
+        static uint8_t upd[16][4][8][3][11];
+        bool have[16];
         for (int k = 0; k < K; k++) {
             ZwFrameParams& p = P[k];
             memset(&p, 0, sizeof p);
@@ -116,11 +172,12 @@ int main()
             for (size_t i = 0; i < sizeof upd[k]; i++) (&upd[k][0][0][0][0])[i] = (uint8_t)(1 + rnd(255));
             rec[k] = synth_records(mbw, mbh, trial % 3);
         }
-        std::vector<uint8_t> got[4], ref;
-        std::vector<uint8_t>* gp[4] = {&got[0], &got[1], &got[2], &got[3]};
-        const ZwFrameParams* pp[4];
-        const uint8_t* rp[4];
-        const uint8_t(*up[4])[8][3][11];
+        std::vector<uint8_t> got[16], ref;
+        std::vector<uint8_t>* gp[16];
+        for (int k = 0; k < 16; k++) gp[k] = &got[k];
+        const ZwFrameParams* pp[16];
+        const uint8_t* rp[16];
+        const uint8_t(*up[16])[8][3][11];
         for (int k = 0; k < K; k++) pp[k] = &P[k], rp[k] = rec[k].data(), up[k] = upd[k];
         zwh::emit_frames(gp, pp, rp, K, P[0].width, P[0].height, have, up);
         for (int k = 0; k < K; k++) {
