@@ -1100,7 +1100,8 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
         const int g = e && *e ? atoi(e) : (zwh::have_code16() ? 16 : 4);
         return g < 1 ? 1 : (g > zwh::EmitWs::kMax ? zwh::EmitWs::kMax : g);
     }();
-    const int G = p->nparts == 1 ? group : 1;
+    // (small chunks -- the seam's batches -- in smaller groups, so that every worker has one)
+    const int G = p->nparts != 1 ? 1 : std::max(1, std::min(group, std::max(4, na / std::max(1, host_threads()))));
     // workers per lane (ZW_EMIT_THREADS; default every host thread: with 8 a lane, the
     // two lanes' emissions used 2 % less CPU but the step was 2 % slower)
     static const int per_lane_env = [] { const char* e = getenv("ZW_EMIT_THREADS"); return e ? atoi(e) : 0; }();
