@@ -548,3 +548,49 @@ def test_seam_concurrent_single_frame_calls(ctx):
     # an invalid call fails on its own without joining (or stalling) a batch
     with pytest.raises(zwebp.ZwError):
         zwebp.encode_frame_lossy(imgs[shapes[0]][0].reshape(-1)[:100], 96, 64, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+
+
+_EMIT_CHILD = r"""
+import os, sys
+sys.path[:0] = [os.path.join(sys.argv[1], "image-webp_amd"), os.path.join(sys.argv[1], "tests")]
+import oracle_lib as O
+import zwebp
+from zwebp.shard import frame_seed
+from zwebp.synth import synth_rgba
+n, w, h, distinct = 256, 64, 48, 8
+imgs = [synth_rgba(w, h, frame_seed(i)) for i in range(distinct)]
+refs = []
+for im in imgs:
+    rc, ref, _ = O.encode(im, w, h, 3, 75, 4)
+    assert rc == 0
+    refs.append(ref)
+ctx = zwebp.Context(0)
+p = zwebp.Pipeline(n, w, h, zwebp.ColorType.Rgba8, 75, 4, ctx=ctx)
+for i in range(n):
+    p.upload(i, imgs[i % distinct])
+p.encode_repeat(2)
+bad = [i for i in range(n) if p.output(i) != refs[i % distinct]]
+assert not bad, (len(bad), bad[:4])
+assert p.kernel_times()[8] > 0  # the emission workers' CPU time
+p.close()
+ctx.close()
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"ZW_CODE16": "0"}, {"ZW_EMIT_GROUP": "7"}, {"ZW_EMIT_GROUP": "16"}],
+                         ids=["four_interleaved", "vector_7_lanes", "vector_16_lanes"])
+def test_emission_groups_bitexact(env):
+    """Host emission (zw_host.cpp chunk_emit -> zwh::emit_frames): a 256-frame
+    chunk in groups of 16 frames whose coders run as the lanes of the AVX-512
+    coder, in groups of 7 (9 lanes masked, and a last group of 4 on the
+    interleaved coder), and with the vector coder off (four frames interleaved):
+    every bitstream equals the oracle's.  A fresh process per case (the knobs
+    are read once)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _EMIT_CHILD, root], env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
