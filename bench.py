@@ -77,6 +77,8 @@ VALU_PEAK_PER_CU_CYCLE = 2.0      # wave64 VALU instructions: 4 SIMD32 x 1 per 2
 CLOCK_GHZ = 2.4
 XFORM_PMC = os.path.join(ROOT, "profiles", "r04_xform_pmc_traffic.json")
 ENCODE_PMC = os.path.join(ROOT, "profiles", "r06_encode_pmc.json")
+# FETCH_SIZE / WRITE_SIZE passes of the frame-pair encode kernels (tools/gpu_pmc_enc_traffic.sh)
+ENCODE_TRAFFIC = os.path.join(ROOT, "profiles", "r06_encode_traffic.json")
 DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
 XMB_PMC = os.path.join(ROOT, "profiles", "r05_xmb_pmc.json")
 
@@ -89,6 +91,16 @@ def pmc_traffic(path, units):
             d = json.load(f)
         return d["traffic_bytes"] / d["units"] * units
     except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+
+
+def encode_traffic(kernel, mbs):
+    """PMC-measured HBM bytes of `kernel` over `mbs` MBs (ENCODE_TRAFFIC, per MB of
+    the profiled frame-pair launch), or None when no profile is committed."""
+    try:
+        with open(ENCODE_TRAFFIC) as f:
+            return json.load(f)[kernel]["traffic_bytes_per_mb"] * mbs
+    except (OSError, KeyError, ValueError):
         return None
 
 
@@ -1080,7 +1092,12 @@ def main():
             mbs2 = lk["launch_frames"] * nmb
             ach2 = ALG_BYTES_PER_MB * mbs2 / (lk["encode_pass2"] * 1e-3) / 1e9
             line["roofline"] = {"bound": "hbm", "achieved": ach2, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": ach2 / HBM_PEAK_GBS, "traffic": None,
+                                "frac": ach2 / HBM_PEAK_GBS,
+                                "traffic": encode_traffic((er or {}).get("kernel", "k_encode_pass2_fp"), mbs2),
+                                "traffic_note": "per chunk: FETCH_SIZE x 2 + WRITE_SIZE of a 512-frame launch "
+                                                "(r06_encode_traffic.json), scaled to the chunk's MBs; 3.8 x the "
+                                                "algorithmic bytes (level-cost tables, row state, the ZwMbOut records "
+                                                "with their side data) at 0.05 of HBM: bytes do not bound this kernel",
                                 "kernel": (er or {}).get("kernel", "k_encode_pass2_fp"),
                                 "alg_bytes_per_mb": ALG_BYTES_PER_MB,
                                 "alg_bytes_note": "Y/U/V source 384 + levels 800 + reconstruction 384 per MB "
