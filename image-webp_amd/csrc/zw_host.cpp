@@ -19,6 +19,7 @@
 #include <time.h>
 #include <condition_variable>
 #include <mutex>
+#include <new>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1101,7 +1102,12 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
         return g < 1 ? 1 : (g > zwh::EmitWs::kMax ? zwh::EmitWs::kMax : g);
     }();
     // (small chunks -- the seam's batches -- in smaller groups, so that every worker has one)
-    const int G = p->nparts != 1 ? 1 : std::max(1, std::min(group, std::max(4, na / std::max(1, host_threads()))));
+    // (and very large frames in groups whose decision arenas stay within 1 GiB of
+    // address space a worker)
+    const int gmem = (int)std::max<size_t>(1, ((size_t)1 << 30) / zwh::emit_arena_bytes(p->mbw, p->mbh));
+    const int G = p->nparts != 1
+                      ? 1
+                      : std::max(1, std::min({group, gmem, std::max(4, na / std::max(1, host_threads()))}));
     // workers per lane (ZW_EMIT_THREADS; default every host thread: with 8 a lane, the
     // two lanes' emissions used 2 % less CPU but the step was 2 % slower)
     static const int per_lane_env = [] { const char* e = getenv("ZW_EMIT_THREADS"); return e ? atoi(e) : 0; }();
@@ -1118,7 +1124,12 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
                 p->ews.pop_back();
             }
         }
-        if (!ws) ws.reset(new zwh::EmitWs);
+        if (!ws) ws.reset(new (std::nothrow) zwh::EmitWs);
+        if (!ws) {
+            int ok = ZW_OK;
+            err.compare_exchange_strong(ok, ZW_ENOMEM);
+            return;
+        }
         struct Done {
             zw_pipe* p;
             std::unique_ptr<zwh::EmitWs>& ws;
@@ -1156,7 +1167,13 @@ static int chunk_emit(zw_pipe* p, const FetchBuf& B, int fa, int na, int par, st
                 hk[k] = p->h_have_upd[hf] != 0;
                 uk[k] = (const uint8_t(*)[8][3][11])(p->h_upd.data() + hf * 4 * 8 * 3 * 11);
             }
-            zwh::emit_frames(outs, Pk, rk, K, p->w, p->h, hk, uk, ws.get());
+            try {
+                zwh::emit_frames(outs, Pk, rk, K, p->w, p->h, hk, uk, ws.get());
+            } catch (const std::bad_alloc&) {  // (the worst-case decision arenas)
+                int ok = ZW_OK;
+                err.compare_exchange_strong(ok, ZW_ENOMEM);
+                return;
+            }
         } else {
             emit_vp8(p, *outs[0], B.pack + B.finfo[2 * i0], hidx(p, par, F + i0), na);
         }

@@ -1270,6 +1270,7 @@ struct EmitWs {
     // so only the pages a frame writes are ever touched
     std::unique_ptr<uint16_t[]> hd, td;
     size_t hcap = 0, tcap = 0;
+    int hk = 0, tk = 0;  // frames the arenas hold
     std::vector<uint8_t> out[kMax], alph;  // (for the caller: container assembly)
 };
 
@@ -1297,6 +1298,13 @@ inline void code_streams(RawBool* const* S, const uint16_t* base, const uint16_t
 // emit_frame of K (1..16) frames of one size at once (one token partition):
 // each MB row's header and token decisions are recorded per frame, then the
 // K frames' coders run side by side.  Byte-identical to emit_frame per frame.
+// Bytes of emit_frames' decision arenas per frame of a group (worst case, mostly
+// never touched): callers size their groups with it.
+inline size_t emit_arena_bytes(int mbw, int mbh)
+{
+    return 2 * ((4 * 8 * 3 * 11 * 9 + 256 + (size_t)mbw * mbh * 160) + ((size_t)mbw * kMbDecisionsMax + 32));
+}
+
 inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* const* P, const uint8_t* const* packed,
                         int K, int width, int height, const bool* have_updated, const uint8_t (*const* upd)[8][3][11],
                         EmitWs* ws = nullptr)
@@ -1314,13 +1322,17 @@ inline void emit_frames(std::vector<uint8_t>* const* out, const ZwFrameParams* c
     // + 3 per MB); a row's token decisions (+ rec_block's slack, + the gather's)
     const size_t hcap = 4 * 8 * 3 * 11 * 9 + 256 + (size_t)mbw * mbh * 160;
     const size_t tcap = (size_t)mbw * kMbDecisionsMax + 32;
-    if (ws->hcap < hcap) {
-        ws->hd.reset(new uint16_t[hcap * EmitWs::kMax + 32]);
+    if (ws->hcap < hcap || ws->hk < K) {
+        ws->hd.reset();
+        ws->hd.reset(new uint16_t[hcap * (size_t)K + 32]);
         ws->hcap = hcap;
+        ws->hk = K;
     }
-    if (ws->tcap < tcap) {
-        ws->td.reset(new uint16_t[tcap * EmitWs::kMax + 32]);
+    if (ws->tcap < tcap || ws->tk < K) {
+        ws->td.reset();
+        ws->td.reset(new uint16_t[tcap * (size_t)K + 32]);
         ws->tcap = tcap;
+        ws->tk = K;
     }
     uint16_t* const hd = ws->hd.get();
     uint16_t* const td = ws->td.get();
